@@ -1,0 +1,155 @@
+"""Headline benchmark: images/sec (whole node), ResNet-56 CIFAR-10, PBT population 8.
+
+    python bench.py                                  # 1 GPU: all 8 members on one device
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One timed "step" = one training step of EVERY population member (forward,
+backward, fused optimizer update), i.e. ``pop * batch`` images across the node.
+Members are split over the ranks (8/N per GPU; on one GPU all 8 run
+population-batched).  Every ``--exploit_every`` steps the full PBT exploit/explore
+cycle runs inside the timed region: score all-gather, truncation selection,
+winner->loser state copy (RCCL send/recv over xGMI across GPUs, D2D on one GPU),
+hyper-parameter perturbation.  Data: a fixed synthetic device batch per member
+(random-normal 32x32x3 images, uniform labels), random-init weights.
+Hyper-parameters are sampled from the reference search space with a fixed seed;
+``batch_size`` is pinned to 128 for every member so per-step work is identical
+across runs (the search space samples 65..255).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+BASELINE_METRIC = "images/sec (whole node) ResNet-56 CIFAR-10 PBT pop=8 at 1/2/4/8 MI355X"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=60)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--pop", type=int, default=8)
+    p.add_argument("--batch", type=int, default=128)
+    p.add_argument("--resnet_size", type=int, default=56)
+    p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
+    p.add_argument("--exploit_every", type=int, default=25)
+    p.add_argument("--seed", type=int, default=2024)
+    p.add_argument("--graph", type=int, default=1, help="capture the population step in a HIP graph")
+    p.add_argument("--profile_json", default=None)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    from distributedtf_amd.parallel.comm import init_distributed
+    from distributedtf_amd.parallel.dataplane import DataPlane
+    from distributedtf_amd.pbt.cluster import partition, sample_population
+    from distributedtf_amd.pbt.exploit import plan_exploit, apply_plan_to_values
+    from distributedtf_amd.models.cifar10_model import Cifar10Model
+
+    comm = init_distributed()
+    rank, world = comm.Get_rank(), comm.Get_size()
+    if world != args.gpus and rank == 0:
+        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+
+    hps = sample_population(args.pop, args.seed)
+    for h in hps:
+        h["batch_size"] = args.batch
+    begin, cnt = partition(args.pop, world)[rank]
+    members = [Cifar10Model(begin + i, hps[begin + i], "/tmp/bench_savedata_%d/model_" % rank, seed=args.seed,
+                            resnet_size=args.resnet_size, device=dev, backend=args.backend,
+                            capacity=max(1, cnt), use_synthetic_data=True, checkpoint_every_round=False)
+               for i in range(cnt)]
+    eng = members[0].engine
+    ds = members[0].dataset()
+    dataplane = DataPlane(comm)
+    owner = {}
+    for r, (b, c) in enumerate(partition(args.pop, world)):
+        for i in range(b, b + c):
+            owner[i] = r
+
+    slots = [m.slot for m in members]
+    batches = [ds.batch_slice(args.batch) for _ in members]
+
+    def step():
+        hp = [m.hparams for m in members]
+        lrs = [m.learning_rate(eng.host_step[m.slot]) for m in members]
+        return eng.train_step(slots, batches, hp, lrs)
+
+    exploits = [0]
+
+    def exploit_cycle(losses):
+        # score = -loss (no eval inside the timed region); full gather/plan/copy/perturb cycle
+        vals = [[m.cluster_id, -float(losses[i].item()), m.hparams] for i, m in enumerate(members)]
+        parts = comm.allgather(vals)
+        allv = [v for p in parts for v in p]
+        plan = plan_exploit(allv)
+        transfers = [(p.src_id, owner[p.src_id], p.dst_id, owner[p.dst_id]) for p in plan]
+        dataplane.execute(transfers, {m.cluster_id: m for m in members})
+        upd = apply_plan_to_values(allv, plan)
+        for m in members:
+            if m.cluster_id in upd:
+                m.set_values(upd[m.cluster_id])
+                m.hparams["batch_size"] = args.batch
+                m.perturb_hparams()
+                m.hparams["batch_size"] = args.batch
+        exploits[0] += 1
+
+    def barrier_sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        comm.barrier()
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        losses = step()
+    barrier_sync()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        losses = step()
+        if args.exploit_every and (k + 1) % args.exploit_every == 0:
+            exploit_cycle(losses)
+    barrier_sync()
+    dt = time.perf_counter() - t0
+    dts = comm.allgather(dt)
+    dt_max = max(dts)
+    images = args.pop * args.batch * args.steps
+    value = images / dt_max
+    if rank == 0:
+        flops = members[0].arch.flops_per_image() * 3.0 * images / dt_max
+        out = {
+            "metric": BASELINE_METRIC,
+            "value": round(value, 1),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * dt_max / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (device-resident random-normal 32x32x3, uniform labels), random-init weights",
+            "config": {"model": "resnet%d_v2_cifar10" % args.resnet_size, "global_batch": args.pop * args.batch,
+                       "per_member_batch": args.batch, "population": args.pop, "seq_len": None,
+                       "parallelism": "pbt_pop%d_%dmembers_per_gpu" % (args.pop, cnt),
+                       "backend": eng.backend.name, "exploit_every": args.exploit_every,
+                       "exploits_timed": exploits[0]},
+            "achieved_tflops": round(flops / 1e12, 2),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        from distributedtf_amd.parallel.comm import shutdown_distributed
+        shutdown_distributed()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,202 @@
+"""Population engine: every member of one GPU resident in HBM, trained together.
+
+Replaces the reference's per-member serial loop that rebuilt a TF graph and
+restored a checkpoint from disk for every ``train`` call
+(``training_worker.py:64-69``, ``resnet_run_loop.py:397-406``).
+
+State layout (one row per member slot, fp32)::
+
+    state[g] = [ params (P) | slot1 (P) | slot2 (P) | bn running stats (R) | step | pad ]
+
+so a member's full training state -- the exploit payload -- is one contiguous
+row: an exploit is a single RCCL send/recv (or D2D copy) of ``state[g]`` with no
+packing.  Gradients live in ``grads[G, P]``; bf16 shadow weights, activations
+and workspaces belong to the backend.
+
+Backends:
+  * ``TorchBackend`` -- per-member PyTorch autograd on views of the flat
+    buffers.  Numerics oracle, CPU path, and the path for architectures without
+    HIP kernels.
+  * ``HipResNetBackend`` (``engine/hip_resnet.py``) -- population-batched
+    CDNA4 kernels: all members' images in one launch per layer.
+The optimizer is one fused launch over every row (``ops.fused_optimizer``) or
+the PyTorch reference on CPU.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import optim as _optim
+
+
+def _align(n: int, a: int = 64) -> int:
+    return (n + a - 1) // a * a
+
+
+class PopulationEngine:
+    def __init__(self, arch, capacity: int, device, backend: str = "auto", compute_dtype=torch.bfloat16,
+                 optimizer_impl: str = "auto"):
+        self.arch = arch
+        self.capacity = int(capacity)
+        self.device = torch.device(device)
+        self.P = arch.n_params
+        self.R = arch.n_running
+        self.n_reg = arch.n_reg
+        self.Pp = _align(self.P, 64)   # 256-B aligned slot offsets -> float4 kernels
+        self.S = _align(3 * self.Pp + self.R + 1)
+        self.state = torch.zeros(self.capacity, self.S, dtype=torch.float32, device=self.device)
+        self.grads = torch.zeros(self.capacity, self.Pp, dtype=torch.float32, device=self.device)
+        self.hyper = torch.zeros(self.capacity, _optim.N_HYPER, dtype=torch.float32, device=self.device)
+        self.free_slots = list(range(self.capacity))
+        self.members: Dict[int, object] = {}
+        self.host_step = [0] * self.capacity
+        self.compute_dtype = compute_dtype
+        if self.device.type == "cpu" and compute_dtype == torch.bfloat16:
+            self.compute_dtype = torch.float32
+        self.backend = make_backend(self, backend)
+        if optimizer_impl == "auto":
+            optimizer_impl = "hip" if self.device.type == "cuda" else "reference"
+        self.optimizer_impl = optimizer_impl
+
+    # ----------------------------------------------------------------- views
+    @property
+    def params(self):
+        return self.state[:, :self.P]
+
+    @property
+    def slot1(self):
+        return self.state[:, self.Pp:self.Pp + self.P]
+
+    @property
+    def slot2(self):
+        return self.state[:, 2 * self.Pp:2 * self.Pp + self.P]
+
+    @property
+    def running(self):
+        return self.state[:, 3 * self.Pp:3 * self.Pp + self.R]
+
+    def step_col(self):
+        return self.state[:, 3 * self.Pp + self.R]
+
+    def state_row(self, slot: int) -> torch.Tensor:
+        return self.state[slot]
+
+    # --------------------------------------------------------------- members
+    def add_member(self, member, hparams: Dict, seed: int) -> int:
+        if not self.free_slots:
+            raise RuntimeError("population engine is full (capacity %d)" % self.capacity)
+        slot = self.free_slots.pop(0)
+        self.members[slot] = member
+        p, r = self.arch.init_params(hparams.get("initializer"), seed)
+        row = self.state[slot]
+        row.zero_()
+        row[:self.P] = p.to(self.device)
+        row[3 * self.Pp:3 * self.Pp + self.R] = r.to(self.device)
+        s1, s2 = _optim.slot_init_values(hparams["opt_case"]["optimizer"])
+        if s1:
+            row[self.Pp:self.Pp + self.P] = s1
+        if s2:
+            row[2 * self.Pp:2 * self.Pp + self.P] = s2
+        self.host_step[slot] = 0
+        self.backend.on_params_changed([slot])
+        return slot
+
+    def remove_member(self, slot: int) -> None:
+        self.members.pop(slot, None)
+        if slot not in self.free_slots:
+            self.free_slots.append(slot)
+            self.free_slots.sort()
+
+    def on_state_imported(self, slot: int) -> None:
+        self.host_step[slot] = int(round(float(self.step_col()[slot].item())))
+        self.backend.on_params_changed([slot])
+
+    # --------------------------------------------------------------- training
+    def set_hyper(self, slot: int, hparams: Dict, lr: float, active: bool = True) -> None:
+        row = _optim.hyper_row(hparams, lr, self.host_step[slot] + 1, active)
+        self.hyper[slot] = torch.tensor(row, dtype=torch.float32)
+
+    def train_step(self, slots: Sequence[int], batches: Sequence[Tuple[torch.Tensor, torch.Tensor]],
+                   hparams: Sequence[Dict], lrs: Sequence[float]) -> torch.Tensor:
+        """One optimizer step for ``slots`` (each with its own batch). Returns
+        per-member cross-entropy losses (device tensor)."""
+        hy = torch.zeros(self.capacity, _optim.N_HYPER, dtype=torch.float32)
+        for s, hp, lr in zip(slots, hparams, lrs):
+            hy[s] = torch.tensor(_optim.hyper_row(hp, lr, self.host_step[s] + 1, True))
+        self.hyper.copy_(hy.to(self.device), non_blocking=True)
+        losses = self.backend.forward_backward(slots, batches)
+        self.apply_optimizer(slots)
+        for s in slots:
+            self.host_step[s] += 1
+        sc = self.step_col()
+        idx = torch.tensor(list(slots), device=self.device, dtype=torch.long)
+        sc.index_add_(0, idx, torch.ones(len(slots), device=self.device))
+        self.backend.on_params_changed(slots)
+        return losses
+
+    def apply_optimizer(self, slots: Sequence[int]) -> None:
+        if self.optimizer_impl == "hip":
+            from ..ops import fused_optimizer
+            fused_optimizer(self.state, self.grads, self.hyper, self.Pp, self.P, self.n_reg,
+                            shadow=self.backend.shadow_weights(), zero_grads=True)
+        else:
+            _optim.apply_reference(self.params, self.grads[:, :self.P], self.slot1, self.slot2, self.hyper,
+                                   self.n_reg, rows=list(slots))
+            self.grads.zero_()
+
+    @torch.no_grad()
+    def evaluate(self, slot: int, x: torch.Tensor, y: torch.Tensor, batch: int = 1000) -> float:
+        correct = 0
+        for i in range(0, x.shape[0], batch):
+            logits = self.backend.infer(slot, x[i:i + batch])
+            correct += int((logits.argmax(dim=1) == y[i:i + batch].to(logits.device)).sum().item())
+        return correct / float(max(1, x.shape[0]))
+
+
+# ----------------------------------------------------------------------- backends
+
+class TorchBackend:
+    """Per-member autograd on flat-buffer views (oracle / fallback path)."""
+
+    name = "torch"
+
+    def __init__(self, engine: PopulationEngine):
+        self.e = engine
+
+    def on_params_changed(self, slots):
+        pass
+
+    def shadow_weights(self):
+        return None
+
+    def forward_backward(self, slots, batches):
+        e = self.e
+        losses = []
+        for s, (x, y) in zip(slots, batches):
+            p = e.params[s].detach().clone().requires_grad_(True)
+            logits = e.arch.forward(p, e.running[s], x, training=True, dtype=e.compute_dtype)
+            loss = F.cross_entropy(logits.float(), y.long())
+            g, = torch.autograd.grad(loss, p)
+            e.grads[s, :e.P].copy_(g)
+            losses.append(loss.detach())
+        return torch.stack(losses) if losses else torch.zeros(0, device=e.device)
+
+    def infer(self, slot, x):
+        e = self.e
+        return e.arch.forward(e.params[slot], e.running[slot], x, training=False, dtype=e.compute_dtype)
+
+
+def make_backend(engine: PopulationEngine, name: str):
+    if name == "auto":
+        name = "hip" if (engine.device.type == "cuda" and getattr(engine.arch, "hip_supported", False)) else "torch"
+    if name == "torch":
+        return TorchBackend(engine)
+    if name == "hip":
+        from .hip_resnet import HipResNetBackend
+        return HipResNetBackend(engine)
+    raise ValueError("unknown backend %r" % name)

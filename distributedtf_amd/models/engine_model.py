@@ -1,0 +1,211 @@
+"""``EngineModel``: a ``ModelBase`` whose state lives in a shared ``PopulationEngine``.
+
+All members of one model family on one rank/device share one engine, so
+``TrainingWorker.train`` -> ``train_population`` runs them TOGETHER: each step
+is one population-wide forward/backward + one fused optimizer launch, and
+members with different batch sizes / epoch lengths simply drop out of the active
+set when their epoch is done.  (The reference trains members one after another,
+each rebuilding its graph and restoring a checkpoint: ``training_worker.py:64``.)
+"""
+
+from __future__ import annotations
+
+import csv
+import math
+import os
+import time
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn.functional as F
+
+from .model_base import ModelBase
+from ..engine.population import PopulationEngine
+
+
+def default_device():
+    if torch.cuda.is_available():
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+class EngineModel(ModelBase):
+    _engines: Dict[tuple, PopulationEngine] = {}
+    _datasets: Dict[tuple, object] = {}
+
+    # subclass hooks ----------------------------------------------------------
+    def make_arch(self):
+        raise NotImplementedError
+
+    def make_dataset(self, device):
+        raise NotImplementedError
+
+    def learning_rate(self, step: int) -> float:
+        raise NotImplementedError
+
+    def steps_per_epoch(self) -> int:
+        raise NotImplementedError
+
+    def csv_row(self, accuracy: float):
+        raise NotImplementedError
+
+    # ------------------------------------------------------------------------
+    def __init__(self, cluster_id, hparams, save_base_dir, seed=None, device=None, backend="auto",
+                 capacity=8, use_synthetic_data=None, data_dir=None, max_train_steps=None,
+                 checkpoint_every_round=True, eval_every_round=True, **kw):
+        super().__init__(cluster_id, hparams, save_base_dir, seed=seed)
+        self.options = dict(kw)
+        self.device = torch.device(device) if device is not None else default_device()
+        self.data_dir = data_dir
+        self.use_synthetic_data = use_synthetic_data
+        self.max_train_steps = max_train_steps
+        self.checkpoint_every_round = checkpoint_every_round
+        self.eval_every_round = eval_every_round
+        self.arch = self.make_arch()
+        key = (type(self).__name__, str(self.device), self.arch.name, backend)
+        eng = EngineModel._engines.get(key)
+        if eng is None or not eng.free_slots:
+            eng = self._grow_or_create(key, eng, capacity, backend)
+        self.engine = eng
+        self._engine_key = key
+        init_seed = (seed if seed is not None else int(time.time() * 1000) % 100000) * 1009 + self.cluster_id
+        self.slot = eng.add_member(self, self.hparams, init_seed)
+        self.last_loss = float("nan")
+        self.images_trained = 0
+
+    def _grow_or_create(self, key, eng, capacity, backend):
+        if eng is None:
+            eng = PopulationEngine(self.arch, capacity, self.device, backend=backend)
+        else:
+            new = PopulationEngine(self.arch, eng.capacity * 2, self.device, backend=backend)
+            new.state[:eng.capacity].copy_(eng.state)
+            new.members = dict(eng.members)
+            new.free_slots = [s for s in range(new.capacity) if s not in new.members]
+            new.host_step[:eng.capacity] = eng.host_step
+            for slot, m in new.members.items():
+                m.engine = new
+            new.backend.on_params_changed(list(new.members))
+            eng = new
+        EngineModel._engines[key] = eng
+        return eng
+
+    @classmethod
+    def reset_engines(cls):
+        EngineModel._engines.clear()
+        EngineModel._datasets.clear()
+
+    def dataset(self):
+        key = (type(self).__name__, str(self.device), self.data_dir, self.use_synthetic_data)
+        ds = EngineModel._datasets.get(key)
+        if ds is None:
+            ds = self.make_dataset(self.device)
+            EngineModel._datasets[key] = ds
+        return ds
+
+    # ------------------------------------------------------------- state API
+    def state_view(self):
+        return self.engine.state_row(self.slot)
+
+    def export_state(self):
+        return self.engine.state_row(self.slot)
+
+    def import_state(self, flat):
+        self.engine.state_row(self.slot).copy_(flat.to(self.engine.state.device, torch.float32))
+        self.on_state_imported()
+
+    def on_state_imported(self):
+        self.engine.on_state_imported(self.slot)
+
+    def release(self):
+        self.engine.remove_member(self.slot)
+
+    @property
+    def global_step(self) -> int:
+        return self.engine.host_step[self.slot]
+
+    def set_values(self, values):
+        super().set_values(values)
+
+    # ------------------------------------------------------------- training
+    def _batch(self, ds, gen):
+        b = int(self.hparams["batch_size"])
+        if hasattr(ds, "batch_slice"):
+            return ds.batch_slice(b)
+        if not hasattr(self, "_perm") or self._perm_pos + b > self._perm.numel():
+            self._perm = torch.randperm(ds.num_train, device=ds.train_x.device, generator=gen)
+            self._perm_pos = 0
+        idx = self._perm[self._perm_pos:self._perm_pos + b]
+        self._perm_pos += b
+        return ds.batch(idx, gen)
+
+    def n_steps(self, num_epoch: int) -> int:
+        n = num_epoch * self.steps_per_epoch()
+        if self.max_train_steps:
+            n = min(n, int(self.max_train_steps))
+        return max(1, n)
+
+    @classmethod
+    def train_population(cls, members: List["EngineModel"], num_epoch: int, total_epochs: int):
+        failed = {}
+        groups: Dict[int, List[EngineModel]] = {}
+        for m in members:
+            groups.setdefault(id(m.engine), []).append(m)
+        for ms in groups.values():
+            eng = ms[0].engine
+            ds = ms[0].dataset()
+            gen = None
+            if ds.device.type == "cuda":
+                gen = torch.Generator(device=ds.device)
+                gen.manual_seed(int(ms[0].rng.random() * 1e9))
+            todo = {m.slot: m.n_steps(num_epoch) for m in ms}
+            by_slot = {m.slot: m for m in ms}
+            done = 0
+            loss_acc = {m.slot: None for m in ms}
+            while True:
+                active = [s for s in sorted(todo) if todo[s] > done]
+                if not active:
+                    break
+                batches = [by_slot[s]._batch(ds, gen) for s in active]
+                hps = [by_slot[s].hparams for s in active]
+                lrs = [by_slot[s].learning_rate(eng.host_step[s]) for s in active]
+                losses = eng.train_step(active, batches, hps, lrs)
+                for i, s in enumerate(active):
+                    by_slot[s].images_trained += int(batches[i][1].shape[0])
+                for i, s in enumerate(active):
+                    loss_acc[s] = losses[i]  # view, no host sync
+                done += 1
+            for m in ms:
+                try:
+                    if loss_acc[m.slot] is not None:
+                        m.last_loss = float(loss_acc[m.slot].item())
+                    m.finish_round(num_epoch)
+                except Exception as e:  # member-level culling
+                    failed[m.cluster_id] = e
+        return failed
+
+    def finish_round(self, num_epoch):
+        if math.isnan(self.last_loss) or math.isinf(self.last_loss):
+            self.accuracy = float("nan")
+        elif self.eval_every_round:
+            x, y = self.dataset().eval_set()
+            self.accuracy = self.engine.evaluate(self.slot, x, y)
+        self.write_learning_curve(self.accuracy)
+        self.epoches_trained += num_epoch
+        if self.checkpoint_every_round:
+            self.save_checkpoint()
+
+    def train(self, num_epoch, total_epochs):
+        failed = type(self).train_population([self], num_epoch, total_epochs)
+        if self.cluster_id in failed:
+            raise failed[self.cluster_id]
+
+    def write_learning_curve(self, accuracy):
+        fields, row = self.csv_row(accuracy)
+        d = self.ensure_save_dir()
+        path = os.path.join(d, "learning_curve.csv")
+        exists = os.path.isfile(path)
+        with open(path, "a", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=fields)
+            if not exists:
+                w.writeheader()
+            w.writerow(row)

@@ -1,0 +1,78 @@
+"""Build the gfx950 kernel library ``ops/libdtf_kernels.so`` in-tree with hipcc.
+
+The library is a plain C ABI (``extern "C" dtf_*`` launchers taking raw device
+pointers and a ``hipStream_t``) loaded with ctypes -- no hipify, no torch
+extension headers, no JIT cache outside the repo.  ``python -m
+distributedtf_amd.ops.build`` (or ``__graft_entry__.build()``) rebuilds it when a
+source is newer than the library.
+"""
+
+from __future__ import annotations
+
+import glob
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libdtf_kernels.so")
+ARCH = os.environ.get("DTF_OFFLOAD_ARCH", "gfx950")
+
+
+def sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+
+
+def needs_build(lib=LIB) -> bool:
+    if not os.path.isfile(lib):
+        return True
+    t = os.path.getmtime(lib)
+    deps = sources() + glob.glob(os.path.join(CSRC, "*.h"))
+    return any(os.path.getmtime(s) > t for s in deps)
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.isfile(c) or c == "hipcc"):
+            return c
+    return "hipcc"
+
+
+def build(force: bool = False, verbose: bool = True, extra_flags=None) -> str:
+    if not force and not needs_build():
+        return LIB
+    objs = []
+    procs = []
+    for src in sources():
+        obj = os.path.join(CSRC, os.path.basename(src) + ".o")
+        cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
+               "-Wno-unused-result", "-munsafe-fp-atomics"] + list(extra_flags or [])
+        procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+        objs.append(obj)
+    failed = False
+    for src, p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            failed = True
+            sys.stderr.write(out.decode(errors="replace"))
+            sys.stderr.write("\nhipcc failed on %s\n" % src)
+        elif verbose and out.strip():
+            sys.stderr.write(out.decode(errors="replace"))
+    if failed:
+        raise RuntimeError("kernel build failed")
+    tmp = LIB + ".tmp"
+    subprocess.check_call([hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", tmp] + objs)
+    os.replace(tmp, LIB)
+    for o in objs:
+        try:
+            os.remove(o)
+        except OSError:
+            pass
+    if verbose:
+        sys.stderr.write("built %s\n" % LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

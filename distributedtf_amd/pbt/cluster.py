@@ -1,0 +1,352 @@
+"""PBT control plane.
+
+Two drivers share the worker, the exploit planner and the report writers:
+
+``PBTCluster`` -- reference-compatible master (``pbt_cluster.py:27-470``).  Rank
+``master_rank`` owns the population and drives ``TrainingWorker.main_loop`` on
+the other ranks with the ``WorkerInstruction`` protocol (ADD_GRAPHS / TRAIN /
+GET / SET / EXPLORE / GET_PROFILING_INFO / EXIT).  The master trains nothing.
+Exploit weight copies go over the data plane between the two worker ranks
+(``exploit_transport="dataplane"``, default) or through the shared filesystem
+exactly like the reference (``"files"``).
+
+``SPMDPopulation`` -- the MI355X-native driver: every rank (one per GPU) trains
+its slice of the population; scores are all-gathered and every rank computes
+the same exploit plan, so there is no idle master and no SET / EXPLORE traffic;
+weights move GPU->GPU over RCCL (or D2D when winner and loser share a GPU).
+"""
+
+from __future__ import annotations
+
+import copy
+import datetime
+import math
+import os
+import shutil
+import time
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+from .exploit import apply_plan_to_values, plan_exploit
+from .hparams import WorkerInstruction, generate_random_hparam
+from . import reports
+
+
+def partition(pop_size: int, n_slots: int) -> List[Tuple[int, int]]:
+    """Contiguous id blocks of ``ceil(pop / n)`` per slot (``pbt_cluster.py:56,66-75``).
+
+    Returns ``[(begin, count), ...]`` of length ``n_slots``; trailing slots may be
+    empty when ``pop < n`` (Appendix A15 handled explicitly).
+    """
+    if n_slots <= 0:
+        raise ValueError("need at least one slot")
+    per = int(math.ceil(pop_size / float(n_slots))) if pop_size else 0
+    out, begin, left = [], 0, pop_size
+    for _ in range(n_slots):
+        cnt = max(0, min(per, left))
+        out.append((begin, cnt))
+        begin += cnt
+        left -= cnt
+    return out
+
+
+def sample_population(pop_size: int, seed: Optional[int] = None) -> List[Dict[str, Any]]:
+    import random
+    rng = random.Random(seed) if seed is not None else random
+    return [generate_random_hparam(rng) for _ in range(pop_size)]
+
+
+EXCLUDE_ON_COPY = ("learning_curve.csv", "theta.csv")
+
+
+def _excluded(name: str) -> bool:
+    return name in EXCLUDE_ON_COPY or name.startswith("events.out") or name.startswith(".nfs")
+
+
+def copy_member_files(src_dir: str, dest_dir: str) -> bool:
+    """Reference ``copyfiles`` rules: replace dest's checkpoint files by src's,
+    keeping dest's own learning curves / event files."""
+    if os.path.abspath(src_dir) == os.path.abspath(dest_dir):
+        print("Warning, src_dir and dest_dir are the same")
+        return False
+    os.makedirs(dest_dir, exist_ok=True)
+    for name in os.listdir(dest_dir):
+        p = os.path.join(dest_dir, name)
+        if os.path.isfile(p) and not _excluded(name):
+            os.remove(p)
+    if os.path.isdir(src_dir):
+        for name in os.listdir(src_dir):
+            p = os.path.join(src_dir, name)
+            if os.path.isfile(p) and not _excluded(name):
+                shutil.copy2(p, dest_dir)
+    return True
+
+
+class _ReportMixin:
+    savedata = "savedata"
+    do_exploit = True
+    do_explore = True
+
+    def dump_all_models_to_json(self, filename):
+        reports.dump_population_json(self.get_all_values(), filename)
+        print("Saving all models to {}".format(filename))
+
+    def report_best_model(self):
+        path = os.path.join(self.savedata, "best_model.json")
+        rep = reports.write_best_model(self.get_all_values(), path)
+        print("Saving best model to {}".format(path))
+        return rep
+
+    def report_plot_for_toy_model(self):
+        return reports.plot_toy(self.savedata, self.do_exploit, self.do_explore)
+
+    def report_accuracy_plot(self):
+        return reports.plot_curves(self.savedata, "acc", self.do_exploit, self.do_explore)
+
+    def report_lr_plot(self):
+        return reports.plot_curves(self.savedata, "lr", self.do_exploit, self.do_explore)
+
+    def report_best3_plot(self):
+        return reports.plot_best3(self.savedata, self.do_exploit, self.do_explore)
+
+
+class PBTCluster(_ReportMixin):
+    """Reference-compatible master (runs on ``master_rank`` only)."""
+
+    def __init__(self, pop_size, comm, master_rank, epochs_per_round, do_exploit=True, do_explore=True,
+                 seed=None, exploit_transport="dataplane", savedata="savedata", hparams=None):
+        self.pop_size = pop_size
+        self.comm = comm
+        self.master_rank = master_rank
+        self.epochs_per_round = epochs_per_round
+        self.do_exploit = do_exploit
+        self.do_explore = do_explore
+        self.exploit_transport = exploit_transport
+        self.savedata = savedata
+        self.seed = seed
+        self.exploit_time = 0.0
+        self.round_times: List[float] = []
+        self.last_plan = []
+        self._initial_hparams = hparams
+        self.dispatch_hparams_to_workers()
+
+    def workers(self) -> List[int]:
+        return [r for r in range(self.comm.Get_size()) if r != self.master_rank]
+
+    def _bcast(self, msg, ranks=None):
+        for r in (self.workers() if ranks is None else ranks):
+            self.comm.isend(msg, r).wait()
+
+    def dispatch_hparams_to_workers(self):
+        hps = self._initial_hparams or sample_population(self.pop_size, self.seed)
+        self.pop_size = len(hps)
+        print("Population size = {}".format(self.pop_size))
+        explore_only = self.do_explore and not self.do_exploit
+        ws = self.workers()
+        self.id_owner: Dict[int, int] = {}
+        for r, (begin, cnt) in zip(ws, partition(self.pop_size, len(ws))):
+            self.comm.isend((WorkerInstruction.ADD_GRAPHS, hps[begin:begin + cnt], begin, explore_only), r).wait()
+            for i in range(begin, begin + cnt):
+                self.id_owner[i] = r
+
+    def kill_all_workers(self):
+        self._bcast((WorkerInstruction.EXIT,))
+
+    def train(self, round_num):
+        start = time.time()
+        for rnd in range(round_num):
+            t0 = time.time()
+            print("\nRound {}".format(rnd))
+            self._bcast((WorkerInstruction.TRAIN, self.epochs_per_round, self.epochs_per_round * round_num))
+            if self.do_exploit:
+                self.exploit()
+            if self.do_explore:
+                self.explore()
+            self.round_times.append(time.time() - t0)
+            print("Round elapsed time: {}\n".format(datetime.timedelta(seconds=self.round_times[-1])))
+        self.flush_all_instructions()
+        total = time.time() - start
+        print("Total elapsed time: {}".format(datetime.timedelta(seconds=total)))
+        return total
+
+    def _gather(self):
+        self._bcast((WorkerInstruction.GET,))
+        values, owner = [], {}
+        for r in self.workers():
+            data = self.comm.recv(r)
+            values += data
+            for d in data:
+                owner[int(d[0])] = r
+        return values, owner
+
+    def exploit(self):
+        values, owner = self._gather()  # the recv is the end-of-TRAIN barrier
+        t0 = time.time()
+        self.pop_size = len(values)
+        plan = plan_exploit(values)
+        self.last_plan = plan
+        updates = apply_plan_to_values(values, plan)
+        per_rank: Dict[int, list] = {r: [] for r in self.workers()}
+        transfers = []
+        for p in plan:
+            print("Copied: {} -> {}".format(p.src_id, p.dst_id))
+            per_rank[owner[p.dst_id]].append(updates[p.dst_id])
+            if self.exploit_transport == "files":
+                copy_member_files(os.path.join(self.savedata, "model_%d" % p.src_id),
+                                  os.path.join(self.savedata, "model_%d" % p.dst_id))
+            else:
+                transfers.append((p.src_id, owner[p.src_id], p.dst_id, owner[p.dst_id]))
+        from_disk = self.exploit_transport == "files"
+        involved = set(per_rank) if transfers else {r for r, v in per_rank.items() if v}
+        for r in self.workers():
+            if r in involved or per_rank[r]:
+                self.comm.isend((WorkerInstruction.SET, per_rank[r], transfers, from_disk), r).wait()
+        self.exploit_time += time.time() - t0
+
+    def explore(self):
+        self._bcast((WorkerInstruction.EXPLORE,))
+
+    def flush_all_instructions(self):
+        self.get_all_values()
+
+    def get_all_values(self):
+        return self._gather()[0]
+
+    def get_profiling_info(self):
+        self._bcast((WorkerInstruction.GET_PROFILING_INFO,))
+        return [self.comm.recv(r) for r in self.workers()]
+
+    def print_profiling_info(self):
+        infos = self.get_profiling_info()
+        n = max(1, len(infos))
+        tr = sum(i[0] for i in infos) / n
+        ex = sum(i[1] for i in infos) / n
+        print("")
+        print("=======Profiling Information========")
+        print("Total train time: {}".format(datetime.timedelta(seconds=tr)))
+        print("Total exploit time: {}".format(datetime.timedelta(seconds=self.exploit_time)))
+        print("Total explore time: {}\n".format(datetime.timedelta(seconds=ex)))
+        return {"train": tr, "exploit": self.exploit_time, "explore": ex}
+
+
+class SPMDPopulation(_ReportMixin):
+    """Every rank trains; exploit plans are computed identically everywhere."""
+
+    def __init__(self, pop_size, comm, target_model_class, epochs_per_round=1, do_exploit=True, do_explore=True,
+                 seed=None, savedata="savedata", model_kwargs=None, dataplane=None, hparams=None,
+                 verbose=True, inject_nan=None):
+        from .worker import TrainingWorker
+        self.comm = comm
+        self.rank = comm.Get_rank()
+        self.world = comm.Get_size()
+        self.epochs_per_round = epochs_per_round
+        self.do_exploit = do_exploit
+        self.do_explore = do_explore
+        self.savedata = savedata
+        self.verbose = verbose
+        self.exploit_time = 0.0
+        self.round_times: List[float] = []
+        self.inject_nan = inject_nan or {}  # {round: [member ids]} fault injection
+        if dataplane is None:
+            from ..parallel.dataplane import DataPlane
+            dataplane = DataPlane(comm)
+        self.dataplane = dataplane
+        hps = hparams if hparams is not None else (
+            sample_population(pop_size, seed) if self.rank == 0 else None)
+        hps = comm.bcast(hps, 0)
+        self.pop_size = len(hps)
+        self.worker = TrainingWorker(comm, 0, target_model_class, save_base_dir=os.path.join(savedata, "model_"),
+                                     seed=seed, model_kwargs=model_kwargs, dataplane=dataplane, verbose=verbose)
+        blocks = partition(self.pop_size, self.world)
+        self.id_owner = {}
+        for r, (b, c) in enumerate(blocks):
+            for i in range(b, b + c):
+                self.id_owner[i] = r
+        begin, cnt = blocks[self.rank]
+        self.worker.add_graphs(copy.deepcopy(hps[begin:begin + cnt]), begin, do_explore and not do_exploit)
+        self.last_plan = []
+
+    def log(self, *a):
+        if self.verbose and self.rank == 0:
+            print(*a, flush=True)
+
+    def get_all_values(self):
+        parts = self.comm.allgather(self.worker.get_all_values())
+        return [v for part in parts for v in part]
+
+    def train_one_round(self, rnd, total_rounds):
+        self.worker.train(self.epochs_per_round, self.epochs_per_round * total_rounds)
+        for mid in self.inject_nan.get(rnd, []):
+            for g in list(self.worker.worker_graphs):
+                if g.cluster_id == mid:
+                    g.accuracy = float("nan")
+                    self.worker._cull(g, "injected nan")
+
+    def exploit(self):
+        parts = self.comm.allgather(self.worker.get_all_values())  # also the end-of-train barrier
+        t0 = time.time()
+        values = [v for part in parts for v in part]
+        owner = {int(v[0]): r for r, part in enumerate(parts) for v in part}
+        self.pop_size = len(values)
+        plan = plan_exploit(values)
+        self.last_plan = plan
+        for p in plan:
+            self.log("Copied: {} -> {}".format(p.src_id, p.dst_id))
+        transfers = [(p.src_id, owner[p.src_id], p.dst_id, owner[p.dst_id]) for p in plan]
+        if transfers:
+            self.dataplane.execute(transfers, self.worker.members_by_id())
+        updates = apply_plan_to_values(values, plan)
+        mine = [u for mid, u in updates.items() if owner[mid] == self.rank]
+        self.worker.set_values(mine)
+        self.exploit_time += time.time() - t0
+
+    def explore(self):
+        self.worker.explore_necessary_graphs()
+
+    def train(self, round_num):
+        start = time.time()
+        for rnd in range(round_num):
+            t0 = time.time()
+            self.log("\nRound {}".format(rnd))
+            self.train_one_round(rnd, round_num)
+            if self.do_exploit:
+                self.exploit()
+            if self.do_explore:
+                self.explore()
+            self.round_times.append(time.time() - t0)
+            self.log("Round elapsed time: {}\n".format(datetime.timedelta(seconds=self.round_times[-1])))
+        self.comm.barrier()
+        total = time.time() - start
+        self.log("Total elapsed time: {}".format(datetime.timedelta(seconds=total)))
+        return total
+
+    def get_profiling_info(self):
+        return self.comm.allgather([self.worker.train_time, self.worker.explore_time])
+
+    def print_profiling_info(self):
+        infos = self.get_profiling_info()
+        n = max(1, len(infos))
+        tr = sum(i[0] for i in infos) / n
+        ex = sum(i[1] for i in infos) / n
+        if self.rank == 0:
+            print("")
+            print("=======Profiling Information========")
+            print("Total train time: {}".format(datetime.timedelta(seconds=tr)))
+            print("Total exploit time: {}".format(datetime.timedelta(seconds=self.exploit_time)))
+            print("Total explore time: {}\n".format(datetime.timedelta(seconds=ex)))
+            print("Exploit data plane: {} transfers, {:.1f} KB, {:.3f}s".format(
+                self.dataplane.transfers_done, self.dataplane.bytes_moved / 1024.0, self.dataplane.seconds))
+        return {"train": tr, "exploit": self.exploit_time, "explore": ex}
+
+    # report writers run on rank 0 but need everyone for the gather
+    def dump_all_models_to_json(self, filename):
+        vals = self.get_all_values()
+        if self.rank == 0:
+            reports.dump_population_json(vals, filename)
+
+    def report_best_model(self):
+        vals = self.get_all_values()
+        if self.rank == 0:
+            return reports.write_best_model(vals, os.path.join(self.savedata, "best_model.json"))
+
+    def kill_all_workers(self):
+        self.comm.barrier()

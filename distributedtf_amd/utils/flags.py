@@ -1,0 +1,151 @@
+"""Typed configuration + CLI.
+
+Replaces the reference's two config tiers: module constants in
+``main_manager.py:32-44`` (+ positional ``argv[1]`` = population size) and the
+vendored absl flag registry that ``cifar10_main.py:239-330`` deletes and
+re-defines from every member's hparam dict on every train call
+(``official/utils/flags/{core,_base,_performance,_benchmark,_misc}.py``).
+
+Here a member's settings are an explicit ``MemberConfig`` derived from its
+hparam dict (no global mutation), and the CLI keeps the reference flag names that
+matter: ``batch_size``, ``train_epochs``, ``epochs_between_evals``,
+``use_synthetic_data``, ``max_train_steps``, ``dtype``, ``loss_scale``,
+``data_format``, ``resnet_size``, ``resnet_version``, ``hooks``,
+``stop_threshold``, ``export_dir``, ``data_dir``, ``model_dir``.
+Validators mirror the reference's: ``loss_scale > 0`` (``_performance.py:125``),
+no fp16 with ResNet v1 (``resnet_run_loop.py:546-549``).
+"""
+
+from __future__ import annotations
+
+import argparse
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional
+
+import torch
+
+DTYPE_MAP = {"fp32": (torch.float32, 1), "fp16": (torch.float16, 128), "bf16": (torch.bfloat16, 1)}
+
+
+def get_dtype(name: str) -> torch.dtype:
+    return DTYPE_MAP[name][0]
+
+
+def get_loss_scale(dtype: str, loss_scale: Optional[float]) -> float:
+    if loss_scale is not None:
+        return float(loss_scale)
+    return float(DTYPE_MAP[dtype][1])
+
+
+def _positive(v):
+    f = float(v)
+    if f <= 0:
+        raise argparse.ArgumentTypeError("loss_scale should be a positive number.")
+    return f
+
+
+def _str2bool(v):
+    if isinstance(v, bool):
+        return v
+    return str(v).lower() in ("1", "true", "yes", "y", "t")
+
+
+@dataclass
+class MemberConfig:
+    """Per-member training settings derived from one hparam dict (no global flags)."""
+    optimizer: str
+    learning_rate: float
+    momentum: float = 0.0
+    grad_decay: float = 0.0
+    decay_steps: int = 0
+    decay_rate: float = 1.0
+    weight_decay: float = 0.0
+    regularizer: Optional[str] = None
+    initializer: Optional[str] = None
+    batch_size: int = 128
+    model_id: int = 0
+
+    @staticmethod
+    def from_hparams(hp: Dict[str, Any], model_id: int = 0) -> "MemberConfig":
+        opt = hp["opt_case"]
+        return MemberConfig(optimizer=opt["optimizer"], learning_rate=float(opt["lr"]),
+                            momentum=float(opt.get("momentum", 0.0)), grad_decay=float(opt.get("grad_decay", 0.0)),
+                            decay_steps=int(hp.get("decay_steps", 0)), decay_rate=float(hp.get("decay_rate", 1.0)),
+                            weight_decay=float(hp.get("weight_decay", 0.0)),
+                            regularizer=None if hp.get("regularizer") in (None, "None") else hp.get("regularizer"),
+                            initializer=None if hp.get("initializer") in (None, "None") else hp.get("initializer"),
+                            batch_size=int(hp.get("batch_size", 128)), model_id=model_id)
+
+
+def build_parser(defaults: Optional[Dict[str, Any]] = None) -> argparse.ArgumentParser:
+    d = dict(population_size=20, train_round=20, epochs_per_round=1, do_exploit=True, do_explore=True,
+             model="mnist")
+    d.update(defaults or {})
+    p = argparse.ArgumentParser(description="MI355X population-based training", conflict_handler="resolve")
+    p.add_argument("pop_size", nargs="?", type=int, default=None, help="population size (reference argv[1])")
+    p.add_argument("--population_size", type=int, default=d["population_size"])
+    p.add_argument("--model", default=d["model"], help="toy | mnist | cifar10 | imagenet")
+    p.add_argument("--mode", default="spmd", choices=["spmd", "master_worker"])
+    p.add_argument("--rounds", "--train_round", dest="train_round", type=int, default=d["train_round"])
+    p.add_argument("--epochs_per_round", type=int, default=d["epochs_per_round"])
+    p.add_argument("--do_exploit", type=_str2bool, default=d["do_exploit"])
+    p.add_argument("--do_explore", type=_str2bool, default=d["do_explore"])
+    p.add_argument("--seed", type=int, default=None)
+    p.add_argument("--savedata", default="savedata")
+    p.add_argument("--results_file", default="test_results.txt")
+    p.add_argument("--exploit_transport", default="dataplane", choices=["dataplane", "files"])
+    p.add_argument("--inject_nan_member", action="append", default=[],
+                   help="fault injection: '<member_id>@<round>' marks the member NaN after that round")
+    # model / training flags (reference names)
+    p.add_argument("--resnet_size", type=int, default=None)
+    p.add_argument("--resnet_version", type=int, default=2, choices=[1, 2])
+    p.add_argument("--data_dir", default=None)
+    p.add_argument("--use_synthetic_data", type=_str2bool, default=None)
+    p.add_argument("--max_train_steps", type=int, default=None)
+    p.add_argument("--debug_steps", type=int, default=None, help="MNIST: steps per 'epoch' (reference used 10)")
+    p.add_argument("--batch_size", type=int, default=None, help="override every member's batch_size")
+    p.add_argument("--dtype", default="bf16", choices=list(DTYPE_MAP))
+    p.add_argument("--loss_scale", type=_positive, default=None)
+    p.add_argument("--data_format", default="channels_last", choices=["channels_last"])
+    p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
+    p.add_argument("--hooks", default="", help="comma list: logging,examples_per_second,profiler,metric")
+    p.add_argument("--stop_threshold", type=float, default=None)
+    p.add_argument("--export_dir", default=None)
+    p.add_argument("--no_checkpoint", action="store_true")
+    return p
+
+
+class MainArgs(argparse.Namespace):
+    def model_kwargs(self) -> Dict[str, Any]:
+        kw: Dict[str, Any] = {}
+        if self.model != "toy":
+            kw["backend"] = self.backend
+            kw["use_synthetic_data"] = self.use_synthetic_data
+            kw["max_train_steps"] = self.max_train_steps
+            kw["checkpoint_every_round"] = not self.no_checkpoint
+            if self.data_dir:
+                kw["data_dir"] = self.data_dir
+        if self.model in ("cifar10", "imagenet"):
+            if self.resnet_size:
+                kw["resnet_size"] = self.resnet_size
+            kw["resnet_version"] = self.resnet_version
+        if self.model == "mnist" and self.debug_steps:
+            kw["debug_steps"] = self.debug_steps
+        return kw
+
+    def inject_nan_schedule(self) -> Dict[int, List[int]]:
+        out: Dict[int, List[int]] = {}
+        for spec in self.inject_nan_member:
+            mid, rnd = spec.split("@")
+            out.setdefault(int(rnd), []).append(int(mid))
+        return out
+
+
+def parse_main_args(argv=None, defaults=None) -> MainArgs:
+    p = build_parser(defaults)
+    args = p.parse_args(argv, namespace=MainArgs())
+    if args.pop_size is not None:
+        args.population_size = args.pop_size
+    if args.resnet_version == 1 and args.dtype == "fp16":
+        p.error("ResNet version 1 is not currently supported with fp16. Please use version 2 instead.")
+    return args

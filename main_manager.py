@@ -1,0 +1,100 @@
+"""Common entry point of all ranks (reference ``main_manager.py:1-73``).
+
+    # reference-style: positional population size, module-level defaults
+    python main_manager.py 20
+    # one process per GPU (SPMD: every rank trains, RCCL exploit copies)
+    torchrun --standalone --nproc-per-node 8 main_manager.py 8 --model cifar10 --resnet_size 56
+    # reference-compatible master/worker protocol (rank 0 trains nothing)
+    torchrun --nproc-per-node 2 main_manager.py 2 --model toy --mode master_worker --rounds 30 \
+        --epochs_per_round 4
+
+Outputs are the reference's: ``savedata/`` (wiped at start), ``initial_hp.json``,
+per-member ``model_<id>/`` (checkpoint + learning curves), ``best_model.json``,
+``{acc,lr,best3[,toy]}_<mode>.png`` and a line appended to ``test_results.txt``.
+"""
+
+from __future__ import annotations
+
+import os
+import shutil
+import sys
+
+##################
+# configurations (reference main_manager.py:32-44)
+##################
+master_rank = 0
+train_round = 20
+population_size = 20
+epochs_per_round = 1
+do_exploit = True
+do_explore = True
+target_model = "mnist"   # 'toy' | 'mnist' | 'cifar10' | 'imagenet'
+
+
+def main(argv=None):
+    from distributedtf_amd.utils.flags import parse_main_args
+    from distributedtf_amd.models import model_class
+    from distributedtf_amd.parallel.comm import init_distributed, backend_name
+    from distributedtf_amd.pbt.cluster import PBTCluster, SPMDPopulation
+    from distributedtf_amd.pbt.worker import TrainingWorker
+    from distributedtf_amd.pbt import reports
+
+    args = parse_main_args(argv, defaults=dict(
+        population_size=population_size, train_round=train_round, epochs_per_round=epochs_per_round,
+        do_exploit=do_exploit, do_explore=do_explore, model=target_model))
+    cls = model_class(args.model)
+    model_kwargs = args.model_kwargs()
+    if args.model == "toy":
+        backend = "gloo"
+    else:
+        backend = None
+    comm = init_distributed(backend=backend)
+    rank, world = comm.Get_rank(), comm.Get_size()
+    savedata = args.savedata
+
+    if rank == master_rank:
+        shutil.rmtree(savedata, ignore_errors=True)
+        os.makedirs(savedata, exist_ok=True)
+    comm.barrier()
+
+    inject = args.inject_nan_schedule()
+    if args.mode == "master_worker":
+        if world < 2:
+            raise SystemExit("master_worker mode needs >= 2 ranks (1 master + workers)")
+        from distributedtf_amd.parallel.dataplane import DataPlane
+        if rank == master_rank:
+            cluster = PBTCluster(args.population_size, comm, master_rank, epochs_per_round=args.epochs_per_round,
+                                 do_exploit=args.do_exploit, do_explore=args.do_explore, seed=args.seed,
+                                 exploit_transport=args.exploit_transport, savedata=savedata)
+        else:
+            worker = TrainingWorker(comm, master_rank, cls, save_base_dir=os.path.join(savedata, "model_"),
+                                    seed=args.seed, model_kwargs=model_kwargs, dataplane=DataPlane(comm))
+            worker.main_loop()
+            return 0
+    else:
+        cluster = SPMDPopulation(args.population_size, comm, cls, epochs_per_round=args.epochs_per_round,
+                                 do_exploit=args.do_exploit, do_explore=args.do_explore, seed=args.seed,
+                                 savedata=savedata, model_kwargs=model_kwargs, inject_nan=inject)
+
+    cluster.dump_all_models_to_json(os.path.join(savedata, "initial_hp.json"))
+    elapsed = cluster.train(args.train_round)
+    if rank == master_rank:
+        reports.append_test_result(world, args.population_size, elapsed, args.results_file)
+    if rank == master_rank or args.mode != "master_worker":
+        if rank == master_rank:
+            if args.model == "toy":
+                cluster.report_plot_for_toy_model()
+            cluster.report_accuracy_plot()
+            cluster.report_lr_plot()
+            cluster.report_best3_plot()
+        cluster.report_best_model()
+        cluster.print_profiling_info()
+        cluster.kill_all_workers()
+    if world > 1:
+        from distributedtf_amd.parallel.comm import shutdown_distributed
+        shutdown_distributed()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,72 @@
+"""Multi-process PBT over torch.distributed (gloo, CPU): the fake-cluster test the
+reference never had (it relied on `mpirun --oversubscribe`)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, tmp, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    os.chdir(tmp)
+    torch.set_num_threads(1)
+    try:
+        from distributedtf_amd.parallel.comm import init_distributed, shutdown_distributed
+        from distributedtf_amd.pbt.cluster import SPMDPopulation
+        from distributedtf_amd.models.cifar10_model import Cifar10Model
+        from distributedtf_amd.pbt.hparams import generate_random_hparam
+        import random
+        comm = init_distributed(backend="gloo")
+        rng = random.Random(3)
+        hps = []
+        for _ in range(4):
+            h = generate_random_hparam(rng)
+            h["batch_size"] = 4
+            hps.append(h)
+        pop = SPMDPopulation(4, comm, Cifar10Model, epochs_per_round=1, seed=5, verbose=False, hparams=hps,
+                             model_kwargs=dict(resnet_size=8, max_train_steps=1, use_synthetic_data=True,
+                                               device="cpu", eval_every_round=True))
+        pop.train(1)
+        plan = [(p.src_id, p.dst_id) for p in pop.last_plan]
+        # bit-exact check: loser state == winner state right after the exploit copy
+        states = {g.cluster_id: g.export_state().clone() for g in pop.worker.worker_graphs}
+        gathered = comm.allgather({k: v for k, v in states.items()})
+        allst = {}
+        for d in gathered:
+            allst.update(d)
+        ok = all(torch.equal(allst[s], allst[d]) for s, d in plan)
+        q.put((rank, plan, ok, sorted(allst)))
+        shutdown_distributed()
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, "ERR", traceback.format_exc(), None))
+
+
+@pytest.mark.timeout(300)
+def test_spmd_gloo_world2_exploit_bit_exact(tmp_path):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=280) for _ in procs]
+    for p in procs:
+        p.join(30)
+    for r in res:
+        assert r[1] != "ERR", r[2]
+    plans = {r[0]: r[1] for r in res}
+    assert plans[0] == plans[1] and len(plans[0]) == 1
+    assert all(r[2] for r in res)
+    assert res[0][3] == [0, 1, 2, 3]

@@ -1,0 +1,579 @@
+"""Population-batched ResNet v2 (CIFAR shape) training step on hand-written gfx950 kernels.
+
+One optimizer step of EVERY resident member is a fixed sequence of ~200 kernel
+launches over population-packed NHWC bf16 tensors (images of all members
+concatenated along N, ``img_slot`` maps image -> member row):
+
+  weight_prep  fp32 master rows -> bf16 OHWI (forward) + IHWO (dgrad) layouts
+  memset       BN statistic accumulators, loss
+  prep_input   fp32 NHWC images -> bf16, channels padded 3 -> 16
+  stem         conv_fwd (no input BN)                           -> x0, stats(x0)
+  per block    [proj conv_fwd 1x1 (BN1+ReLU prologue)]          -> sc
+               conv_fwd 3x3 (BN1+ReLU prologue)                 -> h,  stats(h)
+               conv_fwd 3x3 (BN2+ReLU prologue, + residual)     -> x', stats(x')
+  head         final BN+ReLU, GAP, dense, softmax-CE, dense grads, BN-final reductions
+  bn_running   moving averages of every BN of every member
+  backward     head_bwd_apply -> g_L; per block (reverse): conv_b dgrad (+relu mask, BN2 reductions),
+               conv_b wgrad, [proj dgrad + wgrad], conv_a dgrad (BN2-backward prologue, relu mask,
+               BN1 reductions), conv_a wgrad, bn_bwd_apply (+ identity residual) -> g_{l}; stem wgrad
+  optimizer    one fused launch over all members (engine/optim.py semantics), zeroes grads
+
+The whole sequence is captured once per batch composition into a HIP graph
+(``torch.cuda.CUDAGraph``) and replayed; the Python orchestration below runs
+only at capture time.  BN statistics use 8 replicated accumulators per member
+(see ops/csrc/conv.hip).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Dict, List, Sequence, Tuple
+
+import torch
+
+from .. import ops
+from ..models.resnet import BN_EPS
+
+NREP = 8
+c_void_p, c_int, c_long = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
+
+
+class ConvArgs(ctypes.Structure):
+    _fields_ = [
+        ("x", c_void_p), ("x2", c_void_p), ("dy", c_void_p), ("dy2", c_void_p), ("y", c_void_p),
+        ("res", c_void_p), ("xm", c_void_p), ("w", c_void_p), ("w_mstride", c_long), ("w_off", c_long),
+        ("grads", c_void_p), ("g_mstride", c_long), ("g_off", c_long), ("img_slot", c_void_p), ("work", c_void_p),
+        ("params", c_void_p), ("p_mstride", c_long),
+        ("in_gamma", c_int), ("in_beta", c_int), ("ep_gamma", c_int), ("ep_beta", c_int),
+        ("x_gamma", c_int), ("x_beta", c_int),
+        ("st_in", c_void_p), ("st_in_b", c_void_p), ("st_ep", c_void_p), ("st_x", c_void_p), ("st_out", c_void_p),
+        ("cnt", c_void_p), ("Hi", c_int), ("Wi", c_int), ("Ho", c_int), ("Wo", c_int), ("rows", c_int),
+        ("cin_real", c_int),
+    ]
+
+
+class BnBwdArgs(ctypes.Structure):
+    _fields_ = [
+        ("dz", c_void_p), ("x", c_void_p), ("add", c_void_p), ("out", c_void_p), ("img_slot", c_void_p),
+        ("params", c_void_p), ("p_mstride", c_long), ("gamma_off", c_int), ("st_f", c_void_p), ("st_b", c_void_p),
+        ("cnt", c_void_p), ("hw", c_int), ("C", c_int), ("nimg", c_long),
+    ]
+
+
+class HeadArgs(ctypes.Structure):
+    _fields_ = [
+        ("x", c_void_p), ("labels", c_void_p), ("work", c_void_p), ("params", c_void_p), ("p_mstride", c_long),
+        ("gamma_off", c_int), ("beta_off", c_int), ("dw_off", c_int), ("db_off", c_int), ("grads", c_void_p),
+        ("g_mstride", c_long), ("st_f", c_void_p), ("st_b", c_void_p), ("cnt", c_void_p), ("dfeat", c_void_p),
+        ("loss", c_void_p), ("correct", c_void_p), ("logits_out", c_void_p), ("hw", c_int), ("C", c_int),
+        ("ncls", c_int), ("train", c_int),
+    ]
+
+
+_REGISTERED = False
+
+
+def _register():
+    global _REGISTERED
+    if _REGISTERED:
+        return
+    P = ctypes.POINTER
+    ops.register("dtf_conv_fwd", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                  c_void_p])
+    ops.register("dtf_conv_dgrad", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
+    ops.register("dtf_conv_wgrad", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
+    ops.register("dtf_conv_args_size", [])
+    ops.register("dtf_bnbwd_args_size", [])
+    ops.register("dtf_head_args_size", [])
+    ops.register("dtf_prep_input", [c_void_p, c_void_p, c_long, c_int, c_void_p])
+    ops.register("dtf_weight_prep", [c_void_p, c_long, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_long,
+                                     c_void_p])
+    ops.register("dtf_bn_running_update", [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_long, c_void_p,
+                                           c_int, c_void_p, c_void_p])
+    ops.register("dtf_bn_bwd_apply", [P(BnBwdArgs), c_void_p])
+    ops.register("dtf_head", [P(HeadArgs), c_int, c_void_p])
+    ops.register("dtf_head_bwd_apply", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_int,
+                                        c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p])
+    L = ops.lib()
+    # the library may have been loaded before these were registered: (re)bind signatures
+    for name, args in ops._SIGNATURES.items():
+        fn = getattr(L, name, None)
+        if fn is not None:
+            fn.argtypes = args
+            fn.restype = c_int
+    assert L.dtf_conv_args_size() == ctypes.sizeof(ConvArgs), "ConvArgs ABI mismatch"
+    assert L.dtf_bnbwd_args_size() == ctypes.sizeof(BnBwdArgs), "BnBwdArgs ABI mismatch"
+    assert L.dtf_head_args_size() == ctypes.sizeof(HeadArgs), "HeadArgs ABI mismatch"
+    _REGISTERED = True
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _check(err, what):
+    if err != 0:
+        raise RuntimeError("%s: launch error %d (unsupported shape or HIP error)" % (what, err))
+
+
+def _pick_rows(H, W, n_images, align, target_items=2048, max_rows=None):
+    """Largest divisor R of H with R*W % align == 0 and n_images*(H/R) >= target (else smallest valid)."""
+    cands = [r for r in range(1, H + 1) if H % r == 0 and (r * W) % align == 0]
+    if max_rows:
+        cands = [r for r in cands if r <= max_rows] or cands[:1]
+    best = cands[0]
+    for r in cands:
+        if n_images * (H // r) >= target_items:
+            best = r
+    return best
+
+
+class _Layout:
+    """Static (per architecture) tables: conv / BN metadata and buffer offsets."""
+
+    def __init__(self, engine):
+        prog = engine.arch.prog
+        cfg = prog.cfg
+        if cfg.version != 2 or cfg.bottleneck or cfg.image_size != 32:
+            raise ValueError("HIP ResNet backend supports CIFAR-shape v2 building-block nets")
+        self.prog = prog
+        self.cfg = cfg
+        convs = prog.convs
+        # bf16 weight layouts: forward (OHWI, stem padded to 16 input channels) + dgrad (IHWO)
+        self.fwd_off, self.dgr_off = {}, {}
+        off = 0
+        table = []
+        for c in convs:
+            cin_pad = 16 if c.idx == prog.stem else c.cin
+            self.fwd_off[c.idx] = off
+            off += c.cout * c.k * c.k * cin_pad
+            if c.idx != prog.stem:
+                self.dgr_off[c.idx] = off
+                off += c.cout * c.k * c.k * c.cin
+            table.append([c.off, c.cout, c.cin, c.k, cin_pad, self.fwd_off[c.idx], self.dgr_off.get(c.idx, -1), 0])
+        self.wtot = (off + 63) // 64 * 64
+        self.conv_table = table
+        # spatial size of each BN's input
+        self.bn_hw = {}
+        hw = cfg.image_size
+        for blk in prog.blocks:
+            self.bn_hw[blk.bns[0]] = hw * hw
+            hw_out = hw // blk.stride
+            self.bn_hw[blk.bns[1]] = hw_out * hw_out
+            hw = hw_out
+        self.bn_hw[prog.final_bn] = hw * hw
+        self.final_hw = hw * hw
+        self.bn_table = [[b.run_off, b.c, self.bn_hw[b.idx], b.idx] for b in prog.bns]
+
+
+class HipResNetBackend:
+    name = "hip"
+
+    def __init__(self, engine):
+        _register()
+        self.e = engine
+        self.dev = engine.device
+        self.L = _Layout(engine)
+        cap = engine.capacity
+        self.wf = torch.zeros(cap, self.L.wtot, dtype=torch.bfloat16, device=self.dev)
+        self.wd = torch.zeros(cap, self.L.wtot, dtype=torch.bfloat16, device=self.dev)
+        nb = len(self.L.prog.bns)
+        self.stats_bn_stride = cap * NREP * 128
+        # [fwd | bwd] statistic accumulators: zeroed by ONE memset per step
+        self.stats = torch.zeros(2, nb, cap, NREP, 128, dtype=torch.float32, device=self.dev)
+        self.conv_table_t = torch.tensor(self.L.conv_table, dtype=torch.int32, device=self.dev)
+        self.bn_table_t = torch.tensor(self.L.bn_table, dtype=torch.int32, device=self.dev)
+        self.loss = torch.zeros(cap, dtype=torch.float32, device=self.dev)
+        self.correct = torch.zeros(cap, dtype=torch.float32, device=self.dev)
+        self._plans: Dict[tuple, "_StepPlan"] = {}
+        self.use_graph = os.environ.get("DTF_HIP_GRAPH", "1") == "1"
+
+    # --- engine hooks --------------------------------------------------------------
+    def on_params_changed(self, slots):
+        pass  # weight_prep runs at the start of every step (inside the graph)
+
+    def shadow_weights(self):
+        return None
+
+    def st_f(self, bn):
+        return self.stats[0, bn]
+
+    def st_b(self, bn):
+        return self.stats[1, bn]
+
+    # --- plans ------------------------------------------------------------------------
+    def plan(self, slots: Sequence[int], sizes: Sequence[int]) -> "_StepPlan":
+        key = (tuple(slots), tuple(sizes))
+        p = self._plans.get(key)
+        if p is None:
+            if len(self._plans) > 16:
+                self._plans.clear()
+            p = _StepPlan(self, list(slots), list(sizes))
+            self._plans[key] = p
+        return p
+
+    def train_step(self, slots, batches, hparams, lrs):
+        e = self.e
+        sizes = [int(b[1].shape[0]) for b in batches]
+        p = self.plan(slots, sizes)
+        hy = torch.zeros(e.capacity, 8, dtype=torch.float32)
+        from .optim import hyper_row
+        for s, hp, lr in zip(slots, hparams, lrs):
+            hy[s] = torch.tensor(hyper_row(hp, lr, e.host_step[s] + 1, True))
+        e.hyper.copy_(hy, non_blocking=True)
+        p.load_batch(batches)
+        p.run(train=True)
+        return p.loss_view()
+
+    def forward_backward(self, slots, batches):
+        raise RuntimeError("HipResNetBackend runs whole steps: use train_step")
+
+    @torch.no_grad()
+    def infer(self, slot, x):
+        """Eval-mode forward with running statistics (torch reference ops on bf16 shadow math)."""
+        e = self.e
+        return e.arch.forward(e.params[slot], e.running[slot], x, training=False, dtype=torch.bfloat16)
+
+
+class _StepPlan:
+    """Buffers + prebuilt launch list for one batch composition (slots, per-member sizes)."""
+
+    def __init__(self, be: HipResNetBackend, slots: List[int], sizes: List[int]):
+        self.be = be
+        e = be.e
+        self.e = e
+        self.slots = slots
+        self.sizes = sizes
+        dev = be.dev
+        L = be.L
+        prog = L.prog
+        cfg = L.cfg
+        N = sum(sizes)
+        self.N = N
+        img_slot = []
+        self.first = {}
+        for s, n in zip(slots, sizes):
+            self.first[s] = len(img_slot)
+            img_slot += [s] * n
+        self.img_slot = torch.tensor(img_slot, dtype=torch.int32, device=dev)
+        cnt = torch.zeros(e.capacity, dtype=torch.float32)
+        for s, n in zip(slots, sizes):
+            cnt[s] = float(n)
+        self.cnt = cnt.to(dev)
+        self.slots_t = torch.tensor(slots, dtype=torch.int32, device=dev)
+        self.slots_long = torch.tensor(slots, dtype=torch.long, device=dev)
+        H = cfg.image_size
+        self.x_in = torch.zeros(N, H, H, 3, dtype=torch.float32, device=dev)
+        self.labels = torch.zeros(N, dtype=torch.int32, device=dev)
+        self.xin16 = torch.zeros(N, H, H, 16, dtype=torch.bfloat16, device=dev)
+        # forward activations saved for backward
+        self.xs, self.hs, self.scs = [], [], []
+        hw, c = H, cfg.num_filters
+        self.xs.append(torch.empty(N, hw, hw, c, dtype=torch.bfloat16, device=dev))
+        for blk in prog.blocks:
+            ca = prog.convs[blk.convs[0]]
+            hw_o = hw // blk.stride
+            self.hs.append(torch.empty(N, hw_o, hw_o, ca.cout, dtype=torch.bfloat16, device=dev))
+            self.scs.append(torch.empty(N, hw_o, hw_o, ca.cout, dtype=torch.bfloat16, device=dev)
+                            if blk.proj is not None else None)
+            self.xs.append(torch.empty(N, hw_o, hw_o, ca.cout, dtype=torch.bfloat16, device=dev))
+            hw = hw_o
+        # backward temporaries, one set per resolution
+        self.tmp = {}
+        hw, c = H, cfg.num_filters
+        for st in range(len(cfg.block_sizes)):
+            if st > 0:
+                hw //= 2
+            cc = cfg.num_filters * (2 ** st)
+            self.tmp[hw] = dict(g=[torch.empty(N, hw, hw, cc, dtype=torch.bfloat16, device=dev) for _ in range(2)],
+                                dz2=torch.empty(N, hw, hw, cc, dtype=torch.bfloat16, device=dev),
+                                dz1=torch.empty(N, hw, hw, cc, dtype=torch.bfloat16, device=dev))
+        self.pd = {}  # projection dgrad outputs at block-input resolution
+        hw = H
+        for blk in prog.blocks:
+            if blk.proj is not None:
+                ci = prog.convs[blk.proj].cin
+                self.pd[id(blk)] = torch.empty(N, hw, hw, ci, dtype=torch.bfloat16, device=dev)
+            hw //= blk.stride
+        self.dfeat = torch.zeros(N, cfg.final_size, dtype=torch.float32, device=dev)
+        self._work_cache = {}
+        self.launches = []
+        self._build()
+        self.graph = None
+
+    # -------------------------------------------------------------------- work lists
+    def _work_fwd(self, H_out, W_out, align=16, nimg_per=1, target=2048):
+        rows = _pick_rows(H_out, W_out, self.N, align, target)
+        key = ("f", H_out, W_out, rows)
+        w = self._work_cache.get(key)
+        if w is None:
+            items = []
+            bands = H_out // rows
+            for s, n in zip(self.slots, self.sizes):
+                f = self.first[s]
+                for i in range(n):
+                    for b in range(bands):
+                        items.append([f + i, 1, b, s])
+            w = torch.tensor(items, dtype=torch.int32, device=self.be.dev)
+            self._work_cache[key] = w
+        return rows, w
+
+    def _work_member(self, target_items=256, min_chunk=1):
+        key = ("m", target_items)
+        w = self._work_cache.get(key)
+        if w is None:
+            items = []
+            per_member = max(1, target_items // max(1, len(self.slots)))
+            for s, n in zip(self.slots, self.sizes):
+                chunk = max(min_chunk, -(-n // per_member))
+                f = self.first[s]
+                for i in range(0, n, chunk):
+                    items.append([f + i, min(chunk, n - i), 0, s])
+            w = torch.tensor(items, dtype=torch.int32, device=self.be.dev)
+            self._work_cache[key] = w
+        return w
+
+    # -------------------------------------------------------------------- launches
+    def _base_args(self):
+        be, e = self.be, self.e
+        a = ConvArgs()
+        a.img_slot = _p(self.img_slot)
+        a.params = _p(e.state)
+        a.p_mstride = e.S
+        a.cnt = _p(self.cnt)
+        a.w_mstride = be.L.wtot
+        a.grads = _p(e.grads)
+        a.g_mstride = e.Pp
+        a.cin_real = 0
+        return a
+
+    def _bn(self, idx):
+        b = self.be.L.prog.bns[idx]
+        return b.gamma_off, b.beta_off
+
+    def _add(self, fn, *args):
+        self.launches.append((fn, args))
+
+    def _conv_fwd(self, ci, x, y, stats_bn, in_bn, res=None):
+        be, L = self.be, self.be.L
+        c = L.prog.convs[ci]
+        Hi = x.shape[1]
+        Ho = Hi // c.stride
+        rows, work = self._work_fwd(Ho, Ho)
+        a = self._base_args()
+        a.x, a.y, a.res = _p(x), _p(y), _p(res)
+        a.w, a.w_off = _p(be.wf), L.fwd_off[ci]
+        a.work = _p(work)
+        if in_bn is not None:
+            a.in_gamma, a.in_beta = self._bn(in_bn)
+            a.st_in = _p(be.st_f(in_bn))
+        if stats_bn is not None:
+            a.st_out = _p(be.st_f(stats_bn))
+        a.Hi, a.Wi, a.Ho, a.Wo, a.rows = Hi, Hi, Ho, Ho, rows
+        cin = 16 if ci == L.prog.stem else c.cin
+        P = (c.k - 1) // 2
+        rows_in = (rows - 1) * c.stride + c.k
+        lds = 1280 + rows_in * (Hi + 2 * P) * cin * 2
+        mode = 0 if in_bn is None else 1
+        lib = ops.lib()
+        self._add(lib.dtf_conv_fwd, ctypes.byref(a), cin, c.cout, c.stride, c.k, mode, int(res is not None),
+                  int(stats_bn is not None), work.shape[0], lds)
+        self._keep(a)
+
+    def _conv_dgrad(self, ci, dy, y, Hi, mode, epi, dy2=None, in_bn=None, res=None, xm=None, ep_bn=None):
+        be, L = self.be, self.be.L
+        c = L.prog.convs[ci]
+        Ho = Hi // c.stride
+        rows, work = self._work_fwd(Hi, Hi)
+        a = self._base_args()
+        a.x, a.x2, a.y, a.res, a.xm = _p(dy), _p(dy2), _p(y), _p(res), _p(xm)
+        a.w, a.w_off = _p(be.wd), L.dgr_off[ci]
+        a.work = _p(work)
+        if in_bn is not None:
+            a.in_gamma, a.in_beta = self._bn(in_bn)
+            a.st_in, a.st_in_b = _p(be.st_f(in_bn)), _p(be.st_b(in_bn))
+        if ep_bn is not None:
+            a.ep_gamma, a.ep_beta = self._bn(ep_bn)
+            a.st_ep = _p(be.st_f(ep_bn))
+            a.st_out = _p(be.st_b(ep_bn))
+        a.Hi, a.Wi, a.Ho, a.Wo, a.rows = Hi, Hi, Ho, Ho, rows
+        P, S, K = (c.k - 1) // 2, c.stride, c.k
+        lo = rows - 1 + 0  # worst-case dy rows per band
+        rows_t = (rows - 1 + 2 * P) // S + 2
+        lds = 2304 + rows_t * (Ho + 2) * c.cout * 2
+        lib = ops.lib()
+        self._add(lib.dtf_conv_dgrad, ctypes.byref(a), c.cin, c.cout, S, K, mode, epi, work.shape[0], lds)
+        self._keep(a)
+
+    def _conv_wgrad(self, ci, x, dy, mode_x, mode_dy, x_bn=None, dy_bn=None, dy2=None, cin_real=None):
+        be, L, e = self.be, self.be.L, self.e
+        c = L.prog.convs[ci]
+        Hi = x.shape[1]
+        Ho = Hi // c.stride
+        cin = 16 if ci == L.prog.stem else c.cin
+        rows = _pick_rows(Ho, Ho, 1, 32, target_items=1, max_rows=8)
+        # largest band that keeps LDS small: limit rows so the x tile <= ~24 KB
+        work = self._work_member(target_items=256)
+        a = self._base_args()
+        a.x, a.dy, a.dy2 = _p(x), _p(dy), _p(dy2)
+        a.work = _p(work)
+        a.g_off = c.off
+        a.cin_real = c.cin if cin_real is None else cin_real
+        if x_bn is not None:
+            a.x_gamma, a.x_beta = self._bn(x_bn)
+            a.st_x = _p(be.st_f(x_bn))
+        if dy_bn is not None:
+            a.in_gamma, a.in_beta = self._bn(dy_bn)
+            a.st_in, a.st_in_b = _p(be.st_f(dy_bn)), _p(be.st_b(dy_bn))
+        a.Hi, a.Wi, a.Ho, a.Wo, a.rows = Hi, Hi, Ho, Ho, rows
+        P = (c.k - 1) // 2
+        rows_in = (rows - 1) * c.stride + c.k
+        xt = rows_in * (Hi + 2 * P) * cin
+        xt = (xt + 63) // 64 * 64
+        lds = 1536 + xt * 2 + rows * Ho * c.cout * 2
+        lib = ops.lib()
+        self._add(lib.dtf_conv_wgrad, ctypes.byref(a), cin, c.cout, c.stride, c.k, mode_x, mode_dy, work.shape[0], lds)
+        self._keep(a)
+
+    def _keep(self, obj):
+        if not hasattr(self, "_keepalive"):
+            self._keepalive = []
+        self._keepalive.append(obj)
+
+    def _build(self):
+        be, e, L = self.be, self.e, self.be.L
+        prog, cfg = L.prog, L.cfg
+        lib = ops.lib()
+        N = self.N
+        nslots = len(self.slots)
+        # 0. weights for this step
+        self._add(lib.dtf_weight_prep, _p(e.state), e.S, _p(be.conv_table_t), len(L.conv_table), _p(self.slots_t),
+                  nslots, _p(be.wf), _p(be.wd), L.wtot)
+        self._add("zero", be.stats)
+        self._add("zero", be.loss)
+        self._add("zero", be.correct)
+        self._add(lib.dtf_prep_input, _p(self.x_in), _p(self.xin16), N * cfg.image_size * cfg.image_size, 3)
+        # ---------------- forward
+        first_bn = prog.blocks[0].bns[0]
+        self._conv_fwd(prog.stem, self.xin16, self.xs[0], stats_bn=first_bn, in_bn=None)
+        nblk = len(prog.blocks)
+        for i, blk in enumerate(prog.blocks):
+            bn1, bn2 = blk.bns
+            nxt = prog.blocks[i + 1].bns[0] if i + 1 < nblk else prog.final_bn
+            x, h, y = self.xs[i], self.hs[i], self.xs[i + 1]
+            if blk.proj is not None:
+                self._conv_fwd(blk.proj, x, self.scs[i], stats_bn=None, in_bn=bn1)
+            self._conv_fwd(blk.convs[0], x, h, stats_bn=bn2, in_bn=bn1)
+            res = self.scs[i] if blk.proj is not None else x
+            self._conv_fwd(blk.convs[1], h, y, stats_bn=nxt, in_bn=bn2, res=res)
+        # head (fwd + bwd of GAP/dense/CE + final-BN reductions)
+        fb = prog.final_bn
+        hw = L.final_hw
+        hwork = self._work_member(target_items=512)
+        ha = HeadArgs()
+        ha.x, ha.labels, ha.work = _p(self.xs[-1]), _p(self.labels), _p(hwork)
+        ha.params, ha.p_mstride = _p(e.state), e.S
+        ha.gamma_off, ha.beta_off = self._bn(fb)
+        ha.dw_off, ha.db_off = prog.dense_w_off, prog.dense_b_off
+        ha.grads, ha.g_mstride = _p(e.grads), e.Pp
+        ha.st_f, ha.st_b, ha.cnt = _p(be.st_f(fb)), _p(be.st_b(fb)), _p(self.cnt)
+        ha.dfeat, ha.loss, ha.correct = _p(self.dfeat), _p(be.loss), _p(be.correct)
+        ha.logits_out = None
+        ha.hw, ha.C, ha.ncls, ha.train = hw, cfg.final_size, cfg.num_classes, 1
+        self._keep(ha)
+        self._add(lib.dtf_head, ctypes.byref(ha), hwork.shape[0])
+        self._add(lib.dtf_bn_running_update, _p(e.state), e.S, 3 * e.Pp, _p(be.bn_table_t), len(L.bn_table),
+                  _p(be.stats[0]), be.stats_bn_stride, _p(self.slots_t), nslots, _p(self.cnt))
+        # ---------------- backward
+        hwL = self.xs[-1].shape[1]
+        g_cur = self.tmp[hwL]["g"][0]
+        self._add(lib.dtf_head_bwd_apply, _p(self.xs[-1]), _p(self.dfeat), _p(g_cur), _p(self.img_slot), _p(e.state),
+                  e.S, ha.gamma_off, ha.beta_off, _p(be.st_f(fb)), _p(be.st_b(fb)), _p(self.cnt), hw,
+                  cfg.final_size, N)
+        for i in range(nblk - 1, -1, -1):
+            blk = prog.blocks[i]
+            bn1, bn2 = blk.bns
+            x, h = self.xs[i], self.hs[i]
+            Hi, Ho = x.shape[1], h.shape[1]
+            T = self.tmp[Ho]
+            ca, cb = blk.convs
+            # conv_b: dgrad -> dz2 (mask by BN2(h), BN2 reductions); wgrad
+            self._conv_dgrad(cb, g_cur, T["dz2"], Ho, mode=0, epi=2, xm=h, ep_bn=bn2)
+            self._conv_wgrad(cb, h, g_cur, mode_x=1, mode_dy=0, x_bn=bn2)
+            Tin = self.tmp[Hi]
+            pd = None
+            if blk.proj is not None:
+                pd = self.pd[id(blk)]
+                self._conv_dgrad(blk.proj, g_cur, pd, Hi, mode=0, epi=0)
+                self._conv_wgrad(blk.proj, x, g_cur, mode_x=1, mode_dy=0, x_bn=bn1)
+            # conv_a: dgrad of BN2-backward(dz2, h) [+ proj dgrad], mask by BN1(x), BN1 reductions
+            self._conv_dgrad(ca, T["dz2"], Tin["dz1"], Hi, mode=2, epi=2 | (1 if pd is not None else 0), dy2=h,
+                             in_bn=bn2, res=pd, xm=x, ep_bn=bn1)
+            self._conv_wgrad(ca, x, T["dz2"], mode_x=1, mode_dy=2, x_bn=bn1, dy_bn=bn2, dy2=h)
+            # g_in = BN1-backward(dz1, x) [+ g_out if identity shortcut]
+            g_next = Tin["g"][1] if g_cur is Tin["g"][0] else Tin["g"][0]
+            ba = BnBwdArgs()
+            ba.dz, ba.x, ba.add, ba.out = _p(Tin["dz1"]), _p(x), (None if blk.proj is not None else _p(g_cur)), \
+                _p(g_next)
+            ba.img_slot, ba.params, ba.p_mstride = _p(self.img_slot), _p(e.state), e.S
+            ba.gamma_off = self._bn(bn1)[0]
+            ba.st_f, ba.st_b, ba.cnt = _p(be.st_f(bn1)), _p(be.st_b(bn1)), _p(self.cnt)
+            ba.hw, ba.C, ba.nimg = Hi * Hi, x.shape[3], N
+            self._keep(ba)
+            self._add(lib.dtf_bn_bwd_apply, ctypes.byref(ba))
+            g_cur = g_next
+        # stem wgrad (input = padded image, real channels 3)
+        self._conv_wgrad(prog.stem, self.xin16, g_cur, mode_x=0, mode_dy=0, cin_real=cfg.in_channels)
+        # optimizer over every member row (+ zero grads), step counters
+        self._add("optim", None)
+        self._add("step", None)
+
+    # -------------------------------------------------------------------- execution
+    def load_batch(self, batches):
+        off = 0
+        for (x, y) in batches:
+            n = x.shape[0]
+            self.x_in[off:off + n].copy_(x.reshape(n, *self.x_in.shape[1:]), non_blocking=True)
+            self.labels[off:off + n].copy_(y, non_blocking=True)
+            off += n
+
+    def _run_eager(self):
+        stream = ops.stream()
+        e = self.e
+        for fn, args in self.launches:
+            if fn == "zero":
+                args[0].zero_()
+            elif fn == "optim":
+                ops.fused_optimizer(e.state, e.grads, e.hyper, e.Pp, e.P, e.n_reg, shadow=None, zero_grads=True)
+            elif fn == "step":
+                e.step_col().index_add_(0, self.slots_long, torch.ones(len(self.slots), device=e.device))
+            else:
+                err = fn(*args, ops.stream())
+                if err != 0:
+                    raise RuntimeError("kernel launch %s failed with %d" % (getattr(fn, "__name__", fn), err))
+
+    def run(self, train=True):
+        be = self.be
+        if be.use_graph and self.graph is None and os.environ.get("DTF_HIP_GRAPH", "1") == "1":
+            # warm up once eagerly (allocator, lazy init), then capture
+            self._run_eager()
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                g.capture_begin()
+                self._run_eager()
+                g.capture_end()
+            torch.cuda.current_stream().wait_stream(s)
+            self.graph = g
+            self._captured_once = True
+            return  # the warm-up executed this step
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._run_eager()
+
+    def loss_view(self):
+        return self.be.loss[self.slots_long].clone()

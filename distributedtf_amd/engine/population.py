@@ -125,6 +125,12 @@ class PopulationEngine:
                    hparams: Sequence[Dict], lrs: Sequence[float]) -> torch.Tensor:
         """One optimizer step for ``slots`` (each with its own batch). Returns
         per-member cross-entropy losses (device tensor)."""
+        if hasattr(self.backend, "train_step"):
+            # whole step (fwd, bwd, optimizer, step counters) inside one HIP graph
+            losses = self.backend.train_step(slots, batches, hparams, lrs)
+            for s in slots:
+                self.host_step[s] += 1
+            return losses
         hy = torch.zeros(self.capacity, _optim.N_HYPER, dtype=torch.float32)
         for s, hp, lr in zip(slots, hparams, lrs):
             hy[s] = torch.tensor(_optim.hyper_row(hp, lr, self.host_step[s] + 1, True))

@@ -1,0 +1,636 @@
+// Population-batched implicit-GEMM convolutions for the CIFAR ResNet hot path (gfx950).
+//
+// Tensors are NHWC bf16 with the images of ALL population members packed along N
+// (img_slot[n] = member slot of image n), so one launch serves the whole population
+// and the grid is >> 256 CUs even at per-member batch 65.  Weights are per member:
+// bf16 rows `w + slot*w_mstride + w_off`.
+//
+// MFMA: v_mfma_f32_16x16x32_bf16, A = weights (16 output channels x 32 k),
+// B = activations (32 k x 16 pixels), k = (tap, channel) flattened exactly like the
+// OHWI weight layout, so a lane's 8 k-values are 16 contiguous bytes in both LDS
+// (NHWC tile) and the weight row.  The C/D fragment (4 consecutive channels of one
+// pixel per lane) is stored as one 8-byte packed bf16 write, and a 16-pixel tile
+// of a 16-channel layer is a single contiguous 512-byte store.
+//
+// LDS tiles: [rows][cols][C] bf16 with a zero halo; the 16-byte channel chunks of
+// each pixel are XOR-swizzled by the column index to spread ds_read_b128 lane
+// groups over banks.  The producing BatchNorm (+ReLU) of the input is applied
+// while the tile is staged (global -> regs -> transform -> LDS), and BN statistics
+// of the output are reduced in registers/LDS and added to 8 replicated per-member
+// accumulators (cuts same-address atomic contention 8x); consumers sum the
+// replicas when they derive their per-channel coefficients.
+//
+//  conv_fwd   : y = conv(T_in(x)) [+ res]           epilogue: sum(y), sum(y^2)
+//  conv_dgrad : dx = conv^T(T_dy(dy)) [+ add]       epilogue: relu-mask by BN(x) + sum(dz), sum(dz*xhat)
+//  conv_wgrad : dW += sum_pix T_dy(dy) (x) T_x(x)   operand fragments via ds_read_b64_tr_b16
+// T_* in {identity, BN+ReLU (fwd), BN-backward apply A*dz + B*h + C}.
+#include "common.h"
+
+#define BN_EPS 1e-5f
+#define NREP 8
+
+namespace {
+
+struct ConvArgs {
+  const bf16_t* x;    // primary input (fwd: x; dgrad: dy (or dz of the next BN); wgrad: x)
+  const bf16_t* x2;   // second input of a BN-backward transform (the BN's forward input h)
+  const bf16_t* dy;   // wgrad: dY (or dz)
+  const bf16_t* dy2;  // wgrad: BN-backward second input
+  bf16_t* y;          // output
+  const bf16_t* res;  // fwd: residual to add / dgrad: tensor to add before the mask
+  const bf16_t* xm;   // dgrad epilogue: forward input x of the masking BN
+  const bf16_t* w;    // bf16 weights (fwd OHWI / dgrad IHWO)
+  long w_mstride;
+  long w_off;
+  float* grads;       // wgrad output (fp32, atomically accumulated)
+  long g_mstride;
+  long g_off;
+  const int* img_slot;
+  const int4* work;   // per-WG work item: (img0, nimg, band, slot)
+  const float* params;  // fp32 state rows (gamma / beta)
+  long p_mstride;
+  int in_gamma, in_beta;    // BN applied to the input (fwd) or BN whose backward is applied (dgrad/wgrad dy)
+  int ep_gamma, ep_beta;    // BN used by the dgrad epilogue mask
+  int x_gamma, x_beta;      // wgrad: BN applied to x
+  const float* st_in;       // fwd stats of the input-side BN      [cap][NREP][2][64]
+  const float* st_in_b;     // bwd stats of the input-side BN
+  const float* st_ep;       // fwd stats of the epilogue BN
+  const float* st_x;        // wgrad: fwd stats of x's BN
+  float* st_out;            // stats produced by this kernel
+  const float* cnt;         // per-slot image count (float)
+  int Hi, Wi, Ho, Wo;       // forward input / output spatial dims
+  int rows;                 // rows per band (output rows for fwd/wgrad, dx rows for dgrad)
+  int cin_real;             // wgrad: real input channels (stem: 3)
+};
+
+__device__ __forceinline__ const float* stats_row(const float* base, int slot) {
+  return base + (long)slot * NREP * 128;
+}
+
+// Sum the NREP replicas: returns (sum, sumsq) of channel c.
+__device__ __forceinline__ void stats_sum(const float* row, int c, float& s, float& q) {
+  s = 0.f;
+  q = 0.f;
+#pragma unroll
+  for (int r = 0; r < NREP; ++r) {
+    s += row[r * 128 + c];
+    q += row[r * 128 + 64 + c];
+  }
+}
+
+// Forward BN coefficients: y = x*scale + shift ; also mean / inv-std.
+__device__ __forceinline__ void bn_fwd_coef(const float* st, float n, float gamma, float beta, int c, float& scale,
+                                            float& shift, float& mean, float& inv) {
+  float s, q;
+  stats_sum(st, c, s, q);
+  mean = s / n;
+  float var = fmaxf(q / n - mean * mean, 0.f);
+  inv = rsqrtf(var + BN_EPS);
+  scale = gamma * inv;
+  shift = beta - mean * scale;
+}
+
+// Backward BN apply: dh = A*dz + B*h + C  (training-mode BN gradient).
+__device__ __forceinline__ void bn_bwd_coef(const float* stf, const float* stb, float n, float gamma, int c, float& A,
+                                            float& B, float& C) {
+  float scale, shift, mean, inv;
+  bn_fwd_coef(stf, n, gamma, 0.f, c, scale, shift, mean, inv);
+  float sdz, sdzx;
+  stats_sum(stb, c, sdz, sdzx);
+  float mdz = sdz / n, mdzx = sdzx / n;
+  A = scale;
+  B = -scale * inv * mdzx;
+  C = -scale * mdz + scale * inv * mean * mdzx;
+}
+
+template <int C>
+__device__ __forceinline__ int lds_off(int r, int col, int wp, int chunk) {
+  constexpr int NCH = C / 8;
+  return (r * wp + col) * C + ((chunk ^ (col & (NCH - 1))) << 3);
+}
+
+// Stage a [rows_in][wp][C] tile starting at global row gy0 / col gx0 (halo -> 0).
+// MODE 0: copy, 1: relu(x*c0+c1), 2: c0*x + c1*x2 + c2 (BN backward apply).
+template <int C, int MODE>
+__device__ __forceinline__ void stage_tile(bf16_t* __restrict__ tile, const bf16_t* __restrict__ src,
+                                           const bf16_t* __restrict__ src2, int gy0, int rows_in, int gx0, int wp,
+                                           int H, int W, const float* __restrict__ coef) {
+  constexpr int NCH = C / 8;
+  const int total = rows_in * wp * NCH;
+  for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+    const int chunk = idx % NCH;
+    const int pc = idx / NCH;
+    const int col = pc % wp;
+    const int r = pc / wp;
+    const int gy = gy0 + r, gx = gx0 + col;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+      const long off = ((long)gy * W + gx) * C + chunk * 8;
+      v = *reinterpret_cast<const uint4*>(src + off);
+      if constexpr (MODE != 0) {
+        uint4 v2 = make_uint4(0, 0, 0, 0);
+        if constexpr (MODE == 2) v2 = *reinterpret_cast<const uint4*>(src2 + off);
+        uint32_t w32[4] = {v.x, v.y, v.z, v.w};
+        uint32_t h32[4] = {v2.x, v2.y, v2.z, v2.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = chunk * 8 + 2 * j;
+          float a0 = bf2f((bf16_t)(w32[j] & 0xffff)), a1 = bf2f((bf16_t)(w32[j] >> 16));
+          if constexpr (MODE == 1) {
+            a0 = fmaxf(a0 * coef[c] + coef[64 + c], 0.f);
+            a1 = fmaxf(a1 * coef[c + 1] + coef[64 + c + 1], 0.f);
+          } else {
+            float h0 = bf2f((bf16_t)(h32[j] & 0xffff)), h1 = bf2f((bf16_t)(h32[j] >> 16));
+            a0 = coef[c] * a0 + coef[64 + c] * h0 + coef[128 + c];
+            a1 = coef[c + 1] * a1 + coef[64 + c + 1] * h1 + coef[128 + c + 1];
+          }
+          w32[j] = pack2bf(a0, a1);
+        }
+        v = make_uint4(w32[0], w32[1], w32[2], w32[3]);
+      }
+    }
+    *reinterpret_cast<uint4*>(tile + lds_off<C>(r, col, wp, chunk)) = v;
+  }
+}
+
+// Per-channel transform coefficients into coef[0..191] for MODE 1 / 2.
+template <int C, int MODE>
+__device__ __forceinline__ void make_coef(float* coef, const ConvArgs& a, int slot, float n, const float* st_f,
+                                          const float* st_b, int g_off, int b_off) {
+  if constexpr (MODE == 0) return;
+  const int c = threadIdx.x;
+  if (c < C) {
+    const float* prow = a.params + (long)slot * a.p_mstride;
+    if constexpr (MODE == 1) {
+      float scale, shift, mean, inv;
+      bn_fwd_coef(stats_row(st_f, slot), n, prow[g_off + c], prow[b_off + c], c, scale, shift, mean, inv);
+      coef[c] = scale;
+      coef[64 + c] = shift;
+    } else {
+      float A, B, Cc;
+      bn_bwd_coef(stats_row(st_f, slot), stats_row(st_b, slot), n, prow[g_off + c], c, A, B, Cc);
+      coef[c] = A;
+      coef[64 + c] = B;
+      coef[128 + c] = Cc;
+    }
+  }
+}
+
+__device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// Reduce per-lane partial channel sums (4 channels per lane, 16 lanes share them)
+// into LDS accumulators acc_lds[2][64] (sum, second moment).
+__device__ __forceinline__ void reduce_stats_to_lds(float* acc_lds, const float (&s)[4], const float (&q)[4], int ch0,
+                                                    int lane) {
+  float ss[4], qq[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float a = s[r], b = q[r];
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      a += __shfl_xor(a, o, 64);
+      b += __shfl_xor(b, o, 64);
+    }
+    ss[r] = a;
+    qq[r] = b;
+  }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      atomicAdd(&acc_lds[ch0 + r], ss[r]);
+      atomicAdd(&acc_lds[64 + ch0 + r], qq[r]);
+    }
+  }
+}
+
+__device__ __forceinline__ void flush_stats(float* st_out, const float* acc_lds, int slot, int nch) {
+  const int t = threadIdx.x;
+  if (t < 2 * nch) {
+    const int which = t / nch, c = t % nch;
+    float* row = st_out + (long)slot * NREP * 128 + (blockIdx.x & (NREP - 1)) * 128;
+    atomicAdd(&row[which * 64 + c], acc_lds[which * 64 + c]);
+  }
+}
+
+// --------------------------------------------------------------------------------- forward
+
+template <int CIN, int COUT, int S, int K, int MODE_IN, bool RESID, bool STATS>
+__global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
+  constexpr int NT = COUT / 16;
+  constexpr int WPT = 4 / NT;
+  constexpr int KTOT = K * K * CIN;
+  constexpr int KS = (KTOT + 31) / 32;
+  constexpr int P = (K - 1) / 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* coef = reinterpret_cast<float*>(smem);          // 192 floats
+  float* acc_lds = coef + 192;                           // 128 floats
+  bf16_t* tile = reinterpret_cast<bf16_t*>(smem + 1280);
+
+  const int4 wk = a.work[blockIdx.x];
+  const int img0 = wk.x, nimg = wk.y, band = wk.z, slot = wk.w;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const float n_in = a.cnt[slot] * (float)(a.Hi * a.Wi);
+  make_coef<CIN, MODE_IN>(coef, a, slot, n_in, a.st_in, a.st_in_b, a.in_gamma, a.in_beta);
+  if (STATS && threadIdx.x < 128) acc_lds[threadIdx.x] = 0.f;
+
+  const int ct = wave % NT;
+  bf16x8_t afr[KS];
+  {
+    const bf16_t* wb = a.w + (long)slot * a.w_mstride + a.w_off + (long)(ct * 16 + (lane & 15)) * KTOT;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int k0 = 32 * s + 8 * (lane >> 4);
+      bf16x8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (k0 < KTOT) v = *reinterpret_cast<const bf16x8_t*>(wb + k0);
+      afr[s] = v;
+    }
+  }
+  const int rows = a.rows;
+  const int oy0 = band * rows;
+  const int rows_in = (rows - 1) * S + K;
+  const int wp = a.Wi + 2 * P;
+  const int ntiles = rows * a.Wo / 16;
+  float ssum[4] = {0.f, 0.f, 0.f, 0.f}, ssq[4] = {0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+
+  for (int im = 0; im < nimg; ++im) {
+    const int img = img0 + im;
+    stage_tile<CIN, MODE_IN>(tile, a.x + (long)img * a.Hi * a.Wi * CIN, nullptr, oy0 * S - P, rows_in, -P, wp, a.Hi,
+                             a.Wi, coef);
+    __syncthreads();
+    for (int t = wave / NT; t < ntiles; t += WPT) {
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+      const int p = t * 16 + (lane & 15);
+      const int oy = p / a.Wo, ox = p % a.Wo;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int k0 = 32 * s + 8 * (lane >> 4);
+        bf16x8_t b = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (k0 < KTOT) {
+          const int tap = k0 / CIN, c0 = k0 % CIN;
+          const int ky = tap / K, kx = tap % K;
+          b = *reinterpret_cast<const bf16x8_t*>(tile + lds_off<CIN>(oy * S + ky, ox * S + kx, wp, c0 >> 3));
+        }
+        acc = mfma16(afr[s], b, acc);
+      }
+      const int co0 = ct * 16 + (lane >> 4) * 4;
+      const long o = (((long)img * a.Ho + oy0 + oy) * a.Wo + ox) * COUT + co0;
+      float v[4] = {acc[0], acc[1], acc[2], acc[3]};
+      if constexpr (RESID) {
+        const uint2 r = *reinterpret_cast<const uint2*>(a.res + o);
+        v[0] += bf2f((bf16_t)(r.x & 0xffff));
+        v[1] += bf2f((bf16_t)(r.x >> 16));
+        v[2] += bf2f((bf16_t)(r.y & 0xffff));
+        v[3] += bf2f((bf16_t)(r.y >> 16));
+      }
+      uint2 pk;
+      pk.x = pack2bf(v[0], v[1]);
+      pk.y = pack2bf(v[2], v[3]);
+      *reinterpret_cast<uint2*>(a.y + o) = pk;
+      if constexpr (STATS) {
+        const float r0 = bf2f((bf16_t)(pk.x & 0xffff)), r1 = bf2f((bf16_t)(pk.x >> 16));
+        const float r2 = bf2f((bf16_t)(pk.y & 0xffff)), r3 = bf2f((bf16_t)(pk.y >> 16));
+        ssum[0] += r0; ssq[0] += r0 * r0;
+        ssum[1] += r1; ssq[1] += r1 * r1;
+        ssum[2] += r2; ssq[2] += r2 * r2;
+        ssum[3] += r3; ssq[3] += r3 * r3;
+      }
+    }
+    __syncthreads();
+  }
+  if constexpr (STATS) {
+    reduce_stats_to_lds(acc_lds, ssum, ssq, ct * 16 + (lane >> 4) * 4, lane);
+    __syncthreads();
+    flush_stats(a.st_out, acc_lds, slot, COUT);
+  }
+}
+
+// ---------------------------------------------------------------------------------- dgrad
+// dx[iy,ix,ci] = sum_{ky,kx,co} dy[(iy+P-ky)/S, (ix+P-kx)/S, co] * W[co,ky,kx,ci]
+// Weights in IHWO layout: wt[ci][tap][co] (rows of the A operand are ci).
+// EPI bit0: add `res` (another dx contribution) before the epilogue;
+// EPI bit1: mask by relu(BN_ep(xm)) and accumulate sum(dz), sum(dz*xhat) of BN_ep.
+
+template <int CI, int CO, int S, int K, int MODE_IN, int EPI>
+__global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
+  constexpr int NT = CI / 16;
+  constexpr int WPT = 4 / NT;
+  constexpr int KTOT = K * K * CO;
+  constexpr int KS = (KTOT + 31) / 32;
+  constexpr int P = (K - 1) / 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* coef = reinterpret_cast<float*>(smem);   // input transform (192)
+  float* ecoef = coef + 192;                      // epilogue BN: scale, shift, mean, inv (4 x 64)
+  float* acc_lds = ecoef + 256;                   // 128
+  bf16_t* tile = reinterpret_cast<bf16_t*>(smem + 2304);
+
+  const int4 wk = a.work[blockIdx.x];
+  const int img0 = wk.x, nimg = wk.y, band = wk.z, slot = wk.w;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // dy lives at the forward-output resolution; the BN transformed on load is the one after this conv.
+  make_coef<CO, MODE_IN>(coef, a, slot, a.cnt[slot] * (float)(a.Ho * a.Wo), a.st_in, a.st_in_b, a.in_gamma, a.in_beta);
+  if constexpr (EPI & 2) {
+    const int c = threadIdx.x;
+    if (c < CI) {
+      const float* prow = a.params + (long)slot * a.p_mstride;
+      float scale, shift, mean, inv;
+      bn_fwd_coef(stats_row(a.st_ep, slot), a.cnt[slot] * (float)(a.Hi * a.Wi), prow[a.ep_gamma + c],
+                  prow[a.ep_beta + c], c, scale, shift, mean, inv);
+      ecoef[c] = scale;
+      ecoef[64 + c] = shift;
+      ecoef[128 + c] = mean;
+      ecoef[192 + c] = inv;
+    }
+    if (threadIdx.x < 128) acc_lds[threadIdx.x] = 0.f;
+  }
+  const int ct = wave % NT;
+  bf16x8_t afr[KS];
+  {
+    const bf16_t* wb = a.w + (long)slot * a.w_mstride + a.w_off + (long)(ct * 16 + (lane & 15)) * KTOT;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int k0 = 32 * s + 8 * (lane >> 4);
+      bf16x8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (k0 < KTOT) v = *reinterpret_cast<const bf16x8_t*>(wb + k0);
+      afr[s] = v;
+    }
+  }
+  const int rows = a.rows;
+  const int iy0 = band * rows;
+  // rows of dy needed: oy in [floor((iy0+P-K+1)/S), floor((iy0+rows-1+P)/S)]
+  int lo_num = iy0 + P - K + 1;
+  const int oy_lo = lo_num >= 0 ? lo_num / S : -((-lo_num + S - 1) / S);
+  const int oy_hi = (iy0 + rows - 1 + P) / S;
+  const int rows_t = oy_hi - oy_lo + 1;
+  const int wp = a.Wo + 2;  // dy cols -1..Wo
+  const int ntiles = rows * a.Wi / 16;
+  float ssum[4] = {0.f, 0.f, 0.f, 0.f}, ssq[4] = {0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+
+  for (int im = 0; im < nimg; ++im) {
+    const int img = img0 + im;
+    const long ioff = (long)img * a.Ho * a.Wo * CO;
+    stage_tile<CO, MODE_IN>(tile, a.x + ioff, a.x2 ? a.x2 + ioff : nullptr, oy_lo, rows_t, -1, wp, a.Ho, a.Wo, coef);
+    __syncthreads();
+    for (int t = wave / NT; t < ntiles; t += WPT) {
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+      const int p = t * 16 + (lane & 15);
+      const int iy = iy0 + p / a.Wi, ix = p % a.Wi;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int k0 = 32 * s + 8 * (lane >> 4);
+        bf16x8_t b = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (k0 < KTOT) {
+          const int tap = k0 / CO, c0 = k0 % CO;
+          const int ky = tap / K, kx = tap % K;
+          const int ty = iy + P - ky, tx = ix + P - kx;
+          bool ok = true;
+          int oy = ty, ox = tx;
+          if constexpr (S > 1) {
+            ok = (ty >= 0) && (tx >= 0) && (ty % S == 0) && (tx % S == 0);
+            oy = ty / S;
+            ox = tx / S;
+          }
+          const int lr = oy - oy_lo, lc = ox + 1;
+          if (ok && lr >= 0 && lr < rows_t && lc >= 0 && lc < wp)
+            b = *reinterpret_cast<const bf16x8_t*>(tile + lds_off<CO>(lr, lc, wp, c0 >> 3));
+        }
+        acc = mfma16(afr[s], b, acc);
+      }
+      const int ci0 = ct * 16 + (lane >> 4) * 4;
+      const long o = (((long)img * a.Hi + iy) * a.Wi + ix) * CI + ci0;
+      float v[4] = {acc[0], acc[1], acc[2], acc[3]};
+      if constexpr (EPI & 1) {
+        const uint2 r = *reinterpret_cast<const uint2*>(a.res + o);
+        v[0] += bf2f((bf16_t)(r.x & 0xffff));
+        v[1] += bf2f((bf16_t)(r.x >> 16));
+        v[2] += bf2f((bf16_t)(r.y & 0xffff));
+        v[3] += bf2f((bf16_t)(r.y >> 16));
+      }
+      if constexpr (EPI & 2) {
+        const uint2 xr = *reinterpret_cast<const uint2*>(a.xm + o);
+        const float xv[4] = {bf2f((bf16_t)(xr.x & 0xffff)), bf2f((bf16_t)(xr.x >> 16)), bf2f((bf16_t)(xr.y & 0xffff)),
+                             bf2f((bf16_t)(xr.y >> 16))};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = ci0 + r;
+          const float pre = xv[r] * ecoef[c] + ecoef[64 + c];
+          v[r] = pre > 0.f ? v[r] : 0.f;
+        }
+      }
+      uint2 pk;
+      pk.x = pack2bf(v[0], v[1]);
+      pk.y = pack2bf(v[2], v[3]);
+      *reinterpret_cast<uint2*>(a.y + o) = pk;
+      if constexpr (EPI & 2) {
+        const uint2 xr = *reinterpret_cast<const uint2*>(a.xm + o);
+        const float xv[4] = {bf2f((bf16_t)(xr.x & 0xffff)), bf2f((bf16_t)(xr.x >> 16)), bf2f((bf16_t)(xr.y & 0xffff)),
+                             bf2f((bf16_t)(xr.y >> 16))};
+        const float dz[4] = {bf2f((bf16_t)(pk.x & 0xffff)), bf2f((bf16_t)(pk.x >> 16)), bf2f((bf16_t)(pk.y & 0xffff)),
+                             bf2f((bf16_t)(pk.y >> 16))};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = ci0 + r;
+          ssum[r] += dz[r];
+          ssq[r] += dz[r] * (xv[r] - ecoef[128 + c]) * ecoef[192 + c];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if constexpr (EPI & 2) {
+    reduce_stats_to_lds(acc_lds, ssum, ssq, ct * 16 + (lane >> 4) * 4, lane);
+    __syncthreads();
+    flush_stats(a.st_out, acc_lds, slot, CI);
+  }
+}
+
+// ---------------------------------------------------------------------------------- wgrad
+// dW[co][ky][kx][ci] += sum_{pix} dy[pix][co] * x(pix*S + tap - P)[ci]
+// GEMM M = co, N = (tap, ci), reduction over the output pixels of the WG's images.
+// Both operands are "k = pixel" fragments, read from NHWC LDS tiles with
+// ds_read_b64_tr_b16 (4 pixel-rows x 16 channel-columns, delivered column-major).
+
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ s16x4_t ds_read_tr(const bf16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p));
+}
+
+template <int CIN, int COUT, int S, int K, int MODE_X, int MODE_DY>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
+  constexpr int MT = COUT / 16;
+  constexpr int NTN = K * K * CIN / 16;  // n-tiles: (tap, 16-channel chunk)
+  constexpr int NJ = (NTN + 3) / 4;
+  constexpr int P = (K - 1) / 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* coef_x = reinterpret_cast<float*>(smem);  // 192
+  float* coef_d = coef_x + 192;                   // 192
+  bf16_t* xt = reinterpret_cast<bf16_t*>(smem + 1536);
+
+  const int4 wk = a.work[blockIdx.x];
+  const int img0 = wk.x, nimg = wk.y, slot = wk.w;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  make_coef<CIN, MODE_X>(coef_x, a, slot, a.cnt[slot] * (float)(a.Hi * a.Wi), a.st_x, nullptr, a.x_gamma, a.x_beta);
+  make_coef<COUT, MODE_DY>(coef_d, a, slot, a.cnt[slot] * (float)(a.Ho * a.Wo), a.st_in, a.st_in_b, a.in_gamma,
+                           a.in_beta);
+  const int rows = a.rows;
+  const int rows_in = (rows - 1) * S + K;
+  const int wpx = a.Wi + 2 * P;
+  bf16_t* dt = xt + ((rows_in * wpx * CIN + 63) & ~63);
+  const int npix = rows * a.Wo;
+  const int bands = a.Ho / rows;
+
+  f32x4_t acc[NJ][MT];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[j][m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p4 = i & 3;
+  __syncthreads();
+  for (int im = 0; im < nimg; ++im) {
+    const int img = img0 + im;
+    for (int band = 0; band < bands; ++band) {
+      const int oy0 = band * rows;
+      const long xo = (long)img * a.Hi * a.Wi * CIN;
+      const long yo = (long)img * a.Ho * a.Wo * COUT;
+      stage_tile<CIN, MODE_X>(xt, a.x + xo, nullptr, oy0 * S - P, rows_in, -P, wpx, a.Hi, a.Wi, coef_x);
+      stage_tile<COUT, MODE_DY>(dt, a.dy + yo, a.dy2 ? a.dy2 + yo : nullptr, oy0, rows, 0, a.Wo, a.Ho, a.Wo, coef_d);
+      __syncthreads();
+      for (int k0 = 0; k0 < npix; k0 += 32) {
+        // pixel rows delivered to this lane group: k0 + 8g + q (+4)
+        const int pa = k0 + 8 * g + q, pb = pa + 4;
+        const int ya = pa / a.Wo, xa = pa % a.Wo, yb = pb / a.Wo, xb = pb % a.Wo;
+        bf16x8_t af[MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const int ch = m * 16 + 4 * p4;
+          s16x4_t lo = ds_read_tr(dt + lds_off<COUT>(ya, xa, a.Wo, ch >> 3) + (ch & 7));
+          s16x4_t hi = ds_read_tr(dt + lds_off<COUT>(yb, xb, a.Wo, ch >> 3) + (ch & 7));
+          af[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int nt = wave + 4 * j;
+          if (nt < NTN) {
+            const int tap = (nt * 16) / CIN, cb = (nt * 16) % CIN;
+            const int ky = tap / K, kx = tap % K;
+            const int ch = cb + 4 * p4;
+            s16x4_t lo = ds_read_tr(xt + lds_off<CIN>(ya * S + ky, xa * S + kx, wpx, ch >> 3) + (ch & 7));
+            s16x4_t hi = ds_read_tr(xt + lds_off<CIN>(yb * S + ky, xb * S + kx, wpx, ch >> 3) + (ch & 7));
+            const bf16x8_t bfr = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+            for (int m = 0; m < MT; ++m) acc[j][m] = mfma16(af[m], bfr, acc[j][m]);
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // epilogue: D[co][n] with co = m*16 + 4*(lane>>4) + r, n-col = lane & 15
+  float* gb = a.grads + (long)slot * a.g_mstride + a.g_off;
+  const int KK = K * K;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int nt = wave + 4 * j;
+    if (nt < NTN) {
+      const int tap = (nt * 16) / CIN, ci = (nt * 16) % CIN + (lane & 15);
+      if (ci < a.cin_real) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int co = m * 16 + 4 * (lane >> 4) + r;
+            atomicAdd(gb + ((long)co * KK + tap) * a.cin_real + ci, acc[j][m][r]);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <typename KernelT>
+int launch(KernelT k, int nblocks, size_t lds, hipStream_t st, const ConvArgs& a) {
+  if (nblocks <= 0) return 0;
+  hipLaunchKernelGGL(k, dim3(nblocks), dim3(256), lds, st, a);
+  return DTF_CHECK_LAUNCH();
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------ dispatch
+// cfg: CIN, COUT, S, K and the mode flags select one instantiation.
+
+#define FWD_CASE(CI, CO, S, K, M, R, ST)                                                             \
+  if (cin == CI && cout == CO && s == S && k == K && mode == M && resid == R && stats == ST)         \
+    return launch(conv_fwd_kernel<CI, CO, S, K, M, R, ST>, nblocks, lds, stream, *args);
+
+#define DGRAD_CASE(CI, CO, S, K, M, E)                                                               \
+  if (cin == CI && cout == CO && s == S && k == K && mode == M && epi == E)                          \
+    return launch(conv_dgrad_kernel<CI, CO, S, K, M, E>, nblocks, lds, stream, *args);
+
+#define WGRAD_CASE(CI, CO, S, K, MX, MD)                                                             \
+  if (cin == CI && cout == CO && s == S && k == K && mode_x == MX && mode_dy == MD)                  \
+    return launch(conv_wgrad_kernel<CI, CO, S, K, MX, MD>, nblocks, lds, stream, *args);
+
+DTF_API int dtf_conv_args_size() { return (int)sizeof(ConvArgs); }
+
+DTF_API int dtf_conv_fwd(const ConvArgs* args, int cin, int cout, int s, int k, int mode, int resid, int stats,
+                         int nblocks, int lds, hipStream_t stream) {
+  // stem (input padded to 16 channels, no input BN)
+  FWD_CASE(16, 16, 1, 3, 0, false, true)
+  // stage convs: conv_a (BN1+ReLU on the block input), conv_b (BN2+ReLU, + residual)
+  FWD_CASE(16, 16, 1, 3, 1, false, true)
+  FWD_CASE(16, 16, 1, 3, 1, true, true)
+  FWD_CASE(32, 32, 1, 3, 1, false, true)
+  FWD_CASE(32, 32, 1, 3, 1, true, true)
+  FWD_CASE(64, 64, 1, 3, 1, false, true)
+  FWD_CASE(64, 64, 1, 3, 1, true, true)
+  FWD_CASE(16, 32, 2, 3, 1, false, true)
+  FWD_CASE(32, 64, 2, 3, 1, false, true)
+  // projection shortcuts (1x1, on the pre-activated block input; no stats)
+  FWD_CASE(16, 16, 1, 1, 1, false, false)
+  FWD_CASE(16, 32, 2, 1, 1, false, false)
+  FWD_CASE(32, 64, 2, 1, 1, false, false)
+  return -1;
+}
+
+DTF_API int dtf_conv_dgrad(const ConvArgs* args, int cin, int cout, int s, int k, int mode, int epi, int nblocks,
+                           int lds, hipStream_t stream) {
+  // conv_b dgrad: dy = residual-stream grad (plain), epilogue: mask by BN2(h) + stats
+  DGRAD_CASE(16, 16, 1, 3, 0, 2)
+  DGRAD_CASE(32, 32, 1, 3, 0, 2)
+  DGRAD_CASE(64, 64, 1, 3, 0, 2)
+  // conv_a dgrad: dy = BN2-backward(dz2, h); epilogue: [+ proj dgrad] mask by BN1(x) + stats
+  DGRAD_CASE(16, 16, 1, 3, 2, 2)
+  DGRAD_CASE(32, 32, 1, 3, 2, 2)
+  DGRAD_CASE(64, 64, 1, 3, 2, 2)
+  DGRAD_CASE(16, 16, 1, 3, 2, 3)
+  DGRAD_CASE(16, 32, 2, 3, 2, 3)
+  DGRAD_CASE(32, 64, 2, 3, 2, 3)
+  // projection dgrad (1x1): plain dy, plain output (added by the conv_a dgrad epilogue)
+  DGRAD_CASE(16, 16, 1, 1, 0, 0)
+  DGRAD_CASE(16, 32, 2, 1, 0, 0)
+  DGRAD_CASE(32, 64, 2, 1, 0, 0)
+  return -1;
+}
+
+DTF_API int dtf_conv_wgrad(const ConvArgs* args, int cin, int cout, int s, int k, int mode_x, int mode_dy,
+                           int nblocks, int lds, hipStream_t stream) {
+  WGRAD_CASE(16, 16, 1, 3, 0, 0)  // stem (x = padded image)
+  WGRAD_CASE(16, 16, 1, 3, 1, 0)  // conv_b: x = h (BN2+ReLU), dy = residual grad
+  WGRAD_CASE(32, 32, 1, 3, 1, 0)
+  WGRAD_CASE(64, 64, 1, 3, 1, 0)
+  WGRAD_CASE(16, 16, 1, 3, 1, 2)  // conv_a: x = block input (BN1+ReLU), dy = BN2-backward(dz2, h)
+  WGRAD_CASE(32, 32, 1, 3, 1, 2)
+  WGRAD_CASE(64, 64, 1, 3, 1, 2)
+  WGRAD_CASE(16, 32, 2, 3, 1, 2)
+  WGRAD_CASE(32, 64, 2, 3, 1, 2)
+  WGRAD_CASE(16, 16, 1, 1, 1, 0)  // projections: x = BN1+ReLU(block input), dy = residual grad
+  WGRAD_CASE(16, 32, 2, 1, 1, 0)
+  WGRAD_CASE(32, 64, 2, 1, 1, 0)
+  return -1;
+}

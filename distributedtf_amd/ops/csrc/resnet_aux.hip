@@ -1,0 +1,396 @@
+// Auxiliary population-batched kernels of the CIFAR ResNet step (gfx950):
+//   * prep_input       : fp32 NHWC images -> bf16 NHWC with channels zero-padded to 16
+//   * weight_prep      : fp32 master weights -> bf16 forward (OHWI) + dgrad (IHWO) layouts, all convs x members
+//   * bn_running_update: TF-style moving averages (momentum 0.997, unbiased var) for every BN x member
+//   * bn_bwd_apply     : g = A*dz + B*x + C (+ add): finishes a BatchNorm backward once its reductions are done
+//   * head_fwd_bwd     : final BN+ReLU -> global avg pool -> dense -> softmax CE -> all gradients of the head,
+//                        BN-final backward reductions, per-member loss / correct count
+//   * head_bwd_apply   : residual-stream gradient entering the last block
+#include "common.h"
+
+#define BN_EPS 1e-5f
+#define BN_MOM 0.997f
+#define NREP 8
+
+namespace {
+
+__device__ __forceinline__ void stats_sum(const float* row, int c, float& s, float& q) {
+  s = 0.f;
+  q = 0.f;
+#pragma unroll
+  for (int r = 0; r < NREP; ++r) {
+    s += row[r * 128 + c];
+    q += row[r * 128 + 64 + c];
+  }
+}
+
+__global__ __launch_bounds__(256) void prep_input_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long npix,
+                                                          int c_in) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += stride) {
+    uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float v[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) v[c] = 0.f;
+    for (int c = 0; c < c_in; ++c) v[c] = x[p * c_in + c];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = pack2bf(v[2 * j], v[2 * j + 1]);
+    uint4* dst = reinterpret_cast<uint4*>(y + p * 16);
+    dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  }
+}
+
+// conv table row: {w_off, cout, cin, k, cin_pad, fwd_off, dgr_off, 0} (int32)
+__global__ __launch_bounds__(256) void weight_prep_kernel(const float* __restrict__ state, long s_mstride,
+                                                           const int* __restrict__ table, const int* __restrict__ slots,
+                                                           bf16_t* __restrict__ wf, bf16_t* __restrict__ wd,
+                                                           long w_mstride) {
+  const int* t = table + blockIdx.x * 8;
+  const int slot = slots[blockIdx.y];
+  const int w_off = t[0], cout = t[1], cin = t[2], k = t[3], cin_pad = t[4], fwd_off = t[5], dgr_off = t[6];
+  const int kk = k * k;
+  const float* p = state + (long)slot * s_mstride + w_off;
+  bf16_t* f = wf + (long)slot * w_mstride + fwd_off;
+  bf16_t* d = wd + (long)slot * w_mstride + dgr_off;
+  const int nf = cout * kk * cin_pad;
+  for (int i = threadIdx.x; i < nf; i += blockDim.x) {
+    const int ci = i % cin_pad, rest = i / cin_pad;  // rest = co*kk + tap
+    f[i] = ci < cin ? f2bf(p[rest * cin + ci]) : (bf16_t)0;
+  }
+  if (dgr_off >= 0) {
+    const int nd = cin * kk * cout;
+    for (int i = threadIdx.x; i < nd; i += blockDim.x) {
+      const int co = i % cout, rest = i / cout;  // rest = ci*kk + tap
+      const int tap = rest % kk, ci = rest / kk;
+      d[i] = f2bf(p[(co * kk + tap) * cin + ci]);
+    }
+  }
+}
+
+// bn table row: {run_off (float index into state row), C, hw, stats index}
+__global__ __launch_bounds__(64) void bn_running_update_kernel(float* __restrict__ state, long s_mstride, long run_base,
+                                                                const int* __restrict__ table,
+                                                                const float* __restrict__ stats, long stats_bn_stride,
+                                                                const int* __restrict__ slots,
+                                                                const float* __restrict__ cnt) {
+  const int* t = table + blockIdx.x * 4;
+  const int slot = slots[blockIdx.y];
+  const int c = threadIdx.x;
+  const int C = t[1];
+  if (c >= C) return;
+  const float* row = stats + (long)t[3] * stats_bn_stride + (long)slot * NREP * 128;
+  float s, q;
+  stats_sum(row, c, s, q);
+  const float n = cnt[slot] * (float)t[2];
+  const float mean = s / n;
+  const float var = fmaxf(q / n - mean * mean, 0.f);
+  const float unbiased = n > 1.f ? var * n / (n - 1.f) : var;
+  float* run = state + (long)slot * s_mstride + run_base + t[0];
+  run[c] = BN_MOM * run[c] + (1.f - BN_MOM) * mean;
+  run[C + c] = BN_MOM * run[C + c] + (1.f - BN_MOM) * unbiased;
+}
+
+struct BnBwdArgs {
+  const bf16_t* dz;
+  const bf16_t* x;
+  const bf16_t* add;
+  bf16_t* out;
+  const int* img_slot;
+  const float* params;
+  long p_mstride;
+  int gamma_off;
+  const float* st_f;
+  const float* st_b;
+  const float* cnt;
+  int hw;
+  int C;
+  long nimg;
+};
+
+__device__ __forceinline__ void bwd_coef(const float* stf, const float* stb, float n, float gamma, int c, float& A,
+                                         float& B, float& Cc) {
+  float s, q;
+  stats_sum(stf, c, s, q);
+  const float mean = s / n;
+  const float var = fmaxf(q / n - mean * mean, 0.f);
+  const float inv = rsqrtf(var + BN_EPS);
+  const float scale = gamma * inv;
+  float sdz, sdzx;
+  stats_sum(stb, c, sdz, sdzx);
+  const float mdz = sdz / n, mdzx = sdzx / n;
+  A = scale;
+  B = -scale * inv * mdzx;
+  Cc = -scale * mdz + scale * inv * mean * mdzx;
+}
+
+// One workgroup per image: coefficients of the image's member in LDS, then 8 bf16 per thread.
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a) {
+  __shared__ float co[3 * 64];
+  const int img = blockIdx.x;
+  const int slot = a.img_slot[img];
+  const int C = a.C;
+  if (threadIdx.x < C) {
+    const float* prow = a.params + (long)slot * a.p_mstride;
+    float A, B, Cc;
+    bwd_coef(a.st_f + (long)slot * NREP * 128, a.st_b + (long)slot * NREP * 128, a.cnt[slot] * (float)a.hw,
+             prow[a.gamma_off + threadIdx.x], threadIdx.x, A, B, Cc);
+    co[threadIdx.x] = A;
+    co[64 + threadIdx.x] = B;
+    co[128 + threadIdx.x] = Cc;
+  }
+  __syncthreads();
+  const long base = (long)img * a.hw * C;
+  const int n8 = a.hw * C / 8;
+  for (int i = threadIdx.x; i < n8; i += blockDim.x) {
+    const long o = base + (long)i * 8;
+    const int c0 = (i * 8) % C;
+    uint4 dz = *reinterpret_cast<const uint4*>(a.dz + o);
+    uint4 xv = *reinterpret_cast<const uint4*>(a.x + o);
+    uint4 ad = make_uint4(0, 0, 0, 0);
+    if (a.add) ad = *reinterpret_cast<const uint4*>(a.add + o);
+    uint32_t d32[4] = {dz.x, dz.y, dz.z, dz.w}, x32[4] = {xv.x, xv.y, xv.z, xv.w}, a32[4] = {ad.x, ad.y, ad.z, ad.w};
+    uint32_t r32[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + 2 * j;
+      float v0 = co[c] * bf2f((bf16_t)(d32[j] & 0xffff)) + co[64 + c] * bf2f((bf16_t)(x32[j] & 0xffff)) + co[128 + c];
+      float v1 = co[c + 1] * bf2f((bf16_t)(d32[j] >> 16)) + co[64 + c + 1] * bf2f((bf16_t)(x32[j] >> 16)) +
+                 co[128 + c + 1];
+      v0 += bf2f((bf16_t)(a32[j] & 0xffff));
+      v1 += bf2f((bf16_t)(a32[j] >> 16));
+      r32[j] = pack2bf(v0, v1);
+    }
+    *reinterpret_cast<uint4*>(a.out + o) = make_uint4(r32[0], r32[1], r32[2], r32[3]);
+  }
+}
+
+struct HeadArgs {
+  const bf16_t* x;        // [N, hw, C] last residual-stream tensor (pre final-BN)
+  const int* labels;      // [N]
+  const int4* work;       // (img0, nimg, 0, slot)
+  const float* params;
+  long p_mstride;
+  int gamma_off, beta_off, dw_off, db_off;
+  float* grads;
+  long g_mstride;
+  const float* st_f;      // final-BN forward stats
+  float* st_b;            // final-BN backward reductions (out)
+  const float* cnt;       // per-slot batch size (float)
+  float* dfeat;           // [N, C] fp32 (out): dL/dfeat / hw
+  float* loss;            // [cap] (out, summed mean CE)
+  float* correct;         // [cap] (out)
+  float* logits_out;      // [N, ncls] optional
+  int hw, C, ncls;
+  int train;
+};
+
+// 4 waves per WG, one image per wave iteration, lane = channel (C == 64).
+__global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
+  __shared__ float sc[64], sh[64], mu[64], iv[64];
+  __shared__ float red[4][2][64];
+  __shared__ float dwl[4][16][64];
+  __shared__ float dbl[4][16];
+  const int4 wk = a.work[blockIdx.x];
+  const int img0 = wk.x, nimg = wk.y, slot = wk.w;
+  const int wave = threadIdx.x >> 6, c = threadIdx.x & 63;
+  const float* prow = a.params + (long)slot * a.p_mstride;
+  const float bsz = a.cnt[slot];
+  if (threadIdx.x < 64) {
+    float s, q;
+    stats_sum(a.st_f + (long)slot * NREP * 128, c, s, q);
+    const float n = bsz * (float)a.hw;
+    const float mean = s / n;
+    const float var = fmaxf(q / n - mean * mean, 0.f);
+    const float inv = rsqrtf(var + BN_EPS);
+    sc[c] = prow[a.gamma_off + c] * inv;
+    sh[c] = prow[a.beta_off + c] - mean * sc[c];
+    mu[c] = mean;
+    iv[c] = inv;
+  }
+  __syncthreads();
+  const int ncls = a.ncls;
+  float wcol[16];  // W[j][c] for this lane's channel
+#pragma unroll
+  for (int j = 0; j < 16; ++j) wcol[j] = j < ncls ? prow[a.dw_off + j * a.C + c] : 0.f;
+  float dw[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) dw[j] = 0.f;
+  float db = 0.f;  // lane j < ncls accumulates db[j]
+  float s_dz = 0.f, s_dzx = 0.f, loss_acc = 0.f, corr = 0.f;
+  const float s_c = sc[c], t_c = sh[c], mu_c = mu[c], iv_c = iv[c];
+  const float inv_hw = 1.f / (float)a.hw;
+  for (int im = wave; im < nimg; im += 4) {
+    const int img = img0 + im;
+    const bf16_t* xp = a.x + (long)img * a.hw * a.C + c;
+    float f = 0.f;
+    for (int p = 0; p < a.hw; ++p) f += fmaxf(bf2f(xp[(long)p * a.C]) * s_c + t_c, 0.f);
+    f *= inv_hw;
+    float logit[16];
+    float mx = -3.0e38f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (j < ncls) {
+        logit[j] = wave_sum(wcol[j] * f) + prow[a.db_off + j];
+        mx = fmaxf(mx, logit[j]);
+      }
+    }
+    float se = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (j < ncls) se += __expf(logit[j] - mx);
+    const float lse = mx + __logf(se);
+    const int lab = a.labels[img];
+    float best = -3.0e38f;
+    int arg = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (j < ncls && logit[j] > best) {
+        best = logit[j];
+        arg = j;
+      }
+    if (c == 0) {
+      loss_acc += lse - logit[lab];
+      corr += (arg == lab) ? 1.f : 0.f;
+    }
+    if (a.logits_out && c < ncls) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (j == c) a.logits_out[(long)img * ncls + j] = logit[j];
+    }
+    if (a.train) {
+      float dfeat = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if (j < ncls) {
+          const float dl = (__expf(logit[j] - lse) - (j == lab ? 1.f : 0.f)) / bsz;
+          dfeat += wcol[j] * dl;
+          dw[j] += dl * f;
+          if (c == j) db += dl;
+        }
+      }
+      const float g = dfeat * inv_hw;  // dL/d(post-relu activation), identical for every pixel
+      a.dfeat[(long)img * a.C + c] = g;
+      for (int p = 0; p < a.hw; ++p) {
+        const float xv = bf2f(xp[(long)p * a.C]);
+        if (xv * s_c + t_c > 0.f) {
+          s_dz += g;
+          s_dzx += g * (xv - mu_c) * iv_c;
+        }
+      }
+    }
+  }
+  // reduce over waves through LDS, then one atomic per value
+  red[wave][0][c] = s_dz;
+  red[wave][1][c] = s_dzx;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) dwl[wave][j][c] = dw[j];
+  if (c < 16) dbl[wave][c] = db;
+  const float lw = wave_sum(loss_acc), cw = wave_sum(corr);
+  __syncthreads();
+  if (c == 0) {
+    atomicAdd(&a.loss[slot], lw / bsz);
+    atomicAdd(&a.correct[slot], cw);
+  }
+  if (a.train && wave == 0) {
+    const float v0 = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+    const float v1 = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+    float* row = a.st_b + (long)slot * NREP * 128 + (blockIdx.x & (NREP - 1)) * 128;
+    atomicAdd(&row[c], v0);
+    atomicAdd(&row[64 + c], v1);
+    float* g = a.grads + (long)slot * a.g_mstride;
+    for (int j = 0; j < ncls; ++j)
+      atomicAdd(&g[a.dw_off + j * a.C + c], dwl[0][j][c] + dwl[1][j][c] + dwl[2][j][c] + dwl[3][j][c]);
+    if (c < ncls) atomicAdd(&g[a.db_off + c], dbl[0][c] + dbl[1][c] + dbl[2][c] + dbl[3][c]);
+  }
+}
+
+// g[n,p,c] = A_c * dz + B_c * x + C_c  with  dz = dfeat[n,c] * [x*s+t > 0]  (final BN backward)
+__global__ __launch_bounds__(256) void head_bwd_apply_kernel(const bf16_t* __restrict__ x, const float* __restrict__ dfeat,
+                                                              bf16_t* __restrict__ out, const int* __restrict__ img_slot,
+                                                              const float* __restrict__ params, long p_mstride,
+                                                              int gamma_off, int beta_off, const float* __restrict__ st_f,
+                                                              const float* __restrict__ st_b,
+                                                              const float* __restrict__ cnt, int hw, int C) {
+  __shared__ float co[5 * 64];
+  const int img = blockIdx.x;
+  const int slot = img_slot[img];
+  const int c = threadIdx.x;
+  if (c < C) {
+    const float* prow = params + (long)slot * p_mstride;
+    const float n = cnt[slot] * (float)hw;
+    float s, q;
+    stats_sum(st_f + (long)slot * NREP * 128, c, s, q);
+    const float mean = s / n;
+    const float var = fmaxf(q / n - mean * mean, 0.f);
+    const float inv = rsqrtf(var + BN_EPS);
+    const float scale = prow[gamma_off + c] * inv;
+    float sdz, sdzx;
+    stats_sum(st_b + (long)slot * NREP * 128, c, sdz, sdzx);
+    const float mdz = sdz / n, mdzx = sdzx / n;
+    co[c] = scale;
+    co[64 + c] = -scale * inv * mdzx;
+    co[128 + c] = -scale * mdz + scale * inv * mean * mdzx;
+    co[192 + c] = scale;                                 // forward scale
+    co[256 + c] = prow[beta_off + c] - mean * scale;     // forward shift
+  }
+  __syncthreads();
+  const long base = (long)img * hw * C;
+  const float* df = dfeat + (long)img * C;
+  for (int i = threadIdx.x; i < hw * C; i += blockDim.x) {
+    const int cc = i % C;
+    const float xv = bf2f(x[base + i]);
+    const float dz = (xv * co[192 + cc] + co[256 + cc] > 0.f) ? df[cc] : 0.f;
+    out[base + i] = f2bf(co[cc] * dz + co[64 + cc] * xv + co[128 + cc]);
+  }
+}
+
+}  // namespace
+
+DTF_API int dtf_prep_input(const float* x, bf16_t* y, long npix, int c_in, hipStream_t stream) {
+  long blocks = (npix + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(prep_input_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, y, npix, c_in);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_weight_prep(const float* state, long s_mstride, const int* table, int nconv, const int* slots,
+                            int nslots, bf16_t* wf, bf16_t* wd, long w_mstride, hipStream_t stream) {
+  if (nconv <= 0 || nslots <= 0) return 0;
+  hipLaunchKernelGGL(weight_prep_kernel, dim3(nconv, nslots), dim3(256), 0, stream, state, s_mstride, table, slots, wf,
+                     wd, w_mstride);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_bn_running_update(float* state, long s_mstride, long run_base, const int* table, int nbn,
+                                  const float* stats, long stats_bn_stride, const int* slots, int nslots,
+                                  const float* cnt, hipStream_t stream) {
+  if (nbn <= 0 || nslots <= 0) return 0;
+  hipLaunchKernelGGL(bn_running_update_kernel, dim3(nbn, nslots), dim3(64), 0, stream, state, s_mstride, run_base,
+                     table, stats, stats_bn_stride, slots, cnt);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_bnbwd_args_size() { return (int)sizeof(BnBwdArgs); }
+DTF_API int dtf_head_args_size() { return (int)sizeof(HeadArgs); }
+
+DTF_API int dtf_bn_bwd_apply(const BnBwdArgs* a, hipStream_t stream) {
+  if (a->nimg <= 0) return 0;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((unsigned)a->nimg), dim3(256), 0, stream, *a);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_head(const HeadArgs* a, int nblocks, hipStream_t stream) {
+  if (nblocks <= 0) return 0;
+  hipLaunchKernelGGL(head_kernel, dim3(nblocks), dim3(256), 0, stream, *a);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_head_bwd_apply(const bf16_t* x, const float* dfeat, bf16_t* out, const int* img_slot,
+                               const float* params, long p_mstride, int gamma_off, int beta_off, const float* st_f,
+                               const float* st_b, const float* cnt, int hw, int C, int nimg, hipStream_t stream) {
+  if (nimg <= 0) return 0;
+  hipLaunchKernelGGL(head_bwd_apply_kernel, dim3(nimg), dim3(256), 0, stream, x, dfeat, out, img_slot, params,
+                     p_mstride, gamma_off, beta_off, st_f, st_b, cnt, hw, C);
+  return DTF_CHECK_LAUNCH();
+}

@@ -90,7 +90,7 @@ def _register():
     ops.register("dtf_weight_prep", [c_void_p, c_long, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_long,
                                      c_void_p])
     ops.register("dtf_bn_running_update", [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_long, c_void_p,
-                                           c_int, c_void_p, c_void_p])
+                                           c_int, c_void_p, c_void_p, c_long, c_void_p])
     ops.register("dtf_bn_bwd_apply", [P(BnBwdArgs), c_void_p])
     ops.register("dtf_head", [P(HeadArgs), c_int, c_void_p])
     ops.register("dtf_head_bwd_apply", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_int,
@@ -164,7 +164,7 @@ class _Layout:
             hw = hw_out
         self.bn_hw[prog.final_bn] = hw * hw
         self.final_hw = hw * hw
-        self.bn_table = [[b.run_off, b.c, self.bn_hw[b.idx], b.idx] for b in prog.bns]
+        self.bn_table = [[b.run_off, b.c, self.bn_hw[b.idx], b.idx, b.gamma_off, b.beta_off, 0, 0] for b in prog.bns]
 
 
 class HipResNetBackend:
@@ -484,7 +484,7 @@ class _StepPlan:
         self._keep(ha)
         self._add(lib.dtf_head, ctypes.byref(ha), hwork.shape[0])
         self._add(lib.dtf_bn_running_update, _p(e.state), e.S, 3 * e.Pp, _p(be.bn_table_t), len(L.bn_table),
-                  _p(be.stats[0]), be.stats_bn_stride, _p(self.slots_t), nslots, _p(self.cnt))
+                  _p(be.stats[0]), be.stats_bn_stride, _p(self.slots_t), nslots, _p(self.cnt), None, 0)
         # ---------------- backward
         hwL = self.xs[-1].shape[1]
         g_cur = self.tmp[hwL]["g"][0]
@@ -525,6 +525,9 @@ class _StepPlan:
             g_cur = g_next
         # stem wgrad (input = padded image, real channels 3)
         self._conv_wgrad(prog.stem, self.xin16, g_cur, mode_x=0, mode_dy=0, cin_real=cfg.in_channels)
+        # BN parameter gradients from the backward reductions
+        self._add(lib.dtf_bn_running_update, _p(e.state), e.S, 3 * e.Pp, _p(be.bn_table_t), len(L.bn_table),
+                  _p(be.stats[1]), be.stats_bn_stride, _p(self.slots_t), nslots, _p(self.cnt), _p(e.grads), e.Pp)
         # optimizer over every member row (+ zero grads), step counters
         self._add("optim", None)
         self._add("step", None)

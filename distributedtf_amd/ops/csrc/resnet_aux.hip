@@ -68,13 +68,16 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(const float* __restric
   }
 }
 
-// bn table row: {run_off (float index into state row), C, hw, stats index}
+// bn table row: {run_off (float index into state row), C, hw, stats index, gamma_off, beta_off, 0, 0}
+// grads == nullptr: moving-average update from forward statistics;
+// grads != nullptr: accumulate dgamma / dbeta from backward statistics.
 __global__ __launch_bounds__(64) void bn_running_update_kernel(float* __restrict__ state, long s_mstride, long run_base,
                                                                 const int* __restrict__ table,
                                                                 const float* __restrict__ stats, long stats_bn_stride,
                                                                 const int* __restrict__ slots,
-                                                                const float* __restrict__ cnt) {
-  const int* t = table + blockIdx.x * 4;
+                                                                const float* __restrict__ cnt,
+                                                                float* __restrict__ grads, long g_mstride) {
+  const int* t = table + blockIdx.x * 8;
   const int slot = slots[blockIdx.y];
   const int c = threadIdx.x;
   const int C = t[1];
@@ -82,6 +85,13 @@ __global__ __launch_bounds__(64) void bn_running_update_kernel(float* __restrict
   const float* row = stats + (long)t[3] * stats_bn_stride + (long)slot * NREP * 128;
   float s, q;
   stats_sum(row, c, s, q);
+  if (grads != nullptr) {
+    // parameter gradients of the BN: dgamma = sum(dz * xhat), dbeta = sum(dz) (backward reductions)
+    float* g = grads + (long)slot * g_mstride;
+    g[t[4] + c] += q;
+    g[t[5] + c] += s;
+    return;
+  }
   const float n = cnt[slot] * (float)t[2];
   const float mean = s / n;
   const float var = fmaxf(q / n - mean * mean, 0.f);
@@ -364,10 +374,10 @@ DTF_API int dtf_weight_prep(const float* state, long s_mstride, const int* table
 
 DTF_API int dtf_bn_running_update(float* state, long s_mstride, long run_base, const int* table, int nbn,
                                   const float* stats, long stats_bn_stride, const int* slots, int nslots,
-                                  const float* cnt, hipStream_t stream) {
+                                  const float* cnt, float* grads, long g_mstride, hipStream_t stream) {
   if (nbn <= 0 || nslots <= 0) return 0;
   hipLaunchKernelGGL(bn_running_update_kernel, dim3(nbn, nslots), dim3(64), 0, stream, state, s_mstride, run_base,
-                     table, stats, stats_bn_stride, slots, cnt);
+                     table, stats, stats_bn_stride, slots, cnt, grads, g_mstride);
   return DTF_CHECK_LAUNCH();
 }
 

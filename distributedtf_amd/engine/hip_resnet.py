@@ -303,21 +303,25 @@ class _StepPlan:
         self.graph = None
 
     # -------------------------------------------------------------------- work lists
-    def _work_fwd(self, H_out, W_out, align=16, nimg_per=1, target=2048):
-        rows = _pick_rows(H_out, W_out, self.N, align, target)
-        key = ("f", H_out, W_out, rows)
+    def _work_iters(self, bands, n_wg):
+        """(it0, nit, 0, slot) items over the flattened (image, band) iterations of each member."""
+        key = ("it", bands, n_wg)
         w = self._work_cache.get(key)
         if w is None:
             items = []
-            bands = H_out // rows
+            per_member = max(1, n_wg // max(1, len(self.slots)))
             for s, n in zip(self.slots, self.sizes):
-                f = self.first[s]
-                for i in range(n):
-                    for b in range(bands):
-                        items.append([f + i, 1, b, s])
+                total = n * bands
+                f = self.first[s] * bands
+                chunk = max(1, -(-total // per_member))
+                for i in range(0, total, chunk):
+                    items.append([f + i, min(chunk, total - i), 0, s])
             w = torch.tensor(items, dtype=torch.int32, device=self.be.dev)
             self._work_cache[key] = w
-        return rows, w
+        return w
+
+    def _n_wg(self, act_bytes, weight_bytes, lo=256, hi=2048):
+        return int(max(lo, min(hi, 2 * act_bytes // max(1, weight_bytes))))
 
     def _work_member(self, target_items=256, min_chunk=1):
         key = ("m", target_items)
@@ -360,7 +364,18 @@ class _StepPlan:
         c = L.prog.convs[ci]
         Hi = x.shape[1]
         Ho = Hi // c.stride
-        rows, work = self._work_fwd(Ho, Ho)
+        cin = 16 if ci == L.prog.stem else c.cin
+        P = (c.k - 1) // 2
+        rows = None
+        for r in range(min(8, Ho), 0, -1):
+            rows_in = (r - 1) * c.stride + c.k
+            if Ho % r == 0 and (r * Ho) % 16 == 0 and rows_in * (Hi + 2 * P) * (cin // 8) <= 4 * 256:
+                rows = r
+                break
+        assert rows is not None, ("no valid band for conv", ci)
+        bands = Ho // rows
+        n_wg = self._n_wg(self.N * Hi * Hi * cin * 2, c.cout * c.k * c.k * cin * 2)
+        work = self._work_iters(bands, n_wg)
         a = self._base_args()
         a.x, a.y, a.res = _p(x), _p(y), _p(res)
         a.w, a.w_off = _p(be.wf), L.fwd_off[ci]
@@ -371,10 +386,9 @@ class _StepPlan:
         if stats_bn is not None:
             a.st_out = _p(be.st_f(stats_bn))
         a.Hi, a.Wi, a.Ho, a.Wo, a.rows = Hi, Hi, Ho, Ho, rows
-        cin = 16 if ci == L.prog.stem else c.cin
-        P = (c.k - 1) // 2
         rows_in = (rows - 1) * c.stride + c.k
-        lds = 1280 + rows_in * (Hi + 2 * P) * cin * 2
+        tsz = (rows_in * (Hi + 2 * P) * (cin + 8) + 63) // 64 * 64
+        lds = 1280 + 2 * tsz * 2
         mode = 0 if in_bn is None else 1
         lib = ops.lib()
         self._add(lib.dtf_conv_fwd, ctypes.byref(a), cin, c.cout, c.stride, c.k, mode, int(res is not None),
@@ -384,8 +398,19 @@ class _StepPlan:
     def _conv_dgrad(self, ci, dy, y, Hi, mode, epi, dy2=None, in_bn=None, res=None, xm=None, ep_bn=None):
         be, L = self.be, self.be.L
         c = L.prog.convs[ci]
-        Ho = Hi // c.stride
-        rows, work = self._work_fwd(Hi, Hi)
+        S, K = c.stride, c.k
+        Ho = Hi // S
+        rows = None
+        for r in range(min(8, Hi), 0, -1):
+            rows_t = r + K - 1 if S == 1 else (r + K + S - 2) // S + 1
+            if Hi % r == 0 and (r * Hi) % 16 == 0 and rows_t * (Ho + 2) * (c.cout // 8) <= 4 * 256:
+                rows = r
+                break
+        assert rows is not None, ("no valid band for dgrad", ci)
+        rows_t = rows + K - 1 if S == 1 else (rows + K + S - 2) // S + 1
+        bands = Hi // rows
+        n_wg = self._n_wg(self.N * Ho * Ho * c.cout * 2, c.cout * c.k * c.k * c.cin * 2)
+        work = self._work_iters(bands, n_wg)
         a = self._base_args()
         a.x, a.x2, a.y, a.res, a.xm = _p(dy), _p(dy2), _p(y), _p(res), _p(xm)
         a.w, a.w_off = _p(be.wd), L.dgr_off[ci]
@@ -398,10 +423,8 @@ class _StepPlan:
             a.st_ep = _p(be.st_f(ep_bn))
             a.st_out = _p(be.st_b(ep_bn))
         a.Hi, a.Wi, a.Ho, a.Wo, a.rows = Hi, Hi, Ho, Ho, rows
-        P, S, K = (c.k - 1) // 2, c.stride, c.k
-        lo = rows - 1 + 0  # worst-case dy rows per band
-        rows_t = (rows - 1 + 2 * P) // S + 2
-        lds = 2304 + rows_t * (Ho + 2) * c.cout * 2
+        tsz = (rows_t * (Ho + 2) * (c.cout + 8) + 63) // 64 * 64
+        lds = 2304 + 2 * tsz * 2
         lib = ops.lib()
         self._add(lib.dtf_conv_dgrad, ctypes.byref(a), c.cin, c.cout, S, K, mode, epi, work.shape[0], lds)
         self._keep(a)
@@ -412,9 +435,22 @@ class _StepPlan:
         Hi = x.shape[1]
         Ho = Hi // c.stride
         cin = 16 if ci == L.prog.stem else c.cin
-        rows = _pick_rows(Ho, Ho, 1, 32, target_items=1, max_rows=8)
-        # largest band that keeps LDS small: limit rows so the x tile <= ~24 KB
-        work = self._work_member(target_items=256)
+        P = (c.k - 1) // 2
+        # band rows: R*Wo % 32 == 0, and the register-staged tiles fit 4 (x) / 2 (dy) chunks per thread
+        rows = None
+        for r in range(min(8, Ho), 0, -1):
+            if Ho % r or (r * Ho) % 32:
+                continue
+            rows_in = (r - 1) * c.stride + c.k
+            if rows_in * (Hi + 2 * P) * (cin // 8) <= 4 * 256 and r * Ho * (c.cout // 8) <= 2 * 256:
+                rows = r
+                break
+        if rows is None:
+            rows = _pick_rows(Ho, Ho, 1, 32, target_items=1, max_rows=8)
+        # images per workgroup: bound the fp32 atomic traffic of the per-WG partial dW (~12 MB per launch)
+        wn = c.cout * c.k * c.k * c.cin
+        n_wg = max(64, min(4096, int(12e6 / (4.0 * wn))))
+        work = self._work_iters(Ho // rows, n_wg)
         a = self._base_args()
         a.x, a.dy, a.dy2 = _p(x), _p(dy), _p(dy2)
         a.work = _p(work)
@@ -427,11 +463,11 @@ class _StepPlan:
             a.in_gamma, a.in_beta = self._bn(dy_bn)
             a.st_in, a.st_in_b = _p(be.st_f(dy_bn)), _p(be.st_b(dy_bn))
         a.Hi, a.Wi, a.Ho, a.Wo, a.rows = Hi, Hi, Ho, Ho, rows
-        P = (c.k - 1) // 2
         rows_in = (rows - 1) * c.stride + c.k
-        xt = rows_in * (Hi + 2 * P) * cin
-        xt = (xt + 63) // 64 * 64
-        lds = 1536 + xt * 2 + rows * Ho * c.cout * 2
+        assert 32 % Ho == 0, "wgrad k-step addressing needs Wo | 32"
+        xt = (rows_in * (Hi + 2 * P) * (cin + 8) + 63) // 64 * 64
+        dt = (rows * Ho * (c.cout + 8) + 63) // 64 * 64
+        lds = 1536 + 2 * (xt + dt) * 2  # double-buffered
         lib = ops.lib()
         self._add(lib.dtf_conv_wgrad, ctypes.byref(a), cin, c.cout, c.stride, c.k, mode_x, mode_dy, work.shape[0], lds)
         self._keep(a)

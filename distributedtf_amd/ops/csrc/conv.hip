@@ -12,9 +12,8 @@
 // pixel per lane) is stored as one 8-byte packed bf16 write, and a 16-pixel tile
 // of a 16-channel layer is a single contiguous 512-byte store.
 //
-// LDS tiles: [rows][cols][C] bf16 with a zero halo; the 16-byte channel chunks of
-// each pixel are XOR-swizzled by the column index to spread ds_read_b128 lane
-// groups over banks.  The producing BatchNorm (+ReLU) of the input is applied
+// LDS tiles: [rows][cols][C + 8] bf16 with a zero halo; the 16-byte pad per pixel
+// makes ds_read_b128 pixel-gathers bank-conflict free.  The producing BatchNorm (+ReLU) of the input is applied
 // while the tile is staged (global -> regs -> transform -> LDS), and BN statistics
 // of the output are reduced in registers/LDS and added to 8 replicated per-member
 // accumulators (cuts same-address atomic contention 8x); consumers sum the
@@ -103,10 +102,17 @@ __device__ __forceinline__ void bn_bwd_coef(const float* stf, const float* stb, 
   C = -scale * mdz + scale * inv * mean * mdzx;
 }
 
+// LDS tiles keep 8 bf16 (16 B) of padding after every pixel: a 16-lane group reading
+// 16 consecutive pixels with ds_read_b128 then hits 16 distinct 4-bank groups for
+// C in {16, 32, 64} (pixel strides of 12 / 20 / 36 dwords), and every operand
+// address is an affine function of the pixel index (no swizzle arithmetic in the
+// inner loops).
+template <int C>
+__host__ __device__ constexpr int cpad() { return C + 8; }
+
 template <int C>
 __device__ __forceinline__ int lds_off(int r, int col, int wp, int chunk) {
-  constexpr int NCH = C / 8;
-  return (r * wp + col) * C + ((chunk ^ (col & (NCH - 1))) << 3);
+  return (r * wp + col) * cpad<C>() + (chunk << 3);
 }
 
 // Stage a [rows_in][wp][C] tile starting at global row gy0 / col gx0 (halo -> 0).
@@ -148,6 +154,104 @@ __device__ __forceinline__ void stage_tile(bf16_t* __restrict__ tile, const bf16
         }
         v = make_uint4(w32[0], w32[1], w32[2], w32[3]);
       }
+    }
+    *reinterpret_cast<uint4*>(tile + lds_off<C>(r, col, wp, chunk)) = v;
+  }
+}
+
+// Register-staged variant of stage_tile for double buffering: tile_load issues the
+// global loads (up to MAXC 16-byte chunks per thread) into registers; tile_store
+// applies the transform and writes LDS.  Chunks beyond MAXC*blockDim are staged
+// synchronously by tile_store (correct for any shape, fast when the host sizes
+// bands to fit).
+template <int C, int MODE, int MAXC>
+struct TileRegs {
+  uint4 v[MAXC];
+  uint4 v2[MODE == 2 ? MAXC : 1];
+};
+
+template <int C, int MODE, int MAXC>
+__device__ __forceinline__ void tile_load(TileRegs<C, MODE, MAXC>& R, const bf16_t* __restrict__ src,
+                                          const bf16_t* __restrict__ src2, int gy0, int rows_in, int gx0, int wp, int H,
+                                          int W) {
+  constexpr int NCH = C / 8;
+  const int total = rows_in * wp * NCH;
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int idx = threadIdx.x + j * blockDim.x;
+    R.v[j] = make_uint4(0, 0, 0, 0);
+    if constexpr (MODE == 2) R.v2[j] = make_uint4(0, 0, 0, 0);
+    if (idx < total) {
+      const int chunk = idx % NCH;
+      const int pc = idx / NCH;
+      const int col = pc % wp;
+      const int r = pc / wp;
+      const int gy = gy0 + r, gx = gx0 + col;
+      if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+        const long off = ((long)gy * W + gx) * C + chunk * 8;
+        R.v[j] = *reinterpret_cast<const uint4*>(src + off);
+        if constexpr (MODE == 2) R.v2[j] = *reinterpret_cast<const uint4*>(src2 + off);
+      }
+    }
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ uint4 transform8(uint4 v, uint4 v2, int c0, const float* __restrict__ coef) {
+  if constexpr (MODE == 0) return v;
+  uint32_t w32[4] = {v.x, v.y, v.z, v.w};
+  uint32_t h32[4] = {v2.x, v2.y, v2.z, v2.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = c0 + 2 * j;
+    float a0 = bf2f((bf16_t)(w32[j] & 0xffff)), a1 = bf2f((bf16_t)(w32[j] >> 16));
+    if constexpr (MODE == 1) {
+      a0 = fmaxf(a0 * coef[c] + coef[64 + c], 0.f);
+      a1 = fmaxf(a1 * coef[c + 1] + coef[64 + c + 1], 0.f);
+    } else {
+      float h0 = bf2f((bf16_t)(h32[j] & 0xffff)), h1 = bf2f((bf16_t)(h32[j] >> 16));
+      a0 = coef[c] * a0 + coef[64 + c] * h0 + coef[128 + c];
+      a1 = coef[c + 1] * a1 + coef[64 + c + 1] * h1 + coef[128 + c + 1];
+    }
+    w32[j] = pack2bf(a0, a1);
+  }
+  return make_uint4(w32[0], w32[1], w32[2], w32[3]);
+}
+
+template <int C, int MODE, int MAXC>
+__device__ __forceinline__ void tile_store(bf16_t* __restrict__ tile, const TileRegs<C, MODE, MAXC>& R,
+                                           const bf16_t* __restrict__ src, const bf16_t* __restrict__ src2, int gy0,
+                                           int rows_in, int gx0, int wp, int H, int W,
+                                           const float* __restrict__ coef) {
+  constexpr int NCH = C / 8;
+  const int total = rows_in * wp * NCH;
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int idx = threadIdx.x + j * blockDim.x;
+    if (idx < total) {
+      const int chunk = idx % NCH;
+      const int pc = idx / NCH;
+      const int col = pc % wp;
+      const int r = pc / wp;
+      const int gy = gy0 + r, gx = gx0 + col;
+      uint4 v = R.v[j];
+      if (gy >= 0 && gy < H && gx >= 0 && gx < W) v = transform8<MODE>(v, MODE == 2 ? R.v2[j] : v, chunk * 8, coef);
+      *reinterpret_cast<uint4*>(tile + lds_off<C>(r, col, wp, chunk)) = v;
+    }
+  }
+  for (int idx = threadIdx.x + MAXC * blockDim.x; idx < total; idx += blockDim.x) {  // overflow (rare)
+    const int chunk = idx % NCH;
+    const int pc = idx / NCH;
+    const int col = pc % wp;
+    const int r = pc / wp;
+    const int gy = gy0 + r, gx = gx0 + col;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+      const long off = ((long)gy * W + gx) * C + chunk * 8;
+      uint4 v2 = v;
+      v = *reinterpret_cast<const uint4*>(src + off);
+      if constexpr (MODE == 2) v2 = *reinterpret_cast<const uint4*>(src2 + off);
+      v = transform8<MODE>(v, v2, chunk * 8, coef);
     }
     *reinterpret_cast<uint4*>(tile + lds_off<C>(r, col, wp, chunk)) = v;
   }
@@ -216,6 +320,12 @@ __device__ __forceinline__ void flush_stats(float* st_out, const float* acc_lds,
 
 // --------------------------------------------------------------------------------- forward
 
+// Work items are (it0, nit, -, slot): the workgroup processes iterations
+// it0 .. it0+nit-1 of the flattened (image, band) sequence of ONE member; weights
+// are loaded into registers once, and the next iteration's tile is prefetched
+// into registers (tile_load) while the MFMAs of the current one run, then
+// written to the other LDS buffer (double buffering).
+
 template <int CIN, int COUT, int S, int K, int MODE_IN, bool RESID, bool STATS>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   constexpr int NT = COUT / 16;
@@ -226,10 +336,10 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* coef = reinterpret_cast<float*>(smem);          // 192 floats
   float* acc_lds = coef + 192;                           // 128 floats
-  bf16_t* tile = reinterpret_cast<bf16_t*>(smem + 1280);
+  bf16_t* tile0 = reinterpret_cast<bf16_t*>(smem + 1280);
 
   const int4 wk = a.work[blockIdx.x];
-  const int img0 = wk.x, nimg = wk.y, band = wk.z, slot = wk.w;
+  const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const float n_in = a.cnt[slot] * (float)(a.Hi * a.Wi);
   make_coef<CIN, MODE_IN>(coef, a, slot, n_in, a.st_in, a.st_in_b, a.in_gamma, a.in_beta);
@@ -248,31 +358,47 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
     }
   }
   const int rows = a.rows;
-  const int oy0 = band * rows;
+  const int bands = a.Ho / rows;
   const int rows_in = (rows - 1) * S + K;
   const int wp = a.Wi + 2 * P;
+  const int tsz = (rows_in * wp * cpad<CIN>() + 63) & ~63;
+  bf16_t* tiles[2] = {tile0, tile0 + tsz};
   const int ntiles = rows * a.Wo / 16;
+  const long img_elems = (long)a.Hi * a.Wi * CIN;
+  int tapoff[KS];  // per-lane LDS offset of each k-step's tap/channel chunk
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k0 = 32 * s + 8 * (lane >> 4);
+    const int tap = k0 / CIN, c0 = k0 % CIN;
+    tapoff[s] = ((tap / K) * wp + (tap % K)) * cpad<CIN>() + c0;
+  }
   float ssum[4] = {0.f, 0.f, 0.f, 0.f}, ssq[4] = {0.f, 0.f, 0.f, 0.f};
+  TileRegs<CIN, MODE_IN, 4> rg;
+  __syncthreads();  // coefficients
+  {
+    const int img = it0 / bands, oy0 = (it0 % bands) * rows;
+    tile_load<CIN, MODE_IN, 4>(rg, a.x + img * img_elems, nullptr, oy0 * S - P, rows_in, -P, wp, a.Hi, a.Wi);
+    tile_store<CIN, MODE_IN, 4>(tiles[0], rg, a.x + img * img_elems, nullptr, oy0 * S - P, rows_in, -P, wp, a.Hi,
+                                a.Wi, coef);
+  }
   __syncthreads();
-
-  for (int im = 0; im < nimg; ++im) {
-    const int img = img0 + im;
-    stage_tile<CIN, MODE_IN>(tile, a.x + (long)img * a.Hi * a.Wi * CIN, nullptr, oy0 * S - P, rows_in, -P, wp, a.Hi,
-                             a.Wi, coef);
-    __syncthreads();
+  for (int k = 0; k < nit; ++k) {
+    const int it = it0 + k;
+    const int img = it / bands, oy0 = (it % bands) * rows;
+    const bool more = k + 1 < nit;
+    const int nimg_ = (it + 1) / bands, noy0 = ((it + 1) % bands) * rows;
+    if (more)
+      tile_load<CIN, MODE_IN, 4>(rg, a.x + nimg_ * img_elems, nullptr, noy0 * S - P, rows_in, -P, wp, a.Hi, a.Wi);
+    const bf16_t* tile = tiles[k & 1];
     for (int t = wave / NT; t < ntiles; t += WPT) {
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
       const int p = t * 16 + (lane & 15);
       const int oy = p / a.Wo, ox = p % a.Wo;
+      const bf16_t* tb = tile + (oy * S * wp + ox * S) * cpad<CIN>();
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        const int k0 = 32 * s + 8 * (lane >> 4);
         bf16x8_t b = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (k0 < KTOT) {
-          const int tap = k0 / CIN, c0 = k0 % CIN;
-          const int ky = tap / K, kx = tap % K;
-          b = *reinterpret_cast<const bf16x8_t*>(tile + lds_off<CIN>(oy * S + ky, ox * S + kx, wp, c0 >> 3));
-        }
+        if (32 * s + 8 * (lane >> 4) < KTOT) b = *reinterpret_cast<const bf16x8_t*>(tb + tapoff[s]);
         acc = mfma16(afr[s], b, acc);
       }
       const int co0 = ct * 16 + (lane >> 4) * 4;
@@ -298,6 +424,9 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
         ssum[3] += r3; ssq[3] += r3 * r3;
       }
     }
+    if (more)
+      tile_store<CIN, MODE_IN, 4>(tiles[(k + 1) & 1], rg, a.x + nimg_ * img_elems, nullptr, noy0 * S - P, rows_in, -P,
+                                  wp, a.Hi, a.Wi, coef);
     __syncthreads();
   }
   if constexpr (STATS) {
@@ -312,6 +441,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
 // Weights in IHWO layout: wt[ci][tap][co] (rows of the A operand are ci).
 // EPI bit0: add `res` (another dx contribution) before the epilogue;
 // EPI bit1: mask by relu(BN_ep(xm)) and accumulate sum(dz), sum(dz*xhat) of BN_ep.
+// Bands are over dx rows (forward-input resolution).
 
 template <int CI, int CO, int S, int K, int MODE_IN, int EPI>
 __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
@@ -324,10 +454,10 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
   float* coef = reinterpret_cast<float*>(smem);   // input transform (192)
   float* ecoef = coef + 192;                      // epilogue BN: scale, shift, mean, inv (4 x 64)
   float* acc_lds = ecoef + 256;                   // 128
-  bf16_t* tile = reinterpret_cast<bf16_t*>(smem + 2304);
+  bf16_t* tile0 = reinterpret_cast<bf16_t*>(smem + 2304);
 
   const int4 wk = a.work[blockIdx.x];
-  const int img0 = wk.x, nimg = wk.y, band = wk.z, slot = wk.w;
+  const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // dy lives at the forward-output resolution; the BN transformed on load is the one after this conv.
   make_coef<CO, MODE_IN>(coef, a, slot, a.cnt[slot] * (float)(a.Ho * a.Wo), a.st_in, a.st_in_b, a.in_gamma, a.in_beta);
@@ -358,31 +488,57 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
     }
   }
   const int rows = a.rows;
-  const int iy0 = band * rows;
-  // rows of dy needed: oy in [floor((iy0+P-K+1)/S), floor((iy0+rows-1+P)/S)]
-  int lo_num = iy0 + P - K + 1;
-  const int oy_lo = lo_num >= 0 ? lo_num / S : -((-lo_num + S - 1) / S);
-  const int oy_hi = (iy0 + rows - 1 + P) / S;
-  const int rows_t = oy_hi - oy_lo + 1;
+  const int bands = a.Hi / rows;
+  // dy rows needed by a band starting at iy0: oy in [floor((iy0+P-K+1)/S), floor((iy0+rows-1+P)/S)]
+  auto dy_lo = [&](int iy0) {
+    const int lo_num = iy0 + P - K + 1;
+    return lo_num >= 0 ? lo_num / S : -((-lo_num + S - 1) / S);
+  };
+  const int rows_t = (S == 1) ? rows + K - 1 : (rows + K + S - 2) / S + 1;  // dy rows per band (host: same)
   const int wp = a.Wo + 2;  // dy cols -1..Wo
+  const int tsz = (rows_t * wp * cpad<CO>() + 63) & ~63;
+  bf16_t* tiles[2] = {tile0, tile0 + tsz};
   const int ntiles = rows * a.Wi / 16;
+  const long img_elems = (long)a.Ho * a.Wo * CO;
+  int tapoff[KS];  // stride 1: LDS offset of (dy row/col shift by the flipped tap, channel chunk)
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k0 = 32 * s + 8 * (lane >> 4);
+    const int tap = k0 / CO, c0 = k0 % CO;
+    tapoff[s] = -((tap / K) * wp + (tap % K)) * cpad<CO>() + c0;
+  }
   float ssum[4] = {0.f, 0.f, 0.f, 0.f}, ssq[4] = {0.f, 0.f, 0.f, 0.f};
+  TileRegs<CO, MODE_IN, 4> rg;
   __syncthreads();
-
-  for (int im = 0; im < nimg; ++im) {
-    const int img = img0 + im;
-    const long ioff = (long)img * a.Ho * a.Wo * CO;
-    stage_tile<CO, MODE_IN>(tile, a.x + ioff, a.x2 ? a.x2 + ioff : nullptr, oy_lo, rows_t, -1, wp, a.Ho, a.Wo, coef);
-    __syncthreads();
+  {
+    const int img = it0 / bands, iy0 = (it0 % bands) * rows;
+    const bf16_t* x2 = a.x2 ? a.x2 + img * img_elems : nullptr;
+    tile_load<CO, MODE_IN, 4>(rg, a.x + img * img_elems, x2, dy_lo(iy0), rows_t, -1, wp, a.Ho, a.Wo);
+    tile_store<CO, MODE_IN, 4>(tiles[0], rg, a.x + img * img_elems, x2, dy_lo(iy0), rows_t, -1, wp, a.Ho, a.Wo, coef);
+  }
+  __syncthreads();
+  for (int k = 0; k < nit; ++k) {
+    const int it = it0 + k;
+    const int img = it / bands, iy0 = (it % bands) * rows;
+    const int oy_lo = dy_lo(iy0);
+    const bool more = k + 1 < nit;
+    const int nimg_ = (it + 1) / bands, niy0 = ((it + 1) % bands) * rows;
+    const bf16_t* nx2 = a.x2 ? a.x2 + nimg_ * img_elems : nullptr;
+    if (more) tile_load<CO, MODE_IN, 4>(rg, a.x + nimg_ * img_elems, nx2, dy_lo(niy0), rows_t, -1, wp, a.Ho, a.Wo);
+    const bf16_t* tile = tiles[k & 1];
     for (int t = wave / NT; t < ntiles; t += WPT) {
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
       const int p = t * 16 + (lane & 15);
       const int iy = iy0 + p / a.Wi, ix = p % a.Wi;
+      // stride 1: dy(iy+P-ky, ix+P-kx) lives at tile row iy+P-oy_lo-ky, col ix+P+1-kx
+      const bf16_t* tb = tile + ((iy + P - oy_lo) * wp + ix + P + 1) * cpad<CO>();
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         const int k0 = 32 * s + 8 * (lane >> 4);
         bf16x8_t b = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (k0 < KTOT) {
+        if constexpr (S == 1) {
+          if (k0 < KTOT) b = *reinterpret_cast<const bf16x8_t*>(tb + tapoff[s]);
+        } else if (k0 < KTOT) {
           const int tap = k0 / CO, c0 = k0 % CO;
           const int ky = tap / K, kx = tap % K;
           const int ty = iy + P - ky, tx = ix + P - kx;
@@ -409,10 +565,13 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
         v[2] += bf2f((bf16_t)(r.y & 0xffff));
         v[3] += bf2f((bf16_t)(r.y >> 16));
       }
+      float xv[4] = {0.f, 0.f, 0.f, 0.f};
       if constexpr (EPI & 2) {
         const uint2 xr = *reinterpret_cast<const uint2*>(a.xm + o);
-        const float xv[4] = {bf2f((bf16_t)(xr.x & 0xffff)), bf2f((bf16_t)(xr.x >> 16)), bf2f((bf16_t)(xr.y & 0xffff)),
-                             bf2f((bf16_t)(xr.y >> 16))};
+        xv[0] = bf2f((bf16_t)(xr.x & 0xffff));
+        xv[1] = bf2f((bf16_t)(xr.x >> 16));
+        xv[2] = bf2f((bf16_t)(xr.y & 0xffff));
+        xv[3] = bf2f((bf16_t)(xr.y >> 16));
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int c = ci0 + r;
@@ -425,9 +584,6 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
       pk.y = pack2bf(v[2], v[3]);
       *reinterpret_cast<uint2*>(a.y + o) = pk;
       if constexpr (EPI & 2) {
-        const uint2 xr = *reinterpret_cast<const uint2*>(a.xm + o);
-        const float xv[4] = {bf2f((bf16_t)(xr.x & 0xffff)), bf2f((bf16_t)(xr.x >> 16)), bf2f((bf16_t)(xr.y & 0xffff)),
-                             bf2f((bf16_t)(xr.y >> 16))};
         const float dz[4] = {bf2f((bf16_t)(pk.x & 0xffff)), bf2f((bf16_t)(pk.x >> 16)), bf2f((bf16_t)(pk.y & 0xffff)),
                              bf2f((bf16_t)(pk.y >> 16))};
 #pragma unroll
@@ -438,6 +594,9 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
         }
       }
     }
+    if (more)
+      tile_store<CO, MODE_IN, 4>(tiles[(k + 1) & 1], rg, a.x + nimg_ * img_elems, nx2, dy_lo(niy0), rows_t, -1, wp,
+                                 a.Ho, a.Wo, coef);
     __syncthreads();
   }
   if constexpr (EPI & 2) {
@@ -471,7 +630,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
   bf16_t* xt = reinterpret_cast<bf16_t*>(smem + 1536);
 
   const int4 wk = a.work[blockIdx.x];
-  const int img0 = wk.x, nimg = wk.y, slot = wk.w;
+  const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   make_coef<CIN, MODE_X>(coef_x, a, slot, a.cnt[slot] * (float)(a.Hi * a.Wi), a.st_x, nullptr, a.x_gamma, a.x_beta);
   make_coef<COUT, MODE_DY>(coef_d, a, slot, a.cnt[slot] * (float)(a.Ho * a.Wo), a.st_in, a.st_in_b, a.in_gamma,
@@ -479,7 +638,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
   const int rows = a.rows;
   const int rows_in = (rows - 1) * S + K;
   const int wpx = a.Wi + 2 * P;
-  bf16_t* dt = xt + ((rows_in * wpx * CIN + 63) & ~63);
+  const int xsz = (rows_in * wpx * cpad<CIN>() + 63) & ~63;
+  const int dsz = (rows * a.Wo * cpad<COUT>() + 63) & ~63;
+  bf16_t* xbuf[2] = {xt, xt + xsz + dsz};
+  bf16_t* dbuf[2] = {xt + xsz, xt + 2 * xsz + dsz};
   const int npix = rows * a.Wo;
   const int bands = a.Ho / rows;
 
@@ -490,45 +652,83 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
     for (int m = 0; m < MT; ++m) acc[j][m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p4 = i & 3;
+  TileRegs<CIN, MODE_X, 4> rx;
+  TileRegs<COUT, MODE_DY, 2> rd;
+  auto src_of = [&](int it, const bf16_t*& xs, const bf16_t*& ds, const bf16_t*& ds2, int& oy0) {
+    const int img = (it0 + it) / bands;
+    oy0 = ((it0 + it) % bands) * rows;
+    xs = a.x + (long)img * a.Hi * a.Wi * CIN;
+    const long yo = (long)img * a.Ho * a.Wo * COUT;
+    ds = a.dy + yo;
+    ds2 = a.dy2 ? a.dy2 + yo : nullptr;
+  };
+  __syncthreads();  // coefficients visible
+  {
+    const bf16_t *xs, *ds, *ds2;
+    int oy0;
+    src_of(0, xs, ds, ds2, oy0);
+    tile_load<CIN, MODE_X, 4>(rx, xs, nullptr, oy0 * S - P, rows_in, -P, wpx, a.Hi, a.Wi);
+    tile_load<COUT, MODE_DY, 2>(rd, ds, ds2, oy0, rows, 0, a.Wo, a.Ho, a.Wo);
+    tile_store<CIN, MODE_X, 4>(xbuf[0], rx, xs, nullptr, oy0 * S - P, rows_in, -P, wpx, a.Hi, a.Wi, coef_x);
+    tile_store<COUT, MODE_DY, 2>(dbuf[0], rd, ds, ds2, oy0, rows, 0, a.Wo, a.Ho, a.Wo, coef_d);
+  }
   __syncthreads();
-  for (int im = 0; im < nimg; ++im) {
-    const int img = img0 + im;
-    for (int band = 0; band < bands; ++band) {
-      const int oy0 = band * rows;
-      const long xo = (long)img * a.Hi * a.Wi * CIN;
-      const long yo = (long)img * a.Ho * a.Wo * COUT;
-      stage_tile<CIN, MODE_X>(xt, a.x + xo, nullptr, oy0 * S - P, rows_in, -P, wpx, a.Hi, a.Wi, coef_x);
-      stage_tile<COUT, MODE_DY>(dt, a.dy + yo, a.dy2 ? a.dy2 + yo : nullptr, oy0, rows, 0, a.Wo, a.Ho, a.Wo, coef_d);
-      __syncthreads();
-      for (int k0 = 0; k0 < npix; k0 += 32) {
-        // pixel rows delivered to this lane group: k0 + 8g + q (+4)
-        const int pa = k0 + 8 * g + q, pb = pa + 4;
-        const int ya = pa / a.Wo, xa = pa % a.Wo, yb = pb / a.Wo, xb = pb % a.Wo;
-        bf16x8_t af[MT];
+  for (int it = 0; it < nit; ++it) {
+    const int cur = it & 1;
+    const bf16_t *nxs = nullptr, *nds = nullptr, *nds2 = nullptr;
+    int noy0 = 0;
+    if (it + 1 < nit) {  // prefetch the next (image, band) into registers
+      src_of(it + 1, nxs, nds, nds2, noy0);
+      tile_load<CIN, MODE_X, 4>(rx, nxs, nullptr, noy0 * S - P, rows_in, -P, wpx, a.Hi, a.Wi);
+      tile_load<COUT, MODE_DY, 2>(rd, nds, nds2, noy0, rows, 0, a.Wo, a.Ho, a.Wo);
+    }
+    const bf16_t* xcur = xbuf[cur];
+    const bf16_t* dcur = dbuf[cur];
+    // The 32 pixels of a k-step span RSTEP = 32/Wo whole rows (Wo | 32), so each
+    // lane's pixel (ya, xa) is (kstep*RSTEP + (8g+q)/Wo, (8g+q)%Wo): all LDS
+    // addresses are lane constants plus kstep * increment.
+    const int rstep = 32 / a.Wo;
+    const int pa = 8 * g + q, pb = pa + 4;
+    const int ya = pa / a.Wo, xa = pa % a.Wo, yb = pb / a.Wo, xb = pb % a.Wo;
+    const bf16_t* da = dcur + (ya * a.Wo + xa) * cpad<COUT>() + 4 * p4;
+    const bf16_t* db = dcur + (yb * a.Wo + xb) * cpad<COUT>() + 4 * p4;
+    const bf16_t* xa_ = xcur + (ya * S * wpx + xa * S) * cpad<CIN>() + 4 * p4;
+    const bf16_t* xb_ = xcur + (yb * S * wpx + xb * S) * cpad<CIN>() + 4 * p4;
+    const int dinc = rstep * a.Wo * cpad<COUT>();
+    const int xinc = rstep * S * wpx * cpad<CIN>();
+    int boff[NJ];
 #pragma unroll
-        for (int m = 0; m < MT; ++m) {
-          const int ch = m * 16 + 4 * p4;
-          s16x4_t lo = ds_read_tr(dt + lds_off<COUT>(ya, xa, a.Wo, ch >> 3) + (ch & 7));
-          s16x4_t hi = ds_read_tr(dt + lds_off<COUT>(yb, xb, a.Wo, ch >> 3) + (ch & 7));
-          af[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        }
+    for (int j = 0; j < NJ; ++j) {
+      const int nt = wave + 4 * j;
+      const int tap = (nt * 16) / CIN, cb = (nt * 16) % CIN;
+      boff[j] = ((tap / K) * wpx + (tap % K)) * cpad<CIN>() + cb;
+    }
+    const int nk = npix / 32;
+    for (int ks = 0; ks < nk; ++ks) {
+      bf16x8_t af[MT];
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int nt = wave + 4 * j;
-          if (nt < NTN) {
-            const int tap = (nt * 16) / CIN, cb = (nt * 16) % CIN;
-            const int ky = tap / K, kx = tap % K;
-            const int ch = cb + 4 * p4;
-            s16x4_t lo = ds_read_tr(xt + lds_off<CIN>(ya * S + ky, xa * S + kx, wpx, ch >> 3) + (ch & 7));
-            s16x4_t hi = ds_read_tr(xt + lds_off<CIN>(yb * S + ky, xb * S + kx, wpx, ch >> 3) + (ch & 7));
-            const bf16x8_t bfr = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      for (int m = 0; m < MT; ++m) {
+        s16x4_t lo = ds_read_tr(da + ks * dinc + m * 16);
+        s16x4_t hi = ds_read_tr(db + ks * dinc + m * 16);
+        af[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
 #pragma unroll
-            for (int m = 0; m < MT; ++m) acc[j][m] = mfma16(af[m], bfr, acc[j][m]);
-          }
+      for (int j = 0; j < NJ; ++j) {
+        const int nt = wave + 4 * j;
+        if (nt < NTN) {
+          s16x4_t lo = ds_read_tr(xa_ + ks * xinc + boff[j]);
+          s16x4_t hi = ds_read_tr(xb_ + ks * xinc + boff[j]);
+          const bf16x8_t bfr = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+          for (int m = 0; m < MT; ++m) acc[j][m] = mfma16(af[m], bfr, acc[j][m]);
         }
       }
-      __syncthreads();
     }
+    if (it + 1 < nit) {
+      tile_store<CIN, MODE_X, 4>(xbuf[cur ^ 1], rx, nxs, nullptr, noy0 * S - P, rows_in, -P, wpx, a.Hi, a.Wi, coef_x);
+      tile_store<COUT, MODE_DY, 2>(dbuf[cur ^ 1], rd, nds, nds2, noy0, rows, 0, a.Wo, a.Ho, a.Wo, coef_d);
+    }
+    __syncthreads();
   }
   // epilogue: D[co][n] with co = m*16 + 4*(lane>>4) + r, n-col = lane & 15
   float* gb = a.grads + (long)slot * a.g_mstride + a.g_off;

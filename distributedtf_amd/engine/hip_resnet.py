@@ -320,8 +320,10 @@ class _StepPlan:
             self._work_cache[key] = w
         return w
 
-    def _n_wg(self, act_bytes, weight_bytes, lo=256, hi=2048):
-        return int(max(lo, min(hi, 2 * act_bytes // max(1, weight_bytes))))
+    def _n_wg_iters(self, total_iters, per_wg=4, lo=256, hi=1024):
+        """Enough (image, band) iterations per workgroup for the double-buffered pipeline,
+        while keeping >= lo workgroups (fill 256 CUs) when the batch allows."""
+        return int(max(lo, min(hi, total_iters // per_wg)))
 
     def _work_member(self, target_items=256, min_chunk=1):
         key = ("m", target_items)
@@ -374,7 +376,7 @@ class _StepPlan:
                 break
         assert rows is not None, ("no valid band for conv", ci)
         bands = Ho // rows
-        n_wg = self._n_wg(self.N * Hi * Hi * cin * 2, c.cout * c.k * c.k * cin * 2)
+        n_wg = self._n_wg_iters(self.N * bands)
         work = self._work_iters(bands, n_wg)
         a = self._base_args()
         a.x, a.y, a.res = _p(x), _p(y), _p(res)
@@ -409,7 +411,7 @@ class _StepPlan:
         assert rows is not None, ("no valid band for dgrad", ci)
         rows_t = rows + K - 1 if S == 1 else (rows + K + S - 2) // S + 1
         bands = Hi // rows
-        n_wg = self._n_wg(self.N * Ho * Ho * c.cout * 2, c.cout * c.k * c.k * c.cin * 2)
+        n_wg = self._n_wg_iters(self.N * bands)
         work = self._work_iters(bands, n_wg)
         a = self._base_args()
         a.x, a.x2, a.y, a.res, a.xm = _p(dy), _p(dy2), _p(y), _p(res), _p(xm)
@@ -449,7 +451,8 @@ class _StepPlan:
             rows = _pick_rows(Ho, Ho, 1, 32, target_items=1, max_rows=8)
         # images per workgroup: bound the fp32 atomic traffic of the per-WG partial dW (~12 MB per launch)
         wn = c.cout * c.k * c.k * c.cin
-        n_wg = max(64, min(4096, int(12e6 / (4.0 * wn))))
+        # bound fp32 atomic traffic (~12 MB / launch) and same-address contention (<= 128 WGs per member)
+        n_wg = max(64, min(128 * len(self.slots), int(12e6 / (4.0 * wn))))
         work = self._work_iters(Ho // rows, n_wg)
         a = self._base_args()
         a.x, a.dy, a.dy2 = _p(x), _p(dy), _p(dy2)

@@ -159,11 +159,47 @@ __device__ __forceinline__ void stage_tile(bf16_t* __restrict__ tile, const bf16
   }
 }
 
-// Register-staged variant of stage_tile for double buffering: tile_load issues the
-// global loads (up to MAXC 16-byte chunks per thread) into registers; tile_store
-// applies the transform and writes LDS.  Chunks beyond MAXC*blockDim are staged
-// synchronously by tile_store (correct for any shape, fast when the host sizes
-// bands to fit).
+// Register-staged tile staging for double buffering.  The tile geometry (rows,
+// columns, halo) is identical for every iteration of a workgroup, so each thread's
+// chunk -> (tile row, LDS offset, in-row global offset) mapping is computed once
+// (TileDesc) and an iteration only adds its first global row: no integer division
+// in the steady state.  tile_load issues the 16-byte global loads into registers;
+// tile_store applies the transform (BN+ReLU / BN-backward) and writes LDS.
+// Chunks beyond MAXC*blockDim fall back to synchronous staging in tile_store.
+template <int C, int MAXC>
+struct TileDesc {
+  int loff[MAXC];  // LDS element offset, -1: slot unused
+  int r[MAXC];     // tile row
+  int gxo[MAXC];   // gx*C + chunk*8 inside the image row, -1: halo column
+  int total, rows_in, gx0, wp;
+};
+
+template <int C, int MAXC>
+__device__ __forceinline__ void tile_desc_init(TileDesc<C, MAXC>& d, int rows_in, int gx0, int wp, int W) {
+  constexpr int NCH = C / 8;
+  d.total = rows_in * wp * NCH;
+  d.rows_in = rows_in;
+  d.gx0 = gx0;
+  d.wp = wp;
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int idx = threadIdx.x + j * blockDim.x;
+    d.loff[j] = -1;
+    d.r[j] = 0;
+    d.gxo[j] = -1;
+    if (idx < d.total) {
+      const int chunk = idx % NCH;
+      const int pc = idx / NCH;
+      const int col = pc % wp;
+      const int r = pc / wp;
+      const int gx = gx0 + col;
+      d.loff[j] = lds_off<C>(r, col, wp, chunk);
+      d.r[j] = r;
+      d.gxo[j] = (gx >= 0 && gx < W) ? gx * C + chunk * 8 : -1;
+    }
+  }
+}
+
 template <int C, int MODE, int MAXC>
 struct TileRegs {
   uint4 v[MAXC];
@@ -171,27 +207,19 @@ struct TileRegs {
 };
 
 template <int C, int MODE, int MAXC>
-__device__ __forceinline__ void tile_load(TileRegs<C, MODE, MAXC>& R, const bf16_t* __restrict__ src,
-                                          const bf16_t* __restrict__ src2, int gy0, int rows_in, int gx0, int wp, int H,
-                                          int W) {
-  constexpr int NCH = C / 8;
-  const int total = rows_in * wp * NCH;
+__device__ __forceinline__ void tile_load(TileRegs<C, MODE, MAXC>& R, const TileDesc<C, MAXC>& d,
+                                          const bf16_t* __restrict__ src, const bf16_t* __restrict__ src2, int gy0,
+                                          int H, int W) {
+  const long row = (long)W * C;
 #pragma unroll
   for (int j = 0; j < MAXC; ++j) {
-    const int idx = threadIdx.x + j * blockDim.x;
+    const int gy = gy0 + d.r[j];
     R.v[j] = make_uint4(0, 0, 0, 0);
     if constexpr (MODE == 2) R.v2[j] = make_uint4(0, 0, 0, 0);
-    if (idx < total) {
-      const int chunk = idx % NCH;
-      const int pc = idx / NCH;
-      const int col = pc % wp;
-      const int r = pc / wp;
-      const int gy = gy0 + r, gx = gx0 + col;
-      if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
-        const long off = ((long)gy * W + gx) * C + chunk * 8;
-        R.v[j] = *reinterpret_cast<const uint4*>(src + off);
-        if constexpr (MODE == 2) R.v2[j] = *reinterpret_cast<const uint4*>(src2 + off);
-      }
+    if (d.gxo[j] >= 0 && gy >= 0 && gy < H) {
+      const long off = gy * row + d.gxo[j];
+      R.v[j] = *reinterpret_cast<const uint4*>(src + off);
+      if constexpr (MODE == 2) R.v2[j] = *reinterpret_cast<const uint4*>(src2 + off);
     }
   }
 }
@@ -204,12 +232,12 @@ __device__ __forceinline__ uint4 transform8(uint4 v, uint4 v2, int c0, const flo
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int c = c0 + 2 * j;
-    float a0 = bf2f((bf16_t)(w32[j] & 0xffff)), a1 = bf2f((bf16_t)(w32[j] >> 16));
+    float a0 = __uint_as_float(w32[j] << 16), a1 = __uint_as_float(w32[j] & 0xffff0000u);
     if constexpr (MODE == 1) {
       a0 = fmaxf(a0 * coef[c] + coef[64 + c], 0.f);
       a1 = fmaxf(a1 * coef[c + 1] + coef[64 + c + 1], 0.f);
     } else {
-      float h0 = bf2f((bf16_t)(h32[j] & 0xffff)), h1 = bf2f((bf16_t)(h32[j] >> 16));
+      const float h0 = __uint_as_float(h32[j] << 16), h1 = __uint_as_float(h32[j] & 0xffff0000u);
       a0 = coef[c] * a0 + coef[64 + c] * h0 + coef[128 + c];
       a1 = coef[c + 1] * a1 + coef[64 + c + 1] * h1 + coef[128 + c + 1];
     }
@@ -220,31 +248,27 @@ __device__ __forceinline__ uint4 transform8(uint4 v, uint4 v2, int c0, const flo
 
 template <int C, int MODE, int MAXC>
 __device__ __forceinline__ void tile_store(bf16_t* __restrict__ tile, const TileRegs<C, MODE, MAXC>& R,
-                                           const bf16_t* __restrict__ src, const bf16_t* __restrict__ src2, int gy0,
-                                           int rows_in, int gx0, int wp, int H, int W,
+                                           const TileDesc<C, MAXC>& d, const bf16_t* __restrict__ src,
+                                           const bf16_t* __restrict__ src2, int gy0, int H, int W,
                                            const float* __restrict__ coef) {
   constexpr int NCH = C / 8;
-  const int total = rows_in * wp * NCH;
 #pragma unroll
   for (int j = 0; j < MAXC; ++j) {
-    const int idx = threadIdx.x + j * blockDim.x;
-    if (idx < total) {
-      const int chunk = idx % NCH;
-      const int pc = idx / NCH;
-      const int col = pc % wp;
-      const int r = pc / wp;
-      const int gy = gy0 + r, gx = gx0 + col;
+    if (d.loff[j] >= 0) {
+      const int gy = gy0 + d.r[j];
       uint4 v = R.v[j];
-      if (gy >= 0 && gy < H && gx >= 0 && gx < W) v = transform8<MODE>(v, MODE == 2 ? R.v2[j] : v, chunk * 8, coef);
-      *reinterpret_cast<uint4*>(tile + lds_off<C>(r, col, wp, chunk)) = v;
+      if constexpr (MODE != 0) {
+        if (d.gxo[j] >= 0 && gy >= 0 && gy < H) v = transform8<MODE>(v, MODE == 2 ? R.v2[j] : v, d.gxo[j] & (C - 1), coef);
+      }
+      *reinterpret_cast<uint4*>(tile + d.loff[j]) = v;
     }
   }
-  for (int idx = threadIdx.x + MAXC * blockDim.x; idx < total; idx += blockDim.x) {  // overflow (rare)
+  for (int idx = threadIdx.x + MAXC * blockDim.x; idx < d.total; idx += blockDim.x) {  // overflow (rare)
     const int chunk = idx % NCH;
     const int pc = idx / NCH;
-    const int col = pc % wp;
-    const int r = pc / wp;
-    const int gy = gy0 + r, gx = gx0 + col;
+    const int col = pc % d.wp;
+    const int r = pc / d.wp;
+    const int gy = gy0 + r, gx = d.gx0 + col;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
       const long off = ((long)gy * W + gx) * C + chunk * 8;
@@ -253,7 +277,7 @@ __device__ __forceinline__ void tile_store(bf16_t* __restrict__ tile, const Tile
       if constexpr (MODE == 2) v2 = *reinterpret_cast<const uint4*>(src2 + off);
       v = transform8<MODE>(v, v2, chunk * 8, coef);
     }
-    *reinterpret_cast<uint4*>(tile + lds_off<C>(r, col, wp, chunk)) = v;
+    *reinterpret_cast<uint4*>(tile + lds_off<C>(r, col, d.wp, chunk)) = v;
   }
 }
 
@@ -374,12 +398,13 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   }
   float ssum[4] = {0.f, 0.f, 0.f, 0.f}, ssq[4] = {0.f, 0.f, 0.f, 0.f};
   TileRegs<CIN, MODE_IN, 4> rg;
+  TileDesc<CIN, 4> td;
+  tile_desc_init<CIN, 4>(td, rows_in, -P, wp, a.Wi);
   __syncthreads();  // coefficients
   {
     const int img = it0 / bands, oy0 = (it0 % bands) * rows;
-    tile_load<CIN, MODE_IN, 4>(rg, a.x + img * img_elems, nullptr, oy0 * S - P, rows_in, -P, wp, a.Hi, a.Wi);
-    tile_store<CIN, MODE_IN, 4>(tiles[0], rg, a.x + img * img_elems, nullptr, oy0 * S - P, rows_in, -P, wp, a.Hi,
-                                a.Wi, coef);
+    tile_load<CIN, MODE_IN, 4>(rg, td, a.x + img * img_elems, nullptr, oy0 * S - P, a.Hi, a.Wi);
+    tile_store<CIN, MODE_IN, 4>(tiles[0], rg, td, a.x + img * img_elems, nullptr, oy0 * S - P, a.Hi, a.Wi, coef);
   }
   __syncthreads();
   for (int k = 0; k < nit; ++k) {
@@ -387,13 +412,16 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
     const int img = it / bands, oy0 = (it % bands) * rows;
     const bool more = k + 1 < nit;
     const int nimg_ = (it + 1) / bands, noy0 = ((it + 1) % bands) * rows;
-    if (more)
-      tile_load<CIN, MODE_IN, 4>(rg, a.x + nimg_ * img_elems, nullptr, noy0 * S - P, rows_in, -P, wp, a.Hi, a.Wi);
+    if (more) tile_load<CIN, MODE_IN, 4>(rg, td, a.x + nimg_ * img_elems, nullptr, noy0 * S - P, a.Hi, a.Wi);
     const bf16_t* tile = tiles[k & 1];
     for (int t = wave / NT; t < ntiles; t += WPT) {
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
       const int p = t * 16 + (lane & 15);
       const int oy = p / a.Wo, ox = p % a.Wo;
+      const int co0 = ct * 16 + (lane >> 4) * 4;
+      const long o = (((long)img * a.Ho + oy0 + oy) * a.Wo + ox) * COUT + co0;
+      uint2 r = make_uint2(0, 0);
+      if constexpr (RESID) r = *reinterpret_cast<const uint2*>(a.res + o);  // issued ahead of the MFMA chain
       const bf16_t* tb = tile + (oy * S * wp + ox * S) * cpad<CIN>();
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
@@ -401,11 +429,8 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
         if (32 * s + 8 * (lane >> 4) < KTOT) b = *reinterpret_cast<const bf16x8_t*>(tb + tapoff[s]);
         acc = mfma16(afr[s], b, acc);
       }
-      const int co0 = ct * 16 + (lane >> 4) * 4;
-      const long o = (((long)img * a.Ho + oy0 + oy) * a.Wo + ox) * COUT + co0;
       float v[4] = {acc[0], acc[1], acc[2], acc[3]};
       if constexpr (RESID) {
-        const uint2 r = *reinterpret_cast<const uint2*>(a.res + o);
         v[0] += bf2f((bf16_t)(r.x & 0xffff));
         v[1] += bf2f((bf16_t)(r.x >> 16));
         v[2] += bf2f((bf16_t)(r.y & 0xffff));
@@ -425,8 +450,8 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
       }
     }
     if (more)
-      tile_store<CIN, MODE_IN, 4>(tiles[(k + 1) & 1], rg, a.x + nimg_ * img_elems, nullptr, noy0 * S - P, rows_in, -P,
-                                  wp, a.Hi, a.Wi, coef);
+      tile_store<CIN, MODE_IN, 4>(tiles[(k + 1) & 1], rg, td, a.x + nimg_ * img_elems, nullptr, noy0 * S - P, a.Hi,
+                                  a.Wi, coef);
     __syncthreads();
   }
   if constexpr (STATS) {
@@ -509,12 +534,14 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
   }
   float ssum[4] = {0.f, 0.f, 0.f, 0.f}, ssq[4] = {0.f, 0.f, 0.f, 0.f};
   TileRegs<CO, MODE_IN, 4> rg;
+  TileDesc<CO, 4> td;
+  tile_desc_init<CO, 4>(td, rows_t, -1, wp, a.Wo);
   __syncthreads();
   {
     const int img = it0 / bands, iy0 = (it0 % bands) * rows;
     const bf16_t* x2 = a.x2 ? a.x2 + img * img_elems : nullptr;
-    tile_load<CO, MODE_IN, 4>(rg, a.x + img * img_elems, x2, dy_lo(iy0), rows_t, -1, wp, a.Ho, a.Wo);
-    tile_store<CO, MODE_IN, 4>(tiles[0], rg, a.x + img * img_elems, x2, dy_lo(iy0), rows_t, -1, wp, a.Ho, a.Wo, coef);
+    tile_load<CO, MODE_IN, 4>(rg, td, a.x + img * img_elems, x2, dy_lo(iy0), a.Ho, a.Wo);
+    tile_store<CO, MODE_IN, 4>(tiles[0], rg, td, a.x + img * img_elems, x2, dy_lo(iy0), a.Ho, a.Wo, coef);
   }
   __syncthreads();
   for (int k = 0; k < nit; ++k) {
@@ -524,12 +551,17 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
     const bool more = k + 1 < nit;
     const int nimg_ = (it + 1) / bands, niy0 = ((it + 1) % bands) * rows;
     const bf16_t* nx2 = a.x2 ? a.x2 + nimg_ * img_elems : nullptr;
-    if (more) tile_load<CO, MODE_IN, 4>(rg, a.x + nimg_ * img_elems, nx2, dy_lo(niy0), rows_t, -1, wp, a.Ho, a.Wo);
+    if (more) tile_load<CO, MODE_IN, 4>(rg, td, a.x + nimg_ * img_elems, nx2, dy_lo(niy0), a.Ho, a.Wo);
     const bf16_t* tile = tiles[k & 1];
     for (int t = wave / NT; t < ntiles; t += WPT) {
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
       const int p = t * 16 + (lane & 15);
       const int iy = iy0 + p / a.Wi, ix = p % a.Wi;
+      const int ci0 = ct * 16 + (lane >> 4) * 4;
+      const long o = (((long)img * a.Hi + iy) * a.Wi + ix) * CI + ci0;
+      uint2 rr = make_uint2(0, 0), xr = make_uint2(0, 0);  // epilogue operands, issued ahead of the MFMAs
+      if constexpr (EPI & 1) rr = *reinterpret_cast<const uint2*>(a.res + o);
+      if constexpr (EPI & 2) xr = *reinterpret_cast<const uint2*>(a.xm + o);
       // stride 1: dy(iy+P-ky, ix+P-kx) lives at tile row iy+P-oy_lo-ky, col ix+P+1-kx
       const bf16_t* tb = tile + ((iy + P - oy_lo) * wp + ix + P + 1) * cpad<CO>();
 #pragma unroll
@@ -555,19 +587,15 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
         }
         acc = mfma16(afr[s], b, acc);
       }
-      const int ci0 = ct * 16 + (lane >> 4) * 4;
-      const long o = (((long)img * a.Hi + iy) * a.Wi + ix) * CI + ci0;
       float v[4] = {acc[0], acc[1], acc[2], acc[3]};
       if constexpr (EPI & 1) {
-        const uint2 r = *reinterpret_cast<const uint2*>(a.res + o);
-        v[0] += bf2f((bf16_t)(r.x & 0xffff));
-        v[1] += bf2f((bf16_t)(r.x >> 16));
-        v[2] += bf2f((bf16_t)(r.y & 0xffff));
-        v[3] += bf2f((bf16_t)(r.y >> 16));
+        v[0] += bf2f((bf16_t)(rr.x & 0xffff));
+        v[1] += bf2f((bf16_t)(rr.x >> 16));
+        v[2] += bf2f((bf16_t)(rr.y & 0xffff));
+        v[3] += bf2f((bf16_t)(rr.y >> 16));
       }
       float xv[4] = {0.f, 0.f, 0.f, 0.f};
       if constexpr (EPI & 2) {
-        const uint2 xr = *reinterpret_cast<const uint2*>(a.xm + o);
         xv[0] = bf2f((bf16_t)(xr.x & 0xffff));
         xv[1] = bf2f((bf16_t)(xr.x >> 16));
         xv[2] = bf2f((bf16_t)(xr.y & 0xffff));
@@ -595,8 +623,8 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
       }
     }
     if (more)
-      tile_store<CO, MODE_IN, 4>(tiles[(k + 1) & 1], rg, a.x + nimg_ * img_elems, nx2, dy_lo(niy0), rows_t, -1, wp,
-                                 a.Ho, a.Wo, coef);
+      tile_store<CO, MODE_IN, 4>(tiles[(k + 1) & 1], rg, td, a.x + nimg_ * img_elems, nx2, dy_lo(niy0), a.Ho, a.Wo,
+                                 coef);
     __syncthreads();
   }
   if constexpr (EPI & 2) {
@@ -654,6 +682,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p4 = i & 3;
   TileRegs<CIN, MODE_X, 4> rx;
   TileRegs<COUT, MODE_DY, 2> rd;
+  TileDesc<CIN, 4> tdx;
+  TileDesc<COUT, 2> tdd;
+  tile_desc_init<CIN, 4>(tdx, rows_in, -P, wpx, a.Wi);
+  tile_desc_init<COUT, 2>(tdd, rows, 0, a.Wo, a.Wo);
   auto src_of = [&](int it, const bf16_t*& xs, const bf16_t*& ds, const bf16_t*& ds2, int& oy0) {
     const int img = (it0 + it) / bands;
     oy0 = ((it0 + it) % bands) * rows;
@@ -667,10 +699,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
     const bf16_t *xs, *ds, *ds2;
     int oy0;
     src_of(0, xs, ds, ds2, oy0);
-    tile_load<CIN, MODE_X, 4>(rx, xs, nullptr, oy0 * S - P, rows_in, -P, wpx, a.Hi, a.Wi);
-    tile_load<COUT, MODE_DY, 2>(rd, ds, ds2, oy0, rows, 0, a.Wo, a.Ho, a.Wo);
-    tile_store<CIN, MODE_X, 4>(xbuf[0], rx, xs, nullptr, oy0 * S - P, rows_in, -P, wpx, a.Hi, a.Wi, coef_x);
-    tile_store<COUT, MODE_DY, 2>(dbuf[0], rd, ds, ds2, oy0, rows, 0, a.Wo, a.Ho, a.Wo, coef_d);
+    tile_load<CIN, MODE_X, 4>(rx, tdx, xs, nullptr, oy0 * S - P, a.Hi, a.Wi);
+    tile_load<COUT, MODE_DY, 2>(rd, tdd, ds, ds2, oy0, a.Ho, a.Wo);
+    tile_store<CIN, MODE_X, 4>(xbuf[0], rx, tdx, xs, nullptr, oy0 * S - P, a.Hi, a.Wi, coef_x);
+    tile_store<COUT, MODE_DY, 2>(dbuf[0], rd, tdd, ds, ds2, oy0, a.Ho, a.Wo, coef_d);
   }
   __syncthreads();
   for (int it = 0; it < nit; ++it) {
@@ -679,8 +711,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
     int noy0 = 0;
     if (it + 1 < nit) {  // prefetch the next (image, band) into registers
       src_of(it + 1, nxs, nds, nds2, noy0);
-      tile_load<CIN, MODE_X, 4>(rx, nxs, nullptr, noy0 * S - P, rows_in, -P, wpx, a.Hi, a.Wi);
-      tile_load<COUT, MODE_DY, 2>(rd, nds, nds2, noy0, rows, 0, a.Wo, a.Ho, a.Wo);
+      tile_load<CIN, MODE_X, 4>(rx, tdx, nxs, nullptr, noy0 * S - P, a.Hi, a.Wi);
+      tile_load<COUT, MODE_DY, 2>(rd, tdd, nds, nds2, noy0, a.Ho, a.Wo);
     }
     const bf16_t* xcur = xbuf[cur];
     const bf16_t* dcur = dbuf[cur];
@@ -725,8 +757,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
       }
     }
     if (it + 1 < nit) {
-      tile_store<CIN, MODE_X, 4>(xbuf[cur ^ 1], rx, nxs, nullptr, noy0 * S - P, rows_in, -P, wpx, a.Hi, a.Wi, coef_x);
-      tile_store<COUT, MODE_DY, 2>(dbuf[cur ^ 1], rd, nds, nds2, noy0, rows, 0, a.Wo, a.Ho, a.Wo, coef_d);
+      tile_store<CIN, MODE_X, 4>(xbuf[cur ^ 1], rx, tdx, nxs, nullptr, noy0 * S - P, a.Hi, a.Wi, coef_x);
+      tile_store<COUT, MODE_DY, 2>(dbuf[cur ^ 1], rd, tdd, nds, nds2, noy0, a.Ho, a.Wo, coef_d);
     }
     __syncthreads();
   }

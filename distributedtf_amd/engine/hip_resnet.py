@@ -83,6 +83,7 @@ def _register():
                                   c_void_p])
     ops.register("dtf_conv_dgrad", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_wgrad", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
+    ops.register("dtf_conv_bwd_fused", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_args_size", [])
     ops.register("dtf_bnbwd_args_size", [])
     ops.register("dtf_head_args_size", [])
@@ -475,6 +476,41 @@ class _StepPlan:
         self._add(lib.dtf_conv_wgrad, ctypes.byref(a), cin, c.cout, c.stride, c.k, mode_x, mode_dy, work.shape[0], lds)
         self._keep(a)
 
+    def _conv_bwd_fused(self, ci, dy, dz_out, x, mode_dy, dy2=None, dy_bn=None, x_bn=None, res=None):
+        """dgrad + wgrad of a stride-1 3x3 C->C conv in one launch (see conv_bwd_fused_kernel)."""
+        be, L = self.be, self.be.L
+        c = L.prog.convs[ci]
+        assert c.stride == 1 and c.k == 3 and c.cin == c.cout
+        C, H = c.cin, x.shape[1]
+        rows = None
+        for r in (8, 4, 2):
+            if H % r == 0 and (r * H) % 32 == 0 and (r + 2) * (H + 2) * (C // 8) <= 4 * 256:
+                rows = r
+                break
+        assert rows is not None
+        bands = H // rows
+        wn = 9 * C * C
+        n_wg = max(64, min(128 * len(self.slots), int(16e6 / (4.0 * wn))))
+        n_wg = min(n_wg, self.N * bands)
+        work = self._work_iters(bands, n_wg)
+        a = self._base_args()
+        a.x, a.x2, a.y, a.xm, a.res = _p(dy), _p(dy2), _p(dz_out), _p(x), _p(res)
+        a.w, a.w_off = _p(be.wd), L.dgr_off[ci]
+        a.work = _p(work)
+        a.g_off = c.off
+        if dy_bn is not None:
+            a.in_gamma, a.in_beta = self._bn(dy_bn)
+            a.st_in, a.st_in_b = _p(be.st_f(dy_bn)), _p(be.st_b(dy_bn))
+        a.ep_gamma, a.ep_beta = self._bn(x_bn)
+        a.st_ep = _p(be.st_f(x_bn))
+        a.st_out = _p(be.st_b(x_bn))
+        a.Hi, a.Wi, a.Ho, a.Wo, a.rows = H, H, H, H, rows
+        tsz = ((rows + 2) * (H + 2) * (C + 8) + 63) // 64 * 64
+        lds = 2304 + 4 * tsz * 2
+        lib = ops.lib()
+        self._add(lib.dtf_conv_bwd_fused, ctypes.byref(a), C, mode_dy, int(res is not None), work.shape[0], lds)
+        self._keep(a)
+
     def _keep(self, obj):
         if not hasattr(self, "_keepalive"):
             self._keepalive = []
@@ -537,9 +573,13 @@ class _StepPlan:
             Hi, Ho = x.shape[1], h.shape[1]
             T = self.tmp[Ho]
             ca, cb = blk.convs
+            fused = os.environ.get("DTF_FUSED_BWD", "1") == "1"
             # conv_b: dgrad -> dz2 (mask by BN2(h), BN2 reductions); wgrad
-            self._conv_dgrad(cb, g_cur, T["dz2"], Ho, mode=0, epi=2, xm=h, ep_bn=bn2)
-            self._conv_wgrad(cb, h, g_cur, mode_x=1, mode_dy=0, x_bn=bn2)
+            if fused:
+                self._conv_bwd_fused(cb, g_cur, T["dz2"], h, mode_dy=0, x_bn=bn2)
+            else:
+                self._conv_dgrad(cb, g_cur, T["dz2"], Ho, mode=0, epi=2, xm=h, ep_bn=bn2)
+                self._conv_wgrad(cb, h, g_cur, mode_x=1, mode_dy=0, x_bn=bn2)
             Tin = self.tmp[Hi]
             pd = None
             if blk.proj is not None:
@@ -547,9 +587,13 @@ class _StepPlan:
                 self._conv_dgrad(blk.proj, g_cur, pd, Hi, mode=0, epi=0)
                 self._conv_wgrad(blk.proj, x, g_cur, mode_x=1, mode_dy=0, x_bn=bn1)
             # conv_a: dgrad of BN2-backward(dz2, h) [+ proj dgrad], mask by BN1(x), BN1 reductions
-            self._conv_dgrad(ca, T["dz2"], Tin["dz1"], Hi, mode=2, epi=2 | (1 if pd is not None else 0), dy2=h,
-                             in_bn=bn2, res=pd, xm=x, ep_bn=bn1)
-            self._conv_wgrad(ca, x, T["dz2"], mode_x=1, mode_dy=2, x_bn=bn1, dy_bn=bn2, dy2=h)
+            ca_spec = prog.convs[ca]
+            if fused and ca_spec.stride == 1 and ca_spec.cin == ca_spec.cout:
+                self._conv_bwd_fused(ca, T["dz2"], Tin["dz1"], x, mode_dy=2, dy2=h, dy_bn=bn2, x_bn=bn1, res=pd)
+            else:
+                self._conv_dgrad(ca, T["dz2"], Tin["dz1"], Hi, mode=2, epi=2 | (1 if pd is not None else 0), dy2=h,
+                                 in_bn=bn2, res=pd, xm=x, ep_bn=bn1)
+                self._conv_wgrad(ca, x, T["dz2"], mode_x=1, mode_dy=2, x_bn=bn1, dy_bn=bn2, dy2=h)
             # g_in = BN1-backward(dz1, x) [+ g_out if identity shortcut]
             g_next = Tin["g"][1] if g_cur is Tin["g"][0] else Tin["g"][0]
             ba = BnBwdArgs()

@@ -204,23 +204,27 @@ template <int C, int MODE, int MAXC>
 struct TileRegs {
   uint4 v[MAXC];
   uint4 v2[MODE == 2 ? MAXC : 1];
+  unsigned ok;  // bit j: chunk j is inside the image (else it stages zeros)
 };
 
+// Branch-free: every slot issues its load (an out-of-image chunk reads the image's
+// first chunk and is zeroed at store time), so the compiler sees a fixed number of
+// outstanding loads and can wait for the epilogue operands with a counted vmcnt
+// instead of draining this prefetch.
 template <int C, int MODE, int MAXC>
 __device__ __forceinline__ void tile_load(TileRegs<C, MODE, MAXC>& R, const TileDesc<C, MAXC>& d,
                                           const bf16_t* __restrict__ src, const bf16_t* __restrict__ src2, int gy0,
                                           int H, int W) {
   const long row = (long)W * C;
+  R.ok = 0;
 #pragma unroll
   for (int j = 0; j < MAXC; ++j) {
     const int gy = gy0 + d.r[j];
-    R.v[j] = make_uint4(0, 0, 0, 0);
-    if constexpr (MODE == 2) R.v2[j] = make_uint4(0, 0, 0, 0);
-    if (d.gxo[j] >= 0 && gy >= 0 && gy < H) {
-      const long off = gy * row + d.gxo[j];
-      R.v[j] = *reinterpret_cast<const uint4*>(src + off);
-      if constexpr (MODE == 2) R.v2[j] = *reinterpret_cast<const uint4*>(src2 + off);
-    }
+    const bool ok = (d.gxo[j] >= 0) & (gy >= 0) & (gy < H);
+    const long off = ok ? gy * row + d.gxo[j] : 0;
+    R.ok |= (ok ? 1u : 0u) << j;
+    R.v[j] = *reinterpret_cast<const uint4*>(src + off);
+    if constexpr (MODE == 2) R.v2[j] = *reinterpret_cast<const uint4*>(src2 + off);
   }
 }
 
@@ -255,11 +259,8 @@ __device__ __forceinline__ void tile_store(bf16_t* __restrict__ tile, const Tile
 #pragma unroll
   for (int j = 0; j < MAXC; ++j) {
     if (d.loff[j] >= 0) {
-      const int gy = gy0 + d.r[j];
-      uint4 v = R.v[j];
-      if constexpr (MODE != 0) {
-        if (d.gxo[j] >= 0 && gy >= 0 && gy < H) v = transform8<MODE>(v, MODE == 2 ? R.v2[j] : v, d.gxo[j] & (C - 1), coef);
-      }
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if ((R.ok >> j) & 1u) v = transform8<MODE>(R.v[j], MODE == 2 ? R.v2[j] : R.v[j], d.gxo[j] & (C - 1), coef);
       *reinterpret_cast<uint4*>(tile + d.loff[j]) = v;
     }
   }
@@ -350,6 +351,8 @@ __device__ __forceinline__ void flush_stats(float* st_out, const float* acc_lds,
 // into registers (tile_load) while the MFMAs of the current one run, then
 // written to the other LDS buffer (double buffering).
 
+constexpr int MAXT = 4;  // output tiles per wave per iteration (host-checked)
+
 template <int CIN, int COUT, int S, int K, int MODE_IN, bool RESID, bool STATS>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   constexpr int NT = COUT / 16;
@@ -386,7 +389,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   const int rows_in = (rows - 1) * S + K;
   const int wp = a.Wi + 2 * P;
   const int tsz = (rows_in * wp * cpad<CIN>() + 63) & ~63;
-  bf16_t* tiles[2] = {tile0, tile0 + tsz};
+#define TILEBUF(i) (tile0 + ((i) & 1) * tsz)
   const int ntiles = rows * a.Wo / 16;
   const long img_elems = (long)a.Hi * a.Wi * CIN;
   int tapoff[KS];  // per-lane LDS offset of each k-step's tap/channel chunk
@@ -404,7 +407,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   {
     const int img = it0 / bands, oy0 = (it0 % bands) * rows;
     tile_load<CIN, MODE_IN, 4>(rg, td, a.x + img * img_elems, nullptr, oy0 * S - P, a.Hi, a.Wi);
-    tile_store<CIN, MODE_IN, 4>(tiles[0], rg, td, a.x + img * img_elems, nullptr, oy0 * S - P, a.Hi, a.Wi, coef);
+    tile_store<CIN, MODE_IN, 4>(TILEBUF(0), rg, td, a.x + img * img_elems, nullptr, oy0 * S - P, a.Hi, a.Wi, coef);
   }
   __syncthreads();
   for (int k = 0; k < nit; ++k) {
@@ -412,16 +415,32 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
     const int img = it / bands, oy0 = (it % bands) * rows;
     const bool more = k + 1 < nit;
     const int nimg_ = (it + 1) / bands, noy0 = ((it + 1) % bands) * rows;
+    // epilogue operands of every tile of this iteration first, then the next tile's prefetch:
+    // the residual wait is a counted vmcnt that leaves the prefetch in flight
+    uint2 rres[MAXT];
+    if constexpr (RESID) {
+#pragma unroll
+      for (int i = 0; i < MAXT; ++i) {
+        const int t = min(wave / NT + WPT * i, ntiles - 1);
+        const int p = t * 16 + (lane & 15);
+        const int oy = p / a.Wo, ox = p % a.Wo;
+        rres[i] = *reinterpret_cast<const uint2*>(
+            a.res + (((long)img * a.Ho + oy0 + oy) * a.Wo + ox) * COUT + ct * 16 + (lane >> 4) * 4);
+      }
+    }
     if (more) tile_load<CIN, MODE_IN, 4>(rg, td, a.x + nimg_ * img_elems, nullptr, noy0 * S - P, a.Hi, a.Wi);
-    const bf16_t* tile = tiles[k & 1];
-    for (int t = wave / NT; t < ntiles; t += WPT) {
+    const bf16_t* tile = TILEBUF(k);
+#pragma unroll
+    for (int i = 0; i < MAXT; ++i) {
+      const int t = wave / NT + WPT * i;
+      if (t >= ntiles) break;
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
       const int p = t * 16 + (lane & 15);
       const int oy = p / a.Wo, ox = p % a.Wo;
       const int co0 = ct * 16 + (lane >> 4) * 4;
       const long o = (((long)img * a.Ho + oy0 + oy) * a.Wo + ox) * COUT + co0;
       uint2 r = make_uint2(0, 0);
-      if constexpr (RESID) r = *reinterpret_cast<const uint2*>(a.res + o);  // issued ahead of the MFMA chain
+      if constexpr (RESID) r = rres[i];
       const bf16_t* tb = tile + (oy * S * wp + ox * S) * cpad<CIN>();
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
@@ -450,7 +469,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
       }
     }
     if (more)
-      tile_store<CIN, MODE_IN, 4>(tiles[(k + 1) & 1], rg, td, a.x + nimg_ * img_elems, nullptr, noy0 * S - P, a.Hi,
+      tile_store<CIN, MODE_IN, 4>(TILEBUF(k + 1), rg, td, a.x + nimg_ * img_elems, nullptr, noy0 * S - P, a.Hi,
                                   a.Wi, coef);
     __syncthreads();
   }
@@ -522,7 +541,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
   const int rows_t = (S == 1) ? rows + K - 1 : (rows + K + S - 2) / S + 1;  // dy rows per band (host: same)
   const int wp = a.Wo + 2;  // dy cols -1..Wo
   const int tsz = (rows_t * wp * cpad<CO>() + 63) & ~63;
-  bf16_t* tiles[2] = {tile0, tile0 + tsz};
+#define TILEBUF(i) (tile0 + ((i) & 1) * tsz)
   const int ntiles = rows * a.Wi / 16;
   const long img_elems = (long)a.Ho * a.Wo * CO;
   int tapoff[KS];  // stride 1: LDS offset of (dy row/col shift by the flipped tap, channel chunk)
@@ -541,7 +560,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
     const int img = it0 / bands, iy0 = (it0 % bands) * rows;
     const bf16_t* x2 = a.x2 ? a.x2 + img * img_elems : nullptr;
     tile_load<CO, MODE_IN, 4>(rg, td, a.x + img * img_elems, x2, dy_lo(iy0), a.Ho, a.Wo);
-    tile_store<CO, MODE_IN, 4>(tiles[0], rg, td, a.x + img * img_elems, x2, dy_lo(iy0), a.Ho, a.Wo, coef);
+    tile_store<CO, MODE_IN, 4>(TILEBUF(0), rg, td, a.x + img * img_elems, x2, dy_lo(iy0), a.Ho, a.Wo, coef);
   }
   __syncthreads();
   for (int k = 0; k < nit; ++k) {
@@ -551,17 +570,29 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
     const bool more = k + 1 < nit;
     const int nimg_ = (it + 1) / bands, niy0 = ((it + 1) % bands) * rows;
     const bf16_t* nx2 = a.x2 ? a.x2 + nimg_ * img_elems : nullptr;
+    uint2 rres[MAXT], xres[MAXT];  // epilogue operands, issued before the prefetch (counted vmcnt)
+#pragma unroll
+    for (int i = 0; i < MAXT; ++i) {
+      const int t = min(wave / NT + WPT * i, ntiles - 1);
+      const int p = t * 16 + (lane & 15);
+      const long o = (((long)img * a.Hi + iy0 + p / a.Wi) * a.Wi + p % a.Wi) * CI + ct * 16 + (lane >> 4) * 4;
+      if constexpr (EPI & 1) rres[i] = *reinterpret_cast<const uint2*>(a.res + o);
+      if constexpr (EPI & 2) xres[i] = *reinterpret_cast<const uint2*>(a.xm + o);
+    }
     if (more) tile_load<CO, MODE_IN, 4>(rg, td, a.x + nimg_ * img_elems, nx2, dy_lo(niy0), a.Ho, a.Wo);
-    const bf16_t* tile = tiles[k & 1];
-    for (int t = wave / NT; t < ntiles; t += WPT) {
+    const bf16_t* tile = TILEBUF(k);
+#pragma unroll
+    for (int i = 0; i < MAXT; ++i) {
+      const int t = wave / NT + WPT * i;
+      if (t >= ntiles) break;
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
       const int p = t * 16 + (lane & 15);
       const int iy = iy0 + p / a.Wi, ix = p % a.Wi;
       const int ci0 = ct * 16 + (lane >> 4) * 4;
       const long o = (((long)img * a.Hi + iy) * a.Wi + ix) * CI + ci0;
-      uint2 rr = make_uint2(0, 0), xr = make_uint2(0, 0);  // epilogue operands, issued ahead of the MFMAs
-      if constexpr (EPI & 1) rr = *reinterpret_cast<const uint2*>(a.res + o);
-      if constexpr (EPI & 2) xr = *reinterpret_cast<const uint2*>(a.xm + o);
+      uint2 rr = make_uint2(0, 0), xr = make_uint2(0, 0);
+      if constexpr (EPI & 1) rr = rres[i];
+      if constexpr (EPI & 2) xr = xres[i];
       // stride 1: dy(iy+P-ky, ix+P-kx) lives at tile row iy+P-oy_lo-ky, col ix+P+1-kx
       const bf16_t* tb = tile + ((iy + P - oy_lo) * wp + ix + P + 1) * cpad<CO>();
 #pragma unroll
@@ -623,7 +654,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
       }
     }
     if (more)
-      tile_store<CO, MODE_IN, 4>(tiles[(k + 1) & 1], rg, td, a.x + nimg_ * img_elems, nx2, dy_lo(niy0), a.Ho, a.Wo,
+      tile_store<CO, MODE_IN, 4>(TILEBUF(k + 1), rg, td, a.x + nimg_ * img_elems, nx2, dy_lo(niy0), a.Ho, a.Wo,
                                  coef);
     __syncthreads();
   }
@@ -668,8 +699,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
   const int wpx = a.Wi + 2 * P;
   const int xsz = (rows_in * wpx * cpad<CIN>() + 63) & ~63;
   const int dsz = (rows * a.Wo * cpad<COUT>() + 63) & ~63;
-  bf16_t* xbuf[2] = {xt, xt + xsz + dsz};
-  bf16_t* dbuf[2] = {xt + xsz, xt + 2 * xsz + dsz};
+#define XBUF(i) (xt + ((i) & 1) * (xsz + dsz))
+#define DBUF(i) (xt + xsz + ((i) & 1) * (xsz + dsz))
   const int npix = rows * a.Wo;
   const int bands = a.Ho / rows;
 
@@ -701,8 +732,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
     src_of(0, xs, ds, ds2, oy0);
     tile_load<CIN, MODE_X, 4>(rx, tdx, xs, nullptr, oy0 * S - P, a.Hi, a.Wi);
     tile_load<COUT, MODE_DY, 2>(rd, tdd, ds, ds2, oy0, a.Ho, a.Wo);
-    tile_store<CIN, MODE_X, 4>(xbuf[0], rx, tdx, xs, nullptr, oy0 * S - P, a.Hi, a.Wi, coef_x);
-    tile_store<COUT, MODE_DY, 2>(dbuf[0], rd, tdd, ds, ds2, oy0, a.Ho, a.Wo, coef_d);
+    tile_store<CIN, MODE_X, 4>(XBUF(0), rx, tdx, xs, nullptr, oy0 * S - P, a.Hi, a.Wi, coef_x);
+    tile_store<COUT, MODE_DY, 2>(DBUF(0), rd, tdd, ds, ds2, oy0, a.Ho, a.Wo, coef_d);
   }
   __syncthreads();
   for (int it = 0; it < nit; ++it) {
@@ -714,8 +745,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
       tile_load<CIN, MODE_X, 4>(rx, tdx, nxs, nullptr, noy0 * S - P, a.Hi, a.Wi);
       tile_load<COUT, MODE_DY, 2>(rd, tdd, nds, nds2, noy0, a.Ho, a.Wo);
     }
-    const bf16_t* xcur = xbuf[cur];
-    const bf16_t* dcur = dbuf[cur];
+    const bf16_t* xcur = XBUF(cur);
+    const bf16_t* dcur = DBUF(cur);
     // The 32 pixels of a k-step span RSTEP = 32/Wo whole rows (Wo | 32), so each
     // lane's pixel (ya, xa) is (kstep*RSTEP + (8g+q)/Wo, (8g+q)%Wo): all LDS
     // addresses are lane constants plus kstep * increment.
@@ -731,7 +762,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
     int boff[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int nt = wave + 4 * j;
+      const int nt = min(wave + 4 * j, NTN - 1);  // duplicates (nt >= NTN) are computed, never flushed
       const int tap = (nt * 16) / CIN, cb = (nt * 16) % CIN;
       boff[j] = ((tap / K) * wpx + (tap % K)) * cpad<CIN>() + cb;
     }
@@ -744,21 +775,21 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
         s16x4_t hi = ds_read_tr(db + ks * dinc + m * 16);
         af[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
+      bf16x8_t bfr[NJ];
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const int nt = wave + 4 * j;
-        if (nt < NTN) {
-          s16x4_t lo = ds_read_tr(xa_ + ks * xinc + boff[j]);
-          s16x4_t hi = ds_read_tr(xb_ + ks * xinc + boff[j]);
-          const bf16x8_t bfr = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-          for (int m = 0; m < MT; ++m) acc[j][m] = mfma16(af[m], bfr, acc[j][m]);
-        }
+        s16x4_t lo = ds_read_tr(xa_ + ks * xinc + boff[j]);
+        s16x4_t hi = ds_read_tr(xb_ + ks * xinc + boff[j]);
+        bfr[j] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[j][m] = mfma16(af[m], bfr[j], acc[j][m]);
     }
     if (it + 1 < nit) {
-      tile_store<CIN, MODE_X, 4>(xbuf[cur ^ 1], rx, tdx, nxs, nullptr, noy0 * S - P, a.Hi, a.Wi, coef_x);
-      tile_store<COUT, MODE_DY, 2>(dbuf[cur ^ 1], rd, tdd, nds, nds2, noy0, a.Ho, a.Wo, coef_d);
+      tile_store<CIN, MODE_X, 4>(XBUF(cur ^ 1), rx, tdx, nxs, nullptr, noy0 * S - P, a.Hi, a.Wi, coef_x);
+      tile_store<COUT, MODE_DY, 2>(DBUF(cur ^ 1), rd, tdd, nds, nds2, noy0, a.Ho, a.Wo, coef_d);
     }
     __syncthreads();
   }
@@ -778,6 +809,235 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
             const int co = m * 16 + 4 * (lane >> 4) + r;
             atomicAdd(gb + ((long)co * KK + tap) * a.cin_real + ci, acc[j][m][r]);
           }
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ fused backward
+// One launch = dgrad AND wgrad of a stride-1 3x3 C->C conv (all blocks of a stage
+// except the first), sharing the staged tiles: per (image, band) iteration the
+// workgroup stages
+//   dY tile  rows r0-1..r0+R, cols -1..W : T_dy(dy)   (plain residual grad, or BN2-backward(dz2, h))
+//   X  tile  same geometry               : relu(BN_x(x))  (the conv's forward input activation)
+// then computes the dgrad tiles (weights W^T in registers; epilogue: [+ res],
+// mask by BN_x(x) > 0, BN_x backward reductions, dz out) and the wgrad k-steps
+// (operands from the dY interior and the shifted X tile via ds_read_b64_tr_b16,
+// fp32 accumulators across all iterations, one atomic flush at the end).
+// Compared with separate dgrad + wgrad launches this reads dY, its BN partner and
+// x once instead of twice.
+
+template <int C, int MODE_DY, int EPI>
+__global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
+  constexpr int NT = C / 16;           // dgrad output-channel tiles
+  constexpr int WPT = 4 / NT;
+  constexpr int KTOT = 9 * C;
+  constexpr int KS = (KTOT + 31) / 32;
+  constexpr int MT = C / 16;           // wgrad co tiles
+  constexpr int NTN = 9 * C / 16;      // wgrad (tap, ci) tiles
+  constexpr int NJ = (NTN + 3) / 4;
+  constexpr int CP = cpad<C>();
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* coef_d = reinterpret_cast<float*>(smem);  // dy transform (192)
+  float* ecoef = coef_d + 192;                     // x BN: scale, shift, mean, inv (256)
+  float* acc_lds = ecoef + 256;                    // 128
+  bf16_t* t0 = reinterpret_cast<bf16_t*>(smem + 2304);
+
+  const int4 wk = a.work[blockIdx.x];
+  const int it0 = wk.x, nit = wk.y, slot = wk.w;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int H = a.Hi, W = a.Wi;
+  const float n_hw = a.cnt[slot] * (float)(H * W);
+  make_coef<C, MODE_DY>(coef_d, a, slot, n_hw, a.st_in, a.st_in_b, a.in_gamma, a.in_beta);
+  {
+    const int c = threadIdx.x;
+    if (c < C) {
+      const float* prow = a.params + (long)slot * a.p_mstride;
+      float scale, shift, mean, inv;
+      bn_fwd_coef(stats_row(a.st_ep, slot), n_hw, prow[a.ep_gamma + c], prow[a.ep_beta + c], c, scale, shift, mean,
+                  inv);
+      ecoef[c] = scale;
+      ecoef[64 + c] = shift;
+      ecoef[128 + c] = mean;
+      ecoef[192 + c] = inv;
+    }
+    if (threadIdx.x < 128) acc_lds[threadIdx.x] = 0.f;
+  }
+  const int ct = wave % NT;
+  bf16x8_t afr[KS];
+  {
+    const bf16_t* wb = a.w + (long)slot * a.w_mstride + a.w_off + (long)(ct * 16 + (lane & 15)) * KTOT;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int k0 = 32 * s + 8 * (lane >> 4);
+      bf16x8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (k0 < KTOT) v = *reinterpret_cast<const bf16x8_t*>(wb + k0);
+      afr[s] = v;
+    }
+  }
+  const int rows = a.rows;
+  const int bands = H / rows;
+  const int rows_t = rows + 2, wp = W + 2;
+  const int tsz = (rows_t * wp * CP + 63) & ~63;
+#define FDBUF(i) (t0 + ((i) & 1) * 2 * tsz)
+#define FXBUF(i) (t0 + tsz + ((i) & 1) * 2 * tsz)
+  const long img_elems = (long)H * W * C;
+  const int ntiles = rows * W / 16;
+  int tapoff[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k0 = 32 * s + 8 * (lane >> 4);
+    const int tap = k0 / C, c0 = k0 % C;
+    tapoff[s] = -((tap / 3) * wp + (tap % 3)) * CP + c0;
+  }
+  // wgrad lane constants (pixel rows 8g+q and +4 of each 32-pixel k-step)
+  const int g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
+  const int rstep = 32 / W;
+  const int pa = 8 * g + q, pb = pa + 4;
+  const int ya = pa / W, xa = pa % W, yb = pb / W, xb = pb % W;
+  const int da_off = ((ya + 1) * wp + xa + 1) * CP + 4 * p4, db_off = ((yb + 1) * wp + xb + 1) * CP + 4 * p4;
+  const int xa_off = (ya * wp + xa) * CP + 4 * p4, xb_off = (yb * wp + xb) * CP + 4 * p4;
+  const int kinc = rstep * wp * CP;
+  int boff[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int nt = min(wave + 4 * j, NTN - 1);  // duplicates (nt >= NTN) are computed, never flushed
+    const int tap = (nt * 16) / C, cb = (nt * 16) % C;
+    boff[j] = ((tap / 3) * wp + (tap % 3)) * CP + cb;
+  }
+  f32x4_t wacc[NJ][MT];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) wacc[j][m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  float ssum[4] = {0.f, 0.f, 0.f, 0.f}, ssq[4] = {0.f, 0.f, 0.f, 0.f};
+
+  TileDesc<C, 4> td;
+  tile_desc_init<C, 4>(td, rows_t, -1, wp, W);
+  TileRegs<C, MODE_DY, 4> rd;
+  TileRegs<C, 1, 4> rx;
+  __syncthreads();  // coefficients
+  {
+    const int img = it0 / bands, r0 = (it0 % bands) * rows;
+    const bf16_t* d2 = a.x2 ? a.x2 + img * img_elems : nullptr;
+    tile_load<C, MODE_DY, 4>(rd, td, a.x + img * img_elems, d2, r0 - 1, H, W);
+    tile_load<C, 1, 4>(rx, td, a.xm + img * img_elems, nullptr, r0 - 1, H, W);
+    tile_store<C, MODE_DY, 4>(FDBUF(0), rd, td, a.x + img * img_elems, d2, r0 - 1, H, W, coef_d);
+    tile_store<C, 1, 4>(FXBUF(0), rx, td, a.xm + img * img_elems, nullptr, r0 - 1, H, W, ecoef);
+  }
+  __syncthreads();
+  for (int k = 0; k < nit; ++k) {
+    const int it = it0 + k;
+    const int img = it / bands, r0 = (it % bands) * rows;
+    const bool more = k + 1 < nit;
+    const int nimg_ = (it + 1) / bands, nr0 = ((it + 1) % bands) * rows;
+    const bf16_t* nd2 = a.x2 ? a.x2 + nimg_ * img_elems : nullptr;
+    uint2 rres[MAXT], xres[MAXT];  // epilogue operands before the prefetch (counted vmcnt)
+#pragma unroll
+    for (int i = 0; i < MAXT; ++i) {
+      const int t = min(wave / NT + WPT * i, ntiles - 1);
+      const int p = t * 16 + (lane & 15);
+      const long o = (((long)img * H + r0 + p / W) * W + p % W) * C + ct * 16 + (lane >> 4) * 4;
+      if constexpr (EPI & 1) rres[i] = *reinterpret_cast<const uint2*>(a.res + o);
+      xres[i] = *reinterpret_cast<const uint2*>(a.xm + o);
+    }
+    if (more) {
+      tile_load<C, MODE_DY, 4>(rd, td, a.x + nimg_ * img_elems, nd2, nr0 - 1, H, W);
+      tile_load<C, 1, 4>(rx, td, a.xm + nimg_ * img_elems, nullptr, nr0 - 1, H, W);
+    }
+    const bf16_t* dcur = FDBUF(k);
+    const bf16_t* xcur = FXBUF(k);
+    // ---- dgrad
+#pragma unroll
+    for (int i = 0; i < MAXT; ++i) {
+      const int t = wave / NT + WPT * i;
+      if (t >= ntiles) break;
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+      const int p = t * 16 + (lane & 15);
+      const int iy = r0 + p / W, ix = p % W;
+      const int ci0 = ct * 16 + (lane >> 4) * 4;
+      const long o = (((long)img * H + iy) * W + ix) * C + ci0;
+      uint2 rr = make_uint2(0, 0);
+      if constexpr (EPI & 1) rr = rres[i];
+      const uint2 xr = xres[i];
+      const bf16_t* tb = dcur + ((iy - r0 + 2) * wp + ix + 2) * CP;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        bf16x8_t b = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (32 * s + 8 * (lane >> 4) < KTOT) b = *reinterpret_cast<const bf16x8_t*>(tb + tapoff[s]);
+        acc = mfma16(afr[s], b, acc);
+      }
+      float v[4] = {acc[0], acc[1], acc[2], acc[3]};
+      if constexpr (EPI & 1) {
+        v[0] += bf2f((bf16_t)(rr.x & 0xffff));
+        v[1] += bf2f((bf16_t)(rr.x >> 16));
+        v[2] += bf2f((bf16_t)(rr.y & 0xffff));
+        v[3] += bf2f((bf16_t)(rr.y >> 16));
+      }
+      const float xv[4] = {bf2f((bf16_t)(xr.x & 0xffff)), bf2f((bf16_t)(xr.x >> 16)), bf2f((bf16_t)(xr.y & 0xffff)),
+                           bf2f((bf16_t)(xr.y >> 16))};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = ci0 + r;
+        v[r] = (xv[r] * ecoef[c] + ecoef[64 + c] > 0.f) ? v[r] : 0.f;
+      }
+      uint2 pk;
+      pk.x = pack2bf(v[0], v[1]);
+      pk.y = pack2bf(v[2], v[3]);
+      *reinterpret_cast<uint2*>(a.y + o) = pk;
+      const float dz[4] = {bf2f((bf16_t)(pk.x & 0xffff)), bf2f((bf16_t)(pk.x >> 16)), bf2f((bf16_t)(pk.y & 0xffff)),
+                           bf2f((bf16_t)(pk.y >> 16))};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = ci0 + r;
+        ssum[r] += dz[r];
+        ssq[r] += dz[r] * (xv[r] - ecoef[128 + c]) * ecoef[192 + c];
+      }
+    }
+    // ---- wgrad
+    const int nk = rows * W / 32;
+    for (int ks = 0; ks < nk; ++ks) {
+      bf16x8_t af[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        s16x4_t lo = ds_read_tr(dcur + da_off + ks * kinc + m * 16);
+        s16x4_t hi = ds_read_tr(dcur + db_off + ks * kinc + m * 16);
+        af[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      bf16x8_t bfr[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        s16x4_t lo = ds_read_tr(xcur + xa_off + ks * kinc + boff[j]);
+        s16x4_t hi = ds_read_tr(xcur + xb_off + ks * kinc + boff[j]);
+        bfr[j] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) wacc[j][m] = mfma16(af[m], bfr[j], wacc[j][m]);
+    }
+    if (more) {
+      tile_store<C, MODE_DY, 4>(FDBUF(k + 1), rd, td, a.x + nimg_ * img_elems, nd2, nr0 - 1, H, W, coef_d);
+      tile_store<C, 1, 4>(FXBUF(k + 1), rx, td, a.xm + nimg_ * img_elems, nullptr, nr0 - 1, H, W, ecoef);
+    }
+    __syncthreads();
+  }
+  reduce_stats_to_lds(acc_lds, ssum, ssq, ct * 16 + (lane >> 4) * 4, lane);
+  __syncthreads();
+  flush_stats(a.st_out, acc_lds, slot, C);
+  float* gb = a.grads + (long)slot * a.g_mstride + a.g_off;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int nt = wave + 4 * j;
+    if (nt < NTN) {
+      const int tap = (nt * 16) / C, ci = (nt * 16) % C + (lane & 15);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = m * 16 + 4 * (lane >> 4) + r;
+          atomicAdd(gb + ((long)co * 9 + tap) * C + ci, wacc[j][m][r]);
         }
       }
     }
@@ -847,6 +1107,22 @@ DTF_API int dtf_conv_dgrad(const ConvArgs* args, int cin, int cout, int s, int k
   DGRAD_CASE(16, 16, 1, 1, 0, 0)
   DGRAD_CASE(16, 32, 2, 1, 0, 0)
   DGRAD_CASE(32, 64, 2, 1, 0, 0)
+  return -1;
+}
+
+#define FUSED_CASE(CC, M, E)                                                                          \
+  if (c == CC && mode_dy == M && epi == E)                                                           \
+    return launch(conv_bwd_fused_kernel<CC, M, E>, nblocks, lds, stream, *args);
+
+DTF_API int dtf_conv_bwd_fused(const ConvArgs* args, int c, int mode_dy, int epi, int nblocks, int lds,
+                               hipStream_t stream) {
+  FUSED_CASE(16, 0, 0)  // conv_b: dy = residual grad, x = h (BN2)
+  FUSED_CASE(32, 0, 0)
+  FUSED_CASE(64, 0, 0)
+  FUSED_CASE(16, 2, 0)  // conv_a: dy = BN2-backward(dz2, h), x = block input (BN1)
+  FUSED_CASE(32, 2, 0)
+  FUSED_CASE(64, 2, 0)
+  FUSED_CASE(16, 2, 1)  // conv_a of the first block (+ stride-1 projection dgrad)
   return -1;
 }
 

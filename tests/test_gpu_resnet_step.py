@@ -31,10 +31,11 @@ def _relerr(a, b):
     return float((a.double() - b.double()).norm() / (b.double().norm() + 1e-30))
 
 
-@pytest.mark.parametrize("size", [8, 14])
-@pytest.mark.parametrize("graph", ["1", "0"])
-def test_hip_step_matches_reference(size, graph, monkeypatch):
+@pytest.mark.parametrize("size,graph,fused", [(8, "1", "1"), (14, "1", "1"), (14, "0", "1"), (14, "1", "0"),
+                                              (8, "0", "0")])
+def test_hip_step_matches_reference(size, graph, fused, monkeypatch):
     monkeypatch.setenv("DTF_HIP_GRAPH", graph)
+    monkeypatch.setenv("DTF_FUSED_BWD", fused)
     torch.manual_seed(0)
     arch = ResNetArch(cifar_config(size))
     dev = torch.device("cuda")

@@ -68,22 +68,49 @@ def per_image_standardization(x: torch.Tensor) -> torch.Tensor:
     return ((flat - mean) / adj).reshape(x.shape)
 
 
-def augment_cifar(x_u8: torch.Tensor, gen: Optional[torch.Generator] = None) -> torch.Tensor:
-    """pad 4 -> random crop 32 -> random flip -> standardize. [B,32,32,3] uint8 -> float32."""
+def _mix32(h):
+    h = h.astype(np.uint32)
+    h ^= h >> np.uint32(16)
+    h = (h * np.uint32(0x7FEB352D)).astype(np.uint32)
+    h ^= h >> np.uint32(15)
+    h = (h * np.uint32(0x846CA68B)).astype(np.uint32)
+    h ^= h >> np.uint32(16)
+    return h
+
+
+def augment_params(seed: int, counter: int, n: int):
+    """Crop offsets / flip bits drawn by the HIP augmentation kernel (data.hip) for batch positions 0..n-1."""
+    with np.errstate(over="ignore"):
+        pos = np.arange(n, dtype=np.uint32)
+        inner = _mix32((np.uint32(counter & 0xFFFFFFFF) * np.uint32(0x9E3779B9)).astype(np.uint32) + pos)
+        h = _mix32(np.uint32(seed & 0xFFFFFFFF) ^ inner)
+    return (h % 9).astype(np.int64), ((h >> 8) % 9).astype(np.int64), ((h >> 16) & 1).astype(bool)
+
+
+def augment_cifar_with(x_u8: torch.Tensor, oy, ox, flip) -> torch.Tensor:
+    """pad 4 -> crop at (oy, ox) -> optional horizontal flip -> standardize (cifar10_main.py:98-108)."""
     b = x_u8.shape[0]
     dev = x_u8.device
+    oy, ox, flip = (torch.as_tensor(t, device=dev) for t in (oy, ox, flip))
     x = x_u8.float()
     xp = torch.nn.functional.pad(x.permute(0, 3, 1, 2), (4, 4, 4, 4)).permute(0, 2, 3, 1)
-    oy = torch.randint(0, 9, (b,), device=dev, generator=gen)
-    ox = torch.randint(0, 9, (b,), device=dev, generator=gen)
     ar = torch.arange(32, device=dev)
     rows = (oy[:, None] + ar[None, :])  # [B, 32]
     cols = (ox[:, None] + ar[None, :])
-    flip = torch.rand(b, device=dev, generator=gen) < 0.5
     cols = torch.where(flip[:, None], cols.flip(1), cols)
     bi = torch.arange(b, device=dev)[:, None, None]
     out = xp[bi, rows[:, :, None], cols[:, None, :]]
     return per_image_standardization(out)
+
+
+def augment_cifar(x_u8: torch.Tensor, gen: Optional[torch.Generator] = None) -> torch.Tensor:
+    """pad 4 -> random crop 32 -> random flip -> standardize. [B,32,32,3] uint8 -> float32 (torch ops)."""
+    b = x_u8.shape[0]
+    dev = x_u8.device
+    oy = torch.randint(0, 9, (b,), device=dev, generator=gen)
+    ox = torch.randint(0, 9, (b,), device=dev, generator=gen)
+    flip = torch.rand(b, device=dev, generator=gen) < 0.5
+    return augment_cifar_with(x_u8, oy, ox, flip)
 
 
 def eval_cifar(x_u8: torch.Tensor) -> torch.Tensor:
@@ -117,24 +144,68 @@ def load_mnist(data_dir: str, normalize: bool = False):
     return trx, tr_y, tex, te_y
 
 
-class DeviceDataset:
-    """Train/eval arrays resident on the device with per-member epoch shuffling."""
+class IndexBatch:
+    """A training batch named by dataset rows, materialised lazily.
 
-    def __init__(self, train_x, train_y, test_x, test_y, device, augment=None, eval_transform=None):
-        self.train_x = torch.as_tensor(train_x).to(device)
-        self.train_y = torch.as_tensor(train_y).to(device)
-        self.test_x = torch.as_tensor(test_x).to(device)
-        self.test_y = torch.as_tensor(test_y).to(device)
+    Engines with an on-device input path (the HIP ResNet step) consume the
+    indices directly -- gather, augmentation and the bf16 stem packing run in
+    one kernel inside the captured step graph; every other engine calls
+    :meth:`materialize`.
+    """
+
+    def __init__(self, ds: "DeviceDataset", idx: torch.Tensor):
+        self.ds, self.idx = ds, idx
+
+    def __len__(self):
+        return int(self.idx.numel())
+
+    def materialize(self, gen=None):
+        return self.ds.batch(self.idx, gen)
+
+
+def batch_len(b) -> int:
+    return len(b) if isinstance(b, IndexBatch) else int(b[1].shape[0])
+
+
+class DeviceDataset:
+    """Train/eval arrays resident on the device with per-member epoch shuffling.
+
+    CIFAR-style uint8 32x32x3 data with ``augment=augment_cifar`` on a GPU uses
+    the fused HIP kernel (data.hip) for gather + pad/crop/flip + standardize.
+    """
+
+    def __init__(self, train_x, train_y, test_x, test_y, device, augment=None, eval_transform=None, seed=0):
+        self.train_x = torch.as_tensor(train_x).to(device).contiguous()
+        self.train_y = torch.as_tensor(train_y).to(device).long().contiguous()
+        self.test_x = torch.as_tensor(test_x).to(device).contiguous()
+        self.test_y = torch.as_tensor(test_y).to(device).long().contiguous()
         self.augment = augment
         self.eval_transform = eval_transform
         self._eval_cache = None
-        self.device = device
+        self.device = torch.device(device)
+        self.hip_augment = (self.device.type == "cuda" and augment is augment_cifar
+                            and self.train_x.dtype == torch.uint8 and tuple(self.train_x.shape[1:]) == (32, 32, 3))
+        self.rng_seed = int(seed) & 0x7FFFFFFF
+        self.rng_counter = 0
 
     @property
     def num_train(self):
         return int(self.train_x.shape[0])
 
+    def next_rng(self):
+        """(seed, counter) for one augmentation launch; the counter advances per launch."""
+        self.rng_counter = (self.rng_counter + 1) & 0x7FFFFFFF
+        return self.rng_seed, self.rng_counter
+
     def batch(self, idx: torch.Tensor, gen=None):
+        if self.hip_augment:
+            from .. import ops
+            n = int(idx.numel())
+            x = torch.empty(n, 32, 32, 3, dtype=torch.float32, device=self.device)
+            y = torch.empty(n, dtype=torch.int64, device=self.device)
+            rng = torch.tensor(self.next_rng(), dtype=torch.int32).to(self.device)
+            ops.augment_cifar(self.train_x, self.train_y, idx.long().contiguous(), rng, True, out32=x, lab64=y)
+            return x, y
         x = self.train_x[idx]
         x = self.augment(x, gen) if self.augment is not None else x.float()
         return x, self.train_y[idx]

@@ -33,6 +33,7 @@ from typing import Dict, List, Sequence, Tuple
 import torch
 
 from .. import ops
+from ..data.datasets import IndexBatch, batch_len
 from ..models.resnet import BN_EPS
 
 NREP = 8
@@ -204,20 +205,28 @@ class HipResNetBackend:
         return self.stats[1, bn]
 
     # --- plans ------------------------------------------------------------------------
-    def plan(self, slots: Sequence[int], sizes: Sequence[int]) -> "_StepPlan":
-        key = (tuple(slots), tuple(sizes))
+    accepts_index_batches = True
+
+    def plan(self, slots: Sequence[int], sizes: Sequence[int], src=None) -> "_StepPlan":
+        key = (tuple(slots), tuple(sizes), id(src) if src is not None else None)
         p = self._plans.get(key)
         if p is None:
             if len(self._plans) > 16:
                 self._plans.clear()
-            p = _StepPlan(self, list(slots), list(sizes))
+            p = _StepPlan(self, list(slots), list(sizes), src)
             self._plans[key] = p
         return p
 
     def train_step(self, slots, batches, hparams, lrs):
         e = self.e
-        sizes = [int(b[1].shape[0]) for b in batches]
-        p = self.plan(slots, sizes)
+        src = None
+        if all(isinstance(b, IndexBatch) for b in batches) and batches and all(b.ds is batches[0].ds
+                                                                               for b in batches):
+            src = batches[0].ds  # on-device gather + augmentation inside the step graph
+        else:
+            batches = [b.materialize() if isinstance(b, IndexBatch) else b for b in batches]
+        sizes = [batch_len(b) for b in batches]
+        p = self.plan(slots, sizes, src)
         hy = torch.zeros(e.capacity, 8, dtype=torch.float32)
         from .optim import hyper_row
         for s, hp, lr in zip(slots, hparams, lrs):
@@ -240,7 +249,7 @@ class HipResNetBackend:
 class _StepPlan:
     """Buffers + prebuilt launch list for one batch composition (slots, per-member sizes)."""
 
-    def __init__(self, be: HipResNetBackend, slots: List[int], sizes: List[int]):
+    def __init__(self, be: HipResNetBackend, slots: List[int], sizes: List[int], src=None):
         self.be = be
         e = be.e
         self.e = e
@@ -268,6 +277,10 @@ class _StepPlan:
         self.x_in = torch.zeros(N, H, H, 3, dtype=torch.float32, device=dev)
         self.labels = torch.zeros(N, dtype=torch.int32, device=dev)
         self.xin16 = torch.zeros(N, H, H, 16, dtype=torch.bfloat16, device=dev)
+        self.src = src
+        if src is not None:
+            self.idx = torch.zeros(N, dtype=torch.long, device=dev)
+            self.rng = torch.zeros(2, dtype=torch.int32, device=dev)
         # forward activations saved for backward
         self.xs, self.hs, self.scs = [], [], []
         hw, c = H, cfg.num_filters
@@ -528,7 +541,10 @@ class _StepPlan:
         self._add("zero", be.stats)
         self._add("zero", be.loss)
         self._add("zero", be.correct)
-        self._add(lib.dtf_prep_input, _p(self.x_in), _p(self.xin16), N * cfg.image_size * cfg.image_size, 3)
+        if self.src is not None:
+            self._add("augment", None)  # gather + pad/crop/flip + standardize + bf16 pack (data.hip)
+        else:
+            self._add(lib.dtf_prep_input, _p(self.x_in), _p(self.xin16), N * cfg.image_size * cfg.image_size, 3)
         # ---------------- forward
         first_bn = prog.blocks[0].bns[0]
         self._conv_fwd(prog.stem, self.xin16, self.xs[0], stats_bn=first_bn, in_bn=None)
@@ -618,6 +634,13 @@ class _StepPlan:
     # -------------------------------------------------------------------- execution
     def load_batch(self, batches):
         off = 0
+        if self.src is not None:
+            for b in batches:
+                n = len(b)
+                self.idx[off:off + n].copy_(b.idx, non_blocking=True)
+                off += n
+            self.rng.copy_(torch.tensor(self.src.next_rng(), dtype=torch.int32), non_blocking=True)
+            return
         for (x, y) in batches:
             n = x.shape[0]
             self.x_in[off:off + n].copy_(x.reshape(n, *self.x_in.shape[1:]), non_blocking=True)
@@ -630,6 +653,9 @@ class _StepPlan:
         for fn, args in self.launches:
             if fn == "zero":
                 args[0].zero_()
+            elif fn == "augment":
+                ops.augment_cifar(self.src.train_x, self.src.train_y, self.idx, self.rng, True, out16=self.xin16,
+                                  lab32=self.labels)
             elif fn == "optim":
                 ops.fused_optimizer(e.state, e.grads, e.hyper, e.Pp, e.P, e.n_reg, shadow=None, zero_grads=True)
             elif fn == "step":

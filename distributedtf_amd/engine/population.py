@@ -32,6 +32,7 @@ import torch
 import torch.nn.functional as F
 
 from . import optim as _optim
+from ..data.datasets import IndexBatch
 
 
 def _align(n: int, a: int = 64) -> int:
@@ -125,6 +126,8 @@ class PopulationEngine:
                    hparams: Sequence[Dict], lrs: Sequence[float]) -> torch.Tensor:
         """One optimizer step for ``slots`` (each with its own batch). Returns
         per-member cross-entropy losses (device tensor)."""
+        if not getattr(self.backend, "accepts_index_batches", False):
+            batches = [b.materialize() if isinstance(b, IndexBatch) else b for b in batches]
         if hasattr(self.backend, "train_step"):
             # whole step (fwd, bwd, optimizer, step counters) inside one HIP graph
             losses = self.backend.train_step(slots, batches, hparams, lrs)

@@ -20,6 +20,7 @@ import torch
 import torch.nn.functional as F
 
 from .model_base import ModelBase
+from ..data import datasets
 from ..engine.population import PopulationEngine
 
 
@@ -136,6 +137,8 @@ class EngineModel(ModelBase):
             self._perm_pos = 0
         idx = self._perm[self._perm_pos:self._perm_pos + b]
         self._perm_pos += b
+        if getattr(ds, "hip_augment", False):
+            return datasets.IndexBatch(ds, idx)
         return ds.batch(idx, gen)
 
     def n_steps(self, num_epoch: int) -> int:
@@ -170,7 +173,7 @@ class EngineModel(ModelBase):
                 lrs = [by_slot[s].learning_rate(eng.host_step[s]) for s in active]
                 losses = eng.train_step(active, batches, hps, lrs)
                 for i, s in enumerate(active):
-                    by_slot[s].images_trained += int(batches[i][1].shape[0])
+                    by_slot[s].images_trained += datasets.batch_len(batches[i])
                 for i, s in enumerate(active):
                     loss_acc[s] = losses[i]  # view, no host sync
                 done += 1

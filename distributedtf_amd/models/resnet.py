@@ -294,6 +294,88 @@ def _bn(prog, params, running, x, i, training, update_running=True):
     return y.to(x.dtype)
 
 
+def block_forward(prog: ResNetProgram, params: torch.Tensor, running: torch.Tensor, x: torch.Tensor,
+                  blk: BlockSpec, training: bool = True, dtype=torch.float32, update_running: bool = True):
+    """One residual block on NCHW ``x`` (reference resnet_model.py:127-320).
+
+    v2 (pre-activation, ``_building_block_v2`` / ``_bottleneck_block_v2``): BN+ReLU
+    before every conv; the projection shortcut reads the pre-activated input.
+    v1 (``_building_block_v1`` / ``_bottleneck_block_v1``): conv -> BN (-> ReLU),
+    projection conv -> BN, ReLU after the residual add.
+    """
+    bn = lambda t, i: _bn(prog, params, running, t, i, training, update_running)  # noqa: E731
+    if prog.cfg.version == 2:
+        shortcut = x
+        pre = F.relu(bn(x, blk.bns[0]))
+        if blk.proj is not None:
+            shortcut = _conv(prog, params, pre, blk.proj, dtype)
+        h = _conv(prog, params, pre, blk.convs[0], dtype)
+        for j in range(1, len(blk.convs)):
+            h = F.relu(bn(h, blk.bns[j]))
+            h = _conv(prog, params, h, blk.convs[j], dtype)
+        return h + shortcut
+    shortcut = x
+    if blk.proj is not None:
+        shortcut = bn(_conv(prog, params, x, blk.proj, dtype), blk.proj_bn)
+    h = x
+    n = len(blk.convs)
+    for j in range(n):
+        h = bn(_conv(prog, params, h, blk.convs[j], dtype), blk.bns[j])
+        if j < n - 1:
+            h = F.relu(h)
+    return F.relu(h + shortcut)
+
+
+def single_block_program(cin: int, filters: int, stride: int, projection: bool, version: int,
+                         bottleneck: bool) -> Tuple[ResNetProgram, BlockSpec]:
+    """A one-block program (flat parameter layout of build_program) for block-level tests."""
+    cfg = ResNetConfig(resnet_size=0, version=version, bottleneck=bottleneck, num_classes=1, num_filters=filters,
+                       kernel_size=3, conv_stride=1, first_pool_size=0, first_pool_stride=0, block_sizes=[1],
+                       block_strides=[stride], final_size=(4 * filters if bottleneck else filters), image_size=0,
+                       in_channels=cin)
+    prog = ResNetProgram(cfg)
+    fout = cfg.final_size
+    blk = BlockSpec(stride=stride, convs=[], bns=[])
+
+    def conv(ci, co, k, s):
+        prog.convs.append(ConvSpec(len(prog.convs), ci, co, k, s))
+        return len(prog.convs) - 1
+
+    def bn(c):
+        prog.bns.append(BNSpec(len(prog.bns), c))
+        return len(prog.bns) - 1
+
+    if projection:
+        blk.proj = conv(cin, fout, 1, stride)
+        if version == 1:
+            blk.proj_bn = bn(fout)
+    shapes = ([(cin, filters, 1, 1), (filters, filters, 3, stride), (filters, fout, 1, 1)] if bottleneck
+              else [(cin, filters, 3, stride), (filters, filters, 3, 1)])
+    for (ci, co, k, st) in shapes:
+        if version == 2:
+            blk.bns.append(bn(ci))
+        blk.convs.append(conv(ci, co, k, st))
+        if version == 1:
+            blk.bns.append(bn(co))
+    prog.blocks.append(blk)
+    off = 0
+    for c in prog.convs:
+        c.off = off
+        off += c.numel
+    prog.n_reg = off
+    for b in prog.bns:
+        b.gamma_off, b.beta_off = off, off + b.c
+        off += 2 * b.c
+    prog.dense_w_off = prog.dense_b_off = off
+    prog.n_params = off
+    roff = 0
+    for b in prog.bns:
+        b.run_off = roff
+        roff += 2 * b.c
+    prog.n_running = roff
+    return prog, blk
+
+
 def forward_reference(prog: ResNetProgram, params: torch.Tensor, running: torch.Tensor, x_nhwc: torch.Tensor,
                       training: bool = True, dtype=torch.float32, update_running: bool = True) -> torch.Tensor:
     """Plain-PyTorch forward. ``x_nhwc`` [B, H, W, C]; returns fp32 logits [B, classes]."""
@@ -312,27 +394,7 @@ def forward_reference(prog: ResNetProgram, params: torch.Tensor, running: torch.
         x = F.pad(x, (pad // 2, pad - pad // 2, pad // 2, pad - pad // 2), value=float("-inf"))
         x = F.max_pool2d(x, k, s)
     for blk in prog.blocks:
-        if cfg.version == 2:
-            shortcut = x
-            pre = F.relu(bn(x, blk.bns[0]))
-            if blk.proj is not None:
-                shortcut = _conv(prog, params, pre, blk.proj, dtype)
-            h = _conv(prog, params, pre, blk.convs[0], dtype)
-            for j in range(1, len(blk.convs)):
-                h = F.relu(bn(h, blk.bns[j]))
-                h = _conv(prog, params, h, blk.convs[j], dtype)
-            x = h + shortcut
-        else:
-            shortcut = x
-            if blk.proj is not None:
-                shortcut = bn(_conv(prog, params, x, blk.proj, dtype), blk.proj_bn)
-            h = x
-            n = len(blk.convs)
-            for j in range(n):
-                h = bn(_conv(prog, params, h, blk.convs[j], dtype), blk.bns[j])
-                if j < n - 1:
-                    h = F.relu(h)
-            x = F.relu(h + shortcut)
+        x = block_forward(prog, params, running, x, blk, training, dtype, update_running)
     if cfg.version == 2:
         x = F.relu(bn(x, prog.final_bn))
     feat = x.float().mean(dim=(2, 3))

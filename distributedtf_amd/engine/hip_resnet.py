@@ -84,6 +84,7 @@ def _register():
                                   c_void_p])
     ops.register("dtf_conv_dgrad", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_wgrad", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
+    ops.register("dtf_conv_fwd_s1", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_bwd_fused", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_args_size", [])
     ops.register("dtf_bnbwd_args_size", [])
@@ -407,8 +408,13 @@ class _StepPlan:
         lds = 1280 + 2 * tsz * 2
         mode = 0 if in_bn is None else 1
         lib = ops.lib()
-        self._add(lib.dtf_conv_fwd, ctypes.byref(a), cin, c.cout, c.stride, c.k, mode, int(res is not None),
-                  int(stats_bn is not None), work.shape[0], lds)
+        if (c.k == 3 and c.stride == 1 and cin == c.cout and Hi == 512 // cin and rows == 8
+                and stats_bn is not None and os.environ.get("DTF_FWD_S1", "1") == "1"):
+            # compile-time-geometry kernel of the CIFAR stages (conv_fwd_s1_kernel)
+            self._add(lib.dtf_conv_fwd_s1, ctypes.byref(a), cin, mode, int(res is not None), work.shape[0], lds)
+        else:
+            self._add(lib.dtf_conv_fwd, ctypes.byref(a), cin, c.cout, c.stride, c.k, mode, int(res is not None),
+                      int(stats_bn is not None), work.shape[0], lds)
         self._keep(a)
 
     def _conv_dgrad(self, ci, dy, y, Hi, mode, epi, dy2=None, in_bn=None, res=None, xm=None, ep_bn=None):
@@ -500,10 +506,14 @@ class _StepPlan:
             if H % r == 0 and (r * H) % 32 == 0 and (r + 2) * (H + 2) * (C // 8) <= 4 * 256:
                 rows = r
                 break
-        assert rows is not None
+        # the fused kernel's geometry is compile-time: W = H = 512 / C, 8-row bands
+        assert rows == 8 and H == 512 // C and x.shape[2] == H, (C, H, rows)
         bands = H // rows
         wn = 9 * C * C
-        n_wg = max(64, min(128 * len(self.slots), int(16e6 / (4.0 * wn))))
+        # dW atomic traffic budget per launch (bytes): bounds the workgroup count; 64 channels trade more atomics
+        # for filling more CUs (measured: 16/32 ch best at 16 MB, 64 ch at 32 MB)
+        budget = float(os.environ.get("DTF_FUSED_ATOMIC_BYTES_%d" % C, {64: 32e6}.get(C, 16e6)))
+        n_wg = max(64, min(128 * len(self.slots), int(budget / (4.0 * wn))))
         n_wg = min(n_wg, self.N * bands)
         work = self._work_iters(bands, n_wg)
         a = self._base_args()

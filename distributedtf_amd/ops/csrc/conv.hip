@@ -343,6 +343,101 @@ __device__ __forceinline__ void flush_stats(float* st_out, const float* acc_lds,
   }
 }
 
+// Packed-math helpers (v_pk_fma_f32 / v_cvt_pk_bf16_f32 / v_pk_max_i16): two channels per VALU op.
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v_t __attribute__((ext_vector_type(2)));
+typedef short s16x2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2_t unpk2(uint32_t w) {
+  return (f32x2_t){__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+}
+__device__ __forceinline__ uint32_t pk2(f32x2_t v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v_t));
+}
+// ReLU on two packed bf16: as int16, every negative bf16 (sign bit set) is < 0
+__device__ __forceinline__ uint32_t relu_pk2(uint32_t w) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2_t, w), (s16x2_t){0, 0}));
+}
+__device__ __forceinline__ f32x2_t lds2(const float* p) { return *reinterpret_cast<const f32x2_t*>(p); }
+
+// T(8 channels c0..c0+7): MODE 1 relu(x*coef[c] + coef[64+c]); MODE 2 coef[c]*x + coef[64+c]*h + coef[128+c]
+template <int MODE>
+__device__ __forceinline__ uint4 xform8(uint4 v, uint4 v2, int c0, const float* __restrict__ coef) {
+  if constexpr (MODE == 0) return v;
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  const uint32_t h[4] = {v2.x, v2.y, v2.z, v2.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = c0 + 2 * j;
+    const f32x2_t x = unpk2(w[j]);
+    if constexpr (MODE == 1) {
+      w[j] = relu_pk2(pk2(x * lds2(coef + c) + lds2(coef + 64 + c)));
+    } else {
+      w[j] = pk2(x * lds2(coef + c) + unpk2(h[j]) * lds2(coef + 64 + c) + lds2(coef + 128 + c));
+    }
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// Compile-time tile geometry for a [RT][WP][C] (+8 pad per pixel) LDS tile of rows gy0..gy0+RT-1 and columns
+// -1..W of an H x W x C image.  Each thread owns MAXC 16-byte chunk slots (always the same 8 channels, since
+// 256 % (C/8) == 0); per slot: LDS offset, in-band global offset, and three bit masks (column/slot valid,
+// top halo row, bottom halo row) so an iteration only adds its band's row offset.  Inactive slots stage zeros
+// into pixel 0's pad lanes (never read), keeping load/store branch-free.
+template <int C, int RT, int W, int H>
+struct Stage {
+  static constexpr int WP = W + 2, CP = C + 8, NCH = C / 8, ROW = W * C;
+  static constexpr int TOTAL = RT * WP * NCH, MAXC = (TOTAL + 255) / 256;
+  int loff[MAXC];
+  int goff[MAXC];
+  unsigned okm, top, bot;
+  int c0;
+  __device__ __forceinline__ void init() {
+    c0 = (threadIdx.x % NCH) * 8;
+    okm = top = bot = 0;
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      const int idx = threadIdx.x + 256 * j;
+      const int pc = idx / NCH, col = pc % WP, r = pc / WP;
+      const bool act = idx < TOTAL;
+      loff[j] = act ? (r * WP + col) * CP + c0 : C;
+      goff[j] = (r * ROW + (col - 1) * C + c0) * 2;  // bytes
+      if (act && col >= 1 && col <= W) okm |= 1u << j;
+      if (r == 0) top |= 1u << j;
+      if (r == RT - 1) bot |= 1u << j;
+    }
+  }
+  // first tile row = gy0; rows outside [0, H) are zero
+  __device__ __forceinline__ unsigned mask(int gy0) const {
+    unsigned m = okm;
+    if (gy0 < 0) m &= ~top;
+    if (gy0 + RT > H) m &= ~bot;
+    return m;
+  }
+  template <int MODE>
+  __device__ __forceinline__ void load(uint4 (&v)[MAXC], uint4 (&v2)[MAXC], unsigned m, const bf16_t* img,
+                                       const bf16_t* img2, int gy0) const {
+    // byte offsets in 32 bits: uniform base (SGPR) + lane offset -> saddr global loads
+    const int rb = gy0 * ROW * 2;
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      const uint32_t off = ((m >> j) & 1u) ? (uint32_t)(rb + goff[j]) : 0u;
+      v[j] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(img) + off);
+      if constexpr (MODE == 2) v2[j] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(img2) + off);
+    }
+  }
+  template <int MODE>
+  __device__ __forceinline__ void store(bf16_t* buf, const uint4 (&v)[MAXC], const uint4 (&v2)[MAXC], unsigned m,
+                                        const float* coef) const {
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      uint4 t = make_uint4(0, 0, 0, 0);
+      if ((m >> j) & 1u) t = xform8<MODE>(v[j], v2[j], c0, coef);
+      *reinterpret_cast<uint4*>(buf + loff[j]) = t;
+    }
+  }
+};
+
 // --------------------------------------------------------------------------------- forward
 
 // Work items are (it0, nit, -, slot): the workgroup processes iterations
@@ -478,6 +573,122 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
     __syncthreads();
     flush_stats(a.st_out, acc_lds, slot, COUT);
   }
+}
+
+// Stride-1 3x3 C->C forward of the CIFAR stages (and the stem, C = 16 padded input) with compile-time
+// geometry (W = H = 512/C, 8-row bands), uniform-base + 32-bit lane offsets and packed epilogue math
+// (same scheme as conv_bwd_fused_kernel).
+template <int C, int MODE_IN, bool RESID>
+__global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
+  constexpr int W = 512 / C, H = W, ROWS = 8, BANDS = H / ROWS;
+  constexpr int NT = C / 16, WPT = 4 / NT;
+  constexpr int KTOT = 9 * C, KS = (KTOT + 31) / 32;
+  constexpr int CP = cpad<C>(), RT = ROWS + 2, WP = W + 2;
+  constexpr int TSZ = (RT * WP * CP + 63) & ~63;
+  constexpr int NTILES = ROWS * W / 16;
+  static_assert(NTILES == WPT * MAXT, "every wave owns MAXT output tiles");
+  constexpr int ROW = W * C, IMG = H * ROW;
+  using St = Stage<C, RT, W, H>;
+  constexpr int MAXC = St::MAXC;
+  constexpr int LMODE = MODE_IN == 0 ? 0 : 1;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* coef = reinterpret_cast<float*>(smem);  // 192 floats
+  float* acc_lds = coef + 192;                   // 128 floats
+  bf16_t* tile0 = reinterpret_cast<bf16_t*>(smem + 1280);
+#define SBUF(i) (tile0 + ((i) & 1) * TSZ)
+
+  const int4 wk = a.work[blockIdx.x];
+  const int it0 = wk.x, nit = wk.y, slot = wk.w;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int ct = wave % NT;
+  bf16x8_t afr[KS];
+  {
+    const bf16_t* wb = a.w + (long)slot * a.w_mstride + a.w_off + (long)(ct * 16 + (lane & 15)) * KTOT;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int k0 = 32 * s + 8 * (lane >> 4);
+      bf16x8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (k0 < KTOT) v = *reinterpret_cast<const bf16x8_t*>(wb + k0);
+      afr[s] = v;
+    }
+  }
+  St st;
+  st.init();
+  uint4 tv[MAXC], unused[MAXC];
+  unsigned tm;
+  {
+    const int img = it0 / BANDS, gy0 = (it0 % BANDS) * ROWS - 1;
+    tm = st.mask(gy0);
+    st.template load<LMODE>(tv, unused, tm, a.x + img * IMG, nullptr, gy0);
+  }
+  make_coef<C, MODE_IN>(coef, a, slot, a.cnt[slot] * (float)(H * W), a.st_in, a.st_in_b, a.in_gamma, a.in_beta);
+  if (threadIdx.x < 128) acc_lds[threadIdx.x] = 0.f;
+  int tapoff[KS];  // k-chunks past KTOT have zero weights and read a valid in-tile address
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k0 = 32 * s + 8 * (lane >> 4);
+    const int tap = k0 / C, c0 = k0 % C;
+    tapoff[s] = k0 < KTOT ? ((tap / 3) * WP + (tap % 3)) * CP + c0 : 0;
+  }
+  const int co0 = ct * 16 + (lane >> 4) * 4;
+  int tbo[MAXT];
+  uint32_t pofs[MAXT];
+#pragma unroll
+  for (int i = 0; i < MAXT; ++i) {
+    const int p = (wave / NT + WPT * i) * 16 + (lane & 15);
+    tbo[i] = ((p / W) * WP + p % W) * CP;
+    pofs[i] = p * C + co0;
+  }
+  f32x2_t ssum[2] = {{0.f, 0.f}, {0.f, 0.f}}, ssq[2] = {{0.f, 0.f}, {0.f, 0.f}};
+  __syncthreads();  // coefficients
+  st.template store<LMODE>(SBUF(0), tv, unused, tm, coef);
+  __syncthreads();
+  for (int k = 0; k < nit; ++k) {
+    const int it = it0 + k;
+    const int img = it / BANDS, r0 = (it % BANDS) * ROWS;
+    const bool more = k + 1 < nit;
+    const long band = (long)img * IMG + r0 * ROW;
+    uint2 rres[MAXT];
+    if constexpr (RESID) {
+#pragma unroll
+      for (int i = 0; i < MAXT; ++i) rres[i] = *reinterpret_cast<const uint2*>(a.res + band + pofs[i]);
+    }
+    if (more) {
+      const int nimg = (it + 1) / BANDS, ngy0 = ((it + 1) % BANDS) * ROWS - 1;
+      tm = st.mask(ngy0);
+      st.template load<LMODE>(tv, unused, tm, a.x + nimg * IMG, nullptr, ngy0);
+    }
+    const bf16_t* tile = SBUF(k);
+#pragma unroll
+    for (int i = 0; i < MAXT; ++i) {
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        acc = mfma16(afr[s], *reinterpret_cast<const bf16x8_t*>(tile + tbo[i] + tapoff[s]), acc);
+      f32x2_t v0 = {acc[0], acc[1]}, v1 = {acc[2], acc[3]};
+      if constexpr (RESID) {
+        v0 += unpk2(rres[i].x);
+        v1 += unpk2(rres[i].y);
+      }
+      uint2 pk;
+      pk.x = pk2(v0);
+      pk.y = pk2(v1);
+      *reinterpret_cast<uint2*>(a.y + band + pofs[i]) = pk;
+      const f32x2_t r0v = unpk2(pk.x), r1v = unpk2(pk.y);
+      ssum[0] += r0v;
+      ssum[1] += r1v;
+      ssq[0] += r0v * r0v;
+      ssq[1] += r1v * r1v;
+    }
+    if (more) st.template store<LMODE>(SBUF(k + 1), tv, unused, tm, coef);
+    __syncthreads();
+  }
+#undef SBUF
+  const float s4[4] = {ssum[0].x, ssum[0].y, ssum[1].x, ssum[1].y};
+  const float q4[4] = {ssq[0].x, ssq[0].y, ssq[1].x, ssq[1].y};
+  reduce_stats_to_lds(acc_lds, s4, q4, co0, lane);
+  __syncthreads();
+  flush_stats(a.st_out, acc_lds, slot, C);
 }
 
 // ---------------------------------------------------------------------------------- dgrad
@@ -816,20 +1027,22 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
 }
 
 // ------------------------------------------------------------------ fused backward
-// One launch = dgrad AND wgrad of a stride-1 3x3 C->C conv (all blocks of a stage
-// except the first), sharing the staged tiles: per (image, band) iteration the
-// workgroup stages
-//   dY tile  rows r0-1..r0+R, cols -1..W : T_dy(dy)   (plain residual grad, or BN2-backward(dz2, h))
+// One launch = dgrad AND wgrad of a stride-1 3x3 C->C conv of the CIFAR stages
+// (C = 16/32/64 at W = H = 512/C; 8-row bands), sharing the staged tiles: per
+// (image, band) iteration the workgroup stages
+//   dY tile  rows r0-1..r0+8, cols -1..W : T_dy(dy)   (plain residual grad, or BN2-backward(dz2, h))
 //   X  tile  same geometry               : relu(BN_x(x))  (the conv's forward input activation)
 // then computes the dgrad tiles (weights W^T in registers; epilogue: [+ res],
 // mask by BN_x(x) > 0, BN_x backward reductions, dz out) and the wgrad k-steps
 // (operands from the dY interior and the shifted X tile via ds_read_b64_tr_b16,
 // fp32 accumulators across all iterations, one atomic flush at the end).
-// Compared with separate dgrad + wgrad launches this reads dY, its BN partner and
-// x once instead of twice.
-
+// All geometry is compile-time, every global address is a wave-uniform base plus
+// a 32-bit lane offset fixed for the workgroup, and the elementwise work uses
+// packed fp32 / bf16 math: the VALU budget per MFMA is what bounds these
+// small-channel layers.
 template <int C, int MODE_DY, int EPI>
 __global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
+  constexpr int W = 512 / C, H = W, ROWS = 8, BANDS = H / ROWS;
   constexpr int NT = C / 16;           // dgrad output-channel tiles
   constexpr int WPT = 4 / NT;
   constexpr int KTOT = 9 * C;
@@ -837,33 +1050,25 @@ __global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
   constexpr int MT = C / 16;           // wgrad co tiles
   constexpr int NTN = 9 * C / 16;      // wgrad (tap, ci) tiles
   constexpr int NJ = (NTN + 3) / 4;
-  constexpr int CP = cpad<C>();
+  constexpr int CP = cpad<C>(), RT = ROWS + 2, WP = W + 2;
+  constexpr int TSZ = (RT * WP * CP + 63) & ~63;
+  constexpr int NTILES = ROWS * W / 16;
+  static_assert(NTILES == WPT * MAXT, "every wave owns MAXT dgrad tiles");
+  constexpr int ROW = W * C, IMG = H * ROW;
+  constexpr int NK = ROWS * W / 32, RSTEP = 32 / W, KINC = RSTEP * WP * CP;
+  using St = Stage<C, RT, W, H>;
+  constexpr int MAXC = St::MAXC;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* coef_d = reinterpret_cast<float*>(smem);  // dy transform (192)
-  float* ecoef = coef_d + 192;                     // x BN: scale, shift, mean, inv (256)
+  float* ecoef = coef_d + 192;                     // x BN: scale, shift, -mean*inv, inv (256)
   float* acc_lds = ecoef + 256;                    // 128
   bf16_t* t0 = reinterpret_cast<bf16_t*>(smem + 2304);
+#define FDBUF(i) (t0 + ((i) & 1) * 2 * TSZ)
+#define FXBUF(i) (t0 + TSZ + ((i) & 1) * 2 * TSZ)
 
   const int4 wk = a.work[blockIdx.x];
   const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int H = a.Hi, W = a.Wi;
-  const float n_hw = a.cnt[slot] * (float)(H * W);
-  make_coef<C, MODE_DY>(coef_d, a, slot, n_hw, a.st_in, a.st_in_b, a.in_gamma, a.in_beta);
-  {
-    const int c = threadIdx.x;
-    if (c < C) {
-      const float* prow = a.params + (long)slot * a.p_mstride;
-      float scale, shift, mean, inv;
-      bn_fwd_coef(stats_row(a.st_ep, slot), n_hw, prow[a.ep_gamma + c], prow[a.ep_beta + c], c, scale, shift, mean,
-                  inv);
-      ecoef[c] = scale;
-      ecoef[64 + c] = shift;
-      ecoef[128 + c] = mean;
-      ecoef[192 + c] = inv;
-    }
-    if (threadIdx.x < 128) acc_lds[threadIdx.x] = 0.f;
-  }
   const int ct = wave % NT;
   bf16x8_t afr[KS];
   {
@@ -876,140 +1081,140 @@ __global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
       afr[s] = v;
     }
   }
-  const int rows = a.rows;
-  const int bands = H / rows;
-  const int rows_t = rows + 2, wp = W + 2;
-  const int tsz = (rows_t * wp * CP + 63) & ~63;
-#define FDBUF(i) (t0 + ((i) & 1) * 2 * tsz)
-#define FXBUF(i) (t0 + tsz + ((i) & 1) * 2 * tsz)
-  const long img_elems = (long)H * W * C;
-  const int ntiles = rows * W / 16;
+  St st;
+  st.init();
+  uint4 dv[MAXC], dv2[MAXC], xv_[MAXC], unused[MAXC];
+  unsigned dm, xm;
+  {
+    const int img = it0 / BANDS, gy0 = (it0 % BANDS) * ROWS - 1;
+    dm = xm = st.mask(gy0);
+    st.template load<MODE_DY>(dv, dv2, dm, a.x + img * IMG, a.x2 + img * IMG, gy0);
+    st.template load<1>(xv_, unused, xm, a.xm + img * IMG, nullptr, gy0);
+  }
+  const float n_hw = a.cnt[slot] * (float)(H * W);
+  make_coef<C, MODE_DY>(coef_d, a, slot, n_hw, a.st_in, a.st_in_b, a.in_gamma, a.in_beta);
+  {
+    const int c = threadIdx.x;
+    if (c < C) {
+      const float* prow = a.params + (long)slot * a.p_mstride;
+      float scale, shift, mean, inv;
+      bn_fwd_coef(stats_row(a.st_ep, slot), n_hw, prow[a.ep_gamma + c], prow[a.ep_beta + c], c, scale, shift, mean,
+                  inv);
+      ecoef[c] = scale;
+      ecoef[64 + c] = shift;
+      ecoef[128 + c] = -mean * inv;
+      ecoef[192 + c] = inv;
+    }
+    if (threadIdx.x < 128) acc_lds[threadIdx.x] = 0.f;
+  }
+  // dgrad lane constants; k-chunks past KTOT have zero weights and read a valid in-tile address
   int tapoff[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     const int k0 = 32 * s + 8 * (lane >> 4);
     const int tap = k0 / C, c0 = k0 % C;
-    tapoff[s] = -((tap / 3) * wp + (tap % 3)) * CP + c0;
+    tapoff[s] = k0 < KTOT ? -((tap / 3) * WP + (tap % 3)) * CP + c0 : 0;
+  }
+  const int ci0 = ct * 16 + (lane >> 4) * 4;
+  int tbo[MAXT];
+  uint32_t pofs[MAXT];
+#pragma unroll
+  for (int i = 0; i < MAXT; ++i) {
+    const int p = (wave / NT + WPT * i) * 16 + (lane & 15);
+    tbo[i] = ((p / W + 2) * WP + p % W + 2) * CP;
+    pofs[i] = p * C + ci0;
   }
   // wgrad lane constants (pixel rows 8g+q and +4 of each 32-pixel k-step)
   const int g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
-  const int rstep = 32 / W;
   const int pa = 8 * g + q, pb = pa + 4;
-  const int ya = pa / W, xa = pa % W, yb = pb / W, xb = pb % W;
-  const int da_off = ((ya + 1) * wp + xa + 1) * CP + 4 * p4, db_off = ((yb + 1) * wp + xb + 1) * CP + 4 * p4;
-  const int xa_off = (ya * wp + xa) * CP + 4 * p4, xb_off = (yb * wp + xb) * CP + 4 * p4;
-  const int kinc = rstep * wp * CP;
+  const int da_off = ((pa / W + 1) * WP + pa % W + 1) * CP + 4 * p4;
+  const int db_off = ((pb / W + 1) * WP + pb % W + 1) * CP + 4 * p4;
+  const int xa_off = ((pa / W) * WP + pa % W) * CP + 4 * p4, xb_off = ((pb / W) * WP + pb % W) * CP + 4 * p4;
   int boff[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int nt = min(wave + 4 * j, NTN - 1);  // duplicates (nt >= NTN) are computed, never flushed
     const int tap = (nt * 16) / C, cb = (nt * 16) % C;
-    boff[j] = ((tap / 3) * wp + (tap % 3)) * CP + cb;
+    boff[j] = ((tap / 3) * WP + (tap % 3)) * CP + cb;
   }
   f32x4_t wacc[NJ][MT];
 #pragma unroll
   for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int m = 0; m < MT; ++m) wacc[j][m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  float ssum[4] = {0.f, 0.f, 0.f, 0.f}, ssq[4] = {0.f, 0.f, 0.f, 0.f};
+  f32x2_t ssum[2] = {{0.f, 0.f}, {0.f, 0.f}}, ssq[2] = {{0.f, 0.f}, {0.f, 0.f}};
 
-  TileDesc<C, 4> td;
-  tile_desc_init<C, 4>(td, rows_t, -1, wp, W);
-  TileRegs<C, MODE_DY, 4> rd;
-  TileRegs<C, 1, 4> rx;
   __syncthreads();  // coefficients
-  {
-    const int img = it0 / bands, r0 = (it0 % bands) * rows;
-    const bf16_t* d2 = a.x2 ? a.x2 + img * img_elems : nullptr;
-    tile_load<C, MODE_DY, 4>(rd, td, a.x + img * img_elems, d2, r0 - 1, H, W);
-    tile_load<C, 1, 4>(rx, td, a.xm + img * img_elems, nullptr, r0 - 1, H, W);
-    tile_store<C, MODE_DY, 4>(FDBUF(0), rd, td, a.x + img * img_elems, d2, r0 - 1, H, W, coef_d);
-    tile_store<C, 1, 4>(FXBUF(0), rx, td, a.xm + img * img_elems, nullptr, r0 - 1, H, W, ecoef);
-  }
+  st.template store<MODE_DY>(FDBUF(0), dv, dv2, dm, coef_d);
+  st.template store<1>(FXBUF(0), xv_, unused, xm, ecoef);
   __syncthreads();
   for (int k = 0; k < nit; ++k) {
     const int it = it0 + k;
-    const int img = it / bands, r0 = (it % bands) * rows;
+    const int img = it / BANDS, r0 = (it % BANDS) * ROWS;
     const bool more = k + 1 < nit;
-    const int nimg_ = (it + 1) / bands, nr0 = ((it + 1) % bands) * rows;
-    const bf16_t* nd2 = a.x2 ? a.x2 + nimg_ * img_elems : nullptr;
-    uint2 rres[MAXT], xres[MAXT];  // epilogue operands before the prefetch (counted vmcnt)
+    const long band = (long)img * IMG + r0 * ROW;
+    // epilogue operands before the prefetch (counted vmcnt)
+    uint2 rres[MAXT], xres[MAXT];
 #pragma unroll
     for (int i = 0; i < MAXT; ++i) {
-      const int t = min(wave / NT + WPT * i, ntiles - 1);
-      const int p = t * 16 + (lane & 15);
-      const long o = (((long)img * H + r0 + p / W) * W + p % W) * C + ct * 16 + (lane >> 4) * 4;
-      if constexpr (EPI & 1) rres[i] = *reinterpret_cast<const uint2*>(a.res + o);
-      xres[i] = *reinterpret_cast<const uint2*>(a.xm + o);
+      if constexpr (EPI & 1) rres[i] = *reinterpret_cast<const uint2*>(a.res + band + pofs[i]);
+      xres[i] = *reinterpret_cast<const uint2*>(a.xm + band + pofs[i]);
     }
     if (more) {
-      tile_load<C, MODE_DY, 4>(rd, td, a.x + nimg_ * img_elems, nd2, nr0 - 1, H, W);
-      tile_load<C, 1, 4>(rx, td, a.xm + nimg_ * img_elems, nullptr, nr0 - 1, H, W);
+      const int nimg = (it + 1) / BANDS, ngy0 = ((it + 1) % BANDS) * ROWS - 1;
+      dm = xm = st.mask(ngy0);
+      st.template load<MODE_DY>(dv, dv2, dm, a.x + nimg * IMG, a.x2 + nimg * IMG, ngy0);
+      st.template load<1>(xv_, unused, xm, a.xm + nimg * IMG, nullptr, ngy0);
     }
     const bf16_t* dcur = FDBUF(k);
     const bf16_t* xcur = FXBUF(k);
     // ---- dgrad
+    const f32x2_t sc0 = lds2(ecoef + ci0), sc1 = lds2(ecoef + ci0 + 2);
+    const f32x2_t sh0 = lds2(ecoef + 64 + ci0), sh1 = lds2(ecoef + 64 + ci0 + 2);
+    const f32x2_t nm0 = lds2(ecoef + 128 + ci0), nm1 = lds2(ecoef + 128 + ci0 + 2);
+    const f32x2_t iv0 = lds2(ecoef + 192 + ci0), iv1 = lds2(ecoef + 192 + ci0 + 2);
 #pragma unroll
     for (int i = 0; i < MAXT; ++i) {
-      const int t = wave / NT + WPT * i;
-      if (t >= ntiles) break;
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-      const int p = t * 16 + (lane & 15);
-      const int iy = r0 + p / W, ix = p % W;
-      const int ci0 = ct * 16 + (lane >> 4) * 4;
-      const long o = (((long)img * H + iy) * W + ix) * C + ci0;
-      uint2 rr = make_uint2(0, 0);
-      if constexpr (EPI & 1) rr = rres[i];
-      const uint2 xr = xres[i];
-      const bf16_t* tb = dcur + ((iy - r0 + 2) * wp + ix + 2) * CP;
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        bf16x8_t b = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (32 * s + 8 * (lane >> 4) < KTOT) b = *reinterpret_cast<const bf16x8_t*>(tb + tapoff[s]);
-        acc = mfma16(afr[s], b, acc);
-      }
-      float v[4] = {acc[0], acc[1], acc[2], acc[3]};
+      for (int s = 0; s < KS; ++s)
+        acc = mfma16(afr[s], *reinterpret_cast<const bf16x8_t*>(dcur + tbo[i] + tapoff[s]), acc);
+      f32x2_t v0 = {acc[0], acc[1]}, v1 = {acc[2], acc[3]};
       if constexpr (EPI & 1) {
-        v[0] += bf2f((bf16_t)(rr.x & 0xffff));
-        v[1] += bf2f((bf16_t)(rr.x >> 16));
-        v[2] += bf2f((bf16_t)(rr.y & 0xffff));
-        v[3] += bf2f((bf16_t)(rr.y >> 16));
+        v0 += unpk2(rres[i].x);
+        v1 += unpk2(rres[i].y);
       }
-      const float xv[4] = {bf2f((bf16_t)(xr.x & 0xffff)), bf2f((bf16_t)(xr.x >> 16)), bf2f((bf16_t)(xr.y & 0xffff)),
-                           bf2f((bf16_t)(xr.y >> 16))};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int c = ci0 + r;
-        v[r] = (xv[r] * ecoef[c] + ecoef[64 + c] > 0.f) ? v[r] : 0.f;
-      }
+      const f32x2_t x0 = unpk2(xres[i].x), x1 = unpk2(xres[i].y);
+      const f32x2_t pre0 = x0 * sc0 + sh0, pre1 = x1 * sc1 + sh1;
+      v0.x = pre0.x > 0.f ? v0.x : 0.f;
+      v0.y = pre0.y > 0.f ? v0.y : 0.f;
+      v1.x = pre1.x > 0.f ? v1.x : 0.f;
+      v1.y = pre1.y > 0.f ? v1.y : 0.f;
       uint2 pk;
-      pk.x = pack2bf(v[0], v[1]);
-      pk.y = pack2bf(v[2], v[3]);
-      *reinterpret_cast<uint2*>(a.y + o) = pk;
-      const float dz[4] = {bf2f((bf16_t)(pk.x & 0xffff)), bf2f((bf16_t)(pk.x >> 16)), bf2f((bf16_t)(pk.y & 0xffff)),
-                           bf2f((bf16_t)(pk.y >> 16))};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int c = ci0 + r;
-        ssum[r] += dz[r];
-        ssq[r] += dz[r] * (xv[r] - ecoef[128 + c]) * ecoef[192 + c];
-      }
+      pk.x = pk2(v0);
+      pk.y = pk2(v1);
+      *reinterpret_cast<uint2*>(a.y + band + pofs[i]) = pk;
+      const f32x2_t dz0 = unpk2(pk.x), dz1 = unpk2(pk.y);
+      ssum[0] += dz0;
+      ssum[1] += dz1;
+      ssq[0] += dz0 * (x0 * iv0 + nm0);
+      ssq[1] += dz1 * (x1 * iv1 + nm1);
     }
     // ---- wgrad
-    const int nk = rows * W / 32;
-    for (int ks = 0; ks < nk; ++ks) {
+#pragma unroll
+    for (int ks = 0; ks < NK; ++ks) {
       bf16x8_t af[MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
-        s16x4_t lo = ds_read_tr(dcur + da_off + ks * kinc + m * 16);
-        s16x4_t hi = ds_read_tr(dcur + db_off + ks * kinc + m * 16);
+        s16x4_t lo = ds_read_tr(dcur + da_off + ks * KINC + m * 16);
+        s16x4_t hi = ds_read_tr(dcur + db_off + ks * KINC + m * 16);
         af[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
       bf16x8_t bfr[NJ];
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        s16x4_t lo = ds_read_tr(xcur + xa_off + ks * kinc + boff[j]);
-        s16x4_t hi = ds_read_tr(xcur + xb_off + ks * kinc + boff[j]);
+        s16x4_t lo = ds_read_tr(xcur + xa_off + ks * KINC + boff[j]);
+        s16x4_t hi = ds_read_tr(xcur + xb_off + ks * KINC + boff[j]);
         bfr[j] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll
@@ -1018,12 +1223,18 @@ __global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
         for (int m = 0; m < MT; ++m) wacc[j][m] = mfma16(af[m], bfr[j], wacc[j][m]);
     }
     if (more) {
-      tile_store<C, MODE_DY, 4>(FDBUF(k + 1), rd, td, a.x + nimg_ * img_elems, nd2, nr0 - 1, H, W, coef_d);
-      tile_store<C, 1, 4>(FXBUF(k + 1), rx, td, a.xm + nimg_ * img_elems, nullptr, nr0 - 1, H, W, ecoef);
+      st.template store<MODE_DY>(FDBUF(k + 1), dv, dv2, dm, coef_d);
+      st.template store<1>(FXBUF(k + 1), xv_, unused, xm, ecoef);
     }
     __syncthreads();
   }
-  reduce_stats_to_lds(acc_lds, ssum, ssq, ct * 16 + (lane >> 4) * 4, lane);
+#undef FDBUF
+#undef FXBUF
+  {
+    const float s4[4] = {ssum[0].x, ssum[0].y, ssum[1].x, ssum[1].y};
+    const float q4[4] = {ssq[0].x, ssq[0].y, ssq[1].x, ssq[1].y};
+    reduce_stats_to_lds(acc_lds, s4, q4, ci0, lane);
+  }
   __syncthreads();
   flush_stats(a.st_out, acc_lds, slot, C);
   float* gb = a.grads + (long)slot * a.g_mstride + a.g_off;
@@ -1067,6 +1278,21 @@ int launch(KernelT k, int nblocks, size_t lds, hipStream_t st, const ConvArgs& a
 #define WGRAD_CASE(CI, CO, S, K, MX, MD)                                                             \
   if (cin == CI && cout == CO && s == S && k == K && mode_x == MX && mode_dy == MD)                  \
     return launch(conv_wgrad_kernel<CI, CO, S, K, MX, MD>, nblocks, lds, stream, *args);
+
+DTF_API int dtf_conv_fwd_s1(const ConvArgs* args, int c, int mode, int resid, int nblocks, int lds,
+                            hipStream_t stream) {
+#define S1_CASE(CC, M, R) \
+  if (c == CC && mode == M && resid == R) return launch(conv_fwd_s1_kernel<CC, M, R>, nblocks, lds, stream, *args);
+  S1_CASE(16, 0, false)  // stem (input padded to 16 channels)
+  S1_CASE(16, 1, false)
+  S1_CASE(16, 1, true)
+  S1_CASE(32, 1, false)
+  S1_CASE(32, 1, true)
+  S1_CASE(64, 1, false)
+  S1_CASE(64, 1, true)
+#undef S1_CASE
+  return -1;
+}
 
 DTF_API int dtf_conv_args_size() { return (int)sizeof(ConvArgs); }
 

@@ -50,7 +50,7 @@ class ConvArgs(ctypes.Structure):
         ("x_gamma", c_int), ("x_beta", c_int),
         ("st_in", c_void_p), ("st_in_b", c_void_p), ("st_ep", c_void_p), ("st_x", c_void_p), ("st_out", c_void_p),
         ("cnt", c_void_p), ("Hi", c_int), ("Wi", c_int), ("Ho", c_int), ("Wo", c_int), ("rows", c_int),
-        ("cin_real", c_int),
+        ("cin_real", c_int), ("slab", c_void_p),
     ]
 
 
@@ -85,6 +85,7 @@ def _register():
     ops.register("dtf_conv_dgrad", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_wgrad", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_fwd_s1", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
+    ops.register("dtf_dw_slab_reduce", [c_void_p, c_void_p, c_int, c_void_p, c_long, c_long, c_int, c_void_p])
     ops.register("dtf_conv_bwd_fused", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_args_size", [])
     ops.register("dtf_bnbwd_args_size", [])
@@ -391,7 +392,8 @@ class _StepPlan:
                 break
         assert rows is not None, ("no valid band for conv", ci)
         bands = Ho // rows
-        n_wg = self._n_wg_iters(self.N * bands)
+        per_wg = int(os.environ.get("DTF_FWD_ITERS_%d" % c.cout, 4))
+        n_wg = self._n_wg_iters(self.N * bands, per_wg=per_wg, hi=max(1024, self.N * bands // per_wg))
         work = self._work_iters(bands, n_wg)
         a = self._base_args()
         a.x, a.y, a.res = _p(x), _p(y), _p(res)
@@ -509,12 +511,7 @@ class _StepPlan:
         # the fused kernel's geometry is compile-time: W = H = 512 / C, 8-row bands
         assert rows == 8 and H == 512 // C and x.shape[2] == H, (C, H, rows)
         bands = H // rows
-        wn = 9 * C * C
-        # dW atomic traffic budget per launch (bytes): bounds the workgroup count; 64 channels trade more atomics
-        # for filling more CUs (measured: 16/32 ch best at 16 MB, 64 ch at 32 MB)
-        budget = float(os.environ.get("DTF_FUSED_ATOMIC_BYTES_%d" % C, {64: 32e6}.get(C, 16e6)))
-        n_wg = max(64, min(128 * len(self.slots), int(budget / (4.0 * wn))))
-        n_wg = min(n_wg, self.N * bands)
+        n_wg = self._fused_nwg(C, bands)
         work = self._work_iters(bands, n_wg)
         a = self._base_args()
         a.x, a.x2, a.y, a.xm, a.res = _p(dy), _p(dy2), _p(dz_out), _p(x), _p(res)
@@ -531,8 +528,55 @@ class _StepPlan:
         tsz = ((rows + 2) * (H + 2) * (C + 8) + 63) // 64 * 64
         lds = 2304 + 4 * tsz * 2
         lib = ops.lib()
+        slab = os.environ.get("DTF_DW_SLAB", "1") == "1"
+        if slab:
+            a.slab = _p(self._slab(self._slab_floats()))
         self._add(lib.dtf_conv_bwd_fused, ctypes.byref(a), C, mode_dy, int(res is not None), work.shape[0], lds)
         self._keep(a)
+        if slab:
+            red = self._slab_table(work)
+            self._add(lib.dtf_dw_slab_reduce, a.slab, _p(red), red.shape[0], _p(self.e.grads), self.e.Pp, c.off, C)
+
+    @staticmethod
+    def _slab_elems(C):
+        return ((9 * C // 16 + 3) // 4) * (C // 16) * 4 * 256
+
+    def _fused_nwg(self, C, bands):
+        # per-launch budget for the dW partials (bytes of slab stores, or of atomics without slabs): bounds the
+        # workgroup count of the fused kernel
+        wn = 9 * C * C
+        budget = float(os.environ.get("DTF_FUSED_ATOMIC_BYTES_%d" % C, {64: 32e6}.get(C, 16e6)))
+        n_wg = max(64, min(128 * len(self.slots), int(budget / (4.0 * wn))))
+        return min(n_wg, self.N * bands)
+
+    def _slab_floats(self):
+        cfg = self.be.L.cfg
+        need = 0
+        for st in range(len(cfg.block_sizes)):
+            C = cfg.num_filters * (2 ** st)
+            H = cfg.image_size >> st
+            if C in (16, 32, 64) and H == 512 // C:
+                need = max(need, self._fused_nwg(C, H // 8) * self._slab_elems(C))
+        return need
+
+    def _slab(self, n):
+        if getattr(self, "slab_buf", None) is None or self.slab_buf.numel() < n:
+            assert getattr(self, "slab_buf", None) is None, "slab must be sized once per plan"
+            self.slab_buf = torch.empty(max(n, 1), dtype=torch.float32, device=self.be.dev)
+        return self.slab_buf
+
+    def _slab_table(self, work):
+        """(first wg, n wgs, 0, slot) per member of a work-item array grouped by member."""
+        w = work.cpu().tolist()
+        rows = []
+        for i, it in enumerate(w):
+            if rows and rows[-1][3] == it[3] and rows[-1][0] + rows[-1][1] == i:
+                rows[-1][1] += 1
+            else:
+                rows.append([i, 1, 0, it[3]])
+        t = torch.tensor(rows, dtype=torch.int32, device=self.be.dev)
+        self._keep(t)
+        return t
 
     def _keep(self, obj):
         if not hasattr(self, "_keepalive"):

@@ -60,6 +60,7 @@ struct ConvArgs {
   int Hi, Wi, Ho, Wo;       // forward input / output spatial dims
   int rows;                 // rows per band (output rows for fwd/wgrad, dx rows for dgrad)
   int cin_real;             // wgrad: real input channels (stem: 3)
+  float* slab;              // fused bwd: per-workgroup dW partials (plain stores; reduced by dw_slab_reduce)
 };
 
 __device__ __forceinline__ const float* stats_row(const float* base, int slot) {
@@ -1237,6 +1238,17 @@ __global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
   }
   __syncthreads();
   flush_stats(a.st_out, acc_lds, slot, C);
+  if (a.slab) {
+    // coalesced partial-sum slab [wg][j][m][r][256 threads]; dw_slab_reduce_kernel sums a member's slabs
+    float* sb = a.slab + (long)blockIdx.x * (NJ * MT * 4 * 256) + threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sb[((j * MT + m) * 4 + r) * 256] = wacc[j][m][r];
+    return;
+  }
   float* gb = a.grads + (long)slot * a.g_mstride + a.g_off;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
@@ -1253,6 +1265,41 @@ __global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
       }
     }
   }
+}
+
+// Sum of one member's per-workgroup dW slabs (written by conv_bwd_fused_kernel) into its gradient row.
+// grid (E/32, members), 256 threads = 32 slab elements x 8 workgroup groups (each thread strides over the
+// member's slabs, then an LDS reduction across the 8 groups); red[y] = (first wg, n wgs, -, slot).  Element
+// e of a slab is (j, m, r, thread) -> dW[co][tap][ci] with the MFMA C/D lane mapping of the fused kernel;
+// duplicate tiles (nt >= NTN) are skipped.
+template <int C>
+__global__ __launch_bounds__(256) void dw_slab_reduce_kernel(const float* __restrict__ slab,
+                                                             const int4* __restrict__ red, float* __restrict__ grads,
+                                                             long g_mstride, long g_off) {
+  constexpr int MT = C / 16, NTN = 9 * C / 16, NJ = (NTN + 3) / 4, E = NJ * MT * 4 * 256;
+  __shared__ float part[8][33];
+  const int el = threadIdx.x & 31, gg = threadIdx.x >> 5;
+  const int e = blockIdx.x * 32 + el;
+  const int4 rd = red[blockIdx.y];
+  const float* p = slab + (long)rd.x * E + e;
+  float s0 = 0.f, s1 = 0.f;
+  int g = gg;
+  for (; g + 8 < rd.y; g += 16) {
+    s0 += p[(long)g * E];
+    s1 += p[(long)(g + 8) * E];
+  }
+  if (g < rd.y) s0 += p[(long)g * E];
+  part[gg][el] = s0 + s1;
+  __syncthreads();
+  if (gg != 0) return;
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sum += part[i][el];
+  const int t = e & 255, r = (e >> 8) & 3, m = (e >> 10) % MT, j = (e >> 10) / MT;
+  const int wave = t >> 6, lane = t & 63, nt = wave + 4 * j;
+  if (nt >= NTN) return;
+  const int tap = (nt * 16) / C, ci = (nt * 16) % C + (lane & 15), co = m * 16 + 4 * (lane >> 4) + r;
+  grads[(long)rd.w * g_mstride + g_off + ((long)co * 9 + tap) * C + ci] += sum;
 }
 
 template <typename KernelT>
@@ -1291,6 +1338,23 @@ DTF_API int dtf_conv_fwd_s1(const ConvArgs* args, int c, int mode, int resid, in
   S1_CASE(64, 1, false)
   S1_CASE(64, 1, true)
 #undef S1_CASE
+  return -1;
+}
+
+DTF_API int dtf_dw_slab_reduce(const float* slab, const int4* red, int nmembers, float* grads, long g_mstride,
+                               long g_off, int c, hipStream_t stream) {
+  if (nmembers <= 0) return 0;
+#define RED_CASE(CC)                                                                                        \
+  if (c == CC) {                                                                                            \
+    constexpr int E = ((9 * CC / 16 + 3) / 4) * (CC / 16) * 4 * 256;                                         \
+    hipLaunchKernelGGL(dw_slab_reduce_kernel<CC>, dim3(E / 32, nmembers), dim3(256), 0, stream, slab, red, \
+                       grads, g_mstride, g_off);                                                            \
+    return DTF_CHECK_LAUNCH();                                                                              \
+  }
+  RED_CASE(16)
+  RED_CASE(32)
+  RED_CASE(64)
+#undef RED_CASE
   return -1;
 }
 

@@ -35,6 +35,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--pop", type=int, default=8)
     p.add_argument("--batch", type=int, default=128)
+    p.add_argument("--model", default="resnet", choices=["resnet", "mnist"],
+                   help="resnet = headline CIFAR-10 ResNet (BASELINE configs 3/4); mnist = BASELINE config 2")
     p.add_argument("--resnet_size", type=int, default=56)
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     p.add_argument("--exploit_every", type=int, default=25)
@@ -52,6 +54,7 @@ def main():
     from distributedtf_amd.pbt.cluster import partition, sample_population
     from distributedtf_amd.pbt.exploit import plan_exploit, apply_plan_to_values
     from distributedtf_amd.models.cifar10_model import Cifar10Model
+    from distributedtf_amd.models.mnist_model import MNISTModel
 
     comm = init_distributed()
     rank, world = comm.Get_rank(), comm.Get_size()
@@ -63,10 +66,15 @@ def main():
     for h in hps:
         h["batch_size"] = args.batch
     begin, cnt = partition(args.pop, world)[rank]
-    members = [Cifar10Model(begin + i, hps[begin + i], "/tmp/bench_savedata_%d/model_" % rank, seed=args.seed,
-                            resnet_size=args.resnet_size, device=dev, backend=args.backend,
-                            capacity=max(1, cnt), use_synthetic_data=True, checkpoint_every_round=False)
-               for i in range(cnt)]
+    if args.model == "mnist":
+        make = lambda i: MNISTModel(begin + i, hps[begin + i], "/tmp/bench_savedata_%d/model_" % rank,  # noqa: E731
+                                    seed=args.seed, device=dev, backend=args.backend, capacity=max(1, cnt),
+                                    use_synthetic_data=True, checkpoint_every_round=False)
+    else:
+        make = lambda i: Cifar10Model(begin + i, hps[begin + i], "/tmp/bench_savedata_%d/model_" % rank,  # noqa: E731
+                                      seed=args.seed, resnet_size=args.resnet_size, device=dev, backend=args.backend,
+                                      capacity=max(1, cnt), use_synthetic_data=True, checkpoint_every_round=False)
+    members = [make(i) for i in range(cnt)]
     eng = members[0].engine
     ds = members[0].dataset()
     dataplane = DataPlane(comm)
@@ -125,8 +133,10 @@ def main():
     value = images / dt_max
     if rank == 0:
         flops = members[0].arch.flops_per_image() * 3.0 * images / dt_max
+        metric = BASELINE_METRIC if args.model == "resnet" and args.resnet_size == 56 else \
+            "images/sec (whole node) %s PBT pop=%d" % (members[0].arch.name, args.pop)
         out = {
-            "metric": BASELINE_METRIC,
+            "metric": metric,
             "value": round(value, 1),
             "unit": "images/s",
             "n_gpus": world,
@@ -137,8 +147,9 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic (device-resident random-normal 32x32x3, uniform labels), random-init weights",
-            "config": {"model": "resnet%d_v2_cifar10" % args.resnet_size, "global_batch": args.pop * args.batch,
+            "data": "synthetic (device-resident random-normal %s, uniform labels), random-init weights"
+                    % ("32x32x3" if args.model == "resnet" else "28x28x1"),
+            "config": {"model": ("resnet%d_v2_cifar10" % args.resnet_size) if args.model == "resnet" else "mnist_cnn", "global_batch": args.pop * args.batch,
                        "per_member_batch": args.batch, "population": args.pop, "seq_len": None,
                        "parallelism": "pbt_pop%d_%dmembers_per_gpu" % (args.pop, cnt),
                        "backend": eng.backend.name, "exploit_every": args.exploit_every,

@@ -206,6 +206,9 @@ def make_backend(engine: PopulationEngine, name: str):
     if name == "torch":
         return TorchBackend(engine)
     if name == "hip":
+        if getattr(engine.arch, "name", "") == "mnist_cnn":
+            from .hip_mnist import HipMnistBackend
+            return HipMnistBackend(engine)
         from .hip_resnet import HipResNetBackend
         return HipResNetBackend(engine)
     raise ValueError("unknown backend %r" % name)

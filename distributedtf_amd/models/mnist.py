@@ -25,7 +25,7 @@ _SHAPES = [
 
 class MnistArch:
     name = "mnist_cnn"
-    hip_supported = False
+    hip_supported = True  # engine/hip_mnist.py (ops/csrc/mnist.hip + gemm.hip)
     num_classes = 10
     input_shape = (28, 28, 1)
 
@@ -61,7 +61,9 @@ class MnistArch:
                 p[off:off + w.numel()] = w.flatten()
         return p, torch.zeros(0)
 
-    def forward(self, params, running, x_nhwc, training=True, dtype=torch.float32):
+    def forward(self, params, running, x_nhwc, training=True, dtype=torch.float32, dropout_mask=None):
+        """``dropout_mask`` (bool [B, 1024], True = kept) replaces the random draw, e.g. with the HIP head
+        kernel's counter-hash mask (``engine.hip_mnist.dropout_keep_mask``) for numerics tests."""
         x = x_nhwc.reshape(-1, 28, 28, 1).permute(0, 3, 1, 2).to(dtype)
         w1 = self.view(params, "conv1_w").permute(0, 3, 1, 2).to(dtype)
         w2 = self.view(params, "conv2_w").permute(0, 3, 1, 2).to(dtype)
@@ -72,7 +74,10 @@ class MnistArch:
         x = x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)  # TF flatten order (H, W, C)
         x = F.relu(F.linear(x, self.view(params, "dense1_w").to(dtype), self.view(params, "dense1_b").to(dtype)))
         if training and self.dropout > 0:
-            x = F.dropout(x, self.dropout, training=True)
+            if dropout_mask is not None:
+                x = x * dropout_mask.to(x.device, x.dtype) / (1.0 - self.dropout)
+            else:
+                x = F.dropout(x, self.dropout, training=True)
         return F.linear(x.float(), self.view(params, "dense2_w"), self.view(params, "dense2_b"))
 
     def flops_per_image(self):

@@ -31,6 +31,7 @@ import torch
 
 from .. import ops
 from ..data.datasets import IndexBatch, batch_len
+from .hip_resnet import advance_steps, note_step_advanced, same_batches, upload_hyper
 
 c_void_p, c_int, c_long, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float
 
@@ -193,15 +194,12 @@ class HipMnistBackend:
         batches = [b.materialize() if isinstance(b, IndexBatch) else b for b in batches]
         sizes = [batch_len(b) for b in batches]
         p = self.plan(slots, sizes)
-        from .optim import hyper_row
-        hy = torch.zeros(e.capacity, 8, dtype=torch.float32)
-        for s, hp, lr in zip(slots, hparams, lrs):
-            hy[s] = torch.tensor(hyper_row(hp, lr, e.host_step[s] + 1, True))
-        e.hyper.copy_(hy, non_blocking=True)
+        upload_hyper(e, slots, hparams, lrs)
         self.last_rng = self.next_rng()
         self.rng.copy_(torch.tensor(self.last_rng, dtype=torch.int32), non_blocking=True)
         p.load_batch(batches)
         p.run()
+        note_step_advanced(e, slots)
         return self.loss[p.slots_long].clone()
 
     def forward_backward(self, slots, batches):
@@ -286,6 +284,8 @@ class _MnistPlan:
         return torch.tensor(items, dtype=torch.int32, device=self.be.dev)
 
     def load_batch(self, batches):
+        if same_batches(self, batches):
+            return
         off = 0
         for (x, y) in batches:
             n = x.shape[0]
@@ -320,7 +320,7 @@ class _MnistPlan:
         self._launch(L.dtf_mnist_conv2_wgrad, self.w_c2w)
         self._launch(L.dtf_mnist_conv1_wgrad, self.w_c1w)
         ops.fused_optimizer(e.state, e.grads, e.hyper, e.Pp, e.P, e.n_reg, shadow=be.shadow, zero_grads=True)
-        e.step_col().index_add_(0, self.slots_long, torch.ones(len(self.slots), device=e.device))
+        advance_steps(e, self.slots_long)
 
     def run(self):
         be = self.be

@@ -171,6 +171,54 @@ class _Layout:
         self.bn_table = [[b.run_off, b.c, self.bn_hw[b.idx], b.idx, b.gamma_off, b.beta_off, 0, 0] for b in prog.bns]
 
 
+def upload_hyper(e, slots, hparams, lrs):
+    """Per-member optimizer hyper rows -> device table, skipped when only the step counter moved (the lr
+    schedule is piecewise constant).  The captured step advances the table's step column on the device
+    (``advance_steps``) and ``e._hyper_dev`` mirrors what the device holds, so a skip is exact -- also after
+    an exploit import changes a member's step."""
+    from .optim import H_STEP, hyper_row
+    rows = [(s, hyper_row(hp, lr, e.host_step[s] + 1, True)) for s, hp, lr in zip(slots, hparams, lrs)]
+    dev = getattr(e, "_hyper_dev", None)
+    if dev is not None and dev.get("slots") == tuple(slots) and all(dev.get(s) == r for s, r in rows):
+        return
+    hy = torch.zeros(e.capacity, 8, dtype=torch.float32)
+    for s, r in rows:
+        hy[s] = torch.tensor(r)
+    e.hyper.copy_(hy.pin_memory() if e.device.type == "cuda" else hy, non_blocking=True)
+    e._hyper_dev = {s: list(r) for s, r in rows}
+    e._hyper_dev["slots"] = tuple(slots)
+
+
+def note_step_advanced(e, slots):
+    """Host mirror of ``advance_steps`` (call once per executed step)."""
+    from .optim import H_STEP
+    dev = getattr(e, "_hyper_dev", None)
+    if dev is not None:
+        for s in slots:
+            if s in dev:
+                dev[s][H_STEP] += 1.0
+
+
+def advance_steps(e, slots_long):
+    """Inside the captured step: per-member step counters (state column + hyper table) += 1."""
+    from .optim import H_STEP
+    one = torch.ones(slots_long.numel(), device=e.device)
+    e.step_col().index_add_(0, slots_long, one)
+    e.hyper[:, H_STEP].index_add_(0, slots_long, one)
+
+
+def same_batches(plan, batches) -> bool:
+    """True if ``batches`` are the very (x, y) storages staged last step and unmodified since (tensor version
+    counters); a reference to them is held so their memory cannot be recycled into a different batch."""
+    key = tuple((x.data_ptr(), x.shape, x.stride(), x._version, y.data_ptr(), y.shape, y._version)
+                for x, y in batches)
+    if getattr(plan, "_batch_key", None) == key:
+        return True
+    plan._batch_key = key
+    plan._batch_ref = list(batches)
+    return False
+
+
 class HipResNetBackend:
     name = "hip"
 
@@ -229,13 +277,10 @@ class HipResNetBackend:
             batches = [b.materialize() if isinstance(b, IndexBatch) else b for b in batches]
         sizes = [batch_len(b) for b in batches]
         p = self.plan(slots, sizes, src)
-        hy = torch.zeros(e.capacity, 8, dtype=torch.float32)
-        from .optim import hyper_row
-        for s, hp, lr in zip(slots, hparams, lrs):
-            hy[s] = torch.tensor(hyper_row(hp, lr, e.host_step[s] + 1, True))
-        e.hyper.copy_(hy, non_blocking=True)
+        upload_hyper(e, slots, hparams, lrs)
         p.load_batch(batches)
         p.run(train=True)
+        note_step_advanced(e, slots)
         return p.loss_view()
 
     def forward_backward(self, slots, batches):
@@ -314,6 +359,9 @@ class _StepPlan:
             hw //= blk.stride
         self.dfeat = torch.zeros(N, cfg.final_size, dtype=torch.float32, device=dev)
         self._work_cache = {}
+        # dW slab reductions on a forked stream (joined before the optimizer): off the critical path
+        self.side_reduce = dev.type == "cuda" and os.environ.get("DTF_SIDE_REDUCE", "0") == "1"
+        self.side_stream = torch.cuda.Stream(device=dev) if self.side_reduce else None
         self.launches = []
         self._build()
         self.graph = None
@@ -529,13 +577,19 @@ class _StepPlan:
         lds = 2304 + 4 * tsz * 2
         lib = ops.lib()
         slab = os.environ.get("DTF_DW_SLAB", "1") == "1"
+        side = slab and self.side_reduce
         if slab:
-            a.slab = _p(self._slab(self._slab_floats()))
+            # side-stream reductions run concurrently with later layers: every layer needs its own slab region
+            a.slab = _p(self._layer_slab(work.shape[0] * self._slab_elems(C)) if side else self._slab(self._slab_floats()))
         self._add(lib.dtf_conv_bwd_fused, ctypes.byref(a), C, mode_dy, int(res is not None), work.shape[0], lds)
         self._keep(a)
         if slab:
             red = self._slab_table(work)
-            self._add(lib.dtf_dw_slab_reduce, a.slab, _p(red), red.shape[0], _p(self.e.grads), self.e.Pp, c.off, C)
+            args = (a.slab, _p(red), red.shape[0], _p(self.e.grads), self.e.Pp, c.off, C)
+            if side:
+                self._add("side", (lib.dtf_dw_slab_reduce, args))
+            else:
+                self._add(lib.dtf_dw_slab_reduce, *args)
 
     @staticmethod
     def _slab_elems(C):
@@ -558,6 +612,11 @@ class _StepPlan:
             if C in (16, 32, 64) and H == 512 // C:
                 need = max(need, self._fused_nwg(C, H // 8) * self._slab_elems(C))
         return need
+
+    def _layer_slab(self, n):
+        t = torch.empty(max(n, 1), dtype=torch.float32, device=self.be.dev)
+        self._keep(t)
+        return t
 
     def _slab(self, n):
         if getattr(self, "slab_buf", None) is None or self.slab_buf.numel() < n:
@@ -688,6 +747,8 @@ class _StepPlan:
     # -------------------------------------------------------------------- execution
     def load_batch(self, batches):
         off = 0
+        if self.src is None and same_batches(self, batches):
+            return  # the staged copy is still current (same unmodified source storage)
         if self.src is not None:
             for b in batches:
                 n = len(b)
@@ -702,9 +763,22 @@ class _StepPlan:
             off += n
 
     def _run_eager(self):
-        stream = ops.stream()
         e = self.e
+        main = torch.cuda.current_stream()
+        side = self.side_stream
+        forked = False
         for fn, args in self.launches:
+            if fn == "side":
+                kfn, kargs = args[0]
+                side.wait_stream(main)  # fork: the producing kernel has been enqueued on main
+                err = kfn(*kargs, ctypes.c_void_p(side.cuda_stream))
+                if err != 0:
+                    raise RuntimeError("side-stream launch failed with %d" % err)
+                forked = True
+                continue
+            if fn == "optim" and forked:
+                main.wait_stream(side)  # join before the optimizer reads the gradients
+                forked = False
             if fn == "zero":
                 args[0].zero_()
             elif fn == "augment":
@@ -713,7 +787,7 @@ class _StepPlan:
             elif fn == "optim":
                 ops.fused_optimizer(e.state, e.grads, e.hyper, e.Pp, e.P, e.n_reg, shadow=None, zero_grads=True)
             elif fn == "step":
-                e.step_col().index_add_(0, self.slots_long, torch.ones(len(self.slots), device=e.device))
+                advance_steps(e, self.slots_long)
             else:
                 err = fn(*args, ops.stream())
                 if err != 0:

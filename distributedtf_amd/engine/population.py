@@ -121,6 +121,7 @@ class PopulationEngine:
     def set_hyper(self, slot: int, hparams: Dict, lr: float, active: bool = True) -> None:
         row = _optim.hyper_row(hparams, lr, self.host_step[slot] + 1, active)
         self.hyper[slot] = torch.tensor(row, dtype=torch.float32)
+        self._hyper_dev = None  # invalidate the HIP backends' upload cache
 
     def train_step(self, slots: Sequence[int], batches: Sequence[Tuple[torch.Tensor, torch.Tensor]],
                    hparams: Sequence[Dict], lrs: Sequence[float]) -> torch.Tensor:
@@ -138,6 +139,7 @@ class PopulationEngine:
         for s, hp, lr in zip(slots, hparams, lrs):
             hy[s] = torch.tensor(_optim.hyper_row(hp, lr, self.host_step[s] + 1, True))
         self.hyper.copy_(hy.to(self.device), non_blocking=True)
+        self._hyper_dev = None
         losses = self.backend.forward_backward(slots, batches)
         self.apply_optimizer(slots)
         for s in slots:

@@ -46,21 +46,32 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(const float* __restric
                                                            const int* __restrict__ table, const int* __restrict__ slots,
                                                            bf16_t* __restrict__ wf, bf16_t* __restrict__ wd,
                                                            long w_mstride) {
+  // grid (conv, chunk, member): every conv is split over gridDim.y workgroups so the launch fills the GPU
+  // even for a single member (it sits at the head of the step's critical path).
   const int* t = table + blockIdx.x * 8;
-  const int slot = slots[blockIdx.y];
+  const int slot = slots[blockIdx.z];
   const int w_off = t[0], cout = t[1], cin = t[2], k = t[3], cin_pad = t[4], fwd_off = t[5], dgr_off = t[6];
   const int kk = k * k;
   const float* p = state + (long)slot * s_mstride + w_off;
   bf16_t* f = wf + (long)slot * w_mstride + fwd_off;
   bf16_t* d = wd + (long)slot * w_mstride + dgr_off;
   const int nf = cout * kk * cin_pad;
-  for (int i = threadIdx.x; i < nf; i += blockDim.x) {
-    const int ci = i % cin_pad, rest = i / cin_pad;  // rest = co*kk + tap
-    f[i] = ci < cin ? f2bf(p[rest * cin + ci]) : (bf16_t)0;
+  const int t0 = blockIdx.y * blockDim.x + threadIdx.x, tstride = gridDim.y * blockDim.x;
+  if (cin_pad == cin && (nf & 3) == 0 && (w_off & 3) == 0) {
+    // same OHWI order: 4 elements per thread (float4 in, 4 x bf16 out)
+    for (int i = 4 * t0; i < nf; i += 4 * tstride) {
+      const float4 v = *reinterpret_cast<const float4*>(p + i);
+      *reinterpret_cast<uint2*>(f + i) = make_uint2(pack2bf(v.x, v.y), pack2bf(v.z, v.w));
+    }
+  } else {
+    for (int i = t0; i < nf; i += tstride) {
+      const int ci = i % cin_pad, rest = i / cin_pad;  // rest = co*kk + tap
+      f[i] = ci < cin ? f2bf(p[rest * cin + ci]) : (bf16_t)0;
+    }
   }
   if (dgr_off >= 0) {
     const int nd = cin * kk * cout;
-    for (int i = threadIdx.x; i < nd; i += blockDim.x) {
+    for (int i = t0; i < nd; i += tstride) {
       const int co = i % cout, rest = i / cout;  // rest = ci*kk + tap
       const int tap = rest % kk, ci = rest / kk;
       d[i] = f2bf(p[(co * kk + tap) * cin + ci]);
@@ -152,7 +163,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a) {
   __syncthreads();
   const long base = (long)img * a.hw * C;
   const int n8 = a.hw * C / 8;
-  for (int i = threadIdx.x; i < n8; i += blockDim.x) {
+  for (int i = blockIdx.y * blockDim.x + threadIdx.x; i < n8; i += gridDim.y * blockDim.x) {
     const long o = base + (long)i * 8;
     const int c0 = (i * 8) % C;
     uint4 dz = *reinterpret_cast<const uint4*>(a.dz + o);
@@ -367,8 +378,8 @@ DTF_API int dtf_prep_input(const float* x, bf16_t* y, long npix, int c_in, hipSt
 DTF_API int dtf_weight_prep(const float* state, long s_mstride, const int* table, int nconv, const int* slots,
                             int nslots, bf16_t* wf, bf16_t* wd, long w_mstride, hipStream_t stream) {
   if (nconv <= 0 || nslots <= 0) return 0;
-  hipLaunchKernelGGL(weight_prep_kernel, dim3(nconv, nslots), dim3(256), 0, stream, state, s_mstride, table, slots, wf,
-                     wd, w_mstride);
+  hipLaunchKernelGGL(weight_prep_kernel, dim3(nconv, 16, nslots), dim3(256), 0, stream, state, s_mstride, table, slots,
+                     wf, wd, w_mstride);
   return DTF_CHECK_LAUNCH();
 }
 
@@ -386,7 +397,13 @@ DTF_API int dtf_head_args_size() { return (int)sizeof(HeadArgs); }
 
 DTF_API int dtf_bn_bwd_apply(const BnBwdArgs* a, hipStream_t stream) {
   if (a->nimg <= 0) return 0;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((unsigned)a->nimg), dim3(256), 0, stream, *a);
+  // split every image over several workgroups when the population batch is small (>= ~2048 WGs in flight)
+  const int n8 = a->hw * a->C / 8;
+  int split = (int)((2048 + a->nimg - 1) / a->nimg);
+  const int max_split = (n8 + 255) / 256;
+  if (split > max_split) split = max_split;
+  if (split < 1) split = 1;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((unsigned)a->nimg, split), dim3(256), 0, stream, *a);
   return DTF_CHECK_LAUNCH();
 }
 

@@ -38,6 +38,7 @@ def parse():
     p.add_argument("--model", default="resnet", choices=["resnet", "mnist"],
                    help="resnet = headline CIFAR-10 ResNet (BASELINE configs 3/4); mnist = BASELINE config 2")
     p.add_argument("--resnet_size", type=int, default=56)
+    p.add_argument("--resnet_version", type=int, default=2, choices=[1, 2])
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     p.add_argument("--exploit_every", type=int, default=25)
     p.add_argument("--seed", type=int, default=2024)
@@ -72,7 +73,8 @@ def main():
                                     use_synthetic_data=True, checkpoint_every_round=False)
     else:
         make = lambda i: Cifar10Model(begin + i, hps[begin + i], "/tmp/bench_savedata_%d/model_" % rank,  # noqa: E731
-                                      seed=args.seed, resnet_size=args.resnet_size, device=dev, backend=args.backend,
+                                      seed=args.seed, resnet_size=args.resnet_size, resnet_version=args.resnet_version,
+                                      device=dev, backend=args.backend,
                                       capacity=max(1, cnt), use_synthetic_data=True, checkpoint_every_round=False)
     members = [make(i) for i in range(cnt)]
     eng = members[0].engine
@@ -133,7 +135,7 @@ def main():
     value = images / dt_max
     if rank == 0:
         flops = members[0].arch.flops_per_image() * 3.0 * images / dt_max
-        metric = BASELINE_METRIC if args.model == "resnet" and args.resnet_size == 56 else \
+        metric = BASELINE_METRIC if args.model == "resnet" and args.resnet_size == 56 and args.resnet_version == 2 else \
             "images/sec (whole node) %s PBT pop=%d" % (members[0].arch.name, args.pop)
         out = {
             "metric": metric,
@@ -149,7 +151,8 @@ def main():
             "dtype": "bf16",
             "data": "synthetic (device-resident random-normal %s, uniform labels), random-init weights"
                     % ("32x32x3" if args.model == "resnet" else "28x28x1"),
-            "config": {"model": ("resnet%d_v2_cifar10" % args.resnet_size) if args.model == "resnet" else "mnist_cnn", "global_batch": args.pop * args.batch,
+            "config": {"model": ("resnet%d_v%d_cifar10" % (args.resnet_size, args.resnet_version)) if args.model == "resnet"
+                       else "mnist_cnn", "global_batch": args.pop * args.batch,
                        "per_member_batch": args.batch, "population": args.pop, "seq_len": None,
                        "parallelism": "pbt_pop%d_%dmembers_per_gpu" % (args.pop, cnt),
                        "backend": eng.backend.name, "exploit_every": args.exploit_every,

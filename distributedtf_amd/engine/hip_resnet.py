@@ -62,6 +62,16 @@ class BnBwdArgs(ctypes.Structure):
     ]
 
 
+class BnEwArgs(ctypes.Structure):
+    _fields_ = [
+        ("h1", c_void_p), ("h2", c_void_p), ("add", c_void_p), ("out", c_void_p), ("d", c_void_p),
+        ("img_slot", c_void_p), ("params", c_void_p), ("p_mstride", c_long),
+        ("g1", c_int), ("b1", c_int), ("g2", c_int), ("b2", c_int),
+        ("st1", c_void_p), ("st2", c_void_p), ("sb1", c_void_p), ("sb2", c_void_p), ("cnt", c_void_p),
+        ("hw", c_int), ("C", c_int), ("nimg", c_long),
+    ]
+
+
 class HeadArgs(ctypes.Structure):
     _fields_ = [
         ("x", c_void_p), ("labels", c_void_p), ("work", c_void_p), ("params", c_void_p), ("p_mstride", c_long),
@@ -96,6 +106,9 @@ def _register():
     ops.register("dtf_bn_running_update", [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_long, c_void_p,
                                            c_int, c_void_p, c_void_p, c_long, c_void_p])
     ops.register("dtf_bn_bwd_apply", [P(BnBwdArgs), c_void_p])
+    ops.register("dtf_bn_add_relu", [P(BnEwArgs), c_void_p])
+    ops.register("dtf_bn_bwd_reduce", [P(BnEwArgs), c_void_p])
+    ops.register("dtf_bnew_args_size", [])
     ops.register("dtf_head", [P(HeadArgs), c_int, c_void_p])
     ops.register("dtf_head_bwd_apply", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_int,
                                         c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p])
@@ -109,6 +122,7 @@ def _register():
     assert L.dtf_conv_args_size() == ctypes.sizeof(ConvArgs), "ConvArgs ABI mismatch"
     assert L.dtf_bnbwd_args_size() == ctypes.sizeof(BnBwdArgs), "BnBwdArgs ABI mismatch"
     assert L.dtf_head_args_size() == ctypes.sizeof(HeadArgs), "HeadArgs ABI mismatch"
+    assert L.dtf_bnew_args_size() == ctypes.sizeof(BnEwArgs), "BnEwArgs ABI mismatch"
     _REGISTERED = True
 
 
@@ -139,8 +153,8 @@ class _Layout:
     def __init__(self, engine):
         prog = engine.arch.prog
         cfg = prog.cfg
-        if cfg.version != 2 or cfg.bottleneck or cfg.image_size != 32:
-            raise ValueError("HIP ResNet backend supports CIFAR-shape v2 building-block nets")
+        if cfg.version not in (1, 2) or cfg.bottleneck or cfg.image_size != 32:
+            raise ValueError("HIP ResNet backend supports CIFAR-shape v1/v2 building-block nets")
         self.prog = prog
         self.cfg = cfg
         convs = prog.convs
@@ -161,12 +175,19 @@ class _Layout:
         # spatial size of each BN's input
         self.bn_hw = {}
         hw = cfg.image_size
+        if cfg.version == 1:
+            self.bn_hw[prog.stem_bn] = hw * hw
         for blk in prog.blocks:
-            self.bn_hw[blk.bns[0]] = hw * hw
             hw_out = hw // blk.stride
-            self.bn_hw[blk.bns[1]] = hw_out * hw_out
+            if cfg.version == 2:
+                self.bn_hw[blk.bns[0]] = hw * hw
+                self.bn_hw[blk.bns[1]] = hw_out * hw_out
+            else:  # v1: every BN follows a conv at the block-output resolution
+                for b in blk.bns + ([blk.proj_bn] if blk.proj_bn is not None else []):
+                    self.bn_hw[b] = hw_out * hw_out
             hw = hw_out
-        self.bn_hw[prog.final_bn] = hw * hw
+        if cfg.version == 2:
+            self.bn_hw[prog.final_bn] = hw * hw
         self.final_hw = hw * hw
         self.bn_table = [[b.run_off, b.c, self.bn_hw[b.idx], b.idx, b.gamma_off, b.beta_off, 0, 0] for b in prog.bns]
 
@@ -328,8 +349,11 @@ class _StepPlan:
         if src is not None:
             self.idx = torch.zeros(N, dtype=torch.long, device=dev)
             self.rng = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.v1 = cfg.version == 1
         # forward activations saved for backward
         self.xs, self.hs, self.scs = [], [], []
+        self.hb = []  # v1: conv_b outputs (pre-BN); hs = conv_a outputs, scs = projection outputs (pre-BN)
+        self.h0 = torch.empty(N, H, H, cfg.num_filters, dtype=torch.bfloat16, device=dev) if self.v1 else None
         hw, c = H, cfg.num_filters
         self.xs.append(torch.empty(N, hw, hw, c, dtype=torch.bfloat16, device=dev))
         for blk in prog.blocks:
@@ -339,6 +363,8 @@ class _StepPlan:
             self.scs.append(torch.empty(N, hw_o, hw_o, ca.cout, dtype=torch.bfloat16, device=dev)
                             if blk.proj is not None else None)
             self.xs.append(torch.empty(N, hw_o, hw_o, ca.cout, dtype=torch.bfloat16, device=dev))
+            if self.v1:
+                self.hb.append(torch.empty(N, hw_o, hw_o, ca.cout, dtype=torch.bfloat16, device=dev))
             hw = hw_o
         # backward temporaries, one set per resolution
         self.tmp = {}
@@ -545,7 +571,7 @@ class _StepPlan:
         self._add(lib.dtf_conv_wgrad, ctypes.byref(a), cin, c.cout, c.stride, c.k, mode_x, mode_dy, work.shape[0], lds)
         self._keep(a)
 
-    def _conv_bwd_fused(self, ci, dy, dz_out, x, mode_dy, dy2=None, dy_bn=None, x_bn=None, res=None):
+    def _conv_bwd_fused(self, ci, dy, dz_out, x, mode_dy, dy2=None, dy_bn=None, x_bn=None, res=None, ident_x=False):
         """dgrad + wgrad of a stride-1 3x3 C->C conv in one launch (see conv_bwd_fused_kernel)."""
         be, L = self.be, self.be.L
         c = L.prog.convs[ci]
@@ -569,9 +595,10 @@ class _StepPlan:
         if dy_bn is not None:
             a.in_gamma, a.in_beta = self._bn(dy_bn)
             a.st_in, a.st_in_b = _p(be.st_f(dy_bn)), _p(be.st_b(dy_bn))
-        a.ep_gamma, a.ep_beta = self._bn(x_bn)
-        a.st_ep = _p(be.st_f(x_bn))
-        a.st_out = _p(be.st_b(x_bn))
+        if not ident_x:
+            a.ep_gamma, a.ep_beta = self._bn(x_bn)
+            a.st_ep = _p(be.st_f(x_bn))
+            a.st_out = _p(be.st_b(x_bn))
         a.Hi, a.Wi, a.Ho, a.Wo, a.rows = H, H, H, H, rows
         tsz = ((rows + 2) * (H + 2) * (C + 8) + 63) // 64 * 64
         lds = 2304 + 4 * tsz * 2
@@ -581,7 +608,8 @@ class _StepPlan:
         if slab:
             # side-stream reductions run concurrently with later layers: every layer needs its own slab region
             a.slab = _p(self._layer_slab(work.shape[0] * self._slab_elems(C)) if side else self._slab(self._slab_floats()))
-        self._add(lib.dtf_conv_bwd_fused, ctypes.byref(a), C, mode_dy, int(res is not None), work.shape[0], lds)
+        epi = int(res is not None) | (2 if ident_x else 0)
+        self._add(lib.dtf_conv_bwd_fused, ctypes.byref(a), C, mode_dy, epi, work.shape[0], lds)
         self._keep(a)
         if slab:
             red = self._slab_table(work)
@@ -643,6 +671,8 @@ class _StepPlan:
         self._keepalive.append(obj)
 
     def _build(self):
+        if self.v1:
+            return self._build_v1()
         be, e, L = self.be, self.e, self.be.L
         prog, cfg = L.prog, L.cfg
         lib = ops.lib()
@@ -741,6 +771,120 @@ class _StepPlan:
         self._add(lib.dtf_bn_running_update, _p(e.state), e.S, 3 * e.Pp, _p(be.bn_table_t), len(L.bn_table),
                   _p(be.stats[1]), be.stats_bn_stride, _p(self.slots_t), nslots, _p(self.cnt), _p(e.grads), e.Pp)
         # optimizer over every member row (+ zero grads), step counters
+        self._add("optim", None)
+        self._add("step", None)
+
+    def _bn_ew(self, fn, n_hw_c, bn1, h1, bn2=None, h2=None, add=None, out=None, d=None):
+        """bn_add_relu (forward, out=...) or bn_bwd_reduce (backward, d=...) of a v1 block / the v1 stem."""
+        be, e = self.be, self.e
+        hw, C = n_hw_c
+        a = BnEwArgs()
+        a.h1, a.h2, a.add, a.out, a.d = _p(h1), _p(h2), _p(add), _p(out), _p(d)
+        a.img_slot, a.params, a.p_mstride = _p(self.img_slot), _p(e.state), e.S
+        a.g1, a.b1 = self._bn(bn1)
+        a.st1, a.sb1 = _p(be.st_f(bn1)), _p(be.st_b(bn1))
+        if bn2 is not None:
+            a.g2, a.b2 = self._bn(bn2)
+            a.st2, a.sb2 = _p(be.st_f(bn2)), _p(be.st_b(bn2))
+        a.cnt, a.hw, a.C, a.nimg = _p(self.cnt), hw, C, self.N
+        self._keep(a)
+        self._add(fn, ctypes.byref(a))
+
+    def _build_v1(self):
+        """ResNet v1 (``_building_block_v1``, resnet_model.py:127-168): conv -> BN -> ReLU -> conv -> BN
+        (+ shortcut [projection conv -> BN]) -> ReLU; stem conv -> BN -> ReLU; no final BN.
+
+        Forward: convs read the post-ReLU block input directly (identity prologue) and reduce their own BN
+        statistics; conv_b applies BN_a+ReLU on load; ``bn_add_relu`` materialises the block output.
+        Backward: ``d`` = dL/d(pre-ReLU sum) arrives already masked (head / previous conv_a epilogue);
+        ``bn_bwd_reduce`` takes BN_b's (and BN_p's) reductions; conv_b runs the fused dgrad+wgrad with the
+        BN_b-backward transform on load and the BN_a mask + reductions in the epilogue; conv_a adds the shortcut
+        gradient and masks by the block input (> 0), which yields the previous block's ``d``.
+        """
+        be, e, L = self.be, self.e, self.be.L
+        prog, cfg = L.prog, L.cfg
+        lib = ops.lib()
+        N = self.N
+        nslots = len(self.slots)
+        H = cfg.image_size
+        self._add(lib.dtf_weight_prep, _p(e.state), e.S, _p(be.conv_table_t), len(L.conv_table), _p(self.slots_t),
+                  nslots, _p(be.wf), _p(be.wd), L.wtot)
+        self._add("zero", be.stats)
+        self._add("zero", be.loss)
+        self._add("zero", be.correct)
+        if self.src is not None:
+            self._add("augment", None)
+        else:
+            self._add(lib.dtf_prep_input, _p(self.x_in), _p(self.xin16), N * H * H, 3)
+        # ---------------- forward
+        self._conv_fwd(prog.stem, self.xin16, self.h0, stats_bn=prog.stem_bn, in_bn=None)
+        self._bn_ew(lib.dtf_bn_add_relu, (H * H, cfg.num_filters), prog.stem_bn, self.h0, out=self.xs[0])
+        for i, blk in enumerate(prog.blocks):
+            bna, bnb = blk.bns
+            x, ha, hb, y = self.xs[i], self.hs[i], self.hb[i], self.xs[i + 1]
+            if blk.proj is not None:
+                self._conv_fwd(blk.proj, x, self.scs[i], stats_bn=blk.proj_bn, in_bn=None)
+            self._conv_fwd(blk.convs[0], x, ha, stats_bn=bna, in_bn=None)
+            self._conv_fwd(blk.convs[1], ha, hb, stats_bn=bnb, in_bn=bna)
+            hw_o = y.shape[1] * y.shape[2]
+            if blk.proj is not None:
+                self._bn_ew(lib.dtf_bn_add_relu, (hw_o, y.shape[3]), bnb, hb, bn2=blk.proj_bn, h2=self.scs[i], out=y)
+            else:
+                self._bn_ew(lib.dtf_bn_add_relu, (hw_o, y.shape[3]), bnb, hb, add=x, out=y)
+        # head: GAP + dense + CE on the last block output (no final BN: gamma_off = -1)
+        hw = L.final_hw
+        hwork = self._work_member(target_items=512)
+        ha_ = HeadArgs()
+        ha_.x, ha_.labels, ha_.work = _p(self.xs[-1]), _p(self.labels), _p(hwork)
+        ha_.params, ha_.p_mstride = _p(e.state), e.S
+        ha_.gamma_off, ha_.beta_off = -1, -1
+        ha_.dw_off, ha_.db_off = prog.dense_w_off, prog.dense_b_off
+        ha_.grads, ha_.g_mstride = _p(e.grads), e.Pp
+        ha_.st_f, ha_.st_b, ha_.cnt = _p(be.stats), _p(be.stats), _p(self.cnt)
+        ha_.dfeat, ha_.loss, ha_.correct = _p(self.dfeat), _p(be.loss), _p(be.correct)
+        ha_.logits_out = None
+        ha_.hw, ha_.C, ha_.ncls, ha_.train = hw, cfg.final_size, cfg.num_classes, 1
+        self._keep(ha_)
+        self._add(lib.dtf_head, ctypes.byref(ha_), hwork.shape[0])
+        self._add(lib.dtf_bn_running_update, _p(e.state), e.S, 3 * e.Pp, _p(be.bn_table_t), len(L.bn_table),
+                  _p(be.stats[0]), be.stats_bn_stride, _p(self.slots_t), nslots, _p(self.cnt), None, 0)
+        # ---------------- backward
+        hwL = self.xs[-1].shape[1]
+        d = self.tmp[hwL]["g"][0]
+        self._add(lib.dtf_head_bwd_apply, _p(self.xs[-1]), _p(self.dfeat), _p(d), _p(self.img_slot), _p(e.state),
+                  e.S, -1, -1, _p(be.stats), _p(be.stats), _p(self.cnt), hw, cfg.final_size, N)
+        for i in range(len(prog.blocks) - 1, -1, -1):
+            blk = prog.blocks[i]
+            bna, bnb = blk.bns
+            ca, cb = blk.convs
+            x, ha, hb = self.xs[i], self.hs[i], self.hb[i]
+            Hi, Ho = x.shape[1], ha.shape[1]
+            T, Tin = self.tmp[Ho], self.tmp[Hi]
+            hp = self.scs[i]
+            self._bn_ew(lib.dtf_bn_bwd_reduce, (Ho * Ho, ha.shape[3]), bnb, hb,
+                        bn2=blk.proj_bn if hp is not None else None, h2=hp, d=d)
+            # conv_b: dy = BN_b-backward(d, hb); dz_a = dgrad masked by BN_a(ha) + BN_a reductions; dW_b
+            self._conv_bwd_fused(cb, d, T["dz2"], ha, mode_dy=2, dy2=hb, dy_bn=bnb, x_bn=bna)
+            res = d
+            if hp is not None:
+                res = self.pd[id(blk)]
+                self._conv_dgrad(blk.proj, d, res, Hi, mode=2, epi=0, dy2=hp, in_bn=blk.proj_bn)
+                self._conv_wgrad(blk.proj, x, d, mode_x=0, mode_dy=2, dy_bn=blk.proj_bn, dy2=hp)
+            # conv_a: dy = BN_a-backward(dz_a, ha); + shortcut grad; mask by x > 0 -> previous block's d
+            d_next = Tin["g"][1] if d is Tin["g"][0] else Tin["g"][0]
+            ca_spec = prog.convs[ca]
+            if ca_spec.stride == 1 and ca_spec.cin == ca_spec.cout:
+                self._conv_bwd_fused(ca, T["dz2"], d_next, x, mode_dy=2, dy2=ha, dy_bn=bna, res=res, ident_x=True)
+            else:
+                self._conv_dgrad(ca, T["dz2"], d_next, Hi, mode=2, epi=1 | 4, dy2=ha, in_bn=bna, res=res, xm=x)
+                self._conv_wgrad(ca, x, T["dz2"], mode_x=0, mode_dy=2, dy_bn=bna, dy2=ha)
+            d = d_next
+        # stem: BN_stem reductions of d (= dL/d relu-input of the stem), then wgrad with BN_stem-backward on load
+        self._bn_ew(lib.dtf_bn_bwd_reduce, (H * H, cfg.num_filters), prog.stem_bn, self.h0, d=d)
+        self._conv_wgrad(prog.stem, self.xin16, d, mode_x=0, mode_dy=2, dy_bn=prog.stem_bn, dy2=self.h0,
+                         cin_real=cfg.in_channels)
+        self._add(lib.dtf_bn_running_update, _p(e.state), e.S, 3 * e.Pp, _p(be.bn_table_t), len(L.bn_table),
+                  _p(be.stats[1]), be.stats_bn_stride, _p(self.slots_t), nslots, _p(self.cnt), _p(e.grads), e.Pp)
         self._add("optim", None)
         self._add("step", None)
 

@@ -426,8 +426,8 @@ class ResNetArch:
         self.n_reg = self.prog.n_reg
         self.num_classes = cfg.num_classes
         self.input_shape = (cfg.image_size, cfg.image_size, cfg.in_channels)
-        # population-batched HIP kernels cover the CIFAR-shape building-block nets
-        self.hip_supported = (cfg.image_size == 32 and not cfg.bottleneck and cfg.version == 2)
+        # population-batched HIP kernels cover the CIFAR-shape building-block nets (v1 and v2)
+        self.hip_supported = (cfg.image_size == 32 and not cfg.bottleneck and cfg.version in (1, 2))
 
     @property
     def name(self):

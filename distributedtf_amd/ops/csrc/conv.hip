@@ -701,6 +701,8 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
 
 template <int CI, int CO, int S, int K, int MODE_IN, int EPI>
 __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
+  // EPI bit2 (ResNet v1): the masking activation is an identity-BN ReLU output -> mask by xm > 0, no stats
+  constexpr bool MASK = (EPI & 6) != 0, IDENT = (EPI & 4) != 0, STATS = (EPI & 2) != 0 && !IDENT;
   constexpr int NT = CI / 16;
   constexpr int WPT = 4 / NT;
   constexpr int KTOT = K * K * CO;
@@ -717,13 +719,14 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // dy lives at the forward-output resolution; the BN transformed on load is the one after this conv.
   make_coef<CO, MODE_IN>(coef, a, slot, a.cnt[slot] * (float)(a.Ho * a.Wo), a.st_in, a.st_in_b, a.in_gamma, a.in_beta);
-  if constexpr (EPI & 2) {
+  if constexpr (MASK) {
     const int c = threadIdx.x;
     if (c < CI) {
       const float* prow = a.params + (long)slot * a.p_mstride;
-      float scale, shift, mean, inv;
-      bn_fwd_coef(stats_row(a.st_ep, slot), a.cnt[slot] * (float)(a.Hi * a.Wi), prow[a.ep_gamma + c],
-                  prow[a.ep_beta + c], c, scale, shift, mean, inv);
+      float scale = 1.f, shift = 0.f, mean = 0.f, inv = 1.f;
+      if constexpr (!IDENT)
+        bn_fwd_coef(stats_row(a.st_ep, slot), a.cnt[slot] * (float)(a.Hi * a.Wi), prow[a.ep_gamma + c],
+                    prow[a.ep_beta + c], c, scale, shift, mean, inv);
       ecoef[c] = scale;
       ecoef[64 + c] = shift;
       ecoef[128 + c] = mean;
@@ -789,7 +792,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
       const int p = t * 16 + (lane & 15);
       const long o = (((long)img * a.Hi + iy0 + p / a.Wi) * a.Wi + p % a.Wi) * CI + ct * 16 + (lane >> 4) * 4;
       if constexpr (EPI & 1) rres[i] = *reinterpret_cast<const uint2*>(a.res + o);
-      if constexpr (EPI & 2) xres[i] = *reinterpret_cast<const uint2*>(a.xm + o);
+      if constexpr (MASK) xres[i] = *reinterpret_cast<const uint2*>(a.xm + o);
     }
     if (more) tile_load<CO, MODE_IN, 4>(rg, td, a.x + nimg_ * img_elems, nx2, dy_lo(niy0), a.Ho, a.Wo);
     const bf16_t* tile = TILEBUF(k);
@@ -804,7 +807,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
       const long o = (((long)img * a.Hi + iy) * a.Wi + ix) * CI + ci0;
       uint2 rr = make_uint2(0, 0), xr = make_uint2(0, 0);
       if constexpr (EPI & 1) rr = rres[i];
-      if constexpr (EPI & 2) xr = xres[i];
+      if constexpr (MASK) xr = xres[i];
       // stride 1: dy(iy+P-ky, ix+P-kx) lives at tile row iy+P-oy_lo-ky, col ix+P+1-kx
       const bf16_t* tb = tile + ((iy + P - oy_lo) * wp + ix + P + 1) * cpad<CO>();
 #pragma unroll
@@ -838,7 +841,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
         v[3] += bf2f((bf16_t)(rr.y >> 16));
       }
       float xv[4] = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (EPI & 2) {
+      if constexpr (MASK) {
         xv[0] = bf2f((bf16_t)(xr.x & 0xffff));
         xv[1] = bf2f((bf16_t)(xr.x >> 16));
         xv[2] = bf2f((bf16_t)(xr.y & 0xffff));
@@ -854,7 +857,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
       pk.x = pack2bf(v[0], v[1]);
       pk.y = pack2bf(v[2], v[3]);
       *reinterpret_cast<uint2*>(a.y + o) = pk;
-      if constexpr (EPI & 2) {
+      if constexpr (STATS) {
         const float dz[4] = {bf2f((bf16_t)(pk.x & 0xffff)), bf2f((bf16_t)(pk.x >> 16)), bf2f((bf16_t)(pk.y & 0xffff)),
                              bf2f((bf16_t)(pk.y >> 16))};
 #pragma unroll
@@ -870,7 +873,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
                                  coef);
     __syncthreads();
   }
-  if constexpr (EPI & 2) {
+  if constexpr (STATS) {
     reduce_stats_to_lds(acc_lds, ssum, ssq, ct * 16 + (lane >> 4) * 4, lane);
     __syncthreads();
     flush_stats(a.st_out, acc_lds, slot, CI);
@@ -1098,9 +1101,10 @@ __global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
     const int c = threadIdx.x;
     if (c < C) {
       const float* prow = a.params + (long)slot * a.p_mstride;
-      float scale, shift, mean, inv;
-      bn_fwd_coef(stats_row(a.st_ep, slot), n_hw, prow[a.ep_gamma + c], prow[a.ep_beta + c], c, scale, shift, mean,
-                  inv);
+      float scale = 1.f, shift = 0.f, mean = 0.f, inv = 1.f;  // EPI bit1: identity BN (v1 block input)
+      if constexpr (!(EPI & 2))
+        bn_fwd_coef(stats_row(a.st_ep, slot), n_hw, prow[a.ep_gamma + c], prow[a.ep_beta + c], c, scale, shift,
+                    mean, inv);
       ecoef[c] = scale;
       ecoef[64 + c] = shift;
       ecoef[128 + c] = -mean * inv;
@@ -1237,7 +1241,7 @@ __global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
     reduce_stats_to_lds(acc_lds, s4, q4, ci0, lane);
   }
   __syncthreads();
-  flush_stats(a.st_out, acc_lds, slot, C);
+  if constexpr (!(EPI & 2)) flush_stats(a.st_out, acc_lds, slot, C);
   if (a.slab) {
     // coalesced partial-sum slab [wg][j][m][r][256 threads]; dw_slab_reduce_kernel sums a member's slabs
     float* sb = a.slab + (long)blockIdx.x * (NJ * MT * 4 * 256) + threadIdx.x;
@@ -1330,7 +1334,9 @@ DTF_API int dtf_conv_fwd_s1(const ConvArgs* args, int c, int mode, int resid, in
                             hipStream_t stream) {
 #define S1_CASE(CC, M, R) \
   if (c == CC && mode == M && resid == R) return launch(conv_fwd_s1_kernel<CC, M, R>, nblocks, lds, stream, *args);
-  S1_CASE(16, 0, false)  // stem (input padded to 16 channels)
+  S1_CASE(16, 0, false)  // stem (input padded to 16 channels); v1 conv_a (identity input)
+  S1_CASE(32, 0, false)
+  S1_CASE(64, 0, false)
   S1_CASE(16, 1, false)
   S1_CASE(16, 1, true)
   S1_CASE(32, 1, false)
@@ -1377,6 +1383,14 @@ DTF_API int dtf_conv_fwd(const ConvArgs* args, int cin, int cout, int s, int k, 
   FWD_CASE(16, 16, 1, 1, 1, false, false)
   FWD_CASE(16, 32, 2, 1, 1, false, false)
   FWD_CASE(32, 64, 2, 1, 1, false, false)
+  // ResNet v1: convs read the (post-ReLU) block input directly and feed a BN (stats)
+  FWD_CASE(16, 32, 2, 3, 0, false, true)
+  FWD_CASE(32, 64, 2, 3, 0, false, true)
+  FWD_CASE(16, 16, 1, 1, 0, false, true)
+  FWD_CASE(16, 32, 2, 1, 0, false, true)
+  FWD_CASE(32, 64, 2, 1, 0, false, true)
+  FWD_CASE(32, 32, 1, 3, 0, false, true)
+  FWD_CASE(64, 64, 1, 3, 0, false, true)
   return -1;
 }
 
@@ -1397,6 +1411,16 @@ DTF_API int dtf_conv_dgrad(const ConvArgs* args, int cin, int cout, int s, int k
   DGRAD_CASE(16, 16, 1, 1, 0, 0)
   DGRAD_CASE(16, 32, 2, 1, 0, 0)
   DGRAD_CASE(32, 64, 2, 1, 0, 0)
+  // ResNet v1: projection dgrad of BN_p-backward(dpre, hp); conv_a with identity mask (+ shortcut grad)
+  DGRAD_CASE(16, 16, 1, 1, 2, 0)
+  DGRAD_CASE(16, 32, 2, 1, 2, 0)
+  DGRAD_CASE(32, 64, 2, 1, 2, 0)
+  DGRAD_CASE(16, 32, 2, 3, 2, 5)
+  DGRAD_CASE(32, 64, 2, 3, 2, 5)
+  DGRAD_CASE(16, 16, 1, 3, 2, 5)
+  DGRAD_CASE(16, 16, 1, 3, 2, 4)
+  DGRAD_CASE(32, 32, 1, 3, 2, 4)
+  DGRAD_CASE(64, 64, 1, 3, 2, 4)
   return -1;
 }
 
@@ -1413,6 +1437,9 @@ DTF_API int dtf_conv_bwd_fused(const ConvArgs* args, int c, int mode_dy, int epi
   FUSED_CASE(32, 2, 0)
   FUSED_CASE(64, 2, 0)
   FUSED_CASE(16, 2, 1)  // conv_a of the first block (+ stride-1 projection dgrad)
+  FUSED_CASE(16, 2, 3)  // v1 conv_a: identity-BN block input (+ shortcut grad)
+  FUSED_CASE(32, 2, 3)
+  FUSED_CASE(64, 2, 3)
   return -1;
 }
 
@@ -1430,5 +1457,14 @@ DTF_API int dtf_conv_wgrad(const ConvArgs* args, int cin, int cout, int s, int k
   WGRAD_CASE(16, 16, 1, 1, 1, 0)  // projections: x = BN1+ReLU(block input), dy = residual grad
   WGRAD_CASE(16, 32, 2, 1, 1, 0)
   WGRAD_CASE(32, 64, 2, 1, 1, 0)
+  // ResNet v1: x = block input (identity), dy = BN-backward(dpre, h) (stem, projections, conv_a)
+  WGRAD_CASE(16, 16, 1, 3, 0, 2)
+  WGRAD_CASE(16, 16, 1, 1, 0, 2)
+  WGRAD_CASE(16, 32, 2, 1, 0, 2)
+  WGRAD_CASE(32, 64, 2, 1, 0, 2)
+  WGRAD_CASE(16, 32, 2, 3, 0, 2)
+  WGRAD_CASE(32, 64, 2, 3, 0, 2)
+  WGRAD_CASE(32, 32, 1, 3, 0, 2)
+  WGRAD_CASE(64, 64, 1, 3, 0, 2)
   return -1;
 }

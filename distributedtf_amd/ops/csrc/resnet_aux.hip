@@ -218,16 +218,23 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   const float* prow = a.params + (long)slot * a.p_mstride;
   const float bsz = a.cnt[slot];
   if (threadIdx.x < 64) {
-    float s, q;
-    stats_sum(a.st_f + (long)slot * NREP * 128, c, s, q);
-    const float n = bsz * (float)a.hw;
-    const float mean = s / n;
-    const float var = fmaxf(q / n - mean * mean, 0.f);
-    const float inv = rsqrtf(var + BN_EPS);
-    sc[c] = prow[a.gamma_off + c] * inv;
-    sh[c] = prow[a.beta_off + c] - mean * sc[c];
-    mu[c] = mean;
-    iv[c] = inv;
+    if (a.gamma_off < 0) {  // ResNet v1: no final BN (input is the last block's ReLU output)
+      sc[c] = 1.f;
+      sh[c] = 0.f;
+      mu[c] = 0.f;
+      iv[c] = 1.f;
+    } else {
+      float s, q;
+      stats_sum(a.st_f + (long)slot * NREP * 128, c, s, q);
+      const float n = bsz * (float)a.hw;
+      const float mean = s / n;
+      const float var = fmaxf(q / n - mean * mean, 0.f);
+      const float inv = rsqrtf(var + BN_EPS);
+      sc[c] = prow[a.gamma_off + c] * inv;
+      sh[c] = prow[a.beta_off + c] - mean * sc[c];
+      mu[c] = mean;
+      iv[c] = inv;
+    }
   }
   __syncthreads();
   const int ncls = a.ncls;
@@ -314,11 +321,13 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
     atomicAdd(&a.correct[slot], cw);
   }
   if (a.train && wave == 0) {
-    const float v0 = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
-    const float v1 = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
-    float* row = a.st_b + (long)slot * NREP * 128 + (blockIdx.x & (NREP - 1)) * 128;
-    atomicAdd(&row[c], v0);
-    atomicAdd(&row[64 + c], v1);
+    if (a.gamma_off >= 0) {
+      const float v0 = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+      const float v1 = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+      float* row = a.st_b + (long)slot * NREP * 128 + (blockIdx.x & (NREP - 1)) * 128;
+      atomicAdd(&row[c], v0);
+      atomicAdd(&row[64 + c], v1);
+    }
     float* g = a.grads + (long)slot * a.g_mstride;
     for (int j = 0; j < ncls; ++j)
       atomicAdd(&g[a.dw_off + j * a.C + c], dwl[0][j][c] + dwl[1][j][c] + dwl[2][j][c] + dwl[3][j][c]);
@@ -337,7 +346,13 @@ __global__ __launch_bounds__(256) void head_bwd_apply_kernel(const bf16_t* __res
   const int img = blockIdx.x;
   const int slot = img_slot[img];
   const int c = threadIdx.x;
-  if (c < C) {
+  if (c < C && gamma_off < 0) {  // v1: identity -> g = dfeat * [x > 0] (the last block's ReLU backward)
+    co[c] = 1.f;
+    co[64 + c] = 0.f;
+    co[128 + c] = 0.f;
+    co[192 + c] = 1.f;
+    co[256 + c] = 0.f;
+  } else if (c < C) {
     const float* prow = params + (long)slot * p_mstride;
     const float n = cnt[slot] * (float)hw;
     float s, q;
@@ -363,6 +378,165 @@ __global__ __launch_bounds__(256) void head_bwd_apply_kernel(const bf16_t* __res
     const float xv = bf2f(x[base + i]);
     const float dz = (xv * co[192 + cc] + co[256 + cc] > 0.f) ? df[cc] : 0.f;
     out[base + i] = f2bf(co[cc] * dz + co[64 + cc] * xv + co[128 + cc]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------- ResNet v1
+// BN-apply + residual + ReLU of a v1 block output (also the stem: no addend):
+//   out = relu(BN1(h1) + [BN2(h2) | add | 0])
+struct BnEwArgs {
+  const bf16_t* h1;
+  const bf16_t* h2;
+  const bf16_t* add;
+  bf16_t* out;
+  const bf16_t* d;    // bn_bwd_reduce: gradient w.r.t. the BN outputs (post-ReLU-mask)
+  const int* img_slot;
+  const float* params;
+  long p_mstride;
+  int g1, b1, g2, b2;
+  const float* st1;   // forward stats of BN1 / BN2
+  const float* st2;
+  float* sb1;         // backward reductions of BN1 / BN2 (out)
+  float* sb2;
+  const float* cnt;
+  int hw, C;
+  long nimg;
+};
+
+__device__ __forceinline__ void fwd_coef2(const float* st, float n, float gamma, float beta, int c, float& scale,
+                                          float& shift, float& mean, float& inv) {
+  float s, q;
+  stats_sum(st, c, s, q);
+  mean = s / n;
+  const float var = fmaxf(q / n - mean * mean, 0.f);
+  inv = rsqrtf(var + BN_EPS);
+  scale = gamma * inv;
+  shift = beta - mean * scale;
+}
+
+__global__ __launch_bounds__(256) void bn_add_relu_kernel(BnEwArgs a) {
+  __shared__ float co[4 * 64];
+  const int img = blockIdx.x;
+  const int slot = a.img_slot[img];
+  const int C = a.C;
+  if (threadIdx.x < C) {
+    const int c = threadIdx.x;
+    const float* prow = a.params + (long)slot * a.p_mstride;
+    const float n = a.cnt[slot] * (float)a.hw;
+    float sc, sh, mean, inv;
+    fwd_coef2(a.st1 + (long)slot * NREP * 128, n, prow[a.g1 + c], prow[a.b1 + c], c, sc, sh, mean, inv);
+    co[c] = sc;
+    co[64 + c] = sh;
+    if (a.h2) {
+      fwd_coef2(a.st2 + (long)slot * NREP * 128, n, prow[a.g2 + c], prow[a.b2 + c], c, sc, sh, mean, inv);
+      co[128 + c] = sc;
+      co[192 + c] = sh;
+    }
+  }
+  __syncthreads();
+  const long base = (long)img * a.hw * C;
+  const int n8 = a.hw * C / 8;
+  for (int i = blockIdx.y * blockDim.x + threadIdx.x; i < n8; i += gridDim.y * blockDim.x) {
+    const long o = base + (long)i * 8;
+    const int c0 = (i * 8) % C;
+    const uint4 hv = *reinterpret_cast<const uint4*>(a.h1 + o);
+    uint4 av = make_uint4(0, 0, 0, 0);
+    if (a.h2) av = *reinterpret_cast<const uint4*>(a.h2 + o);
+    else if (a.add) av = *reinterpret_cast<const uint4*>(a.add + o);
+    const uint32_t h32[4] = {hv.x, hv.y, hv.z, hv.w}, a32[4] = {av.x, av.y, av.z, av.w};
+    uint32_t r32[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + 2 * j;
+      float v0 = bf2f((bf16_t)(h32[j] & 0xffff)) * co[c] + co[64 + c];
+      float v1 = bf2f((bf16_t)(h32[j] >> 16)) * co[c + 1] + co[64 + c + 1];
+      const float x0 = bf2f((bf16_t)(a32[j] & 0xffff)), x1 = bf2f((bf16_t)(a32[j] >> 16));
+      if (a.h2) {
+        v0 += x0 * co[128 + c] + co[192 + c];
+        v1 += x1 * co[128 + c + 1] + co[192 + c + 1];
+      } else {
+        v0 += x0;
+        v1 += x1;
+      }
+      r32[j] = pack2bf(fmaxf(v0, 0.f), fmaxf(v1, 0.f));
+    }
+    *reinterpret_cast<uint4*>(a.out + o) = make_uint4(r32[0], r32[1], r32[2], r32[3]);
+  }
+}
+
+// Backward reductions of the BN(s) feeding a v1 block output: sum(d), sum(d * xhat1) [, sum(d * xhat2)], with
+// d = dL/d(pre-ReLU sum) (already masked).  Each thread keeps 8 fixed channels (2048 % C == 0), LDS reduction,
+// one replicated atomic per channel and workgroup.
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnEwArgs a) {
+  __shared__ float co[4 * 64];
+  __shared__ float acc[3 * 64];
+  const int img = blockIdx.x;
+  const int slot = a.img_slot[img];
+  const int C = a.C;
+  if (threadIdx.x < C) {
+    const int c = threadIdx.x;
+    const float* prow = a.params + (long)slot * a.p_mstride;
+    const float n = a.cnt[slot] * (float)a.hw;
+    float sc, sh, mean, inv;
+    fwd_coef2(a.st1 + (long)slot * NREP * 128, n, prow[a.g1 + c], prow[a.b1 + c], c, sc, sh, mean, inv);
+    co[c] = -mean * inv;
+    co[64 + c] = inv;
+    if (a.h2) {
+      fwd_coef2(a.st2 + (long)slot * NREP * 128, n, prow[a.g2 + c], prow[a.b2 + c], c, sc, sh, mean, inv);
+      co[128 + c] = -mean * inv;
+      co[192 + c] = inv;
+    }
+  }
+  if (threadIdx.x < 3 * 64) acc[threadIdx.x] = 0.f;
+  __syncthreads();
+  const long base = (long)img * a.hw * C;
+  const int n8 = a.hw * C / 8;
+  float sd[8], s1[8], s2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sd[k] = s1[k] = s2[k] = 0.f;
+  const int i0 = blockIdx.y * blockDim.x + threadIdx.x;
+  const int c0 = (i0 * 8) % C;
+  for (int i = i0; i < n8; i += gridDim.y * blockDim.x) {
+    const long o = base + (long)i * 8;
+    const uint4 dv = *reinterpret_cast<const uint4*>(a.d + o);
+    const uint4 hv = *reinterpret_cast<const uint4*>(a.h1 + o);
+    uint4 pv = make_uint4(0, 0, 0, 0);
+    if (a.h2) pv = *reinterpret_cast<const uint4*>(a.h2 + o);
+    const uint32_t d32[4] = {dv.x, dv.y, dv.z, dv.w}, h32[4] = {hv.x, hv.y, hv.z, hv.w},
+                   p32[4] = {pv.x, pv.y, pv.z, pv.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = c0 + k;
+      const float dd = bf2f((bf16_t)((d32[k >> 1] >> (16 * (k & 1))) & 0xffff));
+      const float hh = bf2f((bf16_t)((h32[k >> 1] >> (16 * (k & 1))) & 0xffff));
+      sd[k] += dd;
+      s1[k] += dd * (hh * co[64 + c] + co[c]);
+      if (a.h2) {
+        const float pp = bf2f((bf16_t)((p32[k >> 1] >> (16 * (k & 1))) & 0xffff));
+        s2[k] += dd * (pp * co[192 + c] + co[128 + c]);
+      }
+    }
+  }
+  if (i0 < n8) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      atomicAdd(&acc[c0 + k], sd[k]);
+      atomicAdd(&acc[64 + c0 + k], s1[k]);
+      if (a.h2) atomicAdd(&acc[128 + c0 + k], s2[k]);
+    }
+  }
+  __syncthreads();
+  const int rep = (blockIdx.x + blockIdx.y) & (NREP - 1);
+  if (threadIdx.x < C) {
+    const int c = threadIdx.x;
+    float* r1 = a.sb1 + (long)slot * NREP * 128 + rep * 128;
+    atomicAdd(&r1[c], acc[c]);
+    atomicAdd(&r1[64 + c], acc[64 + c]);
+    if (a.h2) {
+      float* r2 = a.sb2 + (long)slot * NREP * 128 + rep * 128;
+      atomicAdd(&r2[c], acc[c]);
+      atomicAdd(&r2[64 + c], acc[128 + c]);
+    }
   }
 }
 
@@ -419,5 +593,27 @@ DTF_API int dtf_head_bwd_apply(const bf16_t* x, const float* dfeat, bf16_t* out,
   if (nimg <= 0) return 0;
   hipLaunchKernelGGL(head_bwd_apply_kernel, dim3(nimg), dim3(256), 0, stream, x, dfeat, out, img_slot, params,
                      p_mstride, gamma_off, beta_off, st_f, st_b, cnt, hw, C);
+  return DTF_CHECK_LAUNCH();
+}
+
+static int ew_split(const BnEwArgs* a) {
+  const int n8 = a->hw * a->C / 8;
+  int split = (int)((2048 + a->nimg - 1) / a->nimg);
+  const int max_split = (n8 + 255) / 256;
+  if (split > max_split) split = max_split;
+  return split < 1 ? 1 : split;
+}
+
+DTF_API int dtf_bnew_args_size() { return (int)sizeof(BnEwArgs); }
+
+DTF_API int dtf_bn_add_relu(const BnEwArgs* a, hipStream_t stream) {
+  if (a->nimg <= 0) return 0;
+  hipLaunchKernelGGL(bn_add_relu_kernel, dim3((unsigned)a->nimg, ew_split(a)), dim3(256), 0, stream, *a);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_bn_bwd_reduce(const BnEwArgs* a, hipStream_t stream) {
+  if (a->nimg <= 0) return 0;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((unsigned)a->nimg, ew_split(a)), dim3(256), 0, stream, *a);
   return DTF_CHECK_LAUNCH();
 }

@@ -31,13 +31,14 @@ def _relerr(a, b):
     return float((a.double() - b.double()).norm() / (b.double().norm() + 1e-30))
 
 
-@pytest.mark.parametrize("size,graph,fused", [(8, "1", "1"), (14, "1", "1"), (14, "0", "1"), (14, "1", "0"),
-                                              (8, "0", "0")])
-def test_hip_step_matches_reference(size, graph, fused, monkeypatch):
+@pytest.mark.parametrize("size,graph,fused,version", [(8, "1", "1", 2), (14, "1", "1", 2), (14, "0", "1", 2),
+                                                      (14, "1", "0", 2), (8, "0", "0", 2),
+                                                      (8, "1", "1", 1), (14, "0", "1", 1), (20, "1", "1", 1)])
+def test_hip_step_matches_reference(size, graph, fused, version, monkeypatch):
     monkeypatch.setenv("DTF_HIP_GRAPH", graph)
     monkeypatch.setenv("DTF_FUSED_BWD", fused)
     torch.manual_seed(0)
-    arch = ResNetArch(cifar_config(size))
+    arch = ResNetArch(cifar_config(size, version=version))
     dev = torch.device("cuda")
     sizes = [8, 12]
     ref = PopulationEngine(arch, 2, dev, backend="torch", compute_dtype=torch.float32, optimizer_impl="hip")

@@ -121,6 +121,10 @@ def main():
 
     for _ in range(args.warmup):
         losses = step()
+    if args.exploit_every and world > 1 and args.warmup > 0:
+        # one untimed exploit cycle: RCCL P2P channels between GPU pairs are set up lazily on first use
+        exploit_cycle(losses)
+        exploits[0] = 0
     barrier_sync()
     t0 = time.perf_counter()
     for k in range(args.steps):

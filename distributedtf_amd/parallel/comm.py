@@ -269,6 +269,12 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0) -
         if backend == "nccl":
             kw["device_id"] = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
         dist.init_process_group(**kw)
+        if backend == "nccl":
+            # create the RCCL communicator now (all ranks), so later P2P batches that involve only some
+            # ranks (exploit copies) never trigger a lazy, partial-world communicator init
+            t = torch.ones(1, device="cuda")
+            dist.all_reduce(t)
+            torch.cuda.synchronize()
     cpu_group = dist.new_group(backend="gloo", timeout=td) if backend != "gloo" else dist.group.WORLD
     try:
         from torch.distributed.distributed_c10d import _get_default_store

@@ -35,16 +35,20 @@ def parse():
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--pop", type=int, default=8)
     p.add_argument("--batch", type=int, default=128)
-    p.add_argument("--model", default="resnet", choices=["resnet", "mnist"],
-                   help="resnet = headline CIFAR-10 ResNet (BASELINE configs 3/4); mnist = BASELINE config 2")
-    p.add_argument("--resnet_size", type=int, default=56)
+    p.add_argument("--model", default="resnet", choices=["resnet", "mnist", "imagenet"],
+                   help="resnet = headline CIFAR-10 ResNet (BASELINE configs 3/4); mnist = config 2; "
+                        "imagenet = ResNet-50 on synthetic 224x224x3 (config 5)")
+    p.add_argument("--resnet_size", type=int, default=None, help="default 56 (CIFAR) / 50 (imagenet)")
     p.add_argument("--resnet_version", type=int, default=2, choices=[1, 2])
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     p.add_argument("--exploit_every", type=int, default=25)
     p.add_argument("--seed", type=int, default=2024)
     p.add_argument("--graph", type=int, default=1, help="capture the population step in a HIP graph")
     p.add_argument("--profile_json", default=None)
-    return p.parse_args()
+    a = p.parse_args()
+    if a.resnet_size is None:
+        a.resnet_size = 50 if a.model == "imagenet" else 56
+    return a
 
 
 def main():
@@ -56,6 +60,7 @@ def main():
     from distributedtf_amd.pbt.exploit import plan_exploit, apply_plan_to_values
     from distributedtf_amd.models.cifar10_model import Cifar10Model
     from distributedtf_amd.models.mnist_model import MNISTModel
+    from distributedtf_amd.models.imagenet_model import ImageNetModel
 
     comm = init_distributed()
     rank, world = comm.Get_rank(), comm.Get_size()
@@ -71,6 +76,10 @@ def main():
         make = lambda i: MNISTModel(begin + i, hps[begin + i], "/tmp/bench_savedata_%d/model_" % rank,  # noqa: E731
                                     seed=args.seed, device=dev, backend=args.backend, capacity=max(1, cnt),
                                     use_synthetic_data=True, checkpoint_every_round=False)
+    elif args.model == "imagenet":
+        make = lambda i: ImageNetModel(begin + i, hps[begin + i], "/tmp/bench_savedata_%d/model_" % rank,  # noqa: E731
+                                       seed=args.seed, resnet_size=args.resnet_size, device=dev, backend=args.backend,
+                                       capacity=max(1, cnt), use_synthetic_data=True, checkpoint_every_round=False)
     else:
         make = lambda i: Cifar10Model(begin + i, hps[begin + i], "/tmp/bench_savedata_%d/model_" % rank,  # noqa: E731
                                       seed=args.seed, resnet_size=args.resnet_size, resnet_version=args.resnet_version,
@@ -154,9 +163,8 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (device-resident random-normal %s, uniform labels), random-init weights"
-                    % ("32x32x3" if args.model == "resnet" else "28x28x1"),
-            "config": {"model": ("resnet%d_v%d_cifar10" % (args.resnet_size, args.resnet_version)) if args.model == "resnet"
-                       else "mnist_cnn", "global_batch": args.pop * args.batch,
+                    % "x".join(str(d) for d in members[0].arch.input_shape),
+            "config": {"model": members[0].arch.name, "global_batch": args.pop * args.batch,
                        "per_member_batch": args.batch, "population": args.pop, "seq_len": None,
                        "parallelism": "pbt_pop%d_%dmembers_per_gpu" % (args.pop, cnt),
                        "backend": eng.backend.name, "exploit_every": args.exploit_every,

@@ -1,0 +1,542 @@
+"""Population-batched ImageNet-shape ResNet (v2 bottleneck) training step on hand-written gfx950 kernels.
+
+Architecture (SURVEY.md C12'; reference block ``_bottleneck_block_v2``, ``resnet/resnet_model.py:267-320``):
+7x7/2 stem (3 -> 64, no BN in v2), 3x3/2 'SAME' max-pool, bottleneck stages [3, 4, 6, 3] with strides
+[1, 2, 2, 2] (BN1+ReLU -> 1x1 -> BN2+ReLU -> 3x3/s -> BN3+ReLU -> 1x1, + shortcut; the first block of a
+stage projects the PRE-ACTIVATED input with a 1x1/s conv), final BN+ReLU, global average pool, dense.
+
+Every conv is one ``convg`` launch (ops/csrc/convg.hip): the producing BN+ReLU is applied while the gathered
+operand is staged (forward), the BN statistics of the output are reduced in the epilogue, and the residual is
+added there.  Backward: the data gradient runs the same kernel on flipped/transposed weights (stride 2:
+transposed gather), with the next BN's backward transform on load and ReLU-mask + BN-backward reductions in
+the epilogue; weight gradients are split-K implicit GEMMs (k = pixels) with atomics into the member's row.
+Per-member BN coefficients (forward scale/shift/mean/inv, backward A/B/C) are finalised by tiny kernels
+between the convs (``convg_aux.hip``), which also update the running statistics / accumulate dgamma, dbeta.
+The dense layer is the grouped bf16 GEMM (gemm.hip) with softmax-CE in between.  The whole step is captured
+into one HIP graph per batch composition.  Eval uses the PyTorch reference forward.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Dict, List
+
+import torch
+
+from .. import ops
+from ..data.datasets import IndexBatch, batch_len
+from .hip_resnet import advance_steps, note_step_advanced, same_batches, upload_hyper
+
+c_void_p, c_int, c_long, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float
+CMAX = 2048
+NPAD_CLS = 1024
+
+
+class CgArgs(ctypes.Structure):
+    _fields_ = [
+        ("x", c_void_p), ("x2", c_void_p), ("dy", c_void_p), ("dy2", c_void_p), ("w", c_void_p),
+        ("w_mstride", c_long), ("w_off", c_long), ("y", c_void_p), ("res", c_void_p), ("xm", c_void_p),
+        ("grads", c_void_p), ("g_mstride", c_long), ("g_off", c_long), ("c_in", c_void_p), ("c_dy", c_void_p),
+        ("c_ep", c_void_p), ("st_out", c_void_p), ("work", c_void_p),
+        ("Hi", c_int), ("Wi", c_int), ("Ci", c_int), ("Ho", c_int), ("Wo", c_int), ("Co", c_int),
+        ("kh", c_int), ("kw", c_int), ("stride", c_int), ("pad", c_int), ("cmax", c_int), ("log2ci", c_int),
+        ("cin_real", c_int),
+    ]
+
+
+class BnFinArgs(ctypes.Structure):
+    _fields_ = [
+        ("state", c_void_p), ("s_mstride", c_long), ("sums", c_void_p), ("coef", c_void_p), ("fcoef", c_void_p),
+        ("grads", c_void_p), ("g_mstride", c_long), ("slots", c_void_p), ("cnt", c_void_p),
+        ("gamma_off", c_int), ("beta_off", c_int), ("run_off", c_int), ("C", c_int), ("hw", c_int), ("cmax", c_int),
+    ]
+
+
+class EwArgs(ctypes.Structure):
+    _fields_ = [("dz", c_void_p), ("h", c_void_p), ("add", c_void_p), ("out", c_void_p), ("coef", c_void_p),
+                ("img_slot", c_void_p), ("hw", c_long), ("C", c_int), ("cmax", c_int), ("nimg", c_long)]
+
+
+class GapArgs(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("coef", c_void_p), ("img_slot", c_void_p), ("feat", c_void_p),
+                ("dfeat", c_void_p), ("sums", c_void_p), ("bcoef", c_void_p), ("out", c_void_p),
+                ("hw", c_int), ("C", c_int), ("cmax", c_int)]
+
+
+_REGISTERED = False
+
+
+def _register():
+    global _REGISTERED
+    if _REGISTERED:
+        return
+    from . import hip_mnist
+    hip_mnist._register()  # grouped GEMM signatures
+    P = ctypes.POINTER
+    reg = ops.register
+    reg("dtf_convg_fwd", [P(CgArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
+    reg("dtf_convg_wgrad", [P(CgArgs), c_int, c_int, c_int, c_void_p])
+    reg("dtf_cg_weight_prep", [c_void_p, c_long, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_long,
+                               c_void_p])
+    reg("dtf_cg_dense_prep", [c_void_p, c_long, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_long,
+                              c_void_p])
+    reg("dtf_cg_bn_final", [P(BnFinArgs), c_int, c_int, c_void_p])
+    reg("dtf_cg_bn_bwd_apply", [P(EwArgs), c_void_p])
+    reg("dtf_cg_prep_input", [c_void_p, c_void_p, c_long, c_int, c_void_p])
+    reg("dtf_cg_maxpool", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                           c_int, c_int, c_void_p])
+    reg("dtf_cg_gap", [P(GapArgs), c_int, c_int, c_void_p])
+    reg("dtf_cg_softmax_ce", [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_long,
+                              c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p])
+    reg("dtf_cg_chan_stats", [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p])
+    for n in ("dtf_cg_args_size", "dtf_bnfin_args_size", "dtf_ew_args_size", "dtf_gap_args_size"):
+        reg(n, [])
+    L = ops.lib()
+    for name, args in ops._SIGNATURES.items():
+        fn = getattr(L, name, None)
+        if fn is not None:
+            fn.argtypes = args
+            fn.restype = c_int
+    for st, fn in ((CgArgs, "dtf_cg_args_size"), (BnFinArgs, "dtf_bnfin_args_size"), (EwArgs, "dtf_ew_args_size"),
+                   (GapArgs, "dtf_gap_args_size")):
+        assert getattr(L, fn)() == ctypes.sizeof(st), "%s ABI mismatch" % st.__name__
+    _REGISTERED = True
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _log2(n):
+    assert n > 0 and n & (n - 1) == 0, n
+    return n.bit_length() - 1
+
+
+class HipImageNetBackend:
+    name = "hip"
+    accepts_index_batches = False
+
+    def __init__(self, engine):
+        _register()
+        self.e = engine
+        self.dev = engine.device
+        prog = engine.arch.prog
+        cfg = prog.cfg
+        if not (cfg.bottleneck and cfg.version == 2 and cfg.first_pool_size == 3 and cfg.first_pool_stride == 2
+                and cfg.kernel_size == 7 and cfg.conv_stride == 2):
+            raise ValueError("HIP ImageNet backend supports the v2 bottleneck ImageNet configuration")
+        if cfg.image_size % 32:
+            raise ValueError("image size must be a multiple of 32")
+        self.prog, self.cfg = prog, cfg
+        cap = engine.capacity
+        # bf16 weights: forward [o][tap][i] (stem input padded 3 -> 8) + flipped/transposed dgrad layout
+        self.fwd_off, self.dgr_off, table = {}, {}, []
+        off = 0
+        for c in prog.convs:
+            cin_pad = 8 if c.idx == prog.stem else c.cin
+            self.fwd_off[c.idx] = off
+            off += c.cout * c.k * c.k * cin_pad
+            if c.idx != prog.stem:
+                self.dgr_off[c.idx] = off
+                off += c.cout * c.k * c.k * c.cin
+            table.append([c.off, c.cout, c.cin, c.k, cin_pad, self.fwd_off[c.idx], self.dgr_off.get(c.idx, -1), 0])
+        self.wtot = (off + 63) // 64 * 64
+        self.w = torch.zeros(cap, self.wtot, dtype=torch.bfloat16, device=self.dev)
+        self.conv_table = torch.tensor(table, dtype=torch.int32, device=self.dev)
+        self.ncls = cfg.num_classes
+        assert self.ncls <= NPAD_CLS and cfg.final_size % 32 == 0
+        self.dense = torch.zeros(cap, NPAD_CLS * cfg.final_size, dtype=torch.bfloat16, device=self.dev)
+        nb = len(prog.bns)
+        self.sums = torch.zeros(2, nb, cap, 2, CMAX, dtype=torch.float32, device=self.dev)   # [fwd|bwd]
+        self.coef = torch.zeros(2, nb, cap, 4, CMAX, dtype=torch.float32, device=self.dev)   # [fwd|bwd]
+        self.loss = torch.zeros(cap, dtype=torch.float32, device=self.dev)
+        self.correct = torch.zeros(cap, dtype=torch.float32, device=self.dev)
+        self._plans: Dict[tuple, "_ImageNetPlan"] = {}
+        self.use_graph = os.environ.get("DTF_HIP_GRAPH", "1") == "1"
+
+    def on_params_changed(self, slots):
+        pass  # weights are re-derived from the fp32 master rows at the start of every step
+
+    def shadow_weights(self):
+        return None
+
+    def plan(self, slots, sizes):
+        key = (tuple(slots), tuple(sizes))
+        p = self._plans.get(key)
+        if p is None:
+            if len(self._plans) > 4:
+                self._plans.clear()
+            p = _ImageNetPlan(self, list(slots), list(sizes))
+            self._plans[key] = p
+        return p
+
+    def train_step(self, slots, batches, hparams, lrs):
+        e = self.e
+        batches = [b.materialize() if isinstance(b, IndexBatch) else b for b in batches]
+        sizes = [batch_len(b) for b in batches]
+        p = self.plan(slots, sizes)
+        upload_hyper(e, slots, hparams, lrs)
+        p.load_batch(batches)
+        p.run()
+        note_step_advanced(e, slots)
+        return self.loss[p.slots_long].clone()
+
+    def forward_backward(self, slots, batches):
+        raise RuntimeError("HipImageNetBackend runs whole steps: use train_step")
+
+    @torch.no_grad()
+    def infer(self, slot, x):
+        e = self.e
+        return e.arch.forward(e.params[slot], e.running[slot], x, training=False, dtype=torch.bfloat16)
+
+
+class _ImageNetPlan:
+    def __init__(self, be: HipImageNetBackend, slots: List[int], sizes: List[int]):
+        self.be, self.e = be, be.e
+        e, dev, prog, cfg = be.e, be.dev, be.prog, be.cfg
+        self.slots, self.sizes = slots, sizes
+        N = sum(sizes)
+        self.N = N
+        img_slot, self.first = [], {}
+        for s, n in zip(slots, sizes):
+            self.first[s] = len(img_slot)
+            img_slot += [s] * n
+        self.img_slot = torch.tensor(img_slot, dtype=torch.int32, device=dev)
+        cnt = torch.zeros(e.capacity, dtype=torch.float32)
+        for s, n in zip(slots, sizes):
+            cnt[s] = float(n)
+        self.cnt = cnt.to(dev)
+        self.slots_t = torch.tensor(slots, dtype=torch.int32, device=dev)
+        self.slots_long = torch.tensor(slots, dtype=torch.long, device=dev)
+        bf = torch.bfloat16
+        H = cfg.image_size
+        self.H = H
+        self.x_in = torch.zeros(N, H, H, cfg.in_channels, dtype=torch.float32, device=dev)
+        self.labels = torch.zeros(N, dtype=torch.int32, device=dev)
+        self.xin8 = torch.zeros(N, H, H, 8, dtype=bf, device=dev)
+        H1 = H // 2
+        H2 = (H1 + 1) // 2
+        self.y0 = torch.empty(N, H1, H1, cfg.num_filters, dtype=bf, device=dev)
+        self.am0 = torch.empty(N, H2, H2, cfg.num_filters, dtype=torch.uint8, device=dev)
+        self.xs, self.h1, self.h2, self.sc = [torch.empty(N, H2, H2, cfg.num_filters, dtype=bf, device=dev)], [], [], []
+        hw, cin = H2, cfg.num_filters
+        self.geo = []  # per block: (H_in, H_out, cin, f, fout)
+        for blk in prog.blocks:
+            c1, c2, c3 = (prog.convs[i] for i in blk.convs)
+            ho = hw // blk.stride
+            self.h1.append(torch.empty(N, hw, hw, c1.cout, dtype=bf, device=dev))
+            self.h2.append(torch.empty(N, ho, ho, c2.cout, dtype=bf, device=dev))
+            self.sc.append(torch.empty(N, ho, ho, c3.cout, dtype=bf, device=dev) if blk.proj is not None else None)
+            self.xs.append(torch.empty(N, ho, ho, c3.cout, dtype=bf, device=dev))
+            self.geo.append((hw, ho, cin, c1.cout, c3.cout))
+            hw, cin = ho, c3.cout
+        self.HL = hw
+        self.feat = torch.empty(N, cfg.final_size, dtype=bf, device=dev)
+        self.logits = torch.empty(N, NPAD_CLS, dtype=torch.float32, device=dev)
+        self.dlog = torch.zeros(N, NPAD_CLS, dtype=bf, device=dev)
+        self.dfeat = torch.empty(N, cfg.final_size, dtype=torch.float32, device=dev)
+        self._tmp: Dict[tuple, torch.Tensor] = {}
+        self._keep = []
+        self.launches = []
+        self._build()
+        self.graph = None
+
+    # ----------------------------------------------------------------------------------------- helpers
+    def tmp(self, name, hw, c):
+        key = (name, hw, c)
+        t = self._tmp.get(key)
+        if t is None:
+            t = torch.empty(self.N, hw, hw, c, dtype=torch.bfloat16, device=self.be.dev)
+            self._tmp[key] = t
+        return t
+
+    def _add(self, fn, *args):
+        self.launches.append((fn, args))
+
+    def _hold(self, obj):
+        self._keep.append(obj)
+        return obj
+
+    def _pix_work(self, hw_out, co, tc):
+        items = []
+        for s, n in zip(self.slots, self.sizes):
+            f = self.first[s]
+            p_end = (f + n) * hw_out * hw_out
+            for p0 in range(f * hw_out * hw_out, p_end, 128):
+                for o0 in range(0, co, tc):
+                    items.append([s, p0, min(p0 + 128, p_end), o0])
+        return self._hold(torch.tensor(items, dtype=torch.int32, device=self.be.dev))
+
+    def _wgrad_work(self, hw_out, co, K):
+        tiles = -(-co // 128) * -(-K // 128)
+        per_member = max(1, -(-4096 // max(1, len(self.slots) * tiles)))
+        items = []
+        for s, n in zip(self.slots, self.sizes):
+            f = self.first[s]
+            p_beg, p_end = f * hw_out * hw_out, (f + n) * hw_out * hw_out
+            chunk = max(512, -(-(p_end - p_beg) // per_member))
+            chunk = (chunk + 31) // 32 * 32
+            for p0 in range(p_beg, p_end, chunk):
+                for o0 in range(0, co, 128):
+                    for n0 in range(0, K, 128):
+                        items.append([s, p0, min(p0 + chunk, p_end), o0 | ((n0 // 8) << 16)])
+        return self._hold(torch.tensor(items, dtype=torch.int32, device=self.be.dev))
+
+    def _args(self):
+        be, e = self.be, self.e
+        a = CgArgs()
+        a.w_mstride = be.wtot
+        a.grads, a.g_mstride = _p(e.grads), e.Pp
+        a.cmax = CMAX
+        return a
+
+    def cf(self, bn):  # forward coefficients of BN `bn`
+        return self.be.coef[0, bn]
+
+    def cb(self, bn):  # backward coefficients
+        return self.be.coef[1, bn]
+
+    def sf(self, bn):
+        return self.be.sums[0, bn]
+
+    def sb(self, bn):
+        return self.be.sums[1, bn]
+
+    def conv(self, ci, src, out, hw_in, mode=0, c_in=None, x2=None, epi=0, res=None, xm=None, c_ep=None, st=None,
+             dgrad=False):
+        """Forward conv (dgrad=False) or data gradient (dgrad=True) of conv `ci` through convg_fwd."""
+        be = self.be
+        c = self.be.prog.convs[ci]
+        k = c.k
+        pad = (k - 1) // 2
+        a = self._args()
+        a.x, a.x2, a.y, a.res, a.xm = _p(src), _p(x2), _p(out), _p(res), _p(xm)
+        a.w = _p(be.w)
+        a.c_in, a.c_ep, a.st_out = _p(c_in), _p(c_ep), _p(st)
+        a.kh = a.kw = k
+        if not dgrad:
+            cin = 8 if ci == be.prog.stem else c.cin
+            hw_out = (hw_in + c.stride - 1) // c.stride
+            a.w_off = be.fwd_off[ci]
+            a.Hi = a.Wi = hw_in
+            a.Ci, a.Co = cin, c.cout
+            a.Ho = a.Wo = hw_out
+            a.stride, a.pad = c.stride, pad
+            trans = 0
+        else:
+            # gathered = dy at the conv's output resolution; output = dx at its input resolution
+            hw_out = hw_in * c.stride
+            a.w_off = be.dgr_off[ci]
+            a.Hi = a.Wi = hw_in
+            a.Ci, a.Co = c.cout, c.cin
+            a.Ho = a.Wo = hw_out
+            a.stride, a.pad = c.stride, k - 1 - pad
+            trans = 1 if c.stride > 1 else 0
+        a.log2ci = _log2(a.Ci)
+        tc = 128 if a.Co >= 128 else 64
+        work = self._pix_work(hw_out, a.Co, tc)
+        a.work = _p(work)
+        self._hold(a)
+        self._add(ops.lib().dtf_convg_fwd, ctypes.byref(a), tc, mode, epi, trans, work.shape[0])
+
+    def wgrad(self, ci, x, dy, hw_in, mode_x=0, c_x=None, mode_dy=0, c_dy=None, dy2=None):
+        be = self.be
+        c = be.prog.convs[ci]
+        a = self._args()
+        cin = 8 if ci == be.prog.stem else c.cin
+        hw_out = (hw_in + c.stride - 1) // c.stride
+        a.x, a.dy, a.dy2 = _p(x), _p(dy), _p(dy2)
+        a.c_in, a.c_dy = _p(c_x), _p(c_dy)
+        a.g_off = c.off
+        a.Hi = a.Wi = hw_in
+        a.Ci, a.Co = cin, c.cout
+        a.Ho = a.Wo = hw_out
+        a.kh = a.kw = c.k
+        a.stride, a.pad = c.stride, (c.k - 1) // 2
+        a.log2ci = _log2(cin)
+        a.cin_real = c.cin
+        work = self._wgrad_work(hw_out, c.cout, c.k * c.k * cin)
+        a.work = _p(work)
+        self._hold(a)
+        self._add(ops.lib().dtf_convg_wgrad, ctypes.byref(a), mode_x, mode_dy, work.shape[0])
+
+    def bn_final(self, bn, hw, backward):
+        be, e = self.be, self.e
+        b = be.prog.bns[bn]
+        a = BnFinArgs()
+        a.state, a.s_mstride = _p(e.state), e.S
+        a.sums = _p(self.sb(bn) if backward else self.sf(bn))
+        a.coef = _p(self.cb(bn) if backward else self.cf(bn))
+        a.fcoef = _p(self.cf(bn))
+        a.grads, a.g_mstride = _p(e.grads), e.Pp
+        a.slots, a.cnt = _p(self.slots_t), _p(self.cnt)
+        a.gamma_off, a.beta_off, a.run_off = b.gamma_off, b.beta_off, 3 * e.Pp + b.run_off
+        a.C, a.hw, a.cmax = b.c, hw * hw, CMAX
+        self._hold(a)
+        self._add(ops.lib().dtf_cg_bn_final, ctypes.byref(a), int(backward), len(self.slots))
+
+    # ------------------------------------------------------------------------------------------ program
+    def _build(self):
+        be, e, prog, cfg = self.be, self.e, self.be.prog, self.be.cfg
+        L = ops.lib()
+        N, H = self.N, self.H
+        ns = len(self.slots)
+        self._add(L.dtf_cg_weight_prep, _p(e.state), e.S, _p(be.conv_table), len(prog.convs), _p(self.slots_t), ns,
+                  _p(be.w), _p(be.w), be.wtot)
+        self._add(L.dtf_cg_dense_prep, _p(e.state), e.S, prog.dense_w_off, be.ncls, NPAD_CLS, cfg.final_size,
+                  _p(self.slots_t), ns, _p(be.dense), NPAD_CLS * cfg.final_size)
+        self._add("zero", be.sums)
+        self._add("zero", be.loss)
+        self._add("zero", be.correct)
+        self._add(L.dtf_cg_prep_input, _p(self.x_in), _p(self.xin8), N * H * H, cfg.in_channels)
+        # ---- stem: conv 7x7/2 (no BN in v2) -> max-pool 3x3/2
+        H1, H2 = H // 2, self.xs[0].shape[1]
+        self.conv(prog.stem, self.xin8, self.y0, H, mode=0, epi=0)
+        self._add(L.dtf_cg_maxpool, _p(self.y0), _p(self.xs[0]), _p(self.am0), None, None, N, H1, H1, H2, H2,
+                  cfg.num_filters, 0)
+        self._add(L.dtf_cg_chan_stats, _p(self.xs[0]), _p(self.img_slot), _p(self.sf(prog.blocks[0].bns[0])), N,
+                  H2 * H2, cfg.num_filters, CMAX)
+        nblk = len(prog.blocks)
+        for i, blk in enumerate(prog.blocks):
+            hi, ho, cin, f, fout = self.geo[i]
+            b1, b2, b3 = blk.bns
+            c1, c2, c3 = blk.convs
+            x = self.xs[i]
+            self.bn_final(b1, hi, False)
+            if blk.proj is not None:
+                self.conv(blk.proj, x, self.sc[i], hi, mode=1, c_in=self.cf(b1), epi=0)
+            self.conv(c1, x, self.h1[i], hi, mode=1, c_in=self.cf(b1), epi=4, st=self.sf(b2))
+            self.bn_final(b2, hi, False)
+            self.conv(c2, self.h1[i], self.h2[i], hi, mode=1, c_in=self.cf(b2), epi=4, st=self.sf(b3))
+            self.bn_final(b3, ho, False)
+            nxt = prog.blocks[i + 1].bns[0] if i + 1 < nblk else prog.final_bn
+            res = self.sc[i] if blk.proj is not None else x
+            self.conv(c3, self.h2[i], self.xs[i + 1], ho, mode=1, c_in=self.cf(b3), epi=5, res=res, st=self.sf(nxt))
+        fb = prog.final_bn
+        HL = self.HL
+        self.bn_final(fb, HL, False)
+        g = GapArgs()
+        g.x, g.coef, g.img_slot, g.feat = _p(self.xs[-1]), _p(self.cf(fb)), _p(self.img_slot), _p(self.feat)
+        g.dfeat, g.sums, g.bcoef = _p(self.dfeat), _p(self.sb(fb)), _p(self.cb(fb))
+        g.hw, g.C, g.cmax = HL * HL, cfg.final_size, CMAX
+        self._hold(g)
+        self._add(L.dtf_cg_gap, ctypes.byref(g), 0, N)
+        # ---- dense + softmax CE
+        from .hip_mnist import GEMM_OUT_ACC, GEMM_OUT_F32, GroupedGemm
+        C = cfg.final_size
+        Dstride = NPAD_CLS * C
+        fwd, dgr, wgr = [], [], []
+        for s, n in zip(self.slots, self.sizes):
+            f0 = self.first[s]
+            fwd.append((f0 * C, s * Dstride, f0 * NPAD_CLS, n, NPAD_CLS, C))
+            dgr.append((f0 * NPAD_CLS, s * Dstride, f0 * C, n, C, NPAD_CLS))
+            wgr.append((f0 * NPAD_CLS, f0 * C, s * e.Pp + prog.dense_w_off, NPAD_CLS, C, n, be.ncls))
+        dev = be.dev
+        self.g_fwd = GroupedGemm(self.feat, be.dense, self.logits, C, C, NPAD_CLS, fwd, False, False, GEMM_OUT_F32, dev)
+        self.g_dgr = GroupedGemm(self.dlog, be.dense, self.dfeat, NPAD_CLS, C, C, dgr, False, True, GEMM_OUT_F32, dev)
+        self.g_wgr = GroupedGemm(self.dlog, self.feat, e.grads, NPAD_CLS, C, C, wgr, True, True, GEMM_OUT_ACC, dev)
+        self._add("gemm", self.g_fwd)
+        self._add(L.dtf_cg_softmax_ce, _p(self.logits), NPAD_CLS, be.ncls, _p(self.labels), _p(self.img_slot),
+                  _p(e.state), e.S, prog.dense_b_off, _p(e.grads), e.Pp, _p(self.cnt), _p(be.loss), _p(be.correct),
+                  _p(self.dlog), N)
+        self._add("gemm", self.g_dgr)
+        self._add("gemm", self.g_wgr)
+        # ---- final BN backward -> gradient at the last block output
+        self._add(L.dtf_cg_gap, ctypes.byref(g), 1, N)
+        self.bn_final(fb, HL, True)
+        gcur = self.tmp("g0", HL, C)
+        g2 = GapArgs()
+        ctypes.memmove(ctypes.addressof(g2), ctypes.addressof(g), ctypes.sizeof(GapArgs))
+        g2.out = _p(gcur)
+        self._hold(g2)
+        self._add(L.dtf_cg_gap, ctypes.byref(g2), 2, N)
+        # ---- blocks, reversed
+        for i in range(nblk - 1, -1, -1):
+            blk = prog.blocks[i]
+            hi, ho, cin, f, fout = self.geo[i]
+            b1, b2, b3 = blk.bns
+            c1, c2, c3 = blk.convs
+            x, h1, h2 = self.xs[i], self.h1[i], self.h2[i]
+            dz3 = self.tmp("dz3", ho, f)
+            self.conv(c3, gcur, dz3, ho, mode=0, epi=6, xm=h2, c_ep=self.cf(b3), st=self.sb(b3), dgrad=True)
+            self.bn_final(b3, ho, True)
+            self.wgrad(c3, h2, gcur, ho, mode_x=1, c_x=self.cf(b3), mode_dy=0)
+            dz2 = self.tmp("dz2", hi, f)
+            self.conv(c2, dz3, dz2, ho, mode=2, c_in=self.cb(b3), x2=h2, epi=6, xm=h1, c_ep=self.cf(b2),
+                      st=self.sb(b2), dgrad=True)
+            self.bn_final(b2, hi, True)
+            self.wgrad(c2, h1, dz3, hi, mode_x=1, c_x=self.cf(b2), mode_dy=2, c_dy=self.cb(b3), dy2=h2)
+            pd = None
+            if blk.proj is not None:
+                pd = self.tmp("pd", hi, cin)
+                self.conv(blk.proj, gcur, pd, ho, mode=0, epi=0, dgrad=True)
+                self.wgrad(blk.proj, x, gcur, hi, mode_x=1, c_x=self.cf(b1), mode_dy=0)
+            dz1 = self.tmp("dz1", hi, cin)
+            self.conv(c1, dz2, dz1, hi, mode=2, c_in=self.cb(b2), x2=h1, epi=6 | (1 if pd is not None else 0),
+                      res=pd, xm=x, c_ep=self.cf(b1), st=self.sb(b1), dgrad=True)
+            self.bn_final(b1, hi, True)
+            self.wgrad(c1, x, dz2, hi, mode_x=1, c_x=self.cf(b1), mode_dy=2, c_dy=self.cb(b2), dy2=h1)
+            gname = "gA" if (i % 2 == 0) else "gB"
+            gnext = self.tmp(gname, hi, cin)
+            ew = EwArgs()
+            ew.dz, ew.h, ew.add, ew.out = _p(dz1), _p(x), (None if blk.proj is not None else _p(gcur)), _p(gnext)
+            ew.coef, ew.img_slot, ew.hw, ew.C, ew.cmax, ew.nimg = _p(self.cb(b1)), _p(self.img_slot), hi * hi, cin, \
+                CMAX, N
+            self._hold(ew)
+            self._add(L.dtf_cg_bn_bwd_apply, ctypes.byref(ew))
+            gcur = gnext
+        # ---- stem: max-pool backward, stem wgrad (padded input, 3 real channels)
+        dy0 = self.tmp("dy0", H1, cfg.num_filters)
+        self._add(L.dtf_cg_maxpool, None, None, _p(self.am0), _p(gcur), _p(dy0), N, H1, H1, H2, H2, cfg.num_filters, 1)
+        self.wgrad(prog.stem, self.xin8, dy0, H, mode_x=0, mode_dy=0)
+        self._add("optim", None)
+        self._add("step", None)
+
+    # ----------------------------------------------------------------------------------------- execution
+    def load_batch(self, batches):
+        if same_batches(self, batches):
+            return
+        off = 0
+        for (x, y) in batches:
+            n = x.shape[0]
+            self.x_in[off:off + n].copy_(x.reshape(n, *self.x_in.shape[1:]), non_blocking=True)
+            self.labels[off:off + n].copy_(y, non_blocking=True)
+            off += n
+
+    def _run_eager(self):
+        e = self.e
+        st = ops.stream()
+        for fn, args in self.launches:
+            if fn == "zero":
+                args[0].zero_()
+            elif fn == "gemm":
+                args[0].launch(st)
+            elif fn == "optim":
+                ops.fused_optimizer(e.state, e.grads, e.hyper, e.Pp, e.P, e.n_reg, shadow=None, zero_grads=True)
+            elif fn == "step":
+                advance_steps(e, self.slots_long)
+            else:
+                err = fn(*args, st)
+                if err != 0:
+                    raise RuntimeError("kernel launch %s failed with %d" % (getattr(fn, "__name__", fn), err))
+
+    def run(self):
+        be = self.be
+        if be.use_graph and self.graph is None:
+            self._run_eager()
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                g.capture_begin()
+                self._run_eager()
+                g.capture_end()
+            torch.cuda.current_stream().wait_stream(s)
+            self.graph = g
+            return
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._run_eager()

@@ -52,7 +52,7 @@ class MnistArgs(ctypes.Structure):
 
 class GemmGroup(ctypes.Structure):
     _fields_ = [("a_off", c_long), ("b_off", c_long), ("c_off", c_long), ("M", c_int), ("N", c_int), ("K", c_int),
-                ("pad", c_int)]
+                ("Ms", c_int)]
 
 
 class GemmArgs(ctypes.Structure):
@@ -109,8 +109,9 @@ class GroupedGemm:
     """One grouped GEMM launch (a list of per-member problems) with its device tables."""
 
     def __init__(self, A, B, C, lda, ldb, ldc, problems, a_km, b_km, out, device):
-        """problems: [(a_off, b_off, c_off, M, N, K)] in elements."""
-        for (_, _, _, M, N, K) in problems:
+        """problems: [(a_off, b_off, c_off, M, N, K[, Ms])] in elements; Ms = rows actually stored (<= M)."""
+        problems = [tuple(p) + (0,) * (7 - len(p)) for p in problems]
+        for (_, _, _, M, N, K, _) in problems:
             if not a_km:
                 assert K % 32 == 0, "row-major A needs K % 32 == 0"
             else:
@@ -122,8 +123,8 @@ class GroupedGemm:
         assert lda % 8 == 0 and ldb % 8 == 0
         groups = (GemmGroup * len(problems))()
         work = []
-        for gi, (ao, bo, co, M, N, K) in enumerate(problems):
-            groups[gi] = GemmGroup(ao, bo, co, M, N, K, 0)
+        for gi, (ao, bo, co, M, N, K, Ms) in enumerate(problems):
+            groups[gi] = GemmGroup(ao, bo, co, M, N, K, Ms)
             for m0 in range(0, M, 64):
                 for n0 in range(0, N, 64):
                     work.append([gi, m0, n0, 0])

@@ -26,6 +26,7 @@ the PyTorch reference on CPU.
 from __future__ import annotations
 
 import math
+import os
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -178,6 +179,9 @@ class TorchBackend:
 
     def __init__(self, engine: PopulationEngine):
         self.e = engine
+        if engine.device.type == "cuda" and os.environ.get("DTF_MIOPEN_FIND", "1") == "1":
+            # MIOpen: benchmark the conv solvers once per shape instead of immediate-mode heuristics
+            torch.backends.cudnn.benchmark = True
 
     def on_params_changed(self, slots):
         pass
@@ -211,6 +215,9 @@ def make_backend(engine: PopulationEngine, name: str):
         if getattr(engine.arch, "name", "") == "mnist_cnn":
             from .hip_mnist import HipMnistBackend
             return HipMnistBackend(engine)
+        if getattr(getattr(engine.arch, "cfg", None), "bottleneck", False):
+            from .hip_imagenet import HipImageNetBackend
+            return HipImageNetBackend(engine)
         from .hip_resnet import HipResNetBackend
         return HipResNetBackend(engine)
     raise ValueError("unknown backend %r" % name)

@@ -1,0 +1,519 @@
+// Generic population-batched NHWC implicit-GEMM convolution for large-channel ResNets (gfx950).
+//
+// Used by the ImageNet-shape ResNet-50 path (stem 7x7/2, bottleneck 1x1 / 3x3 convs, C = 64..2048),
+// where the CIFAR kernels' compile-time small-channel geometry does not apply.  All layouts are NHWC bf16
+// with the images of every member packed along N; weights are per member bf16 rows.
+//
+//  convg_fwd  : out[p][o] = sum_{tap,i} W[o][tap][i] * T_in(src)[gather(p, tap)][i]
+//               GEMM rows = output channels (A = weights, ds_read_b128 from LDS [rows][32+8]),
+//               cols = output pixels (B = gathered activations), v_mfma_f32_16x16x32_bf16.
+//               One kernel serves the forward conv (gather = p*S + tap - P) and the data gradient
+//               (weights flipped/transposed; stride 1: same gather with P' = K-1-P; stride 2: "transposed"
+//               gather q = p + tap - P', valid iff q % S == 0, then q / S).
+//               T_in: identity | BN+ReLU (fwd prologue) | BN-backward apply A*dz + B*h + C (dgrad prologue).
+//               Epilogue: [+ residual], [mask by BN(xm)+ReLU > 0], bf16 store, per-channel sum / second
+//               moment (BN forward statistics, or sum(dz) / sum(dz*xhat) for the BN backward).
+//  convg_wgrad: dW[o][tap][i] += sum_p T_dy(dy)[p][o] * T_x(x)[p*S + tap - P][i], split over pixel ranges,
+//               both operands "k = pixel" fragments via ds_read_b64_tr_b16 from K-major LDS tiles, fp32
+//               atomics into the member's gradient row.
+// Per-member BN coefficients are precomputed by bn_finalize (convg_aux.hip) into [cap][4][CMAX] tables and
+// staged into LDS per workgroup (a workgroup's pixels always belong to one member).
+#include "common.h"
+
+namespace {
+
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ s16x4_t ds_read_tr(const bf16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p));
+}
+
+struct CgArgs {
+  const bf16_t* x;    // gathered operand (fwd: input activations; dgrad: output gradient; wgrad: input)
+  const bf16_t* x2;   // second input of a BN-backward transform
+  const bf16_t* dy;   // wgrad: output-side operand
+  const bf16_t* dy2;  // wgrad: BN-backward second input of dy
+  const bf16_t* w;    // bf16 weights [rows][K] per member
+  long w_mstride, w_off;
+  bf16_t* y;          // output NHWC
+  const bf16_t* res;  // residual added in the epilogue
+  const bf16_t* xm;   // epilogue mask source
+  float* grads;       // wgrad output rows
+  long g_mstride, g_off;
+  const float* c_in;  // transform coefficients of the gathered operand [cap][4][cmax]
+  const float* c_dy;  // wgrad: transform coefficients of dy
+  const float* c_ep;  // epilogue mask BN: scale, shift, mean, inv [cap][4][cmax]
+  float* st_out;      // per-channel sums [cap][2][cmax] (atomics)
+  const int4* work;   // fwd: (slot, p0, p1, o0); wgrad: (slot, p0, p1, o0 | n0 << 16 (in 8-col units))
+  int Hi, Wi, Ci;     // gathered tensor geometry
+  int Ho, Wo, Co;     // output geometry (Co = GEMM rows)
+  int kh, kw, stride, pad;
+  int cmax;
+  int log2ci;
+  int cin_real;       // wgrad: real input channels of a channel-padded operand (stem: 3 of 8); 0 = Ci
+};
+
+constexpr int TP = 128;   // pixels per workgroup tile
+constexpr int RP = 40;    // [rows][32] tile pitch (+16 B)
+
+// ---------------------------------------------------------------------------------------------- fwd / dgrad
+// MODE: 0 identity, 1 relu(x*s + t), 2 A*x + B*x2 + C.   EPI: bit0 residual, bit1 mask, bit2 stats (fwd: y, y^2;
+// with bit1: dz, dz*xhat).  TRANS: transposed (dgrad, stride > 1) gather.
+template <int TC, int MODE, int EPI, bool TRANS>
+__global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
+  constexpr int MT = TC / 32;  // MFMA row tiles per wave (wave covers TC/2 rows)
+  __shared__ __attribute__((aligned(16))) bf16_t sa[2][TC * RP];
+  __shared__ __attribute__((aligned(16))) bf16_t sb[2][TP * RP];
+  extern __shared__ float dyn[];  // transform coefficients: MODE 1: 2*Ci, MODE 2: 3*Ci
+  __shared__ float acc_lds[2][TC];
+  const int4 wk = a.work[blockIdx.x];
+  const int slot = wk.x, p0 = wk.y, p1 = wk.z, o0 = wk.w;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave & 1, wc = wave >> 1;
+  const int Ci = a.Ci, K = a.kh * a.kw * Ci;
+  if constexpr (MODE != 0) {
+    const float* cb = a.c_in + (long)slot * 4 * a.cmax;
+    for (int i = tid; i < Ci; i += 256) {
+      dyn[i] = cb[i];
+      dyn[Ci + i] = cb[a.cmax + i];
+      if constexpr (MODE == 2) dyn[2 * Ci + i] = cb[2 * a.cmax + i];
+    }
+  }
+  if (tid < 2 * TC) (&acc_lds[0][0])[tid] = 0.f;
+  // per-thread B rows (pixels): r = (tid >> 2) + 64 j, chunk c = tid & 3
+  const int cB = tid & 3;
+  int pix_img[2], pix_y[2], pix_x[2];
+  bool pix_ok[2];
+  const int HWo = a.Ho * a.Wo;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int p = p0 + (tid >> 2) + 64 * j;
+    pix_ok[j] = p < p1;
+    const int pp = pix_ok[j] ? p : p0;
+    pix_img[j] = pp / HWo;
+    const int rem = pp - pix_img[j] * HWo;
+    pix_y[j] = rem / a.Wo;
+    pix_x[j] = rem - pix_y[j] * a.Wo;
+  }
+  const bf16_t* wbase = a.w + (long)slot * a.w_mstride + a.w_off;
+  const long img_elems = (long)a.Hi * a.Wi * Ci;
+  auto load_b = [&](int k0, uint4 (&v)[2], uint4 (&v2)[2], int& cch, unsigned& okb) {
+    const int k = k0 + 8 * cB;
+    const int tap = k >> a.log2ci, ci0 = k & (Ci - 1);
+    const int ky = tap / a.kw, kx = tap - ky * a.kw;
+    cch = ci0;
+    okb = 0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      int gy, gx;
+      bool ok = pix_ok[j] && k < K;
+      if constexpr (TRANS) {
+        const int qy = pix_y[j] + ky - a.pad, qx = pix_x[j] + kx - a.pad;
+        ok = ok && qy >= 0 && qx >= 0 && (qy % a.stride) == 0 && (qx % a.stride) == 0;
+        gy = qy / a.stride;
+        gx = qx / a.stride;
+      } else {
+        gy = pix_y[j] * a.stride + ky - a.pad;
+        gx = pix_x[j] * a.stride + kx - a.pad;
+      }
+      ok = ok && gy >= 0 && gy < a.Hi && gx >= 0 && gx < a.Wi;
+      const long off = ok ? (long)pix_img[j] * img_elems + ((long)gy * a.Wi + gx) * Ci + ci0 : -1;
+      v[j] = make_uint4(0, 0, 0, 0);
+      v2[j] = make_uint4(0, 0, 0, 0);
+      if (off >= 0) {
+        v[j] = *reinterpret_cast<const uint4*>(a.x + off);
+        if constexpr (MODE == 2) v2[j] = *reinterpret_cast<const uint4*>(a.x2 + off);
+        okb |= 1u << j;  // unset: zero padding (stays zero after the transform)
+      }
+    }
+  };
+  auto xform_store = [&](bf16_t* dst, const uint4 (&v)[2], const uint4 (&v2)[2], int cch, unsigned okb) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      uint4 t = v[j];
+      if (!((okb >> j) & 1u)) {
+        t = make_uint4(0, 0, 0, 0);
+      } else if constexpr (MODE != 0) {
+        uint32_t w32[4] = {t.x, t.y, t.z, t.w};
+        const uint32_t h32[4] = {v2[j].x, v2[j].y, v2[j].z, v2[j].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = cch + 2 * q;
+          float x0 = __uint_as_float(w32[q] << 16), x1 = __uint_as_float(w32[q] & 0xffff0000u);
+          if constexpr (MODE == 1) {
+            x0 = fmaxf(x0 * dyn[c] + dyn[Ci + c], 0.f);
+            x1 = fmaxf(x1 * dyn[c + 1] + dyn[Ci + c + 1], 0.f);
+          } else {
+            const float h0 = __uint_as_float(h32[q] << 16), h1 = __uint_as_float(h32[q] & 0xffff0000u);
+            x0 = dyn[c] * x0 + dyn[Ci + c] * h0 + dyn[2 * Ci + c];
+            x1 = dyn[c + 1] * x1 + dyn[Ci + c + 1] * h1 + dyn[2 * Ci + c + 1];
+          }
+          w32[q] = pack2bf(x0, x1);
+        }
+        t = make_uint4(w32[0], w32[1], w32[2], w32[3]);
+      }
+      *reinterpret_cast<uint4*>(dst + ((tid >> 2) + 64 * j) * RP + 8 * cB) = t;
+    }
+  };
+  // A (weights): rows o0 + r, r = (tid >> 2) + 64 j (j < TC / 64)
+  constexpr int AJ = TC / 64;
+  auto load_a = [&](int k0, uint4 (&v)[AJ]) {
+#pragma unroll
+    for (int j = 0; j < AJ; ++j) {
+      const int r = (tid >> 2) + 64 * j;
+      const int k = k0 + 8 * cB;
+      v[j] = (o0 + r < a.Co && k < K) ? *reinterpret_cast<const uint4*>(wbase + (long)(o0 + r) * K + k)
+                                      : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_a = [&](bf16_t* dst, const uint4 (&v)[AJ]) {
+#pragma unroll
+    for (int j = 0; j < AJ; ++j) *reinterpret_cast<uint4*>(dst + ((tid >> 2) + 64 * j) * RP + 8 * cB) = v[j];
+  };
+  f32x4_t acc[MT][4];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  __syncthreads();  // coefficients in LDS
+  const int nk = (K + 31) / 32;
+  uint4 ra[AJ], rb[2], rb2[2];
+  int cch;
+  unsigned okb;
+  load_a(0, ra);
+  load_b(0, rb, rb2, cch, okb);
+  store_a(sa[0], ra);
+  xform_store(sb[0], rb, rb2, cch, okb);
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    const int cur = ks & 1;
+    const bool more = ks + 1 < nk;
+    int ncch = 0;
+    if (more) {
+      load_a(32 * (ks + 1), ra);
+      load_b(32 * (ks + 1), rb, rb2, ncch, okb);
+    }
+    bf16x8_t fa[MT], fb[4];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+      fa[m] = *reinterpret_cast<const bf16x8_t*>(sa[cur] + (wr * (TC / 2) + 16 * m + (lane & 15)) * RP +
+                                                 8 * (lane >> 4));
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+      fb[n] = *reinterpret_cast<const bf16x8_t*>(sb[cur] + (wc * 64 + 16 * n + (lane & 15)) * RP + 8 * (lane >> 4));
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(fa[m], fb[n], acc[m][n]);
+    if (more) {
+      store_a(sa[cur ^ 1], ra);
+      xform_store(sb[cur ^ 1], rb, rb2, ncch, okb);
+    }
+    __syncthreads();
+  }
+  // epilogue: lane holds pixel col (lane & 15), rows (output channels) 4*(lane>>4) + r
+  const float* ep = a.c_ep + (long)slot * 4 * a.cmax;
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int oc = o0 + wr * (TC / 2) + 16 * m + 4 * (lane >> 4);
+    float ss[4] = {0.f, 0.f, 0.f, 0.f}, sq[4] = {0.f, 0.f, 0.f, 0.f};
+    float esc[4], esh[4], emu[4], eiv[4];
+    if constexpr (EPI & 2) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = min(oc + r, a.Co - 1);
+        esc[r] = ep[c];
+        esh[r] = ep[a.cmax + c];
+        emu[r] = ep[2 * a.cmax + c];
+        eiv[r] = ep[3 * a.cmax + c];
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int p = p0 + wc * 64 + 16 * n + (lane & 15);
+      if (p >= p1 || oc >= a.Co) continue;
+      const long o = (long)p * a.Co + oc;
+      float v[4] = {acc[m][n][0], acc[m][n][1], acc[m][n][2], acc[m][n][3]};
+      if constexpr (EPI & 1) {
+        const uint2 rr = *reinterpret_cast<const uint2*>(a.res + o);
+        v[0] += bf2f((bf16_t)(rr.x & 0xffff));
+        v[1] += bf2f((bf16_t)(rr.x >> 16));
+        v[2] += bf2f((bf16_t)(rr.y & 0xffff));
+        v[3] += bf2f((bf16_t)(rr.y >> 16));
+      }
+      float xv[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI & 2) {
+        const uint2 xr = *reinterpret_cast<const uint2*>(a.xm + o);
+        xv[0] = bf2f((bf16_t)(xr.x & 0xffff));
+        xv[1] = bf2f((bf16_t)(xr.x >> 16));
+        xv[2] = bf2f((bf16_t)(xr.y & 0xffff));
+        xv[3] = bf2f((bf16_t)(xr.y >> 16));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (xv[r] * esc[r] + esh[r] > 0.f) ? v[r] : 0.f;
+      }
+      uint2 pk;
+      pk.x = pack2bf(v[0], v[1]);
+      pk.y = pack2bf(v[2], v[3]);
+      *reinterpret_cast<uint2*>(a.y + o) = pk;
+      if constexpr (EPI & 4) {
+        const float r4[4] = {bf2f((bf16_t)(pk.x & 0xffff)), bf2f((bf16_t)(pk.x >> 16)), bf2f((bf16_t)(pk.y & 0xffff)),
+                             bf2f((bf16_t)(pk.y >> 16))};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          ss[r] += r4[r];
+          if constexpr (EPI & 2) sq[r] += r4[r] * (xv[r] - emu[r]) * eiv[r];
+          else sq[r] += r4[r] * r4[r];
+        }
+      }
+    }
+    if constexpr (EPI & 4) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float s = ss[r], q = sq[r];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s += __shfl_xor(s, o, 64);
+          q += __shfl_xor(q, o, 64);
+        }
+        if ((lane & 15) == 0 && oc + r < a.Co) {
+          const int lc = oc + r - o0;
+          atomicAdd(&acc_lds[0][lc], s);
+          atomicAdd(&acc_lds[1][lc], q);
+        }
+      }
+    }
+  }
+  if constexpr (EPI & 4) {
+    __syncthreads();
+    if (tid < TC && o0 + tid < a.Co) {
+      float* st = a.st_out + (long)slot * 2 * a.cmax;
+      atomicAdd(st + o0 + tid, acc_lds[0][tid]);
+      atomicAdd(st + a.cmax + o0 + tid, acc_lds[1][tid]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------- wgrad
+// Tile: 128 output channels (rows) x 128 (tap, ci) columns, k = 32 output pixels per step.
+constexpr int WT = 128;
+constexpr int KP = WT + 8;
+
+template <int MODE_X, int MODE_DY>
+__global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16_t sd[2][32 * KP];
+  __shared__ __attribute__((aligned(16))) bf16_t sx[2][32 * KP];
+  extern __shared__ float dyn[];  // x coefficients (2*Ci) then dy coefficients (3*Co)
+  const int4 wk = a.work[blockIdx.x];
+  const int slot = wk.x, p0 = wk.y, p1 = wk.z, o0 = wk.w & 0xffff, n0 = (wk.w >> 16) * 8;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave & 1, wc = wave >> 1;
+  const int Ci = a.Ci, Co = a.Co, K = a.kh * a.kw * Ci;
+  float* cx = dyn;
+  float* cd = dyn + 2 * Ci;
+  if constexpr (MODE_X != 0) {
+    const float* cb = a.c_in + (long)slot * 4 * a.cmax;
+    for (int i = tid; i < Ci; i += 256) {
+      cx[i] = cb[i];
+      cx[Ci + i] = cb[a.cmax + i];
+    }
+  }
+  if constexpr (MODE_DY != 0) {
+    const float* cb = a.c_dy + (long)slot * 4 * a.cmax;
+    for (int i = tid; i < Co; i += 256) {
+      cd[i] = cb[i];
+      cd[Co + i] = cb[a.cmax + i];
+      if constexpr (MODE_DY == 2) cd[2 * Co + i] = cb[2 * a.cmax + i];
+    }
+  }
+  // loads: k-row = tid >> 4 (+16 for j = 1), 8-wide column chunk = tid & 15
+  const int kr = tid >> 4, cc = tid & 15;
+  const int HWo = a.Ho * a.Wo;
+  const long img_x = (long)a.Hi * a.Wi * Ci;
+  // x column chunk -> (tap, ci0), fixed for the workgroup
+  const int xcol = n0 + 8 * cc;
+  const int xtap = xcol >> a.log2ci, xci = xcol & (Ci - 1);
+  const int xky = xtap / a.kw, xkx = xtap - xky * a.kw;
+  const bool xcol_ok = xcol < K;
+  const int dcol = o0 + 8 * cc;
+  const bool dcol_ok = dcol < Co;
+  auto load = [&](int pk0, uint4 (&dv)[2], uint4 (&dv2)[2], uint4 (&xv)[2], unsigned& okm) {
+    okm = 0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int p = pk0 + kr + 16 * j;
+      const bool pin = p < p1;
+      const int pp = pin ? p : p0;
+      const int img = pp / HWo, rem = pp - img * HWo;
+      const int oy = rem / a.Wo, ox = rem - oy * a.Wo;
+      dv[j] = dv2[j] = xv[j] = make_uint4(0, 0, 0, 0);
+      if (pin && dcol_ok) {
+        dv[j] = *reinterpret_cast<const uint4*>(a.dy + (long)pp * Co + dcol);
+        if constexpr (MODE_DY == 2) dv2[j] = *reinterpret_cast<const uint4*>(a.dy2 + (long)pp * Co + dcol);
+        okm |= 1u << j;
+      }
+      const int gy = oy * a.stride + xky - a.pad, gx = ox * a.stride + xkx - a.pad;
+      if (pin && xcol_ok && gy >= 0 && gy < a.Hi && gx >= 0 && gx < a.Wi) {
+        xv[j] = *reinterpret_cast<const uint4*>(a.x + img * img_x + ((long)gy * a.Wi + gx) * Ci + xci);
+        okm |= 4u << j;
+      }
+    }
+  };
+  auto store = [&](bf16_t* d, bf16_t* xx, const uint4 (&dv)[2], const uint4 (&dv2)[2], const uint4 (&xv)[2],
+                   unsigned okm) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      uint4 t = dv[j];
+      if (MODE_DY != 0 && ((okm >> j) & 1u)) {
+        uint32_t w32[4] = {t.x, t.y, t.z, t.w};
+        const uint32_t h32[4] = {dv2[j].x, dv2[j].y, dv2[j].z, dv2[j].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = dcol + 2 * q;
+          float x0 = __uint_as_float(w32[q] << 16), x1 = __uint_as_float(w32[q] & 0xffff0000u);
+          if constexpr (MODE_DY == 1) {
+            x0 = fmaxf(x0 * cd[c] + cd[Co + c], 0.f);
+            x1 = fmaxf(x1 * cd[c + 1] + cd[Co + c + 1], 0.f);
+          } else {
+            const float h0 = __uint_as_float(h32[q] << 16), h1 = __uint_as_float(h32[q] & 0xffff0000u);
+            x0 = cd[c] * x0 + cd[Co + c] * h0 + cd[2 * Co + c];
+            x1 = cd[c + 1] * x1 + cd[Co + c + 1] * h1 + cd[2 * Co + c + 1];
+          }
+          w32[q] = pack2bf(x0, x1);
+        }
+        t = make_uint4(w32[0], w32[1], w32[2], w32[3]);
+      }
+      *reinterpret_cast<uint4*>(d + (kr + 16 * j) * KP + 8 * cc) = t;
+      uint4 u = xv[j];
+      if (MODE_X == 1 && ((okm >> (2 + j)) & 1u)) {
+        uint32_t w32[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = xci + 2 * q;
+          const float x0 = __uint_as_float(w32[q] << 16), x1 = __uint_as_float(w32[q] & 0xffff0000u);
+          w32[q] = pack2bf(fmaxf(x0 * cx[c] + cx[Ci + c], 0.f), fmaxf(x1 * cx[c + 1] + cx[Ci + c + 1], 0.f));
+        }
+        u = make_uint4(w32[0], w32[1], w32[2], w32[3]);
+      }
+      *reinterpret_cast<uint4*>(xx + (kr + 16 * j) * KP + 8 * cc) = u;
+    }
+  };
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  const int nk = (p1 - p0 + 31) / 32;
+  uint4 dv[2], dv2[2], xv[2];
+  unsigned okm;
+  load(p0, dv, dv2, xv, okm);
+  store(sd[0], sx[0], dv, dv2, xv, okm);
+  __syncthreads();
+  const int g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
+  for (int ks = 0; ks < nk; ++ks) {
+    const int cur = ks & 1;
+    const bool more = ks + 1 < nk;
+    if (more) load(p0 + 32 * (ks + 1), dv, dv2, xv, okm);
+    bf16x8_t fa[4], fb[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int cb = wr * 64 + 16 * m + 4 * p4;
+      const s16x4_t lo = ds_read_tr(sd[cur] + (8 * g + q) * KP + cb);
+      const s16x4_t hi = ds_read_tr(sd[cur] + (8 * g + 4 + q) * KP + cb);
+      fa[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int cb = wc * 64 + 16 * n + 4 * p4;
+      const s16x4_t lo = ds_read_tr(sx[cur] + (8 * g + q) * KP + cb);
+      const s16x4_t hi = ds_read_tr(sx[cur] + (8 * g + 4 + q) * KP + cb);
+      fb[n] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(fa[m], fb[n], acc[m][n]);
+    if (more) store(sd[cur ^ 1], sx[cur ^ 1], dv, dv2, xv, okm);
+    __syncthreads();
+  }
+  // D: lane holds column n = lane & 15 ((tap, ci) index), rows (o) 4*(lane>>4) + r
+  float* gr = a.grads + (long)slot * a.g_mstride + a.g_off;
+  const int cr = a.cin_real > 0 ? a.cin_real : Ci;
+  const int Kr = a.kh * a.kw * cr;
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int col = n0 + wc * 64 + 16 * n + (lane & 15);
+    const int tap = col >> a.log2ci, ci = col & (Ci - 1);
+    if (col >= K || ci >= cr) continue;
+    const int colr = tap * cr + ci;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = o0 + wr * 64 + 16 * m + 4 * (lane >> 4) + r;
+        if (o < Co) atomicAdd(gr + (long)o * Kr + colr, acc[m][n][r]);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+DTF_API int dtf_cg_args_size() { return (int)sizeof(CgArgs); }
+
+// flags: tc (64 | 128), mode (0..2), epi (0..7), trans (0/1)
+DTF_API int dtf_convg_fwd(const CgArgs* a, int tc, int mode, int epi, int trans, int nwork, hipStream_t stream) {
+  if (nwork <= 0) return 0;
+  if ((a->Ci & (a->Ci - 1)) != 0 || a->Ci < 8 || (a->Co & 3) != 0) return -2;
+  const size_t dyn = (size_t)(mode == 0 ? 0 : (mode == 1 ? 2 : 3)) * a->Ci * sizeof(float);
+  dim3 grid(nwork), block(256);
+#define CG_CASE(TC_, M_, E_, T_)                                                                  \
+  if (tc == TC_ && mode == M_ && epi == E_ && trans == T_) {                                      \
+    hipLaunchKernelGGL((convg_fwd_kernel<TC_, M_, E_, T_>), grid, block, dyn, stream, *a);       \
+    return DTF_CHECK_LAUNCH();                                                                    \
+  }
+#define CG_ALL_TC(M_, E_, T_) CG_CASE(64, M_, E_, T_) CG_CASE(128, M_, E_, T_)
+  // forward: identity (stem / v1) or BN+ReLU prologue; stats epilogue; optional residual
+  CG_ALL_TC(0, 4, false)
+  CG_ALL_TC(1, 4, false)
+  CG_ALL_TC(1, 0, false)
+  CG_ALL_TC(1, 5, false)
+  CG_ALL_TC(1, 1, false)
+  CG_ALL_TC(0, 0, false)
+  // dgrad: dy plain or BN-backward prologue; [+res] mask + stats epilogue, or plain
+  CG_ALL_TC(0, 6, false)
+  CG_ALL_TC(2, 6, false)
+  CG_ALL_TC(2, 7, false)
+  CG_ALL_TC(0, 0, false)
+  CG_ALL_TC(2, 0, false)
+  CG_ALL_TC(0, 6, true)
+  CG_ALL_TC(2, 6, true)
+  CG_ALL_TC(2, 7, true)
+  CG_ALL_TC(0, 0, true)
+  CG_ALL_TC(2, 0, true)
+#undef CG_ALL_TC
+#undef CG_CASE
+  return -1;
+}
+
+DTF_API int dtf_convg_wgrad(const CgArgs* a, int mode_x, int mode_dy, int nwork, hipStream_t stream) {
+  if (nwork <= 0) return 0;
+  if ((a->Ci & (a->Ci - 1)) != 0 || a->Ci < 8 || (a->Co & 7) != 0) return -2;
+  const size_t dyn = (size_t)(2 * a->Ci + 3 * a->Co) * sizeof(float);
+  dim3 grid(nwork), block(256);
+#define WG_CASE(MX, MD)                                                                     \
+  if (mode_x == MX && mode_dy == MD) {                                                      \
+    hipLaunchKernelGGL((convg_wgrad_kernel<MX, MD>), grid, block, dyn, stream, *a);         \
+    return DTF_CHECK_LAUNCH();                                                              \
+  }
+  WG_CASE(0, 0)
+  WG_CASE(1, 0)
+  WG_CASE(1, 2)
+  WG_CASE(0, 2)
+#undef WG_CASE
+  return -1;
+}

@@ -1,0 +1,514 @@
+// Auxiliary population-batched kernels of the ImageNet-shape ResNet step (gfx950).
+//   cg_weight_prep  : fp32 master rows -> bf16 conv weights (forward [o][tap][i], input channels padded) and
+//                     flipped/transposed dgrad weights [i][K*K-1-tap][o]; dense weights padded to 1024 rows
+//   cg_bn_fwd_final : per (member, channel) BN forward coefficients from the conv-epilogue sums
+//                     (scale, shift, mean, inv) + TF moving averages (momentum 0.997, unbiased variance)
+//   cg_bn_bwd_final : BN backward coefficients A, B, C of dh = A dz + B h + C from (sum dz, sum dz*xhat),
+//                     and dgamma / dbeta into the gradient row
+//   cg_bn_bwd_apply : g = A dz + B h + C (+ add)   (the residual-stream gradient through the first BN of a block)
+//   cg_prep_input   : fp32 NHWC images -> bf16 with channels zero-padded to 8
+//   cg_maxpool_fwd / cg_maxpool_bwd : 3x3/2 'SAME' (TF pads the end) max-pool with a per-output argmax byte;
+//                     the backward gathers (no atomics): every input pixel sums the <= 4 windows choosing it
+//   cg_gap          : final BN+ReLU + global average pool -> bf16 features (dense GEMM operand)
+//   cg_softmax_ce   : + bias, softmax cross-entropy, loss / correct count, dlogits (bf16, padded), dbias
+//   cg_gap_bwd_reduce / cg_gap_bwd_apply : backward of GAP + final BN + ReLU
+#include "common.h"
+
+#define BN_EPS 1e-5f
+#define BN_MOM 0.997f
+
+namespace {
+
+// conv table row: {w_off, cout, cin, k, cin_pad, fwd_off, dgr_off, 0}
+__global__ __launch_bounds__(256) void cg_weight_prep_kernel(const float* __restrict__ state, long s_mstride,
+                                                              const int* __restrict__ table,
+                                                              const int* __restrict__ slots, bf16_t* __restrict__ wf,
+                                                              bf16_t* __restrict__ wd, long w_mstride) {
+  const int* t = table + blockIdx.x * 8;
+  const int slot = slots[blockIdx.z];
+  const int w_off = t[0], cout = t[1], cin = t[2], k = t[3], cin_pad = t[4], fwd_off = t[5], dgr_off = t[6];
+  const int kk = k * k;
+  const float* p = state + (long)slot * s_mstride + w_off;
+  bf16_t* f = wf + (long)slot * w_mstride + fwd_off;
+  const int t0 = blockIdx.y * blockDim.x + threadIdx.x, ts = gridDim.y * blockDim.x;
+  const int nf = cout * kk * cin_pad;
+  if (cin_pad == cin && (nf & 3) == 0) {
+    for (int i = 4 * t0; i < nf; i += 4 * ts) {
+      const float4 v = *reinterpret_cast<const float4*>(p + i);
+      *reinterpret_cast<uint2*>(f + i) = make_uint2(pack2bf(v.x, v.y), pack2bf(v.z, v.w));
+    }
+  } else {
+    for (int i = t0; i < nf; i += ts) {
+      const int ci = i % cin_pad, rest = i / cin_pad;
+      f[i] = ci < cin ? f2bf(p[rest * cin + ci]) : (bf16_t)0;
+    }
+  }
+  if (dgr_off >= 0) {
+    bf16_t* d = wd + (long)slot * w_mstride + dgr_off;
+    const int nd = cin * kk * cout;
+    for (int i = t0; i < nd; i += ts) {
+      const int co = i % cout, rest = i / cout;  // rest = ci*kk + tap'
+      const int tp = rest % kk, ci = rest / kk;
+      d[i] = f2bf(p[(co * kk + (kk - 1 - tp)) * cin + ci]);
+    }
+  }
+}
+
+// dense [ncls][C] fp32 -> bf16 [npad][C] (rows >= ncls zero)
+__global__ __launch_bounds__(256) void cg_dense_prep_kernel(const float* __restrict__ state, long s_mstride, int w_off,
+                                                             int ncls, int npad, int C, const int* __restrict__ slots,
+                                                             bf16_t* __restrict__ out, long o_mstride) {
+  const int slot = slots[blockIdx.y];
+  const float* p = state + (long)slot * s_mstride + w_off;
+  bf16_t* o = out + (long)slot * o_mstride;
+  const int n = npad * C;
+  for (int i = (blockIdx.x * blockDim.x + threadIdx.x) * 2; i < n; i += gridDim.x * blockDim.x * 2) {
+    const int r = i / C;
+    const float v0 = r < ncls ? p[i] : 0.f, v1 = r < ncls ? p[i + 1] : 0.f;
+    *reinterpret_cast<uint32_t*>(o + i) = pack2bf(v0, v1);
+  }
+}
+
+struct BnFinArgs {
+  float* state;        // fp32 state rows (gamma/beta in params, running stats at run_base)
+  long s_mstride;
+  const float* sums;   // [cap][2][cmax]
+  float* coef;         // [cap][4][cmax] out
+  const float* fcoef;  // bwd: forward coefficients of the same BN
+  float* grads;        // bwd: dgamma / dbeta
+  long g_mstride;
+  const int* slots;
+  const float* cnt;    // images per member
+  int gamma_off, beta_off, run_off;  // run_off: absolute float index of running mean in the state row
+  int C, hw, cmax;
+};
+
+__global__ __launch_bounds__(256) void cg_bn_fwd_final_kernel(BnFinArgs a) {
+  const int slot = a.slots[blockIdx.y];
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.C) return;
+  const float* su = a.sums + (long)slot * 2 * a.cmax;
+  const float n = a.cnt[slot] * (float)a.hw;
+  const float mean = su[c] / n;
+  const float var = fmaxf(su[a.cmax + c] / n - mean * mean, 0.f);
+  const float inv = rsqrtf(var + BN_EPS);
+  float* row = a.state + (long)slot * a.s_mstride;
+  const float scale = row[a.gamma_off + c] * inv;
+  float* co = a.coef + (long)slot * 4 * a.cmax;
+  co[c] = scale;
+  co[a.cmax + c] = row[a.beta_off + c] - mean * scale;
+  co[2 * a.cmax + c] = mean;
+  co[3 * a.cmax + c] = inv;
+  float* run = row + a.run_off;
+  const float unb = n > 1.f ? var * n / (n - 1.f) : var;
+  run[c] = BN_MOM * run[c] + (1.f - BN_MOM) * mean;
+  run[a.C + c] = BN_MOM * run[a.C + c] + (1.f - BN_MOM) * unb;
+}
+
+__global__ __launch_bounds__(256) void cg_bn_bwd_final_kernel(BnFinArgs a) {
+  const int slot = a.slots[blockIdx.y];
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.C) return;
+  const float* su = a.sums + (long)slot * 2 * a.cmax;
+  const float* fc = a.fcoef + (long)slot * 4 * a.cmax;
+  const float n = a.cnt[slot] * (float)a.hw;
+  const float sdz = su[c], sdzx = su[a.cmax + c];
+  const float mean = fc[2 * a.cmax + c], inv = fc[3 * a.cmax + c];
+  const float* row = a.state + (long)slot * a.s_mstride;
+  const float scale = row[a.gamma_off + c] * inv;
+  const float m1 = sdz / n, m2 = sdzx / n;
+  float* co = a.coef + (long)slot * 4 * a.cmax;
+  co[c] = scale;
+  co[a.cmax + c] = -scale * inv * m2;
+  co[2 * a.cmax + c] = -scale * m1 + scale * inv * mean * m2;
+  float* g = a.grads + (long)slot * a.g_mstride;
+  g[a.gamma_off + c] += sdzx;
+  g[a.beta_off + c] += sdz;
+}
+
+struct EwArgs {
+  const bf16_t* dz;
+  const bf16_t* h;
+  const bf16_t* add;
+  bf16_t* out;
+  const float* coef;   // [cap][4][cmax]
+  const int* img_slot;
+  long hw;
+  int C, cmax;
+  long nimg;
+};
+
+__global__ __launch_bounds__(256) void cg_bn_bwd_apply_kernel(EwArgs a) {
+  const int img = blockIdx.x;
+  const int slot = a.img_slot[img];
+  const float* co = a.coef + (long)slot * 4 * a.cmax;
+  const long base = (long)img * a.hw * a.C;
+  const long n8 = a.hw * a.C / 8;
+  for (long i = (long)blockIdx.y * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.y * blockDim.x) {
+    const long o = base + i * 8;
+    const int c0 = (int)((i * 8) % a.C);
+    const uint4 dv = *reinterpret_cast<const uint4*>(a.dz + o);
+    const uint4 hv = *reinterpret_cast<const uint4*>(a.h + o);
+    uint4 av = make_uint4(0, 0, 0, 0);
+    if (a.add) av = *reinterpret_cast<const uint4*>(a.add + o);
+    const uint32_t d32[4] = {dv.x, dv.y, dv.z, dv.w}, h32[4] = {hv.x, hv.y, hv.z, hv.w},
+                   a32[4] = {av.x, av.y, av.z, av.w};
+    uint32_t r[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = c0 + 2 * q;
+      const float v0 = co[c] * bf2f((bf16_t)(d32[q] & 0xffff)) + co[a.cmax + c] * bf2f((bf16_t)(h32[q] & 0xffff)) +
+                       co[2 * a.cmax + c] + bf2f((bf16_t)(a32[q] & 0xffff));
+      const float v1 = co[c + 1] * bf2f((bf16_t)(d32[q] >> 16)) +
+                       co[a.cmax + c + 1] * bf2f((bf16_t)(h32[q] >> 16)) + co[2 * a.cmax + c + 1] +
+                       bf2f((bf16_t)(a32[q] >> 16));
+      r[q] = pack2bf(v0, v1);
+    }
+    *reinterpret_cast<uint4*>(a.out + o) = make_uint4(r[0], r[1], r[2], r[3]);
+  }
+}
+
+__global__ __launch_bounds__(256) void cg_prep_input_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
+                                                             long npix, int c_in) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += stride) {
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < c_in; ++c) v[c] = x[p * c_in + c];
+    *reinterpret_cast<uint4*>(y + p * 8) =
+        make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+  }
+}
+
+// 3x3 stride-2 max-pool, output o covers input rows / cols 2o .. 2o+2 (TF 'SAME': the pad is at the end)
+__global__ __launch_bounds__(256) void cg_maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                              uint8_t* __restrict__ am, int H, int W, int Ho, int Wo,
+                                                              int C, long total8) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total8; i += stride) {
+    const int c0 = (int)((i * 8) % C);
+    const long pix = (i * 8) / C;
+    const int ox = (int)(pix % Wo), oy = (int)((pix / Wo) % Ho);
+    const long img = pix / ((long)Wo * Ho);
+    float best[8];
+    uint32_t arg[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      best[k] = -3.0e38f;
+      arg[k] = 0;
+    }
+    for (int t = 0; t < 9; ++t) {
+      const int iy = 2 * oy + t / 3, ix = 2 * ox + t % 3;
+      if (iy >= H || ix >= W) continue;
+      const uint4 v = *reinterpret_cast<const uint4*>(x + ((img * H + iy) * W + ix) * C + c0);
+      const uint32_t w32[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float f = bf2f((bf16_t)((w32[k >> 1] >> (16 * (k & 1))) & 0xffff));
+        if (f > best[k]) {
+          best[k] = f;
+          arg[k] = (uint32_t)t;
+        }
+      }
+    }
+    const long o = pix * C + c0;
+    *reinterpret_cast<uint4*>(y + o) = make_uint4(pack2bf(best[0], best[1]), pack2bf(best[2], best[3]),
+                                                  pack2bf(best[4], best[5]), pack2bf(best[6], best[7]));
+    *reinterpret_cast<uint2*>(am + o) = make_uint2(arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24),
+                                                   arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24));
+  }
+}
+
+__global__ __launch_bounds__(256) void cg_maxpool_bwd_kernel(const bf16_t* __restrict__ g, const uint8_t* __restrict__ am,
+                                                              bf16_t* __restrict__ dx, int H, int W, int Ho, int Wo,
+                                                              int C, long total8) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total8; i += stride) {
+    const int c0 = (int)((i * 8) % C);
+    const long pix = (i * 8) / C;
+    const int ix = (int)(pix % W), iy = (int)((pix / W) % H);
+    const long img = pix / ((long)W * H);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // windows containing iy: oy in {iy/2 - 1 .. iy/2} with 2*oy <= iy <= 2*oy + 2
+    for (int oy = (iy - 2 + 1) / 2; oy <= iy / 2; ++oy) {
+      if (oy < 0 || oy >= Ho || iy - 2 * oy > 2 || iy < 2 * oy) continue;
+      for (int ox = (ix - 2 + 1) / 2; ox <= ix / 2; ++ox) {
+        if (ox < 0 || ox >= Wo || ix - 2 * ox > 2 || ix < 2 * ox) continue;
+        const uint32_t t = (uint32_t)((iy - 2 * oy) * 3 + (ix - 2 * ox));
+        const long o = ((img * Ho + oy) * Wo + ox) * C + c0;
+        const uint2 av = *reinterpret_cast<const uint2*>(am + o);
+        const uint4 gv = *reinterpret_cast<const uint4*>(g + o);
+        const uint32_t g32[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t ak = ((k < 4 ? av.x : av.y) >> (8 * (k & 3))) & 0xffu;
+          if (ak == t) acc[k] += bf2f((bf16_t)((g32[k >> 1] >> (16 * (k & 1))) & 0xffff));
+        }
+      }
+    }
+    *reinterpret_cast<uint4*>(dx + pix * C + c0) = make_uint4(pack2bf(acc[0], acc[1]), pack2bf(acc[2], acc[3]),
+                                                              pack2bf(acc[4], acc[5]), pack2bf(acc[6], acc[7]));
+  }
+}
+
+struct GapArgs {
+  const bf16_t* x;      // [N][hw][C] last block output (pre final BN)
+  const float* coef;    // final BN forward coefficients [cap][4][cmax] (nullptr: identity, v1)
+  const int* img_slot;
+  bf16_t* feat;         // [N][C] bf16
+  const float* dfeat;   // bwd: [N][C] fp32 (dL/dfeat)
+  float* sums;          // bwd: final-BN backward sums [cap][2][cmax]
+  const float* bcoef;   // bwd apply: A, B, C
+  bf16_t* out;          // bwd apply: gradient at x
+  int hw, C, cmax;
+};
+
+// one workgroup per image, thread = channel group of 8 (C <= 2048)
+__global__ __launch_bounds__(256) void cg_gap_kernel(GapArgs a) {
+  const int img = blockIdx.x, slot = a.img_slot[img];
+  const float* co = a.coef ? a.coef + (long)slot * 4 * a.cmax : nullptr;
+  for (int c0 = threadIdx.x * 8; c0 < a.C; c0 += blockDim.x * 8) {
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < a.hw; ++p) {
+      const uint4 v = *reinterpret_cast<const uint4*>(a.x + ((long)img * a.hw + p) * a.C + c0);
+      const uint32_t w32[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float f = bf2f((bf16_t)((w32[k >> 1] >> (16 * (k & 1))) & 0xffff));
+        if (co) f = fmaxf(f * co[c0 + k] + co[a.cmax + c0 + k], 0.f);
+        s[k] += f;
+      }
+    }
+    const float inv = 1.f / (float)a.hw;
+    *reinterpret_cast<uint4*>(a.feat + (long)img * a.C + c0) =
+        make_uint4(pack2bf(s[0] * inv, s[1] * inv), pack2bf(s[2] * inv, s[3] * inv), pack2bf(s[4] * inv, s[5] * inv),
+                   pack2bf(s[6] * inv, s[7] * inv));
+  }
+}
+
+// final-BN backward sums: dz = dfeat/hw * [BN(x) > 0]; sum dz, sum dz*xhat
+__global__ __launch_bounds__(256) void cg_gap_bwd_reduce_kernel(GapArgs a) {
+  const int img = blockIdx.x, slot = a.img_slot[img];
+  const float* co = a.coef + (long)slot * 4 * a.cmax;
+  float* su = a.sums + (long)slot * 2 * a.cmax;
+  const float inv_hw = 1.f / (float)a.hw;
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+    const float g = a.dfeat[(long)img * a.C + c] * inv_hw;
+    const float sc = co[c], sh = co[a.cmax + c], mu = co[2 * a.cmax + c], iv = co[3 * a.cmax + c];
+    float s = 0.f, q = 0.f;
+    for (int p = 0; p < a.hw; ++p) {
+      const float xv = bf2f(a.x[((long)img * a.hw + p) * a.C + c]);
+      if (xv * sc + sh > 0.f) {
+        s += g;
+        q += g * (xv - mu) * iv;
+      }
+    }
+    atomicAdd(su + c, s);
+    atomicAdd(su + a.cmax + c, q);
+  }
+}
+
+__global__ __launch_bounds__(256) void cg_gap_bwd_apply_kernel(GapArgs a) {
+  const int img = blockIdx.x, slot = a.img_slot[img];
+  const float* co = a.coef ? a.coef + (long)slot * 4 * a.cmax : nullptr;
+  const float* bc = a.bcoef ? a.bcoef + (long)slot * 4 * a.cmax : nullptr;
+  const float inv_hw = 1.f / (float)a.hw;
+  const long n = (long)a.hw * a.C;
+  for (long i = threadIdx.x; i < n; i += blockDim.x) {
+    const int c = (int)(i % a.C);
+    const long o = (long)img * n + i;
+    const float xv = bf2f(a.x[o]);
+    const float g = a.dfeat[(long)img * a.C + c] * inv_hw;
+    float r;
+    if (co) {
+      const float dz = (xv * co[c] + co[a.cmax + c] > 0.f) ? g : 0.f;
+      r = bc[c] * dz + bc[a.cmax + c] * xv + bc[2 * a.cmax + c];
+    } else {
+      r = xv > 0.f ? g : 0.f;  // v1: the last block's ReLU
+    }
+    a.out[o] = f2bf(r);
+  }
+}
+
+// one wave per image: logits [N][ld] fp32 (+ bias) -> loss / correct / dlogits bf16 [N][ld] / dbias
+__global__ __launch_bounds__(256) void cg_softmax_ce_kernel(const float* __restrict__ logits, int ld, int ncls,
+                                                             const int* __restrict__ labels,
+                                                             const int* __restrict__ img_slot,
+                                                             const float* __restrict__ state, long s_mstride, int b_off,
+                                                             float* __restrict__ grads, long g_mstride,
+                                                             const float* __restrict__ cnt, float* __restrict__ loss,
+                                                             float* __restrict__ correct, bf16_t* __restrict__ dl,
+                                                             long nimg) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long img = (long)blockIdx.x * 4 + wave;
+  if (img >= nimg) return;
+  const int slot = img_slot[img];
+  const float* bias = state + (long)slot * s_mstride + b_off;
+  const float* lr = logits + img * ld;
+  float mx = -3.0e38f;
+  int arg = 0;
+  for (int j = lane; j < ncls; j += 64) {
+    const float v = lr[j] + bias[j];
+    if (v > mx) {
+      mx = v;
+      arg = j;
+    }
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float om = __shfl_xor(mx, o, 64);
+    const int oa = __shfl_xor(arg, o, 64);
+    if (om > mx || (om == mx && oa < arg)) {
+      mx = om;
+      arg = oa;
+    }
+  }
+  float se = 0.f;
+  for (int j = lane; j < ncls; j += 64) se += __expf(lr[j] + bias[j] - mx);
+  se = wave_sum(se);
+  const float lse = mx + __logf(se);
+  const int lab = labels[img];
+  const float bsz = cnt[slot];
+  float* gb = grads + (long)slot * g_mstride + b_off;
+  for (int j = lane; j < ld; j += 64) {
+    float d = 0.f;
+    if (j < ncls) {
+      d = (__expf(lr[j] + bias[j] - lse) - (j == lab ? 1.f : 0.f)) / bsz;
+      atomicAdd(gb + j, d);
+    }
+    dl[img * ld + j] = f2bf(d);
+  }
+  if (lane == 0) {
+    atomicAdd(loss + slot, (lse - (lr[lab] + bias[lab])) / bsz);
+    atomicAdd(correct + slot, arg == lab ? 1.f : 0.f);
+  }
+}
+
+// per-channel sum / second moment of a [N][hw][C] tensor into [cap][2][cmax] (BN statistics of a tensor no conv
+// epilogue produced, e.g. the max-pool output); thread = 8 fixed channels, LDS reduction, one atomic per WG
+__global__ __launch_bounds__(256) void cg_chan_stats_kernel(const bf16_t* __restrict__ x, const int* __restrict__ img_slot,
+                                                             float* __restrict__ sums, int hw, int C, int cmax) {
+  __shared__ float acc[2][2048];
+  const int img = blockIdx.x, slot = img_slot[img];
+  for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) (&acc[0][0])[(i / C) * 2048 + i % C] = 0.f;
+  __syncthreads();
+  const long n8 = (long)hw * C / 8;
+  const long i0 = (long)blockIdx.y * blockDim.x + threadIdx.x, st = (long)gridDim.y * blockDim.x;
+  if (i0 < n8 && (st * 8) % C == 0) {
+    const int c0 = (int)((i0 * 8) % C);
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, q[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (long i = i0; i < n8; i += st) {
+      const uint4 v = *reinterpret_cast<const uint4*>(x + (long)img * hw * C + i * 8);
+      const uint32_t w32[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float f = bf2f((bf16_t)((w32[k >> 1] >> (16 * (k & 1))) & 0xffff));
+        s[k] += f;
+        q[k] += f * f;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      atomicAdd(&acc[0][c0 + k], s[k]);
+      atomicAdd(&acc[1][c0 + k], q[k]);
+    }
+  }
+  __syncthreads();
+  float* su = sums + (long)slot * 2 * cmax;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    atomicAdd(su + c, acc[0][c]);
+    atomicAdd(su + cmax + c, acc[1][c]);
+  }
+}
+
+}  // namespace
+
+DTF_API int dtf_cg_chan_stats(const bf16_t* x, const int* img_slot, float* sums, int nimg, int hw, int C, int cmax,
+                              hipStream_t stream) {
+  if (nimg <= 0) return 0;
+  if (C > 2048 || C % 8 || 2048 % C) return -2;
+  hipLaunchKernelGGL(cg_chan_stats_kernel, dim3(nimg, 8), dim3(256), 0, stream, x, img_slot, sums, hw, C, cmax);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_bnfin_args_size() { return (int)sizeof(BnFinArgs); }
+DTF_API int dtf_ew_args_size() { return (int)sizeof(EwArgs); }
+DTF_API int dtf_gap_args_size() { return (int)sizeof(GapArgs); }
+
+DTF_API int dtf_cg_weight_prep(const float* state, long s_mstride, const int* table, int nconv, const int* slots,
+                               int nslots, bf16_t* wf, bf16_t* wd, long w_mstride, hipStream_t stream) {
+  if (nconv <= 0 || nslots <= 0) return 0;
+  hipLaunchKernelGGL(cg_weight_prep_kernel, dim3(nconv, 32, nslots), dim3(256), 0, stream, state, s_mstride, table,
+                     slots, wf, wd, w_mstride);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_cg_dense_prep(const float* state, long s_mstride, int w_off, int ncls, int npad, int C,
+                              const int* slots, int nslots, bf16_t* out, long o_mstride, hipStream_t stream) {
+  if (nslots <= 0) return 0;
+  hipLaunchKernelGGL(cg_dense_prep_kernel, dim3(256, nslots), dim3(256), 0, stream, state, s_mstride, w_off, ncls,
+                     npad, C, slots, out, o_mstride);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_cg_bn_final(const BnFinArgs* a, int backward, int nslots, hipStream_t stream) {
+  if (nslots <= 0) return 0;
+  dim3 grid((a->C + 255) / 256, nslots);
+  if (backward)
+    hipLaunchKernelGGL(cg_bn_bwd_final_kernel, grid, dim3(256), 0, stream, *a);
+  else
+    hipLaunchKernelGGL(cg_bn_fwd_final_kernel, grid, dim3(256), 0, stream, *a);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_cg_bn_bwd_apply(const EwArgs* a, hipStream_t stream) {
+  if (a->nimg <= 0) return 0;
+  const long n8 = a->hw * a->C / 8;
+  long split = (4096 + a->nimg - 1) / a->nimg;
+  const long ms = (n8 + 255) / 256;
+  if (split > ms) split = ms;
+  if (split < 1) split = 1;
+  hipLaunchKernelGGL(cg_bn_bwd_apply_kernel, dim3((unsigned)a->nimg, (unsigned)split), dim3(256), 0, stream, *a);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_cg_prep_input(const float* x, bf16_t* y, long npix, int c_in, hipStream_t stream) {
+  long blocks = (npix + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(cg_prep_input_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, y, npix, c_in);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_cg_maxpool(const bf16_t* x, bf16_t* y, uint8_t* am, const bf16_t* g, bf16_t* dx, int N, int H, int W,
+                           int Ho, int Wo, int C, int backward, hipStream_t stream) {
+  if (C % 8) return -2;
+  const long total8 = (long)N * (backward ? H * W : Ho * Wo) * C / 8;
+  long blocks = (total8 + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  if (backward)
+    hipLaunchKernelGGL(cg_maxpool_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, g, am, dx, H, W, Ho, Wo, C,
+                       total8);
+  else
+    hipLaunchKernelGGL(cg_maxpool_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, y, am, H, W, Ho, Wo, C,
+                       total8);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_cg_gap(const GapArgs* a, int which, int nimg, hipStream_t stream) {
+  if (nimg <= 0) return 0;
+  if (which == 0)
+    hipLaunchKernelGGL(cg_gap_kernel, dim3(nimg), dim3(256), 0, stream, *a);
+  else if (which == 1)
+    hipLaunchKernelGGL(cg_gap_bwd_reduce_kernel, dim3(nimg), dim3(256), 0, stream, *a);
+  else
+    hipLaunchKernelGGL(cg_gap_bwd_apply_kernel, dim3(nimg), dim3(256), 0, stream, *a);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_cg_softmax_ce(const float* logits, int ld, int ncls, const int* labels, const int* img_slot,
+                              const float* state, long s_mstride, int b_off, float* grads, long g_mstride,
+                              const float* cnt, float* loss, float* correct, bf16_t* dl, long nimg,
+                              hipStream_t stream) {
+  if (nimg <= 0) return 0;
+  hipLaunchKernelGGL(cg_softmax_ce_kernel, dim3((unsigned)((nimg + 3) / 4)), dim3(256), 0, stream, logits, ld, ncls,
+                     labels, img_slot, state, s_mstride, b_off, grads, g_mstride, cnt, loss, correct, dl, nimg);
+  return DTF_CHECK_LAUNCH();
+}

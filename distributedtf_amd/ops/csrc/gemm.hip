@@ -20,7 +20,7 @@ typedef short s16x4_t __attribute__((ext_vector_type(4)));
 
 struct GemmGroup {
   long a_off, b_off, c_off;
-  int M, N, K, pad;
+  int M, N, K, Ms;  // Ms > 0: store only rows < Ms (operands may be padded past the real row count)
 };
 
 struct GemmArgs {
@@ -132,7 +132,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + 32 * wm + 16 * i + 4 * (lane >> 4) + r;
-        if (m >= gp.M) continue;
+        if (m >= (gp.Ms > 0 ? gp.Ms : gp.M)) continue;
         const long o = gp.c_off + (long)m * a.ldc + n;
         if constexpr (OUT == 0) {
           reinterpret_cast<float*>(a.C)[o] = acc[i][jn][r];

@@ -83,6 +83,7 @@ def _register():
                               c_void_p])
     reg("dtf_cg_bn_final", [P(BnFinArgs), c_int, c_int, c_void_p])
     reg("dtf_cg_bn_bwd_apply", [P(EwArgs), c_void_p])
+    reg("dtf_cg_bn_relu_apply", [P(EwArgs), c_void_p])
     reg("dtf_cg_prep_input", [c_void_p, c_void_p, c_long, c_int, c_void_p])
     reg("dtf_cg_maxpool", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                            c_int, c_int, c_void_p])
@@ -220,6 +221,9 @@ class _ImageNetPlan:
         self.y0 = torch.empty(N, H1, H1, cfg.num_filters, dtype=bf, device=dev)
         self.am0 = torch.empty(N, H2, H2, cfg.num_filters, dtype=torch.uint8, device=dev)
         self.xs, self.h1, self.h2, self.sc = [torch.empty(N, H2, H2, cfg.num_filters, dtype=bf, device=dev)], [], [], []
+        # materialised BN+ReLU outputs (the operands every consumer conv stages as-is, and the weight-gradient
+        # inputs): ax = relu(BN1(x)), a1 = relu(BN2(h1)), a2 = relu(BN3(h2))
+        self.ax, self.a1, self.a2 = [], [], []
         hw, cin = H2, cfg.num_filters
         self.geo = []  # per block: (H_in, H_out, cin, f, fout)
         for blk in prog.blocks:
@@ -227,6 +231,9 @@ class _ImageNetPlan:
             ho = hw // blk.stride
             self.h1.append(torch.empty(N, hw, hw, c1.cout, dtype=bf, device=dev))
             self.h2.append(torch.empty(N, ho, ho, c2.cout, dtype=bf, device=dev))
+            self.ax.append(torch.empty(N, hw, hw, cin, dtype=bf, device=dev))
+            self.a1.append(torch.empty(N, hw, hw, c1.cout, dtype=bf, device=dev))
+            self.a2.append(torch.empty(N, ho, ho, c2.cout, dtype=bf, device=dev))
             self.sc.append(torch.empty(N, ho, ho, c3.cout, dtype=bf, device=dev) if blk.proj is not None else None)
             self.xs.append(torch.empty(N, ho, ho, c3.cout, dtype=bf, device=dev))
             self.geo.append((hw, ho, cin, c1.cout, c3.cout))
@@ -376,6 +383,15 @@ class _ImageNetPlan:
         self._hold(a)
         self._add(ops.lib().dtf_cg_bn_final, ctypes.byref(a), int(backward), len(self.slots))
 
+    def ew(self, fn, h, out, coef, hw, C, dz=None, add=None):
+        """Elementwise BN apply: fn = dtf_cg_bn_relu_apply (out = relu(BN(h))) or dtf_cg_bn_bwd_apply
+        (out = A dz + B h + C [+ add])."""
+        a = EwArgs()
+        a.dz, a.h, a.add, a.out = _p(dz), _p(h), _p(add), _p(out)
+        a.coef, a.img_slot, a.hw, a.C, a.cmax, a.nimg = _p(coef), _p(self.img_slot), hw * hw, C, CMAX, self.N
+        self._hold(a)
+        self._add(fn, ctypes.byref(a))
+
     # ------------------------------------------------------------------------------------------ program
     def _build(self):
         be, e, prog, cfg = self.be, self.e, self.be.prog, self.be.cfg
@@ -403,16 +419,20 @@ class _ImageNetPlan:
             b1, b2, b3 = blk.bns
             c1, c2, c3 = blk.convs
             x = self.xs[i]
+            relu = L.dtf_cg_bn_relu_apply
             self.bn_final(b1, hi, False)
+            self.ew(relu, x, self.ax[i], self.cf(b1), hi, cin)
             if blk.proj is not None:
-                self.conv(blk.proj, x, self.sc[i], hi, mode=1, c_in=self.cf(b1), epi=0)
-            self.conv(c1, x, self.h1[i], hi, mode=1, c_in=self.cf(b1), epi=4, st=self.sf(b2))
+                self.conv(blk.proj, self.ax[i], self.sc[i], hi, mode=0, epi=0)
+            self.conv(c1, self.ax[i], self.h1[i], hi, mode=0, epi=4, st=self.sf(b2))
             self.bn_final(b2, hi, False)
-            self.conv(c2, self.h1[i], self.h2[i], hi, mode=1, c_in=self.cf(b2), epi=4, st=self.sf(b3))
+            self.ew(relu, self.h1[i], self.a1[i], self.cf(b2), hi, f)
+            self.conv(c2, self.a1[i], self.h2[i], hi, mode=0, epi=4, st=self.sf(b3))
             self.bn_final(b3, ho, False)
+            self.ew(relu, self.h2[i], self.a2[i], self.cf(b3), ho, f)
             nxt = prog.blocks[i + 1].bns[0] if i + 1 < nblk else prog.final_bn
             res = self.sc[i] if blk.proj is not None else x
-            self.conv(c3, self.h2[i], self.xs[i + 1], ho, mode=1, c_in=self.cf(b3), epi=5, res=res, st=self.sf(nxt))
+            self.conv(c3, self.a2[i], self.xs[i + 1], ho, mode=0, epi=5, res=res, st=self.sf(nxt))
         fb = prog.final_bn
         HL = self.HL
         self.bn_final(fb, HL, False)
@@ -458,33 +478,34 @@ class _ImageNetPlan:
             b1, b2, b3 = blk.bns
             c1, c2, c3 = blk.convs
             x, h1, h2 = self.xs[i], self.h1[i], self.h2[i]
+            bwd = L.dtf_cg_bn_bwd_apply
+            # conv3: dz3 = dgrad(g) masked by BN3(h2) (+ BN3 reductions); dh2 = BN3-backward(dz3, h2)
             dz3 = self.tmp("dz3", ho, f)
             self.conv(c3, gcur, dz3, ho, mode=0, epi=6, xm=h2, c_ep=self.cf(b3), st=self.sb(b3), dgrad=True)
             self.bn_final(b3, ho, True)
-            self.wgrad(c3, h2, gcur, ho, mode_x=1, c_x=self.cf(b3), mode_dy=0)
+            dh2 = self.tmp("dh2", ho, f)
+            self.ew(bwd, h2, dh2, self.cb(b3), ho, f, dz=dz3)
+            self.wgrad(c3, self.a2[i], gcur, ho)
+            # conv2 (3x3 / s): dz2 = dgrad(dh2) masked by BN2(h1); dh1 = BN2-backward(dz2, h1)
             dz2 = self.tmp("dz2", hi, f)
-            self.conv(c2, dz3, dz2, ho, mode=2, c_in=self.cb(b3), x2=h2, epi=6, xm=h1, c_ep=self.cf(b2),
-                      st=self.sb(b2), dgrad=True)
+            self.conv(c2, dh2, dz2, ho, mode=0, epi=6, xm=h1, c_ep=self.cf(b2), st=self.sb(b2), dgrad=True)
             self.bn_final(b2, hi, True)
-            self.wgrad(c2, h1, dz3, hi, mode_x=1, c_x=self.cf(b2), mode_dy=2, c_dy=self.cb(b3), dy2=h2)
+            dh1 = self.tmp("dh1", hi, f)
+            self.ew(bwd, h1, dh1, self.cb(b2), hi, f, dz=dz2)
+            self.wgrad(c2, self.a1[i], dh2, hi)
             pd = None
             if blk.proj is not None:
                 pd = self.tmp("pd", hi, cin)
                 self.conv(blk.proj, gcur, pd, ho, mode=0, epi=0, dgrad=True)
-                self.wgrad(blk.proj, x, gcur, hi, mode_x=1, c_x=self.cf(b1), mode_dy=0)
+                self.wgrad(blk.proj, self.ax[i], gcur, hi)
+            # conv1: dz1 = (dgrad(dh1) [+ projection dgrad]) masked by BN1(x); g_in = BN1-backward(dz1, x) [+ g]
             dz1 = self.tmp("dz1", hi, cin)
-            self.conv(c1, dz2, dz1, hi, mode=2, c_in=self.cb(b2), x2=h1, epi=6 | (1 if pd is not None else 0),
-                      res=pd, xm=x, c_ep=self.cf(b1), st=self.sb(b1), dgrad=True)
+            self.conv(c1, dh1, dz1, hi, mode=0, epi=6 | (1 if pd is not None else 0), res=pd, xm=x,
+                      c_ep=self.cf(b1), st=self.sb(b1), dgrad=True)
             self.bn_final(b1, hi, True)
-            self.wgrad(c1, x, dz2, hi, mode_x=1, c_x=self.cf(b1), mode_dy=2, c_dy=self.cb(b2), dy2=h1)
-            gname = "gA" if (i % 2 == 0) else "gB"
-            gnext = self.tmp(gname, hi, cin)
-            ew = EwArgs()
-            ew.dz, ew.h, ew.add, ew.out = _p(dz1), _p(x), (None if blk.proj is not None else _p(gcur)), _p(gnext)
-            ew.coef, ew.img_slot, ew.hw, ew.C, ew.cmax, ew.nimg = _p(self.cb(b1)), _p(self.img_slot), hi * hi, cin, \
-                CMAX, N
-            self._hold(ew)
-            self._add(L.dtf_cg_bn_bwd_apply, ctypes.byref(ew))
+            self.wgrad(c1, self.ax[i], dh1, hi)
+            gnext = self.tmp("gA" if (i % 2 == 0) else "gB", hi, cin)
+            self.ew(bwd, x, gnext, self.cb(b1), hi, cin, dz=dz1, add=None if blk.proj is not None else gcur)
             gcur = gnext
         # ---- stem: max-pool backward, stem wgrad (padded input, 3 real channels)
         dy0 = self.tmp("dy0", H1, cfg.num_filters)

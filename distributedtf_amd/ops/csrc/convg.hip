@@ -101,10 +101,31 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   }
   const bf16_t* wbase = a.w + (long)slot * a.w_mstride + a.w_off;
   const long img_elems = (long)a.Hi * a.Wi * Ci;
+  // gather position of this thread's chunk: for Ci >= 32 a 32-wide k-step lies inside one tap, so (ky, kx, ci)
+  // advance incrementally (no division in the loop); Ci < 32 (the channel-padded stem) decomposes k per step
+  int g_ky = 0, g_kx = 0, g_ci = 8 * cB;
+  const bool inc = Ci >= 32;
   auto load_b = [&](int k0, uint4 (&v)[2], uint4 (&v2)[2], int& cch, unsigned& okb) {
     const int k = k0 + 8 * cB;
-    const int tap = k >> a.log2ci, ci0 = k & (Ci - 1);
-    const int ky = tap / a.kw, kx = tap - ky * a.kw;
+    int ky, kx, ci0;
+    if (inc) {
+      ky = g_ky;
+      kx = g_kx;
+      ci0 = g_ci;
+      g_ci += 32;
+      if (g_ci >= Ci) {
+        g_ci -= Ci;
+        if (++g_kx == a.kw) {
+          g_kx = 0;
+          ++g_ky;
+        }
+      }
+    } else {
+      const int tap = k >> a.log2ci;
+      ci0 = k & (Ci - 1);
+      ky = tap / a.kw;
+      kx = tap - ky * a.kw;
+    }
     cch = ci0;
     okb = 0;
 #pragma unroll
@@ -340,6 +361,18 @@ __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
   const bool xcol_ok = xcol < K;
   const int dcol = o0 + 8 * cc;
   const bool dcol_ok = dcol < Co;
+  const float r_hw = 1.0f / (float)HWo, r_w = 1.0f / (float)a.Wo;
+  auto divmod = [](int n, int d, float rd, int& q, int& r) {  // exact for n < 2^24
+    q = (int)((float)n * rd);
+    r = n - q * d;
+    if (r < 0) {
+      --q;
+      r += d;
+    } else if (r >= d) {
+      ++q;
+      r -= d;
+    }
+  };
   auto load = [&](int pk0, uint4 (&dv)[2], uint4 (&dv2)[2], uint4 (&xv)[2], unsigned& okm) {
     okm = 0;
 #pragma unroll
@@ -347,8 +380,9 @@ __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
       const int p = pk0 + kr + 16 * j;
       const bool pin = p < p1;
       const int pp = pin ? p : p0;
-      const int img = pp / HWo, rem = pp - img * HWo;
-      const int oy = rem / a.Wo, ox = rem - oy * a.Wo;
+      int img, rem, oy, ox;
+      divmod(pp, HWo, r_hw, img, rem);
+      divmod(rem, a.Wo, r_w, oy, ox);
       dv[j] = dv2[j] = xv[j] = make_uint4(0, 0, 0, 0);
       if (pin && dcol_ok) {
         dv[j] = *reinterpret_cast<const uint4*>(a.dy + (long)pp * Co + dcol);
@@ -479,6 +513,8 @@ DTF_API int dtf_convg_fwd(const CgArgs* a, int tc, int mode, int epi, int trans,
 #define CG_ALL_TC(M_, E_, T_) CG_CASE(64, M_, E_, T_) CG_CASE(128, M_, E_, T_)
   // forward: identity (stem / v1) or BN+ReLU prologue; stats epilogue; optional residual
   CG_ALL_TC(0, 4, false)
+  CG_ALL_TC(0, 5, false)
+  CG_ALL_TC(0, 7, false)
   CG_ALL_TC(1, 4, false)
   CG_ALL_TC(1, 0, false)
   CG_ALL_TC(1, 5, false)

@@ -168,6 +168,30 @@ __global__ __launch_bounds__(256) void cg_bn_bwd_apply_kernel(EwArgs a) {
   }
 }
 
+// a = relu(BN(h)) with the member's forward coefficients (the activation every consumer conv stages as-is)
+__global__ __launch_bounds__(256) void cg_bn_relu_apply_kernel(EwArgs a) {
+  const int img = blockIdx.x;
+  const int slot = a.img_slot[img];
+  const float* co = a.coef + (long)slot * 4 * a.cmax;
+  const long base = (long)img * a.hw * a.C;
+  const long n8 = a.hw * a.C / 8;
+  for (long i = (long)blockIdx.y * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.y * blockDim.x) {
+    const long o = base + i * 8;
+    const int c0 = (int)((i * 8) % a.C);
+    const uint4 hv = *reinterpret_cast<const uint4*>(a.h + o);
+    const uint32_t h32[4] = {hv.x, hv.y, hv.z, hv.w};
+    uint32_t r[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = c0 + 2 * q;
+      const float v0 = fmaxf(bf2f((bf16_t)(h32[q] & 0xffff)) * co[c] + co[a.cmax + c], 0.f);
+      const float v1 = fmaxf(bf2f((bf16_t)(h32[q] >> 16)) * co[c + 1] + co[a.cmax + c + 1], 0.f);
+      r[q] = pack2bf(v0, v1);
+    }
+    *reinterpret_cast<uint4*>(a.out + o) = make_uint4(r[0], r[1], r[2], r[3]);
+  }
+}
+
 __global__ __launch_bounds__(256) void cg_prep_input_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
                                                              long npix, int c_in) {
   const long stride = (long)gridDim.x * blockDim.x;
@@ -467,6 +491,17 @@ DTF_API int dtf_cg_bn_bwd_apply(const EwArgs* a, hipStream_t stream) {
   if (split > ms) split = ms;
   if (split < 1) split = 1;
   hipLaunchKernelGGL(cg_bn_bwd_apply_kernel, dim3((unsigned)a->nimg, (unsigned)split), dim3(256), 0, stream, *a);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_cg_bn_relu_apply(const EwArgs* a, hipStream_t stream) {
+  if (a->nimg <= 0) return 0;
+  const long n8 = a->hw * a->C / 8;
+  long split = (4096 + a->nimg - 1) / a->nimg;
+  const long ms = (n8 + 255) / 256;
+  if (split > ms) split = ms;
+  if (split < 1) split = 1;
+  hipLaunchKernelGGL(cg_bn_relu_apply_kernel, dim3((unsigned)a->nimg, (unsigned)split), dim3(256), 0, stream, *a);
   return DTF_CHECK_LAUNCH();
 }
 

@@ -265,14 +265,17 @@ class _ImageNetPlan:
         self._keep.append(obj)
         return obj
 
-    def _pix_work(self, hw_out, co, tc):
+    def _pix_work(self, hw_grid, co, tc, classes=(0,)):
+        """(slot, p0, p1, o0 | class << 16) tiles of 128 grid pixels x tc output channels per member; a
+        transposed (stride-2) dgrad runs every parity class (py*2 + px) over the dy-resolution grid."""
         items = []
         for s, n in zip(self.slots, self.sizes):
             f = self.first[s]
-            p_end = (f + n) * hw_out * hw_out
-            for p0 in range(f * hw_out * hw_out, p_end, 128):
-                for o0 in range(0, co, tc):
-                    items.append([s, p0, min(p0 + 128, p_end), o0])
+            p_end = (f + n) * hw_grid * hw_grid
+            for cls in classes:
+                for p0 in range(f * hw_grid * hw_grid, p_end, 128):
+                    for o0 in range(0, co, tc):
+                        items.append([s, p0, min(p0 + 128, p_end), o0 | (cls << 16)])
         return self._hold(torch.tensor(items, dtype=torch.int32, device=self.be.dev))
 
     def _wgrad_work(self, hw_out, co, K):
@@ -342,7 +345,7 @@ class _ImageNetPlan:
             trans = 1 if c.stride > 1 else 0
         a.log2ci = _log2(a.Ci)
         tc = 128 if a.Co >= 128 else 64
-        work = self._pix_work(hw_out, a.Co, tc)
+        work = self._pix_work(hw_in, a.Co, tc, classes=(0, 1, 2, 3)) if trans else self._pix_work(hw_out, a.Co, tc)
         a.work = _p(work)
         self._hold(a)
         self._add(ops.lib().dtf_convg_fwd, ctypes.byref(a), tc, mode, epi, trans, work.shape[0])

@@ -71,10 +71,24 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   extern __shared__ float dyn[];  // transform coefficients: MODE 1: 2*Ci, MODE 2: 3*Ci
   __shared__ float acc_lds[2][TC];
   const int4 wk = a.work[blockIdx.x];
-  const int slot = wk.x, p0 = wk.y, p1 = wk.z, o0 = wk.w;
+  const int slot = wk.x, p0 = wk.y, p1 = wk.z;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wr = wave & 1, wc = wave >> 1;
-  const int Ci = a.Ci, K = a.kh * a.kw * Ci;
+  const int Ci = a.Ci, Kfull = a.kh * a.kw * Ci;
+  // TRANS (stride-2 data gradient): the workgroup covers one output parity class (py, px); pixels are indexed on
+  // the class grid (= the gathered dy grid) and only the taps with (parity + tap - pad) even contribute:
+  // ky = ky0, ky0 + 2, ..  -> K = nky * nkx * Ci instead of kh * kw * Ci with 3/4 of the products zero.
+  int o0 = wk.w, py = 0, px = 0, ky0 = 0, kx0 = 0, nky = a.kh, nkx = a.kw;
+  if constexpr (TRANS) {
+    o0 = wk.w & 0xffff;
+    py = (wk.w >> 17) & 1;
+    px = (wk.w >> 16) & 1;
+    ky0 = (a.pad - py) & 1;
+    kx0 = (a.pad - px) & 1;
+    nky = (a.kh - ky0 + 1) >> 1;
+    nkx = (a.kw - kx0 + 1) >> 1;
+  }
+  const int K = nky * nkx * Ci;
   if constexpr (MODE != 0) {
     const float* cb = a.c_in + (long)slot * 4 * a.cmax;
     for (int i = tid; i < Ci; i += 256) {
@@ -88,7 +102,8 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   const int cB = tid & 3;
   int pix_img[2], pix_y[2], pix_x[2];
   bool pix_ok[2];
-  const int HWo = a.Ho * a.Wo;
+  const int GH = TRANS ? a.Hi : a.Ho, GW = TRANS ? a.Wi : a.Wo;  // pixel grid of the work items
+  const int HWo = GH * GW;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int p = p0 + (tid >> 2) + 64 * j;
@@ -96,47 +111,51 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
     const int pp = pix_ok[j] ? p : p0;
     pix_img[j] = pp / HWo;
     const int rem = pp - pix_img[j] * HWo;
-    pix_y[j] = rem / a.Wo;
-    pix_x[j] = rem - pix_y[j] * a.Wo;
+    pix_y[j] = rem / GW;
+    pix_x[j] = rem - pix_y[j] * GW;
   }
   const bf16_t* wbase = a.w + (long)slot * a.w_mstride + a.w_off;
   const long img_elems = (long)a.Hi * a.Wi * Ci;
   // gather position of this thread's chunk: for Ci >= 32 a 32-wide k-step lies inside one tap, so (ky, kx, ci)
   // advance incrementally (no division in the loop); Ci < 32 (the channel-padded stem) decomposes k per step
-  int g_ky = 0, g_kx = 0, g_ci = 8 * cB;
+  int g_ky = ky0, g_kx = kx0, g_ci = 8 * cB;
   const bool inc = Ci >= 32;
-  auto load_b = [&](int k0, uint4 (&v)[2], uint4 (&v2)[2], int& cch, unsigned& okb) {
-    const int k = k0 + 8 * cB;
-    int ky, kx, ci0;
+  const int kstep = TRANS ? 2 : 1;
+  int cur_ky = 0, cur_kx = 0, cur_ci = 0;  // position of this thread's chunk in the current k-step
+  auto next_pos = [&](int k0) {
     if (inc) {
-      ky = g_ky;
-      kx = g_kx;
-      ci0 = g_ci;
+      cur_ky = g_ky;
+      cur_kx = g_kx;
+      cur_ci = g_ci;
       g_ci += 32;
       if (g_ci >= Ci) {
         g_ci -= Ci;
-        if (++g_kx == a.kw) {
-          g_kx = 0;
-          ++g_ky;
+        g_kx += kstep;
+        if (g_kx >= a.kw) {
+          g_kx = kx0;
+          g_ky += kstep;
         }
       }
-    } else {
+    } else {  // Ci < 32 only occurs for the (non-transposed) channel-padded stem
+      const int k = k0 + 8 * cB;
       const int tap = k >> a.log2ci;
-      ci0 = k & (Ci - 1);
-      ky = tap / a.kw;
-      kx = tap - ky * a.kw;
+      cur_ci = k & (Ci - 1);
+      cur_ky = tap / a.kw;
+      cur_kx = tap - cur_ky * a.kw;
     }
+  };
+  auto load_b = [&](int k0, uint4 (&v)[2], uint4 (&v2)[2], int& cch, unsigned& okb) {
+    const int k = k0 + 8 * cB;
+    const int ky = cur_ky, kx = cur_kx, ci0 = cur_ci;
     cch = ci0;
     okb = 0;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       int gy, gx;
       bool ok = pix_ok[j] && k < K;
-      if constexpr (TRANS) {
-        const int qy = pix_y[j] + ky - a.pad, qx = pix_x[j] + kx - a.pad;
-        ok = ok && qy >= 0 && qx >= 0 && (qy % a.stride) == 0 && (qx % a.stride) == 0;
-        gy = qy / a.stride;
-        gx = qx / a.stride;
+      if constexpr (TRANS) {  // class pixel (2*qy + py): dy row (py + ky - pad) / 2 + qy (even numerator)
+        gy = pix_y[j] + ((py + ky - a.pad) >> 1);
+        gx = pix_x[j] + ((px + kx - a.pad) >> 1);
       } else {
         gy = pix_y[j] * a.stride + ky - a.pad;
         gx = pix_x[j] * a.stride + kx - a.pad;
@@ -183,11 +202,12 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   // A (weights): rows o0 + r, r = (tid >> 2) + 64 j (j < TC / 64)
   constexpr int AJ = TC / 64;
   auto load_a = [&](int k0, uint4 (&v)[AJ]) {
+    const int k = k0 + 8 * cB;
+    const int kcol = TRANS ? (cur_ky * a.kw + cur_kx) * Ci + cur_ci : k;  // column in the full [o][K] row
 #pragma unroll
     for (int j = 0; j < AJ; ++j) {
       const int r = (tid >> 2) + 64 * j;
-      const int k = k0 + 8 * cB;
-      v[j] = (o0 + r < a.Co && k < K) ? *reinterpret_cast<const uint4*>(wbase + (long)(o0 + r) * K + k)
+      v[j] = (o0 + r < a.Co && k < K) ? *reinterpret_cast<const uint4*>(wbase + (long)(o0 + r) * Kfull + kcol)
                                       : make_uint4(0, 0, 0, 0);
     }
   };
@@ -205,6 +225,7 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   uint4 ra[AJ], rb[2], rb2[2];
   int cch;
   unsigned okb;
+  next_pos(0);
   load_a(0, ra);
   load_b(0, rb, rb2, cch, okb);
   store_a(sa[0], ra);
@@ -215,6 +236,7 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
     const bool more = ks + 1 < nk;
     int ncch = 0;
     if (more) {
+      next_pos(32 * (ks + 1));
       load_a(32 * (ks + 1), ra);
       load_b(32 * (ks + 1), rb, rb2, ncch, okb);
     }
@@ -257,7 +279,12 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
     for (int n = 0; n < 4; ++n) {
       const int p = p0 + wc * 64 + 16 * n + (lane & 15);
       if (p >= p1 || oc >= a.Co) continue;
-      const long o = (long)p * a.Co + oc;
+      long pf = p;  // output pixel (full resolution)
+      if constexpr (TRANS) {
+        const int img = p / HWo, rem = p - img * HWo, qy = rem / GW, qx = rem - qy * GW;
+        pf = ((long)img * a.Ho + 2 * qy + py) * a.Wo + 2 * qx + px;
+      }
+      const long o = pf * a.Co + oc;
       float v[4] = {acc[m][n][0], acc[m][n][1], acc[m][n][2], acc[m][n][3]};
       if constexpr (EPI & 1) {
         const uint2 rr = *reinterpret_cast<const uint2*>(a.res + o);

@@ -131,20 +131,17 @@ class HipImageNetBackend:
             raise ValueError("image size must be a multiple of 32")
         self.prog, self.cfg = prog, cfg
         cap = engine.capacity
-        # bf16 weights: forward [o][tap][i] (stem input padded 3 -> 8) + flipped/transposed dgrad layout
-        self.fwd_off, self.dgr_off, table = {}, {}, []
-        off = 0
+        # bf16 weights: the fused optimizer writes a bf16 shadow of every member row in the same pass as the
+        # update; every conv (forward [o][tap][i] rows, and the data gradient reading the same layout k-major)
+        # reads it in place.  Only the stem needs a channel-padded (3 -> 8) copy.
         for c in prog.convs:
-            cin_pad = 8 if c.idx == prog.stem else c.cin
-            self.fwd_off[c.idx] = off
-            off += c.cout * c.k * c.k * cin_pad
-            if c.idx != prog.stem:
-                self.dgr_off[c.idx] = off
-                off += c.cout * c.k * c.k * c.cin
-            table.append([c.off, c.cout, c.cin, c.k, cin_pad, self.fwd_off[c.idx], self.dgr_off.get(c.idx, -1), 0])
-        self.wtot = (off + 63) // 64 * 64
-        self.w = torch.zeros(cap, self.wtot, dtype=torch.bfloat16, device=self.dev)
-        self.conv_table = torch.tensor(table, dtype=torch.int32, device=self.dev)
+            assert c.off % 8 == 0, "conv weights must be 16-byte aligned in the shadow row"
+        self.shadow = torch.zeros(cap, engine.Pp, dtype=torch.bfloat16, device=self.dev)
+        st = prog.convs[prog.stem]
+        self.wtot = (st.cout * st.k * st.k * 8 + 63) // 64 * 64
+        self.w = torch.zeros(cap, self.wtot, dtype=torch.bfloat16, device=self.dev)  # padded stem
+        self.conv_table = torch.tensor([[st.off, st.cout, st.cin, st.k, 8, 0, -1, 0]], dtype=torch.int32,
+                                       device=self.dev)
         self.ncls = cfg.num_classes
         assert self.ncls <= NPAD_CLS and cfg.final_size % 32 == 0
         self.dense = torch.zeros(cap, NPAD_CLS * cfg.final_size, dtype=torch.bfloat16, device=self.dev)
@@ -157,10 +154,13 @@ class HipImageNetBackend:
         self.use_graph = os.environ.get("DTF_HIP_GRAPH", "1") == "1"
 
     def on_params_changed(self, slots):
-        pass  # weights are re-derived from the fp32 master rows at the start of every step
+        slots = list(slots)
+        if slots:  # rows changed outside the optimizer (init, exploit import): refresh their bf16 shadow
+            e = self.e
+            self._rows = ops.shadow_refresh(e.state, self.shadow, slots, e.Pp, e.P)
 
     def shadow_weights(self):
-        return None
+        return self.shadow
 
     def plan(self, slots, sizes):
         key = (tuple(slots), tuple(sizes))
@@ -296,7 +296,7 @@ class _ImageNetPlan:
     def _args(self):
         be, e = self.be, self.e
         a = CgArgs()
-        a.w_mstride = be.wtot
+        a.w_mstride = e.Pp
         a.grads, a.g_mstride = _p(e.grads), e.Pp
         a.cmax = CMAX
         return a
@@ -322,13 +322,14 @@ class _ImageNetPlan:
         pad = (k - 1) // 2
         a = self._args()
         a.x, a.x2, a.y, a.res, a.xm = _p(src), _p(x2), _p(out), _p(res), _p(xm)
-        a.w = _p(be.w)
+        a.w, a.w_off = _p(be.shadow), c.off
+        if ci == be.prog.stem:
+            a.w, a.w_mstride, a.w_off = _p(be.w), be.wtot, 0
         a.c_in, a.c_ep, a.st_out = _p(c_in), _p(c_ep), _p(st)
         a.kh = a.kw = k
         if not dgrad:
             cin = 8 if ci == be.prog.stem else c.cin
             hw_out = (hw_in + c.stride - 1) // c.stride
-            a.w_off = be.fwd_off[ci]
             a.Hi = a.Wi = hw_in
             a.Ci, a.Co = cin, c.cout
             a.Ho = a.Wo = hw_out
@@ -337,15 +338,15 @@ class _ImageNetPlan:
         else:
             # gathered = dy at the conv's output resolution; output = dx at its input resolution
             hw_out = hw_in * c.stride
-            a.w_off = be.dgr_off[ci]
             a.Hi = a.Wi = hw_in
             a.Ci, a.Co = c.cout, c.cin
             a.Ho = a.Wo = hw_out
             a.stride, a.pad = c.stride, k - 1 - pad
-            trans = 1 if c.stride > 1 else 0
+            trans = (1 if c.stride > 1 else 0) | 2  # | 2: A operand k-major from the forward layout
         a.log2ci = _log2(a.Ci)
         tc = 128 if a.Co >= 128 else 64
-        work = self._pix_work(hw_in, a.Co, tc, classes=(0, 1, 2, 3)) if trans else self._pix_work(hw_out, a.Co, tc)
+        work = (self._pix_work(hw_in, a.Co, tc, classes=(0, 1, 2, 3)) if trans & 1
+                else self._pix_work(hw_out, a.Co, tc))
         a.work = _p(work)
         self._hold(a)
         self._add(ops.lib().dtf_convg_fwd, ctypes.byref(a), tc, mode, epi, trans, work.shape[0])
@@ -401,8 +402,8 @@ class _ImageNetPlan:
         L = ops.lib()
         N, H = self.N, self.H
         ns = len(self.slots)
-        self._add(L.dtf_cg_weight_prep, _p(e.state), e.S, _p(be.conv_table), len(prog.convs), _p(self.slots_t), ns,
-                  _p(be.w), _p(be.w), be.wtot)
+        self._add(L.dtf_cg_weight_prep, _p(e.state), e.S, _p(be.conv_table), 1, _p(self.slots_t), ns,
+                  _p(be.w), _p(be.w), be.wtot)  # padded stem only; every other conv reads the shadow
         self._add(L.dtf_cg_dense_prep, _p(e.state), e.S, prog.dense_w_off, be.ncls, NPAD_CLS, cfg.final_size,
                   _p(self.slots_t), ns, _p(be.dense), NPAD_CLS * cfg.final_size)
         self._add("zero", be.sums)
@@ -537,7 +538,8 @@ class _ImageNetPlan:
             elif fn == "gemm":
                 args[0].launch(st)
             elif fn == "optim":
-                ops.fused_optimizer(e.state, e.grads, e.hyper, e.Pp, e.P, e.n_reg, shadow=None, zero_grads=True)
+                ops.fused_optimizer(e.state, e.grads, e.hyper, e.Pp, e.P, e.n_reg, shadow=self.be.shadow,
+                                    zero_grads=True)
             elif fn == "step":
                 advance_steps(e, self.slots_long)
             else:

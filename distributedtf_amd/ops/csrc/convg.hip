@@ -63,10 +63,16 @@ constexpr int RP = 40;    // [rows][32] tile pitch (+16 B)
 // ---------------------------------------------------------------------------------------------- fwd / dgrad
 // MODE: 0 identity, 1 relu(x*s + t), 2 A*x + B*x2 + C.   EPI: bit0 residual, bit1 mask, bit2 stats (fwd: y, y^2;
 // with bit1: dz, dz*xhat).  TRANS: transposed (dgrad, stride > 1) gather.
-template <int TC, int MODE, int EPI, bool TRANS>
+// AKM (data gradient): the A operand (rows = dx channels i, k = (tap', dy channel o)) is read straight from the
+// FORWARD weight layout W[o][tap][i] (k-major: 8 consecutive i per 16-byte load, fragments via
+// ds_read_b64_tr_b16), so no transposed weight copy exists.
+constexpr int KPA = 128 + 8;  // [32][TC] k-major A tile pitch
+
+template <int TC, int MODE, int EPI, bool TRANS, bool AKM = false>
 __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   constexpr int MT = TC / 32;  // MFMA row tiles per wave (wave covers TC/2 rows)
-  __shared__ __attribute__((aligned(16))) bf16_t sa[2][TC * RP];
+  constexpr int SA = (TC * RP > 32 * KPA) ? TC * RP : 32 * KPA;
+  __shared__ __attribute__((aligned(16))) bf16_t sa[2][SA];
   __shared__ __attribute__((aligned(16))) bf16_t sb[2][TP * RP];
   extern __shared__ float dyn[];  // transform coefficients: MODE 1: 2*Ci, MODE 2: 3*Ci
   __shared__ float acc_lds[2][TC];
@@ -201,19 +207,40 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   };
   // A (weights): rows o0 + r, r = (tid >> 2) + 64 j (j < TC / 64)
   constexpr int AJ = TC / 64;
+  constexpr int ACH = TC / 8;  // AKM: 8-row chunks per k row
   auto load_a = [&](int k0, uint4 (&v)[AJ]) {
     const int k = k0 + 8 * cB;
-    const int kcol = TRANS ? (cur_ky * a.kw + cur_kx) * Ci + cur_ci : k;  // column in the full [o][K] row
+    if constexpr (AKM) {
+      // k rows kr = tid / ACH + (256 / ACH) j; all 32 k of a step share one tap (Ci >= 32)
+      const int kk = a.kh * a.kw;
+      const int tapf = kk - 1 - (cur_ky * a.kw + cur_kx);  // forward tap of the flipped tap'
+      const int obase = cur_ci - 8 * cB;                     // first dy channel of this k step
 #pragma unroll
-    for (int j = 0; j < AJ; ++j) {
-      const int r = (tid >> 2) + 64 * j;
-      v[j] = (o0 + r < a.Co && k < K) ? *reinterpret_cast<const uint4*>(wbase + (long)(o0 + r) * Kfull + kcol)
-                                      : make_uint4(0, 0, 0, 0);
+      for (int j = 0; j < AJ; ++j) {
+        const int kr = tid / ACH + (256 / ACH) * j, ch = tid % ACH;
+        const int oc = obase + kr;
+        v[j] = (k0 + kr < K && o0 + 8 * ch < a.Co)
+                   ? *reinterpret_cast<const uint4*>(wbase + ((long)oc * kk + tapf) * a.Co + o0 + 8 * ch)
+                   : make_uint4(0, 0, 0, 0);
+      }
+    } else {
+      const int kcol = TRANS ? (cur_ky * a.kw + cur_kx) * Ci + cur_ci : k;  // column in the full [o][K] row
+#pragma unroll
+      for (int j = 0; j < AJ; ++j) {
+        const int r = (tid >> 2) + 64 * j;
+        v[j] = (o0 + r < a.Co && k < K) ? *reinterpret_cast<const uint4*>(wbase + (long)(o0 + r) * Kfull + kcol)
+                                        : make_uint4(0, 0, 0, 0);
+      }
     }
   };
   auto store_a = [&](bf16_t* dst, const uint4 (&v)[AJ]) {
 #pragma unroll
-    for (int j = 0; j < AJ; ++j) *reinterpret_cast<uint4*>(dst + ((tid >> 2) + 64 * j) * RP + 8 * cB) = v[j];
+    for (int j = 0; j < AJ; ++j) {
+      if constexpr (AKM)
+        *reinterpret_cast<uint4*>(dst + (tid / ACH + (256 / ACH) * j) * KPA + 8 * (tid % ACH)) = v[j];
+      else
+        *reinterpret_cast<uint4*>(dst + ((tid >> 2) + 64 * j) * RP + 8 * cB) = v[j];
+    }
   };
   f32x4_t acc[MT][4];
 #pragma unroll
@@ -242,9 +269,18 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
     }
     bf16x8_t fa[MT], fb[4];
 #pragma unroll
-    for (int m = 0; m < MT; ++m)
-      fa[m] = *reinterpret_cast<const bf16x8_t*>(sa[cur] + (wr * (TC / 2) + 16 * m + (lane & 15)) * RP +
-                                                 8 * (lane >> 4));
+    for (int m = 0; m < MT; ++m) {
+      if constexpr (AKM) {
+        const int g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
+        const int rb = wr * (TC / 2) + 16 * m + 4 * p4;
+        const s16x4_t lo = ds_read_tr(sa[cur] + (8 * g + q) * KPA + rb);
+        const s16x4_t hi = ds_read_tr(sa[cur] + (8 * g + 4 + q) * KPA + rb);
+        fa[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      } else {
+        fa[m] = *reinterpret_cast<const bf16x8_t*>(sa[cur] + (wr * (TC / 2) + 16 * m + (lane & 15)) * RP +
+                                                   8 * (lane >> 4));
+      }
+    }
 #pragma unroll
     for (int n = 0; n < 4; ++n)
       fb[n] = *reinterpret_cast<const bf16x8_t*>(sb[cur] + (wc * 64 + 16 * n + (lane & 15)) * RP + 8 * (lane >> 4));
@@ -528,13 +564,20 @@ DTF_API int dtf_cg_args_size() { return (int)sizeof(CgArgs); }
 
 // flags: tc (64 | 128), mode (0..2), epi (0..7), trans (0/1)
 DTF_API int dtf_convg_fwd(const CgArgs* a, int tc, int mode, int epi, int trans, int nwork, hipStream_t stream) {
+  // trans bit1 (value 2): A operand from the forward weight layout (data gradient, AKM)
+  const int akm = (trans >> 1) & 1;
+  trans &= 1;
   if (nwork <= 0) return 0;
   if ((a->Ci & (a->Ci - 1)) != 0 || a->Ci < 8 || (a->Co & 3) != 0) return -2;
   const size_t dyn = (size_t)(mode == 0 ? 0 : (mode == 1 ? 2 : 3)) * a->Ci * sizeof(float);
   dim3 grid(nwork), block(256);
 #define CG_CASE(TC_, M_, E_, T_)                                                                  \
-  if (tc == TC_ && mode == M_ && epi == E_ && trans == T_) {                                      \
+  if (tc == TC_ && mode == M_ && epi == E_ && trans == T_ && !akm) {                              \
     hipLaunchKernelGGL((convg_fwd_kernel<TC_, M_, E_, T_>), grid, block, dyn, stream, *a);       \
+    return DTF_CHECK_LAUNCH();                                                                    \
+  }                                                                                               \
+  if (tc == TC_ && mode == M_ && epi == E_ && trans == T_ && akm) {                               \
+    hipLaunchKernelGGL((convg_fwd_kernel<TC_, M_, E_, T_, true>), grid, block, dyn, stream, *a); \
     return DTF_CHECK_LAUNCH();                                                                    \
   }
 #define CG_ALL_TC(M_, E_, T_) CG_CASE(64, M_, E_, T_) CG_CASE(128, M_, E_, T_)

@@ -51,6 +51,8 @@ class ConvArgs(ctypes.Structure):
         ("st_in", c_void_p), ("st_in_b", c_void_p), ("st_ep", c_void_p), ("st_x", c_void_p), ("st_out", c_void_p),
         ("cnt", c_void_p), ("Hi", c_int), ("Wi", c_int), ("Ho", c_int), ("Wo", c_int), ("rows", c_int),
         ("cin_real", c_int), ("slab", c_void_p),
+        ("x3", c_void_p), ("xout", c_void_p), ("rslab", c_void_p), ("rtab", c_void_p), ("r_goff", c_long),
+        ("r_c", c_int), ("r_nblk", c_int), ("n_main", c_int),
     ]
 
 
@@ -389,7 +391,10 @@ class _StepPlan:
         self.side_reduce = dev.type == "cuda" and os.environ.get("DTF_SIDE_REDUCE", "0") == "1"
         self.side_stream = torch.cuda.Stream(device=dev) if self.side_reduce else None
         self.launches = []
+        self._pending_slab = None  # (slab ptr, reduce table, C, grad offset) of the last fused launch
+        self._slab_flip = 0
         self._build()
+        assert self._pending_slab is None, "every dW slab must be reduced before the optimizer"
         self.graph = None
 
     # -------------------------------------------------------------------- work lists
@@ -571,11 +576,18 @@ class _StepPlan:
         self._add(lib.dtf_conv_wgrad, ctypes.byref(a), cin, c.cout, c.stride, c.k, mode_x, mode_dy, work.shape[0], lds)
         self._keep(a)
 
-    def _conv_bwd_fused(self, ci, dy, dz_out, x, mode_dy, dy2=None, dy_bn=None, x_bn=None, res=None, ident_x=False):
-        """dgrad + wgrad of a stride-1 3x3 C->C conv in one launch (see conv_bwd_fused_kernel)."""
+    def _conv_bwd_fused(self, ci, dy, dz_out, x, mode_dy, dy2=None, dy_bn=None, x_bn=None, res=None, ident_x=False,
+                        dy3=None, dy_out=None):
+        """dgrad + wgrad of a stride-1 3x3 C->C conv in one launch (see conv_bwd_fused_kernel).
+
+        ``mode_dy`` 3: dY = BN-backward(dy, dy2) + dy3 (the previous block's BN1 backward and the identity
+        shortcut folded into the staging); ``dy_out`` materialises that dY (needed downstream).  The dW slabs
+        of the PREVIOUS fused launch are reduced by trailing workgroups of this one when small enough
+        (``_piggyback``); the rest by a standalone dw_slab_reduce."""
         be, L = self.be, self.be.L
         c = L.prog.convs[ci]
         assert c.stride == 1 and c.k == 3 and c.cin == c.cout
+        assert (mode_dy == 3) == (dy3 is not None)
         C, H = c.cin, x.shape[1]
         rows = None
         for r in (8, 4, 2):
@@ -584,14 +596,18 @@ class _StepPlan:
                 break
         # the fused kernel's geometry is compile-time: W = H = 512 / C, 8-row bands
         assert rows == 8 and H == 512 // C and x.shape[2] == H, (C, H, rows)
+        for t in (dy, dy2, dy3, dy_out, dz_out, x, res):
+            assert t is None or tuple(t.shape) == (self.N, H, H, C), (t.shape, C, H)
         bands = H // rows
         n_wg = self._fused_nwg(C, bands)
         work = self._work_iters(bands, n_wg)
         a = self._base_args()
         a.x, a.x2, a.y, a.xm, a.res = _p(dy), _p(dy2), _p(dz_out), _p(x), _p(res)
+        a.x3, a.xout = _p(dy3), _p(dy_out)
         a.w, a.w_off = _p(be.wd), L.dgr_off[ci]
         a.work = _p(work)
         a.g_off = c.off
+        a.n_main = work.shape[0]
         if dy_bn is not None:
             a.in_gamma, a.in_beta = self._bn(dy_bn)
             a.st_in, a.st_in_b = _p(be.st_f(dy_bn)), _p(be.st_b(dy_bn))
@@ -605,19 +621,51 @@ class _StepPlan:
         lib = ops.lib()
         slab = os.environ.get("DTF_DW_SLAB", "1") == "1"
         side = slab and self.side_reduce
-        if slab:
+        n_red = 0
+        if slab and not side:
+            # ping-pong slab buffers: this launch writes one while its trailing workgroups reduce the other
+            pend = self._pending_slab
+            if pend is not None and self._piggyback(pend):
+                buf, red, rc, goff = pend
+                a.rslab, a.rtab, a.r_c, a.r_goff = buf, _p(red), rc, goff
+                a.r_nblk = self._slab_elems(rc) // 32
+                n_red = a.r_nblk * red.shape[0]
+                self._pending_slab = None
+            else:
+                self._flush_slab()
+            a.slab = _p(self._slab(self._slab_floats())[self._slab_flip])
+            self._slab_flip ^= 1
+        elif side:
             # side-stream reductions run concurrently with later layers: every layer needs its own slab region
-            a.slab = _p(self._layer_slab(work.shape[0] * self._slab_elems(C)) if side else self._slab(self._slab_floats()))
+            a.slab = _p(self._layer_slab(work.shape[0] * self._slab_elems(C)))
         epi = int(res is not None) | (2 if ident_x else 0)
-        self._add(lib.dtf_conv_bwd_fused, ctypes.byref(a), C, mode_dy, epi, work.shape[0], lds)
+        self._add(lib.dtf_conv_bwd_fused, ctypes.byref(a), C, mode_dy, epi, work.shape[0] + n_red, lds)
         self._keep(a)
         if slab:
             red = self._slab_table(work)
-            args = (a.slab, _p(red), red.shape[0], _p(self.e.grads), self.e.Pp, c.off, C)
             if side:
-                self._add("side", (lib.dtf_dw_slab_reduce, args))
+                self._add("side", (lib.dtf_dw_slab_reduce, (a.slab, _p(red), red.shape[0], _p(self.e.grads),
+                                                            self.e.Pp, c.off, C)))
             else:
-                self._add(lib.dtf_dw_slab_reduce, *args)
+                self._pending_slab = (a.slab, red, C, c.off)
+
+    def _piggyback(self, pend):
+        """Reduce the previous launch's slabs inside the next fused launch when that adds few workgroups
+        (the trailing workgroups carry the fused kernel's register budget: low occupancy)."""
+        if os.environ.get("DTF_SLAB_PIGGYBACK", "1") != "1":
+            return False
+        _, red, rc, _ = pend
+        limit = int(os.environ.get("DTF_PIGGYBACK_MAX_WG", "512"))
+        return (self._slab_elems(rc) // 32) * red.shape[0] <= limit
+
+    def _flush_slab(self):
+        """Standalone reduction of a pending slab (no later fused launch can take it)."""
+        pend = self._pending_slab
+        if pend is None:
+            return
+        buf, red, rc, goff = pend
+        self._add(ops.lib().dtf_dw_slab_reduce, buf, _p(red), red.shape[0], _p(self.e.grads), self.e.Pp, goff, rc)
+        self._pending_slab = None
 
     @staticmethod
     def _slab_elems(C):
@@ -647,9 +695,10 @@ class _StepPlan:
         return t
 
     def _slab(self, n):
-        if getattr(self, "slab_buf", None) is None or self.slab_buf.numel() < n:
-            assert getattr(self, "slab_buf", None) is None, "slab must be sized once per plan"
-            self.slab_buf = torch.empty(max(n, 1), dtype=torch.float32, device=self.be.dev)
+        """The plan's two ping-pong slab buffers (sized once for the largest fused layer)."""
+        if getattr(self, "slab_buf", None) is None:
+            self.slab_buf = [torch.empty(max(n, 1), dtype=torch.float32, device=self.be.dev) for _ in range(2)]
+        assert self.slab_buf[0].numel() >= n, "slab must be sized once per plan"
         return self.slab_buf
 
     def _slab_table(self, work):
@@ -725,6 +774,9 @@ class _StepPlan:
         self._add(lib.dtf_head_bwd_apply, _p(self.xs[-1]), _p(self.dfeat), _p(g_cur), _p(self.img_slot), _p(e.state),
                   e.S, ha.gamma_off, ha.beta_off, _p(be.st_f(fb)), _p(be.st_b(fb)), _p(self.cnt), hw,
                   cfg.final_size, N)
+        fused = os.environ.get("DTF_FUSED_BWD", "1") == "1"
+        fold = fused and os.environ.get("DTF_FOLD_BNBWD", "1") == "1"
+        pend = None  # deferred BN1-backward of the block just processed: (dz1, x, add, out, bn1)
         for i in range(nblk - 1, -1, -1):
             blk = prog.blocks[i]
             bn1, bn2 = blk.bns
@@ -732,9 +784,15 @@ class _StepPlan:
             Hi, Ho = x.shape[1], h.shape[1]
             T = self.tmp[Ho]
             ca, cb = blk.convs
-            fused = os.environ.get("DTF_FUSED_BWD", "1") == "1"
             # conv_b: dgrad -> dz2 (mask by BN2(h), BN2 reductions); wgrad
-            if fused:
+            if fused and pend is not None:
+                # the previous block's g = BN1-backward(dz1, x) [+ g] is computed while staging conv_b's dY
+                # and written out once (band interiors) for the projection / next BN-backward
+                dz1p, xp, addp, outp, bn1p = pend
+                self._conv_bwd_fused(cb, dz1p, T["dz2"], h, mode_dy=3 if addp is not None else 2, dy2=xp,
+                                     dy3=addp, dy_out=outp, dy_bn=bn1p, x_bn=bn2)
+                g_cur, pend = outp, None
+            elif fused:
                 self._conv_bwd_fused(cb, g_cur, T["dz2"], h, mode_dy=0, x_bn=bn2)
             else:
                 self._conv_dgrad(cb, g_cur, T["dz2"], Ho, mode=0, epi=2, xm=h, ep_bn=bn2)
@@ -755,24 +813,33 @@ class _StepPlan:
                 self._conv_wgrad(ca, x, T["dz2"], mode_x=1, mode_dy=2, x_bn=bn1, dy_bn=bn2, dy2=h)
             # g_in = BN1-backward(dz1, x) [+ g_out if identity shortcut]
             g_next = Tin["g"][1] if g_cur is Tin["g"][0] else Tin["g"][0]
-            ba = BnBwdArgs()
-            ba.dz, ba.x, ba.add, ba.out = _p(Tin["dz1"]), _p(x), (None if blk.proj is not None else _p(g_cur)), \
-                _p(g_next)
-            ba.img_slot, ba.params, ba.p_mstride = _p(self.img_slot), _p(e.state), e.S
-            ba.gamma_off = self._bn(bn1)[0]
-            ba.st_f, ba.st_b, ba.cnt = _p(be.st_f(bn1)), _p(be.st_b(bn1)), _p(self.cnt)
-            ba.hw, ba.C, ba.nimg = Hi * Hi, x.shape[3], N
-            self._keep(ba)
-            self._add(lib.dtf_bn_bwd_apply, ctypes.byref(ba))
+            add = None if blk.proj is not None else g_cur
+            if fold and i > 0:
+                pend = (Tin["dz1"], x, add, g_next, bn1)
+            else:
+                self._bn_bwd_apply(Tin["dz1"], x, add, g_next, bn1)
             g_cur = g_next
         # stem wgrad (input = padded image, real channels 3)
         self._conv_wgrad(prog.stem, self.xin16, g_cur, mode_x=0, mode_dy=0, cin_real=cfg.in_channels)
         # BN parameter gradients from the backward reductions
+        self._flush_slab()
         self._add(lib.dtf_bn_running_update, _p(e.state), e.S, 3 * e.Pp, _p(be.bn_table_t), len(L.bn_table),
                   _p(be.stats[1]), be.stats_bn_stride, _p(self.slots_t), nslots, _p(self.cnt), _p(e.grads), e.Pp)
         # optimizer over every member row (+ zero grads), step counters
         self._add("optim", None)
         self._add("step", None)
+
+    def _bn_bwd_apply(self, dz, x, add, out, bn):
+        """out = BN-backward(dz, x) [+ add] (bn_bwd_apply_kernel)."""
+        be, e = self.be, self.e
+        ba = BnBwdArgs()
+        ba.dz, ba.x, ba.add, ba.out = _p(dz), _p(x), _p(add), _p(out)
+        ba.img_slot, ba.params, ba.p_mstride = _p(self.img_slot), _p(e.state), e.S
+        ba.gamma_off = self._bn(bn)[0]
+        ba.st_f, ba.st_b, ba.cnt = _p(be.st_f(bn)), _p(be.st_b(bn)), _p(self.cnt)
+        ba.hw, ba.C, ba.nimg = x.shape[1] * x.shape[2], x.shape[3], self.N
+        self._keep(ba)
+        self._add(ops.lib().dtf_bn_bwd_apply, ctypes.byref(ba))
 
     def _bn_ew(self, fn, n_hw_c, bn1, h1, bn2=None, h2=None, add=None, out=None, d=None):
         """bn_add_relu (forward, out=...) or bn_bwd_reduce (backward, d=...) of a v1 block / the v1 stem."""
@@ -883,6 +950,7 @@ class _StepPlan:
         self._bn_ew(lib.dtf_bn_bwd_reduce, (H * H, cfg.num_filters), prog.stem_bn, self.h0, d=d)
         self._conv_wgrad(prog.stem, self.xin16, d, mode_x=0, mode_dy=2, dy_bn=prog.stem_bn, dy2=self.h0,
                          cin_real=cfg.in_channels)
+        self._flush_slab()
         self._add(lib.dtf_bn_running_update, _p(e.state), e.S, 3 * e.Pp, _p(be.bn_table_t), len(L.bn_table),
                   _p(be.stats[1]), be.stats_bn_stride, _p(self.slots_t), nslots, _p(self.cnt), _p(e.grads), e.Pp)
         self._add("optim", None)

@@ -179,8 +179,10 @@ class TorchBackend:
 
     def __init__(self, engine: PopulationEngine):
         self.e = engine
-        if engine.device.type == "cuda" and os.environ.get("DTF_MIOPEN_FIND", "1") == "1":
-            # MIOpen: benchmark the conv solvers once per shape instead of immediate-mode heuristics
+        if engine.device.type == "cuda" and os.environ.get("DTF_MIOPEN_FIND", "0") == "1":
+            # MIOpen: benchmark the conv solvers once per shape instead of immediate-mode heuristics.  Off by
+            # default: on a cold MIOpen cache the bf16 backward find ran a solver that faulted the GPU
+            # ("illegal memory access" surfacing at MIOpen's next module load).
             torch.backends.cudnn.benchmark = True
 
     def on_params_changed(self, slots):

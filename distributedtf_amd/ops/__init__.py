@@ -40,8 +40,10 @@ def lib():
         return _LIB
     with _LOCK:
         if _LIB is None:
-            path = _build.LIB
-            if not os.path.isfile(path) or (os.environ.get("DTF_REBUILD") == "1" and _build.needs_build()):
+            # DTF_LIB: an alternative build of the same sources (e.g. timing-only ablation builds of tools/)
+            path = os.environ.get("DTF_LIB") or _build.LIB
+            if path == _build.LIB and (not os.path.isfile(path) or
+                                       (os.environ.get("DTF_REBUILD") == "1" and _build.needs_build())):
                 _build.build(verbose=False)
             if not os.path.isfile(path):
                 raise RuntimeError("distributedtf_amd kernel library missing: %s" % path)

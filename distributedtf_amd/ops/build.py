@@ -39,39 +39,39 @@ def hipcc() -> str:
     return "hipcc"
 
 
-def build(force: bool = False, verbose: bool = True, extra_flags=None) -> str:
-    if not force and not needs_build():
-        return LIB
+def build(force: bool = False, verbose: bool = True, extra_flags=None, out: str = LIB) -> str:
+    if not force and not needs_build(out):
+        return out
     objs = []
     procs = []
     for src in sources():
-        obj = os.path.join(CSRC, os.path.basename(src) + ".o")
+        obj = os.path.join(CSRC, os.path.basename(src) + ".%d.o" % os.getpid())
         cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
                "-Wno-unused-result", "-munsafe-fp-atomics"] + list(extra_flags or [])
         procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
         objs.append(obj)
     failed = False
     for src, p in procs:
-        out, _ = p.communicate()
+        log, _ = p.communicate()
         if p.returncode != 0:
             failed = True
-            sys.stderr.write(out.decode(errors="replace"))
+            sys.stderr.write(log.decode(errors="replace"))
             sys.stderr.write("\nhipcc failed on %s\n" % src)
-        elif verbose and out.strip():
-            sys.stderr.write(out.decode(errors="replace"))
+        elif verbose and log.strip():
+            sys.stderr.write(log.decode(errors="replace"))
     if failed:
         raise RuntimeError("kernel build failed")
-    tmp = LIB + ".tmp"
+    tmp = out + ".tmp"
     subprocess.check_call([hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", tmp] + objs)
-    os.replace(tmp, LIB)
+    os.replace(tmp, out)
     for o in objs:
         try:
             os.remove(o)
         except OSError:
             pass
     if verbose:
-        sys.stderr.write("built %s\n" % LIB)
-    return LIB
+        sys.stderr.write("built %s\n" % out)
+    return out
 
 
 if __name__ == "__main__":

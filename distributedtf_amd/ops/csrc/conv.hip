@@ -26,6 +26,9 @@
 #include "common.h"
 
 #define BN_EPS 1e-5f
+#ifndef DTF_ABL
+#define DTF_ABL 0  // timing-only ablation bits of conv_bwd_fused_kernel (tools/ablate.sh); 0 in real builds
+#endif
 #define NREP 8
 
 namespace {
@@ -61,6 +64,15 @@ struct ConvArgs {
   int rows;                 // rows per band (output rows for fwd/wgrad, dx rows for dgrad)
   int cin_real;             // wgrad: real input channels (stem: 3)
   float* slab;              // fused bwd: per-workgroup dW partials (plain stores; reduced by dw_slab_reduce)
+  // fused bwd extensions
+  const bf16_t* x3;         // MODE_DY 3: residual-stream gradient added after the BN-backward transform
+  bf16_t* xout;             // materialise the transformed dY (band interior rows) here (null: don't)
+  const float* rslab;       // trailing workgroups (blockIdx >= n_main) reduce these dW slabs of the PREVIOUS
+  const int4* rtab;         //   fused launch: rtab[m] = (first wg, n wgs, -, slot) per member
+  long r_goff;              //   gradient-row offset of that conv
+  int r_c;                  //   its channel count (0: no reduction role)
+  int r_nblk;               //   reduce workgroups per member (E / 32)
+  int n_main;               // workgroups of the convolution role
 };
 
 __device__ __forceinline__ const float* stats_row(const float* base, int slot) {
@@ -380,6 +392,23 @@ __device__ __forceinline__ uint4 xform8(uint4 v, uint4 v2, int c0, const float* 
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// MODE 2: coef[c]*x + coef[64+c]*h + coef[128+c]; MODE 3: the same + r (residual-stream gradient)
+template <int MODE>
+__device__ __forceinline__ uint4 xform8r(uint4 v, uint4 v2, uint4 v3, int c0, const float* __restrict__ coef) {
+  static_assert(MODE == 2 || MODE == 3, "BN-backward staging only");
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  const uint32_t h[4] = {v2.x, v2.y, v2.z, v2.w};
+  const uint32_t r[4] = {v3.x, v3.y, v3.z, v3.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = c0 + 2 * j;
+    f32x2_t t = unpk2(w[j]) * lds2(coef + c) + unpk2(h[j]) * lds2(coef + 64 + c) + lds2(coef + 128 + c);
+    if constexpr (MODE == 3) t += unpk2(r[j]);
+    w[j] = pk2(t);
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 // Compile-time tile geometry for a [RT][WP][C] (+8 pad per pixel) LDS tile of rows gy0..gy0+RT-1 and columns
 // -1..W of an H x W x C image.  Each thread owns MAXC 16-byte chunk slots (always the same 8 channels, since
 // 256 % (C/8) == 0); per slot: LDS offset, in-band global offset, and three bit masks (column/slot valid,
@@ -424,7 +453,7 @@ struct Stage {
     for (int j = 0; j < MAXC; ++j) {
       const uint32_t off = ((m >> j) & 1u) ? (uint32_t)(rb + goff[j]) : 0u;
       v[j] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(img) + off);
-      if constexpr (MODE == 2) v2[j] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(img2) + off);
+      if constexpr (MODE >= 2) v2[j] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(img2) + off);
     }
   }
   template <int MODE>
@@ -435,6 +464,23 @@ struct Stage {
       uint4 t = make_uint4(0, 0, 0, 0);
       if ((m >> j) & 1u) t = xform8<MODE>(v[j], v2[j], c0, coef);
       *reinterpret_cast<uint4*>(buf + loff[j]) = t;
+    }
+  }
+  // MODE 2 / 3 (BN-backward apply [+ residual v3]) staging that also writes the transformed band-interior
+  // chunks (tile rows 1..RT-2, image columns) to `out` (the image base; null: LDS only).
+  template <int MODE>
+  __device__ __forceinline__ void store_x(bf16_t* buf, const uint4 (&v)[MAXC], const uint4 (&v2)[MAXC],
+                                          const uint4 (&v3)[MAXC], unsigned m, const float* coef, bf16_t* out,
+                                          int gy0) const {
+    const unsigned interior = m & ~top & ~bot;
+    const int rb = gy0 * ROW * 2;
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      uint4 t = make_uint4(0, 0, 0, 0);
+      if ((m >> j) & 1u) t = xform8r<MODE>(v[j], v2[j], v3[j], c0, coef);
+      *reinterpret_cast<uint4*>(buf + loff[j]) = t;
+      if (out != nullptr && ((interior >> j) & 1u))
+        *reinterpret_cast<uint4*>(reinterpret_cast<char*>(out) + (uint32_t)(rb + goff[j])) = t;
     }
   }
 };
@@ -1030,6 +1076,36 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
   }
 }
 
+// One workgroup of the dW slab reduction (see dw_slab_reduce_kernel): 32 slab elements of member row `by`.
+template <int C>
+__device__ __forceinline__ void slab_reduce_wg(const float* __restrict__ slab, const int4* __restrict__ red,
+                                               float* __restrict__ grads, long g_mstride, long g_off, int bx, int by,
+                                               float* part /* [8][33] */) {
+  constexpr int MT = C / 16, NTN = 9 * C / 16, NJ = (NTN + 3) / 4, E = NJ * MT * 4 * 256;
+  const int el = threadIdx.x & 31, gg = threadIdx.x >> 5;
+  const int e = bx * 32 + el;
+  const int4 rd = red[by];
+  const float* p = slab + (long)rd.x * E + e;
+  float s0 = 0.f, s1 = 0.f;
+  int g = gg;
+  for (; g + 8 < rd.y; g += 16) {
+    s0 += p[(long)g * E];
+    s1 += p[(long)(g + 8) * E];
+  }
+  if (g < rd.y) s0 += p[(long)g * E];
+  part[gg * 33 + el] = s0 + s1;
+  __syncthreads();
+  if (gg != 0) return;
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sum += part[i * 33 + el];
+  const int r = e & 3, t = (e >> 2) & 255, m = (e >> 10) % MT, j = (e >> 10) / MT;  // slab [j][m][t][r]
+  const int wave = t >> 6, lane = t & 63, nt = wave + 4 * j;
+  if (nt >= NTN) return;
+  const int tap = (nt * 16) / C, ci = (nt * 16) % C + (lane & 15), co = m * 16 + 4 * (lane >> 4) + r;
+  grads[(long)rd.w * g_mstride + g_off + ((long)co * 9 + tap) * C + ci] += sum;
+}
+
 // ------------------------------------------------------------------ fused backward
 // One launch = dgrad AND wgrad of a stride-1 3x3 C->C conv of the CIFAR stages
 // (C = 16/32/64 at W = H = 512/C; 8-row bands), sharing the staged tiles: per
@@ -1070,6 +1146,14 @@ __global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
 #define FDBUF(i) (t0 + ((i) & 1) * 2 * TSZ)
 #define FXBUF(i) (t0 + TSZ + ((i) & 1) * 2 * TSZ)
 
+  if ((int)blockIdx.x >= a.n_main) {  // trailing workgroups: dW slab reduction of the previous fused launch
+    const int r = (int)blockIdx.x - a.n_main;
+    float* part = reinterpret_cast<float*>(smem);
+    if (a.r_c == 16) slab_reduce_wg<16>(a.rslab, a.rtab, a.grads, a.g_mstride, a.r_goff, r % a.r_nblk, r / a.r_nblk, part);
+    else if (a.r_c == 32) slab_reduce_wg<32>(a.rslab, a.rtab, a.grads, a.g_mstride, a.r_goff, r % a.r_nblk, r / a.r_nblk, part);
+    else if (a.r_c == 64) slab_reduce_wg<64>(a.rslab, a.rtab, a.grads, a.g_mstride, a.r_goff, r % a.r_nblk, r / a.r_nblk, part);
+    return;
+  }
   const int4 wk = a.work[blockIdx.x];
   const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1087,13 +1171,16 @@ __global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
   }
   St st;
   st.init();
-  uint4 dv[MAXC], dv2[MAXC], xv_[MAXC], unused[MAXC];
+  // MODE_DY 3: dY = BN-backward(x, x2) + x3; with xout the transformed band interior is also written out
+  constexpr bool XSTORE = MODE_DY >= 2;
+  uint4 dv[MAXC], dv2[MAXC], dv3[MAXC], xv_[MAXC], unused[MAXC];  // dv3: MODE_DY 3 only
   unsigned dm, xm;
+  int cimg = it0 / BANDS, cgy0 = (it0 % BANDS) * ROWS - 1;  // image / first tile row of the staged tile
   {
-    const int img = it0 / BANDS, gy0 = (it0 % BANDS) * ROWS - 1;
-    dm = xm = st.mask(gy0);
-    st.template load<MODE_DY>(dv, dv2, dm, a.x + img * IMG, a.x2 + img * IMG, gy0);
-    st.template load<1>(xv_, unused, xm, a.xm + img * IMG, nullptr, gy0);
+    dm = xm = st.mask(cgy0);
+    st.template load<MODE_DY == 3 ? 2 : MODE_DY>(dv, dv2, dm, a.x + cimg * IMG, a.x2 + cimg * IMG, cgy0);
+    if constexpr (MODE_DY == 3) st.template load<0>(dv3, unused, dm, a.x3 + cimg * IMG, nullptr, cgy0);
+    st.template load<1>(xv_, unused, xm, a.xm + cimg * IMG, nullptr, cgy0);
   }
   const float n_hw = a.cnt[slot] * (float)(H * W);
   make_coef<C, MODE_DY>(coef_d, a, slot, n_hw, a.st_in, a.st_in_b, a.in_gamma, a.in_beta);
@@ -1150,7 +1237,11 @@ __global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
   f32x2_t ssum[2] = {{0.f, 0.f}, {0.f, 0.f}}, ssq[2] = {{0.f, 0.f}, {0.f, 0.f}};
 
   __syncthreads();  // coefficients
-  st.template store<MODE_DY>(FDBUF(0), dv, dv2, dm, coef_d);
+  if constexpr (XSTORE)
+    st.template store_x<MODE_DY == 3 ? 3 : 2>(FDBUF(0), dv, dv2, dv3, dm, coef_d,
+                                              a.xout ? a.xout + cimg * IMG : nullptr, cgy0);
+  else
+    st.template store<MODE_DY>(FDBUF(0), dv, dv2, dm, coef_d);
   st.template store<1>(FXBUF(0), xv_, unused, xm, ecoef);
   __syncthreads();
   for (int k = 0; k < nit; ++k) {
@@ -1166,10 +1257,12 @@ __global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
       xres[i] = *reinterpret_cast<const uint2*>(a.xm + band + pofs[i]);
     }
     if (more) {
-      const int nimg = (it + 1) / BANDS, ngy0 = ((it + 1) % BANDS) * ROWS - 1;
-      dm = xm = st.mask(ngy0);
-      st.template load<MODE_DY>(dv, dv2, dm, a.x + nimg * IMG, a.x2 + nimg * IMG, ngy0);
-      st.template load<1>(xv_, unused, xm, a.xm + nimg * IMG, nullptr, ngy0);
+      cimg = (it + 1) / BANDS;
+      cgy0 = ((it + 1) % BANDS) * ROWS - 1;
+      dm = xm = st.mask(cgy0);
+      st.template load<MODE_DY == 3 ? 2 : MODE_DY>(dv, dv2, dm, a.x + cimg * IMG, a.x2 + cimg * IMG, cgy0);
+      if constexpr (MODE_DY == 3) st.template load<0>(dv3, unused, dm, a.x3 + cimg * IMG, nullptr, cgy0);
+      st.template load<1>(xv_, unused, xm, a.xm + cimg * IMG, nullptr, cgy0);
     }
     const bf16_t* dcur = FDBUF(k);
     const bf16_t* xcur = FXBUF(k);
@@ -1178,6 +1271,7 @@ __global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
     const f32x2_t sh0 = lds2(ecoef + 64 + ci0), sh1 = lds2(ecoef + 64 + ci0 + 2);
     const f32x2_t nm0 = lds2(ecoef + 128 + ci0), nm1 = lds2(ecoef + 128 + ci0 + 2);
     const f32x2_t iv0 = lds2(ecoef + 192 + ci0), iv1 = lds2(ecoef + 192 + ci0 + 2);
+    if constexpr (!(DTF_ABL & 4)) {  // timing-only ablation builds (tools/ablate.sh): skip the dgrad
 #pragma unroll
     for (int i = 0; i < MAXT; ++i) {
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
@@ -1205,7 +1299,9 @@ __global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
       ssq[0] += dz0 * (x0 * iv0 + nm0);
       ssq[1] += dz1 * (x1 * iv1 + nm1);
     }
+    }  // DTF_ABL & 4
     // ---- wgrad
+    if constexpr (!(DTF_ABL & 2)) {  // ablation: skip the wgrad
 #pragma unroll
     for (int ks = 0; ks < NK; ++ks) {
       bf16x8_t af[MT];
@@ -1227,8 +1323,13 @@ __global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
 #pragma unroll
         for (int m = 0; m < MT; ++m) wacc[j][m] = mfma16(af[m], bfr[j], wacc[j][m]);
     }
+    }  // DTF_ABL & 2
     if (more) {
-      st.template store<MODE_DY>(FDBUF(k + 1), dv, dv2, dm, coef_d);
+      if constexpr (XSTORE)
+        st.template store_x<MODE_DY == 3 ? 3 : 2>(FDBUF(k + 1), dv, dv2, dv3, dm, coef_d,
+                                                  a.xout ? a.xout + cimg * IMG : nullptr, cgy0);
+      else
+        st.template store<MODE_DY>(FDBUF(k + 1), dv, dv2, dm, coef_d);
       st.template store<1>(FXBUF(k + 1), xv_, unused, xm, ecoef);
     }
     __syncthreads();
@@ -1243,14 +1344,15 @@ __global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
   __syncthreads();
   if constexpr (!(EPI & 2)) flush_stats(a.st_out, acc_lds, slot, C);
   if (a.slab) {
-    // coalesced partial-sum slab [wg][j][m][r][256 threads]; dw_slab_reduce_kernel sums a member's slabs
-    float* sb = a.slab + (long)blockIdx.x * (NJ * MT * 4 * 256) + threadIdx.x;
+    // partial-sum slab [wg][j][m][256 threads][4]: one 16-byte store per lane per accumulator tile (a 1 KB
+    // row per wave instruction; the store tail is issue-bound); dw_slab_reduce sums a member's slabs
+    f32x4_t* sb = reinterpret_cast<f32x4_t*>(a.slab + (long)blockIdx.x * (NJ * MT * 4 * 256)) + threadIdx.x;
+    if constexpr (!(DTF_ABL & 1)) {
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
+      for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sb[((j * MT + m) * 4 + r) * 256] = wacc[j][m][r];
+        for (int m = 0; m < MT; ++m) sb[(j * MT + m) * 256] = wacc[j][m];
+    }
     return;
   }
   float* gb = a.grads + (long)slot * a.g_mstride + a.g_off;
@@ -1280,30 +1382,8 @@ template <int C>
 __global__ __launch_bounds__(256) void dw_slab_reduce_kernel(const float* __restrict__ slab,
                                                              const int4* __restrict__ red, float* __restrict__ grads,
                                                              long g_mstride, long g_off) {
-  constexpr int MT = C / 16, NTN = 9 * C / 16, NJ = (NTN + 3) / 4, E = NJ * MT * 4 * 256;
-  __shared__ float part[8][33];
-  const int el = threadIdx.x & 31, gg = threadIdx.x >> 5;
-  const int e = blockIdx.x * 32 + el;
-  const int4 rd = red[blockIdx.y];
-  const float* p = slab + (long)rd.x * E + e;
-  float s0 = 0.f, s1 = 0.f;
-  int g = gg;
-  for (; g + 8 < rd.y; g += 16) {
-    s0 += p[(long)g * E];
-    s1 += p[(long)(g + 8) * E];
-  }
-  if (g < rd.y) s0 += p[(long)g * E];
-  part[gg][el] = s0 + s1;
-  __syncthreads();
-  if (gg != 0) return;
-  float sum = 0.f;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) sum += part[i][el];
-  const int t = e & 255, r = (e >> 8) & 3, m = (e >> 10) % MT, j = (e >> 10) / MT;
-  const int wave = t >> 6, lane = t & 63, nt = wave + 4 * j;
-  if (nt >= NTN) return;
-  const int tap = (nt * 16) / C, ci = (nt * 16) % C + (lane & 15), co = m * 16 + 4 * (lane >> 4) + r;
-  grads[(long)rd.w * g_mstride + g_off + ((long)co * 9 + tap) * C + ci] += sum;
+  __shared__ float part[8 * 33];
+  slab_reduce_wg<C>(slab, red, grads, g_mstride, g_off, blockIdx.x, blockIdx.y, part);
 }
 
 template <typename KernelT>
@@ -1433,6 +1513,9 @@ DTF_API int dtf_conv_bwd_fused(const ConvArgs* args, int c, int mode_dy, int epi
   FUSED_CASE(16, 0, 0)  // conv_b: dy = residual grad, x = h (BN2)
   FUSED_CASE(32, 0, 0)
   FUSED_CASE(64, 0, 0)
+  FUSED_CASE(16, 3, 0)  // conv_b with the previous block's BN1-backward + residual folded into the dY staging
+  FUSED_CASE(32, 3, 0)
+  FUSED_CASE(64, 3, 0)
   FUSED_CASE(16, 2, 0)  // conv_a: dy = BN2-backward(dz2, h), x = block input (BN1)
   FUSED_CASE(32, 2, 0)
   FUSED_CASE(64, 2, 0)

@@ -31,12 +31,18 @@ def _relerr(a, b):
     return float((a.double() - b.double()).norm() / (b.double().norm() + 1e-30))
 
 
-@pytest.mark.parametrize("size,graph,fused,version", [(8, "1", "1", 2), (14, "1", "1", 2), (14, "0", "1", 2),
-                                                      (14, "1", "0", 2), (8, "0", "0", 2),
-                                                      (8, "1", "1", 1), (14, "0", "1", 1), (20, "1", "1", 1)])
-def test_hip_step_matches_reference(size, graph, fused, version, monkeypatch):
+@pytest.mark.parametrize("size,graph,fused,version,fold", [(8, "1", "1", 2, "1"), (14, "1", "1", 2, "1"),
+                                                           (14, "0", "1", 2, "1"), (14, "1", "1", 2, "0"),
+                                                           (14, "1", "0", 2, "1"), (8, "0", "0", 2, "1"),
+                                                           (8, "1", "1", 1, "1"), (14, "0", "1", 1, "1"),
+                                                           (20, "1", "1", 1, "1")])
+def test_hip_step_matches_reference(size, graph, fused, version, fold, monkeypatch):
+    """fold=1: BN1-backward folded into the next conv_b staging + dW slab reductions carried by the next fused
+    launch (hip_resnet._conv_bwd_fused); fold=0: standalone bn_bwd_apply / dw_slab_reduce launches."""
     monkeypatch.setenv("DTF_HIP_GRAPH", graph)
     monkeypatch.setenv("DTF_FUSED_BWD", fused)
+    monkeypatch.setenv("DTF_FOLD_BNBWD", fold)
+    monkeypatch.setenv("DTF_SLAB_PIGGYBACK", fold)
     torch.manual_seed(0)
     arch = ResNetArch(cifar_config(size, version=version))
     dev = torch.device("cuda")

@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 if [ -n "$TESTS" ]; then
-  timeout -k 10 400 python -u -m pytest $TESTS -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_targeted.log 2>&1
+  timeout -k 10 400 python -u -m pytest $TESTS -x -v -s --timeout 120 --timeout-method thread > gpurun_out/pytest_targeted.log 2>&1
   rc=$?; tail -25 gpurun_out/pytest_targeted.log
   [ $rc -ne 0 ] && { echo "targeted tests rc=$rc"; exit 1; }
 fi

@@ -541,7 +541,7 @@ class _ImageNetPlan:
                 ops.fused_optimizer(e.state, e.grads, e.hyper, e.Pp, e.P, e.n_reg, shadow=self.be.shadow,
                                     zero_grads=True)
             elif fn == "step":
-                advance_steps(e, self.slots_long)
+                advance_steps(e, self.slots_long, self.slots_t)
             else:
                 err = fn(*args, st)
                 if err != 0:

@@ -321,7 +321,7 @@ class _MnistPlan:
         self._launch(L.dtf_mnist_conv2_wgrad, self.w_c2w)
         self._launch(L.dtf_mnist_conv1_wgrad, self.w_c1w)
         ops.fused_optimizer(e.state, e.grads, e.hyper, e.Pp, e.P, e.n_reg, shadow=be.shadow, zero_grads=True)
-        advance_steps(e, self.slots_long)
+        advance_steps(e, self.slots_long, self.slots_t)
 
     def run(self):
         be = self.be

@@ -104,7 +104,7 @@ def _register():
     ops.register("dtf_head_args_size", [])
     ops.register("dtf_prep_input", [c_void_p, c_void_p, c_long, c_int, c_void_p])
     ops.register("dtf_weight_prep", [c_void_p, c_long, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_long,
-                                     c_void_p])
+                                     c_void_p, c_long, c_void_p])
     ops.register("dtf_bn_running_update", [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_long, c_void_p,
                                            c_int, c_void_p, c_void_p, c_long, c_void_p])
     ops.register("dtf_bn_bwd_apply", [P(BnBwdArgs), c_void_p])
@@ -222,9 +222,14 @@ def note_step_advanced(e, slots):
                 dev[s][H_STEP] += 1.0
 
 
-def advance_steps(e, slots_long):
-    """Inside the captured step: per-member step counters (state column + hyper table) += 1."""
+def advance_steps(e, slots_long, slots_i32=None):
+    """Inside the captured step: per-member step counters (state column + hyper table) += 1 (one kernel when
+    the int32 slot list is given)."""
     from .optim import H_STEP
+    if slots_i32 is not None and e.device.type == "cuda":
+        ops.check(ops.lib().dtf_step_advance(_p(e.state), e.S, 3 * e.Pp + e.R, _p(e.hyper), H_STEP, _p(slots_i32),
+                                             slots_i32.numel(), ops.stream()), "step_advance")
+        return
     one = torch.ones(slots_long.numel(), device=e.device)
     e.step_col().index_add_(0, slots_long, one)
     e.hyper[:, H_STEP].index_add_(0, slots_long, one)
@@ -256,11 +261,15 @@ class HipResNetBackend:
         nb = len(self.L.prog.bns)
         self.stats_bn_stride = cap * NREP * 128
         # [fwd | bwd] statistic accumulators: zeroed by ONE memset per step
-        self.stats = torch.zeros(2, nb, cap, NREP, 128, dtype=torch.float32, device=self.dev)
+        # [fwd | bwd] statistic accumulators + per-member loss / correct count: ONE buffer, zeroed by the step's
+        # weight_prep launch
+        nst = 2 * nb * cap * NREP * 128
+        self.zbuf = torch.zeros(nst + 2 * cap, dtype=torch.float32, device=self.dev)
+        self.stats = self.zbuf[:nst].view(2, nb, cap, NREP, 128)
         self.conv_table_t = torch.tensor(self.L.conv_table, dtype=torch.int32, device=self.dev)
         self.bn_table_t = torch.tensor(self.L.bn_table, dtype=torch.int32, device=self.dev)
-        self.loss = torch.zeros(cap, dtype=torch.float32, device=self.dev)
-        self.correct = torch.zeros(cap, dtype=torch.float32, device=self.dev)
+        self.loss = self.zbuf[nst:nst + cap]
+        self.correct = self.zbuf[nst + cap:]
         self._plans: Dict[tuple, "_StepPlan"] = {}
         self.use_graph = os.environ.get("DTF_HIP_GRAPH", "1") == "1"
 
@@ -617,7 +626,8 @@ class _StepPlan:
             a.st_out = _p(be.st_b(x_bn))
         a.Hi, a.Wi, a.Ho, a.Wo, a.rows = H, H, H, H, rows
         tsz = ((rows + 2) * (H + 2) * (C + 8) + 63) // 64 * 64
-        lds = 2304 + 4 * tsz * 2
+        raw = C >= 64 or os.environ.get("DTF_RAWX16", "0") == "1"  # must match the build (conv.hip RAWX)
+        lds = 2304 + (4 * tsz + (2 * rows * H * (C + 8) if raw else 0)) * 2  # dY/X tiles [+ raw-x interiors]
         lib = ops.lib()
         slab = os.environ.get("DTF_DW_SLAB", "1") == "1"
         side = slab and self.side_reduce
@@ -677,6 +687,9 @@ class _StepPlan:
         wn = 9 * C * C
         budget = float(os.environ.get("DTF_FUSED_ATOMIC_BYTES_%d" % C, {64: 32e6}.get(C, 16e6)))
         n_wg = max(64, min(128 * len(self.slots), int(budget / (4.0 * wn))))
+        # fill the chip when the population is small (a single member: 128 WGs would idle half the CUs); with
+        # dW slabs a workgroup's partial is a plain store, so more workgroups only cost slab bytes
+        n_wg = max(n_wg, int(os.environ.get("DTF_FUSED_MIN_WG", "256")))
         return min(n_wg, self.N * bands)
 
     def _slab_floats(self):
@@ -729,10 +742,7 @@ class _StepPlan:
         nslots = len(self.slots)
         # 0. weights for this step
         self._add(lib.dtf_weight_prep, _p(e.state), e.S, _p(be.conv_table_t), len(L.conv_table), _p(self.slots_t),
-                  nslots, _p(be.wf), _p(be.wd), L.wtot)
-        self._add("zero", be.stats)
-        self._add("zero", be.loss)
-        self._add("zero", be.correct)
+                  nslots, _p(be.wf), _p(be.wd), L.wtot, _p(be.zbuf), be.zbuf.numel())
         if self.src is not None:
             self._add("augment", None)  # gather + pad/crop/flip + standardize + bf16 pack (data.hip)
         else:
@@ -875,10 +885,7 @@ class _StepPlan:
         nslots = len(self.slots)
         H = cfg.image_size
         self._add(lib.dtf_weight_prep, _p(e.state), e.S, _p(be.conv_table_t), len(L.conv_table), _p(self.slots_t),
-                  nslots, _p(be.wf), _p(be.wd), L.wtot)
-        self._add("zero", be.stats)
-        self._add("zero", be.loss)
-        self._add("zero", be.correct)
+                  nslots, _p(be.wf), _p(be.wd), L.wtot, _p(be.zbuf), be.zbuf.numel())
         if self.src is not None:
             self._add("augment", None)
         else:
@@ -999,7 +1006,7 @@ class _StepPlan:
             elif fn == "optim":
                 ops.fused_optimizer(e.state, e.grads, e.hyper, e.Pp, e.P, e.n_reg, shadow=None, zero_grads=True)
             elif fn == "step":
-                advance_steps(e, self.slots_long)
+                advance_steps(e, self.slots_long, self.slots_t)
             else:
                 err = fn(*args, ops.stream())
                 if err != 0:

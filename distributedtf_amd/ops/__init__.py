@@ -27,6 +27,7 @@ _SIGNATURES = {
     "dtf_fused_optimizer": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_long, c_long, c_long, c_long, c_int,
                             c_void_p],
     "dtf_shadow_refresh": [c_void_p, c_void_p, c_void_p, c_int, c_long, c_long, c_long, c_void_p],
+    "dtf_step_advance": [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_int, c_void_p],
 }
 
 

@@ -26,6 +26,12 @@
 #include "common.h"
 
 #define BN_EPS 1e-5f
+#ifndef DTF_FUSED_WAVES
+#define DTF_FUSED_WAVES(C) ((C) <= 32 ? 2 : 1)  // min waves / SIMD the fused bwd kernel is register-capped for
+#endif
+#ifndef DTF_RAWX16
+#define DTF_RAWX16 0
+#endif
 #ifndef DTF_ABL
 #define DTF_ABL 0  // timing-only ablation bits of conv_bwd_fused_kernel (tools/ablate.sh); 0 in real builds
 #endif
@@ -420,6 +426,7 @@ struct Stage {
   static constexpr int TOTAL = RT * WP * NCH, MAXC = (TOTAL + 255) / 256;
   int loff[MAXC];
   int goff[MAXC];
+  int roff[MAXC];  // band-interior chunks: offset in an unhaloed [RT-2][W][CP] tile (store_raw)
   unsigned okm, top, bot;
   int c0;
   __device__ __forceinline__ void init() {
@@ -431,6 +438,7 @@ struct Stage {
       const int pc = idx / NCH, col = pc % WP, r = pc / WP;
       const bool act = idx < TOTAL;
       loff[j] = act ? (r * WP + col) * CP + c0 : C;
+      roff[j] = ((r - 1) * W + (col - 1)) * CP + c0;
       goff[j] = (r * ROW + (col - 1) * C + c0) * 2;  // bytes
       if (act && col >= 1 && col <= W) okm |= 1u << j;
       if (r == 0) top |= 1u << j;
@@ -465,6 +473,13 @@ struct Stage {
       if ((m >> j) & 1u) t = xform8<MODE>(v[j], v2[j], c0, coef);
       *reinterpret_cast<uint4*>(buf + loff[j]) = t;
     }
+  }
+  // The untransformed band-interior chunks (tile rows 1..RT-2, image columns) into `raw` ([RT-2][W][CP]).
+  __device__ __forceinline__ void store_raw(bf16_t* raw, const uint4 (&v)[MAXC], unsigned m) const {
+    const unsigned interior = m & ~top & ~bot;
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j)
+      if ((interior >> j) & 1u) *reinterpret_cast<uint4*>(raw + roff[j]) = v[j];
   }
   // MODE 2 / 3 (BN-backward apply [+ residual v3]) staging that also writes the transformed band-interior
   // chunks (tile rows 1..RT-2, image columns) to `out` (the image base; null: LDS only).
@@ -1121,7 +1136,7 @@ __device__ __forceinline__ void slab_reduce_wg(const float* __restrict__ slab, c
 // packed fp32 / bf16 math: the VALU budget per MFMA is what bounds these
 // small-channel layers.
 template <int C, int MODE_DY, int EPI>
-__global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
+__global__ __launch_bounds__(256, DTF_FUSED_WAVES(C)) void conv_bwd_fused_kernel(ConvArgs a) {
   constexpr int W = 512 / C, H = W, ROWS = 8, BANDS = H / ROWS;
   constexpr int NT = C / 16;           // dgrad output-channel tiles
   constexpr int WPT = 4 / NT;
@@ -1145,6 +1160,12 @@ __global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
   bf16_t* t0 = reinterpret_cast<bf16_t*>(smem + 2304);
 #define FDBUF(i) (t0 + ((i) & 1) * 2 * TSZ)
 #define FXBUF(i) (t0 + TSZ + ((i) & 1) * 2 * TSZ)
+  // raw (untransformed) x of the band interior, for the dgrad epilogue's mask / x-hat: read from LDS instead of
+  // re-reading x from global memory (double-buffered like the tiles)
+  // (C <= 32 keeps the global re-read unless built with DTF_RAWX16: the extra LDS would cost its 2nd WG per CU)
+  constexpr bool RAWX = C >= 64 || DTF_RAWX16;
+  constexpr int RAWSZ = ROWS * W * CP;
+#define FXRAW(i) (t0 + 4 * TSZ + ((i) & 1) * RAWSZ)
 
   if ((int)blockIdx.x >= a.n_main) {  // trailing workgroups: dW slab reduction of the previous fused launch
     const int r = (int)blockIdx.x - a.n_main;
@@ -1208,13 +1229,14 @@ __global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
     tapoff[s] = k0 < KTOT ? -((tap / 3) * WP + (tap % 3)) * CP + c0 : 0;
   }
   const int ci0 = ct * 16 + (lane >> 4) * 4;
-  int tbo[MAXT];
+  int tbo[MAXT], rpo[MAXT];
   uint32_t pofs[MAXT];
 #pragma unroll
   for (int i = 0; i < MAXT; ++i) {
     const int p = (wave / NT + WPT * i) * 16 + (lane & 15);
     tbo[i] = ((p / W + 2) * WP + p % W + 2) * CP;
     pofs[i] = p * C + ci0;
+    rpo[i] = p * CP + ci0;
   }
   // wgrad lane constants (pixel rows 8g+q and +4 of each 32-pixel k-step)
   const int g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
@@ -1243,6 +1265,7 @@ __global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
   else
     st.template store<MODE_DY>(FDBUF(0), dv, dv2, dm, coef_d);
   st.template store<1>(FXBUF(0), xv_, unused, xm, ecoef);
+  if constexpr (RAWX) st.store_raw(FXRAW(0), xv_, xm);
   __syncthreads();
   for (int k = 0; k < nit; ++k) {
     const int it = it0 + k;
@@ -1254,7 +1277,10 @@ __global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < MAXT; ++i) {
       if constexpr (EPI & 1) rres[i] = *reinterpret_cast<const uint2*>(a.res + band + pofs[i]);
-      xres[i] = *reinterpret_cast<const uint2*>(a.xm + band + pofs[i]);
+      if constexpr (RAWX)
+        xres[i] = *reinterpret_cast<const uint2*>(FXRAW(k) + rpo[i]);
+      else
+        xres[i] = *reinterpret_cast<const uint2*>(a.xm + band + pofs[i]);
     }
     if (more) {
       cimg = (it + 1) / BANDS;
@@ -1331,11 +1357,13 @@ __global__ __launch_bounds__(256) void conv_bwd_fused_kernel(ConvArgs a) {
       else
         st.template store<MODE_DY>(FDBUF(k + 1), dv, dv2, dm, coef_d);
       st.template store<1>(FXBUF(k + 1), xv_, unused, xm, ecoef);
+      if constexpr (RAWX) st.store_raw(FXRAW(k + 1), xv_, xm);
     }
     __syncthreads();
   }
 #undef FDBUF
 #undef FXBUF
+#undef FXRAW
   {
     const float s4[4] = {ssum[0].x, ssum[0].y, ssum[1].x, ssum[1].y};
     const float q4[4] = {ssq[0].x, ssq[0].y, ssq[1].x, ssq[1].y};

@@ -134,7 +134,26 @@ __global__ __launch_bounds__(256) void shadow_refresh_kernel(const float* __rest
   }
 }
 
+// Per-member step counters after a captured step: state[slot][col] += 1 and hyper[slot][h_step] += 1.
+__global__ void step_advance_kernel(float* __restrict__ state, long S, long col, float* __restrict__ hyper,
+                                    int h_step, const int* __restrict__ slots, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const int s = slots[i];
+    state[(long)s * S + col] += 1.f;
+    hyper[s * 8 + h_step] += 1.f;
+  }
+}
+
 }  // namespace
+
+DTF_API int dtf_step_advance(float* state, long S, long col, float* hyper, int h_step, const int* slots, int n,
+                             hipStream_t stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(step_advance_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, state, S, col, hyper, h_step,
+                     slots, n);
+  return DTF_CHECK_LAUNCH();
+}
 
 DTF_API int dtf_fused_optimizer(float* state, float* grads, const float* hyper, bf16_t* shadow, int G, long S, long Pp,
                                 long P, long n_reg, int zero_grads, hipStream_t stream) {

@@ -45,7 +45,15 @@ __global__ __launch_bounds__(256) void prep_input_kernel(const float* __restrict
 __global__ __launch_bounds__(256) void weight_prep_kernel(const float* __restrict__ state, long s_mstride,
                                                            const int* __restrict__ table, const int* __restrict__ slots,
                                                            bf16_t* __restrict__ wf, bf16_t* __restrict__ wd,
-                                                           long w_mstride) {
+                                                           long w_mstride, float* __restrict__ zbuf, long zn) {
+  {  // the step's accumulators (BN statistics, loss, correct) start at zero: folded into this first launch
+    const long nb = (long)gridDim.x * gridDim.y * gridDim.z;
+    const long b = blockIdx.x + (long)gridDim.x * (blockIdx.y + (long)gridDim.y * blockIdx.z);
+    const long z4 = zn >> 2;
+    for (long i = b * blockDim.x + threadIdx.x; i < z4; i += nb * blockDim.x)
+      reinterpret_cast<float4*>(zbuf)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (b == 0 && (long)threadIdx.x < zn - 4 * z4) zbuf[4 * z4 + threadIdx.x] = 0.f;
+  }
   // grid (conv, chunk, member): every conv is split over gridDim.y workgroups so the launch fills the GPU
   // even for a single member (it sits at the head of the step's critical path).
   const int* t = table + blockIdx.x * 8;
@@ -550,10 +558,11 @@ DTF_API int dtf_prep_input(const float* x, bf16_t* y, long npix, int c_in, hipSt
 }
 
 DTF_API int dtf_weight_prep(const float* state, long s_mstride, const int* table, int nconv, const int* slots,
-                            int nslots, bf16_t* wf, bf16_t* wd, long w_mstride, hipStream_t stream) {
+                            int nslots, bf16_t* wf, bf16_t* wd, long w_mstride, float* zbuf, long zn,
+                            hipStream_t stream) {
   if (nconv <= 0 || nslots <= 0) return 0;
   hipLaunchKernelGGL(weight_prep_kernel, dim3(nconv, 16, nslots), dim3(256), 0, stream, state, s_mstride, table, slots,
-                     wf, wd, w_mstride);
+                     wf, wd, w_mstride, zbuf, zn);
   return DTF_CHECK_LAUNCH();
 }
 

@@ -687,9 +687,9 @@ class _StepPlan:
         wn = 9 * C * C
         budget = float(os.environ.get("DTF_FUSED_ATOMIC_BYTES_%d" % C, {64: 32e6}.get(C, 16e6)))
         n_wg = max(64, min(128 * len(self.slots), int(budget / (4.0 * wn))))
-        # fill the chip when the population is small (a single member: 128 WGs would idle half the CUs); with
-        # dW slabs a workgroup's partial is a plain store, so more workgroups only cost slab bytes
-        n_wg = max(n_wg, int(os.environ.get("DTF_FUSED_MIN_WG", "256")))
+        # optional floor (e.g. 256: fill every CU for a single member).  Off: measured slower at pop 1 (1.64 vs
+        # 1.60 ms/step), the extra dW slab bytes cost more than the idle CUs
+        n_wg = max(n_wg, int(os.environ.get("DTF_FUSED_MIN_WG", "0")))
         return min(n_wg, self.N * bands)
 
     def _slab_floats(self):

@@ -233,7 +233,7 @@ class SPMDPopulation(_ReportMixin):
 
     def __init__(self, pop_size, comm, target_model_class, epochs_per_round=1, do_exploit=True, do_explore=True,
                  seed=None, savedata="savedata", model_kwargs=None, dataplane=None, hparams=None,
-                 verbose=True, inject_nan=None):
+                 verbose=True, inject_nan=None, resume=False):
         from .worker import TrainingWorker
         self.comm = comm
         self.rank = comm.Get_rank()
@@ -250,19 +250,42 @@ class SPMDPopulation(_ReportMixin):
             from ..parallel.dataplane import DataPlane
             dataplane = DataPlane(comm)
         self.dataplane = dataplane
-        hps = hparams if hparams is not None else (
-            sample_population(pop_size, seed) if self.rank == 0 else None)
-        hps = comm.bcast(hps, 0)
-        self.pop_size = len(hps)
         self.worker = TrainingWorker(comm, 0, target_model_class, save_base_dir=os.path.join(savedata, "model_"),
                                      seed=seed, model_kwargs=model_kwargs, dataplane=dataplane, verbose=verbose)
-        blocks = partition(self.pop_size, self.world)
+        self.start_round = 0
+        state = None
+        if resume:
+            ok = os.path.isfile(os.path.join(savedata, reports.POPULATION_STATE)) if self.rank == 0 else None
+            if comm.bcast(ok, 0):
+                state = comm.bcast(reports.read_population_state(savedata) if self.rank == 0 else None, 0)
+        if state is None:
+            hps = hparams if hparams is not None else (
+                sample_population(pop_size, seed) if self.rank == 0 else None)
+            hps = comm.bcast(hps, 0)
+            self.initial_pop_size = len(hps)
+            rows = [(i, None, hp, 0) for i, hp in enumerate(hps)]
+        else:
+            # whole-run resume: surviving members keep their ids (and owners); state from their checkpoints
+            self.initial_pop_size = int(state["population_size"])
+            self.start_round = int(state["next_round"])
+            rows = [(m["model_id"], m["accuracy"], m["hparams"], m["epoches_trained"]) for m in state["members"]]
+        self.pop_size = len(rows)
+        blocks = partition(self.initial_pop_size, self.world)
         self.id_owner = {}
         for r, (b, c) in enumerate(blocks):
             for i in range(b, b + c):
                 self.id_owner[i] = r
-        begin, cnt = blocks[self.rank]
-        self.worker.add_graphs(copy.deepcopy(hps[begin:begin + cnt]), begin, do_explore and not do_exploit)
+        mine = [r for r in rows if self.id_owner[int(r[0])] == self.rank]
+        self.worker.is_expolore_only = bool(do_explore and not do_exploit)
+        self.worker.add_members([(r[0], copy.deepcopy(r[2])) for r in mine])
+        if state is not None:
+            by_id = self.worker.members_by_id()
+            for mid, acc, _, epochs in mine:
+                g = by_id[int(mid)]
+                if not g.load_checkpoint():
+                    raise RuntimeError("resume: member %d has no checkpoint in %s" % (mid, g.save_dir))
+                g.accuracy, g.epoches_trained = float(acc), int(epochs)
+            self.log("Resumed %d members at round %d" % (len(rows), self.start_round))
         self.last_plan = []
 
     def log(self, *a):
@@ -302,9 +325,23 @@ class SPMDPopulation(_ReportMixin):
     def explore(self):
         self.worker.explore_necessary_graphs()
 
+    def save_round_state(self, next_round):
+        """Resume point: re-save the members whose state changed after their end-of-train checkpoint (exploit
+        destinations), then rank 0 writes the population table."""
+        dsts = {p.dst_id for p in self.last_plan} if self.do_exploit else set()
+        for g in self.worker.worker_graphs:
+            if g.cluster_id in dsts and getattr(g, "checkpoint_every_round", True):
+                g.save_checkpoint()
+        rows = self.comm.allgather([[g.cluster_id, g.get_accuracy(), g.hparams, g.epoches_trained]
+                                    for g in self.worker.worker_graphs])
+        if self.rank == 0:
+            reports.write_population_state(self.savedata, next_round, self.initial_pop_size,
+                                           [r for part in rows for r in part])
+
     def train(self, round_num):
+        """Run rounds ``start_round .. round_num - 1`` (``start_round`` > 0 after a resume)."""
         start = time.time()
-        for rnd in range(round_num):
+        for rnd in range(self.start_round, round_num):
             t0 = time.time()
             self.log("\nRound {}".format(rnd))
             self.train_one_round(rnd, round_num)
@@ -312,6 +349,7 @@ class SPMDPopulation(_ReportMixin):
                 self.exploit()
             if self.do_explore:
                 self.explore()
+            self.save_round_state(rnd + 1)
             self.round_times.append(time.time() - t0)
             self.log("Round elapsed time: {}\n".format(datetime.timedelta(seconds=self.round_times[-1])))
         self.comm.barrier()

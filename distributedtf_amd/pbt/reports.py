@@ -52,6 +52,30 @@ def write_best_model(values: Sequence, filename: str) -> Dict:
     return report
 
 
+POPULATION_STATE = "population_state.json"
+
+
+def write_population_state(savedata: str, next_round: int, population_size: int, rows: Sequence) -> str:
+    """Whole-run resume table (opt-in ``--resume``): the round to run next and,
+    per surviving member, ``[id, accuracy, hparams, epoches_trained]``.  Written atomically (tmp + rename) at the
+    end of every round, after the members' checkpoints."""
+    path = os.path.join(savedata, POPULATION_STATE)
+    blob = {"next_round": int(next_round), "population_size": int(population_size),
+            "members": [{"model_id": int(r[0]), "accuracy": float(r[1]), "hparams": r[2],
+                         "epoches_trained": int(r[3])} for r in sorted(rows, key=lambda r: int(r[0]))]}
+    os.makedirs(savedata, exist_ok=True)
+    tmp = path + ".tmp"
+    with open(tmp, "w") as fp:
+        json.dump(blob, fp, indent=2, sort_keys=True)
+    os.replace(tmp, path)
+    return path
+
+
+def read_population_state(savedata: str) -> Dict:
+    with open(os.path.join(savedata, POPULATION_STATE)) as fp:
+        return json.load(fp)
+
+
 def append_test_result(world_size: int, pop_size: int, seconds: float, path: str = "test_results.txt") -> None:
     with open(path, "a") as f:
         f.write("n = {}, pop_size = {}, time = {}s\n".format(world_size, pop_size, seconds))

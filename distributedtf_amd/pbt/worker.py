@@ -87,6 +87,12 @@ class TrainingWorker:
             g = self.target_model_class(id_begin + i, hp, self.save_base_dir, seed=self.seed, **self.model_kwargs)
             self.worker_graphs.append(g)
 
+    def add_members(self, id_hparams):
+        """Instantiate members with explicit ids (whole-run resume: ids need not be contiguous)."""
+        for mid, hp in id_hparams:
+            self.worker_graphs.append(self.target_model_class(int(mid), hp, self.save_base_dir, seed=self.seed,
+                                                              **self.model_kwargs))
+
     def _cull(self, g, why: str):
         self.worker_graphs.remove(g)
         self.removed_ids.append(g.cluster_id)

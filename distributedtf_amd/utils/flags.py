@@ -112,6 +112,8 @@ def build_parser(defaults: Optional[Dict[str, Any]] = None) -> argparse.Argument
     p.add_argument("--stop_threshold", type=float, default=None)
     p.add_argument("--export_dir", default=None)
     p.add_argument("--no_checkpoint", action="store_true")
+    p.add_argument("--resume", action="store_true",
+                   help="continue a run from savedata/population_state.json + member checkpoints (no wipe)")
     return p
 
 

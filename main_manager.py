@@ -52,8 +52,9 @@ def main(argv=None):
     rank, world = comm.Get_rank(), comm.Get_size()
     savedata = args.savedata
 
-    if rank == master_rank:
+    if rank == master_rank and not args.resume:
         shutil.rmtree(savedata, ignore_errors=True)
+    if rank == master_rank:
         os.makedirs(savedata, exist_ok=True)
     comm.barrier()
 
@@ -74,9 +75,11 @@ def main(argv=None):
     else:
         cluster = SPMDPopulation(args.population_size, comm, cls, epochs_per_round=args.epochs_per_round,
                                  do_exploit=args.do_exploit, do_explore=args.do_explore, seed=args.seed,
-                                 savedata=savedata, model_kwargs=model_kwargs, inject_nan=inject)
+                                 savedata=savedata, model_kwargs=model_kwargs, inject_nan=inject,
+                                 resume=args.resume)
 
-    cluster.dump_all_models_to_json(os.path.join(savedata, "initial_hp.json"))
+    if not args.resume or getattr(cluster, "start_round", 0) == 0:
+        cluster.dump_all_models_to_json(os.path.join(savedata, "initial_hp.json"))
     elapsed = cluster.train(args.train_round)
     if rank == master_rank:
         reports.append_test_result(world, args.population_size, elapsed, args.results_file)

@@ -1,0 +1,60 @@
+"""Opt-in whole-run resume: a run stopped after some rounds continues from
+``savedata/population_state.json`` + the members' checkpoints -- round counter, surviving ids, weights
+(step counters), accuracies and hyper-parameters carry over; culled members stay dead."""
+import json
+import os
+
+import pytest
+
+from distributedtf_amd.models.toy_model import ToyModel
+from distributedtf_amd.parallel.comm import LocalComm
+from distributedtf_amd.pbt.cluster import SPMDPopulation
+from distributedtf_amd.pbt.reports import POPULATION_STATE
+
+from test_toy_and_cluster import _run_threads
+
+
+def _run(world, rounds, resume, out, inject=None):
+    comms = LocalComm.create(world)
+
+    def body(r):
+        pop = SPMDPopulation(6, comms[r], ToyModel, epochs_per_round=2, seed=5, verbose=False, resume=resume,
+                             inject_nan=inject or {})
+        out.setdefault("start", {})[r] = pop.start_round
+        pop.train(rounds)
+        vals = pop.get_all_values()
+        steps = {g.cluster_id: int(g.export_state()[2]) for g in pop.worker.worker_graphs}
+        out.setdefault("vals", {})[r] = vals
+        out.setdefault("steps", {}).update(steps)
+        out.setdefault("epochs", {}).update({g.cluster_id: g.epoches_trained for g in pop.worker.worker_graphs})
+
+    _run_threads([lambda r=r: body(r) for r in range(world)])
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_resume_continues_rounds(tmp_cwd, world):
+    first, second = {}, {}
+    _run(world, 2, False, first, inject={0: [4]})
+    st = json.load(open(os.path.join("savedata", POPULATION_STATE)))
+    assert st["next_round"] == 2 and st["population_size"] == 6
+    assert sorted(m["model_id"] for m in st["members"]) == [0, 1, 2, 3, 5]  # member 4 was culled
+    assert all(m["epoches_trained"] == 4 for m in st["members"])
+    assert set(first["steps"].values()) == {4}
+    # a "new job" resumes and runs rounds 2..4
+    _run(world, 5, True, second)
+    assert set(second["start"].values()) == {2}
+    assert sorted(second["steps"]) == [0, 1, 2, 3, 5]
+    assert set(second["steps"].values()) == {10}  # 5 rounds x 2 epochs, continued from the checkpoints
+    assert set(second["epochs"].values()) == {10}
+    st = json.load(open(os.path.join("savedata", POPULATION_STATE)))
+    assert st["next_round"] == 5
+    # learning curves were appended to, not restarted
+    rows = open("savedata/model_0/learning_curve.csv").read().strip().splitlines()
+    assert len(rows) == 1 + 10
+
+
+def test_resume_without_state_starts_fresh(tmp_cwd):
+    out = {}
+    _run(1, 1, True, out)
+    assert set(out["start"].values()) == {0}
+    assert set(out["steps"].values()) == {2}

@@ -112,6 +112,12 @@ def build_parser(defaults: Optional[Dict[str, Any]] = None) -> argparse.Argument
     p.add_argument("--stop_threshold", type=float, default=None)
     p.add_argument("--export_dir", default=None)
     p.add_argument("--no_checkpoint", action="store_true")
+    p.add_argument("--deterministic", action="store_true",
+                   help="replayable run: seeded RNGs, deterministic torch algorithms, torch backend (the HIP kernels "
+                        "reduce BatchNorm statistics with fp32 atomics, so they are not bitwise replayable)")
+    p.add_argument("--debug_kernels", action="store_true",
+                   help="serialise and synchronise every kernel launch (AMD_SERIALIZE_KERNEL=3, HIP_LAUNCH_BLOCKING"
+                        "=1), no HIP graphs: a faulting kernel is reported at its own launch")
     p.add_argument("--resume", action="store_true",
                    help="continue a run from savedata/population_state.json + member checkpoints (no wipe)")
     return p
@@ -134,6 +140,32 @@ class MainArgs(argparse.Namespace):
         if self.model == "mnist" and self.debug_steps:
             kw["debug_steps"] = self.debug_steps
         return kw
+
+    def apply_runtime_modes(self) -> None:
+        """Environment / library switches of --debug_kernels and --deterministic.  Call before
+        the first GPU use: HIP reads its launch-serialisation variables when the runtime initialises."""
+        import os
+        import random
+        if self.debug_kernels:
+            os.environ["AMD_SERIALIZE_KERNEL"] = "3"
+            os.environ["HIP_LAUNCH_BLOCKING"] = "1"
+            os.environ["DTF_HIP_GRAPH"] = "0"
+        if self.deterministic:
+            seed = 0 if self.seed is None else int(self.seed)
+            if self.seed is None:
+                self.seed = seed
+            random.seed(seed)
+            try:
+                import numpy as np
+                np.random.seed(seed)
+            except ImportError:
+                pass
+            torch.manual_seed(seed)
+            torch.use_deterministic_algorithms(True, warn_only=True)
+            torch.backends.cudnn.benchmark = False
+            torch.backends.cudnn.deterministic = True
+            if self.backend == "auto":
+                self.backend = "torch"
 
     def inject_nan_schedule(self) -> Dict[int, List[int]]:
         out: Dict[int, List[int]] = {}

@@ -42,6 +42,7 @@ def main(argv=None):
     args = parse_main_args(argv, defaults=dict(
         population_size=population_size, train_round=train_round, epochs_per_round=epochs_per_round,
         do_exploit=do_exploit, do_explore=do_explore, model=target_model))
+    args.apply_runtime_modes()  # --debug_kernels / --deterministic, before the first GPU use
     cls = model_class(args.model)
     model_kwargs = args.model_kwargs()
     if args.model == "toy":

@@ -627,7 +627,9 @@ class _StepPlan:
         a.Hi, a.Wi, a.Ho, a.Wo, a.rows = H, H, H, H, rows
         tsz = ((rows + 2) * (H + 2) * (C + 8) + 63) // 64 * 64
         raw = C >= 64 or os.environ.get("DTF_RAWX16", "0") == "1"  # must match the build (conv.hip RAWX)
-        lds = 2304 + (4 * tsz + (2 * rows * H * (C + 8) if raw else 0)) * 2  # dY/X tiles [+ raw-x interiors]
+        sb = C == 16 and mode_dy != 3 and os.environ.get("DTF_FUSED_SB16", "1") == "1"  # must match conv.hip SB
+        nbuf = 2 if sb else 4
+        lds = 2304 + (nbuf * tsz + (2 * rows * H * (C + 8) if raw else 0)) * 2  # dY/X tiles [+ raw-x interiors]
         lib = ops.lib()
         slab = os.environ.get("DTF_DW_SLAB", "1") == "1"
         side = slab and self.side_reduce
@@ -665,7 +667,9 @@ class _StepPlan:
         if os.environ.get("DTF_SLAB_PIGGYBACK", "1") != "1":
             return False
         _, red, rc, _ = pend
-        limit = int(os.environ.get("DTF_PIGGYBACK_MAX_WG", "512"))
+        limit = int(os.environ.get("DTF_PIGGYBACK_MAX_WG", "3000"))
+        if rc == 64 and os.environ.get("DTF_PIGGYBACK_C64", "0") != "1":
+            return False  # 1152 reduce WGs per member at the carrier's occupancy: measured slower (pop 1: +0.1 ms)
         return (self._slab_elems(rc) // 32) * red.shape[0] <= limit
 
     def _flush_slab(self):
@@ -742,7 +746,7 @@ class _StepPlan:
         nslots = len(self.slots)
         # 0. weights for this step
         self._add(lib.dtf_weight_prep, _p(e.state), e.S, _p(be.conv_table_t), len(L.conv_table), _p(self.slots_t),
-                  nslots, _p(be.wf), _p(be.wd), L.wtot, _p(be.zbuf), be.zbuf.numel())
+                  nslots, _p(be.wf), _p(be.wd), L.wtot, *self._zero_args())
         if self.src is not None:
             self._add("augment", None)  # gather + pad/crop/flip + standardize + bf16 pack (data.hip)
         else:
@@ -839,6 +843,14 @@ class _StepPlan:
         self._add("optim", None)
         self._add("step", None)
 
+    def _zero_args(self):
+        """(buffer, n) zeroed by weight_prep; DTF_ZERO_IN_PREP=0 keeps a separate fill launch instead."""
+        be = self.be
+        if os.environ.get("DTF_ZERO_IN_PREP", "1") == "1":
+            return _p(be.zbuf), be.zbuf.numel()
+        self._add("zero", be.zbuf)
+        return None, 0
+
     def _bn_bwd_apply(self, dz, x, add, out, bn):
         """out = BN-backward(dz, x) [+ add] (bn_bwd_apply_kernel)."""
         be, e = self.be, self.e
@@ -885,7 +897,7 @@ class _StepPlan:
         nslots = len(self.slots)
         H = cfg.image_size
         self._add(lib.dtf_weight_prep, _p(e.state), e.S, _p(be.conv_table_t), len(L.conv_table), _p(self.slots_t),
-                  nslots, _p(be.wf), _p(be.wd), L.wtot, _p(be.zbuf), be.zbuf.numel())
+                  nslots, _p(be.wf), _p(be.wd), L.wtot, *self._zero_args())
         if self.src is not None:
             self._add("augment", None)
         else:

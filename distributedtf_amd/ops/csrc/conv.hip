@@ -27,7 +27,14 @@
 
 #define BN_EPS 1e-5f
 #ifndef DTF_FUSED_WAVES
-#define DTF_FUSED_WAVES(C) ((C) <= 32 ? 2 : 1)  // min waves / SIMD the fused bwd kernel is register-capped for
+#define DTF_FUSED_WAVES(C, M) ((C) <= 16 && (M) != 3 && DTF_FUSED_SB16 ? 3 : (C) <= 32 ? 2 : 1)  // min waves / SIMD the fused bwd kernel is register-capped for
+#endif
+#ifndef DTF_SLAB_STORE
+#define DTF_SLAB_STORE 2  // dW slab store form: 0 plain, 1 nontemporal, 2 write-through (sc1) buffer stores
+#endif
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+#ifndef DTF_FUSED_SB16
+#define DTF_FUSED_SB16 1  // C = 16 fused bwd (MODE_DY != 3): single-buffered LDS tiles, 3 WGs / CU instead of 2
 #endif
 #ifndef DTF_RAWX16
 #define DTF_RAWX16 0
@@ -1136,7 +1143,7 @@ __device__ __forceinline__ void slab_reduce_wg(const float* __restrict__ slab, c
 // packed fp32 / bf16 math: the VALU budget per MFMA is what bounds these
 // small-channel layers.
 template <int C, int MODE_DY, int EPI>
-__global__ __launch_bounds__(256, DTF_FUSED_WAVES(C)) void conv_bwd_fused_kernel(ConvArgs a) {
+__global__ __launch_bounds__(256, DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_fused_kernel(ConvArgs a) {
   constexpr int W = 512 / C, H = W, ROWS = 8, BANDS = H / ROWS;
   constexpr int NT = C / 16;           // dgrad output-channel tiles
   constexpr int WPT = 4 / NT;
@@ -1158,8 +1165,10 @@ __global__ __launch_bounds__(256, DTF_FUSED_WAVES(C)) void conv_bwd_fused_kernel
   float* ecoef = coef_d + 192;                     // x BN: scale, shift, -mean*inv, inv (256)
   float* acc_lds = ecoef + 256;                    // 128
   bf16_t* t0 = reinterpret_cast<bf16_t*>(smem + 2304);
-#define FDBUF(i) (t0 + ((i) & 1) * 2 * TSZ)
-#define FXBUF(i) (t0 + TSZ + ((i) & 1) * 2 * TSZ)
+  // SB: single-buffered tiles (one extra barrier per iteration) so that C = 16 fits 3 workgroups per CU in LDS
+  constexpr bool SB = C == 16 && MODE_DY != 3 && DTF_FUSED_SB16;
+#define FDBUF(i) (t0 + (SB ? 0 : ((i) & 1) * 2 * TSZ))
+#define FXBUF(i) (t0 + TSZ + (SB ? 0 : ((i) & 1) * 2 * TSZ))
   // raw (untransformed) x of the band interior, for the dgrad epilogue's mask / x-hat: read from LDS instead of
   // re-reading x from global memory (double-buffered like the tiles)
   // (C <= 32 keeps the global re-read unless built with DTF_RAWX16: the extra LDS would cost its 2nd WG per CU)
@@ -1351,6 +1360,7 @@ __global__ __launch_bounds__(256, DTF_FUSED_WAVES(C)) void conv_bwd_fused_kernel
     }
     }  // DTF_ABL & 2
     if (more) {
+      if constexpr (SB) __syncthreads();  // every wave is done with the current tiles
       if constexpr (XSTORE)
         st.template store_x<MODE_DY == 3 ? 3 : 2>(FDBUF(k + 1), dv, dv2, dv3, dm, coef_d,
                                                   a.xout ? a.xout + cimg * IMG : nullptr, cgy0);
@@ -1376,10 +1386,28 @@ __global__ __launch_bounds__(256, DTF_FUSED_WAVES(C)) void conv_bwd_fused_kernel
     // row per wave instruction; the store tail is issue-bound); dw_slab_reduce sums a member's slabs
     f32x4_t* sb = reinterpret_cast<f32x4_t*>(a.slab + (long)blockIdx.x * (NJ * MT * 4 * 256)) + threadIdx.x;
     if constexpr (!(DTF_ABL & 1)) {
+#if DTF_SLAB_STORE == 2
+      // write-through (sc1) buffer stores: the slab does not sit dirty in L2 at the kernel boundary
+      const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(a.slab + (long)blockIdx.x * (NJ * MT * 4 * 256), 0,
+                                                         NJ * MT * 4 * 256 * 4, 0x00020000);
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
-        for (int m = 0; m < MT; ++m) sb[(j * MT + m) * 256] = wacc[j][m];
+        for (int m = 0; m < MT; ++m)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, wacc[j][m]), rsrc,
+                                                 (((j * MT + m) * 256) + (int)threadIdx.x) * 16, 0, 16);
+#else
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+#if DTF_SLAB_STORE == 1
+          __builtin_nontemporal_store(wacc[j][m], &sb[(j * MT + m) * 256]);
+#else
+          sb[(j * MT + m) * 256] = wacc[j][m];
+#endif
+        }
+#endif
     }
     return;
   }

@@ -18,8 +18,12 @@ Additions for the MI355X engine:
 
 from __future__ import annotations
 
+import atexit
+import copy
 import os
+import queue
 import random
+import threading
 from typing import Any, Dict, List, Optional
 
 import numpy as np
@@ -97,24 +101,97 @@ class ModelBase(object):
     def state_device(self):
         return self.export_state().device
 
-    def save_checkpoint(self) -> None:
-        """Write ``savedata/model_<id>/model.ckpt`` (+ ``checkpoint`` state file)."""
-        import torch
+    def save_checkpoint(self, wait: bool = False) -> None:
+        """Write ``savedata/model_<id>/model.ckpt`` (+ ``checkpoint`` state file).
+
+        The state leaves the GPU through one device->host copy into a pinned buffer (ordered on the current
+        stream, so training can continue immediately); serialisation and the file write run on the background
+        ``CheckpointWriter`` thread.  ``wait=True`` (or ``flush_checkpoints()``) blocks
+        until the file is on disk."""
         d = self.ensure_save_dir()
-        state = self.export_state().detach().to("cpu")
-        torch.save({"state": state, "epoches_trained": self.epoches_trained,
-                    "hparams": self.hparams}, os.path.join(d, "model.ckpt"))
-        with open(os.path.join(d, "checkpoint"), "w") as f:
-            f.write('model_checkpoint_path: "model.ckpt"\n')
+        blob = {"epoches_trained": self.epoches_trained, "hparams": copy.deepcopy(self.hparams)}
+        CheckpointWriter.get().submit(self.export_state().detach(), blob, d)
+        if wait:
+            flush_checkpoints()
 
     def has_checkpoint(self) -> bool:
+        flush_checkpoints()
         return os.path.isfile(os.path.join(self.save_dir, "model.ckpt"))
 
     def load_checkpoint(self) -> bool:
         import torch
+        flush_checkpoints()  # a pending write of this member must land first
         path = os.path.join(self.save_dir, "model.ckpt")
         if not os.path.isfile(path):
             return False
         blob = torch.load(path, map_location="cpu", weights_only=True)
         self.import_state(blob["state"])
         return True
+
+
+class CheckpointWriter:
+    """One background thread per process that writes member checkpoints.
+
+    ``submit`` snapshots the state into a pinned host buffer with a non-blocking copy and records a GPU
+    event; the thread waits for that event, then ``torch.save``s the blob and writes the TF-style
+    ``checkpoint`` state file.  Writes of one directory stay in submission order (single thread)."""
+
+    _inst: Optional["CheckpointWriter"] = None
+    _lock = threading.Lock()
+
+    def __init__(self):
+        self.q: "queue.Queue" = queue.Queue()
+        self.error: Optional[BaseException] = None
+        self.t = threading.Thread(target=self._run, name="dtf-ckpt-writer", daemon=True)
+        self.t.start()
+        atexit.register(self.q.join)  # the daemon thread finishes pending writes before the interpreter exits
+
+    @classmethod
+    def get(cls) -> "CheckpointWriter":
+        with cls._lock:
+            if cls._inst is None:
+                cls._inst = CheckpointWriter()
+            return cls._inst
+
+    def submit(self, state, blob: Dict[str, Any], directory: str) -> None:
+        import torch
+        if state.is_cuda:
+            host = torch.empty(state.shape, dtype=state.dtype, pin_memory=True)
+            host.copy_(state, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            host, ev = state.clone(), None
+        self.q.put((host, ev, blob, os.path.abspath(directory)))  # the cwd may change before the write
+
+    def _run(self):
+        import torch
+        while True:
+            item = self.q.get()
+            try:
+                host, ev, blob, d = item
+                if ev is not None:
+                    ev.synchronize()
+                blob = dict(blob)
+                blob["state"] = host
+                tmp = os.path.join(d, "model.ckpt.tmp")
+                torch.save(blob, tmp)
+                os.replace(tmp, os.path.join(d, "model.ckpt"))
+                with open(os.path.join(d, "checkpoint"), "w") as f:
+                    f.write('model_checkpoint_path: "model.ckpt"\n')
+            except BaseException as e:  # surfaced by flush()
+                self.error = e
+            finally:
+                self.q.task_done()
+
+    def flush(self) -> None:
+        self.q.join()
+        if self.error is not None:
+            e, self.error = self.error, None
+            raise RuntimeError("checkpoint write failed") from e
+
+
+def flush_checkpoints() -> None:
+    """Block until every submitted checkpoint is on disk (no-op when nothing was written)."""
+    if CheckpointWriter._inst is not None:
+        CheckpointWriter._inst.flush()

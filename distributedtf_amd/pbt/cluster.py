@@ -29,6 +29,7 @@ from typing import Any, Dict, List, Optional, Sequence, Tuple
 from .exploit import apply_plan_to_values, plan_exploit
 from .hparams import WorkerInstruction, generate_random_hparam
 from . import reports
+from ..models.model_base import flush_checkpoints
 
 
 def partition(pop_size: int, n_slots: int) -> List[Tuple[int, int]]:
@@ -325,6 +326,39 @@ class SPMDPopulation(_ReportMixin):
     def explore(self):
         self.worker.explore_necessary_graphs()
 
+    def _counters(self):
+        dp = self.dataplane
+        return [sum(int(getattr(g, "images_trained", 0)) for g in self.worker.worker_graphs), self.worker.train_time,
+                self.worker.explore_time, float(dp.bytes_moved), dp.seconds, dp.transfers_done]
+
+    def log_round_metrics(self, rnd, round_s):
+        """Append one JSON line per round to ``savedata/metrics.jsonl``: throughput (images/s of
+        the whole job), per-phase times (train / exploit / explore, max over ranks), exploit data-plane bytes and
+        latency, population accuracy summary."""
+        cur = self._counters()
+        prev = getattr(self, "_prev_counters", None) or [0, 0.0, 0.0, 0.0, 0.0, 0]
+        self._prev_counters = cur
+        delta = [c - p for c, p in zip(cur, prev)]
+        parts = self.comm.allgather([delta, [float(v[1]) for v in self.worker.get_all_values()]])
+        if self.rank != 0:
+            return
+        d = [p[0] for p in parts]
+        accs = [a for p in parts for a in p[1] if a == a]
+        images = sum(x[0] for x in d)
+        rec = {"round": rnd, "round_s": round_s, "images": images,
+               "images_per_s": images / round_s if round_s > 0 else None,
+               "train_s": max(x[1] for x in d), "explore_s": max(x[2] for x in d),
+               "exploit_s": self.exploit_time - getattr(self, "_prev_exploit", 0.0),
+               "exploit_transfers": int(max(x[5] for x in d)), "exploit_bytes": int(sum(x[3] for x in d)),
+               "exploit_dataplane_s": max(x[4] for x in d), "population": len(accs),
+               "best_acc": max(accs) if accs else None, "mean_acc": sum(accs) / len(accs) if accs else None,
+               "world_size": self.world}
+        self._prev_exploit = self.exploit_time
+        import json
+        os.makedirs(self.savedata, exist_ok=True)
+        with open(os.path.join(self.savedata, "metrics.jsonl"), "a") as f:
+            f.write(json.dumps(rec) + "\n")
+
     def save_round_state(self, next_round):
         """Resume point: re-save the members whose state changed after their end-of-train checkpoint (exploit
         destinations), then rank 0 writes the population table."""
@@ -332,6 +366,7 @@ class SPMDPopulation(_ReportMixin):
         for g in self.worker.worker_graphs:
             if g.cluster_id in dsts and getattr(g, "checkpoint_every_round", True):
                 g.save_checkpoint()
+        flush_checkpoints()  # every rank's checkpoints are on disk before the table that names them
         rows = self.comm.allgather([[g.cluster_id, g.get_accuracy(), g.hparams, g.epoches_trained]
                                     for g in self.worker.worker_graphs])
         if self.rank == 0:
@@ -351,6 +386,7 @@ class SPMDPopulation(_ReportMixin):
                 self.explore()
             self.save_round_state(rnd + 1)
             self.round_times.append(time.time() - t0)
+            self.log_round_metrics(rnd, self.round_times[-1])
             self.log("Round elapsed time: {}\n".format(datetime.timedelta(seconds=self.round_times[-1])))
         self.comm.barrier()
         total = time.time() - start

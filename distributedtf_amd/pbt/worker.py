@@ -23,6 +23,8 @@ from typing import Any, Dict, List, Optional
 from .hparams import WorkerInstruction
 
 
+from ..models.model_base import flush_checkpoints
+
 class TrainingWorker:
     def __init__(self, comm, master_rank: int, target_model_class, save_base_dir: str = "./savedata/model_",
                  seed: Optional[int] = None, model_kwargs: Optional[Dict[str, Any]] = None,
@@ -94,6 +96,7 @@ class TrainingWorker:
                                                               **self.model_kwargs))
 
     def _cull(self, g, why: str):
+        flush_checkpoints()  # no pending write may recreate the directory removed below
         self.worker_graphs.remove(g)
         self.removed_ids.append(g.cluster_id)
         shutil.rmtree(self.save_base_dir + str(g.cluster_id), ignore_errors=True)
@@ -117,6 +120,9 @@ class TrainingWorker:
         self.train_time += time.time() - t0
 
     def get_all_values(self):
+        # GET is the end-of-train barrier of the reference protocol: checkpoints are on disk before the master
+        # may copy member directories (exploit_transport="files")
+        flush_checkpoints()
         return [g.get_values() for g in self.worker_graphs]
 
     def set_values(self, values_to_set, reload_from_disk: bool = False):

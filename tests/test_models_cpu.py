@@ -189,6 +189,8 @@ def test_cifar_model_csv_and_checkpoint(tmp_cwd):
                             "initializer", "regularizer", "weight_decay", "batch_size", "model_id"]
     assert rows[0][11:13] == ["momentum", "grad_decay"]
     assert rows[1][2] == "RMSProp" and float(rows[1][3]) == 1e-4
+    from distributedtf_amd.models.model_base import flush_checkpoints
+    flush_checkpoints()  # checkpoints are written by a background thread
     assert os.path.isfile("savedata/model_5/model.ckpt") and os.path.isfile("savedata/model_5/checkpoint")
     before = m.export_state().clone()
     m.train(1, 2)

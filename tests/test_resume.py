@@ -58,3 +58,14 @@ def test_resume_without_state_starts_fresh(tmp_cwd):
     _run(1, 1, True, out)
     assert set(out["start"].values()) == {0}
     assert set(out["steps"].values()) == {2}
+
+
+def test_round_metrics_jsonl(tmp_cwd):
+    out = {}
+    _run(2, 3, False, out)
+    recs = [json.loads(l) for l in open(os.path.join("savedata", "metrics.jsonl"))]
+    assert [r["round"] for r in recs] == [0, 1, 2]
+    for r in recs:
+        assert r["population"] == 6 and r["world_size"] == 2
+        assert r["exploit_transfers"] == 2  # ceil(6/4) = 2 bottom members per round
+        assert r["exploit_bytes"] > 0 and r["round_s"] > 0

@@ -8,7 +8,7 @@ mkdir -p gpurun_out/pmc
 i=0
 for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INSTS_MFMA" \
            "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_WAIT_ANY" \
-           "FETCH_SIZE WRITE_SIZE GRBM_GUI_ACTIVE GRBM_COUNT"; do
+           "FETCH_SIZE GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
   cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-include-regex "${KRE:-conv_}" --output-format csv -d /tmp/pmc$i -o run -- python3 $GRAFT_REPO_ROOT/bench.py $BARGS > $GRAFT_REPO_ROOT/gpurun_out/pmc/run$i.log 2>&1
   rc=$?

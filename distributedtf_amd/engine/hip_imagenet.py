@@ -538,6 +538,7 @@ class _ImageNetPlan:
             elif fn == "gemm":
                 args[0].launch(st)
             elif fn == "optim":
+                e.dp_sync_grads(self.slots)  # data-parallel member groups only (no-op otherwise)
                 ops.fused_optimizer(e.state, e.grads, e.hyper, e.Pp, e.P, e.n_reg, shadow=self.be.shadow,
                                     zero_grads=True)
             elif fn == "step":

@@ -320,6 +320,7 @@ class _MnistPlan:
         self._launch(L.dtf_mnist_conv2_dgrad, self.w_dgrad)
         self._launch(L.dtf_mnist_conv2_wgrad, self.w_c2w)
         self._launch(L.dtf_mnist_conv1_wgrad, self.w_c1w)
+        e.dp_sync_grads(self.slots)  # data-parallel member groups only (no-op otherwise)
         ops.fused_optimizer(e.state, e.grads, e.hyper, e.Pp, e.P, e.n_reg, shadow=be.shadow, zero_grads=True)
         advance_steps(e, self.slots_long, self.slots_t)
 

@@ -1016,6 +1016,7 @@ class _StepPlan:
                 ops.augment_cifar(self.src.train_x, self.src.train_y, self.idx, self.rng, True, out16=self.xin16,
                                   lab32=self.labels)
             elif fn == "optim":
+                e.dp_sync_grads(self.slots)  # data-parallel member groups only (no-op otherwise)
                 ops.fused_optimizer(e.state, e.grads, e.hyper, e.Pp, e.P, e.n_reg, shadow=None, zero_grads=True)
             elif fn == "step":
                 advance_steps(e, self.slots_long, self.slots_t)

@@ -60,6 +60,7 @@ class PopulationEngine:
         self.compute_dtype = compute_dtype
         if self.device.type == "cpu" and compute_dtype == torch.bfloat16:
             self.compute_dtype = torch.float32
+        self.dp = None  # parallel.dataparallel.DPContext when a member is trained by a group of ranks
         self.backend = make_backend(self, backend)
         if optimizer_impl == "auto":
             optimizer_impl = "hip" if self.device.type == "cuda" else "reference"
@@ -142,6 +143,7 @@ class PopulationEngine:
         self.hyper.copy_(hy.to(self.device), non_blocking=True)
         self._hyper_dev = None
         losses = self.backend.forward_backward(slots, batches)
+        self.dp_sync_grads(slots)
         self.apply_optimizer(slots)
         for s in slots:
             self.host_step[s] += 1
@@ -150,6 +152,31 @@ class PopulationEngine:
         sc.index_add_(0, idx, torch.ones(len(slots), device=self.device))
         self.backend.on_params_changed(slots)
         return losses
+
+    # ------------------------------------------------------- data parallelism
+    def set_data_parallel(self, dp) -> None:
+        self.dp = dp
+        if dp is not None and hasattr(self.backend, "use_graph"):
+            self.backend.use_graph = False  # collectives run eagerly between the backward and the optimizer
+
+    def dp_sync_grads(self, slots: Sequence[int]) -> None:
+        """Mean of the members' gradient rows over the member group (before the optimizer)."""
+        if self.dp is None or not slots:
+            return
+        idx = torch.tensor(sorted(slots), device=self.device, dtype=torch.long)
+        g = self.grads.index_select(0, idx)
+        self.dp.allreduce_mean_(g)
+        self.grads.index_copy_(0, idx, g)
+
+    def dp_sync_running(self, slots: Sequence[int]) -> None:
+        """Mean of the BatchNorm running statistics over the member group (end of a round)."""
+        if self.dp is None or not slots or self.R == 0:
+            return
+        idx = torch.tensor(sorted(slots), device=self.device, dtype=torch.long)
+        lo, hi = 3 * self.Pp, 3 * self.Pp + self.R
+        r = self.state[:, lo:hi].index_select(0, idx)
+        self.dp.allreduce_mean_(r)
+        self.state[:, lo:hi].index_copy_(0, idx, r)
 
     def apply_optimizer(self, slots: Sequence[int]) -> None:
         if self.optimizer_impl == "hip":

@@ -53,8 +53,9 @@ class EngineModel(ModelBase):
     # ------------------------------------------------------------------------
     def __init__(self, cluster_id, hparams, save_base_dir, seed=None, device=None, backend="auto",
                  capacity=8, use_synthetic_data=None, data_dir=None, max_train_steps=None,
-                 checkpoint_every_round=True, eval_every_round=True, **kw):
+                 checkpoint_every_round=True, eval_every_round=True, dp=None, **kw):
         super().__init__(cluster_id, hparams, save_base_dir, seed=seed)
+        self.dp = dp  # parallel.dataparallel.DPContext: this member is one replica of a data-parallel group
         self.options = dict(kw)
         self.device = torch.device(device) if device is not None else default_device()
         self.data_dir = data_dir
@@ -68,6 +69,8 @@ class EngineModel(ModelBase):
         if eng is None or not eng.free_slots:
             eng = self._grow_or_create(key, eng, capacity, backend)
         self.engine = eng
+        if dp is not None:
+            eng.set_data_parallel(dp)
         self._engine_key = key
         init_seed = (seed if seed is not None else int(time.time() * 1000) % 100000) * 1009 + self.cluster_id
         self.slot = eng.add_member(self, self.hparams, init_seed)
@@ -128,8 +131,19 @@ class EngineModel(ModelBase):
         super().set_values(values)
 
     # ------------------------------------------------------------- training
+    @property
+    def is_dp_follower(self) -> bool:
+        """Replicas other than the group's first one train and evaluate but write no files."""
+        return self.dp is not None and self.dp.rank != 0
+
+    def save_checkpoint(self, wait: bool = False) -> None:
+        if not self.is_dp_follower:
+            super().save_checkpoint(wait)
+
     def _batch(self, ds, gen):
         b = int(self.hparams["batch_size"])
+        if self.dp is not None:
+            b = max(1, self.dp.local_batch(b))  # this replica's shard of the member's batch
         if hasattr(ds, "batch_slice"):
             return ds.batch_slice(b)
         if not hasattr(self, "_perm") or self._perm_pos + b > self._perm.numel():
@@ -159,7 +173,8 @@ class EngineModel(ModelBase):
             gen = None
             if ds.device.type == "cuda":
                 gen = torch.Generator(device=ds.device)
-                gen.manual_seed(int(ms[0].rng.random() * 1e9))
+                # replicas of a data-parallel group draw different shards (the member rng stays in lockstep)
+                gen.manual_seed(int(ms[0].rng.random() * 1e9) + (7919 * ms[0].dp.rank if ms[0].dp else 0))
             todo = {m.slot: m.n_steps(num_epoch) for m in ms}
             by_slot = {m.slot: m for m in ms}
             done = 0
@@ -177,6 +192,15 @@ class EngineModel(ModelBase):
                 for i, s in enumerate(active):
                     loss_acc[s] = losses[i]  # view, no host sync
                 done += 1
+            dp = ms[0].dp
+            if dp is not None:
+                # same NaN verdict and the same BatchNorm running statistics on every replica
+                eng.dp_sync_running([m.slot for m in ms])
+                for m in ms:
+                    if loss_acc[m.slot] is not None:
+                        t = loss_acc[m.slot].detach().float().reshape(1).clone()
+                        dp.allreduce_mean_(t)
+                        loss_acc[m.slot] = t[0]
             for m in ms:
                 try:
                     if loss_acc[m.slot] is not None:
@@ -203,6 +227,8 @@ class EngineModel(ModelBase):
             raise failed[self.cluster_id]
 
     def write_learning_curve(self, accuracy):
+        if self.is_dp_follower:
+            return
         fields, row = self.csv_row(accuracy)
         d = self.ensure_save_dir()
         path = os.path.join(d, "learning_curve.csv")

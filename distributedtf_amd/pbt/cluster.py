@@ -22,6 +22,7 @@ import copy
 import datetime
 import math
 import os
+import random
 import shutil
 import time
 from typing import Any, Dict, List, Optional, Sequence, Tuple
@@ -234,7 +235,7 @@ class SPMDPopulation(_ReportMixin):
 
     def __init__(self, pop_size, comm, target_model_class, epochs_per_round=1, do_exploit=True, do_explore=True,
                  seed=None, savedata="savedata", model_kwargs=None, dataplane=None, hparams=None,
-                 verbose=True, inject_nan=None, resume=False):
+                 verbose=True, inject_nan=None, resume=False, dp_size=1):
         from .worker import TrainingWorker
         self.comm = comm
         self.rank = comm.Get_rank()
@@ -251,6 +252,16 @@ class SPMDPopulation(_ReportMixin):
             from ..parallel.dataplane import DataPlane
             dataplane = DataPlane(comm)
         self.dataplane = dataplane
+        # intra-member data parallelism (parallel/dataparallel.py): world / dp_size member groups
+        from ..parallel.dataparallel import make_dp_context
+        self.dp_size = max(1, int(dp_size))
+        self.dp = make_dp_context(comm, self.dp_size)
+        self.group_index = self.rank // self.dp_size
+        self.n_groups = self.world // self.dp_size
+        if self.dp is not None:
+            if seed is None:  # replicas must draw identical inits and explore steps
+                seed = comm.bcast(random.randrange(1 << 30) if self.rank == 0 else None, 0)
+            model_kwargs = dict(model_kwargs or {}, dp=self.dp)
         self.worker = TrainingWorker(comm, 0, target_model_class, save_base_dir=os.path.join(savedata, "model_"),
                                      seed=seed, model_kwargs=model_kwargs, dataplane=dataplane, verbose=verbose)
         self.start_round = 0
@@ -271,12 +282,12 @@ class SPMDPopulation(_ReportMixin):
             self.start_round = int(state["next_round"])
             rows = [(m["model_id"], m["accuracy"], m["hparams"], m["epoches_trained"]) for m in state["members"]]
         self.pop_size = len(rows)
-        blocks = partition(self.initial_pop_size, self.world)
-        self.id_owner = {}
+        blocks = partition(self.initial_pop_size, self.n_groups)
+        self.id_owner = {}  # member id -> member group (= rank when dp_size == 1)
         for r, (b, c) in enumerate(blocks):
             for i in range(b, b + c):
                 self.id_owner[i] = r
-        mine = [r for r in rows if self.id_owner[int(r[0])] == self.rank]
+        mine = [r for r in rows if self.id_owner[int(r[0])] == self.group_index]
         self.worker.is_expolore_only = bool(do_explore and not do_exploit)
         self.worker.add_members([(r[0], copy.deepcopy(r[2])) for r in mine])
         if state is not None:
@@ -293,8 +304,17 @@ class SPMDPopulation(_ReportMixin):
         if self.verbose and self.rank == 0:
             print(*a, flush=True)
 
+    @property
+    def is_group_leader(self) -> bool:
+        return self.dp is None or self.dp.rank == 0
+
+    def _values(self):
+        """This rank's share of the population table (replicas other than a group's first report nothing)."""
+        vals = self.worker.get_all_values()
+        return vals if self.is_group_leader else []
+
     def get_all_values(self):
-        parts = self.comm.allgather(self.worker.get_all_values())
+        parts = self.comm.allgather(self._values())
         return [v for part in parts for v in part]
 
     def train_one_round(self, rnd, total_rounds):
@@ -306,20 +326,22 @@ class SPMDPopulation(_ReportMixin):
                     self.worker._cull(g, "injected nan")
 
     def exploit(self):
-        parts = self.comm.allgather(self.worker.get_all_values())  # also the end-of-train barrier
+        parts = self.comm.allgather(self._values())  # also the end-of-train barrier
         t0 = time.time()
         values = [v for part in parts for v in part]
-        owner = {int(v[0]): r for r, part in enumerate(parts) for v in part}
+        owner = {int(v[0]): r // self.dp_size for r, part in enumerate(parts) for v in part}  # member group
         self.pop_size = len(values)
         plan = plan_exploit(values)
         self.last_plan = plan
         for p in plan:
             self.log("Copied: {} -> {}".format(p.src_id, p.dst_id))
-        transfers = [(p.src_id, owner[p.src_id], p.dst_id, owner[p.dst_id]) for p in plan]
+        d = self.dp_size  # replica r of the winner's group -> replica r of the loser's group
+        transfers = [(p.src_id, owner[p.src_id] * d + r, p.dst_id, owner[p.dst_id] * d + r)
+                     for p in plan for r in range(d)]
         if transfers:
             self.dataplane.execute(transfers, self.worker.members_by_id())
         updates = apply_plan_to_values(values, plan)
-        mine = [u for mid, u in updates.items() if owner[mid] == self.rank]
+        mine = [u for mid, u in updates.items() if owner[mid] == self.group_index]
         self.worker.set_values(mine)
         self.exploit_time += time.time() - t0
 
@@ -339,7 +361,7 @@ class SPMDPopulation(_ReportMixin):
         prev = getattr(self, "_prev_counters", None) or [0, 0.0, 0.0, 0.0, 0.0, 0]
         self._prev_counters = cur
         delta = [c - p for c, p in zip(cur, prev)]
-        parts = self.comm.allgather([delta, [float(v[1]) for v in self.worker.get_all_values()]])
+        parts = self.comm.allgather([delta, [float(v[1]) for v in self._values()]])
         if self.rank != 0:
             return
         d = [p[0] for p in parts]
@@ -368,7 +390,7 @@ class SPMDPopulation(_ReportMixin):
                 g.save_checkpoint()
         flush_checkpoints()  # every rank's checkpoints are on disk before the table that names them
         rows = self.comm.allgather([[g.cluster_id, g.get_accuracy(), g.hparams, g.epoches_trained]
-                                    for g in self.worker.worker_graphs])
+                                    for g in self.worker.worker_graphs] if self.is_group_leader else [])
         if self.rank == 0:
             reports.write_population_state(self.savedata, next_round, self.initial_pop_size,
                                            [r for part in rows for r in part])

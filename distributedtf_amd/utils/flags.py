@@ -118,6 +118,8 @@ def build_parser(defaults: Optional[Dict[str, Any]] = None) -> argparse.Argument
     p.add_argument("--debug_kernels", action="store_true",
                    help="serialise and synchronise every kernel launch (AMD_SERIALIZE_KERNEL=3, HIP_LAUNCH_BLOCKING"
                         "=1), no HIP graphs: a faulting kernel is reported at its own launch")
+    p.add_argument("--dp_size", type=int, default=1,
+                   help="ranks per population member (intra-member data parallelism; must divide the world)")
     p.add_argument("--resume", action="store_true",
                    help="continue a run from savedata/population_state.json + member checkpoints (no wipe)")
     return p

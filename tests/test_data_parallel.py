@@ -1,0 +1,85 @@
+"""Intra-member data parallelism (parallel/dataparallel.py) over gloo on CPU: a world of
+4 ranks with --dp_size 2 trains a population of 4 in 2 member groups.  Replicas stay bit-identical (gradients
+are all-reduced before every optimizer step, BN running statistics at the end of each round), only group
+leaders report values / write files, and exploit copies go replica-to-replica."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, tmp, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    os.chdir(tmp)
+    torch.set_num_threads(1)
+    try:
+        from distributedtf_amd.parallel.comm import init_distributed, shutdown_distributed
+        from distributedtf_amd.pbt.cluster import SPMDPopulation
+        from distributedtf_amd.models.cifar10_model import Cifar10Model
+        from distributedtf_amd.models.model_base import flush_checkpoints
+        from distributedtf_amd.pbt.hparams import generate_random_hparam
+        import random
+        comm = init_distributed(backend="gloo")
+        rng = random.Random(4)
+        hps = []
+        for _ in range(4):
+            h = generate_random_hparam(rng)
+            h["batch_size"] = 8
+            h["opt_case"] = {"optimizer": "Momentum", "lr": 0.05, "momentum": 0.9}
+            hps.append(h)
+        pop = SPMDPopulation(4, comm, Cifar10Model, epochs_per_round=1, seed=5, verbose=False, hparams=hps,
+                             dp_size=2, model_kwargs=dict(resnet_size=8, max_train_steps=2, use_synthetic_data=True,
+                                                          device="cpu", eval_every_round=True))
+        pop.train(2)
+        flush_checkpoints()
+        states = {g.cluster_id: g.export_state().clone() for g in pop.worker.worker_graphs}
+        batches = {g.cluster_id: g.dp.local_batch(g.hparams["batch_size"]) for g in pop.worker.worker_graphs}
+        gathered = comm.allgather(states)
+        vals = pop.get_all_values()
+        q.put((rank, gathered, sorted(v[0] for v in vals), [(p.src_id, p.dst_id) for p in pop.last_plan], batches))
+        shutdown_distributed()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, "ERR", traceback.format_exc(), None, None))
+
+
+@pytest.mark.timeout(300)
+def test_dp_groups_world4_dp2(tmp_path):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 4, port, str(tmp_path), q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=280) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(30)
+    for r in res:
+        assert r[1] != "ERR", r[2]
+    gathered = res[0][1]  # per rank: {member id: state}
+    # group 0 = ranks {0, 1} holds members {0, 1}; group 1 = ranks {2, 3} holds {2, 3}
+    assert sorted(gathered[0]) == [0, 1] and sorted(gathered[1]) == [0, 1]
+    assert sorted(gathered[2]) == [2, 3] and sorted(gathered[3]) == [2, 3]
+    for a, b in ((0, 1), (2, 3)):
+        for mid in gathered[a]:
+            assert torch.equal(gathered[a][mid], gathered[b][mid]), "replicas diverged (member %d)" % mid
+    # the population table has every member once; the exploit plan agrees everywhere
+    assert all(r[2] == [0, 1, 2, 3] for r in res)
+    assert len({tuple(r[3]) for r in res}) == 1 and len(res[0][3]) == 1
+    for mid in (0, 1):  # each member's batch is split over its 2 replicas (remainder to replica 0)
+        assert res[0][4][mid] - res[1][4][mid] in (0, 1) and res[1][4][mid] > 0
+    # files: one learning curve per member, written once per round (leader only)
+    for mid in range(4):
+        rows = open(os.path.join(tmp_path, "savedata", "model_%d" % mid, "learning_curve.csv")).read().splitlines()
+        assert len(rows) == 1 + 2, rows

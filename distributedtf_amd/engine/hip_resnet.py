@@ -767,7 +767,7 @@ class _StepPlan:
         # head (fwd + bwd of GAP/dense/CE + final-BN reductions)
         fb = prog.final_bn
         hw = L.final_hw
-        hwork = self._work_member(target_items=512)
+        hwork = self._work_member(target_items=int(os.environ.get("DTF_HEAD_ITEMS", "512")))
         ha = HeadArgs()
         ha.x, ha.labels, ha.work = _p(self.xs[-1]), _p(self.labels), _p(hwork)
         ha.params, ha.p_mstride = _p(e.state), e.S
@@ -919,7 +919,7 @@ class _StepPlan:
                 self._bn_ew(lib.dtf_bn_add_relu, (hw_o, y.shape[3]), bnb, hb, add=x, out=y)
         # head: GAP + dense + CE on the last block output (no final BN: gamma_off = -1)
         hw = L.final_hw
-        hwork = self._work_member(target_items=512)
+        hwork = self._work_member(target_items=int(os.environ.get("DTF_HEAD_ITEMS", "512")))
         ha_ = HeadArgs()
         ha_.x, ha_.labels, ha_.work = _p(self.xs[-1]), _p(self.labels), _p(hwork)
         ha_.params, ha_.p_mstride = _p(e.state), e.S

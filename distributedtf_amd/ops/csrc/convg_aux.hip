@@ -292,6 +292,7 @@ __global__ __launch_bounds__(256) void cg_gap_kernel(GapArgs a) {
   const float* co = a.coef ? a.coef + (long)slot * 4 * a.cmax : nullptr;
   for (int c0 = threadIdx.x * 8; c0 < a.C; c0 += blockDim.x * 8) {
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 7  // several independent loads per round trip (hw = 49 for the 224x224 net)
     for (int p = 0; p < a.hw; ++p) {
       const uint4 v = *reinterpret_cast<const uint4*>(a.x + ((long)img * a.hw + p) * a.C + c0);
       const uint32_t w32[4] = {v.x, v.y, v.z, v.w};
@@ -319,6 +320,7 @@ __global__ __launch_bounds__(256) void cg_gap_bwd_reduce_kernel(GapArgs a) {
     const float g = a.dfeat[(long)img * a.C + c] * inv_hw;
     const float sc = co[c], sh = co[a.cmax + c], mu = co[2 * a.cmax + c], iv = co[3 * a.cmax + c];
     float s = 0.f, q = 0.f;
+#pragma unroll 7
     for (int p = 0; p < a.hw; ++p) {
       const float xv = bf2f(a.x[((long)img * a.hw + p) * a.C + c]);
       if (xv * sc + sh > 0.f) {

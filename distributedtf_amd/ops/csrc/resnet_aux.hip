@@ -260,6 +260,9 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
     const int img = img0 + im;
     const bf16_t* xp = a.x + (long)img * a.hw * a.C + c;
     float f = 0.f;
+    // unrolled so 16 independent loads are in flight per round trip (a runtime-trip loop otherwise pays the
+    // full load latency once per pixel: 64 round trips per image)
+#pragma unroll 16
     for (int p = 0; p < a.hw; ++p) f += fmaxf(bf2f(xp[(long)p * a.C]) * s_c + t_c, 0.f);
     f *= inv_hw;
     float logit[16];
@@ -307,6 +310,7 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
       }
       const float g = dfeat * inv_hw;  // dL/d(post-relu activation), identical for every pixel
       a.dfeat[(long)img * a.C + c] = g;
+#pragma unroll 16
       for (int p = 0; p < a.hw; ++p) {
         const float xv = bf2f(xp[(long)p * a.C]);
         if (xv * s_c + t_c > 0.f) {

@@ -106,7 +106,8 @@ def main():
 
     def exploit_cycle(losses):
         # score = -loss (no eval inside the timed region); full gather/plan/copy/perturb cycle
-        vals = [[m.cluster_id, -float(losses[i].item()), m.hparams] for i, m in enumerate(members)]
+        ls = losses.float().tolist()  # one device sync for the whole population
+        vals = [[m.cluster_id, -ls[i], m.hparams] for i, m in enumerate(members)]
         parts = comm.allgather(vals)
         allv = [v for p in parts for v in p]
         plan = plan_exploit(allv)

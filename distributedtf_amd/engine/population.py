@@ -115,8 +115,10 @@ class PopulationEngine:
             self.free_slots.append(slot)
             self.free_slots.sort()
 
-    def on_state_imported(self, slot: int) -> None:
-        self.host_step[slot] = int(round(float(self.step_col()[slot].item())))
+    def on_state_imported(self, slot: int, step: Optional[int] = None) -> None:
+        """A member's state row was overwritten (exploit).  ``step``: the source's step counter when the caller
+        knows it (same-GPU copy) -- avoids a device sync; otherwise read back from the imported row."""
+        self.host_step[slot] = int(step) if step is not None else int(round(float(self.step_col()[slot].item())))
         self.backend.on_params_changed([slot])
 
     # --------------------------------------------------------------- training

@@ -117,8 +117,8 @@ class EngineModel(ModelBase):
         self.engine.state_row(self.slot).copy_(flat.to(self.engine.state.device, torch.float32))
         self.on_state_imported()
 
-    def on_state_imported(self):
-        self.engine.on_state_imported(self.slot)
+    def on_state_imported(self, step=None):
+        self.engine.on_state_imported(self.slot, step)
 
     def release(self):
         self.engine.remove_member(self.slot)

@@ -78,11 +78,29 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(const float* __restric
     }
   }
   if (dgr_off >= 0) {
-    const int nd = cin * kk * cout;
-    for (int i = t0; i < nd; i += tstride) {
-      const int co = i % cout, rest = i / cout;  // rest = ci*kk + tap
-      const int tap = rest % kk, ci = rest / kk;
-      d[i] = f2bf(p[(co * kk + tap) * cin + ci]);
+    if (cout <= 64 && cin <= 64) {
+      // IHWO = per-tap [co][ci] -> [ci][co] transposes through LDS: coalesced reads along ci, coalesced writes
+      // along co (the direct gather read one cache line per element)
+      __shared__ float tt[64][65];
+      for (int tap = blockIdx.y; tap < kk; tap += gridDim.y) {
+        for (int e = threadIdx.x; e < cout * cin; e += blockDim.x) {
+          const int co = e / cin, ci = e - co * cin;
+          tt[co][ci] = p[(co * kk + tap) * cin + ci];
+        }
+        __syncthreads();
+        for (int e = threadIdx.x; e < cout * cin; e += blockDim.x) {
+          const int ci = e / cout, co = e - ci * cout;
+          d[(ci * kk + tap) * cout + co] = f2bf(tt[co][ci]);
+        }
+        __syncthreads();
+      }
+    } else {
+      const int nd = cin * kk * cout;
+      for (int i = t0; i < nd; i += tstride) {
+        const int co = i % cout, rest = i / cout;  // rest = ci*kk + tap
+        const int tap = rest % kk, ci = rest / kk;
+        d[i] = f2bf(p[(co * kk + tap) * cin + ci]);
+      }
     }
   }
 }

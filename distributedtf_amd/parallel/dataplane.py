@@ -56,7 +56,12 @@ class DataPlane:
                         dst.copy_(src)
                         hook = getattr(dst_m, "on_state_imported", None)
                         if hook is not None:
-                            hook()
+                            # the winner's step counter is known on the host: no device round trip
+                            step = getattr(local_members[src_id], "global_step", None)
+                            if step is not None:
+                                hook(step)
+                            else:
+                                hook()
                     else:
                         dst_m.import_state(src.clone())
                 self.bytes_moved += src.numel() * src.element_size()

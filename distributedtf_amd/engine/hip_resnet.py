@@ -689,7 +689,7 @@ class _StepPlan:
         # per-launch budget for the dW partials (bytes of slab stores, or of atomics without slabs): bounds the
         # workgroup count of the fused kernel
         wn = 9 * C * C
-        budget = float(os.environ.get("DTF_FUSED_ATOMIC_BYTES_%d" % C, {64: 32e6}.get(C, 16e6)))
+        budget = float(os.environ.get("DTF_FUSED_ATOMIC_BYTES_%d" % C, {64: 48e6}.get(C, 16e6)))
         n_wg = max(64, min(128 * len(self.slots), int(budget / (4.0 * wn))))
         # optional floor (e.g. 256: fill every CU for a single member).  Off: measured slower at pop 1 (1.64 vs
         # 1.60 ms/step), the extra dW slab bytes cost more than the idle CUs

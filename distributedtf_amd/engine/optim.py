@@ -111,3 +111,33 @@ def apply_reference(params: torch.Tensor, grads: torch.Tensor, slot1: torch.Tens
             w.sub_(b)
         else:
             raise ValueError("unknown optimizer code %d" % code)
+
+
+# TF1 optimizer slot variable names (tf.train.*Optimizer._create_slots): slot1 / slot2 of the flat state
+TF_SLOT_NAMES = {
+    "gd": (None, None),
+    "Momentum": ("Momentum", None),
+    "Adam": ("Adam", "Adam_1"),
+    "Adagrad": ("Adagrad", None),
+    "Adadelta": ("Adadelta", "Adadelta_1"),
+    "RMSProp": ("RMSProp", "RMSProp_1"),
+}
+
+
+def tf_optimizer_tensors(optimizer: str, trainable, step: int):
+    """Slot tensors (``<var>/<Slot>``) + optimizer non-slot variables of a TF1 checkpoint.
+
+    ``trainable``: iterable of (name, value, slot1_value, slot2_value) with numpy arrays already in TF layout."""
+    import numpy as np
+    n1, n2 = TF_SLOT_NAMES.get(optimizer, (None, None))
+    out = {}
+    for name, _, s1, s2 in trainable:
+        if n1:
+            out["%s/%s" % (name, n1)] = s1
+        if n2:
+            out["%s/%s" % (name, n2)] = s2
+    if optimizer == "Adam":  # AdamOptimizer's beta powers after `step` updates
+        out["beta1_power"] = np.array(0.9 ** step, dtype=np.float32)
+        out["beta2_power"] = np.array(0.999 ** step, dtype=np.float32)
+    out["global_step"] = np.array(step, dtype=np.int64)
+    return out

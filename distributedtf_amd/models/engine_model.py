@@ -53,7 +53,7 @@ class EngineModel(ModelBase):
     # ------------------------------------------------------------------------
     def __init__(self, cluster_id, hparams, save_base_dir, seed=None, device=None, backend="auto",
                  capacity=8, use_synthetic_data=None, data_dir=None, max_train_steps=None,
-                 checkpoint_every_round=True, eval_every_round=True, dp=None, **kw):
+                 checkpoint_every_round=True, eval_every_round=True, dp=None, tf_checkpoint=False, **kw):
         super().__init__(cluster_id, hparams, save_base_dir, seed=seed)
         self.dp = dp  # parallel.dataparallel.DPContext: this member is one replica of a data-parallel group
         self.options = dict(kw)
@@ -62,6 +62,7 @@ class EngineModel(ModelBase):
         self.use_synthetic_data = use_synthetic_data
         self.max_train_steps = max_train_steps
         self.checkpoint_every_round = checkpoint_every_round
+        self.tf_checkpoint = tf_checkpoint  # also export the reference's TF tensor-bundle format every round
         self.eval_every_round = eval_every_round
         self.arch = self.make_arch()
         key = (type(self).__name__, str(self.device), self.arch.name, backend)
@@ -119,6 +120,14 @@ class EngineModel(ModelBase):
 
     def on_state_imported(self, step=None):
         self.engine.on_state_imported(self.slot, step)
+
+    def tf_variables(self):
+        """This member's state as the reference's TF1 checkpoint variables (name -> numpy array)."""
+        e, s = self.engine, self.slot
+        row = e.state[s].detach().float().cpu().numpy()
+        P, Pp, R = e.P, e.Pp, e.R
+        return self.arch.tf_variables(row[:P], row[Pp:Pp + P], row[2 * Pp:2 * Pp + P], row[3 * Pp:3 * Pp + R],
+                                      self.hparams["opt_case"]["optimizer"], int(self.global_step))
 
     def release(self):
         self.engine.remove_member(self.slot)
@@ -220,6 +229,8 @@ class EngineModel(ModelBase):
         self.epoches_trained += num_epoch
         if self.checkpoint_every_round:
             self.save_checkpoint()
+            if self.tf_checkpoint and not self.is_dp_follower:
+                self.export_tf_checkpoint()
 
     def train(self, num_epoch, total_epochs):
         failed = type(self).train_population([self], num_epoch, total_epochs)

@@ -43,6 +43,28 @@ class MnistArch:
         self.n_running = 0
         self.n_reg = 0
 
+    def tf_variables(self, params, slot1, slot2, running, optimizer, step):
+        """Reference ``cnn_model_fn`` names/layouts: conv2d, conv2d_1 (HWIO kernels + bias), dense (3136 x 1024),
+        dense_1 (1024 x 10), optimizer slots, global_step (``mnist_model.py:62-126``)."""
+        from ..engine.optim import tf_optimizer_tensors
+        out, trainable = {}, []
+        names = {"conv1": "conv2d", "conv2": "conv2d_1", "dense1": "dense", "dense2": "dense_1"}
+        for n, (off, shp) in self.offsets.items():
+            layer, kind = n.split("_")
+            numel = 1
+            for d in shp:
+                numel *= d
+            if kind == "w":
+                layout = (lambda a: a.transpose(1, 2, 3, 0)) if len(shp) == 4 else (lambda a: a.T)
+                tf_name = names[layer] + "/kernel"
+            else:
+                layout, tf_name = (lambda a: a), names[layer] + "/bias"
+            t = [layout(a[off:off + numel].reshape(shp)).astype("float32") for a in (params, slot1, slot2)]
+            out[tf_name] = t[0]
+            trainable.append((tf_name, t[0], t[1], t[2]))
+        out.update(tf_optimizer_tensors(optimizer, trainable, step))
+        return out
+
     def view(self, params, name):
         off, shp = self.offsets[name]
         numel = 1

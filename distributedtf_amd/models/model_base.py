@@ -114,6 +114,26 @@ class ModelBase(object):
         if wait:
             flush_checkpoints()
 
+    def tf_variables(self) -> Dict[str, Any]:
+        """name -> numpy array under the reference's TF1 variable names (families that map onto TF layers)."""
+        raise NotImplementedError("%s has no TensorFlow variable mapping" % type(self).__name__)
+
+    def export_tf_checkpoint(self, directory: Optional[str] = None) -> str:
+        """Write the member in the reference's on-disk format: a TF tensor bundle ``model.ckpt-<step>.index`` /
+        ``.data-00000-of-00001`` (byte-compatible with TF 1.x ``Saver``; utils/tf_bundle.py) plus the
+        ``checkpoint`` state file naming it.  Returns the checkpoint prefix."""
+        from ..utils.tf_bundle import write_bundle
+        flush_checkpoints()
+        d = directory or self.ensure_save_dir()
+        tensors = self.tf_variables()
+        step = int(tensors["global_step"]) if "global_step" in tensors else 0
+        prefix = os.path.join(d, "model.ckpt-%d" % step)
+        write_bundle(prefix, tensors)
+        with open(os.path.join(d, "checkpoint"), "w") as f:
+            f.write('model_checkpoint_path: "model.ckpt-%d"\nall_model_checkpoint_paths: "model.ckpt-%d"\n'
+                    % (step, step))
+        return prefix
+
     def has_checkpoint(self) -> bool:
         flush_checkpoints()
         return os.path.isfile(os.path.join(self.save_dir, "model.ckpt"))

@@ -1,0 +1,21 @@
+// Host-side helpers of the runtime (no device code): CRC32C (Castagnoli) for the TensorFlow tensor-bundle
+// checkpoint writer (utils/tf_bundle.py) -- SSE4.2 crc32 instructions, 8 bytes per step.
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+#include <nmmintrin.h>
+
+extern "C" __attribute__((visibility("default"), target("sse4.2"))) uint32_t dtf_crc32c(const uint8_t* p, size_t n,
+                                                                                        uint32_t crc) {
+  uint64_t c = ~crc;
+  while (n >= 8) {
+    uint64_t v;
+    std::memcpy(&v, p, 8);
+    c = _mm_crc32_u64(c, v);
+    p += 8;
+    n -= 8;
+  }
+  uint32_t c32 = (uint32_t)c;
+  while (n--) c32 = _mm_crc32_u8(c32, *p++);
+  return ~c32;
+}

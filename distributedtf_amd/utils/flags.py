@@ -112,6 +112,8 @@ def build_parser(defaults: Optional[Dict[str, Any]] = None) -> argparse.Argument
     p.add_argument("--stop_threshold", type=float, default=None)
     p.add_argument("--export_dir", default=None)
     p.add_argument("--no_checkpoint", action="store_true")
+    p.add_argument("--tf_checkpoint", action="store_true",
+                   help="also write each member's checkpoint as a TF 1.x tensor bundle (model.ckpt-<step>.*)")
     p.add_argument("--deterministic", action="store_true",
                    help="replayable run: seeded RNGs, deterministic torch algorithms, torch backend (the HIP kernels "
                         "reduce BatchNorm statistics with fp32 atomics, so they are not bitwise replayable)")
@@ -133,6 +135,7 @@ class MainArgs(argparse.Namespace):
             kw["use_synthetic_data"] = self.use_synthetic_data
             kw["max_train_steps"] = self.max_train_steps
             kw["checkpoint_every_round"] = not self.no_checkpoint
+            kw["tf_checkpoint"] = bool(getattr(self, "tf_checkpoint", False))
             if self.data_dir:
                 kw["data_dir"] = self.data_dir
         if self.model in ("cifar10", "imagenet"):

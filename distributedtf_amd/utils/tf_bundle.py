@@ -1,4 +1,4 @@
-"""Read-only parser for TensorFlow tensor-bundle checkpoints (``model.ckpt.index`` + ``.data-*``).
+"""TensorFlow tensor-bundle checkpoints (``model.ckpt.index`` + ``.data-*``): reader and writer.
 
 Used by the golden-fixture tests (reference ``official/utils/testing/reference_data``,
 SURVEY §4): the reference's only numerics fixtures are TF 1.x checkpoints, and
@@ -12,6 +12,12 @@ Format notes (public LevelDB / TF tensor_bundle specs):
   block = entries (shared varint, non-shared varint, value-len varint, key delta, value) + restarts + trailer
   (1-byte compression type, 4-byte crc); BundleEntryProto: 1 dtype, 2 shape{2 dim{1 size}}, 3 shard_id,
   4 offset, 5 size, 6 crc32c.
+
+The writer (``write_bundle``) produces the same layout TF 1.x ``Saver`` writes -- one data shard, an index
+SSTable (header entry under the empty key, entries sorted by name, restart interval 16, uncompressed blocks with
+masked CRC32C trailers, empty metaindex, footer) -- so a member's state can be exported in the reference's
+checkpoint format (``ModelBase.export_tf_checkpoint``).  CRC32C runs natively (``ops/csrc/host.hip``, SSE4.2)
+with a pure-Python fallback.
 """
 
 from __future__ import annotations
@@ -147,3 +153,129 @@ def load_bundle(prefix: str) -> Dict[str, np.ndarray]:
         raw = shards[sid][e["offset"]:e["offset"] + e["size"]]
         out[name] = np.frombuffer(raw, dtype=dt).reshape(e["shape"]).copy()
     return out
+
+
+# ------------------------------------------------------------------------------------------------- writer
+_NP2TF = {np.dtype(v): k for k, v in _DTYPES.items()}
+_CRC_TABLE = None
+
+
+def _crc32c_py(data: bytes, crc: int = 0) -> int:
+    global _CRC_TABLE
+    if _CRC_TABLE is None:
+        tab = []
+        for i in range(256):
+            c = i
+            for _ in range(8):
+                c = (c >> 1) ^ 0x82F63B78 if c & 1 else c >> 1
+            tab.append(c)
+        _CRC_TABLE = tab
+    c = crc ^ 0xFFFFFFFF
+    for b in data:
+        c = _CRC_TABLE[(c ^ b) & 0xFF] ^ (c >> 8)
+    return c ^ 0xFFFFFFFF
+
+
+def crc32c(data: bytes) -> int:
+    """CRC32C (Castagnoli): the native SSE4.2 routine of the kernel library when it loads, else Python."""
+    try:
+        import ctypes
+        from .. import ops
+        fn = ops.lib().dtf_crc32c
+        fn.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32]
+        fn.restype = ctypes.c_uint32
+        return int(fn(bytes(data), len(data), 0))
+    except Exception:
+        return _crc32c_py(bytes(data))
+
+
+def masked_crc32c(data: bytes) -> int:
+    c = crc32c(data)
+    return ((((c >> 15) | (c << 17)) & 0xFFFFFFFF) + 0xA282EAD8) & 0xFFFFFFFF
+
+
+def _put_varint(v: int) -> bytes:
+    out = bytearray()
+    while True:
+        b = v & 0x7F
+        v >>= 7
+        if v:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def _pb_varint(field: int, v: int) -> bytes:
+    return _put_varint(field << 3) + _put_varint(v) if v else b""
+
+
+def _pb_bytes(field: int, b: bytes) -> bytes:
+    return _put_varint((field << 3) | 2) + _put_varint(len(b)) + b
+
+
+def _entry_proto(dtype: int, shape, offset: int, size: int, crc: int) -> bytes:
+    dims = b"".join(_pb_bytes(2, _pb_varint(1, int(d)) if d else b"") for d in shape)
+    msg = _pb_varint(1, dtype) + _pb_bytes(2, dims)
+    msg += _pb_varint(4, offset) + _pb_varint(5, size)
+    return msg + _put_varint((6 << 3) | 5) + struct.pack("<I", crc)
+
+
+def _block(entries, restart_interval: int = 16) -> bytes:
+    buf, restarts, last = bytearray(), [], b""
+    for i, (k, v) in enumerate(entries):
+        if i % restart_interval == 0:
+            restarts.append(len(buf))
+            shared = 0
+        else:
+            shared = 0
+            while shared < min(len(k), len(last)) and k[shared] == last[shared]:
+                shared += 1
+        buf += _put_varint(shared) + _put_varint(len(k) - shared) + _put_varint(len(v)) + k[shared:] + v
+        last = k
+    if not restarts:
+        restarts = [0]
+    for r in restarts:
+        buf += struct.pack("<I", r)
+    buf += struct.pack("<I", len(restarts))
+    return bytes(buf)
+
+
+def _with_trailer(block: bytes) -> bytes:
+    return block + b"\x00" + struct.pack("<I", masked_crc32c(block + b"\x00"))
+
+
+def write_bundle(prefix: str, tensors: Dict[str, np.ndarray]) -> None:
+    """Write ``prefix.index`` + ``prefix.data-00000-of-00001`` holding ``tensors`` (name -> array)."""
+    names = sorted(tensors)
+    data, entries, off = bytearray(), [], 0
+    for n in names:
+        a = np.asarray(tensors[n])
+        if not a.flags.c_contiguous:  # (np.ascontiguousarray would turn scalars into shape (1,))
+            a = a.copy()
+        dt = _NP2TF.get(a.dtype)
+        if dt is None:
+            raise ValueError("unsupported dtype %s for %s" % (a.dtype, n))
+        raw = a.astype(a.dtype.newbyteorder("<"), copy=False).tobytes()
+        entries.append((n.encode(), _entry_proto(dt, a.shape, off, len(raw), masked_crc32c(raw))))
+        data += raw
+        off += len(raw)
+    header = _pb_varint(1, 1) + _pb_bytes(3, _pb_varint(1, 1))  # num_shards 1, version {producer 1}
+    dblock = _with_trailer(_block([(b"", header)] + entries))
+    meta = _with_trailer(_block([]))
+    last_key = entries[-1][0] if entries else b""
+    # LevelDB BytewiseComparator::FindShortSuccessor of the block's last key (what TF's table builder stores)
+    for i, byte in enumerate(last_key):
+        if byte != 0xFF:
+            last_key = last_key[:i] + bytes([byte + 1])
+            break
+    index = _with_trailer(_block([(last_key, _put_varint(0) + _put_varint(len(dblock) - 5))]))
+    meta_off = len(dblock)
+    index_off = meta_off + len(meta)
+    footer = _put_varint(meta_off) + _put_varint(len(meta) - 5) + _put_varint(index_off) + _put_varint(len(index) - 5)
+    footer += b"\x00" * (40 - len(footer)) + struct.pack("<Q", _MAGIC)
+    os.makedirs(os.path.dirname(prefix) or ".", exist_ok=True)
+    with open(prefix + ".data-00000-of-00001", "wb") as f:
+        f.write(bytes(data))
+    with open(prefix + ".index", "wb") as f:
+        f.write(dblock + meta + index + footer)

@@ -129,6 +129,35 @@ class EngineModel(ModelBase):
         return self.arch.tf_variables(row[:P], row[Pp:Pp + P], row[2 * Pp:2 * Pp + P], row[3 * Pp:3 * Pp + R],
                                       self.hparams["opt_case"]["optimizer"], int(self.global_step))
 
+    def import_tf_checkpoint(self, prefix: str) -> int:
+        """Load a TF tensor bundle written under the reference's variable names (ours or TF's own ``Saver``)
+        into this member: weights, BN moving statistics, the optimizer slots present in the bundle, global_step.
+        The name -> state-row mapping is ``tf_variables`` evaluated on position indices, so every layout
+        transform is inverted exactly.  Returns the number of tensors applied."""
+        import numpy as np
+        from ..utils.tf_bundle import load_bundle
+        e, s = self.engine, self.slot
+        P, Pp, R = e.P, e.Pp, e.R
+        ar = np.arange(max(P, R), dtype=np.float64)
+        pos = self.arch.tf_variables(ar[:P], Pp + ar[:P], 2 * Pp + ar[:P], 3 * Pp + ar[:R],
+                                     self.hparams["opt_case"]["optimizer"], 0, dtype="float64")
+        tensors = load_bundle(prefix)
+        row = e.state[s].detach().cpu().numpy().copy()
+        used = 0
+        for name, where in pos.items():
+            if name in ("global_step", "beta1_power", "beta2_power") or name not in tensors:
+                continue
+            val = np.asarray(tensors[name], dtype=np.float32)
+            if val.shape != where.shape:
+                raise ValueError("%s: checkpoint shape %s != model %s" % (name, val.shape, where.shape))
+            row[where.astype(np.int64).ravel()] = val.ravel()
+            used += 1
+        step = int(np.asarray(tensors.get("global_step", 0)).reshape(-1)[0]) if "global_step" in tensors else 0
+        row[3 * Pp + R] = float(step)
+        e.state[s].copy_(torch.from_numpy(row).to(e.state.device))
+        self.on_state_imported(step)
+        return used
+
     def release(self):
         self.engine.remove_member(self.slot)
 

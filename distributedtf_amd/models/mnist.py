@@ -43,7 +43,7 @@ class MnistArch:
         self.n_running = 0
         self.n_reg = 0
 
-    def tf_variables(self, params, slot1, slot2, running, optimizer, step):
+    def tf_variables(self, params, slot1, slot2, running, optimizer, step, dtype="float32"):
         """Reference ``cnn_model_fn`` names/layouts: conv2d, conv2d_1 (HWIO kernels + bias), dense (3136 x 1024),
         dense_1 (1024 x 10), optimizer slots, global_step (``mnist_model.py:62-126``)."""
         from ..engine.optim import tf_optimizer_tensors
@@ -59,7 +59,7 @@ class MnistArch:
                 tf_name = names[layer] + "/kernel"
             else:
                 layout, tf_name = (lambda a: a), names[layer] + "/bias"
-            t = [layout(a[off:off + numel].reshape(shp)).astype("float32") for a in (params, slot1, slot2)]
+            t = [layout(a[off:off + numel].reshape(shp)).astype(dtype) for a in (params, slot1, slot2)]
             out[tf_name] = t[0]
             trainable.append((tf_name, t[0], t[1], t[2]))
         out.update(tf_optimizer_tensors(optimizer, trainable, step))

@@ -416,7 +416,7 @@ def regularization_loss(prog_n_reg: int, params: torch.Tensor, regularizer: Opti
 
 
 def tf_variables(prog: ResNetProgram, params, slot1, slot2, running, optimizer: str, step: int,
-                 scope: str = "resnet_model"):
+                 scope: str = "resnet_model", dtype="float32"):
     """The member's training state under the reference's TF variable names and layouts
     (``resnet_model.py``: ``tf.layers.conv2d`` kernels HWIO named conv2d, conv2d_1, .. in creation order;
     ``batch_normalization[_N]/{gamma,beta,moving_mean,moving_variance}``; ``dense/{kernel [C, classes], bias}``;
@@ -426,7 +426,7 @@ def tf_variables(prog: ResNetProgram, params, slot1, slot2, running, optimizer: 
     out, trainable = {}, []
 
     def var(name, sl, reshape, layout):
-        t = [layout(a[sl].reshape(reshape)).astype("float32") for a in (params, slot1, slot2)]
+        t = [layout(a[sl].reshape(reshape)).astype(dtype) for a in (params, slot1, slot2)]
         out[name] = t[0]
         trainable.append((name, t[0], t[1], t[2]))
 
@@ -438,8 +438,8 @@ def tf_variables(prog: ResNetProgram, params, slot1, slot2, running, optimizer: 
         base = "%sbatch_normalization%s" % (pre, "_%d" % b.idx if b.idx else "")
         var(base + "/gamma", slice(b.gamma_off, b.gamma_off + b.c), (b.c,), lambda v: v)
         var(base + "/beta", slice(b.beta_off, b.beta_off + b.c), (b.c,), lambda v: v)
-        out[base + "/moving_mean"] = running[b.run_off:b.run_off + b.c].astype("float32")
-        out[base + "/moving_variance"] = running[b.run_off + b.c:b.run_off + 2 * b.c].astype("float32")
+        out[base + "/moving_mean"] = running[b.run_off:b.run_off + b.c].astype(dtype)
+        out[base + "/moving_variance"] = running[b.run_off + b.c:b.run_off + 2 * b.c].astype(dtype)
     ncls, C = cfg.num_classes, cfg.final_size
     var(pre + "dense/kernel", slice(prog.dense_w_off, prog.dense_w_off + ncls * C), (ncls, C), lambda w: w.T)
     var(pre + "dense/bias", slice(prog.dense_b_off, prog.dense_b_off + ncls), (ncls,), lambda v: v)
@@ -471,8 +471,8 @@ class ResNetArch:
     def init_params(self, initializer, seed):
         return init_params(self.prog, initializer, seed)
 
-    def tf_variables(self, params, slot1, slot2, running, optimizer, step):
-        return tf_variables(self.prog, params, slot1, slot2, running, optimizer, step)
+    def tf_variables(self, params, slot1, slot2, running, optimizer, step, dtype="float32"):
+        return tf_variables(self.prog, params, slot1, slot2, running, optimizer, step, dtype=dtype)
 
     def forward(self, params, running, x_nhwc, training=True, dtype=torch.float32):
         return forward_reference(self.prog, params, running, x_nhwc, training=training, dtype=dtype)

@@ -74,3 +74,17 @@ def test_mnist_member_export_names(tmp_cwd):
     assert t["conv2d/kernel"].shape == (5, 5, 1, 32) and t["conv2d_1/kernel"].shape == (5, 5, 32, 64)
     assert t["dense/kernel"].shape == (3136, 1024) and t["dense_1/kernel"].shape == (1024, 10)
     assert "dense_1/bias/Momentum" in t
+
+
+@pytest.mark.parametrize("opt", ["Momentum", "Adam"])
+def test_tf_checkpoint_round_trip_into_member(tmp_cwd, opt):
+    from distributedtf_amd.models.cifar10_model import Cifar10Model
+    a = Cifar10Model(0, _hp(opt), "savedata/model_", seed=1, resnet_size=8, device="cpu", max_train_steps=3,
+                     use_synthetic_data=True)
+    a.train(1, 1)
+    prefix = a.export_tf_checkpoint()
+    b = Cifar10Model(1, _hp(opt), "savedata/model_", seed=2, resnet_size=8, device="cpu", use_synthetic_data=True)
+    assert not torch.equal(a.export_state(), b.export_state())
+    n = b.import_tf_checkpoint(prefix)
+    assert n > 0 and b.global_step == 3
+    torch.testing.assert_close(b.export_state(), a.export_state(), rtol=0, atol=0)

@@ -43,7 +43,9 @@ def _worker(rank, world, port, tmp, q):
                                                           device="cpu", eval_every_round=True))
         pop.train(2)
         flush_checkpoints()
-        states = {g.cluster_id: g.export_state().clone() for g in pop.worker.worker_graphs}
+        # numpy copies: torch CPU tensors would travel through the queue as shared-memory file descriptors, which
+        # the parent cannot open once this process has exited
+        states = {g.cluster_id: g.export_state().detach().cpu().numpy().copy() for g in pop.worker.worker_graphs}
         batches = {g.cluster_id: g.dp.local_batch(g.hparams["batch_size"]) for g in pop.worker.worker_graphs}
         gathered = comm.allgather(states)
         vals = pop.get_all_values()
@@ -73,7 +75,7 @@ def test_dp_groups_world4_dp2(tmp_path):
     assert sorted(gathered[2]) == [2, 3] and sorted(gathered[3]) == [2, 3]
     for a, b in ((0, 1), (2, 3)):
         for mid in gathered[a]:
-            assert torch.equal(gathered[a][mid], gathered[b][mid]), "replicas diverged (member %d)" % mid
+            assert (gathered[a][mid] == gathered[b][mid]).all(), "replicas diverged (member %d)" % mid
     # the population table has every member once; the exploit plan agrees everywhere
     assert all(r[2] == [0, 1, 2, 3] for r in res)
     assert len({tuple(r[3]) for r in res}) == 1 and len(res[0][3]) == 1

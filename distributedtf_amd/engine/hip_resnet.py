@@ -632,6 +632,8 @@ class _StepPlan:
         lds = 2304 + (nbuf * tsz + (2 * rows * H * (C + 8) if raw else 0)) * 2  # dY/X tiles [+ raw-x interiors]
         lib = ops.lib()
         slab = os.environ.get("DTF_DW_SLAB", "1") == "1"
+        if C == 64 and os.environ.get("DTF_DW_SLAB_C64", "1") != "1":
+            slab = False  # fp32 atomics straight into the gradient row (no reduce launch)
         side = slab and self.side_reduce
         n_red = 0
         if slab and not side:

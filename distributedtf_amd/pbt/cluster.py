@@ -31,6 +31,7 @@ from .exploit import apply_plan_to_values, plan_exploit
 from .hparams import WorkerInstruction, generate_random_hparam
 from . import reports
 from ..models.model_base import flush_checkpoints
+from ..utils.profiling import roctx_range
 
 
 def partition(pop_size: int, n_slots: int) -> List[Tuple[int, int]]:
@@ -401,12 +402,17 @@ class SPMDPopulation(_ReportMixin):
         for rnd in range(self.start_round, round_num):
             t0 = time.time()
             self.log("\nRound {}".format(rnd))
-            self.train_one_round(rnd, round_num)
+            # roctx ranges (rocprofv3 --marker-trace, DTF_ROCTX=1) around the PBT phases
+            with roctx_range("pbt/round%d/train" % rnd):
+                self.train_one_round(rnd, round_num)
             if self.do_exploit:
-                self.exploit()
+                with roctx_range("pbt/round%d/exploit" % rnd):
+                    self.exploit()
             if self.do_explore:
-                self.explore()
-            self.save_round_state(rnd + 1)
+                with roctx_range("pbt/round%d/explore" % rnd):
+                    self.explore()
+            with roctx_range("pbt/round%d/checkpoint" % rnd):
+                self.save_round_state(rnd + 1)
             self.round_times.append(time.time() - t0)
             self.log_round_metrics(rnd, self.round_times[-1])
             self.log("Round elapsed time: {}\n".format(datetime.timedelta(seconds=self.round_times[-1])))

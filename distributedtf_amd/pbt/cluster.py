@@ -27,7 +27,7 @@ import shutil
 import time
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
-from .exploit import apply_plan_to_values, plan_exploit
+from .exploit import apply_plan_to_values, plan_exploit, plan_reseed
 from .hparams import WorkerInstruction, generate_random_hparam
 from . import reports
 from ..models.model_base import flush_checkpoints
@@ -185,7 +185,7 @@ class PBTCluster(_ReportMixin):
         values, owner = self._gather()  # the recv is the end-of-TRAIN barrier
         t0 = time.time()
         self.pop_size = len(values)
-        plan = plan_exploit(values)
+        plan = plan_reseed(values) if getattr(self, "reseed_dead", False) else plan_exploit(values)
         self.last_plan = plan
         updates = apply_plan_to_values(values, plan)
         per_rank: Dict[int, list] = {r: [] for r in self.workers()}
@@ -236,7 +236,7 @@ class SPMDPopulation(_ReportMixin):
 
     def __init__(self, pop_size, comm, target_model_class, epochs_per_round=1, do_exploit=True, do_explore=True,
                  seed=None, savedata="savedata", model_kwargs=None, dataplane=None, hparams=None,
-                 verbose=True, inject_nan=None, resume=False, dp_size=1):
+                 verbose=True, inject_nan=None, resume=False, dp_size=1, reseed_dead=False):
         from .worker import TrainingWorker
         self.comm = comm
         self.rank = comm.Get_rank()
@@ -265,6 +265,8 @@ class SPMDPopulation(_ReportMixin):
             model_kwargs = dict(model_kwargs or {}, dp=self.dp)
         self.worker = TrainingWorker(comm, 0, target_model_class, save_base_dir=os.path.join(savedata, "model_"),
                                      seed=seed, model_kwargs=model_kwargs, dataplane=dataplane, verbose=verbose)
+        self.worker.reseed_dead = bool(reseed_dead)
+        self.reseed_dead = bool(reseed_dead)
         self.start_round = 0
         state = None
         if resume:
@@ -324,7 +326,8 @@ class SPMDPopulation(_ReportMixin):
             for g in list(self.worker.worker_graphs):
                 if g.cluster_id == mid:
                     g.accuracy = float("nan")
-                    self.worker._cull(g, "injected nan")
+                    if not self.reseed_dead:
+                        self.worker._cull(g, "injected nan")
 
     def exploit(self):
         parts = self.comm.allgather(self._values())  # also the end-of-train barrier
@@ -332,7 +335,7 @@ class SPMDPopulation(_ReportMixin):
         values = [v for part in parts for v in part]
         owner = {int(v[0]): r // self.dp_size for r, part in enumerate(parts) for v in part}  # member group
         self.pop_size = len(values)
-        plan = plan_exploit(values)
+        plan = plan_reseed(values) if getattr(self, "reseed_dead", False) else plan_exploit(values)
         self.last_plan = plan
         for p in plan:
             self.log("Copied: {} -> {}".format(p.src_id, p.dst_id))

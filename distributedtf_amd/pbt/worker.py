@@ -43,6 +43,7 @@ class TrainingWorker:
         self.train_time = 0.0
         self.explore_time = 0.0
         self.removed_ids: List[int] = []
+        self.reseed_dead = False  # SPMD --reseed_dead: NaN members stay and are re-seeded at the next exploit
 
     def log(self, *a):
         if self.verbose:
@@ -115,7 +116,7 @@ class TrainingWorker:
                     continue
                 self.log("Model {} epoch = {},  acc = {}".format(g.cluster_id, g.epoches_trained, g.get_accuracy()))
                 acc = g.get_accuracy()
-                if acc is None or (isinstance(acc, float) and math.isnan(acc)):
+                if (acc is None or (isinstance(acc, float) and math.isnan(acc))) and not self.reseed_dead:
                     self._cull(g, "nan accuracy")
         self.train_time += time.time() - t0
 

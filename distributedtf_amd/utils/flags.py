@@ -122,6 +122,8 @@ def build_parser(defaults: Optional[Dict[str, Any]] = None) -> argparse.Argument
                         "=1), no HIP graphs: a faulting kernel is reported at its own launch")
     p.add_argument("--dp_size", type=int, default=1,
                    help="ranks per population member (intra-member data parallelism; must divide the world)")
+    p.add_argument("--reseed_dead", action="store_true",
+                   help="re-seed members with NaN accuracy from the best members instead of culling them")
     p.add_argument("--resume", action="store_true",
                    help="continue a run from savedata/population_state.json + member checkpoints (no wipe)")
     return p

@@ -77,7 +77,7 @@ def main(argv=None):
         cluster = SPMDPopulation(args.population_size, comm, cls, epochs_per_round=args.epochs_per_round,
                                  do_exploit=args.do_exploit, do_explore=args.do_explore, seed=args.seed,
                                  savedata=savedata, model_kwargs=model_kwargs, inject_nan=inject,
-                                 resume=args.resume, dp_size=args.dp_size)
+                                 resume=args.resume, dp_size=args.dp_size, reseed_dead=args.reseed_dead)
 
     if not args.resume or getattr(cluster, "start_round", 0) == 0:
         cluster.dump_all_models_to_json(os.path.join(savedata, "initial_hp.json"))

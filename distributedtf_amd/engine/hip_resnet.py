@@ -128,6 +128,18 @@ def _register():
     _REGISTERED = True
 
 
+def _cpad(c: int) -> int:
+    """LDS pixel pitch (bf16 elements) of a C-channel tile: must match conv.hip ``cpad<C>()``."""
+    if os.environ.get("DTF_CPAD_OLD", "0") == "1":
+        return c + 8
+    return {16: 16, 32: 48, 64: 80}.get(c, c + 8)
+
+
+def _cpad_fwd(c: int) -> int:
+    """conv_fwd_s1 pitch (conv.hip ``cpad_fwd<C>()``)."""
+    return 24 if c == 16 and os.environ.get("DTF_CPAD_OLD", "0") != "1" else _cpad(c)
+
+
 def _p(t):
     return None if t is None else t.data_ptr()
 
@@ -494,7 +506,7 @@ class _StepPlan:
             a.st_out = _p(be.st_f(stats_bn))
         a.Hi, a.Wi, a.Ho, a.Wo, a.rows = Hi, Hi, Ho, Ho, rows
         rows_in = (rows - 1) * c.stride + c.k
-        tsz = (rows_in * (Hi + 2 * P) * (cin + 8) + 63) // 64 * 64
+        tsz = (rows_in * (Hi + 2 * P) * max(_cpad(cin), _cpad_fwd(cin)) + 8 + 63) // 64 * 64
         lds = 1280 + 2 * tsz * 2
         mode = 0 if in_bn is None else 1
         lib = ops.lib()
@@ -535,7 +547,7 @@ class _StepPlan:
             a.st_ep = _p(be.st_f(ep_bn))
             a.st_out = _p(be.st_b(ep_bn))
         a.Hi, a.Wi, a.Ho, a.Wo, a.rows = Hi, Hi, Ho, Ho, rows
-        tsz = (rows_t * (Ho + 2) * (c.cout + 8) + 63) // 64 * 64
+        tsz = (rows_t * (Ho + 2) * _cpad(c.cout) + 63) // 64 * 64
         lds = 2304 + 2 * tsz * 2
         lib = ops.lib()
         self._add(lib.dtf_conv_dgrad, ctypes.byref(a), c.cin, c.cout, S, K, mode, epi, work.shape[0], lds)
@@ -578,8 +590,8 @@ class _StepPlan:
         a.Hi, a.Wi, a.Ho, a.Wo, a.rows = Hi, Hi, Ho, Ho, rows
         rows_in = (rows - 1) * c.stride + c.k
         assert 32 % Ho == 0, "wgrad k-step addressing needs Wo | 32"
-        xt = (rows_in * (Hi + 2 * P) * (cin + 8) + 63) // 64 * 64
-        dt = (rows * Ho * (c.cout + 8) + 63) // 64 * 64
+        xt = (rows_in * (Hi + 2 * P) * _cpad(cin) + 63) // 64 * 64
+        dt = (rows * Ho * _cpad(c.cout) + 63) // 64 * 64
         lds = 1536 + 2 * (xt + dt) * 2  # double-buffered
         lib = ops.lib()
         self._add(lib.dtf_conv_wgrad, ctypes.byref(a), cin, c.cout, c.stride, c.k, mode_x, mode_dy, work.shape[0], lds)
@@ -625,11 +637,11 @@ class _StepPlan:
             a.st_ep = _p(be.st_f(x_bn))
             a.st_out = _p(be.st_b(x_bn))
         a.Hi, a.Wi, a.Ho, a.Wo, a.rows = H, H, H, H, rows
-        tsz = ((rows + 2) * (H + 2) * (C + 8) + 63) // 64 * 64
+        tsz = ((rows + 2) * (H + 2) * _cpad(C) + 8 + 63) // 64 * 64
         raw = C >= 64 or os.environ.get("DTF_RAWX16", "0") == "1"  # must match the build (conv.hip RAWX)
         sb = C == 16 and mode_dy != 3 and os.environ.get("DTF_FUSED_SB16", "1") == "1"  # must match conv.hip SB
         nbuf = 2 if sb else 4
-        lds = 2304 + (nbuf * tsz + (2 * rows * H * (C + 8) if raw else 0)) * 2  # dY/X tiles [+ raw-x interiors]
+        lds = 2304 + (nbuf * tsz + (2 * rows * H * _cpad(C) if raw else 0)) * 2  # dY/X tiles [+ raw-x interiors]
         lib = ops.lib()
         slab = os.environ.get("DTF_DW_SLAB", "1") == "1"
         if C == 64 and os.environ.get("DTF_DW_SLAB_C64", "1") != "1":

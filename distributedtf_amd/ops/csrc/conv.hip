@@ -12,8 +12,8 @@
 // pixel per lane) is stored as one 8-byte packed bf16 write, and a 16-pixel tile
 // of a 16-channel layer is a single contiguous 512-byte store.
 //
-// LDS tiles: [rows][cols][C + 8] bf16 with a zero halo; the 16-byte pad per pixel
-// makes ds_read_b128 pixel-gathers bank-conflict free.  The producing BatchNorm (+ReLU) of the input is applied
+// LDS tiles: [rows][cols][cpad<C>()] bf16 with a zero halo; the pixel pitch keeps the
+// ds_read_b128 pixel gathers free of bank conflicts (see cpad).  The producing BatchNorm (+ReLU) of the input is applied
 // while the tile is staged (global -> regs -> transform -> LDS), and BN statistics
 // of the output are reduced in registers/LDS and added to 8 replicated per-member
 // accumulators (cuts same-address atomic contention 8x); consumers sum the
@@ -28,6 +28,9 @@
 #define BN_EPS 1e-5f
 #ifndef DTF_FUSED_WAVES
 #define DTF_FUSED_WAVES(C, M) ((C) <= 16 && (M) != 3 && DTF_FUSED_SB16 ? 3 : (C) <= 32 ? 2 : 1)  // min waves / SIMD the fused bwd kernel is register-capped for
+#endif
+#ifndef DTF_CPAD_OLD
+#define DTF_CPAD_OLD 0  // 1: the previous uniform C + 8 LDS pixel pitch (A/B builds)
 #endif
 #ifndef DTF_SLAB_STORE
 #define DTF_SLAB_STORE 2  // dW slab store form: 0 plain, 1 nontemporal, 2 write-through (sc1) buffer stores
@@ -128,13 +131,28 @@ __device__ __forceinline__ void bn_bwd_coef(const float* stf, const float* stb, 
   C = -scale * mdz + scale * inv * mean * mdzx;
 }
 
-// LDS tiles keep 8 bf16 (16 B) of padding after every pixel: a 16-lane group reading
-// 16 consecutive pixels with ds_read_b128 then hits 16 distinct 4-bank groups for
-// C in {16, 32, 64} (pixel strides of 12 / 20 / 36 dwords), and every operand
-// address is an affine function of the pixel index (no swizzle arithmetic in the
-// inner loops).
+// LDS tiles are [rows][cols][cpad<C>()] bf16: the pixel pitch is picked per channel count so that the
+// MFMA operand gathers (ds_read_b128 of 16 consecutive pixels per lane group), the wgrad transposed reads and
+// the staging stores hit distinct banks under gfx950's lane grouping; every operand address stays an affine
+// function of the pixel index (no swizzle arithmetic in the inner loops).
 template <int C>
-__host__ __device__ constexpr int cpad() { return C + 8; }
+__host__ __device__ constexpr int cpad() {
+#if DTF_CPAD_OLD
+  return C + 8;
+#else
+  // pixel pitch in bf16: chosen with the gfx950 LDS lane-group banking of ds_read_b128 (4 x 16 lanes) /
+  // ds_read_b64_tr_b16 / ds_write_b128 for the tiles' access patterns (tools/lds_banks.py): 16 -> no pad,
+  // 32 -> +16, 64 -> +16 (the uniform +8 pad left 2-3-way conflicts on the MFMA operand gathers)
+  return C == 16 ? 16 : C == 32 ? 48 : C == 64 ? 80 : C + 8;
+#endif
+}
+
+// Forward (conv_fwd_s1) pitch: the C = 16 forward measured faster with the +8 pad (1 vs 3 MFMA-operand
+// gathers per row pair, different occupancy) -- the fused backward keeps the unpadded pitch.
+template <int C>
+__host__ __device__ constexpr int cpad_fwd() {
+  return (C == 16 && !DTF_CPAD_OLD) ? 24 : cpad<C>();
+}
 
 template <int C>
 __device__ __forceinline__ int lds_off(int r, int col, int wp, int chunk) {
@@ -427,9 +445,9 @@ __device__ __forceinline__ uint4 xform8r(uint4 v, uint4 v2, uint4 v3, int c0, co
 // 256 % (C/8) == 0); per slot: LDS offset, in-band global offset, and three bit masks (column/slot valid,
 // top halo row, bottom halo row) so an iteration only adds its band's row offset.  Inactive slots stage zeros
 // into pixel 0's pad lanes (never read), keeping load/store branch-free.
-template <int C, int RT, int W, int H>
+template <int C, int RT, int W, int H, int CPV = cpad<C>()>
 struct Stage {
-  static constexpr int WP = W + 2, CP = C + 8, NCH = C / 8, ROW = W * C;
+  static constexpr int WP = W + 2, CP = CPV, NCH = C / 8, ROW = W * C;
   static constexpr int TOTAL = RT * WP * NCH, MAXC = (TOTAL + 255) / 256;
   int loff[MAXC];
   int goff[MAXC];
@@ -444,7 +462,7 @@ struct Stage {
       const int idx = threadIdx.x + 256 * j;
       const int pc = idx / NCH, col = pc % WP, r = pc / WP;
       const bool act = idx < TOTAL;
-      loff[j] = act ? (r * WP + col) * CP + c0 : C;
+      loff[j] = act ? (r * WP + col) * CP + c0 : RT * WP * CP;  // inactive: the 8-element slack past the tile
       roff[j] = ((r - 1) * W + (col - 1)) * CP + c0;
       goff[j] = (r * ROW + (col - 1) * C + c0) * 2;  // bytes
       if (act && col >= 1 && col <= W) okm |= 1u << j;
@@ -652,12 +670,12 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
   constexpr int W = 512 / C, H = W, ROWS = 8, BANDS = H / ROWS;
   constexpr int NT = C / 16, WPT = 4 / NT;
   constexpr int KTOT = 9 * C, KS = (KTOT + 31) / 32;
-  constexpr int CP = cpad<C>(), RT = ROWS + 2, WP = W + 2;
-  constexpr int TSZ = (RT * WP * CP + 63) & ~63;
+  constexpr int CP = cpad_fwd<C>(), RT = ROWS + 2, WP = W + 2;
+  constexpr int TSZ = (RT * WP * CP + 8 + 63) & ~63;  // + slack for inactive staging slots
   constexpr int NTILES = ROWS * W / 16;
   static_assert(NTILES == WPT * MAXT, "every wave owns MAXT output tiles");
   constexpr int ROW = W * C, IMG = H * ROW;
-  using St = Stage<C, RT, W, H>;
+  using St = Stage<C, RT, W, H, CP>;
   constexpr int MAXC = St::MAXC;
   constexpr int LMODE = MODE_IN == 0 ? 0 : 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1153,7 +1171,7 @@ __global__ __launch_bounds__(256, DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_fus
   constexpr int NTN = 9 * C / 16;      // wgrad (tap, ci) tiles
   constexpr int NJ = (NTN + 3) / 4;
   constexpr int CP = cpad<C>(), RT = ROWS + 2, WP = W + 2;
-  constexpr int TSZ = (RT * WP * CP + 63) & ~63;
+  constexpr int TSZ = (RT * WP * CP + 8 + 63) & ~63;  // + slack for inactive staging slots
   constexpr int NTILES = ROWS * W / 16;
   static_assert(NTILES == WPT * MAXT, "every wave owns MAXT dgrad tiles");
   constexpr int ROW = W * C, IMG = H * ROW;

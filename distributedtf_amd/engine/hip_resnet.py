@@ -705,9 +705,9 @@ class _StepPlan:
         wn = 9 * C * C
         budget = float(os.environ.get("DTF_FUSED_ATOMIC_BYTES_%d" % C, {64: 48e6}.get(C, 16e6)))
         n_wg = max(64, min(128 * len(self.slots), int(budget / (4.0 * wn))))
-        # optional floor (e.g. 256: fill every CU for a single member).  Off: measured slower at pop 1 (1.64 vs
-        # 1.60 ms/step), the extra dW slab bytes cost more than the idle CUs
-        n_wg = max(n_wg, int(os.environ.get("DTF_FUSED_MIN_WG", "0")))
+        # floor of 256 workgroups: a single member would otherwise run the C = 16 / 32 layers on 128 of the 256
+        # CUs (pop 1: 1.54 -> 1.50 ms/step; larger populations already exceed it)
+        n_wg = max(n_wg, int(os.environ.get("DTF_FUSED_MIN_WG", "256")))
         return min(n_wg, self.N * bands)
 
     def _slab_floats(self):

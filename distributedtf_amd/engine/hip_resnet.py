@@ -409,7 +409,15 @@ class _StepPlan:
         self.dfeat = torch.zeros(N, cfg.final_size, dtype=torch.float32, device=dev)
         self._work_cache = {}
         # dW slab reductions on a forked stream (joined before the optimizer): off the critical path
-        self.side_reduce = dev.type == "cuda" and os.environ.get("DTF_SIDE_REDUCE", "0") == "1"
+        # DTF_SIDE_REDUCE: "1" = every channel width, "0" = none, or a comma list of widths (e.g. "64")
+        sr = os.environ.get("DTF_SIDE_REDUCE", "0").strip()
+        if dev.type != "cuda" or sr in ("", "0"):
+            self.side_cs = frozenset()
+        elif sr == "1":
+            self.side_cs = frozenset((16, 32, 64))
+        else:
+            self.side_cs = frozenset(int(v) for v in sr.split(",") if v)
+        self.side_reduce = bool(self.side_cs)
         self.side_stream = torch.cuda.Stream(device=dev) if self.side_reduce else None
         self.launches = []
         self._pending_slab = None  # (slab ptr, reduce table, C, grad offset) of the last fused launch
@@ -646,7 +654,7 @@ class _StepPlan:
         slab = os.environ.get("DTF_DW_SLAB", "1") == "1"
         if C == 64 and os.environ.get("DTF_DW_SLAB_C64", "1") != "1":
             slab = False  # fp32 atomics straight into the gradient row (no reduce launch)
-        side = slab and self.side_reduce
+        side = slab and C in self.side_cs
         n_red = 0
         if slab and not side:
             # ping-pong slab buffers: this launch writes one while its trailing workgroups reduce the other
@@ -707,7 +715,12 @@ class _StepPlan:
         n_wg = max(64, min(128 * len(self.slots), int(budget / (4.0 * wn))))
         # floor of 256 workgroups: a single member would otherwise run the C = 16 / 32 layers on 128 of the 256
         # CUs (pop 1: 1.54 -> 1.50 ms/step; larger populations already exceed it)
-        n_wg = max(n_wg, int(os.environ.get("DTF_FUSED_MIN_WG", "256")))
+        n_wg = max(n_wg, int(os.environ.get("DTF_FUSED_MIN_WG_%d" % C, os.environ.get("DTF_FUSED_MIN_WG", "256"))))
+        # per-member cap: fewer, fuller workgroups write fewer dW slab bytes.  C = 32 at 128 per member (2 bands
+        # each): pop 1 1.52 -> 1.44-1.47 ms/step over two runs (profiles/r1_s7_variants.log); pop >= 2 unchanged
+        cap = int(os.environ.get("DTF_FUSED_MAX_WG_%d" % C, {32: "128"}.get(C, "0")))
+        if cap > 0:
+            n_wg = min(n_wg, cap * len(self.slots))
         return min(n_wg, self.N * bands)
 
     def _slab_floats(self):

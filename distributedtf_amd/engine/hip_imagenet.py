@@ -151,7 +151,7 @@ class HipImageNetBackend:
         self.loss = torch.zeros(cap, dtype=torch.float32, device=self.dev)
         self.correct = torch.zeros(cap, dtype=torch.float32, device=self.dev)
         self._plans: Dict[tuple, "_ImageNetPlan"] = {}
-        self.use_graph = os.environ.get("DTF_HIP_GRAPH", "1") == "1"
+        self.use_graph = (os.environ.get("DTF_HIP_GRAPH", "1") == "1" and os.environ.get("DTF_DEBUG", "0") != "1")
 
     def on_params_changed(self, slots):
         slots = list(slots)

@@ -164,7 +164,7 @@ class HipMnistBackend:
         self.rng_counter = 0
         self.drop_rate = float(getattr(arch, "dropout", 0.4))
         self._plans: Dict[tuple, "_MnistPlan"] = {}
-        self.use_graph = os.environ.get("DTF_HIP_GRAPH", "1") == "1"
+        self.use_graph = (os.environ.get("DTF_HIP_GRAPH", "1") == "1" and os.environ.get("DTF_DEBUG", "0") != "1")
 
     # engine hooks ----------------------------------------------------------------------------
     def on_params_changed(self, slots):

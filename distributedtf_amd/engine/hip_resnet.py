@@ -283,7 +283,7 @@ class HipResNetBackend:
         self.loss = self.zbuf[nst:nst + cap]
         self.correct = self.zbuf[nst + cap:]
         self._plans: Dict[tuple, "_StepPlan"] = {}
-        self.use_graph = os.environ.get("DTF_HIP_GRAPH", "1") == "1"
+        self.use_graph = (os.environ.get("DTF_HIP_GRAPH", "1") == "1" and os.environ.get("DTF_DEBUG", "0") != "1")
 
     # --- engine hooks --------------------------------------------------------------
     def on_params_changed(self, slots):
@@ -1054,7 +1054,7 @@ class _StepPlan:
 
     def run(self, train=True):
         be = self.be
-        if be.use_graph and self.graph is None and os.environ.get("DTF_HIP_GRAPH", "1") == "1":
+        if be.use_graph and self.graph is None and (os.environ.get("DTF_HIP_GRAPH", "1") == "1" and os.environ.get("DTF_DEBUG", "0") != "1"):
             # warm up once eagerly (allocator, lazy init), then capture
             self._run_eager()
             torch.cuda.synchronize()

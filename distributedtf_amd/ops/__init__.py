@@ -42,10 +42,15 @@ def lib():
     with _LOCK:
         if _LIB is None:
             # DTF_LIB: an alternative build of the same sources (e.g. timing-only ablation builds of tools/)
-            path = os.environ.get("DTF_LIB") or _build.LIB
-            if path == _build.LIB and (not os.path.isfile(path) or
-                                       (os.environ.get("DTF_REBUILD") == "1" and _build.needs_build())):
-                _build.build(verbose=False)
+            debug = debug_mode()
+            default = _build.LIB_DEBUG if debug else _build.LIB
+            path = os.environ.get("DTF_LIB") or default
+            if path == default and (not os.path.isfile(path) or
+                                    (os.environ.get("DTF_REBUILD") == "1" and _build.needs_build(path))):
+                if debug:
+                    _build.build_debug(verbose=False)
+                else:
+                    _build.build(verbose=False)
             if not os.path.isfile(path):
                 raise RuntimeError("distributedtf_amd kernel library missing: %s" % path)
             L = ctypes.CDLL(path)
@@ -55,8 +60,77 @@ def lib():
                     continue
                 fn.argtypes = args
                 fn.restype = c_int
-            _LIB = L
+            _LIB = _DebugLib(L) if debug else L
     return _LIB
+
+
+def debug_mode() -> bool:
+    """DTF_DEBUG=1 (set by ``--debug_kernels``): load the debug build and check every launch synchronously."""
+    return os.environ.get("DTF_DEBUG", "0") == "1"
+
+
+class _DebugLib:
+    """Debug-mode view of the kernel library.
+
+    Every ``dtf_*`` launcher call is followed by a device synchronisation and a read of the per-source device
+    error words (``dtf_debug_error_<tu>``): a failed workgroup check, a failed host-side argument check (return
+    code >= 100000) or an asynchronous HIP error is raised as a RuntimeError naming the launcher, at the launch that
+    caused it instead of at some later synchronisation.  HIP-graph capture is off in this mode (flags.py).
+    """
+
+    def __init__(self, L):
+        self._L = L
+        self._err_fns = []
+        self.launches = 0
+
+    def _error_words(self):
+        if not self._err_fns:
+            import glob as _glob
+            names = [os.path.basename(p)[:-4] for p in _glob.glob(os.path.join(_build.CSRC, "*.hip"))]
+            for n in names:
+                fn = getattr(self._L, "dtf_debug_error_" + n, None)
+                if fn is not None:
+                    fn.argtypes = []
+                    fn.restype = c_int
+                    self._err_fns.append((n, fn))
+        return self._err_fns
+
+    def __getattr__(self, name):
+        fn = getattr(self._L, name)
+        if (not name.startswith("dtf_") or name.startswith("dtf_debug_") or name.endswith("_size")
+                or name == "dtf_crc32c" or not torch.cuda.is_available()):
+            return fn
+        return _CheckedLaunch(self, name, fn)
+
+
+class _CheckedLaunch:
+    """A launcher of the debug library: calls through, then synchronises and checks (see _DebugLib).
+    ``argtypes`` / ``restype`` read and write the underlying ctypes function."""
+
+    def __init__(self, owner, name, fn):
+        object.__setattr__(self, "_o", (owner, name, fn))
+
+    def __getattr__(self, attr):
+        return getattr(self._o[2], attr)
+
+    def __setattr__(self, attr, value):
+        setattr(self._o[2], attr, value)
+
+    def __call__(self, *args):
+        owner, name, fn = self._o
+        rc = fn(*args)
+        owner.launches += 1
+        if isinstance(rc, int) and rc >= 100000:
+            raise RuntimeError("%s: host-side argument check failed (csrc line %d)" % (name, rc - 100000))
+        try:
+            torch.cuda.synchronize()
+        except RuntimeError as e:
+            raise RuntimeError("%s: asynchronous HIP error after launch: %s" % (name, e)) from e
+        for tu, ef in owner._error_words():
+            v = ef()
+            if v > 0:
+                raise RuntimeError("%s: device check failed in %s.hip line %d" % (name, tu, v))
+        return rc
 
 
 def available() -> bool:

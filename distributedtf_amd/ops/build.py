@@ -17,6 +17,10 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libdtf_kernels.so")
+# Debug build of the same sources (-DDTF_DEBUG: workgroup-uniform device checks that record and skip instead of
+# trapping, host-side launch-argument checks; -g).  Loaded instead of LIB when DTF_DEBUG=1 (ops.lib()).
+LIB_DEBUG = os.path.join(HERE, "libdtf_kernels_debug.so")
+DEBUG_FLAGS = ["-DDTF_DEBUG=1", "-g"]
 ARCH = os.environ.get("DTF_OFFLOAD_ARCH", "gfx950")
 
 
@@ -74,5 +78,12 @@ def build(force: bool = False, verbose: bool = True, extra_flags=None, out: str 
     return out
 
 
+def build_debug(force: bool = False, verbose: bool = True) -> str:
+    return build(force=force, verbose=verbose, extra_flags=DEBUG_FLAGS, out=LIB_DEBUG)
+
+
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    if "--debug" in sys.argv:
+        build_debug(force="--force" in sys.argv)
+    else:
+        build(force="--force" in sys.argv)

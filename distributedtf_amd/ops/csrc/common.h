@@ -11,6 +11,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 
 #define DTF_API extern "C" __attribute__((visibility("default")))
 
@@ -43,3 +44,42 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 #define DTF_CHECK_LAUNCH() (int)hipGetLastError()
+
+// Debug build (ops/build.py --debug -> libdtf_kernels_debug.so, selected by DTF_DEBUG=1).
+// A violated device check never traps (a trapping wave can take the whole GPU down): the workgroup records the
+// failing source line in a device error word with a global atomic, prints once, and skips its work, so no
+// out-of-range access is issued.  The host reads the word back after each synchronous launch
+// (dtf_debug_error(); ops.lib() does this in debug mode) and raises with the launcher's name.
+// DTF_WG_CHECK(cond) must be workgroup-uniform and placed before the first barrier.
+#ifdef DTF_DEBUG
+// One error word per translation unit (no relocatable device code); DTF_DEBUG_EXPORT(tu) defines the host getter
+// dtf_debug_error_<tu>() that returns and clears it.
+static __device__ int dtf_debug_err;
+#define DTF_DEBUG_EXPORT(tu)                                                                        \
+  DTF_API int dtf_debug_error_##tu() {                                                              \
+    int v = 0, z = 0;                                                                               \
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(dtf_debug_err), sizeof(int)) != hipSuccess) return -1;   \
+    if (v) (void)hipMemcpyToSymbol(HIP_SYMBOL(dtf_debug_err), &z, sizeof(int));                     \
+    return v;                                                                                       \
+  }
+#define DTF_WG_CHECK(cond)                                                                          \
+  do {                                                                                              \
+    if (!(cond)) {                                                                                  \
+      if (threadIdx.x == 0 && atomicCAS(&dtf_debug_err, 0, __LINE__) == 0)                          \
+        printf("DTF_WG_CHECK failed %s:%d: %s (block %d)\n", __FILE__, __LINE__, #cond, (int)blockIdx.x); \
+      return;                                                                                       \
+    }                                                                                               \
+  } while (0)
+#define DTF_HOST_CHECK(cond)                                                                        \
+  do {                                                                                              \
+    if (!(cond)) {                                                                                  \
+      fprintf(stderr, "DTF_HOST_CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #cond);              \
+      return 100000 + __LINE__;                                                                     \
+    }                                                                                               \
+  } while (0)
+#else
+#define DTF_WG_CHECK(cond) ((void)0)
+#define DTF_DEBUG_EXPORT(tu)
+#define DTF_HOST_CHECK(cond) ((void)0)
+#endif
+#define DTF_ALIGNED16(p) ((((uintptr_t)(p)) & 15) == 0)

@@ -548,6 +548,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   bf16_t* tile0 = reinterpret_cast<bf16_t*>(smem + 1280);
 
   const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
   const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const float n_in = a.cnt[slot] * (float)(a.Hi * a.Wi);
@@ -685,6 +686,7 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
 #define SBUF(i) (tile0 + ((i) & 1) * TSZ)
 
   const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
   const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ct = wave % NT;
@@ -801,6 +803,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
   bf16_t* tile0 = reinterpret_cast<bf16_t*>(smem + 2304);
 
   const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
   const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // dy lives at the forward-output resolution; the BN transformed on load is the one after this conv.
@@ -990,6 +993,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
   bf16_t* xt = reinterpret_cast<bf16_t*>(smem + 1536);
 
   const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
   const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   make_coef<CIN, MODE_X>(coef_x, a, slot, a.cnt[slot] * (float)(a.Hi * a.Wi), a.st_x, nullptr, a.x_gamma, a.x_beta);
@@ -1203,6 +1207,7 @@ __global__ __launch_bounds__(256, DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_fus
     return;
   }
   const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
   const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ct = wave % NT;
@@ -1463,6 +1468,10 @@ __global__ __launch_bounds__(256) void dw_slab_reduce_kernel(const float* __rest
 template <typename KernelT>
 int launch(KernelT k, int nblocks, size_t lds, hipStream_t st, const ConvArgs& a) {
   if (nblocks <= 0) return 0;
+  DTF_HOST_CHECK(lds <= 160 * 1024);
+  DTF_HOST_CHECK(a.work != nullptr);
+  DTF_HOST_CHECK(DTF_ALIGNED16(a.x) && DTF_ALIGNED16(a.w) && DTF_ALIGNED16(a.y) && DTF_ALIGNED16(a.dy));
+  DTF_HOST_CHECK(a.Hi > 0 && a.Wi > 0 && a.Ho > 0 && a.Wo > 0 && a.rows > 0 && a.Ho <= a.Hi);
   hipLaunchKernelGGL(k, dim3(nblocks), dim3(256), lds, st, a);
   return DTF_CHECK_LAUNCH();
 }
@@ -1517,6 +1526,8 @@ DTF_API int dtf_dw_slab_reduce(const float* slab, const int4* red, int nmembers,
 #undef RED_CASE
   return -1;
 }
+
+DTF_DEBUG_EXPORT(conv)
 
 DTF_API int dtf_conv_args_size() { return (int)sizeof(ConvArgs); }
 

@@ -157,6 +157,7 @@ class MainArgs(argparse.Namespace):
             os.environ["AMD_SERIALIZE_KERNEL"] = "3"
             os.environ["HIP_LAUNCH_BLOCKING"] = "1"
             os.environ["DTF_HIP_GRAPH"] = "0"
+            os.environ["DTF_DEBUG"] = "1"  # debug kernel build + per-launch checks (ops._DebugLib)
         if self.deterministic:
             seed = 0 if self.seed is None else int(self.seed)
             if self.seed is None:

@@ -7,14 +7,15 @@ from distributedtf_amd.utils.flags import parse_main_args
 
 
 def test_debug_kernels_sets_hip_serialisation(monkeypatch):
-    for k in ("AMD_SERIALIZE_KERNEL", "HIP_LAUNCH_BLOCKING", "DTF_HIP_GRAPH"):
+    for k in ("AMD_SERIALIZE_KERNEL", "HIP_LAUNCH_BLOCKING", "DTF_HIP_GRAPH", "DTF_DEBUG"):
         monkeypatch.delenv(k, raising=False)
     a = parse_main_args(["4", "--model", "cifar10", "--debug_kernels"])
     a.apply_runtime_modes()
     assert os.environ["AMD_SERIALIZE_KERNEL"] == "3"
     assert os.environ["HIP_LAUNCH_BLOCKING"] == "1"
     assert os.environ["DTF_HIP_GRAPH"] == "0"
-    for k in ("AMD_SERIALIZE_KERNEL", "HIP_LAUNCH_BLOCKING", "DTF_HIP_GRAPH"):
+    assert os.environ["DTF_DEBUG"] == "1"
+    for k in ("AMD_SERIALIZE_KERNEL", "HIP_LAUNCH_BLOCKING", "DTF_HIP_GRAPH", "DTF_DEBUG"):
         monkeypatch.delenv(k, raising=False)
 
 

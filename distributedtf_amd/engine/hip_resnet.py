@@ -364,6 +364,7 @@ class _StepPlan:
         self.cnt = cnt.to(dev)
         self.slots_t = torch.tensor(slots, dtype=torch.int32, device=dev)
         self.slots_long = torch.tensor(slots, dtype=torch.long, device=dev)
+        self.loss_sel = torch.zeros(len(slots), dtype=be.loss.dtype, device=dev)
         H = cfg.image_size
         self.x_in = torch.zeros(N, H, H, 3, dtype=torch.float32, device=dev)
         self.labels = torch.zeros(N, dtype=torch.int32, device=dev)
@@ -1051,6 +1052,8 @@ class _StepPlan:
                 err = fn(*args, ops.stream())
                 if err != 0:
                     raise RuntimeError("kernel launch %s failed with %d" % (getattr(fn, "__name__", fn), err))
+        # per-member losses gathered inside the step (graph) so a replay leaves one copy for loss_view
+        torch.index_select(self.be.loss, 0, self.slots_long, out=self.loss_sel)
 
     def run(self, train=True):
         be = self.be
@@ -1075,4 +1078,5 @@ class _StepPlan:
             self._run_eager()
 
     def loss_view(self):
-        return self.be.loss[self.slots_long].clone()
+        # a copy: callers keep per-step losses across later replays (engine_model.loss_acc)
+        return self.loss_sel.clone()

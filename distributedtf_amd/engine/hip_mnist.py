@@ -31,7 +31,7 @@ import torch
 
 from .. import ops
 from ..data.datasets import IndexBatch, batch_len
-from .hip_resnet import advance_steps, note_step_advanced, same_batches, upload_hyper
+from .hip_resnet import PinnedStager, advance_steps, note_step_advanced, same_batches, upload_hyper
 
 c_void_p, c_int, c_long, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float
 
@@ -176,6 +176,11 @@ class HipMnistBackend:
     def shadow_weights(self):
         return self.shadow
 
+    def _upload_rng(self, v):
+        if getattr(self, "_rng_stage", None) is None:
+            self._rng_stage = PinnedStager(2, torch.int32)
+        self._rng_stage.upload(self.rng, v)
+
     def next_rng(self):
         self.rng_counter = (self.rng_counter + 1) & 0x7FFFFFFF
         return self.rng_seed, self.rng_counter
@@ -197,11 +202,11 @@ class HipMnistBackend:
         p = self.plan(slots, sizes)
         upload_hyper(e, slots, hparams, lrs)
         self.last_rng = self.next_rng()
-        self.rng.copy_(torch.tensor(self.last_rng, dtype=torch.int32), non_blocking=True)
+        self._upload_rng(self.last_rng)
         p.load_batch(batches)
         p.run()
         note_step_advanced(e, slots)
-        return self.loss[p.slots_long].clone()
+        return p.loss_sel.clone()  # gathered inside the step graph
 
     def forward_backward(self, slots, batches):
         raise RuntimeError("HipMnistBackend runs whole steps: use train_step")
@@ -230,6 +235,7 @@ class _MnistPlan:
         self.cnt = cnt.to(dev)
         self.slots_t = torch.tensor(slots, dtype=torch.int32, device=dev)
         self.slots_long = torch.tensor(slots, dtype=torch.long, device=dev)
+        self.loss_sel = torch.zeros(len(slots), dtype=be.loss.dtype, device=dev)
         bf = torch.bfloat16
         self.x = torch.zeros(N, 28, 28, dtype=torch.float32, device=dev)
         self.labels = torch.zeros(N, dtype=torch.int32, device=dev)
@@ -323,6 +329,7 @@ class _MnistPlan:
         e.dp_sync_grads(self.slots)  # data-parallel member groups only (no-op otherwise)
         ops.fused_optimizer(e.state, e.grads, e.hyper, e.Pp, e.P, e.n_reg, shadow=be.shadow, zero_grads=True)
         advance_steps(e, self.slots_long, self.slots_t)
+        torch.index_select(be.loss, 0, self.slots_long, out=self.loss_sel)
 
     def run(self):
         be = self.be

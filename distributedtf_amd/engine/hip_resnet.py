@@ -224,6 +224,31 @@ def upload_hyper(e, slots, hparams, lrs):
     e._hyper_dev["slots"] = tuple(slots)
 
 
+class PinnedStager:
+    """Small per-step host->device uploads through one pinned staging buffer.
+
+    A pageable ``non_blocking`` copy is staged synchronously and waits for the stream to drain, so the host
+    cannot queue step k+1 while step k runs.  Here the host waits only for the previous upload from this stager
+    (issued at the start of the previous step) before overwriting the staging buffer."""
+
+    def __init__(self, n, dtype):
+        self.host = torch.empty(n, dtype=dtype).pin_memory() if torch.cuda.is_available() else None
+        self.evt = None
+
+    def upload(self, dst, values):
+        if dst.device.type != "cuda" or self.host is None:
+            dst.copy_(torch.tensor(list(values), dtype=dst.dtype))
+            return
+        if self.evt is None:
+            self.evt = torch.cuda.Event()
+        else:
+            self.evt.synchronize()
+        for i, v in enumerate(values):
+            self.host[i] = v
+        dst.copy_(self.host[:len(values)], non_blocking=True)
+        self.evt.record()
+
+
 def note_step_advanced(e, slots):
     """Host mirror of ``advance_steps`` (call once per executed step)."""
     from .optim import H_STEP
@@ -1013,7 +1038,9 @@ class _StepPlan:
                 n = len(b)
                 self.idx[off:off + n].copy_(b.idx, non_blocking=True)
                 off += n
-            self.rng.copy_(torch.tensor(self.src.next_rng(), dtype=torch.int32), non_blocking=True)
+            if getattr(self, "_rng_stage", None) is None:
+                self._rng_stage = PinnedStager(2, torch.int32)
+            self._rng_stage.upload(self.rng, self.src.next_rng())
             return
         for (x, y) in batches:
             n = x.shape[0]

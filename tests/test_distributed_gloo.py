@@ -70,3 +70,38 @@ def test_spmd_gloo_world2_exploit_bit_exact(tmp_path):
     assert plans[0] == plans[1] and len(plans[0]) == 1
     assert all(r[2] for r in res)
     assert res[0][3] == [0, 1, 2, 3]
+
+
+def _gather_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    try:
+        from distributedtf_amd.parallel.comm import init_distributed, shutdown_distributed
+        comm = init_distributed(backend="gloo")
+        small = comm.allgather([[rank, -0.5 * rank, {"lr": 0.1 * rank, "name": "m%d" % rank}]])
+        # one rank over the slot: every rank must take the fallback together
+        mixed = comm.allgather(b"x" * (comm.GATHER_SLOT + 10) if rank == 1 else rank)
+        empty = comm.allgather(None)
+        q.put((rank, small, [len(m) if isinstance(m, bytes) else m for m in mixed], empty))
+        shutdown_distributed()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, "ERR", traceback.format_exc(), None))
+
+
+@pytest.mark.timeout(120)
+def test_allgather_fixed_slot_and_fallback():
+    world, port = 3, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=100) for _ in range(world)], key=lambda t: t[0])
+    for p in ps:
+        p.join(30)
+    for rank, small, mixed, empty in res:
+        assert small != "ERR", mixed
+        assert small == [[[r, -0.5 * r, {"lr": 0.1 * r, "name": "m%d" % r}]] for r in range(world)]
+        assert mixed == [0, 8192 + 10, 2]
+        assert empty == [None] * world

@@ -104,9 +104,23 @@ def main():
 
     exploits = [0]
 
-    def exploit_cycle(losses):
-        # score = -loss (no eval inside the timed region); full gather/plan/copy/perturb cycle
-        ls = losses.float().tolist()  # one device sync for the whole population
+    def exploit_start(losses):
+        """Queue the population's loss readback (pinned, non-blocking) behind the step that produced it."""
+        host = torch.empty(losses.numel(), dtype=torch.float32, pin_memory=dev.type == "cuda")
+        host.copy_(losses.float(), non_blocking=True)
+        evt = torch.cuda.Event() if dev.type == "cuda" else None
+        if evt is not None:
+            evt.record()
+        return host, evt
+
+    def exploit_cycle(pending):
+        # score = -loss (no eval inside the timed region); full gather/plan/copy/perturb cycle.  Called after
+        # the NEXT step has been queued, so the readback wait, the metric all-gather and the planning run on
+        # the host while the GPU executes that step; the winners' weights copied are the ones after it.
+        host, evt = pending
+        if evt is not None:
+            evt.synchronize()  # only the readback, not the step queued behind it
+        ls = host.tolist()
         vals = [[m.cluster_id, -ls[i], m.hparams] for i, m in enumerate(members)]
         parts = comm.allgather(vals)
         allv = [v for p in parts for v in p]
@@ -133,14 +147,20 @@ def main():
         losses = step()
     if args.exploit_every and world > 1 and args.warmup > 0:
         # one untimed exploit cycle: RCCL P2P channels between GPU pairs are set up lazily on first use
-        exploit_cycle(losses)
+        exploit_cycle(exploit_start(losses))
         exploits[0] = 0
     barrier_sync()
     t0 = time.perf_counter()
+    pending = None
     for k in range(args.steps):
         losses = step()
+        if pending is not None:
+            exploit_cycle(pending)  # overlaps the step just queued
+            pending = None
         if args.exploit_every and (k + 1) % args.exploit_every == 0:
-            exploit_cycle(losses)
+            pending = exploit_start(losses)
+    if pending is not None:
+        exploit_cycle(pending)  # an exploit due after the last step still runs inside the timed region
     barrier_sync()
     dt = time.perf_counter() - t0
     dts = comm.allgather(dt)

@@ -77,6 +77,7 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   extern __shared__ float dyn[];  // transform coefficients: MODE 1: 2*Ci, MODE 2: 3*Ci
   __shared__ float acc_lds[2][TC];
   const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z >= wk.y);
   const int slot = wk.x, p0 = wk.y, p1 = wk.z;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wr = wave & 1, wc = wave >> 1;
@@ -392,6 +393,7 @@ __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t sx[2][32 * KP];
   extern __shared__ float dyn[];  // x coefficients (2*Ci) then dy coefficients (3*Co)
   const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z >= wk.y);
   const int slot = wk.x, p0 = wk.y, p1 = wk.z, o0 = wk.w & 0xffff, n0 = (wk.w >> 16) * 8;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wr = wave & 1, wc = wave >> 1;
@@ -623,3 +625,5 @@ DTF_API int dtf_convg_wgrad(const CgArgs* a, int mode_x, int mode_dy, int nwork,
 #undef WG_CASE
   return -1;
 }
+
+DTF_DEBUG_EXPORT(convg)

@@ -84,6 +84,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t sa[2][TILE_ELEMS];
   __shared__ __attribute__((aligned(16))) bf16_t sb[2][TILE_ELEMS];
   const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z >= 0);
   const GemmGroup gp = a.groups[wk.x];
   const int m0 = wk.y, n0 = wk.z;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -177,3 +178,5 @@ DTF_API int dtf_gemm_bf16(const GemmArgs* a, int mode, int nwork, hipStream_t st
 #undef DTF_GEMM_CASE
   return DTF_CHECK_LAUNCH();
 }
+
+DTF_DEBUG_EXPORT(gemm)

@@ -138,6 +138,7 @@ constexpr int C2_TP = 40;  // tile pixel pitch (bf16)
 __global__ __launch_bounds__(256) void mnist_conv2_fwd_kernel(MnistArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t tile[18 * 18 * C2_TP];
   const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0);
   const int img0 = wk.x, nimg = wk.y, slot = wk.w;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kg = lane >> 4, j = lane & 15;
   for (int i = tid; i < 18 * 18 * C2_TP / 8; i += 256) reinterpret_cast<uint4*>(tile)[i] = make_uint4(0, 0, 0, 0);
@@ -249,6 +250,7 @@ constexpr int D2_TP = 72;
 __global__ __launch_bounds__(256) void mnist_conv2_dgrad_kernel(MnistArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t tile[18 * 18 * D2_TP];
   const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0);
   const int img0 = wk.x, nimg = wk.y, slot = wk.w;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kg = lane >> 4, j = lane & 15;
   for (int i = tid; i < 18 * 18 * D2_TP / 8; i += 256) reinterpret_cast<uint4*>(tile)[i] = make_uint4(0, 0, 0, 0);
@@ -309,6 +311,7 @@ __global__ __launch_bounds__(256) void mnist_conv2_wgrad_kernel(MnistArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t xt[18 * 18 * W2_XP];
   __shared__ float dbred[4][64];
   const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0);
   const int img0 = wk.x, nimg = wk.y, slot = wk.w;
   const int ng = blockIdx.y;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -398,6 +401,7 @@ __global__ __launch_bounds__(256) void mnist_conv1_wgrad_kernel(MnistArgs a) {
   __shared__ float xs[32 * 33];
   __shared__ float red[8][32][27];
   const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0);
   const int img0 = wk.x, nimg = wk.y, slot = wk.w;
   const int tid = threadIdx.x, c = tid & 31, qg = tid >> 5;
   float acc[26];
@@ -445,6 +449,7 @@ __global__ __launch_bounds__(256) void mnist_conv1_wgrad_kernel(MnistArgs a) {
 __global__ __launch_bounds__(256) void mnist_head_kernel(MnistArgs a) {
   __shared__ float red[2][4][10];
   const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0);
   const int img0 = wk.x, nimg = wk.y, slot = wk.w;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, f0 = 4 * tid;
   const float* prow = a.params + (long)slot * a.p_mstride;
@@ -622,3 +627,5 @@ DTF_API int dtf_mnist_conv1_wgrad(const MnistArgs* a, int nwork, hipStream_t str
   hipLaunchKernelGGL(mnist_conv1_wgrad_kernel, dim3(nwork), dim3(256), 0, stream, *a);
   return DTF_CHECK_LAUNCH();
 }
+
+DTF_DEBUG_EXPORT(mnist)

@@ -239,6 +239,7 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   __shared__ float dwl[4][16][64];
   __shared__ float dbl[4][16];
   const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0);
   const int img0 = wk.x, nimg = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, c = threadIdx.x & 63;
   const float* prow = a.params + (long)slot * a.p_mstride;
@@ -648,3 +649,5 @@ DTF_API int dtf_bn_bwd_reduce(const BnEwArgs* a, hipStream_t stream) {
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((unsigned)a->nimg, ew_split(a)), dim3(256), 0, stream, *a);
   return DTF_CHECK_LAUNCH();
 }
+
+DTF_DEBUG_EXPORT(resnet_aux)

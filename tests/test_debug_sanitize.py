@@ -85,3 +85,16 @@ def test_debug_build_on_gpu():
                        capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "debug probe ok" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [["--model", "mnist", "--pop", "2", "--batch", "16"],
+                                  ["--model", "imagenet", "--pop", "2", "--batch", "2"]])
+def test_debug_build_other_families_on_gpu(args):
+    """MNIST and ImageNet steps through the debug library: every launch synchronised and checked."""
+    env = dict(os.environ, DTF_DEBUG="1")
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "1",
+                        "--exploit_every", "0"] + args, env=env, capture_output=True, text=True, timeout=240,
+                       cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert '"metric"' in r.stdout

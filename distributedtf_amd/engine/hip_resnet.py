@@ -470,6 +470,24 @@ class _StepPlan:
             self._work_cache[key] = w
         return w
 
+    @staticmethod
+    def _fwd_split(cin, n_items):
+        # DTF_FWD_SPLIT64: "auto" (split when fewer than 256 items), "1" always, "0" never (default: the split
+        # measured within run-to-run noise at pop 1/2/8, profiles/r1_s7_fwd_split64_ab.log)
+        mode = os.environ.get("DTF_FWD_SPLIT64", "0")
+        if cin != 64 or mode == "0":
+            return False
+        return mode == "1" or n_items < 256
+
+    def _split_work(self, work):
+        key = ("split", work.data_ptr())
+        w = self._work_cache.get(key)
+        if w is None:
+            w = work.repeat_interleave(2, dim=0).contiguous()
+            w[1::2, 2] = 1
+            self._work_cache[key] = w
+        return w
+
     def _n_wg_iters(self, total_iters, per_wg=4, lo=256, hi=1024):
         """Enough (image, band) iterations per workgroup for the double-buffered pipeline,
         while keeping >= lo workgroups (fill 256 CUs) when the batch allows."""
@@ -547,6 +565,12 @@ class _StepPlan:
         if (c.k == 3 and c.stride == 1 and cin == c.cout and Hi == 512 // cin and rows == 8
                 and stats_bn is not None and os.environ.get("DTF_FWD_S1", "1") == "1"):
             # compile-time-geometry kernel of the CIFAR stages (conv_fwd_s1_kernel)
+            if self._fwd_split(cin, work.shape[0]):
+                # C = 64 with few work items (one member: 128 images = 128 items): two workgroups per item,
+                # each computing half of the output channels (work.z), to fill the 256 CUs
+                work = self._split_work(work)
+                a.work = _p(work)
+                mode |= 4
             self._add(lib.dtf_conv_fwd_s1, ctypes.byref(a), cin, mode, int(res is not None), work.shape[0], lds)
         else:
             self._add(lib.dtf_conv_fwd, ctypes.byref(a), cin, c.cout, c.stride, c.k, mode, int(res is not None),

@@ -666,15 +666,18 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
 // Stride-1 3x3 C->C forward of the CIFAR stages (and the stem, C = 16 padded input) with compile-time
 // geometry (W = H = 512/C, 8-row bands), uniform-base + 32-bit lane offsets and packed epilogue math
 // (same scheme as conv_bwd_fused_kernel).
-template <int C, int MODE_IN, bool RESID>
+// SPLIT = 2: the output channels are split over two workgroups per work item (work.z = which half), so a
+// single member's 8x8 C = 64 layer (one image per item) launches 256 workgroups instead of 128.
+template <int C, int MODE_IN, bool RESID, int SPLIT = 1>
 __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
   constexpr int W = 512 / C, H = W, ROWS = 8, BANDS = H / ROWS;
-  constexpr int NT = C / 16, WPT = 4 / NT;
+  constexpr int NT = C / 16 / SPLIT, WPT = 4 / NT;  // NT: output-channel tiles of this workgroup
   constexpr int KTOT = 9 * C, KS = (KTOT + 31) / 32;
   constexpr int CP = cpad_fwd<C>(), RT = ROWS + 2, WP = W + 2;
   constexpr int TSZ = (RT * WP * CP + 8 + 63) & ~63;  // + slack for inactive staging slots
   constexpr int NTILES = ROWS * W / 16;
-  static_assert(NTILES == WPT * MAXT, "every wave owns MAXT output tiles");
+  constexpr int MT = NTILES / WPT;  // output pixel tiles per wave per iteration
+  static_assert(NTILES == WPT * MT && MT <= MAXT, "every wave owns MT output tiles");
   constexpr int ROW = W * C, IMG = H * ROW;
   using St = Stage<C, RT, W, H, CP>;
   constexpr int MAXC = St::MAXC;
@@ -689,7 +692,7 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
   DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
   const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int ct = wave % NT;
+  const int ct = wave % NT + (SPLIT > 1 ? wk.z * NT : 0);
   bf16x8_t afr[KS];
   {
     const bf16_t* wb = a.w + (long)slot * a.w_mstride + a.w_off + (long)(ct * 16 + (lane & 15)) * KTOT;
@@ -720,10 +723,10 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
     tapoff[s] = k0 < KTOT ? ((tap / 3) * WP + (tap % 3)) * CP + c0 : 0;
   }
   const int co0 = ct * 16 + (lane >> 4) * 4;
-  int tbo[MAXT];
-  uint32_t pofs[MAXT];
+  int tbo[MT];
+  uint32_t pofs[MT];
 #pragma unroll
-  for (int i = 0; i < MAXT; ++i) {
+  for (int i = 0; i < MT; ++i) {
     const int p = (wave / NT + WPT * i) * 16 + (lane & 15);
     tbo[i] = ((p / W) * WP + p % W) * CP;
     pofs[i] = p * C + co0;
@@ -737,10 +740,10 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
     const int img = it / BANDS, r0 = (it % BANDS) * ROWS;
     const bool more = k + 1 < nit;
     const long band = (long)img * IMG + r0 * ROW;
-    uint2 rres[MAXT];
+    uint2 rres[MT];
     if constexpr (RESID) {
 #pragma unroll
-      for (int i = 0; i < MAXT; ++i) rres[i] = *reinterpret_cast<const uint2*>(a.res + band + pofs[i]);
+      for (int i = 0; i < MT; ++i) rres[i] = *reinterpret_cast<const uint2*>(a.res + band + pofs[i]);
     }
     if (more) {
       const int nimg = (it + 1) / BANDS, ngy0 = ((it + 1) % BANDS) * ROWS - 1;
@@ -749,7 +752,7 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
     }
     const bf16_t* tile = SBUF(k);
 #pragma unroll
-    for (int i = 0; i < MAXT; ++i) {
+    for (int i = 0; i < MT; ++i) {
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < KS; ++s)
@@ -1507,6 +1510,14 @@ DTF_API int dtf_conv_fwd_s1(const ConvArgs* args, int c, int mode, int resid, in
   S1_CASE(64, 1, false)
   S1_CASE(64, 1, true)
 #undef S1_CASE
+  // mode bit 2: output channels split over two workgroups per work item (C = 64)
+#define S1_SPLIT_CASE(CC, M, R)                   \
+  if (c == CC && mode == (M | 4) && resid == R) \
+    return launch(conv_fwd_s1_kernel<CC, M, R, 2>, nblocks, lds, stream, *args);
+  S1_SPLIT_CASE(64, 0, false)
+  S1_SPLIT_CASE(64, 1, false)
+  S1_SPLIT_CASE(64, 1, true)
+#undef S1_SPLIT_CASE
   return -1;
 }
 

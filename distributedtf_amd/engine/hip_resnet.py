@@ -632,7 +632,8 @@ class _StepPlan:
         # images per workgroup: bound the fp32 atomic traffic of the per-WG partial dW (~12 MB per launch)
         wn = c.cout * c.k * c.k * c.cin
         # bound fp32 atomic traffic (~12 MB / launch) and same-address contention (<= 128 WGs per member)
-        n_wg = max(64, min(128 * len(self.slots), int(12e6 / (4.0 * wn))))
+        per_member = int(os.environ.get("DTF_WGRAD_WG_PER_MEMBER", "128"))
+        n_wg = max(64, min(per_member * len(self.slots), int(12e6 / (4.0 * wn))))
         work = self._work_iters(Ho // rows, n_wg)
         a = self._base_args()
         a.x, a.dy, a.dy2 = _p(x), _p(dy), _p(dy2)

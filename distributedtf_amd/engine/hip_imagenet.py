@@ -181,7 +181,7 @@ class HipImageNetBackend:
         p.load_batch(batches)
         p.run()
         note_step_advanced(e, slots)
-        return self.loss[p.slots_long].clone()
+        return p.loss_sel.clone()  # gathered inside the step graph
 
     def forward_backward(self, slots, batches):
         raise RuntimeError("HipImageNetBackend runs whole steps: use train_step")
@@ -210,6 +210,7 @@ class _ImageNetPlan:
         self.cnt = cnt.to(dev)
         self.slots_t = torch.tensor(slots, dtype=torch.int32, device=dev)
         self.slots_long = torch.tensor(slots, dtype=torch.long, device=dev)
+        self.loss_sel = torch.zeros(len(slots), dtype=be.loss.dtype, device=dev)
         bf = torch.bfloat16
         H = cfg.image_size
         self.H = H
@@ -547,6 +548,8 @@ class _ImageNetPlan:
                 err = fn(*args, st)
                 if err != 0:
                     raise RuntimeError("kernel launch %s failed with %d" % (getattr(fn, "__name__", fn), err))
+        # per-member losses gathered inside the step (graph) so a replay leaves one copy for train_step
+        torch.index_select(self.be.loss, 0, self.slots_long, out=self.loss_sel)
 
     def run(self):
         be = self.be

@@ -19,6 +19,8 @@ needs_hipcc = pytest.mark.skipif(not os.path.isfile(HIPCC), reason="hipcc not in
 @needs_hipcc
 def test_host_code_under_asan_ubsan(tmp_path):
     script = os.path.join(ROOT, "tools", "sanitize", "run_host_asan.sh")
+    if not os.path.isfile(script):
+        pytest.skip("tools/sanitize not shipped to this machine (.gpurunignore: host-only CPU check)")
     ok = subprocess.run(["bash", script, str(tmp_path)], capture_output=True, text=True, timeout=300)
     assert ok.returncode == 0, ok.stdout + ok.stderr
     assert "host_check: ok" in ok.stdout

@@ -41,13 +41,17 @@ def parse():
     p.add_argument("--resnet_size", type=int, default=None, help="default 56 (CIFAR) / 50 (imagenet)")
     p.add_argument("--resnet_version", type=int, default=2, choices=[1, 2])
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
-    p.add_argument("--exploit_every", type=int, default=25)
+    p.add_argument("--exploit_every", type=int, default=None,
+                   help="steps between PBT exploit/explore cycles inside the timed region; default "
+                        "min(25, max(1, steps // 2)) so every timed run holds at least one cycle; 0 = none")
     p.add_argument("--seed", type=int, default=2024)
     p.add_argument("--graph", type=int, default=1, help="capture the population step in a HIP graph")
     p.add_argument("--profile_json", default=None)
     a = p.parse_args()
     if a.resnet_size is None:
         a.resnet_size = 50 if a.model == "imagenet" else 56
+    if a.exploit_every is None:
+        a.exploit_every = min(25, max(1, a.steps // 2))
     return a
 
 
@@ -103,6 +107,7 @@ def main():
         return eng.train_step(slots, batches, hp, lrs)
 
     exploits = [0]
+    exploit_s = []  # host wall time of each timed exploit/explore cycle (gather + plan + copy + perturb)
 
     def exploit_start(losses):
         """Queue the population's loss readback (pinned, non-blocking) behind the step that produced it."""
@@ -118,6 +123,7 @@ def main():
         # the NEXT step has been queued, so the readback wait, the metric all-gather and the planning run on
         # the host while the GPU executes that step; the winners' weights copied are the ones after it.
         host, evt = pending
+        tc = time.perf_counter()
         if evt is not None:
             evt.synchronize()  # only the readback, not the step queued behind it
         ls = host.tolist()
@@ -135,6 +141,7 @@ def main():
                 m.perturb_hparams()
                 m.hparams["batch_size"] = args.batch
         exploits[0] += 1
+        exploit_s.append(time.perf_counter() - tc)
 
     def barrier_sync():
         if dev.type == "cuda":
@@ -149,6 +156,7 @@ def main():
         # one untimed exploit cycle: RCCL P2P channels between GPU pairs are set up lazily on first use
         exploit_cycle(exploit_start(losses))
         exploits[0] = 0
+        exploit_s.clear()
     barrier_sync()
     t0 = time.perf_counter()
     pending = None
@@ -190,6 +198,7 @@ def main():
                        "parallelism": "pbt_pop%d_%dmembers_per_gpu" % (args.pop, cnt),
                        "backend": eng.backend.name, "exploit_every": args.exploit_every,
                        "exploits_timed": exploits[0]},
+            "exploit_ms_mean": round(1000.0 * sum(exploit_s) / len(exploit_s), 3) if exploit_s else None,
             "achieved_tflops": round(flops / 1e12, 2),
         }
         print(json.dumps(out), flush=True)

@@ -36,7 +36,7 @@ from .. import ops
 from ..data.datasets import IndexBatch, batch_len
 from ..models.resnet import BN_EPS
 
-NREP = 8
+NREP = int(os.environ.get("DTF_NREP", "8"))  # BN stat replicas: must match the build (common.h DTF_NREP)
 c_void_p, c_int, c_long = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
 
 
@@ -53,6 +53,7 @@ class ConvArgs(ctypes.Structure):
         ("cin_real", c_int), ("slab", c_void_p),
         ("x3", c_void_p), ("xout", c_void_p), ("rslab", c_void_p), ("rtab", c_void_p), ("r_goff", c_long),
         ("r_c", c_int), ("r_nblk", c_int), ("n_main", c_int),
+        ("u_items", c_int), ("u_chunk", c_int), ("u_per", c_int), ("u_pad", c_int),
     ]
 
 
@@ -99,6 +100,7 @@ def _register():
     ops.register("dtf_conv_fwd_s1", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_dw_slab_reduce", [c_void_p, c_void_p, c_int, c_void_p, c_long, c_long, c_int, c_void_p])
     ops.register("dtf_conv_bwd_fused", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
+    ops.register("dtf_conv_bwd_role", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_args_size", [])
     ops.register("dtf_bnbwd_args_size", [])
     ops.register("dtf_head_args_size", [])
@@ -387,6 +389,9 @@ class _StepPlan:
         for s, n in zip(slots, sizes):
             cnt[s] = float(n)
         self.cnt = cnt.to(dev)
+        # uniform population: work items of the stage kernels computed from blockIdx (ConvArgs.u_items)
+        self.uniform = (len(set(sizes)) == 1 and list(slots) == list(range(len(slots)))
+                        and os.environ.get("DTF_UNIFORM_WORK", "1") == "1")
         self.slots_t = torch.tensor(slots, dtype=torch.int32, device=dev)
         self.slots_long = torch.tensor(slots, dtype=torch.long, device=dev)
         self.loss_sel = torch.zeros(len(slots), dtype=be.loss.dtype, device=dev)
@@ -434,6 +439,7 @@ class _StepPlan:
             hw //= blk.stride
         self.dfeat = torch.zeros(N, cfg.final_size, dtype=torch.float32, device=dev)
         self._work_cache = {}
+        self._uniform_geo = {}
         # dW slab reductions on a forked stream (joined before the optimizer): off the critical path
         # DTF_SIDE_REDUCE: "1" = every channel width, "0" = none, or a comma list of widths (e.g. "64")
         sr = os.environ.get("DTF_SIDE_REDUCE", "0").strip()
@@ -443,7 +449,14 @@ class _StepPlan:
             self.side_cs = frozenset((16, 32, 64))
         else:
             self.side_cs = frozenset(int(v) for v in sr.split(",") if v)
-        self.side_reduce = bool(self.side_cs)
+        # Split backward (small populations: the step is latency-bound, one workgroup per CU): every stride-1 conv's
+        # dgrad runs on the main stream (the critical path) and its wgrad on a side stream, concurrently with the
+        # next layers' dgrads; backward temporaries are then never reused (the side stream reads them later).
+        # DTF_SPLIT_BWD: "auto" (populations of <= DTF_SPLIT_MAX_POP members, default 2), "1", "0".
+        sp = os.environ.get("DTF_SPLIT_BWD", "auto")
+        self.split = dev.type == "cuda" and not cfg.version == 1 and (
+            sp == "1" or (sp == "auto" and len(slots) <= int(os.environ.get("DTF_SPLIT_MAX_POP", "2"))))
+        self.side_reduce = bool(self.side_cs) or self.split
         self.side_stream = torch.cuda.Stream(device=dev) if self.side_reduce else None
         self.launches = []
         self._pending_slab = None  # (slab ptr, reduce table, C, grad offset) of the last fused launch
@@ -466,9 +479,18 @@ class _StepPlan:
                 chunk = max(1, -(-total // per_member))
                 for i in range(0, total, chunk):
                     items.append([f + i, min(chunk, total - i), 0, s])
+                # uniform geometry (identical for every member when self.uniform): items, chunk, iterations
+                geo = (-(-total // chunk), chunk, total)
             w = torch.tensor(items, dtype=torch.int32, device=self.be.dev)
             self._work_cache[key] = w
+            self._uniform_geo[w.data_ptr()] = geo
         return w
+
+    def _set_uniform(self, a, work):
+        """Arithmetic work items (ConvArgs.u_*) for a _work_iters array when the population is uniform."""
+        if self.uniform:
+            a.u_items, a.u_chunk, a.u_per = self._uniform_geo[work.data_ptr()]
+            assert a.u_items * len(self.slots) == work.shape[0]
 
     @staticmethod
     def _fwd_split(cin, n_items):
@@ -571,6 +593,9 @@ class _StepPlan:
                 work = self._split_work(work)
                 a.work = _p(work)
                 mode |= 4
+            else:
+                self._set_uniform(a, work)
+            a.cin_real = self._stamp_row("fwd", "fwd_s1 C=%d in=%d res=%d" % (cin, mode, res is not None))  # launch ordinal for DTF_STAMP diagnostic builds (unused otherwise)
             self._add(lib.dtf_conv_fwd_s1, ctypes.byref(a), cin, mode, int(res is not None), work.shape[0], lds)
         else:
             self._add(lib.dtf_conv_fwd, ctypes.byref(a), cin, c.cout, c.stride, c.k, mode, int(res is not None),
@@ -653,7 +678,8 @@ class _StepPlan:
         dt = (rows * Ho * _cpad(c.cout) + 63) // 64 * 64
         lds = 1536 + 2 * (xt + dt) * 2  # double-buffered
         lib = ops.lib()
-        self._add(lib.dtf_conv_wgrad, ctypes.byref(a), cin, c.cout, c.stride, c.k, mode_x, mode_dy, work.shape[0], lds)
+        launch = self._side if self.split else self._add
+        launch(lib.dtf_conv_wgrad, ctypes.byref(a), cin, c.cout, c.stride, c.k, mode_x, mode_dy, work.shape[0], lds)
         self._keep(a)
 
     def _conv_bwd_fused(self, ci, dy, dz_out, x, mode_dy, dy2=None, dy_bn=None, x_bn=None, res=None, ident_x=False,
@@ -679,6 +705,9 @@ class _StepPlan:
         for t in (dy, dy2, dy3, dy_out, dz_out, x, res):
             assert t is None or tuple(t.shape) == (self.N, H, H, C), (t.shape, C, H)
         bands = H // rows
+        if self.split:
+            return self._conv_bwd_split(ci, c, C, H, rows, bands, dy, dz_out, x, mode_dy, dy2, dy_bn, x_bn, res,
+                                        ident_x, dy3, dy_out)
         n_wg = self._fused_nwg(C, bands)
         work = self._work_iters(bands, n_wg)
         a = self._base_args()
@@ -688,6 +717,7 @@ class _StepPlan:
         a.work = _p(work)
         a.g_off = c.off
         a.n_main = work.shape[0]
+        self._set_uniform(a, work)
         if dy_bn is not None:
             a.in_gamma, a.in_beta = self._bn(dy_bn)
             a.st_in, a.st_in_b = _p(be.st_f(dy_bn)), _p(be.st_b(dy_bn))
@@ -724,6 +754,7 @@ class _StepPlan:
             # side-stream reductions run concurrently with later layers: every layer needs its own slab region
             a.slab = _p(self._layer_slab(work.shape[0] * self._slab_elems(C)))
         epi = int(res is not None) | (2 if ident_x else 0)
+        a.cin_real = self._stamp_row("fused", "fused C=%d mdy=%d epi=%d" % (C, mode_dy, epi))
         self._add(lib.dtf_conv_bwd_fused, ctypes.byref(a), C, mode_dy, epi, work.shape[0] + n_red, lds)
         self._keep(a)
         if slab:
@@ -733,6 +764,62 @@ class _StepPlan:
                                                             self.e.Pp, c.off, C)))
             else:
                 self._pending_slab = (a.slab, red, C, c.off)
+
+    def _conv_bwd_split(self, ci, c, C, H, rows, bands, dy, dz_out, x, mode_dy, dy2, dy_bn, x_bn, res, ident_x, dy3,
+                        dy_out):
+        """Split backward of a stride-1 C->C conv: dgrad role on the main stream (one (image, band) item per
+        workgroup: the most workgroups a latency-bound small population can use), wgrad role on the side stream
+        reading the materialised dY (``dy`` itself, or the dgrad launch's ``xout``) and writing per-layer dW slabs
+        that a side-stream reduction adds into the gradient row."""
+        be, L = self.be, self.be.L
+        lib = ops.lib()
+        tsz = ((rows + 2) * (H + 2) * _cpad(C) + 8 + 63) // 64 * 64
+        epi = int(res is not None) | (2 if ident_x else 0)
+        # ---- dgrad role
+        nd = int(os.environ.get("DTF_SPLIT_DG_ITERS", "1"))
+        work = self._work_iters(bands, max(1, (self.N * bands) // nd))
+        a = self._base_args()
+        dmat = dy
+        if mode_dy >= 2:
+            dmat = dy_out if dy_out is not None else self._fresh_like(dz_out)
+        a.x, a.x2, a.y, a.xm, a.res = _p(dy), _p(dy2), _p(dz_out), _p(x), _p(res)
+        a.x3, a.xout = _p(dy3), _p(dmat if mode_dy >= 2 else None)
+        a.w, a.w_off = _p(be.wd), L.dgr_off[ci]
+        a.work = _p(work)
+        a.g_off = c.off
+        a.n_main = work.shape[0]
+        self._set_uniform(a, work)
+        if dy_bn is not None:
+            a.in_gamma, a.in_beta = self._bn(dy_bn)
+            a.st_in, a.st_in_b = _p(be.st_f(dy_bn)), _p(be.st_b(dy_bn))
+        if not ident_x:
+            a.ep_gamma, a.ep_beta = self._bn(x_bn)
+            a.st_ep = _p(be.st_f(x_bn))
+            a.st_out = _p(be.st_b(x_bn))
+        a.Hi, a.Wi, a.Ho, a.Wo, a.rows = H, H, H, H, rows
+        a.cin_real = self._stamp_row("fused", "dgrad C=%d mdy=%d epi=%d" % (C, mode_dy, epi))
+        self._keep(a)
+        self._add(lib.dtf_conv_bwd_role, ctypes.byref(a), C, mode_dy, epi, 1, work.shape[0], 2304 + 2 * tsz * 2)
+        # ---- wgrad role (side stream)
+        per = int(os.environ.get("DTF_SPLIT_WG_%d" % C, {16: "128", 32: "128", 64: "64"}[C]))
+        wwork = self._work_iters(bands, max(1, min(self.N * bands, per * len(self.slots))))
+        b = self._base_args()
+        b.x, b.xm = _p(dmat), _p(x)
+        b.work = _p(wwork)
+        b.g_off = c.off
+        b.n_main = wwork.shape[0]
+        self._set_uniform(b, wwork)
+        if not ident_x:
+            b.ep_gamma, b.ep_beta = self._bn(x_bn)
+            b.st_ep = _p(be.st_f(x_bn))
+        b.Hi, b.Wi, b.Ho, b.Wo, b.rows = H, H, H, H, rows
+        b.slab = _p(self._layer_slab(wwork.shape[0] * self._slab_elems(C)))
+        b.cin_real = -1
+        self._keep(b)
+        red = self._slab_table(wwork)
+        self._side(lib.dtf_conv_bwd_role, ctypes.byref(b), C, 0, 2 if ident_x else 0, 2, wwork.shape[0],
+                   2304 + 4 * tsz * 2)
+        self._side(lib.dtf_dw_slab_reduce, b.slab, _p(red), red.shape[0], _p(self.e.grads), self.e.Pp, c.off, C)
 
     def _piggyback(self, pend):
         """Reduce the previous launch's slabs inside the next fused launch when that adds few workgroups
@@ -809,6 +896,40 @@ class _StepPlan:
         self._keep(t)
         return t
 
+    def _stamp_row(self, kind, label=""):
+        """Row of the DTF_STAMP diagnostic buffer for the next launch of ``kind`` (fwd: 0.., fused: 64..)."""
+        if not hasattr(self, "_stamp_n"):
+            self._stamp_n = {"fwd": 0, "fused": 0}
+        row = self._stamp_n[kind] + (64 if kind == "fused" else 0)
+        self._stamp_n[kind] += 1
+        self.stamp_rows = getattr(self, "stamp_rows", []) + [(row, label)]
+        return row
+
+    def _tmp_for(self, hw):
+        """Backward temporaries at resolution ``hw``: the plan's shared ping-pong set, or (split mode) a fresh
+        lazily allocated set that no later layer overwrites."""
+        if not self.split:
+            return self.tmp[hw]
+        plan = self
+        proto = self.tmp[hw]
+
+        class _Fresh(dict):
+            def __missing__(self, key):
+                ref = proto[key]
+                v = [plan._fresh_like(t) for t in ref] if isinstance(ref, list) else plan._fresh_like(ref)
+                self[key] = v
+                return v
+        return _Fresh()
+
+    def _fresh_like(self, t):
+        u = torch.empty_like(t)
+        self._keep(u)
+        return u
+
+    def _side(self, fn, *args):
+        """Launch on the side stream (forked after everything queued so far on the main stream)."""
+        self._add("side", (fn, args))
+
     def _keep(self, obj):
         if not hasattr(self, "_keepalive"):
             self._keepalive = []
@@ -874,7 +995,7 @@ class _StepPlan:
             bn1, bn2 = blk.bns
             x, h = self.xs[i], self.hs[i]
             Hi, Ho = x.shape[1], h.shape[1]
-            T = self.tmp[Ho]
+            T = self._tmp_for(Ho)
             ca, cb = blk.convs
             # conv_b: dgrad -> dz2 (mask by BN2(h), BN2 reductions); wgrad
             if fused and pend is not None:
@@ -889,7 +1010,7 @@ class _StepPlan:
             else:
                 self._conv_dgrad(cb, g_cur, T["dz2"], Ho, mode=0, epi=2, xm=h, ep_bn=bn2)
                 self._conv_wgrad(cb, h, g_cur, mode_x=1, mode_dy=0, x_bn=bn2)
-            Tin = self.tmp[Hi]
+            Tin = self._tmp_for(Hi) if Hi != Ho else T
             pd = None
             if blk.proj is not None:
                 pd = self.pd[id(blk)]

@@ -82,4 +82,10 @@ static __device__ int dtf_debug_err;
 #define DTF_DEBUG_EXPORT(tu)
 #define DTF_HOST_CHECK(cond) ((void)0)
 #endif
+// BatchNorm statistic accumulators: NREP replicated [2][64] rows per member and BN; a workgroup adds its partial
+// sums to replica (blockIdx % NREP) so same-address float atomics serialise NREP-fold less.  Must match
+// engine/hip_resnet.py (DTF_NREP).
+#ifndef DTF_NREP
+#define DTF_NREP 8
+#endif
 #define DTF_ALIGNED16(p) ((((uintptr_t)(p)) & 15) == 0)

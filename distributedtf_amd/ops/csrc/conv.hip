@@ -45,7 +45,36 @@ typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 #ifndef DTF_ABL
 #define DTF_ABL 0  // timing-only ablation bits of conv_bwd_fused_kernel (tools/ablate.sh); 0 in real builds
 #endif
-#define NREP 8
+#define NREP DTF_NREP
+#ifndef DTF_STAMP
+#define DTF_STAMP 0  // diagnostic build (tools/stamps.py): per-workgroup s_memrealtime stamps of the fwd_s1 / fused bwd
+#endif                // phases; the launch ordinal rides in ConvArgs.cin_real (unused by those kernels)
+#if DTF_STAMP
+#define STAMP_LAUNCHES 128
+#define STAMP_WGS 512
+__device__ unsigned long long dtf_stamps[STAMP_LAUNCHES][STAMP_WGS][16];
+#define STAMP_DECL unsigned long long st_[16] = {0};
+#define STAMP(i) (st_[i] = __builtin_amdgcn_s_memrealtime())
+#define STAMP_DRAIN(i) (__builtin_amdgcn_s_waitcnt(0), st_[i] = __builtin_amdgcn_s_memrealtime())
+#if DTF_STAMP >= 2  // fine prologue stamps: each drains the loads issued so far (serialises them: read shares)
+#define STAMP_FINE(i) STAMP_DRAIN(i)
+#else
+#define STAMP_FINE(i) ((void)0)
+#endif
+#define STAMP_FLUSH(row, extra)                                                                        \
+  do {                                                                                                 \
+    if (threadIdx.x == 0 && (row) >= 0 && (row) < STAMP_LAUNCHES && blockIdx.x < STAMP_WGS) {          \
+      st_[7] = (extra);                                                                                \
+      for (int i_ = 0; i_ < 16; ++i_) dtf_stamps[row][blockIdx.x][i_] = st_[i_];                        \
+    }                                                                                                  \
+  } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(i) ((void)0)
+#define STAMP_FINE(i) ((void)0)
+#define STAMP_DRAIN(i) ((void)0)
+#define STAMP_FLUSH(row, extra) ((void)0)
+#endif
 
 namespace {
 
@@ -89,7 +118,20 @@ struct ConvArgs {
   int r_c;                  //   its channel count (0: no reduction role)
   int r_nblk;               //   reduce workgroups per member (E / 32)
   int n_main;               // workgroups of the convolution role
+  // Uniform populations (every member the same batch, slots 0..n-1 packed in order): the work item of workgroup b
+  // is arithmetic -- member b / u_items, iterations [k * u_chunk, ...) of its u_per -- instead of a dependent
+  // load of work[b] (one memory round trip less before every address of the kernel).  u_items = 0: use `work`.
+  int u_items, u_chunk, u_per, u_pad;
 };
+
+__device__ __forceinline__ int4 work_item(const ConvArgs& a) {
+  if (a.u_items > 0) {
+    const int m = (int)blockIdx.x / a.u_items, k = (int)blockIdx.x - m * a.u_items;
+    const int it0 = k * a.u_chunk;
+    return make_int4(m * a.u_per + it0, min(a.u_chunk, a.u_per - it0), 0, m);
+  }
+  return a.work[blockIdx.x];
+}
 
 __device__ __forceinline__ const float* stats_row(const float* base, int slot) {
   return base + (long)slot * NREP * 128;
@@ -345,6 +387,81 @@ __device__ __forceinline__ void make_coef(float* coef, const ConvArgs& a, int sl
       coef[c] = A;
       coef[64 + c] = B;
       coef[128 + c] = Cc;
+    }
+  }
+}
+
+// Two-phase BN coefficients: coef_issue loads the replicated statistics + gamma/beta into registers at the top of a
+// kernel (before its tile and weight loads), coef_finish derives the coefficients once they have arrived -- the
+// in-order vmcnt wait then covers only the statistics, the tile / weight loads stay in flight behind them.
+// MODE 1: forward scale/shift (st_f, gamma, beta); MODE 2/3: backward A, B, C (st_f, st_b, gamma).
+template <int MODE>
+struct CoefLd {
+  float fs[NREP], fq[NREP], bs[MODE >= 2 ? NREP : 1], bq[MODE >= 2 ? NREP : 1];
+  float g, b;
+};
+
+template <int C, int MODE>
+__device__ __forceinline__ void coef_issue(CoefLd<MODE>& L, const ConvArgs& a, int slot, const float* st_f,
+                                           const float* st_b, int g_off, int b_off) {
+  if constexpr (MODE == 0) return;
+  const int c = threadIdx.x;
+  if (c < C) {
+    const float* rf = stats_row(st_f, slot) + c;
+#pragma unroll
+    for (int r = 0; r < NREP; ++r) {
+      L.fs[r] = rf[r * 128];
+      L.fq[r] = rf[r * 128 + 64];
+    }
+    if constexpr (MODE >= 2) {
+      const float* rb = stats_row(st_b, slot) + c;
+#pragma unroll
+      for (int r = 0; r < NREP; ++r) {
+        L.bs[r] = rb[r * 128];
+        L.bq[r] = rb[r * 128 + 64];
+      }
+    }
+    const float* prow = a.params + (long)slot * a.p_mstride;
+    L.g = prow[g_off + c];
+    if constexpr (MODE == 1) L.b = prow[b_off + c];
+  }
+}
+
+// mean / inv-std of the forward statistics in L
+template <int MODE>
+__device__ __forceinline__ void coef_moments(const CoefLd<MODE>& L, float n, float& mean, float& inv) {
+  float s = 0.f, q = 0.f;
+#pragma unroll
+  for (int r = 0; r < NREP; ++r) {
+    s += L.fs[r];
+    q += L.fq[r];
+  }
+  mean = s / n;
+  inv = rsqrtf(fmaxf(q / n - mean * mean, 0.f) + BN_EPS);
+}
+
+template <int C, int MODE>
+__device__ __forceinline__ void coef_finish(float* coef, const CoefLd<MODE>& L, float n) {
+  if constexpr (MODE == 0) return;
+  const int c = threadIdx.x;
+  if (c < C) {
+    float mean, inv;
+    coef_moments<MODE>(L, n, mean, inv);
+    const float scale = L.g * inv;
+    if constexpr (MODE == 1) {
+      coef[c] = scale;
+      coef[64 + c] = L.b - mean * scale;
+    } else {
+      float sdz = 0.f, sdzx = 0.f;
+#pragma unroll
+      for (int r = 0; r < NREP; ++r) {
+        sdz += L.bs[r];
+        sdzx += L.bq[r];
+      }
+      const float mdz = sdz / n, mdzx = sdzx / n;
+      coef[c] = scale;
+      coef[64 + c] = -scale * inv * mdzx;
+      coef[128 + c] = -scale * mdz + scale * inv * mean * mdzx;
     }
   }
 }
@@ -687,12 +804,26 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
   float* acc_lds = coef + 192;                   // 128 floats
   bf16_t* tile0 = reinterpret_cast<bf16_t*>(smem + 1280);
 #define SBUF(i) (tile0 + ((i) & 1) * TSZ)
-
-  const int4 wk = a.work[blockIdx.x];
+  STAMP_DECL
+  STAMP(0);
+  const int4 wk = work_item(a);
   DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
   const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ct = wave % NT + (SPLIT > 1 ? wk.z * NT : 0);
+  // prologue loads in the order they are consumed: BN statistics -> input tile -> weights
+  CoefLd<MODE_IN == 0 ? 0 : 1> cl;
+  coef_issue<C, MODE_IN == 0 ? 0 : 1>(cl, a, slot, a.st_in, a.st_in_b, a.in_gamma, a.in_beta);
+  const float n_in = a.cnt[slot] * (float)(H * W);
+  St st;
+  st.init();
+  uint4 tv[MAXC], unused[MAXC];
+  unsigned tm;
+  {
+    const int img = it0 / BANDS, gy0 = (it0 % BANDS) * ROWS - 1;
+    tm = st.mask(gy0);
+    st.template load<LMODE>(tv, unused, tm, a.x + img * IMG, nullptr, gy0);
+  }
   bf16x8_t afr[KS];
   {
     const bf16_t* wb = a.w + (long)slot * a.w_mstride + a.w_off + (long)(ct * 16 + (lane & 15)) * KTOT;
@@ -704,16 +835,7 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
       afr[s] = v;
     }
   }
-  St st;
-  st.init();
-  uint4 tv[MAXC], unused[MAXC];
-  unsigned tm;
-  {
-    const int img = it0 / BANDS, gy0 = (it0 % BANDS) * ROWS - 1;
-    tm = st.mask(gy0);
-    st.template load<LMODE>(tv, unused, tm, a.x + img * IMG, nullptr, gy0);
-  }
-  make_coef<C, MODE_IN>(coef, a, slot, a.cnt[slot] * (float)(H * W), a.st_in, a.st_in_b, a.in_gamma, a.in_beta);
+  coef_finish<C, MODE_IN == 0 ? 0 : 1>(coef, cl, n_in);
   if (threadIdx.x < 128) acc_lds[threadIdx.x] = 0.f;
   int tapoff[KS];  // k-chunks past KTOT have zero weights and read a valid in-tile address
 #pragma unroll
@@ -733,8 +855,10 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
   }
   f32x2_t ssum[2] = {{0.f, 0.f}, {0.f, 0.f}}, ssq[2] = {{0.f, 0.f}, {0.f, 0.f}};
   __syncthreads();  // coefficients
+  STAMP(1);
   st.template store<LMODE>(SBUF(0), tv, unused, tm, coef);
   __syncthreads();
+  STAMP(2);
   for (int k = 0; k < nit; ++k) {
     const int it = it0 + k;
     const int img = it / BANDS, r0 = (it % BANDS) * ROWS;
@@ -776,11 +900,14 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
     __syncthreads();
   }
 #undef SBUF
+  STAMP(3);
   const float s4[4] = {ssum[0].x, ssum[0].y, ssum[1].x, ssum[1].y};
   const float q4[4] = {ssq[0].x, ssq[0].y, ssq[1].x, ssq[1].y};
   reduce_stats_to_lds(acc_lds, s4, q4, co0, lane);
   __syncthreads();
   flush_stats(a.st_out, acc_lds, slot, C);
+  STAMP_DRAIN(4);
+  STAMP_FLUSH(a.cin_real, nit);
 }
 
 // ---------------------------------------------------------------------------------- dgrad
@@ -1167,8 +1294,12 @@ __device__ __forceinline__ void slab_reduce_wg(const float* __restrict__ slab, c
 // a 32-bit lane offset fixed for the workgroup, and the elementwise work uses
 // packed fp32 / bf16 math: the VALU budget per MFMA is what bounds these
 // small-channel layers.
-template <int C, int MODE_DY, int EPI>
-__global__ __launch_bounds__(256, DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_fused_kernel(ConvArgs a) {
+// ROLE (split backward of small populations, engine/hip_resnet.py DTF_SPLIT_BWD): 0 = dgrad + wgrad (fused),
+// 1 = dgrad only (critical path: no X tile, no wgrad; the transformed dY may be materialised via xout for the
+// wgrad), 2 = wgrad only (runs on a side stream beside the next layers' dgrads; no dgrad / stats / xout).
+template <int C, int MODE_DY, int EPI, int ROLE = 0>
+__global__ __launch_bounds__(256, ROLE == 1 ? 2 : DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_fused_kernel(ConvArgs a) {
+  constexpr bool DG = ROLE != 2, WG = ROLE != 1;
   constexpr int W = 512 / C, H = W, ROWS = 8, BANDS = H / ROWS;
   constexpr int NT = C / 16;           // dgrad output-channel tiles
   constexpr int WPT = 4 / NT;
@@ -1191,15 +1322,18 @@ __global__ __launch_bounds__(256, DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_fus
   float* acc_lds = ecoef + 256;                    // 128
   bf16_t* t0 = reinterpret_cast<bf16_t*>(smem + 2304);
   // SB: single-buffered tiles (one extra barrier per iteration) so that C = 16 fits 3 workgroups per CU in LDS
-  constexpr bool SB = C == 16 && MODE_DY != 3 && DTF_FUSED_SB16;
-#define FDBUF(i) (t0 + (SB ? 0 : ((i) & 1) * 2 * TSZ))
-#define FXBUF(i) (t0 + TSZ + (SB ? 0 : ((i) & 1) * 2 * TSZ))
+  constexpr bool SB = C == 16 && MODE_DY != 3 && DTF_FUSED_SB16 && ROLE == 0;
+  constexpr int BSTR = WG ? 2 * TSZ : TSZ;  // dgrad-only: dY tiles only
+#define FDBUF(i) (t0 + (SB ? 0 : ((i) & 1) * BSTR))
+#define FXBUF(i) (t0 + TSZ + (SB ? 0 : ((i) & 1) * BSTR))
   // raw (untransformed) x of the band interior, for the dgrad epilogue's mask / x-hat: read from LDS instead of
   // re-reading x from global memory (double-buffered like the tiles)
   // (C <= 32 keeps the global re-read unless built with DTF_RAWX16: the extra LDS would cost its 2nd WG per CU)
-  constexpr bool RAWX = C >= 64 || DTF_RAWX16;
+  constexpr bool RAWX = ROLE == 0 && (C >= 64 || DTF_RAWX16);
   constexpr int RAWSZ = ROWS * W * CP;
 #define FXRAW(i) (t0 + 4 * TSZ + ((i) & 1) * RAWSZ)
+  STAMP_DECL
+  STAMP(0);
 
   if ((int)blockIdx.x >= a.n_main) {  // trailing workgroups: dW slab reduction of the previous fused launch
     const int r = (int)blockIdx.x - a.n_main;
@@ -1209,22 +1343,19 @@ __global__ __launch_bounds__(256, DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_fus
     else if (a.r_c == 64) slab_reduce_wg<64>(a.rslab, a.rtab, a.grads, a.g_mstride, a.r_goff, r % a.r_nblk, r / a.r_nblk, part);
     return;
   }
-  const int4 wk = a.work[blockIdx.x];
+  const int4 wk = work_item(a);
   DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
   const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ct = wave % NT;
-  bf16x8_t afr[KS];
-  {
-    const bf16_t* wb = a.w + (long)slot * a.w_mstride + a.w_off + (long)(ct * 16 + (lane & 15)) * KTOT;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int k0 = 32 * s + 8 * (lane >> 4);
-      bf16x8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (k0 < KTOT) v = *reinterpret_cast<const bf16x8_t*>(wb + k0);
-      afr[s] = v;
-    }
-  }
+  STAMP_FINE(8);
+  // prologue loads in the order they are consumed: BN statistics (dY transform, x BN) -> tiles -> weights
+  CoefLd<MODE_DY == 0 ? 0 : 2> cld;
+  coef_issue<C, MODE_DY == 0 ? 0 : 2>(cld, a, slot, a.st_in, a.st_in_b, a.in_gamma, a.in_beta);
+  CoefLd<1> cle;
+  if constexpr (!(EPI & 2)) coef_issue<C, 1>(cle, a, slot, a.st_ep, nullptr, a.ep_gamma, a.ep_beta);
+  const float n_hw = a.cnt[slot] * (float)(H * W);
+  STAMP_FINE(9);
   St st;
   st.init();
   // MODE_DY 3: dY = BN-backward(x, x2) + x3; with xout the transformed band interior is also written out
@@ -1236,18 +1367,32 @@ __global__ __launch_bounds__(256, DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_fus
     dm = xm = st.mask(cgy0);
     st.template load<MODE_DY == 3 ? 2 : MODE_DY>(dv, dv2, dm, a.x + cimg * IMG, a.x2 + cimg * IMG, cgy0);
     if constexpr (MODE_DY == 3) st.template load<0>(dv3, unused, dm, a.x3 + cimg * IMG, nullptr, cgy0);
-    st.template load<1>(xv_, unused, xm, a.xm + cimg * IMG, nullptr, cgy0);
+    if constexpr (WG) st.template load<1>(xv_, unused, xm, a.xm + cimg * IMG, nullptr, cgy0);
   }
-  const float n_hw = a.cnt[slot] * (float)(H * W);
-  make_coef<C, MODE_DY>(coef_d, a, slot, n_hw, a.st_in, a.st_in_b, a.in_gamma, a.in_beta);
+  STAMP_FINE(10);
+  bf16x8_t afr[KS];
+  if constexpr (DG) {
+    const bf16_t* wb = a.w + (long)slot * a.w_mstride + a.w_off + (long)(ct * 16 + (lane & 15)) * KTOT;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int k0 = 32 * s + 8 * (lane >> 4);
+      bf16x8_t v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (k0 < KTOT) v = *reinterpret_cast<const bf16x8_t*>(wb + k0);
+      afr[s] = v;
+    }
+  }
+  STAMP_FINE(12);
+  coef_finish<C, MODE_DY == 0 ? 0 : 2>(coef_d, cld, n_hw);
+  STAMP_FINE(13);
   {
     const int c = threadIdx.x;
     if (c < C) {
-      const float* prow = a.params + (long)slot * a.p_mstride;
       float scale = 1.f, shift = 0.f, mean = 0.f, inv = 1.f;  // EPI bit1: identity BN (v1 block input)
-      if constexpr (!(EPI & 2))
-        bn_fwd_coef(stats_row(a.st_ep, slot), n_hw, prow[a.ep_gamma + c], prow[a.ep_beta + c], c, scale, shift,
-                    mean, inv);
+      if constexpr (!(EPI & 2)) {
+        coef_moments<1>(cle, n_hw, mean, inv);
+        scale = cle.g * inv;
+        shift = cle.b - mean * scale;
+      }
       ecoef[c] = scale;
       ecoef[64 + c] = shift;
       ecoef[128 + c] = -mean * inv;
@@ -1255,6 +1400,7 @@ __global__ __launch_bounds__(256, DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_fus
     }
     if (threadIdx.x < 128) acc_lds[threadIdx.x] = 0.f;
   }
+  STAMP_FINE(11);
   // dgrad lane constants; k-chunks past KTOT have zero weights and read a valid in-tile address
   int tapoff[KS];
 #pragma unroll
@@ -1294,14 +1440,16 @@ __global__ __launch_bounds__(256, DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_fus
   f32x2_t ssum[2] = {{0.f, 0.f}, {0.f, 0.f}}, ssq[2] = {{0.f, 0.f}, {0.f, 0.f}};
 
   __syncthreads();  // coefficients
-  if constexpr (XSTORE)
+  STAMP(1);
+  if constexpr (XSTORE && DG)
     st.template store_x<MODE_DY == 3 ? 3 : 2>(FDBUF(0), dv, dv2, dv3, dm, coef_d,
                                               a.xout ? a.xout + cimg * IMG : nullptr, cgy0);
   else
     st.template store<MODE_DY>(FDBUF(0), dv, dv2, dm, coef_d);
-  st.template store<1>(FXBUF(0), xv_, unused, xm, ecoef);
+  if constexpr (WG) st.template store<1>(FXBUF(0), xv_, unused, xm, ecoef);
   if constexpr (RAWX) st.store_raw(FXRAW(0), xv_, xm);
   __syncthreads();
+  STAMP(2);
   for (int k = 0; k < nit; ++k) {
     const int it = it0 + k;
     const int img = it / BANDS, r0 = (it % BANDS) * ROWS;
@@ -1309,6 +1457,7 @@ __global__ __launch_bounds__(256, DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_fus
     const long band = (long)img * IMG + r0 * ROW;
     // epilogue operands before the prefetch (counted vmcnt)
     uint2 rres[MAXT], xres[MAXT];
+    if constexpr (DG) {
 #pragma unroll
     for (int i = 0; i < MAXT; ++i) {
       if constexpr (EPI & 1) rres[i] = *reinterpret_cast<const uint2*>(a.res + band + pofs[i]);
@@ -1317,13 +1466,14 @@ __global__ __launch_bounds__(256, DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_fus
       else
         xres[i] = *reinterpret_cast<const uint2*>(a.xm + band + pofs[i]);
     }
+    }
     if (more) {
       cimg = (it + 1) / BANDS;
       cgy0 = ((it + 1) % BANDS) * ROWS - 1;
       dm = xm = st.mask(cgy0);
       st.template load<MODE_DY == 3 ? 2 : MODE_DY>(dv, dv2, dm, a.x + cimg * IMG, a.x2 + cimg * IMG, cgy0);
       if constexpr (MODE_DY == 3) st.template load<0>(dv3, unused, dm, a.x3 + cimg * IMG, nullptr, cgy0);
-      st.template load<1>(xv_, unused, xm, a.xm + cimg * IMG, nullptr, cgy0);
+      if constexpr (WG) st.template load<1>(xv_, unused, xm, a.xm + cimg * IMG, nullptr, cgy0);
     }
     const bf16_t* dcur = FDBUF(k);
     const bf16_t* xcur = FXBUF(k);
@@ -1332,7 +1482,7 @@ __global__ __launch_bounds__(256, DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_fus
     const f32x2_t sh0 = lds2(ecoef + 64 + ci0), sh1 = lds2(ecoef + 64 + ci0 + 2);
     const f32x2_t nm0 = lds2(ecoef + 128 + ci0), nm1 = lds2(ecoef + 128 + ci0 + 2);
     const f32x2_t iv0 = lds2(ecoef + 192 + ci0), iv1 = lds2(ecoef + 192 + ci0 + 2);
-    if constexpr (!(DTF_ABL & 4)) {  // timing-only ablation builds (tools/ablate.sh): skip the dgrad
+    if constexpr (DG && !(DTF_ABL & 4)) {  // timing-only ablation builds (tools/ablate.sh): skip the dgrad
 #pragma unroll
     for (int i = 0; i < MAXT; ++i) {
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
@@ -1362,7 +1512,7 @@ __global__ __launch_bounds__(256, DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_fus
     }
     }  // DTF_ABL & 4
     // ---- wgrad
-    if constexpr (!(DTF_ABL & 2)) {  // ablation: skip the wgrad
+    if constexpr (WG && !(DTF_ABL & 2)) {  // ablation: skip the wgrad
 #pragma unroll
     for (int ks = 0; ks < NK; ++ks) {
       bf16x8_t af[MT];
@@ -1387,12 +1537,12 @@ __global__ __launch_bounds__(256, DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_fus
     }  // DTF_ABL & 2
     if (more) {
       if constexpr (SB) __syncthreads();  // every wave is done with the current tiles
-      if constexpr (XSTORE)
+      if constexpr (XSTORE && DG)
         st.template store_x<MODE_DY == 3 ? 3 : 2>(FDBUF(k + 1), dv, dv2, dv3, dm, coef_d,
                                                   a.xout ? a.xout + cimg * IMG : nullptr, cgy0);
       else
         st.template store<MODE_DY>(FDBUF(k + 1), dv, dv2, dm, coef_d);
-      st.template store<1>(FXBUF(k + 1), xv_, unused, xm, ecoef);
+      if constexpr (WG) st.template store<1>(FXBUF(k + 1), xv_, unused, xm, ecoef);
       if constexpr (RAWX) st.store_raw(FXRAW(k + 1), xv_, xm);
     }
     __syncthreads();
@@ -1400,13 +1550,20 @@ __global__ __launch_bounds__(256, DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_fus
 #undef FDBUF
 #undef FXBUF
 #undef FXRAW
-  {
+  STAMP(3);
+  if constexpr (DG) {
     const float s4[4] = {ssum[0].x, ssum[0].y, ssum[1].x, ssum[1].y};
     const float q4[4] = {ssq[0].x, ssq[0].y, ssq[1].x, ssq[1].y};
     reduce_stats_to_lds(acc_lds, s4, q4, ci0, lane);
+    __syncthreads();
   }
-  __syncthreads();
-  if constexpr (!(EPI & 2)) flush_stats(a.st_out, acc_lds, slot, C);
+  if constexpr (DG && !(EPI & 2)) flush_stats(a.st_out, acc_lds, slot, C);
+  STAMP(4);
+  if constexpr (!WG) {
+    STAMP_DRAIN(5);
+    STAMP_FLUSH(a.cin_real, nit);
+    return;
+  }
   if (a.slab) {
     // partial-sum slab [wg][j][m][256 threads][4]: one 16-byte store per lane per accumulator tile (a 1 KB
     // row per wave instruction; the store tail is issue-bound); dw_slab_reduce sums a member's slabs
@@ -1435,6 +1592,8 @@ __global__ __launch_bounds__(256, DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_fus
         }
 #endif
     }
+    STAMP_DRAIN(5);
+    STAMP_FLUSH(a.cin_real, nit);
     return;
   }
   float* gb = a.grads + (long)slot * a.g_mstride + a.g_off;
@@ -1453,6 +1612,8 @@ __global__ __launch_bounds__(256, DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_fus
       }
     }
   }
+  STAMP_DRAIN(5);
+  STAMP_FLUSH(a.cin_real, nit);
 }
 
 // Sum of one member's per-workgroup dW slabs (written by conv_bwd_fused_kernel) into its gradient row.
@@ -1540,6 +1701,18 @@ DTF_API int dtf_dw_slab_reduce(const float* slab, const int4* red, int nmembers,
 
 DTF_DEBUG_EXPORT(conv)
 
+// Diagnostic stamp buffer (DTF_STAMP builds): [launch row][workgroup][8] u64; returns -1 in normal builds.
+DTF_API int dtf_stamp_read(void* dst, long bytes) {
+#if DTF_STAMP
+  if (bytes > (long)sizeof(dtf_stamps)) bytes = (long)sizeof(dtf_stamps);
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(dtf_stamps), bytes);
+#else
+  (void)dst;
+  (void)bytes;
+  return -1;
+#endif
+}
+
 DTF_API int dtf_conv_args_size() { return (int)sizeof(ConvArgs); }
 
 DTF_API int dtf_conv_fwd(const ConvArgs* args, int cin, int cout, int s, int k, int mode, int resid, int stats,
@@ -1619,6 +1792,24 @@ DTF_API int dtf_conv_bwd_fused(const ConvArgs* args, int c, int mode_dy, int epi
   FUSED_CASE(16, 2, 3)  // v1 conv_a: identity-BN block input (+ shortcut grad)
   FUSED_CASE(32, 2, 3)
   FUSED_CASE(64, 2, 3)
+  return -1;
+}
+
+// Split backward roles (ROLE 1 dgrad / ROLE 2 wgrad of conv_bwd_fused_kernel).
+DTF_API int dtf_conv_bwd_role(const ConvArgs* args, int c, int mode_dy, int epi, int role, int nblocks, int lds,
+                              hipStream_t stream) {
+#define ROLE_CASE(CC, M, E, R)                                      \
+  if (c == CC && mode_dy == M && epi == E && role == R)            \
+    return launch(conv_bwd_fused_kernel<CC, M, E, R>, nblocks, lds, stream, *args);
+  ROLE_CASE(16, 0, 0, 1) ROLE_CASE(32, 0, 0, 1) ROLE_CASE(64, 0, 0, 1)
+  ROLE_CASE(16, 3, 0, 1) ROLE_CASE(32, 3, 0, 1) ROLE_CASE(64, 3, 0, 1)
+  ROLE_CASE(16, 2, 0, 1) ROLE_CASE(32, 2, 0, 1) ROLE_CASE(64, 2, 0, 1)
+  ROLE_CASE(16, 2, 1, 1)
+  ROLE_CASE(16, 2, 3, 1) ROLE_CASE(32, 2, 3, 1) ROLE_CASE(64, 2, 3, 1)
+  // wgrad role: dY is always a materialised tensor (MODE 0); EPI bit 1 = identity-BN x (v1)
+  ROLE_CASE(16, 0, 0, 2) ROLE_CASE(32, 0, 0, 2) ROLE_CASE(64, 0, 0, 2)
+  ROLE_CASE(16, 0, 2, 2) ROLE_CASE(32, 0, 2, 2) ROLE_CASE(64, 0, 2, 2)
+#undef ROLE_CASE
   return -1;
 }
 

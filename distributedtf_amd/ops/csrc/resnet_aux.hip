@@ -10,7 +10,7 @@
 
 #define BN_EPS 1e-5f
 #define BN_MOM 0.997f
-#define NREP 8
+#define NREP DTF_NREP
 
 namespace {
 

@@ -452,8 +452,9 @@ class _StepPlan:
         # Split backward (small populations: the step is latency-bound, one workgroup per CU): every stride-1 conv's
         # dgrad runs on the main stream (the critical path) and its wgrad on a side stream, concurrently with the
         # next layers' dgrads; backward temporaries are then never reused (the side stream reads them later).
-        # DTF_SPLIT_BWD: "auto" (populations of <= DTF_SPLIT_MAX_POP members, default 2), "1", "0".
-        sp = os.environ.get("DTF_SPLIT_BWD", "auto")
+        # DTF_SPLIT_BWD: "auto" (populations of <= DTF_SPLIT_MAX_POP members, default 2), "1", "0" (default: on this
+        # ROCm the graph's cross-queue dependencies cost ~10 us each, pop 1 measured 2.30 vs 1.45 ms/step).
+        sp = os.environ.get("DTF_SPLIT_BWD", "0")
         self.split = dev.type == "cuda" and not cfg.version == 1 and (
             sp == "1" or (sp == "auto" and len(slots) <= int(os.environ.get("DTF_SPLIT_MAX_POP", "2"))))
         self.side_reduce = bool(self.side_cs) or self.split

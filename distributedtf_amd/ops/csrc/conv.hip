@@ -854,6 +854,13 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
     pofs[i] = p * C + co0;
   }
   f32x2_t ssum[2] = {{0.f, 0.f}, {0.f, 0.f}}, ssq[2] = {{0.f, 0.f}, {0.f, 0.f}};
+  // residual operands one iteration ahead (software-pipelined: their latency hides behind staging / MFMAs)
+  uint2 nres[MT];
+  if constexpr (RESID) {
+    const long band0 = (long)(it0 / BANDS) * IMG + (it0 % BANDS) * ROWS * ROW;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) nres[i] = *reinterpret_cast<const uint2*>(a.res + band0 + pofs[i]);
+  }
   __syncthreads();  // coefficients
   STAMP(1);
   st.template store<LMODE>(SBUF(0), tv, unused, tm, coef);
@@ -867,12 +874,17 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
     uint2 rres[MT];
     if constexpr (RESID) {
 #pragma unroll
-      for (int i = 0; i < MT; ++i) rres[i] = *reinterpret_cast<const uint2*>(a.res + band + pofs[i]);
+      for (int i = 0; i < MT; ++i) rres[i] = nres[i];
     }
     if (more) {
       const int nimg = (it + 1) / BANDS, ngy0 = ((it + 1) % BANDS) * ROWS - 1;
       tm = st.mask(ngy0);
       st.template load<LMODE>(tv, unused, tm, a.x + nimg * IMG, nullptr, ngy0);
+      if constexpr (RESID) {
+        const long nband = (long)nimg * IMG + ((it + 1) % BANDS) * ROWS * ROW;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) nres[i] = *reinterpret_cast<const uint2*>(a.res + nband + pofs[i]);
+      }
     }
     const bf16_t* tile = SBUF(k);
 #pragma unroll
@@ -1438,6 +1450,17 @@ __global__ __launch_bounds__(256, ROLE == 1 ? 2 : DTF_FUSED_WAVES(C, MODE_DY)) v
 #pragma unroll
     for (int m = 0; m < MT; ++m) wacc[j][m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
   f32x2_t ssum[2] = {{0.f, 0.f}, {0.f, 0.f}}, ssq[2] = {{0.f, 0.f}, {0.f, 0.f}};
+  // dgrad epilogue operands from global memory one iteration ahead (software-pipelined)
+  uint2 nres[MAXT], nxres[MAXT];
+  auto epi_load = [&](int it_) {
+    const long b_ = (long)(it_ / BANDS) * IMG + (it_ % BANDS) * ROWS * ROW;
+#pragma unroll
+    for (int i = 0; i < MAXT; ++i) {
+      if constexpr (EPI & 1) nres[i] = *reinterpret_cast<const uint2*>(a.res + b_ + pofs[i]);
+      if constexpr (!RAWX) nxres[i] = *reinterpret_cast<const uint2*>(a.xm + b_ + pofs[i]);
+    }
+  };
+  if constexpr (DG) epi_load(it0);
 
   __syncthreads();  // coefficients
   STAMP(1);
@@ -1460,11 +1483,11 @@ __global__ __launch_bounds__(256, ROLE == 1 ? 2 : DTF_FUSED_WAVES(C, MODE_DY)) v
     if constexpr (DG) {
 #pragma unroll
     for (int i = 0; i < MAXT; ++i) {
-      if constexpr (EPI & 1) rres[i] = *reinterpret_cast<const uint2*>(a.res + band + pofs[i]);
+      if constexpr (EPI & 1) rres[i] = nres[i];
       if constexpr (RAWX)
         xres[i] = *reinterpret_cast<const uint2*>(FXRAW(k) + rpo[i]);
       else
-        xres[i] = *reinterpret_cast<const uint2*>(a.xm + band + pofs[i]);
+        xres[i] = nxres[i];
     }
     }
     if (more) {
@@ -1474,6 +1497,7 @@ __global__ __launch_bounds__(256, ROLE == 1 ? 2 : DTF_FUSED_WAVES(C, MODE_DY)) v
       st.template load<MODE_DY == 3 ? 2 : MODE_DY>(dv, dv2, dm, a.x + cimg * IMG, a.x2 + cimg * IMG, cgy0);
       if constexpr (MODE_DY == 3) st.template load<0>(dv3, unused, dm, a.x3 + cimg * IMG, nullptr, cgy0);
       if constexpr (WG) st.template load<1>(xv_, unused, xm, a.xm + cimg * IMG, nullptr, cgy0);
+      if constexpr (DG) epi_load(it + 1);
     }
     const bf16_t* dcur = FDBUF(k);
     const bf16_t* xcur = FXBUF(k);

@@ -109,6 +109,8 @@ def _register():
                                      c_void_p, c_long, c_void_p])
     ops.register("dtf_bn_running_update", [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_long, c_void_p,
                                            c_int, c_void_p, c_void_p, c_long, c_void_p])
+    ops.register("dtf_bn_eval_stats", [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_long, c_void_p, c_int,
+                                       c_void_p, c_void_p])
     ops.register("dtf_bn_bwd_apply", [P(BnBwdArgs), c_void_p])
     ops.register("dtf_bn_add_relu", [P(BnEwArgs), c_void_p])
     ops.register("dtf_bn_bwd_reduce", [P(BnEwArgs), c_void_p])
@@ -357,22 +359,64 @@ class HipResNetBackend:
     def forward_backward(self, slots, batches):
         raise RuntimeError("HipResNetBackend runs whole steps: use train_step")
 
+    def train_correct(self, slots):
+        """Correct predictions of each member's last training batch (head kernel count; device tensor)."""
+        return self.correct[torch.as_tensor(list(slots), dtype=torch.long, device=self.dev)]
+
     @torch.no_grad()
     def infer(self, slot, x):
-        """Eval-mode forward with running statistics (torch reference ops on bf16 shadow math)."""
-        e = self.e
-        return e.arch.forward(e.params[slot], e.running[slot], x, training=False, dtype=torch.bfloat16)
+        """Eval-mode logits of one member on the HIP forward kernels (moving BN statistics)."""
+        p = self.eval_plan([slot], int(x.shape[0]))
+        logits = p.want_logits()
+        p.load_eval(x, torch.zeros(x.shape[0], dtype=torch.int32, device=x.device))
+        p.run_eval()
+        return logits.clone()
+
+    def eval_plan(self, slots, m):
+        key = (tuple(slots), int(m))
+        plans = self.__dict__.setdefault("_eval_plans", {})
+        p = plans.get(key)
+        if p is None:
+            if len(plans) > 8:
+                plans.clear()
+            p = _StepPlan(self, list(slots), [int(m)] * len(slots), None, eval_mode=True)
+            plans[key] = p
+        return p
+
+    @torch.no_grad()
+    def evaluate_population(self, slots, x, y, chunk=None):
+        """Eval accuracy of every member in ``slots`` on (x, y) in one population-batched forward per chunk of
+        ``chunk`` images (all members see the same chunk); one host sync at the end."""
+        n = int(x.shape[0])
+        if n == 0 or not slots:
+            return {s: 0.0 for s in slots}
+        chunk = min(n, int(chunk or os.environ.get("DTF_EVAL_CHUNK", "2000")))
+        used = []
+        for i in range(0, n, chunk):
+            m = min(chunk, n - i)
+            p = self.eval_plan(slots, m)
+            if all(p is not q for q in used):
+                p.ev_acc.zero_()
+                used.append(p)
+            p.load_eval(x[i:i + m], y[i:i + m])
+            p.run_eval()
+        correct = used[0].ev_acc[0].clone()
+        for p in used[1:]:
+            correct += p.ev_acc[0]
+        vals = correct.cpu().tolist()
+        return {s: vals[s] / float(n) for s in slots}
 
 
 class _StepPlan:
     """Buffers + prebuilt launch list for one batch composition (slots, per-member sizes)."""
 
-    def __init__(self, be: HipResNetBackend, slots: List[int], sizes: List[int], src=None):
+    def __init__(self, be: HipResNetBackend, slots: List[int], sizes: List[int], src=None, eval_mode=False):
         self.be = be
         e = be.e
         self.e = e
         self.slots = slots
         self.sizes = sizes
+        self.eval = bool(eval_mode)
         dev = be.dev
         L = be.L
         prog = L.prog
@@ -404,22 +448,47 @@ class _StepPlan:
             self.idx = torch.zeros(N, dtype=torch.long, device=dev)
             self.rng = torch.zeros(2, dtype=torch.int32, device=dev)
         self.v1 = cfg.version == 1
-        # forward activations saved for backward
+        # forward activations saved for backward (eval: nothing is saved -- per-resolution buffers are reused,
+        # the residual stream ping-pongs between two)
         self.xs, self.hs, self.scs = [], [], []
         self.hb = []  # v1: conv_b outputs (pre-BN); hs = conv_a outputs, scs = projection outputs (pre-BN)
         self.h0 = torch.empty(N, H, H, cfg.num_filters, dtype=torch.bfloat16, device=dev) if self.v1 else None
+        pool = {}
+
+        def act(kind, hw_, c_, i_=0):
+            if not self.eval:
+                return torch.empty(N, hw_, hw_, c_, dtype=torch.bfloat16, device=dev)
+            key = (kind, hw_, c_, i_ % 2 if kind == "x" else 0)
+            if key not in pool:
+                pool[key] = torch.empty(N, hw_, hw_, c_, dtype=torch.bfloat16, device=dev)
+            return pool[key]
+
         hw, c = H, cfg.num_filters
-        self.xs.append(torch.empty(N, hw, hw, c, dtype=torch.bfloat16, device=dev))
-        for blk in prog.blocks:
+        self.xs.append(act("x", hw, c, 0))
+        for bi, blk in enumerate(prog.blocks):
             ca = prog.convs[blk.convs[0]]
             hw_o = hw // blk.stride
-            self.hs.append(torch.empty(N, hw_o, hw_o, ca.cout, dtype=torch.bfloat16, device=dev))
-            self.scs.append(torch.empty(N, hw_o, hw_o, ca.cout, dtype=torch.bfloat16, device=dev)
-                            if blk.proj is not None else None)
-            self.xs.append(torch.empty(N, hw_o, hw_o, ca.cout, dtype=torch.bfloat16, device=dev))
+            self.hs.append(act("h", hw_o, ca.cout))
+            self.scs.append(act("sc", hw_o, ca.cout) if blk.proj is not None else None)
+            self.xs.append(act("x", hw_o, ca.cout, bi + 1))
             if self.v1:
-                self.hb.append(torch.empty(N, hw_o, hw_o, ca.cout, dtype=torch.bfloat16, device=dev))
+                self.hb.append(act("hb", hw_o, ca.cout))
             hw = hw_o
+        if self.eval:
+            nb = len(prog.bns)
+            cap = e.capacity
+            # moving statistics in accumulator form (bn_eval_stats) + a sink for the conv epilogues' statistics
+            self.ev_stats = torch.zeros(nb, cap, NREP, 128, dtype=torch.float32, device=dev)
+            self.ev_sink = torch.zeros(cap, NREP, 128, dtype=torch.float32, device=dev)
+            self.ev_acc = torch.zeros(2, cap, dtype=torch.float32, device=dev)  # [correct, summed mean CE] per slot
+            self.logits = None  # [N, ncls] fp32 when requested (tests)
+            self._work_cache, self._uniform_geo = {}, {}
+            self.side_cs, self.split, self.side_reduce, self.side_stream = frozenset(), False, False, None
+            self.launches = []
+            self._pending_slab = None
+            self._build_eval()
+            self.graph = None
+            return
         # backward temporaries, one set per resolution
         self.tmp = {}
         hw, c = H, cfg.num_filters
@@ -576,9 +645,9 @@ class _StepPlan:
         a.work = _p(work)
         if in_bn is not None:
             a.in_gamma, a.in_beta = self._bn(in_bn)
-            a.st_in = _p(be.st_f(in_bn))
+            a.st_in = _p(self._st_r(in_bn))
         if stats_bn is not None:
-            a.st_out = _p(be.st_f(stats_bn))
+            a.st_out = _p(self._st_w(stats_bn))
         a.Hi, a.Wi, a.Ho, a.Wo, a.rows = Hi, Hi, Ho, Ho, rows
         rows_in = (rows - 1) * c.stride + c.k
         tsz = (rows_in * (Hi + 2 * P) * max(_cpad(cin), _cpad_fwd(cin)) + 8 + 63) // 64 * 64
@@ -952,18 +1021,8 @@ class _StepPlan:
         else:
             self._add(lib.dtf_prep_input, _p(self.x_in), _p(self.xin16), N * cfg.image_size * cfg.image_size, 3)
         # ---------------- forward
-        first_bn = prog.blocks[0].bns[0]
-        self._conv_fwd(prog.stem, self.xin16, self.xs[0], stats_bn=first_bn, in_bn=None)
+        self._forward_v2()
         nblk = len(prog.blocks)
-        for i, blk in enumerate(prog.blocks):
-            bn1, bn2 = blk.bns
-            nxt = prog.blocks[i + 1].bns[0] if i + 1 < nblk else prog.final_bn
-            x, h, y = self.xs[i], self.hs[i], self.xs[i + 1]
-            if blk.proj is not None:
-                self._conv_fwd(blk.proj, x, self.scs[i], stats_bn=None, in_bn=bn1)
-            self._conv_fwd(blk.convs[0], x, h, stats_bn=bn2, in_bn=bn1)
-            res = self.scs[i] if blk.proj is not None else x
-            self._conv_fwd(blk.convs[1], h, y, stats_bn=nxt, in_bn=bn2, res=res)
         # head (fwd + bwd of GAP/dense/CE + final-BN reductions)
         fb = prog.final_bn
         hw = L.final_hw
@@ -1043,6 +1102,104 @@ class _StepPlan:
         self._add("optim", None)
         self._add("step", None)
 
+    def _forward_v2(self):
+        """Stem + every pre-activation block (BN+ReLU prologues, BN-statistic epilogues, residual adds)."""
+        prog = self.be.L.prog
+        first_bn = prog.blocks[0].bns[0]
+        self._conv_fwd(prog.stem, self.xin16, self.xs[0], stats_bn=first_bn, in_bn=None)
+        nblk = len(prog.blocks)
+        for i, blk in enumerate(prog.blocks):
+            bn1, bn2 = blk.bns
+            nxt = prog.blocks[i + 1].bns[0] if i + 1 < nblk else prog.final_bn
+            x, h, y = self.xs[i], self.hs[i], self.xs[i + 1]
+            if blk.proj is not None:
+                self._conv_fwd(blk.proj, x, self.scs[i], stats_bn=None, in_bn=bn1)
+            self._conv_fwd(blk.convs[0], x, h, stats_bn=bn2, in_bn=bn1)
+            res = self.scs[i] if blk.proj is not None else x
+            self._conv_fwd(blk.convs[1], h, y, stats_bn=nxt, in_bn=bn2, res=res)
+
+    def _forward_v1(self):
+        """v1 stem (conv -> BN -> ReLU) + post-activation blocks (``_building_block_v1``)."""
+        prog, cfg = self.be.L.prog, self.be.L.cfg
+        lib = ops.lib()
+        H = cfg.image_size
+        self._conv_fwd(prog.stem, self.xin16, self.h0, stats_bn=prog.stem_bn, in_bn=None)
+        self._bn_ew(lib.dtf_bn_add_relu, (H * H, cfg.num_filters), prog.stem_bn, self.h0, out=self.xs[0])
+        for i, blk in enumerate(prog.blocks):
+            bna, bnb = blk.bns
+            x, ha, hb, y = self.xs[i], self.hs[i], self.hb[i], self.xs[i + 1]
+            if blk.proj is not None:
+                self._conv_fwd(blk.proj, x, self.scs[i], stats_bn=blk.proj_bn, in_bn=None)
+            self._conv_fwd(blk.convs[0], x, ha, stats_bn=bna, in_bn=None)
+            self._conv_fwd(blk.convs[1], ha, hb, stats_bn=bnb, in_bn=bna)
+            hw_o = y.shape[1] * y.shape[2]
+            if blk.proj is not None:
+                self._bn_ew(lib.dtf_bn_add_relu, (hw_o, y.shape[3]), bnb, hb, bn2=blk.proj_bn, h2=self.scs[i], out=y)
+            else:
+                self._bn_ew(lib.dtf_bn_add_relu, (hw_o, y.shape[3]), bnb, hb, add=x, out=y)
+
+    # ----- eval mode: BN with moving statistics (resnet_run_loop.py:463-466 ``classifier.evaluate``)
+    def _st_r(self, bn):
+        """Statistics a BN consumer normalises with: this step's batch statistics, or (eval) the moving ones."""
+        return self.ev_stats[bn] if self.eval else self.be.st_f(bn)
+
+    def _st_w(self, bn):
+        """Where a conv epilogue adds the statistics of its output (eval: a sink nobody reads)."""
+        return self.ev_sink if self.eval else self.be.st_f(bn)
+
+    def _build_eval(self):
+        """Forward-only launch list of an eval chunk: bf16 weights of the evaluated members, moving statistics in
+        accumulator form, input packing, the training forward kernels reading those statistics, and the head
+        in inference mode (per-member correct count; optional logits)."""
+        be, e, L = self.be, self.e, self.be.L
+        prog, cfg = L.prog, L.cfg
+        lib = ops.lib()
+        nslots = len(self.slots)
+        self._add(lib.dtf_weight_prep, _p(e.state), e.S, _p(be.conv_table_t), len(L.conv_table), _p(self.slots_t),
+                  nslots, _p(be.wf), _p(be.wd), L.wtot, None, 0)
+        self._add(lib.dtf_bn_eval_stats, _p(e.state), e.S, 3 * e.Pp, _p(be.bn_table_t), len(L.bn_table),
+                  _p(self.ev_stats), be.stats_bn_stride, _p(self.slots_t), nslots, _p(self.cnt))
+        self._add(lib.dtf_prep_input, _p(self.x_in), _p(self.xin16), self.N * cfg.image_size * cfg.image_size, 3)
+        if self.v1:
+            self._forward_v1()
+        else:
+            self._forward_v2()
+        hwork = self._work_member(target_items=int(os.environ.get("DTF_HEAD_ITEMS", "512")))
+        ha = HeadArgs()
+        ha.x, ha.labels, ha.work = _p(self.xs[-1]), _p(self.labels), _p(hwork)
+        ha.params, ha.p_mstride = _p(e.state), e.S
+        if self.v1:
+            ha.gamma_off, ha.beta_off = -1, -1
+            ha.st_f = _p(self.ev_sink)
+        else:
+            ha.gamma_off, ha.beta_off = self._bn(prog.final_bn)
+            ha.st_f = _p(self._st_r(prog.final_bn))
+        ha.dw_off, ha.db_off = prog.dense_w_off, prog.dense_b_off
+        ha.grads, ha.g_mstride = None, e.Pp
+        ha.st_b, ha.cnt = _p(self.ev_sink), _p(self.cnt)
+        ha.dfeat, ha.correct, ha.loss = None, _p(self.ev_acc[0]), _p(self.ev_acc[1])
+        ha.logits_out = None
+        ha.hw, ha.C, ha.ncls, ha.train = L.final_hw, cfg.final_size, cfg.num_classes, 0
+        self._keep(ha)
+        self._head_args = ha
+        self._add(lib.dtf_head, ctypes.byref(ha), hwork.shape[0])
+
+    def want_logits(self):
+        """Also write fp32 logits [N, ncls] of the next eval runs (numerics tests)."""
+        if self.logits is None:
+            self.logits = torch.zeros(self.N, self.be.L.cfg.num_classes, dtype=torch.float32, device=self.be.dev)
+            self._head_args.logits_out = _p(self.logits)
+        return self.logits
+
+    def load_eval(self, x, y):
+        """The same eval images for every member: [m, H, W, 3] fp32 -> this plan's [members * m] input."""
+        m = x.shape[0]
+        k = len(self.slots)
+        assert all(n == m for n in self.sizes), "eval plans hold the same chunk for every member"
+        self.x_in.view(k, m, *self.x_in.shape[1:]).copy_(x.reshape(1, m, *self.x_in.shape[1:]).expand(k, -1, -1, -1,
+                                                                                                       -1))
+        self.labels.view(k, m).copy_(y.reshape(1, m).expand(k, -1))
+
     def _zero_args(self):
         """(buffer, n) zeroed by weight_prep; DTF_ZERO_IN_PREP=0 keeps a separate fill launch instead."""
         be = self.be
@@ -1071,10 +1228,10 @@ class _StepPlan:
         a.h1, a.h2, a.add, a.out, a.d = _p(h1), _p(h2), _p(add), _p(out), _p(d)
         a.img_slot, a.params, a.p_mstride = _p(self.img_slot), _p(e.state), e.S
         a.g1, a.b1 = self._bn(bn1)
-        a.st1, a.sb1 = _p(be.st_f(bn1)), _p(be.st_b(bn1))
+        a.st1, a.sb1 = _p(self._st_r(bn1)), _p(be.st_b(bn1))
         if bn2 is not None:
             a.g2, a.b2 = self._bn(bn2)
-            a.st2, a.sb2 = _p(be.st_f(bn2)), _p(be.st_b(bn2))
+            a.st2, a.sb2 = _p(self._st_r(bn2)), _p(be.st_b(bn2))
         a.cnt, a.hw, a.C, a.nimg = _p(self.cnt), hw, C, self.N
         self._keep(a)
         self._add(fn, ctypes.byref(a))
@@ -1103,20 +1260,7 @@ class _StepPlan:
         else:
             self._add(lib.dtf_prep_input, _p(self.x_in), _p(self.xin16), N * H * H, 3)
         # ---------------- forward
-        self._conv_fwd(prog.stem, self.xin16, self.h0, stats_bn=prog.stem_bn, in_bn=None)
-        self._bn_ew(lib.dtf_bn_add_relu, (H * H, cfg.num_filters), prog.stem_bn, self.h0, out=self.xs[0])
-        for i, blk in enumerate(prog.blocks):
-            bna, bnb = blk.bns
-            x, ha, hb, y = self.xs[i], self.hs[i], self.hb[i], self.xs[i + 1]
-            if blk.proj is not None:
-                self._conv_fwd(blk.proj, x, self.scs[i], stats_bn=blk.proj_bn, in_bn=None)
-            self._conv_fwd(blk.convs[0], x, ha, stats_bn=bna, in_bn=None)
-            self._conv_fwd(blk.convs[1], ha, hb, stats_bn=bnb, in_bn=bna)
-            hw_o = y.shape[1] * y.shape[2]
-            if blk.proj is not None:
-                self._bn_ew(lib.dtf_bn_add_relu, (hw_o, y.shape[3]), bnb, hb, bn2=blk.proj_bn, h2=self.scs[i], out=y)
-            else:
-                self._bn_ew(lib.dtf_bn_add_relu, (hw_o, y.shape[3]), bnb, hb, add=x, out=y)
+        self._forward_v1()
         # head: GAP + dense + CE on the last block output (no final BN: gamma_off = -1)
         hw = L.final_hw
         hwork = self._work_member(target_items=int(os.environ.get("DTF_HEAD_ITEMS", "512")))
@@ -1227,7 +1371,12 @@ class _StepPlan:
                 if err != 0:
                     raise RuntimeError("kernel launch %s failed with %d" % (getattr(fn, "__name__", fn), err))
         # per-member losses gathered inside the step (graph) so a replay leaves one copy for loss_view
-        torch.index_select(self.be.loss, 0, self.slots_long, out=self.loss_sel)
+        if not self.eval:
+            torch.index_select(self.be.loss, 0, self.slots_long, out=self.loss_sel)
+
+    def run_eval(self):
+        assert self.eval
+        self._run_eager()
 
     def run(self, train=True):
         be = self.be

@@ -42,7 +42,7 @@ def _align(n: int, a: int = 64) -> int:
 
 class PopulationEngine:
     def __init__(self, arch, capacity: int, device, backend: str = "auto", compute_dtype=torch.bfloat16,
-                 optimizer_impl: str = "auto"):
+                 optimizer_impl: str = "auto", loss_scale: float = 1.0):
         self.arch = arch
         self.capacity = int(capacity)
         self.device = torch.device(device)
@@ -60,6 +60,7 @@ class PopulationEngine:
         self.compute_dtype = compute_dtype
         if self.device.type == "cpu" and compute_dtype == torch.bfloat16:
             self.compute_dtype = torch.float32
+        self.loss_scale = float(loss_scale)  # static loss scaling of the PyTorch path (fp16; resnet_run_loop.py:284)
         self.dp = None  # parallel.dataparallel.DPContext when a member is trained by a group of ranks
         self.backend = make_backend(self, backend)
         if optimizer_impl == "auto":
@@ -191,7 +192,18 @@ class PopulationEngine:
             self.grads.zero_()
 
     @torch.no_grad()
+    def evaluate_population(self, slots: Sequence[int], x: torch.Tensor, y: torch.Tensor) -> Dict[int, float]:
+        """Eval accuracy of every member in ``slots`` (moving BN statistics): one population-batched forward per
+        chunk on backends that have it (HIP), else member by member."""
+        slots = list(slots)
+        if hasattr(self.backend, "evaluate_population") and slots:
+            return self.backend.evaluate_population(slots, x, y)
+        return {s: self.evaluate(s, x, y) for s in slots}
+
+    @torch.no_grad()
     def evaluate(self, slot: int, x: torch.Tensor, y: torch.Tensor, batch: int = 1000) -> float:
+        if hasattr(self.backend, "evaluate_population"):
+            return self.backend.evaluate_population([slot], x, y)[slot]
         correct = 0
         for i in range(0, x.shape[0], batch):
             logits = self.backend.infer(slot, x[i:i + batch])
@@ -227,7 +239,11 @@ class TorchBackend:
             p = e.params[s].detach().clone().requires_grad_(True)
             logits = e.arch.forward(p, e.running[s], x, training=True, dtype=e.compute_dtype)
             loss = F.cross_entropy(logits.float(), y.long())
-            g, = torch.autograd.grad(loss, p)
+            if e.loss_scale != 1.0:
+                g, = torch.autograd.grad(loss * e.loss_scale, p)
+                g = g / e.loss_scale
+            else:
+                g, = torch.autograd.grad(loss, p)
             e.grads[s, :e.P].copy_(g)
             losses.append(loss.detach())
         return torch.stack(losses) if losses else torch.zeros(0, device=e.device)
@@ -239,7 +255,10 @@ class TorchBackend:
 
 def make_backend(engine: PopulationEngine, name: str):
     if name == "auto":
-        name = "hip" if (engine.device.type == "cuda" and getattr(engine.arch, "hip_supported", False)) else "torch"
+        name = "hip" if (engine.device.type == "cuda" and getattr(engine.arch, "hip_supported", False)
+                         and engine.compute_dtype == torch.bfloat16) else "torch"
+    if name == "hip" and engine.compute_dtype != torch.bfloat16:
+        raise ValueError("the HIP kernels compute in bf16 (got %s): use the torch backend" % engine.compute_dtype)
     if name == "torch":
         return TorchBackend(engine)
     if name == "hip":

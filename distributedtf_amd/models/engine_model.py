@@ -22,12 +22,44 @@ import torch.nn.functional as F
 from .model_base import ModelBase
 from ..data import datasets
 from ..engine.population import PopulationEngine
+from ..utils.profiling import timed_phase
 
 
 def default_device():
     if torch.cuda.is_available():
         return torch.device("cuda", torch.cuda.current_device())
     return torch.device("cpu")
+
+
+class _LazyValues(dict):
+    """Hook values: host scalars up front, device-derived ones (``cross_entropy``, ``train_accuracy``: one
+    readback) only when a hook asks for them."""
+
+    def __init__(self, fetch, base):
+        super().__init__(base)
+        self._fetch = fetch
+
+    def _device(self):
+        if not dict.__contains__(self, "cross_entropy"):
+            h = self._fetch()
+            dict.__setitem__(self, "cross_entropy", h["ce"])
+            if h.get("acc") is not None:
+                dict.__setitem__(self, "train_accuracy", h["acc"])
+
+    def __missing__(self, key):
+        if key in ("cross_entropy", "train_accuracy"):
+            self._device()
+            if dict.__contains__(self, key):
+                return dict.__getitem__(self, key)
+        raise KeyError(key)
+
+    def __contains__(self, key):
+        if key in ("cross_entropy", "train_accuracy"):
+            self._device()
+        return dict.__contains__(self, key)
+
+    def get(self, key, default=None):
+        return self[key] if key in self else default
 
 
 class EngineModel(ModelBase):
@@ -53,8 +85,16 @@ class EngineModel(ModelBase):
     # ------------------------------------------------------------------------
     def __init__(self, cluster_id, hparams, save_base_dir, seed=None, device=None, backend="auto",
                  capacity=8, use_synthetic_data=None, data_dir=None, max_train_steps=None,
-                 checkpoint_every_round=True, eval_every_round=True, dp=None, tf_checkpoint=False, **kw):
+                 checkpoint_every_round=True, eval_every_round=True, dp=None, tf_checkpoint=False, ready_steps=None,
+                 stop_threshold=None, batch_size=None, dtype="bf16", loss_scale=1.0, **kw):
         super().__init__(cluster_id, hparams, save_base_dir, seed=seed)
+        from ..utils.flags import get_dtype
+        self.compute_dtype = get_dtype(dtype)  # --dtype: bf16 (HIP kernels) | fp32 / fp16 (PyTorch backend)
+        self.loss_scale = float(loss_scale or 1.0)
+        self.ready_steps = int(ready_steps) if ready_steps else None  # PBT ready interval in steps (--ready_steps)
+        self.stop_threshold = stop_threshold  # --stop_threshold: end a member's train call once eval passes it
+        self.batch_size_override = int(batch_size) if batch_size else None  # --batch_size
+        self._pin_batch_size()
         self.dp = dp  # parallel.dataparallel.DPContext: this member is one replica of a data-parallel group
         self.options = dict(kw)
         self.device = torch.device(device) if device is not None else default_device()
@@ -65,7 +105,7 @@ class EngineModel(ModelBase):
         self.tf_checkpoint = tf_checkpoint  # also export the reference's TF tensor-bundle format every round
         self.eval_every_round = eval_every_round
         self.arch = self.make_arch()
-        key = (type(self).__name__, str(self.device), self.arch.name, backend)
+        key = (type(self).__name__, str(self.device), self.arch.name, backend, self.compute_dtype, self.loss_scale)
         eng = EngineModel._engines.get(key)
         if eng is None or not eng.free_slots:
             eng = self._grow_or_create(key, eng, capacity, backend)
@@ -79,10 +119,11 @@ class EngineModel(ModelBase):
         self.images_trained = 0
 
     def _grow_or_create(self, key, eng, capacity, backend):
+        kw = dict(backend=backend, compute_dtype=self.compute_dtype, loss_scale=self.loss_scale)
         if eng is None:
-            eng = PopulationEngine(self.arch, capacity, self.device, backend=backend)
+            eng = PopulationEngine(self.arch, capacity, self.device, **kw)
         else:
-            new = PopulationEngine(self.arch, eng.capacity * 2, self.device, backend=backend)
+            new = PopulationEngine(self.arch, eng.capacity * 2, self.device, **kw)
             new.state[:eng.capacity].copy_(eng.state)
             new.members = dict(eng.members)
             new.free_slots = [s for s in range(new.capacity) if s not in new.members]
@@ -165,8 +206,17 @@ class EngineModel(ModelBase):
     def global_step(self) -> int:
         return self.engine.host_step[self.slot]
 
+    def _pin_batch_size(self):
+        if self.batch_size_override:
+            self.hparams["batch_size"] = self.batch_size_override
+
     def set_values(self, values):
         super().set_values(values)
+        self._pin_batch_size()
+
+    def perturb_hparams(self):
+        super().perturb_hparams()
+        self._pin_batch_size()  # --batch_size fixes every member's batch (explore would move it)
 
     # ------------------------------------------------------------- training
     @property
@@ -194,13 +244,50 @@ class EngineModel(ModelBase):
         return ds.batch(idx, gen)
 
     def n_steps(self, num_epoch: int) -> int:
+        """Steps of one ``train`` call: ``ready_steps`` when set (a fixed PBT ready interval in steps), else
+        ``num_epoch`` epochs capped by ``max_train_steps``."""
+        if self.ready_steps:
+            return int(self.ready_steps)
         n = num_epoch * self.steps_per_epoch()
         if self.max_train_steps:
             n = min(n, int(self.max_train_steps))
         return max(1, n)
 
+    def cycle_steps(self, num_epoch: int) -> List[int]:
+        """Steps of each train -> eval cycle of one call.  The reference evaluates (and appends a CSV row, checks
+        the stop threshold) after every epoch (``resnet_run_loop.py:446-508``, ``mnist_model.py:161-172``);
+        with ``ready_steps`` the whole call is one cycle."""
+        total = self.n_steps(num_epoch)
+        if self.ready_steps or num_epoch <= 1:
+            return [total]
+        spe = self.steps_per_epoch()
+        out = []
+        for _ in range(num_epoch):
+            n = min(spe, total - sum(out))
+            out.append(max(0, n))
+        return out
+
+    @classmethod
+    def _hooks(cls, eng, m):
+        """Training hooks of this engine's population (``--hooks``; reference hooks_helper.get_train_hooks,
+        resnet_run_loop.py:423-426), created once and kept across rounds."""
+        hs = getattr(eng, "train_hooks", None)
+        if hs is None:
+            from ..utils.hooks import get_train_hooks
+            names = m.options.get("hooks") or ""
+            n = int(m.options.get("hook_every_n") or 100)
+            hs = get_train_hooks(names, batch_size=int(m.hparams["batch_size"]), every_n_iter=n, every_n_steps=n,
+                                 every_n_secs_steps=n, warm_steps=min(5, n),
+                                 model_dir=m.options.get("model_dir") or os.path.dirname(m.save_dir) or ".")
+            for h in hs:
+                h.begin()
+            eng.train_hooks = hs
+            eng.hook_step = 0
+        return hs
+
     @classmethod
     def train_population(cls, members: List["EngineModel"], num_epoch: int, total_epochs: int):
+        from ..utils.model_helpers import past_stop_threshold
         failed = {}
         groups: Dict[int, List[EngineModel]] = {}
         for m in members:
@@ -213,10 +300,47 @@ class EngineModel(ModelBase):
                 gen = torch.Generator(device=ds.device)
                 # replicas of a data-parallel group draw different shards (the member rng stays in lockstep)
                 gen.manual_seed(int(ms[0].rng.random() * 1e9) + (7919 * ms[0].dp.rank if ms[0].dp else 0))
-            todo = {m.slot: m.n_steps(num_epoch) for m in ms}
+            hooks = cls._hooks(eng, ms[0])
+            plan = {m.slot: m.cycle_steps(num_epoch) for m in ms}
             by_slot = {m.slot: m for m in ms}
-            done = 0
-            loss_acc = {m.slot: None for m in ms}
+            live = list(ms)  # members still training in this call (NaN / stop threshold end a member's call)
+            for cycle in range(max(len(v) for v in plan.values())):
+                todo = {m.slot: plan[m.slot][cycle] for m in live if cycle < len(plan[m.slot])}
+                cyc = [by_slot[s] for s in todo]
+                if not cyc:
+                    break
+                cls._train_cycle(eng, ds, gen, by_slot, todo, hooks)
+                # eval of every finite member of this engine together (one batched forward per chunk)
+                ev = [m for m in cyc if m.eval_every_round and math.isfinite(m.last_loss)]
+                accs = {}
+                if ev:
+                    with timed_phase("eval"):
+                        x, y = ms[0].dataset().eval_set()
+                        accs = eng.evaluate_population([m.slot for m in ev], x, y)
+                for m in cyc:
+                    try:
+                        m.end_cycle(accs.get(m.slot))
+                    except Exception as e:  # member-level culling
+                        failed[m.cluster_id] = e
+                live = [m for m in cyc if m.cluster_id not in failed and math.isfinite(m.accuracy)
+                        and not past_stop_threshold(m.stop_threshold, m.accuracy)]
+            for m in ms:
+                if m.cluster_id in failed:
+                    continue
+                try:
+                    m.finish_round(num_epoch)
+                except Exception as e:  # member-level culling
+                    failed[m.cluster_id] = e
+        return failed
+
+    @classmethod
+    def _train_cycle(cls, eng, ds, gen, by_slot, todo, hooks):
+        """``todo[slot]`` population steps of every listed member (members drop out of the active set when their
+        count is reached), then one readback of the members' last losses."""
+        done = 0
+        loss_acc = {s: None for s in todo}
+        ms = [by_slot[s] for s in todo]
+        with timed_phase("train_steps"):
             while True:
                 active = [s for s in sorted(todo) if todo[s] > done]
                 if not active:
@@ -225,11 +349,16 @@ class EngineModel(ModelBase):
                 hps = [by_slot[s].hparams for s in active]
                 lrs = [by_slot[s].learning_rate(eng.host_step[s]) for s in active]
                 losses = eng.train_step(active, batches, hps, lrs)
+                n_img = 0
                 for i, s in enumerate(active):
-                    by_slot[s].images_trained += datasets.batch_len(batches[i])
-                for i, s in enumerate(active):
+                    b = datasets.batch_len(batches[i])
+                    by_slot[s].images_trained += b
+                    n_img += b
                     loss_acc[s] = losses[i]  # view, no host sync
                 done += 1
+                if hooks:
+                    eng.hook_step += 1
+                    cls._run_hooks(eng, hooks, [by_slot[s] for s in active], losses, lrs, n_img)
             dp = ms[0].dp
             if dp is not None:
                 # same NaN verdict and the same BatchNorm running statistics on every replica
@@ -239,27 +368,60 @@ class EngineModel(ModelBase):
                         t = loss_acc[m.slot].detach().float().reshape(1).clone()
                         dp.allreduce_mean_(t)
                         loss_acc[m.slot] = t[0]
-            for m in ms:
-                try:
-                    if loss_acc[m.slot] is not None:
-                        m.last_loss = float(loss_acc[m.slot].item())
-                    m.finish_round(num_epoch)
-                except Exception as e:  # member-level culling
-                    failed[m.cluster_id] = e
-        return failed
+            present = [m for m in ms if loss_acc[m.slot] is not None]
+            if present:
+                # every member's last loss in one readback (also where the host waits for the queued steps)
+                vals = torch.stack([loss_acc[m.slot].float().reshape(()) for m in present]).cpu().tolist()
+                for m, v in zip(present, vals):
+                    m.last_loss = float(v)
 
-    def finish_round(self, num_epoch):
+    @staticmethod
+    def _run_hooks(eng, hooks, active, losses, lrs, n_img):
+        """Drive the step hooks; device values (cross entropy, train accuracy) are read back only when a hook
+        wants this step (the reference's LoggingTensorHook every 100 steps)."""
+        step = eng.hook_step
+        due = [h for h in hooks if h.wants(step)]
+        if not due:
+            return
+        host = {}
+
+        def device_values():
+            if not host:
+                host["ce"] = losses.float().cpu().tolist()
+                corr = getattr(eng.backend, "train_correct", None)
+                c = corr([m.slot for m in active]) if corr is not None else None
+                host["acc"] = None if c is None else [float(v) / max(1, int(m.hparams["batch_size"]))
+                                                      for v, m in zip(c.cpu().tolist(), active)]
+            return host
+
+        values = _LazyValues(device_values, {"images": n_img, "model_ids": [m.cluster_id for m in active],
+                                             "learning_rate": list(lrs), "sync": eng.device.type == "cuda"})
+        for h in due:
+            h.after_step(step, values)
+
+    def end_cycle(self, accuracy=None):
+        """After one train -> eval cycle: accuracy, benchmark-logger eval record, a ``learning_curve.csv`` row."""
         if math.isnan(self.last_loss) or math.isinf(self.last_loss):
             self.accuracy = float("nan")
+        elif accuracy is not None:
+            self.accuracy = accuracy
         elif self.eval_every_round:
             x, y = self.dataset().eval_set()
             self.accuracy = self.engine.evaluate(self.slot, x, y)
+        if not self.is_dp_follower:
+            from ..utils.logger import get_benchmark_logger
+            get_benchmark_logger().log_evaluation_result(
+                {"accuracy": float(self.accuracy), "loss": float(self.last_loss), "global_step": int(self.global_step),
+                 "model_id": int(self.cluster_id)})
         self.write_learning_curve(self.accuracy)
+
+    def finish_round(self, num_epoch):
         self.epoches_trained += num_epoch
         if self.checkpoint_every_round:
-            self.save_checkpoint()
-            if self.tf_checkpoint and not self.is_dp_follower:
-                self.export_tf_checkpoint()
+            with timed_phase("checkpoint"):
+                self.save_checkpoint()
+                if self.tf_checkpoint and not self.is_dp_follower:
+                    self.export_tf_checkpoint()
 
     def train(self, num_epoch, total_epochs):
         failed = type(self).train_population([self], num_epoch, total_epochs)

@@ -101,16 +101,26 @@ class ModelBase(object):
     def state_device(self):
         return self.export_state().device
 
+    # PBT round whose state the next checkpoint holds (set by the round loop); None: untagged
+    ckpt_round: Optional[int] = None
+    # the TF tensor bundle (``--tf_checkpoint``) owns the ``checkpoint`` state file when set
+    tf_checkpoint = False
+
     def save_checkpoint(self, wait: bool = False) -> None:
         """Write ``savedata/model_<id>/model.ckpt`` (+ ``checkpoint`` state file).
 
+        With a round tag (``ckpt_round``) the file is ``model.ckpt-r<round>`` and ``model.ckpt`` is a hard link to
+        it; the last two rounds are kept, so a whole-run resume can load exactly the round the population table
+        names even when a crash left some members one round ahead (``load_checkpoint(round_tag=...)``).
         The state leaves the GPU through one device->host copy into a pinned buffer (ordered on the current
         stream, so training can continue immediately); serialisation and the file write run on the background
         ``CheckpointWriter`` thread.  ``wait=True`` (or ``flush_checkpoints()``) blocks
         until the file is on disk."""
         d = self.ensure_save_dir()
-        blob = {"epoches_trained": self.epoches_trained, "hparams": copy.deepcopy(self.hparams)}
-        CheckpointWriter.get().submit(self.export_state().detach(), blob, d)
+        blob = {"epoches_trained": self.epoches_trained, "hparams": copy.deepcopy(self.hparams),
+                "round": self.ckpt_round}
+        CheckpointWriter.get().submit(self.export_state().detach(), blob, d, tag=self.ckpt_round,
+                                      state_file=not self.tf_checkpoint)
         if wait:
             flush_checkpoints()
 
@@ -138,10 +148,12 @@ class ModelBase(object):
         flush_checkpoints()
         return os.path.isfile(os.path.join(self.save_dir, "model.ckpt"))
 
-    def load_checkpoint(self) -> bool:
+    def load_checkpoint(self, round_tag: Optional[int] = None) -> bool:
+        """Load ``model.ckpt`` (latest) or, with ``round_tag``, exactly ``model.ckpt-r<round_tag>``."""
         import torch
         flush_checkpoints()  # a pending write of this member must land first
-        path = os.path.join(self.save_dir, "model.ckpt")
+        name = "model.ckpt" if round_tag is None else "model.ckpt-r%d" % int(round_tag)
+        path = os.path.join(self.save_dir, name)
         if not os.path.isfile(path):
             return False
         blob = torch.load(path, map_location="cpu", weights_only=True)
@@ -173,7 +185,8 @@ class CheckpointWriter:
                 cls._inst = CheckpointWriter()
             return cls._inst
 
-    def submit(self, state, blob: Dict[str, Any], directory: str) -> None:
+    def submit(self, state, blob: Dict[str, Any], directory: str, tag: Optional[int] = None,
+               state_file: bool = True) -> None:
         import torch
         if state.is_cuda:
             host = torch.empty(state.shape, dtype=state.dtype, pin_memory=True)
@@ -182,23 +195,47 @@ class CheckpointWriter:
             ev.record()
         else:
             host, ev = state.clone(), None
-        self.q.put((host, ev, blob, os.path.abspath(directory)))  # the cwd may change before the write
+        # the cwd may change before the write: absolute directory
+        self.q.put((host, ev, blob, os.path.abspath(directory), tag, state_file))
+
+    @staticmethod
+    def _write(host, blob, d, tag, state_file):
+        import torch
+        blob = dict(blob)
+        blob["state"] = host
+        tmp = os.path.join(d, "model.ckpt.tmp")
+        torch.save(blob, tmp)
+        latest = os.path.join(d, "model.ckpt")
+        if tag is None:
+            os.replace(tmp, latest)
+        else:
+            tagged = os.path.join(d, "model.ckpt-r%d" % int(tag))
+            os.replace(tmp, tagged)
+            link = os.path.join(d, "model.ckpt.lnk")
+            try:
+                if os.path.lexists(link):
+                    os.remove(link)
+                os.link(tagged, link)
+            except OSError:  # no hard links on this filesystem: copy
+                import shutil
+                shutil.copyfile(tagged, link)
+            os.replace(link, latest)
+            for f in os.listdir(d):  # keep this round and the previous one
+                if f.startswith("model.ckpt-r") and f[len("model.ckpt-r"):].isdigit() \
+                        and int(f[len("model.ckpt-r"):]) < int(tag) - 1:
+                    os.remove(os.path.join(d, f))
+        if state_file:
+            with open(os.path.join(d, "checkpoint"), "w") as f:
+                f.write('model_checkpoint_path: "model.ckpt"\n')
 
     def _run(self):
-        import torch
         while True:
             item = self.q.get()
             try:
-                host, ev, blob, d = item
+                host, ev, blob, d, tag, state_file = item
                 if ev is not None:
                     ev.synchronize()
-                blob = dict(blob)
-                blob["state"] = host
-                tmp = os.path.join(d, "model.ckpt.tmp")
-                torch.save(blob, tmp)
-                os.replace(tmp, os.path.join(d, "model.ckpt"))
-                with open(os.path.join(d, "checkpoint"), "w") as f:
-                    f.write('model_checkpoint_path: "model.ckpt"\n')
+                self._write(host, blob, d, tag, state_file)
             except BaseException as e:  # surfaced by flush()
                 self.error = e
             finally:

@@ -138,6 +138,33 @@ __global__ __launch_bounds__(64) void bn_running_update_kernel(float* __restrict
   run[C + c] = BN_MOM * run[C + c] + (1.f - BN_MOM) * unbiased;
 }
 
+// Eval mode: BatchNorm with the moving statistics.  Every consumer derives its coefficients from replicated
+// (sum, sum of squares) accumulators and the per-member count n = cnt * hw, so the moving mean / variance are
+// written in that form (replica 0: n*mean, n*(var + mean^2); replicas 1.. zero) and the training kernels
+// normalise with them unchanged.  Relative error of the recovered variance ~ 1e-7 * mean^2 / var (fp32).
+__global__ __launch_bounds__(64) void bn_eval_stats_kernel(const float* __restrict__ state, long s_mstride,
+                                                            long run_base, const int* __restrict__ table,
+                                                            float* __restrict__ stats, long stats_bn_stride,
+                                                            const int* __restrict__ slots,
+                                                            const float* __restrict__ cnt) {
+  const int* t = table + blockIdx.x * 8;
+  const int slot = slots[blockIdx.y];
+  const int c = threadIdx.x;
+  const int C = t[1];
+  float* row = stats + (long)t[3] * stats_bn_stride + (long)slot * NREP * 128;
+  if (c >= C) return;
+  const float* run = state + (long)slot * s_mstride + run_base + t[0];
+  const float n = cnt[slot] * (float)t[2];
+  const float mean = run[c], var = run[C + c];
+  row[c] = n * mean;
+  row[64 + c] = n * (var + mean * mean);
+#pragma unroll
+  for (int r = 1; r < NREP; ++r) {
+    row[r * 128 + c] = 0.f;
+    row[r * 128 + 64 + c] = 0.f;
+  }
+}
+
 struct BnBwdArgs {
   const bf16_t* dz;
   const bf16_t* x;
@@ -595,6 +622,15 @@ DTF_API int dtf_bn_running_update(float* state, long s_mstride, long run_base, c
   if (nbn <= 0 || nslots <= 0) return 0;
   hipLaunchKernelGGL(bn_running_update_kernel, dim3(nbn, nslots), dim3(64), 0, stream, state, s_mstride, run_base,
                      table, stats, stats_bn_stride, slots, cnt, grads, g_mstride);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_bn_eval_stats(const float* state, long s_mstride, long run_base, const int* table, int nbn,
+                              float* stats, long stats_bn_stride, const int* slots, int nslots, const float* cnt,
+                              hipStream_t stream) {
+  if (nbn <= 0 || nslots <= 0) return 0;
+  hipLaunchKernelGGL(bn_eval_stats_kernel, dim3(nbn, nslots), dim3(64), 0, stream, state, s_mstride, run_base, table,
+                     stats, stats_bn_stride, slots, cnt);
   return DTF_CHECK_LAUNCH();
 }
 

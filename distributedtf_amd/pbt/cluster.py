@@ -99,6 +99,24 @@ class _ReportMixin:
         print("Saving best model to {}".format(path))
         return rep
 
+    def export_best_model(self, export_dir):
+        """``--export_dir`` in master/worker mode: the master owns no member, so it exports the best member's
+        flushed checkpoint from the shared savedata (``model.ckpt`` + ``model.json`` metadata)."""
+        import json
+        import shutil
+        vals = self.get_all_values()
+        if not vals:
+            return None
+        best = reports.best_member(vals)
+        os.makedirs(export_dir, exist_ok=True)
+        src = os.path.join(self.savedata, "model_%d" % int(best[0]), "model.ckpt")
+        if os.path.isfile(src):
+            shutil.copyfile(src, os.path.join(export_dir, "model.ckpt"))
+        with open(os.path.join(export_dir, "model.json"), "w") as f:
+            json.dump({"model_id": int(best[0]), "accuracy": float(best[1]), "hparams": best[2]}, f, indent=2,
+                      sort_keys=True)
+        return export_dir
+
     def report_plot_for_toy_model(self):
         return reports.plot_toy(self.savedata, self.do_exploit, self.do_explore)
 
@@ -116,8 +134,9 @@ class PBTCluster(_ReportMixin):
     """Reference-compatible master (runs on ``master_rank`` only)."""
 
     def __init__(self, pop_size, comm, master_rank, epochs_per_round, do_exploit=True, do_explore=True,
-                 seed=None, exploit_transport="dataplane", savedata="savedata", hparams=None):
+                 seed=None, exploit_transport="dataplane", savedata="savedata", hparams=None, reseed_dead=False):
         self.pop_size = pop_size
+        self.reseed_dead = bool(reseed_dead)  # workers learn it with ADD_GRAPHS (keep NaN members for re-seeding)
         self.comm = comm
         self.master_rank = master_rank
         self.epochs_per_round = epochs_per_round
@@ -147,7 +166,8 @@ class PBTCluster(_ReportMixin):
         ws = self.workers()
         self.id_owner: Dict[int, int] = {}
         for r, (begin, cnt) in zip(ws, partition(self.pop_size, len(ws))):
-            self.comm.isend((WorkerInstruction.ADD_GRAPHS, hps[begin:begin + cnt], begin, explore_only), r).wait()
+            self.comm.isend((WorkerInstruction.ADD_GRAPHS, hps[begin:begin + cnt], begin, explore_only,
+                             self.reseed_dead), r).wait()
             for i in range(begin, begin + cnt):
                 self.id_owner[i] = r
 
@@ -284,6 +304,7 @@ class SPMDPopulation(_ReportMixin):
             self.initial_pop_size = int(state["population_size"])
             self.start_round = int(state["next_round"])
             rows = [(m["model_id"], m["accuracy"], m["hparams"], m["epoches_trained"]) for m in state["members"]]
+            csv_lines = {int(m["model_id"]): m.get("csv_lines", {}) for m in state["members"]}
         self.pop_size = len(rows)
         blocks = partition(self.initial_pop_size, self.n_groups)
         self.id_owner = {}  # member id -> member group (= rank when dp_size == 1)
@@ -295,11 +316,15 @@ class SPMDPopulation(_ReportMixin):
         self.worker.add_members([(r[0], copy.deepcopy(r[2])) for r in mine])
         if state is not None:
             by_id = self.worker.members_by_id()
+            tag = state.get("ckpt_round")  # exactly the round the table describes (members may be one ahead)
             for mid, acc, _, epochs in mine:
                 g = by_id[int(mid)]
-                if not g.load_checkpoint():
-                    raise RuntimeError("resume: member %d has no checkpoint in %s" % (mid, g.save_dir))
+                if not g.load_checkpoint(round_tag=tag):
+                    raise RuntimeError("resume: member %d has no checkpoint%s in %s"
+                                       % (mid, "" if tag is None else " of round %d" % tag, g.save_dir))
                 g.accuracy, g.epoches_trained = float(acc), int(epochs)
+                # drop learning-curve rows a crashed round appended after the table was written
+                reports.truncate_member_csvs(g.save_dir, csv_lines.get(int(mid), {}))
             self.log("Resumed %d members at round %d" % (len(rows), self.start_round))
         self.last_plan = []
 
@@ -361,14 +386,21 @@ class SPMDPopulation(_ReportMixin):
         """Append one JSON line per round to ``savedata/metrics.jsonl``: throughput (images/s of
         the whole job), per-phase times (train / exploit / explore, max over ranks), exploit data-plane bytes and
         latency, population accuracy summary."""
+        from ..utils.profiling import PHASES
         cur = self._counters()
         prev = getattr(self, "_prev_counters", None) or [0, 0.0, 0.0, 0.0, 0.0, 0]
         self._prev_counters = cur
         delta = [c - p for c, p in zip(cur, prev)]
-        parts = self.comm.allgather([delta, [float(v[1]) for v in self._values()]])
+        phases = PHASES.since(getattr(self, "_prev_phases", {}))
+        self._prev_phases = PHASES.snapshot()
+        parts = self.comm.allgather([delta, [float(v[1]) for v in self._values()], phases])
         if self.rank != 0:
             return
         d = [p[0] for p in parts]
+        phase_s = {}
+        for p in parts:  # member-level phases inside the round (train steps, eval, checkpoint, hooks): max over ranks
+            for k, v in p[2].items():
+                phase_s[k] = max(phase_s.get(k, 0.0), v)
         accs = [a for p in parts for a in p[1] if a == a]
         images = sum(x[0] for x in d)
         rec = {"round": rnd, "round_s": round_s, "images": images,
@@ -378,7 +410,7 @@ class SPMDPopulation(_ReportMixin):
                "exploit_transfers": int(max(x[5] for x in d)), "exploit_bytes": int(sum(x[3] for x in d)),
                "exploit_dataplane_s": max(x[4] for x in d), "population": len(accs),
                "best_acc": max(accs) if accs else None, "mean_acc": sum(accs) / len(accs) if accs else None,
-               "world_size": self.world}
+               "world_size": self.world, "phases_s": phase_s}
         self._prev_exploit = self.exploit_time
         import json
         os.makedirs(self.savedata, exist_ok=True)
@@ -392,12 +424,18 @@ class SPMDPopulation(_ReportMixin):
         for g in self.worker.worker_graphs:
             if g.cluster_id in dsts and getattr(g, "checkpoint_every_round", True):
                 g.save_checkpoint()
+                if getattr(g, "tf_checkpoint", False) and self.is_group_leader:
+                    # the reference's directory holds the winner's TF checkpoint after the copy: re-export the
+                    # bundle of the imported state and drop the loser's stale one
+                    reports.remove_tf_bundles(g.save_dir)
+                    g.export_tf_checkpoint()
         flush_checkpoints()  # every rank's checkpoints are on disk before the table that names them
-        rows = self.comm.allgather([[g.cluster_id, g.get_accuracy(), g.hparams, g.epoches_trained]
+        rows = self.comm.allgather([[g.cluster_id, g.get_accuracy(), g.hparams, g.epoches_trained,
+                                     reports.member_csv_lines(g.save_dir)]
                                     for g in self.worker.worker_graphs] if self.is_group_leader else [])
         if self.rank == 0:
             reports.write_population_state(self.savedata, next_round, self.initial_pop_size,
-                                           [r for part in rows for r in part])
+                                           [r for part in rows for r in part], ckpt_round=next_round - 1)
 
     def train(self, round_num):
         """Run rounds ``start_round .. round_num - 1`` (``start_round`` > 0 after a resume)."""
@@ -405,6 +443,8 @@ class SPMDPopulation(_ReportMixin):
         for rnd in range(self.start_round, round_num):
             t0 = time.time()
             self.log("\nRound {}".format(rnd))
+            for g in self.worker.worker_graphs:
+                g.ckpt_round = rnd  # checkpoints written in this round are tagged with it
             # roctx ranges (rocprofv3 --marker-trace, DTF_ROCTX=1) around the PBT phases
             with roctx_range("pbt/round%d/train" % rnd):
                 self.train_one_round(rnd, round_num)
@@ -452,6 +492,20 @@ class SPMDPopulation(_ReportMixin):
         vals = self.get_all_values()
         if self.rank == 0:
             return reports.write_best_model(vals, os.path.join(self.savedata, "best_model.json"))
+
+    def export_best_model(self, export_dir):
+        """``--export_dir`` (reference resnet_run_loop.py:510-514 SavedModel export): the rank that owns the best
+        member writes its inference weights + metadata (utils/export.export_member)."""
+        vals = self.get_all_values()
+        if not vals:
+            return None
+        best = int(reports.best_member(vals)[0])
+        g = self.worker.members_by_id().get(best)
+        if g is not None and self.is_group_leader:
+            from ..utils.export import export_member
+            export_member(g, export_dir)
+        self.comm.barrier()
+        return export_dir
 
     def kill_all_workers(self):
         self.comm.barrier()

@@ -16,7 +16,7 @@ from __future__ import annotations
 import csv
 import json
 import os
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -43,8 +43,13 @@ def dump_population_json(values: Sequence, filename: str) -> None:
         json.dump(report, fp, indent=4, sort_keys=True)
 
 
+def best_member(values: Sequence):
+    """The ``[id, acc, hparams]`` row best_model.json reports (last of the ascending ranking)."""
+    return _ranked(values)[-1]
+
+
 def write_best_model(values: Sequence, filename: str) -> Dict:
-    best = _ranked(values)[-1]
+    best = best_member(values)
     report = {"best_model_id": int(best[0]), "best_acc": float(best[1]), "best_hparams": best[2]}
     os.makedirs(os.path.dirname(filename) or ".", exist_ok=True)
     with open(filename, "w") as fp:
@@ -55,20 +60,61 @@ def write_best_model(values: Sequence, filename: str) -> Dict:
 POPULATION_STATE = "population_state.json"
 
 
-def write_population_state(savedata: str, next_round: int, population_size: int, rows: Sequence) -> str:
-    """Whole-run resume table (opt-in ``--resume``): the round to run next and,
-    per surviving member, ``[id, accuracy, hparams, epoches_trained]``.  Written atomically (tmp + rename) at the
-    end of every round, after the members' checkpoints."""
+def write_population_state(savedata: str, next_round: int, population_size: int, rows: Sequence,
+                           ckpt_round: Optional[int] = None) -> str:
+    """Whole-run resume table (opt-in ``--resume``): the round to run next, the round
+    tag of the member checkpoints it pairs with (``model.ckpt-r<ckpt_round>``) and, per surviving member,
+    ``[id, accuracy, hparams, epoches_trained(, csv line counts)]``.  Written atomically (tmp + rename) at the end
+    of every round, after the members' checkpoints."""
     path = os.path.join(savedata, POPULATION_STATE)
-    blob = {"next_round": int(next_round), "population_size": int(population_size),
-            "members": [{"model_id": int(r[0]), "accuracy": float(r[1]), "hparams": r[2],
-                         "epoches_trained": int(r[3])} for r in sorted(rows, key=lambda r: int(r[0]))]}
+    members = []
+    for r in sorted(rows, key=lambda r: int(r[0])):
+        m = {"model_id": int(r[0]), "accuracy": float(r[1]), "hparams": r[2], "epoches_trained": int(r[3])}
+        if len(r) > 4:
+            m["csv_lines"] = dict(r[4])
+        members.append(m)
+    blob = {"next_round": int(next_round), "population_size": int(population_size), "members": members}
+    if ckpt_round is not None:
+        blob["ckpt_round"] = int(ckpt_round)
     os.makedirs(savedata, exist_ok=True)
     tmp = path + ".tmp"
     with open(tmp, "w") as fp:
         json.dump(blob, fp, indent=2, sort_keys=True)
     os.replace(tmp, path)
     return path
+
+
+def member_csv_lines(save_dir: str) -> Dict[str, int]:
+    """Line count of every CSV in a member directory (learning_curve.csv, theta.csv)."""
+    out = {}
+    if os.path.isdir(save_dir):
+        for f in sorted(os.listdir(save_dir)):
+            if f.endswith(".csv"):
+                with open(os.path.join(save_dir, f)) as fp:
+                    out[f] = sum(1 for _ in fp)
+    return out
+
+
+def truncate_member_csvs(save_dir: str, lines: Dict[str, int]) -> None:
+    """Cut each CSV back to the line count recorded with the population table (resume after a crashed round)."""
+    for f, n in lines.items():
+        path = os.path.join(save_dir, f)
+        if not os.path.isfile(path):
+            continue
+        with open(path) as fp:
+            keep = fp.readlines()
+        if len(keep) > int(n):
+            with open(path, "w") as fp:
+                fp.writelines(keep[:int(n)])
+
+
+def remove_tf_bundles(save_dir: str) -> None:
+    """Delete the TF tensor bundles (``model.ckpt-<step>.index`` / ``.data-*``) of a member directory."""
+    if not os.path.isdir(save_dir):
+        return
+    for f in os.listdir(save_dir):
+        if f.startswith("model.ckpt-") and (f.endswith(".index") or ".data-" in f) and not f.startswith("model.ckpt-r"):
+            os.remove(os.path.join(save_dir, f))
 
 
 def read_population_state(savedata: str) -> Dict:

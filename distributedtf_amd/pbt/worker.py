@@ -50,9 +50,15 @@ class TrainingWorker:
             print(*a, flush=True)
 
     # ------------------------------------------------------ reference protocol
+    def _handle_add(self, d):
+        """(ADD_GRAPHS, hparams, begin[, explore_only[, reseed_dead]]) -- the trailing fields are extensions."""
+        if len(d) > 4:
+            self.reseed_dead = bool(d[4])
+        self.add_graphs(d[1], d[2], d[3] if len(d) > 3 else False)
+
     def main_loop(self):
         handlers = {
-            WorkerInstruction.ADD_GRAPHS: lambda d: self.add_graphs(d[1], d[2], d[3] if len(d) > 3 else False),
+            WorkerInstruction.ADD_GRAPHS: lambda d: self._handle_add(d),
             WorkerInstruction.TRAIN: lambda d: self.train(d[1], d[2]),
             WorkerInstruction.GET: lambda d: self.comm.send(self.get_all_values(), self.master_rank),
             WorkerInstruction.SET: lambda d: self._handle_set(d),

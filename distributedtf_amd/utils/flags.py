@@ -108,9 +108,21 @@ def build_parser(defaults: Optional[Dict[str, Any]] = None) -> argparse.Argument
     p.add_argument("--loss_scale", type=_positive, default=None)
     p.add_argument("--data_format", default="channels_last", choices=["channels_last"])
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
-    p.add_argument("--hooks", default="", help="comma list: logging,examples_per_second,profiler,metric")
-    p.add_argument("--stop_threshold", type=float, default=None)
-    p.add_argument("--export_dir", default=None)
+    p.add_argument("--hooks", default="",
+                   help="comma list of training hooks: logging (lr / cross_entropy / train_accuracy of every member "
+                        "every 100 steps), examples_per_second, profiler (torch.profiler chrome trace every 1000 "
+                        "steps into savedata/), metric (the logging values into the benchmark logger)")
+    p.add_argument("--log_every_n_steps", type=int, default=100,
+                   help="period of the logging / metric / examples_per_second hooks (reference: 100 steps)")
+    p.add_argument("--stop_threshold", type=float, default=None,
+                   help="a member's train call ends once its eval accuracy reaches this (resnet_run_loop.py:505)")
+    p.add_argument("--export_dir", default=None, help="export the best member's inference weights here at the end")
+    p.add_argument("--ready_steps", type=int, default=None,
+                   help="PBT ready interval in optimizer steps: every member trains exactly this many steps per round "
+                        "(instead of epochs_per_round epochs), so the population stays in lockstep")
+    p.add_argument("--benchmark_logger_type", default="BaseBenchmarkLogger",
+                   choices=["BaseBenchmarkLogger", "BenchmarkFileLogger"])
+    p.add_argument("--benchmark_log_dir", default=None, help="BenchmarkFileLogger: metric.log / benchmark_run.log")
     p.add_argument("--no_checkpoint", action="store_true")
     p.add_argument("--tf_checkpoint", action="store_true",
                    help="also write each member's checkpoint as a TF 1.x tensor bundle (model.ckpt-<step>.*)")
@@ -140,6 +152,17 @@ class MainArgs(argparse.Namespace):
             kw["tf_checkpoint"] = bool(getattr(self, "tf_checkpoint", False))
             if self.data_dir:
                 kw["data_dir"] = self.data_dir
+            kw["dtype"] = self.dtype
+            kw["loss_scale"] = get_loss_scale(self.dtype, self.loss_scale)
+            kw["hooks"] = self.hooks
+            kw["hook_every_n"] = self.log_every_n_steps
+            kw["model_dir"] = self.savedata
+            if self.stop_threshold is not None:
+                kw["stop_threshold"] = self.stop_threshold
+            if self.ready_steps:
+                kw["ready_steps"] = self.ready_steps
+            if self.batch_size:
+                kw["batch_size"] = self.batch_size
         if self.model in ("cifar10", "imagenet"):
             if self.resnet_size:
                 kw["resnet_size"] = self.resnet_size
@@ -190,4 +213,15 @@ def parse_main_args(argv=None, defaults=None) -> MainArgs:
         args.population_size = args.pop_size
     if args.resnet_version == 1 and args.dtype == "fp16":
         p.error("ResNet version 1 is not currently supported with fp16. Please use version 2 instead.")
+    if args.dtype != "bf16" and args.model != "toy":
+        # the hand-written MI355X kernels compute in bf16 (fp32 master weights / statistics); fp32 and fp16 (static
+        # loss scaling) run on the PyTorch backend
+        if args.backend == "hip":
+            p.error("--dtype %s: the HIP kernels compute in bf16; use --backend torch (or auto)" % args.dtype)
+        args.backend = "torch"
+    elif args.loss_scale is not None and args.loss_scale != 1 and args.backend != "torch" and args.model != "toy":
+        p.error("--loss_scale applies to the fp16 / fp32 PyTorch path; bf16 needs no loss scaling "
+                "(pass --backend torch to scale anyway)")
+    if args.benchmark_logger_type == "BenchmarkFileLogger" and not args.benchmark_log_dir:
+        p.error("--benchmark_logger_type BenchmarkFileLogger needs --benchmark_log_dir")
     return args

@@ -54,6 +54,8 @@ class ExamplesPerSecondHook(StepHook):
         self.logger = metric_logger or get_benchmark_logger()
         self.total_steps = 0
         self.total_time = 0.0
+        self.total_images = 0
+        self._images = 0  # since the last report
         self._last_t = None
         self._last_step = None
         self.current = None
@@ -67,20 +69,32 @@ class ExamplesPerSecondHook(StepHook):
         self._last_step = 0
 
     def after_step(self, step, values=None):
+        """``values["images"]``: images of this step (a population step trains every active member's batch;
+        default ``batch_size``); ``values["sync"]``: drain the device before reading the clock on report steps
+        (steps are queued asynchronously, so host time alone would count queueing, not work)."""
+        values = values or {}
         if step <= self.warm_steps:
             self._last_t = time.perf_counter()
             self._last_step = step
+            self._images = 0
             return
+        self._images += int(values.get("images", self.batch_size))
+        nsteps = step - self._last_step
+        if self.every_n_steps and nsteps < self.every_n_steps:
+            return
+        if values.get("sync"):
+            import torch
+            torch.cuda.synchronize()
         now = time.perf_counter()
         elapsed = now - self._last_t
-        nsteps = step - self._last_step
-        due = (self.every_n_steps and nsteps >= self.every_n_steps) or (self.every_n_secs and elapsed >= self.every_n_secs)
-        if not due:
+        if not self.every_n_steps and elapsed < self.every_n_secs:
             return
         self.total_steps += nsteps
         self.total_time += elapsed
-        self.current = self.batch_size * nsteps / elapsed if elapsed > 0 else 0.0
-        self.average = self.batch_size * self.total_steps / self.total_time if self.total_time > 0 else 0.0
+        self.total_images += self._images
+        self.current = self._images / elapsed if elapsed > 0 else 0.0
+        self.average = self.total_images / self.total_time if self.total_time > 0 else 0.0
+        self._images = 0
         self.logger.log_metric("average_examples_per_sec", self.average, global_step=step)
         self.logger.log_metric("current_examples_per_sec", self.current, global_step=step)
         self._last_t, self._last_step = now, step
@@ -92,14 +106,21 @@ class LoggingHook(StepHook):
     def __init__(self, tensors=_TENSORS_TO_LOG, every_n_steps: int = 100, printer: Callable = None):
         self.tensors = tuple(tensors)
         self.every_n_steps = every_n_steps
-        self.printer = printer or (lambda s: log.info(s))
+        self.printer = printer or (lambda s: print(s, flush=True))
         self.records: List[Dict[str, Any]] = []
 
     def after_step(self, step, values):
         rec = {k: values[k] for k in self.tensors if k in values}
+        ids = values.get("model_ids")
         rec["step"] = step
         self.records.append(rec)
-        self.printer(", ".join("%s = %s" % (k, rec[k]) for k in rec))
+        if ids is None:
+            self.printer(", ".join("%s = %s" % (k, rec[k]) for k in rec))
+            return
+        # population step: one line per member (each value is a per-member list)
+        for i, mid in enumerate(ids):
+            self.printer("step = %d, model_id = %d, " % (step, mid) +
+                         ", ".join("%s = %.6g" % (k, rec[k][i]) for k in self.tensors if k in rec))
 
 
 class LoggingMetricHook(LoggingHook):
@@ -110,9 +131,16 @@ class LoggingMetricHook(LoggingHook):
         self.logger = metric_logger or get_benchmark_logger()
 
     def after_step(self, step, values):
+        ids = values.get("model_ids")
         for k in self.tensors:
-            if k in values:
-                self.logger.log_metric(k, float(values[k]), global_step=step)
+            if k not in values:
+                continue
+            v = values[k]
+            if ids is None:
+                self.logger.log_metric(k, float(v), global_step=step)
+            else:
+                for mid, x in zip(ids, v):
+                    self.logger.log_metric(k, float(x), global_step=step, extras={"model_id": mid})
 
 
 class ProfilerHook(StepHook):
@@ -156,7 +184,7 @@ class ProfilerHook(StepHook):
 
 
 def _logging(**kw):
-    return LoggingHook(every_n_steps=kw.get("every_n_iter", 100))
+    return LoggingHook(every_n_steps=kw.get("every_n_iter", 100), printer=kw.get("printer"))
 
 
 def _profiler(**kw):

@@ -109,6 +109,7 @@ class BaseBenchmarkLogger:
 
 class BenchmarkFileLogger(BaseBenchmarkLogger):
     def __init__(self, logging_dir: str):
+        logging_dir = os.path.abspath(logging_dir)  # the cwd may change during a run
         self._logging_dir = logging_dir
         os.makedirs(logging_dir, exist_ok=True)
         self._metric_path = os.path.join(logging_dir, METRIC_LOG_FILE_NAME)
@@ -168,6 +169,9 @@ def get_benchmark_logger():
 
 @contextlib.contextmanager
 def benchmark_context(flag_obj=None):
+    """Configure the process-wide logger for one run; the previous logger is restored afterwards."""
+    global _benchmark_logger
+    prev = _benchmark_logger
     bl = config_benchmark_logger(flag_obj)
     try:
         yield bl
@@ -175,3 +179,6 @@ def benchmark_context(flag_obj=None):
     except Exception:
         bl.on_finish(RUN_STATUS_FAILURE)
         raise
+    finally:
+        with _logger_lock:
+            _benchmark_logger = prev

@@ -64,6 +64,22 @@ class PhaseTimers:
     def summary(self):
         return {k: {"seconds": v, "calls": self.count[k]} for k, v in self.total.items()}
 
+    def snapshot(self):
+        return dict(self.total)
+
+    def since(self, snap):
+        """Seconds per phase accumulated after ``snapshot()`` returned ``snap``."""
+        return {k: v - snap.get(k, 0.0) for k, v in self.total.items() if v - snap.get(k, 0.0) > 0.0}
+
+
+# Process-wide phase timers of the member-level work inside a PBT round (train steps, eval, checkpoint writes,
+# hooks); the round loop reports their per-round deltas in metrics.jsonl.
+PHASES = PhaseTimers()
+
+
+def timed_phase(name: str):
+    return PHASES.phase(name)
+
 
 class GpuStepTimer:
     """Records a HIP event pair around each step; resolves lazily (no per-step sync)."""

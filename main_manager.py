@@ -67,7 +67,8 @@ def main(argv=None):
         if rank == master_rank:
             cluster = PBTCluster(args.population_size, comm, master_rank, epochs_per_round=args.epochs_per_round,
                                  do_exploit=args.do_exploit, do_explore=args.do_explore, seed=args.seed,
-                                 exploit_transport=args.exploit_transport, savedata=savedata)
+                                 exploit_transport=args.exploit_transport, savedata=savedata,
+                                 reseed_dead=args.reseed_dead)
         else:
             worker = TrainingWorker(comm, master_rank, cls, save_base_dir=os.path.join(savedata, "model_"),
                                     seed=args.seed, model_kwargs=model_kwargs, dataplane=DataPlane(comm))
@@ -79,21 +80,33 @@ def main(argv=None):
                                  savedata=savedata, model_kwargs=model_kwargs, inject_nan=inject,
                                  resume=args.resume, dp_size=args.dp_size, reseed_dead=args.reseed_dead)
 
-    if not args.resume or getattr(cluster, "start_round", 0) == 0:
-        cluster.dump_all_models_to_json(os.path.join(savedata, "initial_hp.json"))
-    elapsed = cluster.train(args.train_round)
-    if rank == master_rank:
-        reports.append_test_result(world, args.population_size, elapsed, args.results_file)
-    if rank == master_rank or args.mode != "master_worker":
+    from distributedtf_amd.utils import logger as bench_logger
+    # benchmark logger (reference logger.benchmark_context / log_run_info, cifar10_main.py:314-318,
+    # resnet_run_loop.py:408-421): rank 0 owns the files, other ranks log through python logging
+    log_flags = args if rank == master_rank else None
+    with bench_logger.benchmark_context(log_flags) as blog:
         if rank == master_rank:
-            if args.model == "toy":
-                cluster.report_plot_for_toy_model()
-            cluster.report_accuracy_plot()
-            cluster.report_lr_plot()
-            cluster.report_best3_plot()
-        cluster.report_best_model()
-        cluster.print_profiling_info()
-        cluster.kill_all_workers()
+            blog.log_run_info(args.model if args.model != "cifar10" else "resnet%s" % (args.resnet_size or 50),
+                              {"toy": "toy", "mnist": "mnist", "cifar10": "cifar10", "imagenet": "imagenet"}.get(
+                                  args.model, args.model),
+                              {k: v for k, v in vars(args).items() if not k.startswith("_")})
+        if not args.resume or getattr(cluster, "start_round", 0) == 0:
+            cluster.dump_all_models_to_json(os.path.join(savedata, "initial_hp.json"))
+        elapsed = cluster.train(args.train_round)
+        if rank == master_rank:
+            reports.append_test_result(world, args.population_size, elapsed, args.results_file)
+        if rank == master_rank or args.mode != "master_worker":
+            if rank == master_rank:
+                if args.model == "toy":
+                    cluster.report_plot_for_toy_model()
+                cluster.report_accuracy_plot()
+                cluster.report_lr_plot()
+                cluster.report_best3_plot()
+            cluster.report_best_model()
+            if args.export_dir:
+                cluster.export_best_model(args.export_dir)  # resnet_run_loop.py:510-514
+            cluster.print_profiling_info()
+            cluster.kill_all_workers()
     if world > 1:
         from distributedtf_amd.parallel.comm import shutdown_distributed
         shutdown_distributed()

@@ -16,7 +16,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, tmp, q):
+def _worker(rank, world, port, tmp, q, pop=4):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     os.chdir(tmp)
@@ -30,11 +30,11 @@ def _worker(rank, world, port, tmp, q):
         comm = init_distributed(backend="gloo")
         rng = random.Random(3)
         hps = []
-        for _ in range(4):
+        for _ in range(pop):
             h = generate_random_hparam(rng)
             h["batch_size"] = 4
             hps.append(h)
-        pop = SPMDPopulation(4, comm, Cifar10Model, epochs_per_round=1, seed=5, verbose=False, hparams=hps,
+        pop = SPMDPopulation(len(hps), comm, Cifar10Model, epochs_per_round=1, seed=5, verbose=False, hparams=hps,
                              model_kwargs=dict(resnet_size=8, max_train_steps=1, use_synthetic_data=True,
                                                device="cpu", eval_every_round=True))
         pop.train(1)
@@ -53,23 +53,26 @@ def _worker(rank, world, port, tmp, q):
         q.put((rank, "ERR", traceback.format_exc(), None))
 
 
-@pytest.mark.timeout(300)
-def test_spmd_gloo_world2_exploit_bit_exact(tmp_path):
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("world,pop", [(2, 4), (8, 8)])
+def test_spmd_gloo_exploit_bit_exact(tmp_path, world, pop):
+    """Every rank computes the same plan; cross-rank copies (batch_isend_irecv) leave loser == winner bit-exact.
+    world 8 / pop 8 is the headline layout (one member per rank, every exploit copy crosses ranks)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, str(tmp_path), q, pop)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=280) for _ in procs]
+    res = [q.get(timeout=380) for _ in procs]
     for p in procs:
         p.join(30)
     for r in res:
         assert r[1] != "ERR", r[2]
     plans = {r[0]: r[1] for r in res}
-    assert plans[0] == plans[1] and len(plans[0]) == 1
+    assert all(plans[k] == plans[0] for k in plans) and len(plans[0]) == -(-pop // 4)
     assert all(r[2] for r in res)
-    assert res[0][3] == [0, 1, 2, 3]
+    assert res[0][3] == list(range(pop))
 
 
 def _gather_worker(rank, world, port, q):

@@ -1,0 +1,96 @@
+"""Every main_manager flag reaches the training loop (CPU, PyTorch backend, ResNet-8 on synthetic data).
+
+Reference wiring: ``resnet_run_loop.py:419-426`` (run info + train hooks), ``:466`` (log_evaluation_result),
+``:469-503`` (one learning-curve row per eval cycle), ``:505-508`` (stop threshold), ``:510-514`` (export),
+``official/utils/logs/hooks_helper.py:33-35,97-132`` (hook registry).
+"""
+import csv
+import json
+import os
+
+import pytest
+
+import main_manager
+from distributedtf_amd.models.engine_model import EngineModel
+from distributedtf_amd.utils import logger as bench_logger
+
+BASE = ["2", "--model", "cifar10", "--resnet_size", "8", "--use_synthetic_data", "true", "--seed", "4",
+        "--backend", "torch"]
+
+
+def _run(tmp_path, monkeypatch, *extra):
+    monkeypatch.chdir(tmp_path)
+    EngineModel.reset_engines()
+    assert main_manager.main(BASE + list(extra)) == 0
+
+
+def _curves(sd="savedata"):
+    out = {}
+    for d in sorted(os.listdir(sd)):
+        p = os.path.join(sd, d, "learning_curve.csv")
+        if os.path.isfile(p):
+            out[d] = list(csv.DictReader(open(p)))
+    return out
+
+
+def test_hooks_logger_and_export(tmp_path, monkeypatch, capsys):
+    _run(tmp_path, monkeypatch, "--max_train_steps", "4", "--rounds", "2", "--hooks",
+         "logging,examples_per_second,metric", "--log_every_n_steps", "2", "--benchmark_logger_type",
+         "BenchmarkFileLogger", "--benchmark_log_dir", "bench_logs", "--export_dir", "exported")
+    out = capsys.readouterr().out
+    assert "cross_entropy" in out and "learning_rate" in out and "model_id" in out  # LoggingHook lines
+    metrics = [json.loads(l) for l in open("bench_logs/metric.log")]
+    names = {m["name"] for m in metrics}
+    assert {"accuracy", "loss", "average_examples_per_sec", "current_examples_per_sec", "cross_entropy"} <= names
+    acc = [m for m in metrics if m["name"] == "accuracy"]
+    assert len(acc) == 4  # 2 members x 2 rounds (log_evaluation_result per eval)
+    run = json.load(open("bench_logs/benchmark_run.log"))
+    assert run["status"] == "success" and run["model_name"] == "resnet8"
+    assert os.path.isfile("exported/model.safetensors")
+    meta = json.load(open("exported/model.json"))
+    best = json.load(open("savedata/best_model.json"))
+    assert meta["model_id"] == best["best_model_id"]
+
+
+def test_epoch_cycles_and_stop_threshold(tmp_path, monkeypatch):
+    """epochs_per_round 2 -> two train/eval cycles (two CSV rows) per round; a stop threshold every eval passes
+    ends each member's call after its first cycle."""
+    monkeypatch.setattr("distributedtf_amd.models.cifar10_model.Cifar10Model.steps_per_epoch", lambda self: 2)
+    _run(tmp_path, monkeypatch, "--rounds", "1", "--epochs_per_round", "2")
+    rows = _curves()
+    assert all(len(r) == 2 for r in rows.values()), rows
+    assert all(r[0]["epochs"] == r[1]["epochs"] == "0" for r in rows.values())  # epoch_index of the call
+    os.chdir(tmp_path)
+    import shutil
+    shutil.rmtree("savedata")
+    _run(tmp_path, monkeypatch, "--rounds", "1", "--epochs_per_round", "2", "--stop_threshold", "0.0")
+    rows = _curves()
+    assert all(len(r) == 1 for r in rows.values()), rows
+
+
+def test_ready_steps_and_batch_size(tmp_path, monkeypatch):
+    _run(tmp_path, monkeypatch, "--rounds", "2", "--ready_steps", "3", "--batch_size", "16")
+    recs = [json.loads(l) for l in open("savedata/metrics.jsonl")]
+    assert [r["images"] for r in recs] == [2 * 3 * 16, 2 * 3 * 16]  # explore cannot move the pinned batch
+    for r in _curves().values():
+        assert all(row["batch_size"] == "16" for row in r)
+
+
+def test_dtype_routing():
+    from distributedtf_amd.utils.flags import parse_main_args
+    a = parse_main_args(["--model", "cifar10", "--dtype", "fp32"])
+    assert a.backend == "torch" and a.model_kwargs()["dtype"] == "fp32"
+    with pytest.raises(SystemExit):
+        parse_main_args(["--model", "cifar10", "--dtype", "fp32", "--backend", "hip"])
+    with pytest.raises(SystemExit):
+        parse_main_args(["--model", "cifar10", "--loss_scale", "8"])  # bf16 HIP path: no loss scaling
+    a = parse_main_args(["--model", "cifar10", "--dtype", "fp16"])
+    assert a.backend == "torch" and a.model_kwargs()["loss_scale"] == 128
+    with pytest.raises(SystemExit):
+        parse_main_args(["--benchmark_logger_type", "BenchmarkFileLogger"])
+
+
+def test_fp16_loss_scaled_training_is_finite(tmp_path, monkeypatch):
+    _run(tmp_path, monkeypatch, "--rounds", "1", "--max_train_steps", "2", "--dtype", "fp32", "--loss_scale", "64")
+    best = json.load(open("savedata/best_model.json"))
+    assert best["best_acc"] == best["best_acc"]

@@ -69,3 +69,38 @@ def test_round_metrics_jsonl(tmp_cwd):
         assert r["population"] == 6 and r["world_size"] == 2
         assert r["exploit_transfers"] == 2  # ceil(6/4) = 2 bottom members per round
         assert r["exploit_bytes"] > 0 and r["round_s"] > 0
+
+
+def test_resume_after_crash_between_checkpoints_and_table(tmp_cwd):
+    """members finish round r+1 (checkpoints + learning-curve rows written) but the job dies before the
+    population table of round r+1 is written.  Resume must load exactly the round-r checkpoints the table pairs
+    with (round-tagged files) and drop the crashed round's CSV rows -- no extra round of training, no duplicate
+    learning-curve rows."""
+    first = {}
+    _run(1, 2, False, first)
+    assert os.path.isfile("savedata/model_0/model.ckpt-r1")
+
+    def crash(self, next_round):
+        raise RuntimeError("simulated crash before the round-%d table" % next_round)
+
+    orig = SPMDPopulation.save_round_state
+    SPMDPopulation.save_round_state = crash
+    try:
+        with pytest.raises(RuntimeError):
+            comms = LocalComm.create(1)
+            pop = SPMDPopulation(6, comms[0], ToyModel, epochs_per_round=2, seed=5, verbose=False, resume=True)
+            pop.train(3)
+    finally:
+        SPMDPopulation.save_round_state = orig
+    from distributedtf_amd.models.model_base import flush_checkpoints
+    flush_checkpoints()
+    assert os.path.isfile("savedata/model_0/model.ckpt-r2")  # the crashed round's checkpoints exist ...
+    assert len(open("savedata/model_0/learning_curve.csv").read().strip().splitlines()) == 1 + 6
+    second = {}
+    _run(1, 5, True, second)  # ... but the resume pairs the table (round 2 next) with the round-1 files
+    assert set(second["start"].values()) == {2}
+    assert set(second["steps"].values()) == {10}
+    assert set(second["epochs"].values()) == {10}
+    rows = open("savedata/model_0/learning_curve.csv").read().strip().splitlines()
+    assert len(rows) == 1 + 10
+    assert not os.path.exists("savedata/model_0/model.ckpt-r2")  # only the last two round tags are kept

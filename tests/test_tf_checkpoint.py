@@ -88,3 +88,33 @@ def test_tf_checkpoint_round_trip_into_member(tmp_cwd, opt):
     n = b.import_tf_checkpoint(prefix)
     assert n > 0 and b.global_step == 3
     torch.testing.assert_close(b.export_state(), a.export_state(), rtol=0, atol=0)
+
+
+def test_exploit_destination_gets_winner_tf_bundle(tmp_cwd):
+    """with --tf_checkpoint an exploit destination's directory must hold the WINNER's TF checkpoint
+    (the reference copies the files: pbt_cluster.py:145-147) -- the bundle is re-exported from the imported state,
+    the loser's stale bundle is removed, and the ``checkpoint`` state file names the new bundle."""
+    import glob as _glob
+    from distributedtf_amd.models.cifar10_model import Cifar10Model
+    from distributedtf_amd.models.engine_model import EngineModel
+    from distributedtf_amd.parallel.comm import SingleComm
+    from distributedtf_amd.pbt.cluster import SPMDPopulation
+    EngineModel.reset_engines()
+    hps = [dict(_hp("Momentum"), batch_size=4 + i) for i in range(4)]
+    pop = SPMDPopulation(4, SingleComm(), Cifar10Model, epochs_per_round=1, seed=3, verbose=False, hparams=hps,
+                         model_kwargs=dict(resnet_size=8, device="cpu", backend="torch", use_synthetic_data=True,
+                                           max_train_steps=2 + 0, tf_checkpoint=True))
+    pop.train(1)
+    (p,) = pop.last_plan
+    members = pop.worker.members_by_id()
+    dst = members[p.dst_id]
+    bundles = _glob.glob(os.path.join(dst.save_dir, "model.ckpt-*.index"))
+    assert len(bundles) == 1, bundles
+    state = open(os.path.join(dst.save_dir, "checkpoint")).read()
+    step = members[p.src_id].global_step
+    assert 'model_checkpoint_path: "model.ckpt-%d"' % step in state
+    fresh = Cifar10Model(9, _hp("Momentum"), "savedata/model_", seed=7, resnet_size=8, device="cpu", backend="torch",
+                         use_synthetic_data=True)
+    fresh.import_tf_checkpoint(bundles[0][:-len(".index")])
+    torch.testing.assert_close(fresh.export_state(), dst.export_state(), rtol=0, atol=0)
+    torch.testing.assert_close(dst.export_state(), members[p.src_id].export_state(), rtol=0, atol=0)

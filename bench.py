@@ -47,6 +47,9 @@ def parse():
     p.add_argument("--seed", type=int, default=2024)
     p.add_argument("--graph", type=int, default=1, help="capture the population step in a HIP graph")
     p.add_argument("--profile_json", default=None)
+    p.add_argument("--ragged", action="store_true",
+                   help="keep the sampled per-member batch sizes (65..255) and let explore perturb them (real PBT: "
+                        "a new batch composition after every exploit); default pins every member to --batch")
     a = p.parse_args()
     if a.resnet_size is None:
         a.resnet_size = 50 if a.model == "imagenet" else 56
@@ -73,8 +76,9 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
 
     hps = sample_population(args.pop, args.seed)
-    for h in hps:
-        h["batch_size"] = args.batch
+    if not args.ragged:
+        for h in hps:
+            h["batch_size"] = args.batch
     begin, cnt = partition(args.pop, world)[rank]
     if args.model == "mnist":
         make = lambda i: MNISTModel(begin + i, hps[begin + i], "/tmp/bench_savedata_%d/model_" % rank,  # noqa: E731
@@ -100,11 +104,14 @@ def main():
 
     slots = [m.slot for m in members]
     batches = [ds.batch_slice(args.batch) for _ in members]
+    images_done = [0]
 
     def step():
         hp = [m.hparams for m in members]
         lrs = [m.learning_rate(eng.host_step[m.slot]) for m in members]
-        return eng.train_step(slots, batches, hp, lrs)
+        bt = batches if not args.ragged else [ds.batch_slice(int(m.hparams["batch_size"])) for m in members]
+        images_done[0] += sum(int(b[1].shape[0]) for b in bt)
+        return eng.train_step(slots, bt, hp, lrs)
 
     exploits = [0]
     exploit_s = []  # host wall time of each timed exploit/explore cycle (gather + plan + copy + perturb)
@@ -137,9 +144,11 @@ def main():
         for m in members:
             if m.cluster_id in upd:
                 m.set_values(upd[m.cluster_id])
-                m.hparams["batch_size"] = args.batch
+                if not args.ragged:
+                    m.hparams["batch_size"] = args.batch
                 m.perturb_hparams()
-                m.hparams["batch_size"] = args.batch
+                if not args.ragged:
+                    m.hparams["batch_size"] = args.batch
         exploits[0] += 1
         exploit_s.append(time.perf_counter() - tc)
 
@@ -158,6 +167,7 @@ def main():
         exploits[0] = 0
         exploit_s.clear()
     barrier_sync()
+    images_done[0] = 0
     t0 = time.perf_counter()
     pending = None
     for k in range(args.steps):
@@ -173,7 +183,8 @@ def main():
     dt = time.perf_counter() - t0
     dts = comm.allgather(dt)
     dt_max = max(dts)
-    images = args.pop * args.batch * args.steps
+    # images trained in the timed steps, summed over ranks (ragged: each member's own, changing batch size)
+    images = sum(comm.allgather(images_done[0]))
     value = images / dt_max
     if rank == 0:
         flops = members[0].arch.flops_per_image() * 3.0 * images / dt_max
@@ -193,8 +204,10 @@ def main():
             "dtype": "bf16",
             "data": "synthetic (device-resident random-normal %s, uniform labels), random-init weights"
                     % "x".join(str(d) for d in members[0].arch.input_shape),
-            "config": {"model": members[0].arch.name, "global_batch": args.pop * args.batch,
-                       "per_member_batch": args.batch, "population": args.pop, "seq_len": None,
+            "config": {"model": members[0].arch.name,
+                       "global_batch": args.pop * args.batch if not args.ragged else round(images / args.steps, 1),
+                       "per_member_batch": args.batch if not args.ragged else "sampled 65..255 (ragged)",
+                       "population": args.pop, "seq_len": None,
                        "parallelism": "pbt_pop%d_%dmembers_per_gpu" % (args.pop, cnt),
                        "backend": eng.backend.name, "exploit_every": args.exploit_every,
                        "exploits_timed": exploits[0]},

@@ -13,7 +13,8 @@ the epilogue; weight gradients are split-K implicit GEMMs (k = pixels) with atom
 Per-member BN coefficients (forward scale/shift/mean/inv, backward A/B/C) are finalised by tiny kernels
 between the convs (``convg_aux.hip``), which also update the running statistics / accumulate dgamma, dbeta.
 The dense layer is the grouped bf16 GEMM (gemm.hip) with softmax-CE in between.  The whole step is captured
-into one HIP graph per batch composition.  Eval uses the PyTorch reference forward.
+into one HIP graph per batch composition.  Eval (``evaluate_population``) runs the same forward kernels for every
+member at once with BN coefficients from the moving statistics.
 """
 
 from __future__ import annotations
@@ -186,15 +187,58 @@ class HipImageNetBackend:
     def forward_backward(self, slots, batches):
         raise RuntimeError("HipImageNetBackend runs whole steps: use train_step")
 
+    def train_correct(self, slots):
+        """Correct predictions of each member's last training batch (softmax-CE kernel count; device tensor)."""
+        return self.correct[torch.as_tensor(list(slots), dtype=torch.long, device=self.dev)]
+
+    def eval_plan(self, slots, m):
+        key = ("eval", tuple(slots), int(m))
+        p = self._plans.get(key)
+        if p is None:
+            if len(self._plans) > 4:
+                self._plans.clear()
+            p = _ImageNetPlan(self, list(slots), [int(m)] * len(slots), eval_mode=True)
+            self._plans[key] = p
+        return p
+
     @torch.no_grad()
     def infer(self, slot, x):
+        """Eval-mode logits of one member on the HIP forward kernels (moving BN statistics)."""
+        p = self.eval_plan([slot], int(x.shape[0]))
+        p.load_eval(x, torch.zeros(x.shape[0], dtype=torch.int32, device=x.device))
+        p.run_eval()
         e = self.e
-        return e.arch.forward(e.params[slot], e.running[slot], x, training=False, dtype=torch.bfloat16)
+        b = e.state[slot, self.prog.dense_b_off:self.prog.dense_b_off + self.ncls]
+        return p.logits[:, :self.ncls] + b
+
+    @torch.no_grad()
+    def evaluate_population(self, slots, x, y, chunk=None):
+        """Eval accuracy of every member in ``slots``: one population-batched forward per chunk of the eval set
+        (BN with moving statistics, the same convg / GAP / dense kernels as training); one host sync."""
+        n = int(x.shape[0])
+        if n == 0 or not slots:
+            return {s: 0.0 for s in slots}
+        chunk = min(n, int(chunk or os.environ.get("DTF_EVAL_CHUNK_IMAGENET", "64")))
+        used = []
+        for i in range(0, n, chunk):
+            m = min(chunk, n - i)
+            p = self.eval_plan(slots, m)
+            if all(p is not q for q in used):
+                p.ev_acc.zero_()
+                used.append(p)
+            p.load_eval(x[i:i + m], y[i:i + m])
+            p.run_eval()
+        correct = used[0].ev_acc[0].clone()
+        for p in used[1:]:
+            correct += p.ev_acc[0]
+        vals = correct.cpu().tolist()
+        return {s: vals[s] / float(n) for s in slots}
 
 
 class _ImageNetPlan:
-    def __init__(self, be: HipImageNetBackend, slots: List[int], sizes: List[int]):
+    def __init__(self, be: HipImageNetBackend, slots: List[int], sizes: List[int], eval_mode: bool = False):
         self.be, self.e = be, be.e
+        self.eval = bool(eval_mode)
         e, dev, prog, cfg = be.e, be.dev, be.prog, be.cfg
         self.slots, self.sizes = slots, sizes
         N = sum(sizes)
@@ -219,24 +263,41 @@ class _ImageNetPlan:
         self.xin8 = torch.zeros(N, H, H, 8, dtype=bf, device=dev)
         H1 = H // 2
         H2 = (H1 + 1) // 2
+        pool = {}
+
+        def act(kind, hw_, c_, i_=0, dtype=bf):
+            """Activation buffer; eval plans save nothing for a backward, so buffers are shared per shape (the
+            residual stream ping-pongs between two)."""
+            if not self.eval:
+                return torch.empty(N, hw_, hw_, c_, dtype=dtype, device=dev)
+            key = (kind, hw_, c_, i_ % 2 if kind == "x" else 0)
+            if key not in pool:
+                pool[key] = torch.empty(N, hw_, hw_, c_, dtype=dtype, device=dev)
+            return pool[key]
+
         self.y0 = torch.empty(N, H1, H1, cfg.num_filters, dtype=bf, device=dev)
         self.am0 = torch.empty(N, H2, H2, cfg.num_filters, dtype=torch.uint8, device=dev)
-        self.xs, self.h1, self.h2, self.sc = [torch.empty(N, H2, H2, cfg.num_filters, dtype=bf, device=dev)], [], [], []
+        self.xs, self.h1, self.h2, self.sc = [act("x", H2, cfg.num_filters, 0)], [], [], []
         # materialised BN+ReLU outputs (the operands every consumer conv stages as-is, and the weight-gradient
-        # inputs): ax = relu(BN1(x)), a1 = relu(BN2(h1)), a2 = relu(BN3(h2))
+        # inputs): ax = relu(BN1(x)), a1 = relu(BN2(h1)), a2 = relu(BN3(h2)) -- only without prologue folding
+        # (DTF_CG_FOLD=0) and in eval plans; folded, the consumers apply BN+ReLU / BN-backward while staging
+        # (off by default: folding measured slower, 114.7 -> 135.7 ms/step at pop 8 x 128 -- the transform is
+        # repeated for every output-channel tile and its coefficient LDS costs occupancy; profiles/r2_imagenet_fold_ab.log)
+        self.fold = (not self.eval) and os.environ.get("DTF_CG_FOLD", "0") == "1"
         self.ax, self.a1, self.a2 = [], [], []
         hw, cin = H2, cfg.num_filters
         self.geo = []  # per block: (H_in, H_out, cin, f, fout)
-        for blk in prog.blocks:
+        for bi, blk in enumerate(prog.blocks):
             c1, c2, c3 = (prog.convs[i] for i in blk.convs)
             ho = hw // blk.stride
-            self.h1.append(torch.empty(N, hw, hw, c1.cout, dtype=bf, device=dev))
-            self.h2.append(torch.empty(N, ho, ho, c2.cout, dtype=bf, device=dev))
-            self.ax.append(torch.empty(N, hw, hw, cin, dtype=bf, device=dev))
-            self.a1.append(torch.empty(N, hw, hw, c1.cout, dtype=bf, device=dev))
-            self.a2.append(torch.empty(N, ho, ho, c2.cout, dtype=bf, device=dev))
-            self.sc.append(torch.empty(N, ho, ho, c3.cout, dtype=bf, device=dev) if blk.proj is not None else None)
-            self.xs.append(torch.empty(N, ho, ho, c3.cout, dtype=bf, device=dev))
+            self.h1.append(act("h1", hw, c1.cout))
+            self.h2.append(act("h2", ho, c2.cout))
+            if not self.fold:
+                self.ax.append(act("ax", hw, cin))
+                self.a1.append(act("a1", hw, c1.cout))
+                self.a2.append(act("a2", ho, c2.cout))
+            self.sc.append(act("sc", ho, c3.cout) if blk.proj is not None else None)
+            self.xs.append(act("x", ho, c3.cout, bi + 1))
             self.geo.append((hw, ho, cin, c1.cout, c3.cout))
             hw, cin = ho, c3.cout
         self.HL = hw
@@ -247,7 +308,14 @@ class _ImageNetPlan:
         self._tmp: Dict[tuple, torch.Tensor] = {}
         self._keep = []
         self.launches = []
-        self._build()
+        if self.eval:
+            nb = len(prog.bns)
+            self.ev_coef = torch.zeros(nb, e.capacity, 4, CMAX, dtype=torch.float32, device=dev)
+            self.ev_sink = torch.zeros(e.capacity, 2, CMAX, dtype=torch.float32, device=dev)  # conv-epilogue stats
+            self.ev_acc = torch.zeros(2, e.capacity, dtype=torch.float32, device=dev)  # [correct, summed CE]
+            self._build_eval()
+        else:
+            self._build()
         self.graph = None
 
     # ----------------------------------------------------------------------------------------- helpers
@@ -302,8 +370,8 @@ class _ImageNetPlan:
         a.cmax = CMAX
         return a
 
-    def cf(self, bn):  # forward coefficients of BN `bn`
-        return self.be.coef[0, bn]
+    def cf(self, bn):  # forward coefficients of BN `bn` (eval: from the moving statistics, the plan's own buffer)
+        return self.ev_coef[bn] if self.eval else self.be.coef[0, bn]
 
     def cb(self, bn):  # backward coefficients
         return self.be.coef[1, bn]
@@ -378,8 +446,8 @@ class _ImageNetPlan:
         b = be.prog.bns[bn]
         a = BnFinArgs()
         a.state, a.s_mstride = _p(e.state), e.S
-        a.sums = _p(self.sb(bn) if backward else self.sf(bn))
-        a.coef = _p(self.cb(bn) if backward else self.cf(bn))
+        a.sums = _p(self.sb(bn) if backward == 1 else self.sf(bn))
+        a.coef = _p(self.cb(bn) if backward == 1 else self.cf(bn))  # backward 2: eval (moving statistics)
         a.fcoef = _p(self.cf(bn))
         a.grads, a.g_mstride = _p(e.grads), e.Pp
         a.slots, a.cnt = _p(self.slots_t), _p(self.cnt)
@@ -419,13 +487,27 @@ class _ImageNetPlan:
         self._add(L.dtf_cg_chan_stats, _p(self.xs[0]), _p(self.img_slot), _p(self.sf(prog.blocks[0].bns[0])), N,
                   H2 * H2, cfg.num_filters, CMAX)
         nblk = len(prog.blocks)
+        fold = self.fold
         for i, blk in enumerate(prog.blocks):
             hi, ho, cin, f, fout = self.geo[i]
             b1, b2, b3 = blk.bns
             c1, c2, c3 = blk.convs
             x = self.xs[i]
             relu = L.dtf_cg_bn_relu_apply
+            nxt = prog.blocks[i + 1].bns[0] if i + 1 < nblk else prog.final_bn
+            res = self.sc[i] if blk.proj is not None else x
             self.bn_final(b1, hi, False)
+            if fold:
+                # BN+ReLU applied while each consumer stages its operand (convg MODE 1): no materialised activation
+                if blk.proj is not None:
+                    self.conv(blk.proj, x, self.sc[i], hi, mode=1, c_in=self.cf(b1), epi=0)
+                self.conv(c1, x, self.h1[i], hi, mode=1, c_in=self.cf(b1), epi=4, st=self.sf(b2))
+                self.bn_final(b2, hi, False)
+                self.conv(c2, self.h1[i], self.h2[i], hi, mode=1, c_in=self.cf(b2), epi=4, st=self.sf(b3))
+                self.bn_final(b3, ho, False)
+                self.conv(c3, self.h2[i], self.xs[i + 1], ho, mode=1, c_in=self.cf(b3), epi=5, res=res,
+                          st=self.sf(nxt))
+                continue
             self.ew(relu, x, self.ax[i], self.cf(b1), hi, cin)
             if blk.proj is not None:
                 self.conv(blk.proj, self.ax[i], self.sc[i], hi, mode=0, epi=0)
@@ -435,8 +517,6 @@ class _ImageNetPlan:
             self.conv(c2, self.a1[i], self.h2[i], hi, mode=0, epi=4, st=self.sf(b3))
             self.bn_final(b3, ho, False)
             self.ew(relu, self.h2[i], self.a2[i], self.cf(b3), ho, f)
-            nxt = prog.blocks[i + 1].bns[0] if i + 1 < nblk else prog.final_bn
-            res = self.sc[i] if blk.proj is not None else x
             self.conv(c3, self.a2[i], self.xs[i + 1], ho, mode=0, epi=5, res=res, st=self.sf(nxt))
         fb = prog.final_bn
         HL = self.HL
@@ -484,6 +564,32 @@ class _ImageNetPlan:
             c1, c2, c3 = blk.convs
             x, h1, h2 = self.xs[i], self.h1[i], self.h2[i]
             bwd = L.dtf_cg_bn_bwd_apply
+            if fold:
+                # BN-backward applied while the next dgrad / wgrad stage their dy operand (convg MODE 2); the
+                # forward BN+ReLU of each wgrad's x operand likewise (MODE_X 1)
+                dz3 = self.tmp("dz3", ho, f)
+                self.conv(c3, gcur, dz3, ho, mode=0, epi=6, xm=h2, c_ep=self.cf(b3), st=self.sb(b3), dgrad=True)
+                self.bn_final(b3, ho, True)
+                self.wgrad(c3, h2, gcur, ho, mode_x=1, c_x=self.cf(b3))
+                dz2 = self.tmp("dz2", hi, f)
+                self.conv(c2, dz3, dz2, ho, mode=2, c_in=self.cb(b3), x2=h2, epi=6, xm=h1, c_ep=self.cf(b2),
+                          st=self.sb(b2), dgrad=True)
+                self.bn_final(b2, hi, True)
+                self.wgrad(c2, h1, dz3, hi, mode_x=1, c_x=self.cf(b2), mode_dy=2, c_dy=self.cb(b3), dy2=h2)
+                pd = None
+                if blk.proj is not None:
+                    pd = self.tmp("pd", hi, cin)
+                    self.conv(blk.proj, gcur, pd, ho, mode=0, epi=0, dgrad=True)
+                    self.wgrad(blk.proj, x, gcur, hi, mode_x=1, c_x=self.cf(b1))
+                dz1 = self.tmp("dz1", hi, cin)
+                self.conv(c1, dz2, dz1, hi, mode=2, c_in=self.cb(b2), x2=h1, epi=6 | (1 if pd is not None else 0),
+                          res=pd, xm=x, c_ep=self.cf(b1), st=self.sb(b1), dgrad=True)
+                self.bn_final(b1, hi, True)
+                self.wgrad(c1, x, dz2, hi, mode_x=1, c_x=self.cf(b1), mode_dy=2, c_dy=self.cb(b2), dy2=h1)
+                gnext = self.tmp("gA" if (i % 2 == 0) else "gB", hi, cin)
+                self.ew(bwd, x, gnext, self.cb(b1), hi, cin, dz=dz1, add=None if blk.proj is not None else gcur)
+                gcur = gnext
+                continue
             # conv3: dz3 = dgrad(g) masked by BN3(h2) (+ BN3 reductions); dh2 = BN3-backward(dz3, h2)
             dz3 = self.tmp("dz3", ho, f)
             self.conv(c3, gcur, dz3, ho, mode=0, epi=6, xm=h2, c_ep=self.cf(b3), st=self.sb(b3), dgrad=True)
@@ -519,6 +625,75 @@ class _ImageNetPlan:
         self._add("optim", None)
         self._add("step", None)
 
+    def _build_eval(self):
+        """Forward-only launch list of an eval chunk (resnet_run_loop.py:463-466): padded stem / dense weights of the
+        evaluated members, BN coefficients from the moving statistics (cg_bn_final mode 2), the training forward
+        kernels with their statistic epilogues drained into a sink, GAP, dense GEMM and a gradient-free
+        softmax-CE that only counts loss / correct predictions."""
+        be, e, prog, cfg = self.be, self.e, self.be.prog, self.be.cfg
+        L = ops.lib()
+        N, H = self.N, self.H
+        ns = len(self.slots)
+        sink = self.ev_sink
+        self._add(L.dtf_cg_weight_prep, _p(e.state), e.S, _p(be.conv_table), 1, _p(self.slots_t), ns,
+                  _p(be.w), _p(be.w), be.wtot)
+        self._add(L.dtf_cg_dense_prep, _p(e.state), e.S, prog.dense_w_off, be.ncls, NPAD_CLS, cfg.final_size,
+                  _p(self.slots_t), ns, _p(be.dense), NPAD_CLS * cfg.final_size)
+        for b in range(len(prog.bns)):
+            hw = 1  # the eval coefficients do not depend on the spatial size
+            self.bn_final(b, hw, 2)
+        self._add(L.dtf_cg_prep_input, _p(self.x_in), _p(self.xin8), N * H * H, cfg.in_channels)
+        H1, H2 = H // 2, self.xs[0].shape[1]
+        self.conv(prog.stem, self.xin8, self.y0, H, mode=0, epi=0)
+        self._add(L.dtf_cg_maxpool, _p(self.y0), _p(self.xs[0]), _p(self.am0), None, None, N, H1, H1, H2, H2,
+                  cfg.num_filters, 0)
+        relu = L.dtf_cg_bn_relu_apply
+        for i, blk in enumerate(prog.blocks):
+            hi, ho, cin, f, fout = self.geo[i]
+            b1, b2, b3 = blk.bns
+            c1, c2, c3 = blk.convs
+            x = self.xs[i]
+            self.ew(relu, x, self.ax[i], self.cf(b1), hi, cin)
+            if blk.proj is not None:
+                self.conv(blk.proj, self.ax[i], self.sc[i], hi, mode=0, epi=0)
+            self.conv(c1, self.ax[i], self.h1[i], hi, mode=0, epi=4, st=sink)
+            self.ew(relu, self.h1[i], self.a1[i], self.cf(b2), hi, f)
+            self.conv(c2, self.a1[i], self.h2[i], hi, mode=0, epi=4, st=sink)
+            self.ew(relu, self.h2[i], self.a2[i], self.cf(b3), ho, f)
+            res = self.sc[i] if blk.proj is not None else x
+            self.conv(c3, self.a2[i], self.xs[i + 1], ho, mode=0, epi=5, res=res, st=sink)
+        fb = prog.final_bn
+        HL = self.HL
+        g = GapArgs()
+        g.x, g.coef, g.img_slot, g.feat = _p(self.xs[-1]), _p(self.cf(fb)), _p(self.img_slot), _p(self.feat)
+        g.dfeat, g.sums, g.bcoef = _p(self.dfeat), _p(sink), _p(self.cf(fb))
+        g.hw, g.C, g.cmax = HL * HL, cfg.final_size, CMAX
+        self._hold(g)
+        self._add(L.dtf_cg_gap, ctypes.byref(g), 0, N)
+        from .hip_mnist import GEMM_OUT_F32, GroupedGemm
+        C = cfg.final_size
+        Dstride = NPAD_CLS * C
+        fwd = [(self.first[s] * C, s * Dstride, self.first[s] * NPAD_CLS, n, NPAD_CLS, C)
+               for s, n in zip(self.slots, self.sizes)]
+        self.g_fwd = GroupedGemm(self.feat, be.dense, self.logits, C, C, NPAD_CLS, fwd, False, False, GEMM_OUT_F32,
+                                 be.dev)
+        self._add("gemm", self.g_fwd)
+        self._add(L.dtf_cg_softmax_ce, _p(self.logits), NPAD_CLS, be.ncls, _p(self.labels), _p(self.img_slot),
+                  _p(e.state), e.S, prog.dense_b_off, None, e.Pp, _p(self.cnt), _p(self.ev_acc[1]),
+                  _p(self.ev_acc[0]), None, N)
+
+    def load_eval(self, x, y):
+        """The same eval images for every member: [m, H, W, C] fp32 -> this plan's [members * m] input."""
+        m, k = x.shape[0], len(self.slots)
+        assert all(n == m for n in self.sizes)
+        shp = tuple(self.x_in.shape[1:])
+        self.x_in.view(k, m, *shp).copy_(x.reshape(1, m, *shp).expand(k, *([-1] * (len(shp) + 1))))
+        self.labels.view(k, m).copy_(y.reshape(1, m).expand(k, -1))
+
+    def run_eval(self):
+        assert self.eval
+        self._run_eager()
+
     # ----------------------------------------------------------------------------------------- execution
     def load_batch(self, batches):
         if same_batches(self, batches):
@@ -549,7 +724,8 @@ class _ImageNetPlan:
                 if err != 0:
                     raise RuntimeError("kernel launch %s failed with %d" % (getattr(fn, "__name__", fn), err))
         # per-member losses gathered inside the step (graph) so a replay leaves one copy for train_step
-        torch.index_select(self.be.loss, 0, self.slots_long, out=self.loss_sel)
+        if not self.eval:
+            torch.index_select(self.be.loss, 0, self.slots_long, out=self.loss_sel)
 
     def run(self):
         be = self.be

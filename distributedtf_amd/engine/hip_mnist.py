@@ -17,7 +17,8 @@ launch sequence over population-packed tensors (``ops/csrc/mnist.hip``, ``ops/cs
   optimizer    fused launch over all members; also refreshes the bf16 shadow read by conv2 / dense1
 
 The sequence is captured once per batch composition into a HIP graph and replayed.
-Eval runs the PyTorch reference forward (dropout off) on the fp32 master weights.
+Eval runs the forward kernels (conv1, conv2, the dense1 grouped GEMM, the head with dropout off) for every
+member at once over chunks of the eval set (``evaluate_population``).
 """
 
 from __future__ import annotations
@@ -211,15 +212,57 @@ class HipMnistBackend:
     def forward_backward(self, slots, batches):
         raise RuntimeError("HipMnistBackend runs whole steps: use train_step")
 
+    def train_correct(self, slots):
+        """Correct predictions of each member's last training batch (head kernel count; device tensor)."""
+        return self.correct[torch.as_tensor(list(slots), dtype=torch.long, device=self.dev)]
+
+    def eval_plan(self, slots, m):
+        key = ("eval", tuple(slots), int(m))
+        p = self._plans.get(key)
+        if p is None:
+            if len(self._plans) > 16:
+                self._plans.clear()
+            p = _MnistPlan(self, list(slots), [int(m)] * len(slots), eval_mode=True)
+            self._plans[key] = p
+        return p
+
     @torch.no_grad()
     def infer(self, slot, x):
-        e = self.e
-        return e.arch.forward(e.params[slot], e.running[slot], x, training=False, dtype=torch.float32)
+        """Eval-mode logits of one member on the HIP forward kernels (dropout off)."""
+        p = self.eval_plan([slot], int(x.shape[0]))
+        logits = p.want_logits()
+        p.load_eval(x, torch.zeros(x.shape[0], dtype=torch.int32, device=x.device))
+        p.run_eval()
+        return logits.clone()
+
+    @torch.no_grad()
+    def evaluate_population(self, slots, x, y, chunk=None):
+        """Eval accuracy of every member in ``slots``: one population-batched forward (conv1, conv2, dense1 grouped
+        GEMM, head without dropout) per chunk of the eval set; one host sync at the end."""
+        n = int(x.shape[0])
+        if n == 0 or not slots:
+            return {s: 0.0 for s in slots}
+        chunk = min(n, int(chunk or os.environ.get("DTF_EVAL_CHUNK", "2500")))
+        used = []
+        for i in range(0, n, chunk):
+            m = min(chunk, n - i)
+            p = self.eval_plan(slots, m)
+            if all(p is not q for q in used):
+                p.ev_acc.zero_()
+                used.append(p)
+            p.load_eval(x[i:i + m], y[i:i + m])
+            p.run_eval()
+        correct = used[0].ev_acc[0].clone()
+        for p in used[1:]:
+            correct += p.ev_acc[0]
+        vals = correct.cpu().tolist()
+        return {s: vals[s] / float(n) for s in slots}
 
 
 class _MnistPlan:
-    def __init__(self, be: HipMnistBackend, slots: List[int], sizes: List[int]):
+    def __init__(self, be: HipMnistBackend, slots: List[int], sizes: List[int], eval_mode: bool = False):
         self.be, self.e = be, be.e
+        self.eval = bool(eval_mode)
         e, dev = be.e, be.dev
         self.slots, self.sizes = slots, sizes
         N = sum(sizes)
@@ -244,9 +287,13 @@ class _MnistPlan:
         self.p2 = torch.empty(N, 3136, dtype=bf, device=dev)
         self.am2 = torch.empty(N, 3136, dtype=torch.uint8, device=dev)
         self.z = torch.empty(N, 1024, dtype=torch.float32, device=dev)
-        self.dz = torch.empty(N, 1024, dtype=bf, device=dev)
-        self.dp2 = torch.empty(N, 3136, dtype=bf, device=dev)
-        self.dp1 = torch.empty(N, 196, 32, dtype=bf, device=dev)
+        # backward temporaries (eval plans: forward only)
+        nb = 1 if self.eval else N
+        self.dz = torch.empty(nb, 1024, dtype=bf, device=dev)
+        self.dp2 = torch.empty(nb, 3136, dtype=bf, device=dev)
+        self.dp1 = torch.empty(nb, 196, 32, dtype=bf, device=dev)
+        self.ev_acc = torch.zeros(2, e.capacity, dtype=torch.float32, device=dev)  # eval: [correct, summed CE]
+        self.logits = None
         o = be.offs
         a = MnistArgs()
         a.x, a.labels, a.img_slot = _p(self.x), _p(self.labels), _p(self.img_slot)
@@ -261,7 +308,9 @@ class _MnistPlan:
         a.off_c1w, a.off_c1b, a.off_c2w, a.off_c2b = o["conv1_w"], o["conv1_b"], o["conv2_w"], o["conv2_b"]
         a.off_d1w, a.off_d1b, a.off_d2w, a.off_d2b = o["dense1_w"], o["dense1_b"], o["dense2_w"], o["dense2_b"]
         a.drop_rate = be.drop_rate
-        a.train = 1
+        a.train = 0 if self.eval else 1
+        if self.eval:  # counts accumulate over the eval chunks in the plan's own buffers
+            a.loss, a.correct = _p(self.ev_acc[1]), _p(self.ev_acc[0])
         self.args = a
         # work lists (img0, nimg, 0, slot): image chunks of one member
         self.w_fwd = self._chunks(max(1, -(-N // 512)))
@@ -278,9 +327,32 @@ class _MnistPlan:
             dgr.append((f * 1024, s * Pp + d1, f * 3136, n, 3136, 1024))     # dP2 = dZ W
             wgr.append((f * 1024, f * 3136, s * Pp + d1, 1024, 3136, n))     # dW += dZ^T P2
         self.g_fwd = GroupedGemm(self.p2, be.shadow, self.z, 3136, 3136, 1024, fwd, False, False, GEMM_OUT_F32, dev)
-        self.g_dgr = GroupedGemm(self.dz, be.shadow, self.dp2, 1024, 3136, 3136, dgr, False, True, GEMM_OUT_BF16, dev)
-        self.g_wgr = GroupedGemm(self.dz, self.p2, e.grads, 1024, 3136, 3136, wgr, True, True, GEMM_OUT_ACC, dev)
+        if not self.eval:
+            self.g_dgr = GroupedGemm(self.dz, be.shadow, self.dp2, 1024, 3136, 3136, dgr, False, True, GEMM_OUT_BF16,
+                                     dev)
+            self.g_wgr = GroupedGemm(self.dz, self.p2, e.grads, 1024, 3136, 3136, wgr, True, True, GEMM_OUT_ACC, dev)
         self.graph = None
+
+    # ---- eval (mnist_model.py:167-172 ``mnist_classifier.evaluate``: dropout off)
+    def want_logits(self):
+        if self.logits is None:
+            self.logits = torch.zeros(self.N, 10, dtype=torch.float32, device=self.be.dev)
+            self.args.logits_out = _p(self.logits)
+        return self.logits
+
+    def load_eval(self, x, y):
+        m, k = x.shape[0], len(self.slots)
+        assert all(n == m for n in self.sizes)
+        self.x.view(k, m, 28, 28).copy_(x.reshape(1, m, 28, 28).expand(k, -1, -1, -1))
+        self.labels.view(k, m).copy_(y.reshape(1, m).expand(k, -1))
+
+    def run_eval(self):
+        assert self.eval
+        L, st = ops.lib(), ops.stream()
+        self._launch(L.dtf_mnist_conv1, n=self.N)
+        self._launch(L.dtf_mnist_conv2_fwd, self.w_fwd)
+        self.g_fwd.launch(st)
+        self._launch(L.dtf_mnist_head, self.w_head)
 
     def _chunks(self, chunk):
         items = []

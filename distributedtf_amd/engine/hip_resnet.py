@@ -813,7 +813,7 @@ class _StepPlan:
             if pend is not None and self._piggyback(pend):
                 buf, red, rc, goff = pend
                 a.rslab, a.rtab, a.r_c, a.r_goff = buf, _p(red), rc, goff
-                a.r_nblk = self._slab_elems(rc) // 32
+                a.r_nblk = self._reduce_wgs(rc, work.shape[0], red.shape[0])
                 n_red = a.r_nblk * red.shape[0]
                 self._pending_slab = None
             else:
@@ -898,9 +898,28 @@ class _StepPlan:
             return False
         _, red, rc, _ = pend
         limit = int(os.environ.get("DTF_PIGGYBACK_MAX_WG", "3000"))
-        if rc == 64 and os.environ.get("DTF_PIGGYBACK_C64", "0") != "1":
-            return False  # 1152 reduce WGs per member at the carrier's occupancy: measured slower (pop 1: +0.1 ms)
+        if rc == 64:
+            # C = 64: looping reduce workgroups that fill the carrier's last partial wave of CUs (_reduce_wgs).
+            # Off: measured slower (pop 1 1.39 -> 1.58 ms, pop 8 3.70 -> 4.30 ms; profiles/r2_piggyback_c64_ab.log):
+            # a looping workgroup's strided slab reads are latency-bound; one workgroup per 32 slab elements (1152
+            # per member) was also slower (pop 1: +0.1 ms)
+            return os.environ.get("DTF_PIGGYBACK_C64", "0") == "1"
         return (self._slab_elems(rc) // 32) * red.shape[0] <= limit
+
+    def _reduce_wgs(self, rc, n_main, n_members):
+        """Reduce workgroups per member of a piggybacked slab reduction.  C = 16 / 32: one per 32 slab elements.
+        C = 64: as many as the CUs the carrier leaves idle in its last wave (>= 64 in total), each looping over
+        its share of the 1152 element blocks -- at one member the 128 carrier workgroups of a C = 64 layer
+        occupy half the GPU, the reduction runs on the other half."""
+        nb = self._slab_elems(rc) // 32
+        if rc != 64:
+            return nb
+        per_wave = int(os.environ.get("DTF_PIGGYBACK_WAVE", "256"))
+        t = -(-n_main // per_wave) * per_wave - n_main
+        if t < 64:
+            t += per_wave
+        t = int(os.environ.get("DTF_PIGGYBACK_C64_WGS", t))
+        return max(1, min(nb, t // max(1, n_members)))
 
     def _flush_slab(self):
         """Standalone reduction of a pending slab (no later fused launch can take it)."""

@@ -1263,33 +1263,39 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
 }
 
 // One workgroup of the dW slab reduction (see dw_slab_reduce_kernel): 32 slab elements of member row `by`.
+// Blocks bx0, bx0 + bstride, ... of 32 slab elements (workgroup-uniform loop: every thread reaches each barrier).
 template <int C>
 __device__ __forceinline__ void slab_reduce_wg(const float* __restrict__ slab, const int4* __restrict__ red,
-                                               float* __restrict__ grads, long g_mstride, long g_off, int bx, int by,
-                                               float* part /* [8][33] */) {
+                                               float* __restrict__ grads, long g_mstride, long g_off, int bx0, int by,
+                                               float* part /* [8][33] */, int bstride) {
   constexpr int MT = C / 16, NTN = 9 * C / 16, NJ = (NTN + 3) / 4, E = NJ * MT * 4 * 256;
   const int el = threadIdx.x & 31, gg = threadIdx.x >> 5;
-  const int e = bx * 32 + el;
   const int4 rd = red[by];
-  const float* p = slab + (long)rd.x * E + e;
-  float s0 = 0.f, s1 = 0.f;
-  int g = gg;
-  for (; g + 8 < rd.y; g += 16) {
-    s0 += p[(long)g * E];
-    s1 += p[(long)(g + 8) * E];
-  }
-  if (g < rd.y) s0 += p[(long)g * E];
-  part[gg * 33 + el] = s0 + s1;
-  __syncthreads();
-  if (gg != 0) return;
-  float sum = 0.f;
+  for (int bx = bx0; bx < E / 32; bx += bstride) {
+    const int e = bx * 32 + el;
+    const float* p = slab + (long)rd.x * E + e;
+    float s0 = 0.f, s1 = 0.f;
+    int g = gg;
+    for (; g + 8 < rd.y; g += 16) {
+      s0 += p[(long)g * E];
+      s1 += p[(long)(g + 8) * E];
+    }
+    if (g < rd.y) s0 += p[(long)g * E];
+    part[gg * 33 + el] = s0 + s1;
+    __syncthreads();
+    if (gg == 0) {
+      float sum = 0.f;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) sum += part[i * 33 + el];
-  const int r = e & 3, t = (e >> 2) & 255, m = (e >> 10) % MT, j = (e >> 10) / MT;  // slab [j][m][t][r]
-  const int wave = t >> 6, lane = t & 63, nt = wave + 4 * j;
-  if (nt >= NTN) return;
-  const int tap = (nt * 16) / C, ci = (nt * 16) % C + (lane & 15), co = m * 16 + 4 * (lane >> 4) + r;
-  grads[(long)rd.w * g_mstride + g_off + ((long)co * 9 + tap) * C + ci] += sum;
+      for (int i = 0; i < 8; ++i) sum += part[i * 33 + el];
+      const int r = e & 3, t = (e >> 2) & 255, m = (e >> 10) % MT, j = (e >> 10) / MT;  // slab [j][m][t][r]
+      const int wave = t >> 6, lane = t & 63, nt = wave + 4 * j;
+      if (nt < NTN) {
+        const int tap = (nt * 16) / C, ci = (nt * 16) % C + (lane & 15), co = m * 16 + 4 * (lane >> 4) + r;
+        grads[(long)rd.w * g_mstride + g_off + ((long)co * 9 + tap) * C + ci] += sum;
+      }
+    }
+    __syncthreads();  // part is rewritten by the next block
+  }
 }
 
 // ------------------------------------------------------------------ fused backward
@@ -1350,9 +1356,11 @@ __global__ __launch_bounds__(256, ROLE == 1 ? 2 : DTF_FUSED_WAVES(C, MODE_DY)) v
   if ((int)blockIdx.x >= a.n_main) {  // trailing workgroups: dW slab reduction of the previous fused launch
     const int r = (int)blockIdx.x - a.n_main;
     float* part = reinterpret_cast<float*>(smem);
-    if (a.r_c == 16) slab_reduce_wg<16>(a.rslab, a.rtab, a.grads, a.g_mstride, a.r_goff, r % a.r_nblk, r / a.r_nblk, part);
-    else if (a.r_c == 32) slab_reduce_wg<32>(a.rslab, a.rtab, a.grads, a.g_mstride, a.r_goff, r % a.r_nblk, r / a.r_nblk, part);
-    else if (a.r_c == 64) slab_reduce_wg<64>(a.rslab, a.rtab, a.grads, a.g_mstride, a.r_goff, r % a.r_nblk, r / a.r_nblk, part);
+    // r_nblk reduce workgroups per member, each looping over every r_nblk-th block of 32 slab elements
+    const int bx = r % a.r_nblk, by = r / a.r_nblk;
+    if (a.r_c == 16) slab_reduce_wg<16>(a.rslab, a.rtab, a.grads, a.g_mstride, a.r_goff, bx, by, part, a.r_nblk);
+    else if (a.r_c == 32) slab_reduce_wg<32>(a.rslab, a.rtab, a.grads, a.g_mstride, a.r_goff, bx, by, part, a.r_nblk);
+    else if (a.r_c == 64) slab_reduce_wg<64>(a.rslab, a.rtab, a.grads, a.g_mstride, a.r_goff, bx, by, part, a.r_nblk);
     return;
   }
   const int4 wk = work_item(a);
@@ -1650,7 +1658,7 @@ __global__ __launch_bounds__(256) void dw_slab_reduce_kernel(const float* __rest
                                                              const int4* __restrict__ red, float* __restrict__ grads,
                                                              long g_mstride, long g_off) {
   __shared__ float part[8 * 33];
-  slab_reduce_wg<C>(slab, red, grads, g_mstride, g_off, blockIdx.x, blockIdx.y, part);
+  slab_reduce_wg<C>(slab, red, grads, g_mstride, g_off, blockIdx.x, blockIdx.y, part, gridDim.x);
 }
 
 template <typename KernelT>

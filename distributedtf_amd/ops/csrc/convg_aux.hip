@@ -105,6 +105,22 @@ __global__ __launch_bounds__(256) void cg_bn_fwd_final_kernel(BnFinArgs a) {
   run[a.C + c] = BN_MOM * run[a.C + c] + (1.f - BN_MOM) * unb;
 }
 
+// Eval mode: coefficients from the moving statistics (no update): scale, shift, mean, inv
+__global__ __launch_bounds__(256) void cg_bn_eval_final_kernel(BnFinArgs a) {
+  const int slot = a.slots[blockIdx.y];
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.C) return;
+  const float* row = a.state + (long)slot * a.s_mstride;
+  const float mean = row[a.run_off + c], var = row[a.run_off + a.C + c];
+  const float inv = rsqrtf(var + BN_EPS);
+  const float scale = row[a.gamma_off + c] * inv;
+  float* co = a.coef + (long)slot * 4 * a.cmax;
+  co[c] = scale;
+  co[a.cmax + c] = row[a.beta_off + c] - mean * scale;
+  co[2 * a.cmax + c] = mean;
+  co[3 * a.cmax + c] = inv;
+}
+
 __global__ __launch_bounds__(256) void cg_bn_bwd_final_kernel(BnFinArgs a) {
   const int slot = a.slots[blockIdx.y];
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -393,14 +409,14 @@ __global__ __launch_bounds__(256) void cg_softmax_ce_kernel(const float* __restr
   const float lse = mx + __logf(se);
   const int lab = labels[img];
   const float bsz = cnt[slot];
-  float* gb = grads + (long)slot * g_mstride + b_off;
+  float* gb = grads != nullptr ? grads + (long)slot * g_mstride + b_off : nullptr;
   for (int j = lane; j < ld; j += 64) {
     float d = 0.f;
     if (j < ncls) {
       d = (__expf(lr[j] + bias[j] - lse) - (j == lab ? 1.f : 0.f)) / bsz;
-      atomicAdd(gb + j, d);
+      if (grads != nullptr) atomicAdd(gb + j, d);
     }
-    dl[img * ld + j] = f2bf(d);
+    if (dl != nullptr) dl[img * ld + j] = f2bf(d);  // eval (no grads / dlogits): loss and correct count only
   }
   if (lane == 0) {
     atomicAdd(loss + slot, (lse - (lr[lab] + bias[lab])) / bsz);
@@ -478,7 +494,9 @@ DTF_API int dtf_cg_dense_prep(const float* state, long s_mstride, int w_off, int
 DTF_API int dtf_cg_bn_final(const BnFinArgs* a, int backward, int nslots, hipStream_t stream) {
   if (nslots <= 0) return 0;
   dim3 grid((a->C + 255) / 256, nslots);
-  if (backward)
+  if (backward == 2)  // eval: moving statistics
+    hipLaunchKernelGGL(cg_bn_eval_final_kernel, grid, dim3(256), 0, stream, *a);
+  else if (backward)
     hipLaunchKernelGGL(cg_bn_bwd_final_kernel, grid, dim3(256), 0, stream, *a);
   else
     hipLaunchKernelGGL(cg_bn_fwd_final_kernel, grid, dim3(256), 0, stream, *a);

@@ -33,7 +33,7 @@ def _population(arch, n, monkeypatch, seed=0):
     for b in arch.prog.bns:
         eng.state[:n, b.gamma_off:b.gamma_off + b.c] = (1.0 + 0.2 * torch.randn(n, b.c, generator=g)).to(dev)
         eng.state[:n, b.beta_off:b.beta_off + b.c] = (0.1 * torch.randn(n, b.c, generator=g)).to(dev)
-    calib = torch.randn(64, 32, 32, 3, generator=g).to(dev)
+    calib = torch.randn(16 if arch.input_shape[0] > 32 else 64, *arch.input_shape, generator=g).to(dev)
     monkeypatch.setattr(resnet_mod, "BN_MOMENTUM", 0.0)
     with torch.no_grad():
         for s in range(n):
@@ -78,11 +78,64 @@ def test_hip_evaluate_population_accuracy(n_eval, chunk):
         assert abs(acc[s] - ref_acc) <= 0.04, (s, acc[s], ref_acc)
     assert acc[0] >= 0.95
     # the engine-level entry point gives the same numbers
-    acc2 = eng.evaluate_population(slots, x, y)
+    acc2 = eng.evaluate_population(slots, x, y)  # default chunking: other work splits, near-ties may flip
     for s in slots:
-        assert abs(acc2[s] - acc[s]) <= 1e-6
+        assert abs(acc2[s] - acc[s]) <= 2.5 / n_eval
     # training state untouched by eval: the next training step is unaffected (no stats/weight aliasing)
     before = eng.state.clone()
     eng.backend.evaluate_population(slots, x, y, chunk=chunk)
     torch.cuda.synchronize()
     assert torch.equal(before, eng.state)
+
+
+def test_hip_mnist_eval_matches_reference():
+    """MNIST eval on the HIP forward kernels (dropout off; mnist_model.py:167-172) vs the fp32 oracle."""
+    from distributedtf_amd.models.mnist import MnistArch
+    arch = MnistArch()
+    dev = torch.device("cuda")
+    eng = PopulationEngine(arch, 3, dev, backend="hip")
+    assert eng.backend.__class__.__name__ == "HipMnistBackend"
+    hp = {"opt_case": {"optimizer": "gd", "lr": 0.1}, "batch_size": 16, "initializer": "he_init"}
+    slots = [eng.add_member(None, dict(hp), seed=20 + i) for i in range(3)]
+    g = torch.Generator().manual_seed(5)
+    for name in ("conv1_b", "conv2_b", "dense1_b", "dense2_b"):
+        off, shp = arch.offsets[name]
+        eng.state[:, off:off + shp[0]] = (0.05 * torch.randn(3, shp[0], generator=g)).to(dev)
+    eng.backend.on_params_changed(slots)
+    x = (torch.rand(300, 28, 28, 1, generator=g) * 255.0).to(dev)
+    refs = [arch.forward(eng.params[s], eng.running[s], x, training=False, dtype=torch.float32) for s in slots]
+    for s, ref in zip(slots, refs):
+        hip = eng.backend.infer(s, x)
+        assert _relerr(hip, ref) < 0.03, (s, _relerr(hip, ref))
+    y = refs[1].argmax(1)
+    acc = eng.backend.evaluate_population(slots, x, y, chunk=128)
+    for s, ref in zip(slots, refs):
+        assert abs(acc[s] - float((ref.argmax(1) == y).float().mean())) <= 0.03
+    assert acc[1] >= 0.97
+
+
+def test_hip_imagenet_eval_matches_reference(monkeypatch):
+    """ImageNet-shape ResNet-50 v2 eval (64x64 input, 1001 classes) on the HIP kernels vs the fp32 oracle."""
+    from distributedtf_amd.models.resnet import imagenet_config
+    arch = ResNetArch(imagenet_config(50, 2, num_classes=1001, image_size=64))
+    eng, g = _population(arch, 2, monkeypatch, seed=9)
+    assert eng.backend.__class__.__name__ == "HipImageNetBackend"
+    dev = eng.state.device
+    x = torch.randn(12, 64, 64, 3, generator=g).to(dev)
+    refs = [arch.forward(eng.params[s], eng.running[s].clone(), x, training=False, dtype=torch.float32)
+            for s in range(2)]
+    r16 = [arch.forward(eng.params[s], eng.running[s].clone(), x, training=False, dtype=torch.bfloat16).float()
+           for s in range(2)]
+    for s in range(2):
+        hip = eng.backend.infer(s, x)
+        # tolerance = what a bf16 PyTorch forward of the same 50 layers deviates from fp32, x2.5
+        tol = max(2.5 * _relerr(r16[s], refs[s]), 0.05)
+        print("member %d: hip rel %.4f, torch-bf16 rel %.4f" % (s, _relerr(hip, refs[s]), _relerr(r16[s], refs[s])))
+        assert _relerr(hip, refs[s]) < tol, (s, _relerr(hip, refs[s]), tol)
+    # accuracy vs labels = the fp32 oracle's predictions of member 0: the HIP eval must agree with the oracle about
+    # as well as a bf16 PyTorch forward does (random-init ResNet-50 logits are near-ties at bf16 precision)
+    y = refs[0].argmax(1)
+    acc = eng.backend.evaluate_population([0, 1], x, y, chunk=5)
+    for s in range(2):
+        acc16 = float((r16[s].argmax(1) == y).float().mean())
+        assert acc[s] >= acc16 - 0.2, (s, acc[s], acc16)

@@ -101,6 +101,7 @@ def _register():
     ops.register("dtf_dw_slab_reduce", [c_void_p, c_void_p, c_int, c_void_p, c_long, c_long, c_int, c_void_p])
     ops.register("dtf_conv_bwd_fused", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_bwd_role", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
+    ops.register("dtf_conv_bwd_dual", [P(ConvArgs), P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_args_size", [])
     ops.register("dtf_bnbwd_args_size", [])
     ops.register("dtf_head_args_size", [])
@@ -526,6 +527,13 @@ class _StepPlan:
         sp = os.environ.get("DTF_SPLIT_BWD", "0")
         self.split = dev.type == "cuda" and not cfg.version == 1 and (
             sp == "1" or (sp == "auto" and len(slots) <= int(os.environ.get("DTF_SPLIT_MAX_POP", "2"))))
+        # Dual backward (small populations): each stride-1 conv's dgrad and wgrad run as two workgroup roles of ONE
+        # launch (conv_bwd_dual_kernel) -- no cross-stream dependencies; the layer costs max(dgrad, wgrad) instead of
+        # their sum when the population leaves CUs idle.  DTF_DUAL_BWD: "auto" (<= DTF_DUAL_MAX_POP members,
+        # default 2), "1", "0".
+        dm = os.environ.get("DTF_DUAL_BWD", "auto")
+        self.dual = (dev.type == "cuda" and not self.split and not cfg.version == 1 and (
+            dm == "1" or (dm == "auto" and len(slots) <= int(os.environ.get("DTF_DUAL_MAX_POP", "2")))))
         self.side_reduce = bool(self.side_cs) or self.split
         self.side_stream = torch.cuda.Stream(device=dev) if self.side_reduce else None
         self.launches = []
@@ -778,6 +786,9 @@ class _StepPlan:
         if self.split:
             return self._conv_bwd_split(ci, c, C, H, rows, bands, dy, dz_out, x, mode_dy, dy2, dy_bn, x_bn, res,
                                         ident_x, dy3, dy_out)
+        if self.dual:
+            return self._conv_bwd_dual(ci, c, C, H, rows, bands, dy, dz_out, x, mode_dy, dy2, dy_bn, x_bn, res,
+                                       ident_x, dy3, dy_out)
         n_wg = self._fused_nwg(C, bands)
         work = self._work_iters(bands, n_wg)
         a = self._base_args()
@@ -890,6 +901,72 @@ class _StepPlan:
         self._side(lib.dtf_conv_bwd_role, ctypes.byref(b), C, 0, 2 if ident_x else 0, 2, wwork.shape[0],
                    2304 + 4 * tsz * 2)
         self._side(lib.dtf_dw_slab_reduce, b.slab, _p(red), red.shape[0], _p(self.e.grads), self.e.Pp, c.off, C)
+
+    def _conv_bwd_dual(self, ci, c, C, H, rows, bands, dy, dz_out, x, mode_dy, dy2, dy_bn, x_bn, res, ident_x, dy3,
+                       dy_out):
+        """Dual backward of a stride-1 C->C conv (conv_bwd_dual_kernel): dgrad-role workgroups (one (image, band)
+        iteration each by default: the critical path) and wgrad-role workgroups (DTF_DUAL_WG_<C> per member, each
+        over a run of iterations, writing a dW slab) in one launch; both stage the same transformed dY.  The
+        slabs are reduced by the trailing workgroups of the next backward launch (or a standalone reduction)."""
+        be, L = self.be, self.be.L
+        lib = ops.lib()
+        tsz = ((rows + 2) * (H + 2) * _cpad(C) + 8 + 63) // 64 * 64
+        epi = int(res is not None) | (2 if ident_x else 0)
+        # ---- dgrad role
+        nd = int(os.environ.get("DTF_DUAL_DG_ITERS", "1"))
+        work = self._work_iters(bands, max(1, (self.N * bands) // nd))
+        a = self._base_args()
+        a.x, a.x2, a.y, a.xm, a.res = _p(dy), _p(dy2), _p(dz_out), _p(x), _p(res)
+        a.x3, a.xout = _p(dy3), _p(dy_out if mode_dy >= 2 else None)
+        a.w, a.w_off = _p(be.wd), L.dgr_off[ci]
+        a.work = _p(work)
+        a.g_off = c.off
+        a.n_main = work.shape[0]
+        self._set_uniform(a, work)
+        if dy_bn is not None:
+            a.in_gamma, a.in_beta = self._bn(dy_bn)
+            a.st_in, a.st_in_b = _p(be.st_f(dy_bn)), _p(be.st_b(dy_bn))
+        if not ident_x:
+            a.ep_gamma, a.ep_beta = self._bn(x_bn)
+            a.st_ep = _p(be.st_f(x_bn))
+            a.st_out = _p(be.st_b(x_bn))
+        a.Hi, a.Wi, a.Ho, a.Wo, a.rows = H, H, H, H, rows
+        a.cin_real = self._stamp_row("fused", "fused-dg C=%d mdy=%d epi=%d" % (C, mode_dy, epi))
+        # ---- wgrad role (same staging of dY / X; own work split)
+        per = int(os.environ.get("DTF_DUAL_WG_%d" % C, {16: "128", 32: "128", 64: "64"}[C]))
+        wwork = self._work_iters(bands, max(1, min(self.N * bands, per * len(self.slots))))
+        b = self._base_args()
+        b.x, b.x2, b.x3, b.xm = _p(dy), _p(dy2), _p(dy3), _p(x)
+        b.work = _p(wwork)
+        b.g_off = c.off
+        b.n_main = wwork.shape[0]
+        self._set_uniform(b, wwork)
+        if dy_bn is not None:
+            b.in_gamma, b.in_beta = self._bn(dy_bn)
+            b.st_in, b.st_in_b = _p(be.st_f(dy_bn)), _p(be.st_b(dy_bn))
+        if not ident_x:
+            b.ep_gamma, b.ep_beta = self._bn(x_bn)
+            b.st_ep = _p(be.st_f(x_bn))
+        b.Hi, b.Wi, b.Ho, b.Wo, b.rows = H, H, H, H, rows
+        b.slab = _p(self._layer_slab(wwork.shape[0] * self._slab_elems(C)))
+        b.cin_real = self._stamp_row("fused", "fused-wg C=%d mdy=%d epi=%d" % (C, mode_dy, epi))
+        # ---- trailing reduction of the previous backward launch's slabs
+        n_red = 0
+        pend = self._pending_slab
+        if pend is not None and self._piggyback(pend):
+            buf, red, rc, goff = pend
+            a.rslab, a.rtab, a.r_c, a.r_goff = buf, _p(red), rc, goff
+            a.r_nblk = self._reduce_wgs(rc, a.n_main + b.n_main, red.shape[0])
+            n_red = a.r_nblk * red.shape[0]
+            self._pending_slab = None
+        else:
+            self._flush_slab()
+        self._keep(a)
+        self._keep(b)
+        lds = 2304 + 4 * tsz * 2  # the wgrad role's dY + X tiles (double-buffered); the dgrad role uses half
+        self._add(lib.dtf_conv_bwd_dual, ctypes.byref(a), ctypes.byref(b), C, mode_dy, epi,
+                  a.n_main + b.n_main + n_red, lds)
+        self._pending_slab = (b.slab, self._slab_table(wwork), C, c.off)
 
     def _piggyback(self, pend):
         """Reduce the previous launch's slabs inside the next fused launch when that adds few workgroups

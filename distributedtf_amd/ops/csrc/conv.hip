@@ -50,7 +50,7 @@ typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 #define DTF_STAMP 0  // diagnostic build (tools/stamps.py): per-workgroup s_memrealtime stamps of the fwd_s1 / fused bwd
 #endif                // phases; the launch ordinal rides in ConvArgs.cin_real (unused by those kernels)
 #if DTF_STAMP
-#define STAMP_LAUNCHES 128
+#define STAMP_LAUNCHES 256
 #define STAMP_WGS 512
 __device__ unsigned long long dtf_stamps[STAMP_LAUNCHES][STAMP_WGS][16];
 #define STAMP_DECL unsigned long long st_[16] = {0};
@@ -124,14 +124,16 @@ struct ConvArgs {
   int u_items, u_chunk, u_per, u_pad;
 };
 
-__device__ __forceinline__ int4 work_item(const ConvArgs& a) {
+__device__ __forceinline__ int4 work_item_at(const ConvArgs& a, int b) {
   if (a.u_items > 0) {
-    const int m = (int)blockIdx.x / a.u_items, k = (int)blockIdx.x - m * a.u_items;
+    const int m = b / a.u_items, k = b - m * a.u_items;
     const int it0 = k * a.u_chunk;
     return make_int4(m * a.u_per + it0, min(a.u_chunk, a.u_per - it0), 0, m);
   }
-  return a.work[blockIdx.x];
+  return a.work[b];
 }
+
+__device__ __forceinline__ int4 work_item(const ConvArgs& a) { return work_item_at(a, (int)blockIdx.x); }
 
 __device__ __forceinline__ const float* stats_row(const float* base, int slot) {
   return base + (long)slot * NREP * 128;
@@ -495,13 +497,17 @@ __device__ __forceinline__ void reduce_stats_to_lds(float* acc_lds, const float 
   }
 }
 
-__device__ __forceinline__ void flush_stats(float* st_out, const float* acc_lds, int slot, int nch) {
+__device__ __forceinline__ void flush_stats_r(float* st_out, const float* acc_lds, int slot, int nch, int rep) {
   const int t = threadIdx.x;
   if (t < 2 * nch) {
     const int which = t / nch, c = t % nch;
-    float* row = st_out + (long)slot * NREP * 128 + (blockIdx.x & (NREP - 1)) * 128;
+    float* row = st_out + (long)slot * NREP * 128 + (rep & (NREP - 1)) * 128;
     atomicAdd(&row[which * 64 + c], acc_lds[which * 64 + c]);
   }
+}
+
+__device__ __forceinline__ void flush_stats(float* st_out, const float* acc_lds, int slot, int nch) {
+  flush_stats_r(st_out, acc_lds, slot, nch, (int)blockIdx.x);
 }
 
 // Packed-math helpers (v_pk_fma_f32 / v_cvt_pk_bf16_f32 / v_pk_max_i16): two channels per VALU op.
@@ -1315,8 +1321,9 @@ __device__ __forceinline__ void slab_reduce_wg(const float* __restrict__ slab, c
 // ROLE (split backward of small populations, engine/hip_resnet.py DTF_SPLIT_BWD): 0 = dgrad + wgrad (fused),
 // 1 = dgrad only (critical path: no X tile, no wgrad; the transformed dY may be materialised via xout for the
 // wgrad), 2 = wgrad only (runs on a side stream beside the next layers' dgrads; no dgrad / stats / xout).
-template <int C, int MODE_DY, int EPI, int ROLE = 0>
-__global__ __launch_bounds__(256, ROLE == 1 ? 2 : DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_fused_kernel(ConvArgs a) {
+// Body of one workgroup; `bid` = the workgroup's index within its role (work item, stats replica, dW slab row).
+template <int C, int MODE_DY, int EPI, int ROLE>
+__device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, char* smem) {
   constexpr bool DG = ROLE != 2, WG = ROLE != 1;
   constexpr int W = 512 / C, H = W, ROWS = 8, BANDS = H / ROWS;
   constexpr int NT = C / 16;           // dgrad output-channel tiles
@@ -1334,7 +1341,6 @@ __global__ __launch_bounds__(256, ROLE == 1 ? 2 : DTF_FUSED_WAVES(C, MODE_DY)) v
   constexpr int NK = ROWS * W / 32, RSTEP = 32 / W, KINC = RSTEP * WP * CP;
   using St = Stage<C, RT, W, H>;
   constexpr int MAXC = St::MAXC;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   float* coef_d = reinterpret_cast<float*>(smem);  // dy transform (192)
   float* ecoef = coef_d + 192;                     // x BN: scale, shift, -mean*inv, inv (256)
   float* acc_lds = ecoef + 256;                    // 128
@@ -1352,18 +1358,7 @@ __global__ __launch_bounds__(256, ROLE == 1 ? 2 : DTF_FUSED_WAVES(C, MODE_DY)) v
 #define FXRAW(i) (t0 + 4 * TSZ + ((i) & 1) * RAWSZ)
   STAMP_DECL
   STAMP(0);
-
-  if ((int)blockIdx.x >= a.n_main) {  // trailing workgroups: dW slab reduction of the previous fused launch
-    const int r = (int)blockIdx.x - a.n_main;
-    float* part = reinterpret_cast<float*>(smem);
-    // r_nblk reduce workgroups per member, each looping over every r_nblk-th block of 32 slab elements
-    const int bx = r % a.r_nblk, by = r / a.r_nblk;
-    if (a.r_c == 16) slab_reduce_wg<16>(a.rslab, a.rtab, a.grads, a.g_mstride, a.r_goff, bx, by, part, a.r_nblk);
-    else if (a.r_c == 32) slab_reduce_wg<32>(a.rslab, a.rtab, a.grads, a.g_mstride, a.r_goff, bx, by, part, a.r_nblk);
-    else if (a.r_c == 64) slab_reduce_wg<64>(a.rslab, a.rtab, a.grads, a.g_mstride, a.r_goff, bx, by, part, a.r_nblk);
-    return;
-  }
-  const int4 wk = work_item(a);
+  const int4 wk = work_item_at(a, bid);
   DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
   const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1472,9 +1467,9 @@ __global__ __launch_bounds__(256, ROLE == 1 ? 2 : DTF_FUSED_WAVES(C, MODE_DY)) v
 
   __syncthreads();  // coefficients
   STAMP(1);
-  if constexpr (XSTORE && DG)
+  if constexpr (XSTORE)  // (the wgrad role stages the same transform but never writes xout)
     st.template store_x<MODE_DY == 3 ? 3 : 2>(FDBUF(0), dv, dv2, dv3, dm, coef_d,
-                                              a.xout ? a.xout + cimg * IMG : nullptr, cgy0);
+                                              (DG && a.xout) ? a.xout + cimg * IMG : nullptr, cgy0);
   else
     st.template store<MODE_DY>(FDBUF(0), dv, dv2, dm, coef_d);
   if constexpr (WG) st.template store<1>(FXBUF(0), xv_, unused, xm, ecoef);
@@ -1569,9 +1564,9 @@ __global__ __launch_bounds__(256, ROLE == 1 ? 2 : DTF_FUSED_WAVES(C, MODE_DY)) v
     }  // DTF_ABL & 2
     if (more) {
       if constexpr (SB) __syncthreads();  // every wave is done with the current tiles
-      if constexpr (XSTORE && DG)
+      if constexpr (XSTORE)
         st.template store_x<MODE_DY == 3 ? 3 : 2>(FDBUF(k + 1), dv, dv2, dv3, dm, coef_d,
-                                                  a.xout ? a.xout + cimg * IMG : nullptr, cgy0);
+                                                  (DG && a.xout) ? a.xout + cimg * IMG : nullptr, cgy0);
       else
         st.template store<MODE_DY>(FDBUF(k + 1), dv, dv2, dm, coef_d);
       if constexpr (WG) st.template store<1>(FXBUF(k + 1), xv_, unused, xm, ecoef);
@@ -1589,7 +1584,7 @@ __global__ __launch_bounds__(256, ROLE == 1 ? 2 : DTF_FUSED_WAVES(C, MODE_DY)) v
     reduce_stats_to_lds(acc_lds, s4, q4, ci0, lane);
     __syncthreads();
   }
-  if constexpr (DG && !(EPI & 2)) flush_stats(a.st_out, acc_lds, slot, C);
+  if constexpr (DG && !(EPI & 2)) flush_stats_r(a.st_out, acc_lds, slot, C, bid);
   STAMP(4);
   if constexpr (!WG) {
     STAMP_DRAIN(5);
@@ -1599,11 +1594,11 @@ __global__ __launch_bounds__(256, ROLE == 1 ? 2 : DTF_FUSED_WAVES(C, MODE_DY)) v
   if (a.slab) {
     // partial-sum slab [wg][j][m][256 threads][4]: one 16-byte store per lane per accumulator tile (a 1 KB
     // row per wave instruction; the store tail is issue-bound); dw_slab_reduce sums a member's slabs
-    f32x4_t* sb = reinterpret_cast<f32x4_t*>(a.slab + (long)blockIdx.x * (NJ * MT * 4 * 256)) + threadIdx.x;
+    f32x4_t* sb = reinterpret_cast<f32x4_t*>(a.slab + (long)bid * (NJ * MT * 4 * 256)) + threadIdx.x;
     if constexpr (!(DTF_ABL & 1)) {
 #if DTF_SLAB_STORE == 2
       // write-through (sc1) buffer stores: the slab does not sit dirty in L2 at the kernel boundary
-      const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(a.slab + (long)blockIdx.x * (NJ * MT * 4 * 256), 0,
+      const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(a.slab + (long)bid * (NJ * MT * 4 * 256), 0,
                                                          NJ * MT * 4 * 256 * 4, 0x00020000);
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
@@ -1646,6 +1641,45 @@ __global__ __launch_bounds__(256, ROLE == 1 ? 2 : DTF_FUSED_WAVES(C, MODE_DY)) v
   }
   STAMP_DRAIN(5);
   STAMP_FLUSH(a.cin_real, nit);
+}
+
+// Trailing workgroups of a backward launch: dW slab reduction of the PREVIOUS launch (r = index among them).
+__device__ __forceinline__ void trailing_reduce(const ConvArgs& a, int r, char* smem) {
+  float* part = reinterpret_cast<float*>(smem);
+  // r_nblk reduce workgroups per member, each looping over every r_nblk-th block of 32 slab elements
+  const int bx = r % a.r_nblk, by = r / a.r_nblk;
+  if (a.r_c == 16) slab_reduce_wg<16>(a.rslab, a.rtab, a.grads, a.g_mstride, a.r_goff, bx, by, part, a.r_nblk);
+  else if (a.r_c == 32) slab_reduce_wg<32>(a.rslab, a.rtab, a.grads, a.g_mstride, a.r_goff, bx, by, part, a.r_nblk);
+  else if (a.r_c == 64) slab_reduce_wg<64>(a.rslab, a.rtab, a.grads, a.g_mstride, a.r_goff, bx, by, part, a.r_nblk);
+}
+
+template <int C, int MODE_DY, int EPI, int ROLE = 0>
+__global__ __launch_bounds__(256, ROLE == 1 ? 2 : DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_fused_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if ((int)blockIdx.x >= a.n_main) {
+    trailing_reduce(a, (int)blockIdx.x - a.n_main, smem);
+    return;
+  }
+  conv_bwd_body<C, MODE_DY, EPI, ROLE>(a, (int)blockIdx.x, smem);
+}
+
+// Dual backward (small populations, engine/hip_resnet.py DTF_DUAL_BWD): ONE launch whose workgroups take
+// different roles of the same layer -- [0, a.n_main): dgrad role (args a: staging, dgrad MFMAs, mask / stats
+// epilogue, dz out); [a.n_main, + b.n_main): wgrad role (args b: its own work split over the same (image, band)
+// iterations, the same dY / X staging, wgrad MFMAs, dW slab); then the trailing slab reduction of the previous
+// launch (a.r_*).  The two roles run side by side on different CUs, so the layer costs max(dgrad, wgrad) instead
+// of their sum while a small population leaves most CUs idle.
+template <int C, int MODE_DY, int EPI>
+__global__ __launch_bounds__(256, DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_dual_kernel(ConvArgs a, ConvArgs b) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int bx = (int)blockIdx.x;
+  if (bx < a.n_main) {
+    conv_bwd_body<C, MODE_DY, EPI, 1>(a, bx, smem);
+  } else if (bx < a.n_main + b.n_main) {
+    conv_bwd_body<C, MODE_DY, EPI & 2, 2>(b, bx - a.n_main, smem);
+  } else {
+    trailing_reduce(a, bx - a.n_main - b.n_main, smem);
+  }
 }
 
 // Sum of one member's per-workgroup dW slabs (written by conv_bwd_fused_kernel) into its gradient row.
@@ -1842,6 +1876,25 @@ DTF_API int dtf_conv_bwd_role(const ConvArgs* args, int c, int mode_dy, int epi,
   ROLE_CASE(16, 0, 0, 2) ROLE_CASE(32, 0, 0, 2) ROLE_CASE(64, 0, 0, 2)
   ROLE_CASE(16, 0, 2, 2) ROLE_CASE(32, 0, 2, 2) ROLE_CASE(64, 0, 2, 2)
 #undef ROLE_CASE
+  return -1;
+}
+
+DTF_API int dtf_conv_bwd_dual(const ConvArgs* a, const ConvArgs* b, int c, int mode_dy, int epi, int nblocks, int lds,
+                              hipStream_t stream) {
+  if (nblocks <= 0) return 0;
+  DTF_HOST_CHECK(lds <= 160 * 1024);
+  DTF_HOST_CHECK(a->work != nullptr && b->work != nullptr && a->n_main >= 0 && b->n_main >= 0);
+  DTF_HOST_CHECK(nblocks >= a->n_main + b->n_main);
+#define DUAL_CASE(CC, M, E)                                                                                  \
+  if (c == CC && mode_dy == M && epi == E) {                                                                \
+    hipLaunchKernelGGL((conv_bwd_dual_kernel<CC, M, E>), dim3(nblocks), dim3(256), lds, stream, *a, *b);    \
+    return DTF_CHECK_LAUNCH();                                                                              \
+  }
+  DUAL_CASE(16, 0, 0) DUAL_CASE(32, 0, 0) DUAL_CASE(64, 0, 0)
+  DUAL_CASE(16, 3, 0) DUAL_CASE(32, 3, 0) DUAL_CASE(64, 3, 0)
+  DUAL_CASE(16, 2, 0) DUAL_CASE(32, 2, 0) DUAL_CASE(64, 2, 0)
+  DUAL_CASE(16, 2, 1)
+#undef DUAL_CASE
   return -1;
 }
 

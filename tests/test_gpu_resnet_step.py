@@ -117,6 +117,17 @@ def test_hip_step_matches_reference(size, graph, fused, version, fold, split, mo
     _compare_step(ResNetArch(cifar_config(size, version=version)), [8, 12])
 
 
+@pytest.mark.parametrize("size,graph,dual,sizes", [(14, "1", "1", [8, 12]), (20, "0", "1", [8, 12]),
+                                                   (14, "1", "1", [16]), (8, "1", "0", [16])])
+def test_hip_step_dual_backward(size, graph, dual, sizes, monkeypatch):
+    """Dual backward (dgrad and wgrad roles of one launch, conv_bwd_dual_kernel; the default for populations of
+    <= 2 members) vs the fp32 oracle, with and without graphs, ragged and single-member populations."""
+    monkeypatch.setenv("DTF_HIP_GRAPH", graph)
+    monkeypatch.setenv("DTF_DUAL_BWD", dual)
+    monkeypatch.setenv("DTF_SPLIT_BWD", "0")
+    _compare_step(ResNetArch(cifar_config(size, version=2)), sizes)
+
+
 @pytest.mark.parametrize("size,sizes,split", [(56, [128] * 8, "0"), (56, [128], "auto"), (56, [128], "0"),
                                               (110, [128, 128], "auto")])
 def test_hip_step_benchmark_shapes(size, sizes, split, monkeypatch):

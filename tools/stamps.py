@@ -46,7 +46,7 @@ def run(args):
     for _ in range(args.steps):
         eng.train_step([m.slot for m in ms], batches, [m.hparams for m in ms], [0.1 for _ in ms])
     torch.cuda.synchronize()
-    buf = np.zeros((128, 512, 16), dtype=np.uint64)
+    buf = np.zeros((256, 512, 16), dtype=np.uint64)
     L = ops.lib()
     L.dtf_stamp_read.argtypes = [ctypes.c_void_p, ctypes.c_long]
     assert L.dtf_stamp_read(buf.ctypes.data, buf.nbytes) == 0, "not a DTF_STAMP build"

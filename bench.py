@@ -44,6 +44,10 @@ def parse():
     p.add_argument("--exploit_every", type=int, default=None,
                    help="steps between PBT exploit/explore cycles inside the timed region; default "
                         "min(25, max(1, steps // 2)) so every timed run holds at least one cycle; 0 = none")
+    p.add_argument("--exploit_lag", type=int, default=3,
+                   help="steps queued behind an exploit's loss readback before the host runs the cycle (metric "
+                        "all-gather, plan, weight copies, explore): the GPU keeps that many steps of work while the "
+                        "host gathers and plans, so the cycle does not drain the queue")
     p.add_argument("--seed", type=int, default=2024)
     p.add_argument("--graph", type=int, default=1, help="capture the population step in a HIP graph")
     p.add_argument("--profile_json", default=None)
@@ -169,16 +173,16 @@ def main():
     barrier_sync()
     images_done[0] = 0
     t0 = time.perf_counter()
-    pending = None
+    pending = []  # (due step, readback) of started exploit cycles
+    lag = max(1, args.exploit_lag)
     for k in range(args.steps):
         losses = step()
-        if pending is not None:
-            exploit_cycle(pending)  # overlaps the step just queued
-            pending = None
+        while pending and pending[0][0] <= k:
+            exploit_cycle(pending.pop(0)[1])  # overlaps the steps queued since its readback
         if args.exploit_every and (k + 1) % args.exploit_every == 0:
-            pending = exploit_start(losses)
-    if pending is not None:
-        exploit_cycle(pending)  # an exploit due after the last step still runs inside the timed region
+            pending.append((k + lag, exploit_start(losses)))
+    for _, pend in pending:
+        exploit_cycle(pend)  # an exploit due after the last step still runs inside the timed region
     barrier_sync()
     dt = time.perf_counter() - t0
     dts = comm.allgather(dt)

@@ -531,9 +531,14 @@ class _StepPlan:
         # launch (conv_bwd_dual_kernel) -- no cross-stream dependencies; the layer costs max(dgrad, wgrad) instead of
         # their sum when the population leaves CUs idle.  DTF_DUAL_BWD: "auto" (<= DTF_DUAL_MAX_POP members,
         # default 2), "1", "0".
+        # DTF_DUAL_CS: channel widths that use it (default 32, 64: at one member the C = 64 layers drop from 13.5 to
+        # 9.8 us, C = 32 from 12.2 to 11.4 us, C = 16 rises from 11.4 to 14 us -- its fused kernel already fills the
+        # GPU with single-band work items; profiles/r2_dual_pop1_breakdown.txt).
         dm = os.environ.get("DTF_DUAL_BWD", "auto")
         self.dual = (dev.type == "cuda" and not self.split and not cfg.version == 1 and (
             dm == "1" or (dm == "auto" and len(slots) <= int(os.environ.get("DTF_DUAL_MAX_POP", "2")))))
+        self.dual_cs = frozenset(int(v) for v in os.environ.get("DTF_DUAL_CS", "32,64").split(",") if v) \
+            if dm != "1" else frozenset((16, 32, 64))
         self.side_reduce = bool(self.side_cs) or self.split
         self.side_stream = torch.cuda.Stream(device=dev) if self.side_reduce else None
         self.launches = []
@@ -786,7 +791,7 @@ class _StepPlan:
         if self.split:
             return self._conv_bwd_split(ci, c, C, H, rows, bands, dy, dz_out, x, mode_dy, dy2, dy_bn, x_bn, res,
                                         ident_x, dy3, dy_out)
-        if self.dual:
+        if self.dual and C in self.dual_cs:
             return self._conv_bwd_dual(ci, c, C, H, rows, bands, dy, dz_out, x, mode_dy, dy2, dy_bn, x_bn, res,
                                        ident_x, dy3, dy_out)
         n_wg = self._fused_nwg(C, bands)

@@ -123,24 +123,50 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   }
   const bf16_t* wbase = a.w + (long)slot * a.w_mstride + a.w_off;
   const long img_elems = (long)a.Hi * a.Wi * Ci;
-  // gather position of this thread's chunk: for Ci >= 32 a 32-wide k-step lies inside one tap, so (ky, kx, ci)
-  // advance incrementally (no division in the loop); Ci < 32 (the channel-padded stem) decomposes k per step
-  int g_ky = ky0, g_kx = kx0, g_ci = 8 * cB;
+  // gather position of this thread's chunk: for Ci >= 32 a 32-wide k-step lies inside one tap, so the tap
+  // indices (ty, tx) along the (possibly parity-strided) tap grid and ci advance incrementally (no division in the
+  // loop); Ci < 32 (the channel-padded stem) decomposes k per step
   const bool inc = Ci >= 32;
   const int kstep = TRANS ? 2 : 1;
+  int g_ty = 0, g_tx = 0, g_ci = 8 * cB;
   int cur_ky = 0, cur_kx = 0, cur_ci = 0;  // position of this thread's chunk in the current k-step
+  int cur_ty = 0, cur_tx = 0;              // the same as indices into the tap grid (ky = ky0 + kstep * ty)
+  // Per-pixel gather origin, hoisted out of the k loop: tap (ty, tx) of pixel j reads row y0 + ty, column x0 + tx
+  // of the gathered image (forward: y0 = y*S - P; stride-2 data gradient: the class-grid origin), valid iff bit
+  // ty of rmask and bit tx of cmask are set; pbase = element offset of (img, y0, x0) (may be negative: only used
+  // when valid).  A k-step then costs one mask test and one add per pixel.
+  long pbase[2];
+  unsigned rmask[2], cmask[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    int y0, x0;
+    if constexpr (TRANS) {  // class pixel (2*qy + py): dy row (py + ky - pad) / 2 + qy (even numerator)
+      y0 = pix_y[j] + ((py + ky0 - a.pad) >> 1);
+      x0 = pix_x[j] + ((px + kx0 - a.pad) >> 1);
+    } else {
+      y0 = pix_y[j] * a.stride - a.pad;
+      x0 = pix_x[j] * a.stride - a.pad;
+    }
+    unsigned rm = 0, cm = 0;
+    for (int t = 0; t < nky; ++t) rm |= (unsigned)(y0 + t >= 0 && y0 + t < a.Hi) << t;
+    for (int t = 0; t < nkx; ++t) cm |= (unsigned)(x0 + t >= 0 && x0 + t < a.Wi) << t;
+    rmask[j] = pix_ok[j] ? rm : 0u;
+    cmask[j] = cm;
+    pbase[j] = (long)pix_img[j] * img_elems + ((long)y0 * a.Wi + x0) * Ci;
+  }
   auto next_pos = [&](int k0) {
     if (inc) {
-      cur_ky = g_ky;
-      cur_kx = g_kx;
+      cur_ty = g_ty;
+      cur_tx = g_tx;
+      cur_ky = ky0 + kstep * g_ty;
+      cur_kx = kx0 + kstep * g_tx;
       cur_ci = g_ci;
       g_ci += 32;
       if (g_ci >= Ci) {
         g_ci -= Ci;
-        g_kx += kstep;
-        if (g_kx >= a.kw) {
-          g_kx = kx0;
-          g_ky += kstep;
+        if (++g_tx >= nkx) {
+          g_tx = 0;
+          ++g_ty;
         }
       }
     } else {  // Ci < 32 only occurs for the (non-transposed) channel-padded stem
@@ -149,29 +175,23 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
       cur_ci = k & (Ci - 1);
       cur_ky = tap / a.kw;
       cur_kx = tap - cur_ky * a.kw;
+      cur_ty = cur_ky;
+      cur_tx = cur_kx;
     }
   };
   auto load_b = [&](int k0, uint4 (&v)[2], uint4 (&v2)[2], int& cch, unsigned& okb) {
     const int k = k0 + 8 * cB;
-    const int ky = cur_ky, kx = cur_kx, ci0 = cur_ci;
+    const int ty = cur_ty, tx = cur_tx, ci0 = cur_ci;
+    const int toff = (ty * a.Wi + tx) * Ci + ci0;
     cch = ci0;
     okb = 0;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      int gy, gx;
-      bool ok = pix_ok[j] && k < K;
-      if constexpr (TRANS) {  // class pixel (2*qy + py): dy row (py + ky - pad) / 2 + qy (even numerator)
-        gy = pix_y[j] + ((py + ky - a.pad) >> 1);
-        gx = pix_x[j] + ((px + kx - a.pad) >> 1);
-      } else {
-        gy = pix_y[j] * a.stride + ky - a.pad;
-        gx = pix_x[j] * a.stride + kx - a.pad;
-      }
-      ok = ok && gy >= 0 && gy < a.Hi && gx >= 0 && gx < a.Wi;
-      const long off = ok ? (long)pix_img[j] * img_elems + ((long)gy * a.Wi + gx) * Ci + ci0 : -1;
+      const bool ok = ((rmask[j] >> ty) & (cmask[j] >> tx) & 1u) && k < K;
       v[j] = make_uint4(0, 0, 0, 0);
       v2[j] = make_uint4(0, 0, 0, 0);
-      if (off >= 0) {
+      if (ok) {
+        const long off = pbase[j] + toff;
         v[j] = *reinterpret_cast<const uint4*>(a.x + off);
         if constexpr (MODE == 2) v2[j] = *reinterpret_cast<const uint4*>(a.x2 + off);
         okb |= 1u << j;  // unset: zero padding (stays zero after the transform)
@@ -438,25 +458,41 @@ __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
       r -= d;
     }
   };
+  // Pixel table of a k-step (32 output pixels), computed by the first 32 threads one k-step ahead and shared
+  // through LDS (every pixel used to be decomposed by all 16 column-chunk threads of its row):
+  // {dy element offset, x image base, oy*S - P, ox*S - P}; an out-of-range pixel gets oy*S - P = -2^30.
+  __shared__ int4 pinfo[2][32];
+  auto make_pinfo = [&](int pk0) {
+    if (tid < 32) {
+      const int p = pk0 + tid;
+      int4 inf = make_int4(0, 0, -(1 << 30), 0);
+      if (p < p1) {
+        int img, rem, oy, ox;
+        divmod(p, HWo, r_hw, img, rem);
+        divmod(rem, a.Wo, r_w, oy, ox);
+        inf = make_int4((int)((unsigned)p * (unsigned)Co), (int)((unsigned)img * (unsigned)img_x),
+                        oy * a.stride - a.pad, ox * a.stride - a.pad);
+      }
+      pinfo[(pk0 - p0) / 32 & 1][tid] = inf;
+    }
+  };
   auto load = [&](int pk0, uint4 (&dv)[2], uint4 (&dv2)[2], uint4 (&xv)[2], unsigned& okm) {
     okm = 0;
+    const int par = (pk0 - p0) / 32 & 1;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int p = pk0 + kr + 16 * j;
-      const bool pin = p < p1;
-      const int pp = pin ? p : p0;
-      int img, rem, oy, ox;
-      divmod(pp, HWo, r_hw, img, rem);
-      divmod(rem, a.Wo, r_w, oy, ox);
+      const int4 inf = pinfo[par][kr + 16 * j];
+      const bool pin = inf.z > -(1 << 29);
       dv[j] = dv2[j] = xv[j] = make_uint4(0, 0, 0, 0);
       if (pin && dcol_ok) {
-        dv[j] = *reinterpret_cast<const uint4*>(a.dy + (long)pp * Co + dcol);
-        if constexpr (MODE_DY == 2) dv2[j] = *reinterpret_cast<const uint4*>(a.dy2 + (long)pp * Co + dcol);
+        const bf16_t* dp = a.dy + (unsigned)inf.x + dcol;
+        dv[j] = *reinterpret_cast<const uint4*>(dp);
+        if constexpr (MODE_DY == 2) dv2[j] = *reinterpret_cast<const uint4*>(a.dy2 + (unsigned)inf.x + dcol);
         okm |= 1u << j;
       }
-      const int gy = oy * a.stride + xky - a.pad, gx = ox * a.stride + xkx - a.pad;
+      const int gy = inf.z + xky, gx = inf.w + xkx;
       if (pin && xcol_ok && gy >= 0 && gy < a.Hi && gx >= 0 && gx < a.Wi) {
-        xv[j] = *reinterpret_cast<const uint4*>(a.x + img * img_x + ((long)gy * a.Wi + gx) * Ci + xci);
+        xv[j] = *reinterpret_cast<const uint4*>(a.x + (unsigned)inf.y + (unsigned)((gy * a.Wi + gx) * Ci + xci));
         okm |= 4u << j;
       }
     }
@@ -505,8 +541,10 @@ __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
   for (int m = 0; m < 4; ++m)
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[m][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  __syncthreads();
   const int nk = (p1 - p0 + 31) / 32;
+  make_pinfo(p0);
+  if (nk > 1) make_pinfo(p0 + 32);
+  __syncthreads();  // coefficients + the first two pixel tables
   uint4 dv[2], dv2[2], xv[2];
   unsigned okm;
   load(p0, dv, dv2, xv, okm);
@@ -517,6 +555,8 @@ __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
     const int cur = ks & 1;
     const bool more = ks + 1 < nk;
     if (more) load(p0 + 32 * (ks + 1), dv, dv2, xv, okm);
+    // table of k-step ks + 2 into the slot k-step ks read (its readers passed the previous barrier)
+    if (ks + 2 < nk) make_pinfo(p0 + 32 * (ks + 2));
     bf16x8_t fa[4], fb[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {

@@ -414,6 +414,10 @@ class _ImageNetPlan:
             trans = (1 if c.stride > 1 else 0) | 2  # | 2: A operand k-major from the forward layout
         a.log2ci = _log2(a.Ci)
         tc = 128 if a.Co >= 128 else 64
+        if a.Co >= 256 and os.environ.get("DTF_CG_TC256", "0") == "1":
+            # 128 x 64 per wave: more MFMA work per LDS byte, but one wave per SIMD -- measured slower (pop 8 x 128:
+            # 111.7 -> 123.4 ms/step, profiles/r2_imagenet_tc256_ab.log), so off
+            tc = 256
         work = (self._pix_work(hw_in, a.Co, tc, classes=(0, 1, 2, 3)) if trans & 1
                 else self._pix_work(hw_out, a.Co, tc))
         a.work = _p(work)

@@ -36,7 +36,12 @@ from .. import ops
 from ..data.datasets import IndexBatch, batch_len
 from ..models.resnet import BN_EPS
 
-NREP = int(os.environ.get("DTF_NREP", "8"))  # BN stat replicas: must match the build (common.h DTF_NREP)
+def _nrep() -> int:
+    """BN statistic replicas: must match the loaded build (common.h DTF_NREP; 64 in the deterministic build)."""
+    return 64 if ops.deterministic_mode() else int(os.environ.get("DTF_NREP", "8"))
+
+
+DET_WG_PER_MEMBER = 64  # deterministic mode: statistic-producing launches use <= this many workgroups per member
 c_void_p, c_int, c_long = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
 
 
@@ -301,6 +306,10 @@ class HipResNetBackend:
         self.wf = torch.zeros(cap, self.L.wtot, dtype=torch.bfloat16, device=self.dev)
         self.wd = torch.zeros(cap, self.L.wtot, dtype=torch.bfloat16, device=self.dev)
         nb = len(self.L.prog.bns)
+        self.det = ops.deterministic_mode()
+        if self.det and self.L.cfg.version != 2:
+            raise ValueError("the deterministic HIP build covers the ResNet v2 step; use --backend torch for v1")
+        NREP = self.nrep = _nrep()
         self.stats_bn_stride = cap * NREP * 128
         # [fwd | bwd] statistic accumulators: zeroed by ONE memset per step
         # [fwd | bwd] statistic accumulators + per-member loss / correct count: ONE buffer, zeroed by the step's
@@ -479,8 +488,8 @@ class _StepPlan:
             nb = len(prog.bns)
             cap = e.capacity
             # moving statistics in accumulator form (bn_eval_stats) + a sink for the conv epilogues' statistics
-            self.ev_stats = torch.zeros(nb, cap, NREP, 128, dtype=torch.float32, device=dev)
-            self.ev_sink = torch.zeros(cap, NREP, 128, dtype=torch.float32, device=dev)
+            self.ev_stats = torch.zeros(nb, cap, be.nrep, 128, dtype=torch.float32, device=dev)
+            self.ev_sink = torch.zeros(cap, be.nrep, 128, dtype=torch.float32, device=dev)
             self.ev_acc = torch.zeros(2, cap, dtype=torch.float32, device=dev)  # [correct, summed mean CE] per slot
             self.logits = None  # [N, ncls] fp32 when requested (tests)
             self._work_cache, self._uniform_geo = {}, {}
@@ -596,7 +605,19 @@ class _StepPlan:
     def _n_wg_iters(self, total_iters, per_wg=4, lo=256, hi=1024):
         """Enough (image, band) iterations per workgroup for the double-buffered pipeline,
         while keeping >= lo workgroups (fill 256 CUs) when the batch allows."""
-        return int(max(lo, min(hi, total_iters // per_wg)))
+        return self._det_cap(int(max(lo, min(hi, total_iters // per_wg))))
+
+    def _det_cap(self, n_wg):
+        """Deterministic mode: at most DET_WG_PER_MEMBER workgroups per member, so each statistic replica of a
+        member receives at most one atomic add (onto zero) per launch."""
+        if self.be.det:
+            return min(n_wg, DET_WG_PER_MEMBER * len(self.slots))
+        return n_wg
+
+    def _head_items(self):
+        # deterministic mode: one head workgroup per member (its dense-gradient / statistic atomics are then the
+        # only writers)
+        return len(self.slots) if self.be.det else int(os.environ.get("DTF_HEAD_ITEMS", "512"))
 
     def _work_member(self, target_items=256, min_chunk=1):
         key = ("m", target_items)
@@ -742,6 +763,8 @@ class _StepPlan:
         # bound fp32 atomic traffic (~12 MB / launch) and same-address contention (<= 128 WGs per member)
         per_member = int(os.environ.get("DTF_WGRAD_WG_PER_MEMBER", "128"))
         n_wg = max(64, min(per_member * len(self.slots), int(12e6 / (4.0 * wn))))
+        if self.be.det:
+            n_wg = len(self.slots)  # one workgroup per member: every dW element is added once (fixed order)
         work = self._work_iters(Ho // rows, n_wg)
         a = self._base_args()
         a.x, a.dy, a.dy2 = _p(x), _p(dy), _p(dy2)
@@ -919,7 +942,7 @@ class _StepPlan:
         epi = int(res is not None) | (2 if ident_x else 0)
         # ---- dgrad role
         nd = int(os.environ.get("DTF_DUAL_DG_ITERS", "1"))
-        work = self._work_iters(bands, max(1, (self.N * bands) // nd))
+        work = self._work_iters(bands, self._det_cap(max(1, (self.N * bands) // nd)))
         a = self._base_args()
         a.x, a.x2, a.y, a.xm, a.res = _p(dy), _p(dy2), _p(dz_out), _p(x), _p(res)
         a.x3, a.xout = _p(dy3), _p(dy_out if mode_dy >= 2 else None)
@@ -1030,7 +1053,7 @@ class _StepPlan:
         cap = int(os.environ.get("DTF_FUSED_MAX_WG_%d" % C, {32: "128"}.get(C, "0")))
         if cap > 0:
             n_wg = min(n_wg, cap * len(self.slots))
-        return min(n_wg, self.N * bands)
+        return self._det_cap(min(n_wg, self.N * bands))
 
     def _slab_floats(self):
         cfg = self.be.L.cfg
@@ -1127,7 +1150,7 @@ class _StepPlan:
         # head (fwd + bwd of GAP/dense/CE + final-BN reductions)
         fb = prog.final_bn
         hw = L.final_hw
-        hwork = self._work_member(target_items=int(os.environ.get("DTF_HEAD_ITEMS", "512")))
+        hwork = self._work_member(target_items=self._head_items())
         ha = HeadArgs()
         ha.x, ha.labels, ha.work = _p(self.xs[-1]), _p(self.labels), _p(hwork)
         ha.params, ha.p_mstride = _p(e.state), e.S

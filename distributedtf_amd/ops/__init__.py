@@ -43,12 +43,15 @@ def lib():
         if _LIB is None:
             # DTF_LIB: an alternative build of the same sources (e.g. timing-only ablation builds of tools/)
             debug = debug_mode()
-            default = _build.LIB_DEBUG if debug else _build.LIB
+            det = deterministic_mode()
+            default = _build.LIB_DEBUG if debug else (_build.LIB_DET if det else _build.LIB)
             path = os.environ.get("DTF_LIB") or default
             if path == default and (not os.path.isfile(path) or
                                     (os.environ.get("DTF_REBUILD") == "1" and _build.needs_build(path))):
                 if debug:
                     _build.build_debug(verbose=False)
+                elif det:
+                    _build.build_det(verbose=False)
                 else:
                     _build.build(verbose=False)
             if not os.path.isfile(path):
@@ -62,6 +65,12 @@ def lib():
                 fn.restype = c_int
             _LIB = _DebugLib(L) if debug else L
     return _LIB
+
+
+def deterministic_mode() -> bool:
+    """DTF_DETERMINISTIC=1 (set by ``--deterministic``): the deterministic kernel build (64 statistic replicas) and
+    workgroup caps that make every reduction order fixed (engine/hip_resnet.py)."""
+    return os.environ.get("DTF_DETERMINISTIC", "0") == "1"
 
 
 def debug_mode() -> bool:

@@ -21,6 +21,11 @@ LIB = os.path.join(HERE, "libdtf_kernels.so")
 # trapping, host-side launch-argument checks; -g).  Loaded instead of LIB when DTF_DEBUG=1 (ops.lib()).
 LIB_DEBUG = os.path.join(HERE, "libdtf_kernels_debug.so")
 DEBUG_FLAGS = ["-DDTF_DEBUG=1", "-g"]
+# Deterministic build (--deterministic / DTF_DETERMINISTIC=1): 64 BatchNorm-statistic replicas, so that with at
+# most 64 workgroups per member per launch (engine/hip_resnet.py caps them) every replica receives at most one
+# atomic add onto zero and the consumers sum the replicas in a fixed order -- bitwise-replayable statistics.
+LIB_DET = os.path.join(HERE, "libdtf_kernels_det.so")
+DET_FLAGS = ["-DDTF_DETERMINISTIC=1", "-DDTF_NREP=64"]
 ARCH = os.environ.get("DTF_OFFLOAD_ARCH", "gfx950")
 
 
@@ -82,8 +87,14 @@ def build_debug(force: bool = False, verbose: bool = True) -> str:
     return build(force=force, verbose=verbose, extra_flags=DEBUG_FLAGS, out=LIB_DEBUG)
 
 
+def build_det(force: bool = False, verbose: bool = True) -> str:
+    return build(force=force, verbose=verbose, extra_flags=DET_FLAGS, out=LIB_DET)
+
+
 if __name__ == "__main__":
     if "--debug" in sys.argv:
         build_debug(force="--force" in sys.argv)
+    elif "--det" in sys.argv:
+        build_det(force="--force" in sys.argv)
     else:
         build(force="--force" in sys.argv)

@@ -397,9 +397,12 @@ __device__ __forceinline__ void make_coef(float* coef, const ConvArgs& a, int sl
 // kernel (before its tile and weight loads), coef_finish derives the coefficients once they have arrived -- the
 // in-order vmcnt wait then covers only the statistics, the tile / weight loads stay in flight behind them.
 // MODE 1: forward scale/shift (st_f, gamma, beta); MODE 2/3: backward A, B, C (st_f, st_b, gamma).
+// With many replicas (deterministic builds: DTF_NREP = 64, one per workgroup of a member) the loads are summed as
+// they are issued (in replica order) instead of being held in registers.
+constexpr int CREP = NREP <= 8 ? NREP : 1;
 template <int MODE>
 struct CoefLd {
-  float fs[NREP], fq[NREP], bs[MODE >= 2 ? NREP : 1], bq[MODE >= 2 ? NREP : 1];
+  float fs[CREP], fq[CREP], bs[MODE >= 2 ? CREP : 1], bq[MODE >= 2 ? CREP : 1];
   float g, b;
 };
 
@@ -410,17 +413,33 @@ __device__ __forceinline__ void coef_issue(CoefLd<MODE>& L, const ConvArgs& a, i
   const int c = threadIdx.x;
   if (c < C) {
     const float* rf = stats_row(st_f, slot) + c;
+    if constexpr (CREP == NREP) {
 #pragma unroll
-    for (int r = 0; r < NREP; ++r) {
-      L.fs[r] = rf[r * 128];
-      L.fq[r] = rf[r * 128 + 64];
+      for (int r = 0; r < NREP; ++r) {
+        L.fs[r] = rf[r * 128];
+        L.fq[r] = rf[r * 128 + 64];
+      }
+    } else {
+      L.fs[0] = L.fq[0] = 0.f;
+      for (int r = 0; r < NREP; ++r) {
+        L.fs[0] += rf[r * 128];
+        L.fq[0] += rf[r * 128 + 64];
+      }
     }
     if constexpr (MODE >= 2) {
       const float* rb = stats_row(st_b, slot) + c;
+      if constexpr (CREP == NREP) {
 #pragma unroll
-      for (int r = 0; r < NREP; ++r) {
-        L.bs[r] = rb[r * 128];
-        L.bq[r] = rb[r * 128 + 64];
+        for (int r = 0; r < NREP; ++r) {
+          L.bs[r] = rb[r * 128];
+          L.bq[r] = rb[r * 128 + 64];
+        }
+      } else {
+        L.bs[0] = L.bq[0] = 0.f;
+        for (int r = 0; r < NREP; ++r) {
+          L.bs[0] += rb[r * 128];
+          L.bq[0] += rb[r * 128 + 64];
+        }
       }
     }
     const float* prow = a.params + (long)slot * a.p_mstride;
@@ -434,7 +453,7 @@ template <int MODE>
 __device__ __forceinline__ void coef_moments(const CoefLd<MODE>& L, float n, float& mean, float& inv) {
   float s = 0.f, q = 0.f;
 #pragma unroll
-  for (int r = 0; r < NREP; ++r) {
+  for (int r = 0; r < CREP; ++r) {
     s += L.fs[r];
     q += L.fq[r];
   }
@@ -456,7 +475,7 @@ __device__ __forceinline__ void coef_finish(float* coef, const CoefLd<MODE>& L, 
     } else {
       float sdz = 0.f, sdzx = 0.f;
 #pragma unroll
-      for (int r = 0; r < NREP; ++r) {
+      for (int r = 0; r < CREP; ++r) {
         sdz += L.bs[r];
         sdzx += L.bq[r];
       }
@@ -488,6 +507,21 @@ __device__ __forceinline__ void reduce_stats_to_lds(float* acc_lds, const float 
     ss[r] = a;
     qq[r] = b;
   }
+#ifdef DTF_DETERMINISTIC
+  // waves that share channels add in wave order (the LDS float adds are then order-fixed); callers invoke this
+  // with workgroup-uniform control flow
+  const int wv = (int)threadIdx.x >> 6;
+  for (int w = 0; w < (int)blockDim.x / 64; ++w) {
+    if (wv == w && (lane & 15) == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        acc_lds[ch0 + r] += ss[r];
+        acc_lds[64 + ch0 + r] += qq[r];
+      }
+    }
+    __syncthreads();
+  }
+#else
   if ((lane & 15) == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -495,6 +529,7 @@ __device__ __forceinline__ void reduce_stats_to_lds(float* acc_lds, const float 
       atomicAdd(&acc_lds[64 + ch0 + r], qq[r]);
     }
   }
+#endif
 }
 
 __device__ __forceinline__ void flush_stats_r(float* st_out, const float* acc_lds, int slot, int nch, int rep) {

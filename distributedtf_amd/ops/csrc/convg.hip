@@ -66,10 +66,9 @@ constexpr int RP = 40;    // [rows][32] tile pitch (+16 B)
 // AKM (data gradient): the A operand (rows = dx channels i, k = (tap', dy channel o)) is read straight from the
 // FORWARD weight layout W[o][tap][i] (k-major: 8 consecutive i per 16-byte load, fragments via
 // ds_read_b64_tr_b16), so no transposed weight copy exists.
-constexpr int KPA = 128 + 8;  // [32][TC] k-major A tile pitch
-
 template <int TC, int MODE, int EPI, bool TRANS, bool AKM = false>
 __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
+  constexpr int KPA = TC + 8;  // [32][TC] k-major A tile pitch
   constexpr int MT = TC / 32;  // MFMA row tiles per wave (wave covers TC/2 rows)
   constexpr int SA = (TC * RP > 32 * KPA) ? TC * RP : 32 * KPA;
   __shared__ __attribute__((aligned(16))) bf16_t sa[2][SA];
@@ -104,7 +103,7 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
       if constexpr (MODE == 2) dyn[2 * Ci + i] = cb[2 * a.cmax + i];
     }
   }
-  if (tid < 2 * TC) (&acc_lds[0][0])[tid] = 0.f;
+  for (int i = tid; i < 2 * TC; i += 256) (&acc_lds[0][0])[i] = 0.f;
   // per-thread B rows (pixels): r = (tid >> 2) + 64 j, chunk c = tid & 3
   const int cB = tid & 3;
   int pix_img[2], pix_y[2], pix_x[2];
@@ -622,7 +621,9 @@ DTF_API int dtf_convg_fwd(const CgArgs* a, int tc, int mode, int epi, int trans,
     hipLaunchKernelGGL((convg_fwd_kernel<TC_, M_, E_, T_, true>), grid, block, dyn, stream, *a); \
     return DTF_CHECK_LAUNCH();                                                                    \
   }
-#define CG_ALL_TC(M_, E_, T_) CG_CASE(64, M_, E_, T_) CG_CASE(128, M_, E_, T_)
+// TC = 256 (Co >= 256): a 128 x 64 tile per wave -- 1.33x the MFMA work per LDS byte of the 64 x 64 tile, whose
+// operand reads alone saturate the LDS bandwidth at the MFMA rate
+#define CG_ALL_TC(M_, E_, T_) CG_CASE(64, M_, E_, T_) CG_CASE(128, M_, E_, T_) CG_CASE(256, M_, E_, T_)
   // forward: identity (stem / v1) or BN+ReLU prologue; stats epilogue; optional residual
   CG_ALL_TC(0, 4, false)
   CG_ALL_TC(0, 5, false)

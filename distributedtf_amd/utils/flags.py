@@ -127,8 +127,9 @@ def build_parser(defaults: Optional[Dict[str, Any]] = None) -> argparse.Argument
     p.add_argument("--tf_checkpoint", action="store_true",
                    help="also write each member's checkpoint as a TF 1.x tensor bundle (model.ckpt-<step>.*)")
     p.add_argument("--deterministic", action="store_true",
-                   help="replayable run: seeded RNGs, deterministic torch algorithms, torch backend (the HIP kernels "
-                        "reduce BatchNorm statistics with fp32 atomics, so they are not bitwise replayable)")
+                   help="bitwise-replayable run: seeded RNGs; the CIFAR ResNet v2 HIP step runs the deterministic "
+                        "kernel build (fixed-order BatchNorm-statistic and weight-gradient reductions, "
+                        "libdtf_kernels_det.so); other families use deterministic torch algorithms")
     p.add_argument("--debug_kernels", action="store_true",
                    help="serialise and synchronise every kernel launch (AMD_SERIALIZE_KERNEL=3, HIP_LAUNCH_BLOCKING"
                         "=1), no HIP graphs: a faulting kernel is reported at its own launch")
@@ -195,8 +196,10 @@ class MainArgs(argparse.Namespace):
             torch.use_deterministic_algorithms(True, warn_only=True)
             torch.backends.cudnn.benchmark = False
             torch.backends.cudnn.deterministic = True
-            if self.backend == "auto":
-                self.backend = "torch"
+            os.environ["DTF_DETERMINISTIC"] = "1"  # ops.lib() loads the deterministic build
+            hip_det = self.model == "cifar10" and int(getattr(self, "resnet_version", 2)) == 2
+            if self.backend == "auto" and not hip_det:
+                self.backend = "torch"  # the MNIST / ImageNet / v1 HIP paths keep atomic reductions
 
     def inject_nan_schedule(self) -> Dict[int, List[int]]:
         out: Dict[int, List[int]] = {}

@@ -94,3 +94,25 @@ def test_fp16_loss_scaled_training_is_finite(tmp_path, monkeypatch):
     _run(tmp_path, monkeypatch, "--rounds", "1", "--max_train_steps", "2", "--dtype", "fp32", "--loss_scale", "64")
     best = json.load(open("savedata/best_model.json"))
     assert best["best_acc"] == best["best_acc"]
+
+
+def test_deterministic_flag_selects_det_build(monkeypatch):
+    """--deterministic keeps the HIP backend for the CIFAR ResNet v2 step (deterministic kernel build, selected by
+    DTF_DETERMINISTIC) and moves the families whose HIP kernels keep atomic reductions to the torch backend."""
+    from distributedtf_amd import ops
+    from distributedtf_amd.ops import build as kb
+    from distributedtf_amd.utils.flags import parse_main_args
+    monkeypatch.delenv("DTF_DETERMINISTIC", raising=False)
+    a = parse_main_args(["--model", "cifar10", "--deterministic"])
+    a.apply_runtime_modes()
+    try:
+        assert os.environ.get("DTF_DETERMINISTIC") == "1" and ops.deterministic_mode()
+        assert a.backend == "auto" and a.seed == 0
+        b = parse_main_args(["--model", "mnist", "--deterministic"])
+        b.apply_runtime_modes()
+        assert b.backend == "torch"
+        assert kb.LIB_DET.endswith("libdtf_kernels_det.so") and "-DDTF_NREP=64" in kb.DET_FLAGS
+    finally:
+        os.environ.pop("DTF_DETERMINISTIC", None)
+        import torch
+        torch.use_deterministic_algorithms(False)

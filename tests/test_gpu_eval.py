@@ -5,6 +5,8 @@ BatchNorm with the moving mean / variance, accuracy over the whole eval set.  Th
 the batch statistics of a calibration batch (momentum 0 for one fp32 training-mode forward) so the eval activations
 stay normalised through every layer, as after real training.
 """
+import os
+
 import pytest
 import torch
 
@@ -139,3 +141,22 @@ def test_hip_imagenet_eval_matches_reference(monkeypatch):
     for s in range(2):
         acc16 = float((r16[s].argmax(1) == y).float().mean())
         assert acc[s] >= acc16 - 0.2, (s, acc[s], acc16)
+
+
+def test_deterministic_build_is_bitwise_replayable():
+    """--deterministic on the HIP path (verdict r1 #10): the deterministic kernel build (64 statistic replicas, one
+    atomic per replica, wave-ordered LDS reductions, one wgrad / head workgroup per member) replays bitwise.  Runs in
+    a subprocess: the library is chosen when it is first loaded."""
+    import subprocess
+    import sys as _sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DTF_DETERMINISTIC="1")
+    r = subprocess.run([_sys.executable, os.path.join(root, "tools", "det_check.py")], env=env, capture_output=True,
+                       text=True, timeout=240)
+    print(r.stdout[-2000:])
+    assert r.returncode == 0 and "DET_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+    # and the deterministic step matches the fp32 oracle like the regular build (ResNet-14, ragged pop 2, graphs)
+    r = subprocess.run([_sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
+                        os.path.join(root, "tests", "test_gpu_resnet_step.py") + "::test_hip_step_matches_reference",
+                        "-k", "14-1-1-2-1-0"], env=env, capture_output=True, text=True, timeout=240, cwd=root)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]

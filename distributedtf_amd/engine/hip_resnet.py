@@ -62,6 +62,10 @@ class ConvArgs(ctypes.Structure):
     ]
 
 
+class SlabJob(ctypes.Structure):
+    _fields_ = [("slab", c_void_p), ("red", c_void_p), ("g_off", c_long), ("nmem", c_int), ("pad", c_int)]
+
+
 class BnBwdArgs(ctypes.Structure):
     _fields_ = [
         ("dz", c_void_p), ("x", c_void_p), ("add", c_void_p), ("out", c_void_p), ("img_slot", c_void_p),
@@ -107,6 +111,8 @@ def _register():
     ops.register("dtf_conv_bwd_fused", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_bwd_role", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_bwd_dual", [P(ConvArgs), P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
+    ops.register("dtf_dw_slab_reduce_multi", [c_void_p, c_int, c_int, c_void_p, c_long, c_int, c_void_p])
+    ops.register("dtf_slab_job_size", [])
     ops.register("dtf_conv_args_size", [])
     ops.register("dtf_bnbwd_args_size", [])
     ops.register("dtf_head_args_size", [])
@@ -132,6 +138,7 @@ def _register():
             fn.argtypes = args
             fn.restype = c_int
     assert L.dtf_conv_args_size() == ctypes.sizeof(ConvArgs), "ConvArgs ABI mismatch"
+    assert L.dtf_slab_job_size() == ctypes.sizeof(SlabJob), "SlabJob ABI mismatch"
     assert L.dtf_bnbwd_args_size() == ctypes.sizeof(BnBwdArgs), "BnBwdArgs ABI mismatch"
     assert L.dtf_head_args_size() == ctypes.sizeof(HeadArgs), "HeadArgs ABI mismatch"
     assert L.dtf_bnew_args_size() == ctypes.sizeof(BnEwArgs), "BnEwArgs ABI mismatch"
@@ -553,8 +560,12 @@ class _StepPlan:
         self.launches = []
         self._pending_slab = None  # (slab ptr, reduce table, C, grad offset) of the last fused launch
         self._slab_flip = 0
+        # C = 64 dW slabs reduced together by ONE launch after the backward (instead of 17 small reductions):
+        # every such layer keeps its own slab (DTF_DEFER_C64)
+        self.defer64 = dev.type == "cuda" and os.environ.get("DTF_DEFER_C64", "1") == "1"
+        self._deferred = []
         self._build()
-        assert self._pending_slab is None, "every dW slab must be reduced before the optimizer"
+        assert self._pending_slab is None and not self._deferred, "every dW slab must be reduced before the optimizer"
         self.graph = None
 
     # -------------------------------------------------------------------- work lists
@@ -845,8 +856,21 @@ class _StepPlan:
         if C == 64 and os.environ.get("DTF_DW_SLAB_C64", "1") != "1":
             slab = False  # fp32 atomics straight into the gradient row (no reduce launch)
         side = slab and C in self.side_cs
+        defer = slab and not side and C == 64 and self.defer64
         n_red = 0
-        if slab and not side:
+        if defer:
+            # own slab, reduced after the backward; the previous launch's pending slab still rides on this launch
+            pend = self._pending_slab
+            if pend is not None and self._piggyback(pend):
+                buf, red, rc, goff = pend
+                a.rslab, a.rtab, a.r_c, a.r_goff = buf, _p(red), rc, goff
+                a.r_nblk = self._reduce_wgs(rc, work.shape[0], red.shape[0])
+                n_red = a.r_nblk * red.shape[0]
+                self._pending_slab = None
+            else:
+                self._flush_slab()
+            a.slab = _p(self._layer_slab(work.shape[0] * self._slab_elems(C)))
+        elif slab and not side:
             # ping-pong slab buffers: this launch writes one while its trailing workgroups reduce the other
             pend = self._pending_slab
             if pend is not None and self._piggyback(pend):
@@ -871,6 +895,8 @@ class _StepPlan:
             if side:
                 self._add("side", (lib.dtf_dw_slab_reduce, (a.slab, _p(red), red.shape[0], _p(self.e.grads),
                                                             self.e.Pp, c.off, C)))
+            elif defer:
+                self._deferred.append((a.slab, red, c.off))
             else:
                 self._pending_slab = (a.slab, red, C, c.off)
 
@@ -994,7 +1020,10 @@ class _StepPlan:
         lds = 2304 + 4 * tsz * 2  # the wgrad role's dY + X tiles (double-buffered); the dgrad role uses half
         self._add(lib.dtf_conv_bwd_dual, ctypes.byref(a), ctypes.byref(b), C, mode_dy, epi,
                   a.n_main + b.n_main + n_red, lds)
-        self._pending_slab = (b.slab, self._slab_table(wwork), C, c.off)
+        if C == 64 and self.defer64:
+            self._deferred.append((b.slab, self._slab_table(wwork), c.off))
+        else:
+            self._pending_slab = (b.slab, self._slab_table(wwork), C, c.off)
 
     def _piggyback(self, pend):
         """Reduce the previous launch's slabs inside the next fused launch when that adds few workgroups
@@ -1025,6 +1054,21 @@ class _StepPlan:
             t += per_wave
         t = int(os.environ.get("DTF_PIGGYBACK_C64_WGS", t))
         return max(1, min(nb, t // max(1, n_members)))
+
+    def _flush_deferred(self):
+        """One reduction launch over every deferred C = 64 slab (dw_slab_reduce_multi_kernel)."""
+        if not self._deferred:
+            return
+        jobs = (SlabJob * len(self._deferred))()
+        nmax = 0
+        for i, (buf, red, goff) in enumerate(self._deferred):
+            jobs[i] = SlabJob(buf, _p(red), goff, red.shape[0], 0)
+            nmax = max(nmax, red.shape[0])
+        jt = torch.frombuffer(bytearray(bytes(jobs)), dtype=torch.uint8).to(self.be.dev)
+        self._keep(jt)
+        self._add(ops.lib().dtf_dw_slab_reduce_multi, _p(jt), len(self._deferred), nmax, _p(self.e.grads),
+                  self.e.Pp, 64)
+        self._deferred = []
 
     def _flush_slab(self):
         """Standalone reduction of a pending slab (no later fused launch can take it)."""
@@ -1220,6 +1264,7 @@ class _StepPlan:
         self._conv_wgrad(prog.stem, self.xin16, g_cur, mode_x=0, mode_dy=0, cin_real=cfg.in_channels)
         # BN parameter gradients from the backward reductions
         self._flush_slab()
+        self._flush_deferred()
         self._add(lib.dtf_bn_running_update, _p(e.state), e.S, 3 * e.Pp, _p(be.bn_table_t), len(L.bn_table),
                   _p(be.stats[1]), be.stats_bn_stride, _p(self.slots_t), nslots, _p(self.cnt), _p(e.grads), e.Pp)
         # optimizer over every member row (+ zero grads), step counters
@@ -1438,6 +1483,7 @@ class _StepPlan:
         self._conv_wgrad(prog.stem, self.xin16, d, mode_x=0, mode_dy=2, dy_bn=prog.stem_bn, dy2=self.h0,
                          cin_real=cfg.in_channels)
         self._flush_slab()
+        self._flush_deferred()
         self._add(lib.dtf_bn_running_update, _p(e.state), e.S, 3 * e.Pp, _p(be.bn_table_t), len(L.bn_table),
                   _p(be.stats[1]), be.stats_bn_stride, _p(self.slots_t), nslots, _p(self.cnt), _p(e.grads), e.Pp)
         self._add("optim", None)

@@ -1730,6 +1730,25 @@ __global__ __launch_bounds__(256) void dw_slab_reduce_kernel(const float* __rest
   slab_reduce_wg<C>(slab, red, grads, g_mstride, g_off, blockIdx.x, blockIdx.y, part, gridDim.x);
 }
 
+// One launch for the dW slabs of several layers (deferred C = 64 reductions, engine/hip_resnet.py DTF_DEFER_C64):
+// blockIdx.z = layer, y = member row of that layer's reduce table, x = 32-element block.
+struct SlabJob {
+  const float* slab;
+  const int4* red;
+  long g_off;
+  int nmem;
+  int pad;
+};
+
+template <int C>
+__global__ __launch_bounds__(256) void dw_slab_reduce_multi_kernel(const SlabJob* __restrict__ jobs,
+                                                                   float* __restrict__ grads, long g_mstride) {
+  __shared__ float part[8 * 33];
+  const SlabJob j = jobs[blockIdx.z];
+  if ((int)blockIdx.y >= j.nmem) return;  // workgroup-uniform
+  slab_reduce_wg<C>(j.slab, j.red, grads, g_mstride, j.g_off, blockIdx.x, blockIdx.y, part, gridDim.x);
+}
+
 template <typename KernelT>
 int launch(KernelT k, int nblocks, size_t lds, hipStream_t st, const ConvArgs& a) {
   if (nblocks <= 0) return 0;
@@ -1797,6 +1816,26 @@ DTF_API int dtf_dw_slab_reduce(const float* slab, const int4* red, int nmembers,
   RED_CASE(32)
   RED_CASE(64)
 #undef RED_CASE
+  return -1;
+}
+
+DTF_API int dtf_slab_job_size() { return (int)sizeof(SlabJob); }
+
+DTF_API int dtf_dw_slab_reduce_multi(const void* jobs, int njobs, int max_members, float* grads, long g_mstride, int c,
+                                     hipStream_t stream) {
+  if (njobs <= 0 || max_members <= 0) return 0;
+  DTF_HOST_CHECK(jobs != nullptr && njobs <= 65535);
+#define REDM_CASE(CC)                                                                                        \
+  if (c == CC) {                                                                                            \
+    constexpr int E = ((9 * CC / 16 + 3) / 4) * (CC / 16) * 4 * 256;                                         \
+    hipLaunchKernelGGL(dw_slab_reduce_multi_kernel<CC>, dim3(E / 32, max_members, njobs), dim3(256), 0,     \
+                       stream, reinterpret_cast<const SlabJob*>(jobs), grads, g_mstride);                   \
+    return DTF_CHECK_LAUNCH();                                                                              \
+  }
+  REDM_CASE(16)
+  REDM_CASE(32)
+  REDM_CASE(64)
+#undef REDM_CASE
   return -1;
 }
 

@@ -66,6 +66,10 @@ class SlabJob(ctypes.Structure):
     _fields_ = [("slab", c_void_p), ("red", c_void_p), ("g_off", c_long), ("nmem", c_int), ("pad", c_int)]
 
 
+class DenseJob(ctypes.Structure):
+    _fields_ = [("slab", c_void_p), ("red", c_void_p), ("g_off", c_long), ("kel", c_int), ("nmem", c_int)]
+
+
 class BnBwdArgs(ctypes.Structure):
     _fields_ = [
         ("dz", c_void_p), ("x", c_void_p), ("add", c_void_p), ("out", c_void_p), ("img_slot", c_void_p),
@@ -113,6 +117,8 @@ def _register():
     ops.register("dtf_conv_bwd_dual", [P(ConvArgs), P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_dw_slab_reduce_multi", [c_void_p, c_int, c_int, c_void_p, c_long, c_int, c_void_p])
     ops.register("dtf_slab_job_size", [])
+    ops.register("dtf_dense_job_size", [])
+    ops.register("dtf_dense_slab_reduce_multi", [c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_void_p])
     ops.register("dtf_conv_args_size", [])
     ops.register("dtf_bnbwd_args_size", [])
     ops.register("dtf_head_args_size", [])
@@ -139,6 +145,7 @@ def _register():
             fn.restype = c_int
     assert L.dtf_conv_args_size() == ctypes.sizeof(ConvArgs), "ConvArgs ABI mismatch"
     assert L.dtf_slab_job_size() == ctypes.sizeof(SlabJob), "SlabJob ABI mismatch"
+    assert L.dtf_dense_job_size() == ctypes.sizeof(DenseJob), "DenseJob ABI mismatch"
     assert L.dtf_bnbwd_args_size() == ctypes.sizeof(BnBwdArgs), "BnBwdArgs ABI mismatch"
     assert L.dtf_head_args_size() == ctypes.sizeof(HeadArgs), "HeadArgs ABI mismatch"
     assert L.dtf_bnew_args_size() == ctypes.sizeof(BnEwArgs), "BnEwArgs ABI mismatch"
@@ -564,8 +571,14 @@ class _StepPlan:
         # every such layer keeps its own slab (DTF_DEFER_C64)
         self.defer64 = dev.type == "cuda" and os.environ.get("DTF_DEFER_C64", "1") == "1"
         self._deferred = []
+        # standalone wgrad launches (stem, projections, strided convs) write dense per-workgroup dW partials reduced
+        # in one launch after the backward (no contended fp32 atomics; fixed order).  Not with the side-stream split
+        # backward (its wgrads are joined only before the optimizer).
+        self.wslab = (dev.type == "cuda" and not self.split and os.environ.get("DTF_WGRAD_SLAB", "1") == "1")
+        self._deferred_dense = []
         self._build()
-        assert self._pending_slab is None and not self._deferred, "every dW slab must be reduced before the optimizer"
+        assert self._pending_slab is None and not self._deferred and not self._deferred_dense, \
+            "every dW slab must be reduced before the optimizer"
         self.graph = None
 
     # -------------------------------------------------------------------- work lists
@@ -774,7 +787,7 @@ class _StepPlan:
         # bound fp32 atomic traffic (~12 MB / launch) and same-address contention (<= 128 WGs per member)
         per_member = int(os.environ.get("DTF_WGRAD_WG_PER_MEMBER", "128"))
         n_wg = max(64, min(per_member * len(self.slots), int(12e6 / (4.0 * wn))))
-        if self.be.det:
+        if self.be.det and not self.wslab:
             n_wg = len(self.slots)  # one workgroup per member: every dW element is added once (fixed order)
         work = self._work_iters(Ho // rows, n_wg)
         a = self._base_args()
@@ -795,6 +808,10 @@ class _StepPlan:
         dt = (rows * Ho * _cpad(c.cout) + 63) // 64 * 64
         lds = 1536 + 2 * (xt + dt) * 2  # double-buffered
         lib = ops.lib()
+        if self.wslab:
+            kel = c.cout * c.k * c.k * a.cin_real
+            a.slab = _p(self._layer_slab(work.shape[0] * kel))
+            self._deferred_dense.append((a.slab, self._slab_table(work), c.off, kel))
         launch = self._side if self.split else self._add
         launch(lib.dtf_conv_wgrad, ctypes.byref(a), cin, c.cout, c.stride, c.k, mode_x, mode_dy, work.shape[0], lds)
         self._keep(a)
@@ -1056,7 +1073,20 @@ class _StepPlan:
         return max(1, min(nb, t // max(1, n_members)))
 
     def _flush_deferred(self):
-        """One reduction launch over every deferred C = 64 slab (dw_slab_reduce_multi_kernel)."""
+        """One reduction launch over every deferred C = 64 slab (dw_slab_reduce_multi_kernel) and one over every
+        dense wgrad slab (dense_slab_reduce_multi_kernel)."""
+        if self._deferred_dense:
+            jobs = (DenseJob * len(self._deferred_dense))()
+            nmax = bmax = 0
+            for i, (buf, red, goff, kel) in enumerate(self._deferred_dense):
+                jobs[i] = DenseJob(buf, _p(red), goff, kel, red.shape[0])
+                nmax = max(nmax, red.shape[0])
+                bmax = max(bmax, -(-kel // 32))
+            jt = torch.frombuffer(bytearray(bytes(jobs)), dtype=torch.uint8).to(self.be.dev)
+            self._keep(jt)
+            self._add(ops.lib().dtf_dense_slab_reduce_multi, _p(jt), len(self._deferred_dense), nmax,
+                      min(bmax, int(os.environ.get("DTF_DENSE_REDUCE_BLOCKS", "256"))), _p(self.e.grads), self.e.Pp)
+            self._deferred_dense = []
         if not self._deferred:
             return
         jobs = (SlabJob * len(self._deferred))()

@@ -1281,9 +1281,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
     }
     __syncthreads();
   }
-  // epilogue: D[co][n] with co = m*16 + 4*(lane>>4) + r, n-col = lane & 15
-  float* gb = a.grads + (long)slot * a.g_mstride + a.g_off;
+  // epilogue: D[co][n] with co = m*16 + 4*(lane>>4) + r, n-col = lane & 15.  With a slab: this workgroup's dense
+  // partial dW (every element of [co][tap][ci < cin_real] written once, plain stores), summed in workgroup order by
+  // dense_slab_reduce_multi_kernel; else fp32 atomics into the gradient row.
   const int KK = K * K;
+  const long kel = (long)COUT * KK * a.cin_real;
+  float* gb = a.slab ? a.slab + (long)blockIdx.x * kel : a.grads + (long)slot * a.g_mstride + a.g_off;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int nt = wave + 4 * j;
@@ -1295,11 +1298,57 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int co = m * 16 + 4 * (lane >> 4) + r;
-            atomicAdd(gb + ((long)co * KK + tap) * a.cin_real + ci, acc[j][m][r]);
+            const long e = ((long)co * KK + tap) * a.cin_real + ci;
+            if (a.slab)
+              gb[e] = acc[j][m][r];
+            else
+              atomicAdd(gb + e, acc[j][m][r]);
           }
         }
       }
     }
+  }
+}
+
+// Dense dW slabs of several wgrad launches (conv_wgrad_kernel with a slab), reduced after the backward in one launch:
+// blockIdx.z = job, y = member row of its reduce table (first wg, n wgs, -, slot), x (+ gridDim.x ...) = 32-element
+// block; 8 thread groups stride over the member's slabs, an LDS sum in group order (fixed summation order).
+struct DenseJob {
+  const float* slab;
+  const int4* red;
+  long g_off;
+  int kel;
+  int nmem;
+};
+
+__global__ __launch_bounds__(256) void dense_slab_reduce_multi_kernel(const DenseJob* __restrict__ jobs,
+                                                                      float* __restrict__ grads, long g_mstride) {
+  __shared__ float part[8 * 33];
+  const DenseJob j = jobs[blockIdx.z];
+  if ((int)blockIdx.y >= j.nmem) return;  // workgroup-uniform
+  const int el = threadIdx.x & 31, gg = threadIdx.x >> 5;
+  const int4 rd = j.red[blockIdx.y];
+  for (int bx = blockIdx.x; bx * 32 < j.kel; bx += gridDim.x) {
+    const int e = bx * 32 + el;
+    const bool ok = e < j.kel;
+    float s0 = 0.f, s1 = 0.f;
+    int g = gg;
+    for (; g + 8 < rd.y; g += 16) {
+      if (ok) {
+        s0 += j.slab[(long)(rd.x + g) * j.kel + e];
+        s1 += j.slab[(long)(rd.x + g + 8) * j.kel + e];
+      }
+    }
+    if (g < rd.y && ok) s0 += j.slab[(long)(rd.x + g) * j.kel + e];
+    part[gg * 33 + el] = s0 + s1;
+    __syncthreads();
+    if (gg == 0 && ok) {
+      float sum = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sum += part[i * 33 + el];
+      grads[(long)rd.w * g_mstride + j.g_off + e] += sum;
+    }
+    __syncthreads();
   }
 }
 
@@ -1820,6 +1869,16 @@ DTF_API int dtf_dw_slab_reduce(const float* slab, const int4* red, int nmembers,
 }
 
 DTF_API int dtf_slab_job_size() { return (int)sizeof(SlabJob); }
+DTF_API int dtf_dense_job_size() { return (int)sizeof(DenseJob); }
+
+DTF_API int dtf_dense_slab_reduce_multi(const void* jobs, int njobs, int max_members, int max_blocks, float* grads,
+                                        long g_mstride, hipStream_t stream) {
+  if (njobs <= 0 || max_members <= 0 || max_blocks <= 0) return 0;
+  DTF_HOST_CHECK(jobs != nullptr && njobs <= 65535);
+  hipLaunchKernelGGL(dense_slab_reduce_multi_kernel, dim3(max_blocks, max_members, njobs), dim3(256), 0, stream,
+                     reinterpret_cast<const DenseJob*>(jobs), grads, g_mstride);
+  return DTF_CHECK_LAUNCH();
+}
 
 DTF_API int dtf_dw_slab_reduce_multi(const void* jobs, int njobs, int max_members, float* grads, long g_mstride, int c,
                                      hipStream_t stream) {

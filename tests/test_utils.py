@@ -108,13 +108,13 @@ def test_past_stop_threshold():
         model_helpers.past_stop_threshold(0.5, "x")
 
 
-def test_synthetic_data_and_batch_split():
-    x, y = model_helpers.generate_synthetic_data([2, 3], 5, torch.float32, [2], 1)
-    assert float(x.sum()) == 30 and y.tolist() == [1, 1]
-    assert model_helpers.per_device_batch_size(64, 4) == 16
-    with pytest.raises(ValueError):
-        model_helpers.per_device_batch_size(65, 4)
-    assert model_helpers.get_distribution_strategy(2)["kind"] == "member_data_parallel"
+def test_member_dp_batch_split():
+    """Intra-member DP splits a member's batch over its ranks (uneven sizes allowed, unlike
+    distribution_utils.per_device_batch_size): the shards always add up to the member's batch."""
+    from distributedtf_amd.parallel.dataparallel import DPContext
+    for b in (64, 65, 127):
+        shards = [DPContext(group=None, size=4, rank=r, group_index=0, n_groups=1).local_batch(b) for r in range(4)]
+        assert sum(shards) == b and max(shards) - min(shards) <= 1
 
 
 def test_serving_spec():

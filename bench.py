@@ -119,6 +119,7 @@ def main():
 
     exploits = [0]
     exploit_s = []  # host wall time of each timed exploit/explore cycle (gather + plan + copy + perturb)
+    exploit_wait_s = []  # time each cycle waited for its loss readback (steps queued ahead still executing)
 
     def exploit_start(losses):
         """Queue the population's loss readback (pinned, non-blocking) behind the step that produced it."""
@@ -134,9 +135,11 @@ def main():
         # the NEXT step has been queued, so the readback wait, the metric all-gather and the planning run on
         # the host while the GPU executes that step; the winners' weights copied are the ones after it.
         host, evt = pending
-        tc = time.perf_counter()
+        tw = time.perf_counter()
         if evt is not None:
             evt.synchronize()  # only the readback, not the step queued behind it
+        tc = time.perf_counter()
+        exploit_wait_s.append(tc - tw)  # GPU still running the steps queued before the readback
         ls = host.tolist()
         vals = [[m.cluster_id, -ls[i], m.hparams] for i, m in enumerate(members)]
         parts = comm.allgather(vals)
@@ -170,6 +173,7 @@ def main():
         exploit_cycle(exploit_start(losses))
         exploits[0] = 0
         exploit_s.clear()
+        exploit_wait_s.clear()
     barrier_sync()
     images_done[0] = 0
     t0 = time.perf_counter()
@@ -216,6 +220,8 @@ def main():
                        "backend": eng.backend.name, "exploit_every": args.exploit_every,
                        "exploits_timed": exploits[0]},
             "exploit_ms_mean": round(1000.0 * sum(exploit_s) / len(exploit_s), 3) if exploit_s else None,
+            "exploit_readback_wait_ms_mean": (round(1000.0 * sum(exploit_wait_s) / len(exploit_wait_s), 3)
+                                              if exploit_wait_s else None),
             "achieved_tflops": round(flops / 1e12, 2),
         }
         print(json.dumps(out), flush=True)

@@ -722,14 +722,12 @@ class _ImageNetPlan:
                 ops.fused_optimizer(e.state, e.grads, e.hyper, e.Pp, e.P, e.n_reg, shadow=self.be.shadow,
                                     zero_grads=True)
             elif fn == "step":
-                advance_steps(e, self.slots_long, self.slots_t)
+                # step counters + per-member losses gathered inside the step (graph): a replay leaves one copy
+                advance_steps(e, self.slots_long, self.slots_t, self.be.loss, self.loss_sel)
             else:
                 err = fn(*args, st)
                 if err != 0:
                     raise RuntimeError("kernel launch %s failed with %d" % (getattr(fn, "__name__", fn), err))
-        # per-member losses gathered inside the step (graph) so a replay leaves one copy for train_step
-        if not self.eval:
-            torch.index_select(self.be.loss, 0, self.slots_long, out=self.loss_sel)
 
     def run(self):
         be = self.be

@@ -400,8 +400,7 @@ class _MnistPlan:
         self._launch(L.dtf_mnist_conv1_wgrad, self.w_c1w)
         e.dp_sync_grads(self.slots)  # data-parallel member groups only (no-op otherwise)
         ops.fused_optimizer(e.state, e.grads, e.hyper, e.Pp, e.P, e.n_reg, shadow=be.shadow, zero_grads=True)
-        advance_steps(e, self.slots_long, self.slots_t)
-        torch.index_select(be.loss, 0, self.slots_long, out=self.loss_sel)
+        advance_steps(e, self.slots_long, self.slots_t, be.loss, self.loss_sel)
 
     def run(self):
         be = self.be

@@ -94,7 +94,7 @@ class HeadArgs(ctypes.Structure):
         ("gamma_off", c_int), ("beta_off", c_int), ("dw_off", c_int), ("db_off", c_int), ("grads", c_void_p),
         ("g_mstride", c_long), ("st_f", c_void_p), ("st_b", c_void_p), ("cnt", c_void_p), ("dfeat", c_void_p),
         ("loss", c_void_p), ("correct", c_void_p), ("logits_out", c_void_p), ("hw", c_int), ("C", c_int),
-        ("ncls", c_int), ("train", c_int),
+        ("ncls", c_int), ("train", c_int), ("slab", c_void_p), ("slab_b", c_void_p),
     ]
 
 
@@ -127,6 +127,8 @@ def _register():
                                      c_void_p, c_long, c_void_p])
     ops.register("dtf_bn_running_update", [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_long, c_void_p,
                                            c_int, c_void_p, c_void_p, c_long, c_void_p])
+    ops.register("dtf_bn_step_end", [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_void_p, c_long, c_void_p,
+                                     c_int, c_void_p, c_void_p, c_long, c_void_p])
     ops.register("dtf_bn_eval_stats", [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_long, c_void_p, c_int,
                                        c_void_p, c_void_p])
     ops.register("dtf_bn_bwd_apply", [P(BnBwdArgs), c_void_p])
@@ -283,17 +285,20 @@ def note_step_advanced(e, slots):
                 dev[s][H_STEP] += 1.0
 
 
-def advance_steps(e, slots_long, slots_i32=None):
-    """Inside the captured step: per-member step counters (state column + hyper table) += 1 (one kernel when
-    the int32 slot list is given)."""
+def advance_steps(e, slots_long, slots_i32=None, loss=None, loss_sel=None):
+    """Inside the captured step: per-member step counters (state column + hyper table) += 1 and, given
+    ``loss``/``loss_sel``, the per-member losses gathered in slot-list order (one kernel when the int32 slot list is
+    given)."""
     from .optim import H_STEP
     if slots_i32 is not None and e.device.type == "cuda":
-        ops.check(ops.lib().dtf_step_advance(_p(e.state), e.S, 3 * e.Pp + e.R, _p(e.hyper), H_STEP, _p(slots_i32),
-                                             slots_i32.numel(), ops.stream()), "step_advance")
+        ops.check(ops.lib().dtf_step_end(_p(e.state), e.S, 3 * e.Pp + e.R, _p(e.hyper), H_STEP, _p(slots_i32),
+                                         slots_i32.numel(), _p(loss), _p(loss_sel), ops.stream()), "step_end")
         return
     one = torch.ones(slots_long.numel(), device=e.device)
     e.step_col().index_add_(0, slots_long, one)
     e.hyper[:, H_STEP].index_add_(0, slots_long, one)
+    if loss_sel is not None:
+        torch.index_select(loss, 0, slots_long, out=loss_sel)
 
 
 def same_batches(plan, batches) -> bool:
@@ -1139,6 +1144,20 @@ class _StepPlan:
                 need = max(need, self._fused_nwg(C, H // 8) * self._slab_elems(C))
         return need
 
+    def _head_slab(self, ha, hwork):
+        """Dense-layer gradients of the head as per-workgroup slabs, reduced with the deferred wgrad slabs (instead
+        of every head workgroup adding the same ncls x C addresses atomically)."""
+        if not self.wslab:
+            return
+        nwg, ncls, C = hwork.shape[0], ha.ncls, ha.C
+        sw = self._layer_slab(nwg * ncls * C)
+        sb = self._layer_slab(nwg * ncls)
+        ha.slab, ha.slab_b = _p(sw), _p(sb)
+        red = self._slab_table(hwork)
+        prog = self.be.L.prog
+        self._deferred_dense.append((ha.slab, red, prog.dense_w_off, ncls * C))
+        self._deferred_dense.append((ha.slab_b, red, prog.dense_b_off, ncls))
+
     def _layer_slab(self, n):
         t = torch.empty(max(n, 1), dtype=torch.float32, device=self.be.dev)
         self._keep(t)
@@ -1235,10 +1254,10 @@ class _StepPlan:
         ha.dfeat, ha.loss, ha.correct = _p(self.dfeat), _p(be.loss), _p(be.correct)
         ha.logits_out = None
         ha.hw, ha.C, ha.ncls, ha.train = hw, cfg.final_size, cfg.num_classes, 1
+        self._head_slab(ha, hwork)
         self._keep(ha)
         self._add(lib.dtf_head, ctypes.byref(ha), hwork.shape[0])
-        self._add(lib.dtf_bn_running_update, _p(e.state), e.S, 3 * e.Pp, _p(be.bn_table_t), len(L.bn_table),
-                  _p(be.stats[0]), be.stats_bn_stride, _p(self.slots_t), nslots, _p(self.cnt), None, 0)
+        # (the moving-statistics update of the forward BNs runs at the end of the step, with the BN gradients)
         # ---------------- backward
         hwL = self.xs[-1].shape[1]
         g_cur = self.tmp[hwL]["g"][0]
@@ -1295,8 +1314,9 @@ class _StepPlan:
         # BN parameter gradients from the backward reductions
         self._flush_slab()
         self._flush_deferred()
-        self._add(lib.dtf_bn_running_update, _p(e.state), e.S, 3 * e.Pp, _p(be.bn_table_t), len(L.bn_table),
-                  _p(be.stats[1]), be.stats_bn_stride, _p(self.slots_t), nslots, _p(self.cnt), _p(e.grads), e.Pp)
+        self._add(lib.dtf_bn_step_end, _p(e.state), e.S, 3 * e.Pp, _p(be.bn_table_t), len(L.bn_table),
+                  _p(be.stats[0]), _p(be.stats[1]), be.stats_bn_stride, _p(self.slots_t), nslots, _p(self.cnt),
+                  _p(e.grads), e.Pp)
         # optimizer over every member row (+ zero grads), step counters
         self._add("optim", None)
         self._add("step", None)
@@ -1473,10 +1493,10 @@ class _StepPlan:
         ha_.dfeat, ha_.loss, ha_.correct = _p(self.dfeat), _p(be.loss), _p(be.correct)
         ha_.logits_out = None
         ha_.hw, ha_.C, ha_.ncls, ha_.train = hw, cfg.final_size, cfg.num_classes, 1
+        self._head_slab(ha_, hwork)
         self._keep(ha_)
         self._add(lib.dtf_head, ctypes.byref(ha_), hwork.shape[0])
-        self._add(lib.dtf_bn_running_update, _p(e.state), e.S, 3 * e.Pp, _p(be.bn_table_t), len(L.bn_table),
-                  _p(be.stats[0]), be.stats_bn_stride, _p(self.slots_t), nslots, _p(self.cnt), None, 0)
+        # (the moving-statistics update of the forward BNs runs at the end of the step, with the BN gradients)
         # ---------------- backward
         hwL = self.xs[-1].shape[1]
         d = self.tmp[hwL]["g"][0]
@@ -1514,8 +1534,9 @@ class _StepPlan:
                          cin_real=cfg.in_channels)
         self._flush_slab()
         self._flush_deferred()
-        self._add(lib.dtf_bn_running_update, _p(e.state), e.S, 3 * e.Pp, _p(be.bn_table_t), len(L.bn_table),
-                  _p(be.stats[1]), be.stats_bn_stride, _p(self.slots_t), nslots, _p(self.cnt), _p(e.grads), e.Pp)
+        self._add(lib.dtf_bn_step_end, _p(e.state), e.S, 3 * e.Pp, _p(be.bn_table_t), len(L.bn_table),
+                  _p(be.stats[0]), _p(be.stats[1]), be.stats_bn_stride, _p(self.slots_t), nslots, _p(self.cnt),
+                  _p(e.grads), e.Pp)
         self._add("optim", None)
         self._add("step", None)
 
@@ -1565,14 +1586,13 @@ class _StepPlan:
                 e.dp_sync_grads(self.slots)  # data-parallel member groups only (no-op otherwise)
                 ops.fused_optimizer(e.state, e.grads, e.hyper, e.Pp, e.P, e.n_reg, shadow=None, zero_grads=True)
             elif fn == "step":
-                advance_steps(e, self.slots_long, self.slots_t)
+                # step counters + per-member losses gathered inside the step (graph) so a replay leaves one copy
+                # for loss_view
+                advance_steps(e, self.slots_long, self.slots_t, self.be.loss, self.loss_sel)
             else:
                 err = fn(*args, ops.stream())
                 if err != 0:
                     raise RuntimeError("kernel launch %s failed with %d" % (getattr(fn, "__name__", fn), err))
-        # per-member losses gathered inside the step (graph) so a replay leaves one copy for loss_view
-        if not self.eval:
-            torch.index_select(self.be.loss, 0, self.slots_long, out=self.loss_sel)
 
     def run_eval(self):
         assert self.eval

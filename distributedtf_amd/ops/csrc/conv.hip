@@ -1789,13 +1789,49 @@ struct SlabJob {
   int pad;
 };
 
+// blockIdx.z = job (one layer), y = member row of its reduce table, x = block of 256 slab elements.  Thread t reads
+// elements 4*(t%64)..+3 (float4) of every 4th slab starting at t/64, four loads in flight; the 4 partial sums meet
+// in LDS and thread t finishes element t (fixed summation order).
 template <int C>
 __global__ __launch_bounds__(256) void dw_slab_reduce_multi_kernel(const SlabJob* __restrict__ jobs,
                                                                    float* __restrict__ grads, long g_mstride) {
-  __shared__ float part[8 * 33];
+  constexpr int MT = C / 16, NTN = 9 * C / 16, NJ = (NTN + 3) / 4, E = NJ * MT * 4 * 256;
+  static_assert(E % 256 == 0, "whole 256-element blocks");
+  __shared__ float4 part[4][64];
   const SlabJob j = jobs[blockIdx.z];
   if ((int)blockIdx.y >= j.nmem) return;  // workgroup-uniform
-  slab_reduce_wg<C>(j.slab, j.red, grads, g_mstride, j.g_off, blockIdx.x, blockIdx.y, part, gridDim.x);
+  const int4 rd = j.red[blockIdx.y];
+  const int q = threadIdx.x & 63, gg = threadIdx.x >> 6;
+  const int e0 = blockIdx.x * 256;
+  const float4* p = reinterpret_cast<const float4*>(j.slab + (long)rd.x * E + e0) + q;
+  constexpr long E4 = E / 4;
+  float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0, s3 = s0;
+  int g = gg;
+  for (; g + 12 < rd.y; g += 16) {
+    const float4 a0 = p[(long)g * E4], a1 = p[(long)(g + 4) * E4], a2 = p[(long)(g + 8) * E4],
+                 a3 = p[(long)(g + 12) * E4];
+    s0.x += a0.x; s0.y += a0.y; s0.z += a0.z; s0.w += a0.w;
+    s1.x += a1.x; s1.y += a1.y; s1.z += a1.z; s1.w += a1.w;
+    s2.x += a2.x; s2.y += a2.y; s2.z += a2.z; s2.w += a2.w;
+    s3.x += a3.x; s3.y += a3.y; s3.z += a3.z; s3.w += a3.w;
+  }
+  for (; g < rd.y; g += 4) {
+    const float4 a0 = p[(long)g * E4];
+    s0.x += a0.x; s0.y += a0.y; s0.z += a0.z; s0.w += a0.w;
+  }
+  part[gg][q] = make_float4((s0.x + s1.x) + (s2.x + s3.x), (s0.y + s1.y) + (s2.y + s3.y),
+                            (s0.z + s1.z) + (s2.z + s3.z), (s0.w + s1.w) + (s2.w + s3.w));
+  __syncthreads();
+  const float* pf = reinterpret_cast<const float*>(part);
+  const int t0 = threadIdx.x;
+  const float sum = (pf[t0] + pf[256 + t0]) + (pf[512 + t0] + pf[768 + t0]);
+  const int e = e0 + t0;
+  const int r = e & 3, t = (e >> 2) & 255, m = (e >> 10) % MT, jj = (e >> 10) / MT;  // slab [j][m][t][r]
+  const int wave = t >> 6, lane = t & 63, nt = wave + 4 * jj;
+  if (nt < NTN) {
+    const int tap = (nt * 16) / C, ci = (nt * 16) % C + (lane & 15), co = m * 16 + 4 * (lane >> 4) + r;
+    grads[(long)rd.w * g_mstride + j.g_off + ((long)co * 9 + tap) * C + ci] += sum;
+  }
 }
 
 template <typename KernelT>
@@ -1887,7 +1923,7 @@ DTF_API int dtf_dw_slab_reduce_multi(const void* jobs, int njobs, int max_member
 #define REDM_CASE(CC)                                                                                        \
   if (c == CC) {                                                                                            \
     constexpr int E = ((9 * CC / 16 + 3) / 4) * (CC / 16) * 4 * 256;                                         \
-    hipLaunchKernelGGL(dw_slab_reduce_multi_kernel<CC>, dim3(E / 32, max_members, njobs), dim3(256), 0,     \
+    hipLaunchKernelGGL(dw_slab_reduce_multi_kernel<CC>, dim3(E / 256, max_members, njobs), dim3(256), 0,    \
                        stream, reinterpret_cast<const SlabJob*>(jobs), grads, g_mstride);                   \
     return DTF_CHECK_LAUNCH();                                                                              \
   }

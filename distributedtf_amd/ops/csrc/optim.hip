@@ -134,14 +134,17 @@ __global__ __launch_bounds__(256) void shadow_refresh_kernel(const float* __rest
   }
 }
 
-// Per-member step counters after a captured step: state[slot][col] += 1 and hyper[slot][h_step] += 1.
+// Per-member step counters after a captured step: state[slot][col] += 1 and hyper[slot][h_step] += 1; optionally
+// the step's per-member losses gathered in slot-list order (loss_sel[i] = loss[slots[i]]).
 __global__ void step_advance_kernel(float* __restrict__ state, long S, long col, float* __restrict__ hyper,
-                                    int h_step, const int* __restrict__ slots, int n) {
+                                    int h_step, const int* __restrict__ slots, int n, const float* __restrict__ loss,
+                                    float* __restrict__ loss_sel) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
     const int s = slots[i];
     state[(long)s * S + col] += 1.f;
     hyper[s * 8 + h_step] += 1.f;
+    if (loss_sel != nullptr) loss_sel[i] = loss[s];
   }
 }
 
@@ -151,7 +154,15 @@ DTF_API int dtf_step_advance(float* state, long S, long col, float* hyper, int h
                              hipStream_t stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(step_advance_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, state, S, col, hyper, h_step,
-                     slots, n);
+                     slots, n, (const float*)nullptr, (float*)nullptr);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_step_end(float* state, long S, long col, float* hyper, int h_step, const int* slots, int n,
+                         const float* loss, float* loss_sel, hipStream_t stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(step_advance_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, state, S, col, hyper, h_step,
+                     slots, n, loss, loss_sel);
   return DTF_CHECK_LAUNCH();
 }
 

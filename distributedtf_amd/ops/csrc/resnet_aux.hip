@@ -113,12 +113,17 @@ __global__ __launch_bounds__(64) void bn_running_update_kernel(float* __restrict
                                                                 const float* __restrict__ stats, long stats_bn_stride,
                                                                 const int* __restrict__ slots,
                                                                 const float* __restrict__ cnt,
-                                                                float* __restrict__ grads, long g_mstride) {
+                                                                float* __restrict__ grads, long g_mstride,
+                                                                const float* __restrict__ stats_fwd) {
   const int* t = table + blockIdx.x * 8;
   const int slot = slots[blockIdx.y];
   const int c = threadIdx.x;
   const int C = t[1];
   if (c >= C) return;
+  if (blockIdx.z == 1) {  // combined launch: z = 1 is the moving-statistics update from the forward statistics
+    stats = stats_fwd;
+    grads = nullptr;
+  }
   const float* row = stats + (long)t[3] * stats_bn_stride + (long)slot * NREP * 128;
   float s, q;
   stats_sum(row, c, s, q);
@@ -257,20 +262,48 @@ struct HeadArgs {
   float* logits_out;      // [N, ncls] optional
   int hw, C, ncls;
   int train;
+  float* slab;            // optional [nblocks][ncls * C] per-workgroup dense-weight gradients (else atomics)
+  float* slab_b;          // optional [nblocks][ncls] per-workgroup bias gradients
 };
 
-// 4 waves per WG, one image per wave iteration, lane = channel (C == 64).
+// Head of the CIFAR ResNet (C == 64 final channels, hw % 32 == 0, hw <= 128, ncls <= 16).  One image at a time
+// per workgroup, all 4 waves on it: thread t stages pixels t/8 + 32k, channels 8*(t%8)..+7 as 16-byte loads (the
+// whole 8 KB image in two load instructions per thread), keeps them in registers for the backward reductions, and
+// the pooled feature is summed lane-group -> wave (xor shuffles) -> workgroup (LDS, one barrier per image; the
+// LDS buffer alternates by image parity).  Every wave then computes the logits / softmax / dL/dfeat redundantly
+// (no second barrier); wave 0 accumulates the dense gradients, written as a per-workgroup slab (reduced after the
+// backward in fixed order) instead of thousands of same-address fp32 atomics.
+constexpr int HEAD_MAXK = 4;  // 32-pixel rounds per image (hw <= 128)
+
+__device__ __forceinline__ float xor_sum_8_16_32(float v) {
+  v += __shfl_xor(v, 8, 64);
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
 __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   __shared__ float sc[64], sh[64], mu[64], iv[64];
+  __shared__ float fpart[2][4][64];
   __shared__ float red[4][2][64];
-  __shared__ float dwl[4][16][64];
-  __shared__ float dbl[4][16];
   const int4 wk = a.work[blockIdx.x];
-  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0);
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0 && a.C == 64 && a.hw % 32 == 0 && a.hw <= 32 * HEAD_MAXK &&
+               a.ncls <= 16);
   const int img0 = wk.x, nimg = wk.y, slot = wk.w;
-  const int wave = threadIdx.x >> 6, c = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane;
+  const int cg = threadIdx.x & 7, c8 = cg * 8, pix0 = threadIdx.x >> 3;  // this thread's 8 channels / first pixel
   const float* prow = a.params + (long)slot * a.p_mstride;
   const float bsz = a.cnt[slot];
+  const int nk = a.hw / 32;
+  // first image's loads before the coefficient math
+  uint4 xv[HEAD_MAXK];
+  auto load_img = [&](int img) {
+    const bf16_t* xp = a.x + (long)img * a.hw * 64 + c8;
+#pragma unroll
+    for (int k = 0; k < HEAD_MAXK; ++k)
+      if (k < nk) xv[k] = *reinterpret_cast<const uint4*>(xp + (long)(pix0 + 32 * k) * 64);
+  };
+  load_img(img0);
   if (threadIdx.x < 64) {
     if (a.gamma_off < 0) {  // ResNet v1: no final BN (input is the last block's ReLU output)
       sc[c] = 1.f;
@@ -290,33 +323,66 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
       iv[c] = inv;
     }
   }
-  __syncthreads();
   const int ncls = a.ncls;
-  float wcol[16];  // W[j][c] for this lane's channel
+  float wcol[16];  // W[j][c] for lane c
 #pragma unroll
-  for (int j = 0; j < 16; ++j) wcol[j] = j < ncls ? prow[a.dw_off + j * a.C + c] : 0.f;
+  for (int j = 0; j < 16; ++j) wcol[j] = j < ncls ? prow[a.dw_off + j * 64 + c] : 0.f;
+  const float bias = lane < ncls ? prow[a.db_off + lane] : 0.f;
+  __syncthreads();
+  float s8[8], t8[8], m8[8], i8[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    s8[i] = sc[c8 + i];
+    t8[i] = sh[c8 + i];
+    m8[i] = mu[c8 + i];
+    i8[i] = iv[c8 + i];
+  }
   float dw[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) dw[j] = 0.f;
-  float db = 0.f;  // lane j < ncls accumulates db[j]
-  float s_dz = 0.f, s_dzx = 0.f, loss_acc = 0.f, corr = 0.f;
-  const float s_c = sc[c], t_c = sh[c], mu_c = mu[c], iv_c = iv[c];
+  float db = 0.f;  // lane j < ncls of wave 0: db[j]
+  float sdz[8], sdzx[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sdz[i] = sdzx[i] = 0.f;
+  float loss_acc = 0.f, corr = 0.f;
   const float inv_hw = 1.f / (float)a.hw;
-  for (int im = wave; im < nimg; im += 4) {
+  for (int im = 0; im < nimg; ++im) {
     const int img = img0 + im;
-    const bf16_t* xp = a.x + (long)img * a.hw * a.C + c;
-    float f = 0.f;
-    // unrolled so 16 independent loads are in flight per round trip (a runtime-trip loop otherwise pays the
-    // full load latency once per pixel: 64 round trips per image)
-#pragma unroll 16
-    for (int p = 0; p < a.hw; ++p) f += fmaxf(bf2f(xp[(long)p * a.C]) * s_c + t_c, 0.f);
-    f *= inv_hw;
+    // ---- pooled relu(BN(x)) of this thread's pixels, 8 channels
+    float f8[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f8[i] = 0.f;
+#pragma unroll
+    for (int k = 0; k < HEAD_MAXK; ++k) {
+      if (k < nk) {
+        const uint32_t w4[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f8[2 * j] += fmaxf(bf2f((bf16_t)(w4[j] & 0xffff)) * s8[2 * j] + t8[2 * j], 0.f);
+          f8[2 * j + 1] += fmaxf(bf2f((bf16_t)(w4[j] >> 16)) * s8[2 * j + 1] + t8[2 * j + 1], 0.f);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f8[i] = xor_sum_8_16_32(f8[i]);
+    float* fp = fpart[im & 1][wave];
+    if (lane < 8) {
+      *reinterpret_cast<float4*>(fp + c8) = make_float4(f8[0], f8[1], f8[2], f8[3]);
+      *reinterpret_cast<float4*>(fp + c8 + 4) = make_float4(f8[4], f8[5], f8[6], f8[7]);
+    }
+    __syncthreads();
+    const float f = (fpart[im & 1][0][c] + fpart[im & 1][1][c] + fpart[im & 1][2][c] + fpart[im & 1][3][c]) * inv_hw;
+    uint4 xcur[HEAD_MAXK];
+#pragma unroll
+    for (int k = 0; k < HEAD_MAXK; ++k) xcur[k] = xv[k];
+    if (im + 1 < nimg) load_img(img + 1);  // next image in flight during the softmax / backward math
+    // ---- logits / softmax / CE (every wave, redundantly)
     float logit[16];
     float mx = -3.0e38f;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       if (j < ncls) {
-        logit[j] = wave_sum(wcol[j] * f) + prow[a.db_off + j];
+        logit[j] = wave_sum(wcol[j] * f) + __shfl(bias, j, 64);
         mx = fmaxf(mx, logit[j]);
       }
     }
@@ -326,22 +392,28 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
       if (j < ncls) se += __expf(logit[j] - mx);
     const float lse = mx + __logf(se);
     const int lab = a.labels[img];
-    float best = -3.0e38f;
-    int arg = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-      if (j < ncls && logit[j] > best) {
-        best = logit[j];
-        arg = j;
-      }
-    if (c == 0) {
-      loss_acc += lse - logit[lab];
-      corr += (arg == lab) ? 1.f : 0.f;
-    }
-    if (a.logits_out && c < ncls) {
+    if (wave == 0) {
+      float best = -3.0e38f;
+      int arg = 0;
 #pragma unroll
       for (int j = 0; j < 16; ++j)
-        if (j == c) a.logits_out[(long)img * ncls + j] = logit[j];
+        if (j < ncls && logit[j] > best) {
+          best = logit[j];
+          arg = j;
+        }
+      if (lane == 0) {
+        float ll = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (j == lab) ll = logit[j];
+        loss_acc += lse - ll;
+        corr += (arg == lab) ? 1.f : 0.f;
+      }
+      if (a.logits_out && lane < ncls) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (j == lane) a.logits_out[(long)img * ncls + j] = logit[j];
+      }
     }
     if (a.train) {
       float dfeat = 0.f;
@@ -350,46 +422,80 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
         if (j < ncls) {
           const float dl = (__expf(logit[j] - lse) - (j == lab ? 1.f : 0.f)) / bsz;
           dfeat += wcol[j] * dl;
-          dw[j] += dl * f;
-          if (c == j) db += dl;
+          if (wave == 0) {
+            dw[j] += dl * f;
+            if (lane == j) db += dl;
+          }
         }
       }
       const float g = dfeat * inv_hw;  // dL/d(post-relu activation), identical for every pixel
-      a.dfeat[(long)img * a.C + c] = g;
-#pragma unroll 16
-      for (int p = 0; p < a.hw; ++p) {
-        const float xv = bf2f(xp[(long)p * a.C]);
-        if (xv * s_c + t_c > 0.f) {
-          s_dz += g;
-          s_dzx += g * (xv - mu_c) * iv_c;
+      if (wave == 0) a.dfeat[(long)img * 64 + c] = g;
+      float g8[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g8[i] = __shfl(g, c8 + i, 64);
+#pragma unroll
+      for (int k = 0; k < HEAD_MAXK; ++k) {
+        if (k < nk) {
+          const uint32_t w4[4] = {xcur[k].x, xcur[k].y, xcur[k].z, xcur[k].w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int i = 2 * j + h;
+              const float x = bf2f((bf16_t)(h ? (w4[j] >> 16) : (w4[j] & 0xffff)));
+              if (x * s8[i] + t8[i] > 0.f) {
+                sdz[i] += g8[i];
+                sdzx[i] += g8[i] * (x - m8[i]) * i8[i];
+              }
+            }
+          }
         }
       }
     }
   }
-  // reduce over waves through LDS, then one atomic per value
-  red[wave][0][c] = s_dz;
-  red[wave][1][c] = s_dzx;
+  // ---- workgroup reductions: BN-final backward sums (per channel), dense gradients, loss / correct
+  if (a.train) {
 #pragma unroll
-  for (int j = 0; j < 16; ++j) dwl[wave][j][c] = dw[j];
-  if (c < 16) dbl[wave][c] = db;
-  const float lw = wave_sum(loss_acc), cw = wave_sum(corr);
-  __syncthreads();
-  if (c == 0) {
-    atomicAdd(&a.loss[slot], lw / bsz);
-    atomicAdd(&a.correct[slot], cw);
-  }
-  if (a.train && wave == 0) {
-    if (a.gamma_off >= 0) {
-      const float v0 = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
-      const float v1 = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
-      float* row = a.st_b + (long)slot * NREP * 128 + (blockIdx.x & (NREP - 1)) * 128;
-      atomicAdd(&row[c], v0);
-      atomicAdd(&row[64 + c], v1);
+    for (int i = 0; i < 8; ++i) {
+      sdz[i] = xor_sum_8_16_32(sdz[i]);
+      sdzx[i] = xor_sum_8_16_32(sdzx[i]);
     }
-    float* g = a.grads + (long)slot * a.g_mstride;
-    for (int j = 0; j < ncls; ++j)
-      atomicAdd(&g[a.dw_off + j * a.C + c], dwl[0][j][c] + dwl[1][j][c] + dwl[2][j][c] + dwl[3][j][c]);
-    if (c < ncls) atomicAdd(&g[a.db_off + c], dbl[0][c] + dbl[1][c] + dbl[2][c] + dbl[3][c]);
+    if (lane < 8) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        red[wave][0][c8 + i] = sdz[i];
+        red[wave][1][c8 + i] = sdzx[i];
+      }
+    }
+  }
+  __syncthreads();
+  if (wave == 0) {
+    if (lane == 0) {
+      atomicAdd(&a.loss[slot], loss_acc / bsz);
+      atomicAdd(&a.correct[slot], corr);
+    }
+    if (a.train) {
+      if (a.gamma_off >= 0) {
+        const float v0 = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+        const float v1 = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+        float* row = a.st_b + (long)slot * NREP * 128 + (blockIdx.x & (NREP - 1)) * 128;
+        atomicAdd(&row[c], v0);
+        atomicAdd(&row[64 + c], v1);
+      }
+      if (a.slab != nullptr) {
+        float* sl = a.slab + (long)blockIdx.x * ncls * 64;
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (j < ncls) sl[j * 64 + c] = dw[j];
+        if (lane < ncls) a.slab_b[(long)blockIdx.x * ncls + lane] = db;
+      } else {
+        float* g = a.grads + (long)slot * a.g_mstride;
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (j < ncls) atomicAdd(&g[a.dw_off + j * 64 + c], dw[j]);
+        if (lane < ncls) atomicAdd(&g[a.db_off + lane], db);
+      }
+    }
   }
 }
 
@@ -621,7 +727,19 @@ DTF_API int dtf_bn_running_update(float* state, long s_mstride, long run_base, c
                                   const float* cnt, float* grads, long g_mstride, hipStream_t stream) {
   if (nbn <= 0 || nslots <= 0) return 0;
   hipLaunchKernelGGL(bn_running_update_kernel, dim3(nbn, nslots), dim3(64), 0, stream, state, s_mstride, run_base,
-                     table, stats, stats_bn_stride, slots, cnt, grads, g_mstride);
+                     table, stats, stats_bn_stride, slots, cnt, grads, g_mstride, (const float*)nullptr);
+  return DTF_CHECK_LAUNCH();
+}
+
+// End of a training step, one launch: BN parameter gradients from the backward reductions (z = 0) and the moving
+// mean / variance update from the forward statistics (z = 1).
+DTF_API int dtf_bn_step_end(float* state, long s_mstride, long run_base, const int* table, int nbn,
+                            const float* stats_fwd, const float* stats_bwd, long stats_bn_stride, const int* slots,
+                            int nslots, const float* cnt, float* grads, long g_mstride, hipStream_t stream) {
+  if (nbn <= 0 || nslots <= 0) return 0;
+  DTF_HOST_CHECK(stats_fwd != nullptr && stats_bwd != nullptr && grads != nullptr);
+  hipLaunchKernelGGL(bn_running_update_kernel, dim3(nbn, nslots, 2), dim3(64), 0, stream, state, s_mstride, run_base,
+                     table, stats_bwd, stats_bn_stride, slots, cnt, grads, g_mstride, stats_fwd);
   return DTF_CHECK_LAUNCH();
 }
 
@@ -651,6 +769,8 @@ DTF_API int dtf_bn_bwd_apply(const BnBwdArgs* a, hipStream_t stream) {
 
 DTF_API int dtf_head(const HeadArgs* a, int nblocks, hipStream_t stream) {
   if (nblocks <= 0) return 0;
+  // the kernel's fixed geometry (checked here in every build: a mismatch would read past the image)
+  if (a->C != 64 || a->hw % 32 != 0 || a->hw > 32 * HEAD_MAXK || a->ncls > 16 || a->ncls < 1) return -22;
   hipLaunchKernelGGL(head_kernel, dim3(nblocks), dim3(256), 0, stream, *a);
   return DTF_CHECK_LAUNCH();
 }

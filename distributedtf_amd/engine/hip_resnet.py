@@ -66,6 +66,11 @@ class SlabJob(ctypes.Structure):
     _fields_ = [("slab", c_void_p), ("red", c_void_p), ("g_off", c_long), ("nmem", c_int), ("pad", c_int)]
 
 
+class WorkGenDesc(ctypes.Structure):
+    _fields_ = [("dst", c_void_p), ("per", c_int), ("bands", c_int), ("min_chunk", c_int), ("split", c_int),
+                ("pad0", c_int), ("pad1", c_int)]
+
+
 class DenseJob(ctypes.Structure):
     _fields_ = [("slab", c_void_p), ("red", c_void_p), ("g_off", c_long), ("kel", c_int), ("nmem", c_int)]
 
@@ -127,6 +132,8 @@ def _register():
                                      c_void_p, c_long, c_void_p])
     ops.register("dtf_bn_running_update", [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_long, c_void_p,
                                            c_int, c_void_p, c_void_p, c_long, c_void_p])
+    ops.register("dtf_work_gen", [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p])
+    ops.register("dtf_workgen_desc_size", [])
     ops.register("dtf_bn_step_end", [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_void_p, c_long, c_void_p,
                                      c_int, c_void_p, c_void_p, c_long, c_void_p])
     ops.register("dtf_bn_eval_stats", [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_long, c_void_p, c_int,
@@ -148,6 +155,7 @@ def _register():
     assert L.dtf_conv_args_size() == ctypes.sizeof(ConvArgs), "ConvArgs ABI mismatch"
     assert L.dtf_slab_job_size() == ctypes.sizeof(SlabJob), "SlabJob ABI mismatch"
     assert L.dtf_dense_job_size() == ctypes.sizeof(DenseJob), "DenseJob ABI mismatch"
+    assert L.dtf_workgen_desc_size() == ctypes.sizeof(WorkGenDesc), "WorkGenDesc ABI mismatch"
     assert L.dtf_bnbwd_args_size() == ctypes.sizeof(BnBwdArgs), "BnBwdArgs ABI mismatch"
     assert L.dtf_head_args_size() == ctypes.sizeof(HeadArgs), "HeadArgs ABI mismatch"
     assert L.dtf_bnew_args_size() == ctypes.sizeof(BnEwArgs), "BnEwArgs ABI mismatch"
@@ -359,14 +367,28 @@ class HipResNetBackend:
     # --- plans ------------------------------------------------------------------------
     accepts_index_batches = True
 
+    def _elastic_cap(self, sizes):
+        """Per-member capacity of an elastic plan for these batch sizes, or None for an exact plan.  Mixed batch
+        sizes (PBT samples and perturbs them, constants.py:91-93) run on one capacity-keyed plan whose work tables
+        are regenerated on the device every step (DTF_ELASTIC: "auto" = mixed sizes only, "1", "0")."""
+        mode = os.environ.get("DTF_ELASTIC", "auto")
+        cap = int(os.environ.get("DTF_ELASTIC_MAXB", "256"))
+        if (mode == "0" or self.dev.type != "cuda" or self.L.cfg.version == 1 or self.e.dp is not None
+                or max(sizes) > cap or (mode == "auto" and len(set(sizes)) == 1)):
+            return None
+        return cap
+
     def plan(self, slots: Sequence[int], sizes: Sequence[int], src=None) -> "_StepPlan":
-        key = (tuple(slots), tuple(sizes), id(src) if src is not None else None)
+        cap = self._elastic_cap(sizes) if sizes else None
+        key = (tuple(slots), ("elastic", cap) if cap else tuple(sizes), id(src) if src is not None else None)
         p = self._plans.get(key)
         if p is None:
             if len(self._plans) > 16:
                 self._plans.clear()
-            p = _StepPlan(self, list(slots), list(sizes), src)
+            p = _StepPlan(self, list(slots), list(sizes), src, elastic_cap=cap)
             self._plans[key] = p
+        if cap:
+            p.set_sizes(list(sizes))
         return p
 
     def train_step(self, slots, batches, hparams, lrs):
@@ -439,12 +461,20 @@ class HipResNetBackend:
 class _StepPlan:
     """Buffers + prebuilt launch list for one batch composition (slots, per-member sizes)."""
 
-    def __init__(self, be: HipResNetBackend, slots: List[int], sizes: List[int], src=None, eval_mode=False):
+    def __init__(self, be: HipResNetBackend, slots: List[int], sizes: List[int], src=None, eval_mode=False,
+                 elastic_cap=None):
         self.be = be
         e = be.e
         self.e = e
         self.slots = slots
+        # elastic plan: buffers / layout for elastic_cap images per member, the real sizes live in self.cnt and
+        # the work tables are rebuilt from them on the device at the start of every step (work_gen_kernel)
+        self.elastic = bool(elastic_cap) and not eval_mode
+        self.real_sizes = list(sizes)
+        if self.elastic:
+            sizes = [int(elastic_cap)] * len(slots)
         self.sizes = sizes
+        self._wgen = []
         self.eval = bool(eval_mode)
         dev = be.dev
         L = be.L
@@ -463,8 +493,14 @@ class _StepPlan:
             cnt[s] = float(n)
         self.cnt = cnt.to(dev)
         # uniform population: work items of the stage kernels computed from blockIdx (ConvArgs.u_items)
-        self.uniform = (len(set(sizes)) == 1 and list(slots) == list(range(len(slots)))
+        self.uniform = (len(set(sizes)) == 1 and list(slots) == list(range(len(slots))) and not self.elastic
                         and os.environ.get("DTF_UNIFORM_WORK", "1") == "1")
+        if self.elastic:
+            for s, n in zip(slots, self.real_sizes):
+                cnt[s] = float(n)
+            self.cnt = cnt.to(dev)
+            self.first_t = torch.tensor([self.first[s] for s in slots], dtype=torch.int32, device=dev)
+            self._cnt_stage = None
         self.slots_t = torch.tensor(slots, dtype=torch.int32, device=dev)
         self.slots_long = torch.tensor(slots, dtype=torch.long, device=dev)
         self.loss_sel = torch.zeros(len(slots), dtype=be.loss.dtype, device=dev)
@@ -584,6 +620,8 @@ class _StepPlan:
         self._build()
         assert self._pending_slab is None and not self._deferred and not self._deferred_dense, \
             "every dW slab must be reduced before the optimizer"
+        if self.elastic:
+            self._work_gen_launch()
         self.graph = None
 
     # -------------------------------------------------------------------- work lists
@@ -591,6 +629,9 @@ class _StepPlan:
         """(it0, nit, 0, slot) items over the flattened (image, band) iterations of each member."""
         key = ("it", bands, n_wg)
         w = self._work_cache.get(key)
+        if w is None and self.elastic:
+            w = self._elastic_table(max(1, n_wg // max(1, len(self.slots))), bands, 1)
+            self._work_cache[key] = w
         if w is None:
             items = []
             per_member = max(1, n_wg // max(1, len(self.slots)))
@@ -613,6 +654,48 @@ class _StepPlan:
             a.u_items, a.u_chunk, a.u_per = self._uniform_geo[work.data_ptr()]
             assert a.u_items * len(self.slots) == work.shape[0]
 
+    # ------------------------------------------------------------------ elastic plans
+    def _elastic_table(self, per, bands, min_chunk, split=False):
+        """A work table of `per` rows per member (x2 when split) filled on the device each step from the real batch
+        sizes (work_gen_kernel; same split rule as _work_iters / _work_member, empty rows past a member's end)."""
+        rows = 2 if split else 1
+        host = []
+        for s, n in zip(self.slots, self.real_sizes):
+            total, f = n * bands, self.first[s] * bands
+            chunk = max(min_chunk, -(-total // per), 1)
+            for j in range(per):
+                st = j * chunk
+                nit = min(chunk, total - st) if st < total else 0
+                for z in range(rows):
+                    host.append([f + st if nit > 0 else f, nit, z, s])
+        w = torch.tensor(host, dtype=torch.int32, device=self.be.dev)
+        self._wgen.append((w, per, bands, min_chunk, int(split)))
+        self.__dict__.setdefault("_wgen_params", {})[w.data_ptr()] = (per, bands, min_chunk)
+        return w
+
+    def _work_gen_launch(self):
+        """First launch of an elastic step: regenerate every work table from the per-member sizes (self.cnt)."""
+        descs = (WorkGenDesc * len(self._wgen))()
+        for i, (w, per, bands, mc, sp) in enumerate(self._wgen):
+            descs[i] = WorkGenDesc(w.data_ptr(), per, bands, mc, sp, 0, 0)
+        dt = torch.frombuffer(bytearray(bytes(descs)), dtype=torch.uint8).to(self.be.dev)
+        self._keep(dt)
+        self.launches.insert(0, (ops.lib().dtf_work_gen, (_p(dt), len(self._wgen), _p(self.slots_t),
+                                                          _p(self.first_t), len(self.slots), _p(self.cnt))))
+
+    def set_sizes(self, sizes):
+        """Elastic plan: the real per-member batch sizes of the next step (device cnt; read by the step graph)."""
+        assert self.elastic and len(sizes) == len(self.slots) and max(sizes) <= self.sizes[0]
+        if list(sizes) == self.real_sizes:
+            return
+        self.real_sizes = list(sizes)
+        vals = [0.0] * self.e.capacity
+        for s, n in zip(self.slots, sizes):
+            vals[s] = float(n)
+        if self._cnt_stage is None:
+            self._cnt_stage = PinnedStager(self.e.capacity, torch.float32)
+        self._cnt_stage.upload(self.cnt, vals)
+
     @staticmethod
     def _fwd_split(cin, n_items):
         # DTF_FWD_SPLIT64: "auto" (split when fewer than 256 items), "1" always, "0" never (default: the split
@@ -625,6 +708,10 @@ class _StepPlan:
     def _split_work(self, work):
         key = ("split", work.data_ptr())
         w = self._work_cache.get(key)
+        if w is None and self.elastic:
+            per, bands, min_chunk = self._wgen_params[work.data_ptr()]
+            w = self._elastic_table(per, bands, min_chunk, split=True)
+            self._work_cache[key] = w
         if w is None:
             w = work.repeat_interleave(2, dim=0).contiguous()
             w[1::2, 2] = 1
@@ -651,6 +738,9 @@ class _StepPlan:
     def _work_member(self, target_items=256, min_chunk=1):
         key = ("m", target_items)
         w = self._work_cache.get(key)
+        if w is None and self.elastic:
+            w = self._elastic_table(max(1, target_items // max(1, len(self.slots))), 1, min_chunk)
+            self._work_cache[key] = w
         if w is None:
             items = []
             per_member = max(1, target_items // max(1, len(self.slots)))
@@ -1542,23 +1632,21 @@ class _StepPlan:
 
     # -------------------------------------------------------------------- execution
     def load_batch(self, batches):
-        off = 0
+        # member regions start at self.first[slot] (packed for exact plans, capacity-strided for elastic ones)
         if self.src is None and same_batches(self, batches):
             return  # the staged copy is still current (same unmodified source storage)
         if self.src is not None:
-            for b in batches:
-                n = len(b)
+            for s, b in zip(self.slots, batches):
+                n, off = len(b), self.first[s]
                 self.idx[off:off + n].copy_(b.idx, non_blocking=True)
-                off += n
             if getattr(self, "_rng_stage", None) is None:
                 self._rng_stage = PinnedStager(2, torch.int32)
             self._rng_stage.upload(self.rng, self.src.next_rng())
             return
-        for (x, y) in batches:
-            n = x.shape[0]
+        for s, (x, y) in zip(self.slots, batches):
+            n, off = x.shape[0], self.first[s]
             self.x_in[off:off + n].copy_(x.reshape(n, *self.x_in.shape[1:]), non_blocking=True)
             self.labels[off:off + n].copy_(y, non_blocking=True)
-            off += n
 
     def _run_eager(self):
         e = self.e

@@ -706,7 +706,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
   bf16_t* tile0 = reinterpret_cast<bf16_t*>(smem + 1280);
 
   const int4 wk = a.work[blockIdx.x];
-  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
   const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const float n_in = a.cnt[slot] * (float)(a.Hi * a.Wi);
@@ -848,7 +848,7 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
   STAMP_DECL
   STAMP(0);
   const int4 wk = work_item(a);
-  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
   const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ct = wave % NT + (SPLIT > 1 ? wk.z * NT : 0);
@@ -986,7 +986,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
   bf16_t* tile0 = reinterpret_cast<bf16_t*>(smem + 2304);
 
   const int4 wk = a.work[blockIdx.x];
-  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
   const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // dy lives at the forward-output resolution; the BN transformed on load is the one after this conv.
@@ -1176,7 +1176,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
   bf16_t* xt = reinterpret_cast<bf16_t*>(smem + 1536);
 
   const int4 wk = a.work[blockIdx.x];
-  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
   const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   make_coef<CIN, MODE_X>(coef_x, a, slot, a.cnt[slot] * (float)(a.Hi * a.Wi), a.st_x, nullptr, a.x_gamma, a.x_beta);
@@ -1443,7 +1443,7 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
   STAMP_DECL
   STAMP(0);
   const int4 wk = work_item_at(a, bid);
-  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
   const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ct = wave % NT;

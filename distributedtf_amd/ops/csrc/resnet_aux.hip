@@ -143,6 +143,37 @@ __global__ __launch_bounds__(64) void bn_running_update_kernel(float* __restrict
   run[C + c] = BN_MOM * run[C + c] + (1.f - BN_MOM) * unbiased;
 }
 
+// Elastic (capacity-keyed) step plans: every work table of the captured step is regenerated on the device from
+// the per-member batch sizes (cnt) at the start of each replay, so a batch-size change needs no new plan or graph.
+// Member m owns `per` rows (x2 for a split table): row j covers iterations [j*chunk, j*chunk + chunk) of the
+// member's n * bands (image, band) iterations, chunk = max(min_chunk, ceil(n * bands / per)); rows past the end get
+// nit = 0 (the kernels skip their loop and write zero partials) and point at the member's first iteration.
+struct WorkGenDesc {
+  int4* dst;
+  int per, bands, min_chunk, split;
+  int pad0, pad1;
+};
+
+__global__ __launch_bounds__(256) void work_gen_kernel(const WorkGenDesc* __restrict__ descs,
+                                                       const int* __restrict__ slots, const int* __restrict__ first,
+                                                       const float* __restrict__ cnt) {
+  const WorkGenDesc d = descs[blockIdx.x];
+  const int m = blockIdx.y;
+  const int slot = slots[m];
+  const int total = (int)cnt[slot] * d.bands;
+  const int f = first[m] * d.bands;
+  int chunk = (total + d.per - 1) / d.per;
+  if (chunk < d.min_chunk) chunk = d.min_chunk;
+  if (chunk < 1) chunk = 1;
+  const int rows = d.split ? 2 : 1;
+  for (int j = threadIdx.x; j < d.per; j += blockDim.x) {
+    const int start = j * chunk;
+    const int nit = start < total ? min(chunk, total - start) : 0;
+    const int it0 = nit > 0 ? f + start : f;
+    for (int z = 0; z < rows; ++z) d.dst[((long)m * d.per + j) * rows + z] = make_int4(it0, nit, z, slot);
+  }
+}
+
 // Eval mode: BatchNorm with the moving statistics.  Every consumer derives its coefficients from replicated
 // (sum, sum of squares) accumulators and the per-member count n = cnt * hw, so the moving mean / variance are
 // written in that form (replica 0: n*mean, n*(var + mean^2); replicas 1.. zero) and the training kernels
@@ -287,7 +318,7 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   __shared__ float fpart[2][4][64];
   __shared__ float red[4][2][64];
   const int4 wk = a.work[blockIdx.x];
-  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0 && a.C == 64 && a.hw % 32 == 0 && a.hw <= 32 * HEAD_MAXK &&
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.w >= 0 && a.C == 64 && a.hw % 32 == 0 && a.hw <= 32 * HEAD_MAXK &&
                a.ncls <= 16);
   const int img0 = wk.x, nimg = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane;
@@ -740,6 +771,17 @@ DTF_API int dtf_bn_step_end(float* state, long s_mstride, long run_base, const i
   DTF_HOST_CHECK(stats_fwd != nullptr && stats_bwd != nullptr && grads != nullptr);
   hipLaunchKernelGGL(bn_running_update_kernel, dim3(nbn, nslots, 2), dim3(64), 0, stream, state, s_mstride, run_base,
                      table, stats_bwd, stats_bn_stride, slots, cnt, grads, g_mstride, stats_fwd);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_workgen_desc_size() { return (int)sizeof(WorkGenDesc); }
+
+DTF_API int dtf_work_gen(const void* descs, int ndesc, const int* slots, const int* first, int nslots,
+                         const float* cnt, hipStream_t stream) {
+  if (ndesc <= 0 || nslots <= 0) return 0;
+  DTF_HOST_CHECK(descs != nullptr && slots != nullptr && first != nullptr && cnt != nullptr && ndesc <= 65535);
+  hipLaunchKernelGGL(work_gen_kernel, dim3(ndesc, nslots), dim3(256), 0, stream,
+                     reinterpret_cast<const WorkGenDesc*>(descs), slots, first, cnt);
   return DTF_CHECK_LAUNCH();
 }
 

@@ -41,7 +41,7 @@ def _perturb_bn(arch, engines, n, g):
             e.state[:n, b.beta_off:b.beta_off + b.c] = noise_b.to(dev)
 
 
-def _compare_step(arch, sizes, floor=0.06, seed=0):
+def _compare_step(arch, sizes, floor=0.06, seed=0, warm_sizes=None, check=None):
     """Two optimizer steps on the same batches: step 1 with lr = 0 (the eager warm-up that also captures the HIP
     graph), step 2 with lr = 1 (the first graph REPLAY: device-side step advance, hyper-table refresh, in-graph
     loss gather).  Step 2's parameter delta is its gradient, compared per layer with the fp32 oracle."""
@@ -68,8 +68,17 @@ def _compare_step(arch, sizes, floor=0.06, seed=0):
         y = torch.randint(0, 10, (bs,), generator=g).to(dev)
         batches.append((x, y))
     hps = [_hp(bs) for bs in sizes]
+    if warm_sizes is not None:  # an earlier step with other batch sizes (elastic plans: no new plan / capture)
+        warm = [(torch.randn(bs, 32, 32, 3, generator=g).to(dev), torch.randint(0, 10, (bs,), generator=g).to(dev))
+                for bs in warm_sizes]
+        for e in (ref, r16, hip):
+            e.train_step(slots, warm, [_hp(bs) for bs in warm_sizes], [0.0] * n)
+            e.train_step(slots, warm, [_hp(bs) for bs in warm_sizes], [0.0] * n)
+        plans0 = dict(hip.backend._plans)
     for e in (ref, r16, hip):
         e.train_step(slots, batches, hps, [0.0] * n)
+    if check is not None:
+        check(hip, plans0 if warm_sizes is not None else None)
     before = hip.params.clone()
     assert torch.equal(before, ref.params)
     l_ref = ref.train_step(slots, batches, hps, [1.0] * n)
@@ -126,6 +135,28 @@ def test_hip_step_dual_backward(size, graph, dual, sizes, monkeypatch):
     monkeypatch.setenv("DTF_DUAL_BWD", dual)
     monkeypatch.setenv("DTF_SPLIT_BWD", "0")
     _compare_step(ResNetArch(cifar_config(size, version=2)), sizes)
+
+
+@pytest.mark.parametrize("elastic", ["auto", "0"])
+def test_hip_step_elastic_plan(elastic, monkeypatch):
+    """Mixed batch sizes run on ONE capacity-keyed plan (DTF_ELASTIC): the work tables are regenerated on the device
+    from the per-member sizes each step, so a batch-size change (PBT explore of batch_size) reuses the captured
+    graph.  Warm-up with sizes (20, 9, 14), then the compared graph replay with (12, 17, 6) vs the fp32 oracle;
+    DTF_ELASTIC=0 (exact plans, one per size tuple) as the control."""
+    monkeypatch.setenv("DTF_HIP_GRAPH", "1")
+    monkeypatch.setenv("DTF_ELASTIC", elastic)
+    monkeypatch.setenv("DTF_ELASTIC_MAXB", "24")
+
+    def check(hip, plans0):
+        plans = hip.backend._plans
+        if elastic == "auto":
+            assert len(plans) == 1 and list(plans) == list(plans0), list(plans)
+            p = next(iter(plans.values()))
+            assert p.elastic and p.graph is not None and p.graph is plans0[next(iter(plans0))].graph
+        else:
+            assert len(plans) == 2 and not any(p.elastic for p in plans.values())
+
+    _compare_step(ResNetArch(cifar_config(14, version=2)), [12, 17, 6], warm_sizes=[20, 9, 14], check=check)
 
 
 @pytest.mark.parametrize("size,sizes,split", [(56, [128] * 8, "0"), (56, [128], "auto"), (56, [128], "0"),

@@ -132,6 +132,7 @@ def _register():
                                      c_void_p, c_long, c_void_p])
     ops.register("dtf_bn_running_update", [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_long, c_void_p,
                                            c_int, c_void_p, c_void_p, c_long, c_void_p])
+    ops.register("dtf_wpitch", [c_int])
     ops.register("dtf_work_gen", [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p])
     ops.register("dtf_workgen_desc_size", [])
     ops.register("dtf_bn_step_end", [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_void_p, c_long, c_void_p,
@@ -167,6 +168,17 @@ def _cpad(c: int) -> int:
     if os.environ.get("DTF_CPAD_OLD", "0") == "1":
         return c + 8
     return {16: 16, 32: 48, 64: 80}.get(c, c + 8)
+
+
+_WPITCH = {}
+
+
+def _wpitch(c: int) -> int:
+    """LDS row pitch (pixels) of the stage kernels' C-channel tiles, as compiled into the loaded library."""
+    if c not in _WPITCH:
+        _WPITCH[c] = int(ops.lib().dtf_wpitch(c))
+        assert _WPITCH[c] >= 512 // c + 2, ("unexpected LDS pitch", c, _WPITCH[c])
+    return _WPITCH[c]
 
 
 def _cpad_fwd(c: int) -> int:
@@ -819,6 +831,7 @@ class _StepPlan:
             else:
                 self._set_uniform(a, work)
             a.cin_real = self._stamp_row("fwd", "fwd_s1 C=%d in=%d res=%d" % (cin, mode, res is not None))  # launch ordinal for DTF_STAMP diagnostic builds (unused otherwise)
+            lds = 1280 + 2 * ((rows_in * _wpitch(cin) * _cpad_fwd(cin) + 8 + 63) // 64 * 64) * 2
             self._add(lib.dtf_conv_fwd_s1, ctypes.byref(a), cin, mode, int(res is not None), work.shape[0], lds)
         else:
             self._add(lib.dtf_conv_fwd, ctypes.byref(a), cin, c.cout, c.stride, c.k, mode, int(res is not None),
@@ -958,7 +971,7 @@ class _StepPlan:
             a.st_ep = _p(be.st_f(x_bn))
             a.st_out = _p(be.st_b(x_bn))
         a.Hi, a.Wi, a.Ho, a.Wo, a.rows = H, H, H, H, rows
-        tsz = ((rows + 2) * (H + 2) * _cpad(C) + 8 + 63) // 64 * 64
+        tsz = ((rows + 2) * _wpitch(C) * _cpad(C) + 8 + 63) // 64 * 64
         raw = C >= 64 or os.environ.get("DTF_RAWX16", "0") == "1"  # must match the build (conv.hip RAWX)
         sb = C == 16 and mode_dy != 3 and os.environ.get("DTF_FUSED_SB16", "1") == "1"  # must match conv.hip SB
         nbuf = 2 if sb else 4
@@ -1020,7 +1033,7 @@ class _StepPlan:
         that a side-stream reduction adds into the gradient row."""
         be, L = self.be, self.be.L
         lib = ops.lib()
-        tsz = ((rows + 2) * (H + 2) * _cpad(C) + 8 + 63) // 64 * 64
+        tsz = ((rows + 2) * _wpitch(C) * _cpad(C) + 8 + 63) // 64 * 64
         epi = int(res is not None) | (2 if ident_x else 0)
         # ---- dgrad role
         nd = int(os.environ.get("DTF_SPLIT_DG_ITERS", "1"))
@@ -1076,7 +1089,7 @@ class _StepPlan:
         slabs are reduced by the trailing workgroups of the next backward launch (or a standalone reduction)."""
         be, L = self.be, self.be.L
         lib = ops.lib()
-        tsz = ((rows + 2) * (H + 2) * _cpad(C) + 8 + 63) // 64 * 64
+        tsz = ((rows + 2) * _wpitch(C) * _cpad(C) + 8 + 63) // 64 * 64
         epi = int(res is not None) | (2 if ident_x else 0)
         # ---- dgrad role
         nd = int(os.environ.get("DTF_DUAL_DG_ITERS", "1"))

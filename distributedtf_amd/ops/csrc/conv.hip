@@ -191,6 +191,19 @@ __host__ __device__ constexpr int cpad() {
 #endif
 }
 
+// LDS row pitch (pixels) of the stage kernels' [RT][WP][CP] tiles (conv_fwd_s1, fused / dual backward).  C = 64
+// (W = 8): a 16-pixel MFMA operand gather spans two image rows; with a 16-pixel row pitch the two rows land
+// in disjoint bank halves of the ds_read_b128 lane groups (4 instead of 8 cycles per gather, tools/lds_banks.py;
+// the extra 6 columns are never staged).  Measured: no step-time change at pop 1 / pop 8 (these kernels wait on
+// global memory, not LDS; profiles/r2_wp64_ab.log), so the dense pitch (10) stays the default.
+#ifndef DTF_WP64
+#define DTF_WP64 10
+#endif
+template <int C>
+__host__ __device__ constexpr int wpitch() {
+  return C == 64 ? DTF_WP64 : 512 / C + 2;
+}
+
 // Forward (conv_fwd_s1) pitch: the C = 16 forward measured faster with the +8 pad (1 vs 3 MFMA-operand
 // gathers per row pair, different occupancy) -- the fused backward keeps the unpadded pitch.
 template <int C>
@@ -603,10 +616,11 @@ __device__ __forceinline__ uint4 xform8r(uint4 v, uint4 v2, uint4 v3, int c0, co
 // 256 % (C/8) == 0); per slot: LDS offset, in-band global offset, and three bit masks (column/slot valid,
 // top halo row, bottom halo row) so an iteration only adds its band's row offset.  Inactive slots stage zeros
 // into pixel 0's pad lanes (never read), keeping load/store branch-free.
-template <int C, int RT, int W, int H, int CPV = cpad<C>()>
+template <int C, int RT, int W, int H, int CPV = cpad<C>(), int WPV = W + 2>
 struct Stage {
-  static constexpr int WP = W + 2, CP = CPV, NCH = C / 8, ROW = W * C;
-  static constexpr int TOTAL = RT * WP * NCH, MAXC = (TOTAL + 255) / 256;
+  static constexpr int WD = W + 2, WP = WPV, CP = CPV, NCH = C / 8, ROW = W * C;  // WD staged columns, WP pitch
+  static_assert(WP >= WD, "row pitch covers the staged columns");
+  static constexpr int TOTAL = RT * WD * NCH, MAXC = (TOTAL + 255) / 256;
   int loff[MAXC];
   int goff[MAXC];
   int roff[MAXC];  // band-interior chunks: offset in an unhaloed [RT-2][W][CP] tile (store_raw)
@@ -618,7 +632,7 @@ struct Stage {
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
       const int idx = threadIdx.x + 256 * j;
-      const int pc = idx / NCH, col = pc % WP, r = pc / WP;
+      const int pc = idx / NCH, col = pc % WD, r = pc / WD;
       const bool act = idx < TOTAL;
       loff[j] = act ? (r * WP + col) * CP + c0 : RT * WP * CP;  // inactive: the 8-element slack past the tile
       roff[j] = ((r - 1) * W + (col - 1)) * CP + c0;
@@ -831,13 +845,13 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
   constexpr int W = 512 / C, H = W, ROWS = 8, BANDS = H / ROWS;
   constexpr int NT = C / 16 / SPLIT, WPT = 4 / NT;  // NT: output-channel tiles of this workgroup
   constexpr int KTOT = 9 * C, KS = (KTOT + 31) / 32;
-  constexpr int CP = cpad_fwd<C>(), RT = ROWS + 2, WP = W + 2;
+  constexpr int CP = cpad_fwd<C>(), RT = ROWS + 2, WP = wpitch<C>();
   constexpr int TSZ = (RT * WP * CP + 8 + 63) & ~63;  // + slack for inactive staging slots
   constexpr int NTILES = ROWS * W / 16;
   constexpr int MT = NTILES / WPT;  // output pixel tiles per wave per iteration
   static_assert(NTILES == WPT * MT && MT <= MAXT, "every wave owns MT output tiles");
   constexpr int ROW = W * C, IMG = H * ROW;
-  using St = Stage<C, RT, W, H, CP>;
+  using St = Stage<C, RT, W, H, CP, WP>;
   constexpr int MAXC = St::MAXC;
   constexpr int LMODE = MODE_IN == 0 ? 0 : 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1417,13 +1431,13 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
   constexpr int MT = C / 16;           // wgrad co tiles
   constexpr int NTN = 9 * C / 16;      // wgrad (tap, ci) tiles
   constexpr int NJ = (NTN + 3) / 4;
-  constexpr int CP = cpad<C>(), RT = ROWS + 2, WP = W + 2;
+  constexpr int CP = cpad<C>(), RT = ROWS + 2, WP = wpitch<C>();
   constexpr int TSZ = (RT * WP * CP + 8 + 63) & ~63;  // + slack for inactive staging slots
   constexpr int NTILES = ROWS * W / 16;
   static_assert(NTILES == WPT * MAXT, "every wave owns MAXT dgrad tiles");
   constexpr int ROW = W * C, IMG = H * ROW;
   constexpr int NK = ROWS * W / 32, RSTEP = 32 / W, KINC = RSTEP * WP * CP;
-  using St = Stage<C, RT, W, H>;
+  using St = Stage<C, RT, W, H, CP, WP>;
   constexpr int MAXC = St::MAXC;
   float* coef_d = reinterpret_cast<float*>(smem);  // dy transform (192)
   float* ecoef = coef_d + 192;                     // x BN: scale, shift, -mean*inv, inv (256)
@@ -1949,6 +1963,8 @@ DTF_API int dtf_stamp_read(void* dst, long bytes) {
 }
 
 DTF_API int dtf_conv_args_size() { return (int)sizeof(ConvArgs); }
+// LDS row pitch of the stage kernels (the host sizes their dynamic LDS with it)
+DTF_API int dtf_wpitch(int c) { return c == 16 ? wpitch<16>() : c == 32 ? wpitch<32>() : c == 64 ? wpitch<64>() : -1; }
 
 DTF_API int dtf_conv_fwd(const ConvArgs* args, int cin, int cout, int s, int k, int mode, int resid, int stats,
                          int nblocks, int lds, hipStream_t stream) {

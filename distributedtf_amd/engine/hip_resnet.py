@@ -133,6 +133,7 @@ def _register():
     ops.register("dtf_bn_running_update", [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_long, c_void_p,
                                            c_int, c_void_p, c_void_p, c_long, c_void_p])
     ops.register("dtf_wpitch", [c_int])
+    ops.register("dtf_conv_trans_multi", [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_work_gen", [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p])
     ops.register("dtf_workgen_desc_size", [])
     ops.register("dtf_bn_step_end", [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_void_p, c_long, c_void_p,
@@ -784,6 +785,9 @@ class _StepPlan:
         return b.gamma_off, b.beta_off
 
     def _add(self, fn, *args):
+        if getattr(self, "_grab", None) is not None:
+            self._grab.append((fn, args))  # collected for a combined multi-role launch
+            return
         self.launches.append((fn, args))
 
     def _conv_fwd(self, ci, x, y, stats_bn, in_bn, res=None):
@@ -871,6 +875,27 @@ class _StepPlan:
         lib = ops.lib()
         self._add(lib.dtf_conv_dgrad, ctypes.byref(a), c.cin, c.cout, S, K, mode, epi, work.shape[0], lds)
         self._keep(a)
+
+    def _trans_multi(self, ca_spec):
+        """Combined stage-transition backward launch (conv_trans_multi_kernel): DTF_TRANS_MULTI (default on) for the
+        3x3 / 2 conv_a of a projection block with 16->32 or 32->64 channels; not with the side-stream split."""
+        return (os.environ.get("DTF_TRANS_MULTI", "1") == "1" and not self.split and ca_spec.stride == 2
+                and ca_spec.k == 3 and (ca_spec.cin, ca_spec.cout) in ((16, 32), (32, 64)))
+
+    def _add_trans_multi(self, grabbed, ca_spec):
+        (f_c, args_c), (f_a, args_a), (f_b, args_b) = grabbed
+        lib = ops.lib()
+        assert f_c is lib.dtf_conv_wgrad and f_a is lib.dtf_conv_dgrad and f_b is lib.dtf_conv_wgrad
+        # (byref(args), cin, cout, S, K, mode.., mode.., nblocks, lds)
+        assert args_c[1:6] == (ca_spec.cin, ca_spec.cout, 2, 3, 1) and args_c[6] == 2
+        assert args_a[1:7] == (ca_spec.cin, ca_spec.cout, 2, 1, 0, 0)
+        assert args_b[1:7] == (ca_spec.cin, ca_spec.cout, 2, 1, 1, 0)
+        ac, aa, ab = args_c[0]._obj, args_a[0]._obj, args_b[0]._obj
+        ac.n_main, aa.n_main, ab.n_main = args_c[7], args_a[7], args_b[7]
+        nblocks = args_c[7] + args_a[7] + args_b[7]
+        lds = max(args_c[8], args_a[8], args_b[8])
+        self._add(lib.dtf_conv_trans_multi, ctypes.byref(ac), ctypes.byref(aa), ctypes.byref(ab), ca_spec.cin,
+                  ca_spec.cout, nblocks, lds)
 
     def _conv_wgrad(self, ci, x, dy, mode_x, mode_dy, x_bn=None, dy_bn=None, dy2=None, cin_real=None):
         be, L, e = self.be, self.be.L, self.e
@@ -1392,13 +1417,26 @@ class _StepPlan:
                 self._conv_wgrad(cb, h, g_cur, mode_x=1, mode_dy=0, x_bn=bn2)
             Tin = self._tmp_for(Hi) if Hi != Ho else T
             pd = None
-            if blk.proj is not None:
+            ca_spec = prog.convs[ca]
+            if blk.proj is not None and self._trans_multi(ca_spec):
+                # stage transition: conv_a wgrad + projection dgrad + projection wgrad in one launch
+                pd = self.pd[id(blk)]
+                self._grab = []
+                self._conv_wgrad(ca, x, T["dz2"], mode_x=1, mode_dy=2, x_bn=bn1, dy_bn=bn2, dy2=h)
+                self._conv_dgrad(blk.proj, g_cur, pd, Hi, mode=0, epi=0)
+                self._conv_wgrad(blk.proj, x, g_cur, mode_x=1, mode_dy=0, x_bn=bn1)
+                grabbed, self._grab = self._grab, None
+                self._add_trans_multi(grabbed, ca_spec)
+                self._conv_dgrad(ca, T["dz2"], Tin["dz1"], Hi, mode=2, epi=2 | 1, dy2=h, in_bn=bn2, res=pd, xm=x,
+                                 ep_bn=bn1)
+            elif blk.proj is not None:
                 pd = self.pd[id(blk)]
                 self._conv_dgrad(blk.proj, g_cur, pd, Hi, mode=0, epi=0)
                 self._conv_wgrad(blk.proj, x, g_cur, mode_x=1, mode_dy=0, x_bn=bn1)
             # conv_a: dgrad of BN2-backward(dz2, h) [+ proj dgrad], mask by BN1(x), BN1 reductions
-            ca_spec = prog.convs[ca]
-            if fused and ca_spec.stride == 1 and ca_spec.cin == ca_spec.cout:
+            if blk.proj is not None and self._trans_multi(ca_spec):
+                pass  # conv_a done above
+            elif fused and ca_spec.stride == 1 and ca_spec.cin == ca_spec.cout:
                 self._conv_bwd_fused(ca, T["dz2"], Tin["dz1"], x, mode_dy=2, dy2=h, dy_bn=bn2, x_bn=bn1, res=pd)
             else:
                 self._conv_dgrad(ca, T["dz2"], Tin["dz1"], Hi, mode=2, epi=2 | (1 if pd is not None else 0), dy2=h,

@@ -985,7 +985,7 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
 // Bands are over dx rows (forward-input resolution).
 
 template <int CI, int CO, int S, int K, int MODE_IN, int EPI>
-__global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
+__device__ __forceinline__ void conv_dgrad_body(const ConvArgs& a, const int bid, char* smem) {
   // EPI bit2 (ResNet v1): the masking activation is an identity-BN ReLU output -> mask by xm > 0, no stats
   constexpr bool MASK = (EPI & 6) != 0, IDENT = (EPI & 4) != 0, STATS = (EPI & 2) != 0 && !IDENT;
   constexpr int NT = CI / 16;
@@ -993,13 +993,12 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
   constexpr int KTOT = K * K * CO;
   constexpr int KS = (KTOT + 31) / 32;
   constexpr int P = (K - 1) / 2;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   float* coef = reinterpret_cast<float*>(smem);   // input transform (192)
   float* ecoef = coef + 192;                      // epilogue BN: scale, shift, mean, inv (4 x 64)
   float* acc_lds = ecoef + 256;                   // 128
   bf16_t* tile0 = reinterpret_cast<bf16_t*>(smem + 2304);
 
-  const int4 wk = a.work[blockIdx.x];
+  const int4 wk = a.work[bid];
   DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
   const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1162,7 +1161,7 @@ __global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
   if constexpr (STATS) {
     reduce_stats_to_lds(acc_lds, ssum, ssq, ct * 16 + (lane >> 4) * 4, lane);
     __syncthreads();
-    flush_stats(a.st_out, acc_lds, slot, CI);
+    flush_stats_r(a.st_out, acc_lds, slot, CI, bid);
   }
 }
 
@@ -1178,18 +1177,23 @@ __device__ __forceinline__ s16x4_t ds_read_tr(const bf16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p));
 }
 
+template <int CI, int CO, int S, int K, int MODE_IN, int EPI>
+__global__ __launch_bounds__(256) void conv_dgrad_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  conv_dgrad_body<CI, CO, S, K, MODE_IN, EPI>(a, (int)blockIdx.x, smem);
+}
+
 template <int CIN, int COUT, int S, int K, int MODE_X, int MODE_DY>
-__global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
+__device__ __forceinline__ void conv_wgrad_body(const ConvArgs& a, const int bid, char* smem) {
   constexpr int MT = COUT / 16;
   constexpr int NTN = K * K * CIN / 16;  // n-tiles: (tap, 16-channel chunk)
   constexpr int NJ = (NTN + 3) / 4;
   constexpr int P = (K - 1) / 2;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   float* coef_x = reinterpret_cast<float*>(smem);  // 192
   float* coef_d = coef_x + 192;                   // 192
   bf16_t* xt = reinterpret_cast<bf16_t*>(smem + 1536);
 
-  const int4 wk = a.work[blockIdx.x];
+  const int4 wk = a.work[bid];
   DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
   const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1300,7 +1304,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
   // dense_slab_reduce_multi_kernel; else fp32 atomics into the gradient row.
   const int KK = K * K;
   const long kel = (long)COUT * KK * a.cin_real;
-  float* gb = a.slab ? a.slab + (long)blockIdx.x * kel : a.grads + (long)slot * a.g_mstride + a.g_off;
+  float* gb = a.slab ? a.slab + (long)bid * kel : a.grads + (long)slot * a.g_mstride + a.g_off;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int nt = wave + 4 * j;
@@ -1322,6 +1326,28 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
       }
     }
   }
+}
+
+template <int CIN, int COUT, int S, int K, int MODE_X, int MODE_DY>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  conv_wgrad_body<CIN, COUT, S, K, MODE_X, MODE_DY>(a, (int)blockIdx.x, smem);
+}
+
+// Stage transition of the pre-activation ResNet backward (projection block), three independent roles in ONE
+// launch, all reading the block output gradient g (and dz2 of conv_a): [0, c.n_main) conv_a (3x3 / 2) wgrad,
+// then the projection (1x1 / 2) dgrad (-> pd, added by conv_a's dgrad next), then the projection wgrad.
+// Replaces three launches of a latency-bound small population with one.
+template <int CI, int CO>
+__global__ __launch_bounds__(256) void conv_trans_multi_kernel(ConvArgs c, ConvArgs a, ConvArgs b) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int bx = (int)blockIdx.x;
+  if (bx < c.n_main)
+    conv_wgrad_body<CI, CO, 2, 3, 1, 2>(c, bx, smem);
+  else if (bx < c.n_main + a.n_main)
+    conv_dgrad_body<CI, CO, 2, 1, 0, 0>(a, bx - c.n_main, smem);
+  else
+    conv_wgrad_body<CI, CO, 2, 1, 1, 0>(b, bx - c.n_main - a.n_main, smem);
 }
 
 // Dense dW slabs of several wgrad launches (conv_wgrad_kernel with a slab), reduced after the backward in one launch:
@@ -1963,6 +1989,23 @@ DTF_API int dtf_stamp_read(void* dst, long bytes) {
 }
 
 DTF_API int dtf_conv_args_size() { return (int)sizeof(ConvArgs); }
+
+// conv_trans_multi_kernel: c = conv_a wgrad (3x3 s2), a = projection dgrad (1x1 s2), b = projection wgrad
+DTF_API int dtf_conv_trans_multi(const ConvArgs* c, const ConvArgs* a, const ConvArgs* b, int ci, int co, int nblocks,
+                                 int lds, hipStream_t stream) {
+  DTF_HOST_CHECK(c->work != nullptr && a->work != nullptr && b->work != nullptr);
+  DTF_HOST_CHECK(nblocks == c->n_main + a->n_main + b->n_main && lds <= 160 * 1024);
+  if (nblocks <= 0) return 0;
+#define TM_CASE(CI_, CO_)                                                                                   \
+  if (ci == CI_ && co == CO_) {                                                                           \
+    hipLaunchKernelGGL((conv_trans_multi_kernel<CI_, CO_>), dim3(nblocks), dim3(256), lds, stream, *c, *a, *b); \
+    return DTF_CHECK_LAUNCH();                                                                            \
+  }
+  TM_CASE(16, 32)
+  TM_CASE(32, 64)
+#undef TM_CASE
+  return -1;
+}
 // LDS row pitch of the stage kernels (the host sizes their dynamic LDS with it)
 DTF_API int dtf_wpitch(int c) { return c == 16 ? wpitch<16>() : c == 32 ? wpitch<32>() : c == 64 ? wpitch<64>() : -1; }
 

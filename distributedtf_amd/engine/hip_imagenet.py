@@ -32,6 +32,12 @@ from .hip_resnet import advance_steps, note_step_advanced, same_batches, upload_
 c_void_p, c_int, c_long, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float
 CMAX = 2048
 NPAD_CLS = 1024
+# k depth per LDS stage of the convg forward / data-gradient kernel (32 or 64)
+_CG_BK = int(os.environ.get("DTF_CG_BK", "64"))
+# weight gradient: pixels per k-step (32 or 64), target items per launch, minimum pixels per split-K chunk
+_CG_WPK = int(os.environ.get("DTF_CG_WPK", "32"))
+_CG_WG_TARGET = int(os.environ.get("DTF_CG_WG_TARGET", "1024"))
+_CG_WG_MINCHUNK = int(os.environ.get("DTF_CG_WG_MINCHUNK", "2048"))
 
 
 class CgArgs(ctypes.Structure):
@@ -348,14 +354,19 @@ class _ImageNetPlan:
         return self._hold(torch.tensor(items, dtype=torch.int32, device=self.be.dev))
 
     def _wgrad_work(self, hw_out, co, K):
+        """(slot, p0, p1, o0 | n0/8 << 16) split-K items of the weight gradient: 128 x 128 dW tiles per member, the
+        member's pixels split into chunks so that the launch has about ``_CG_WG_TARGET`` items.  Every item
+        atomically adds its full fp32 tile into the member's gradient row, so the split count is a trade: more
+        items fill the chip, but each split adds 64 KB of atomic traffic per tile (the chip absorbs about 1.3 TB/s
+        of atomic adds).  The former 4096-item target moved ~14 GB of atomics per pop-8 ResNet-50 step."""
         tiles = -(-co // 128) * -(-K // 128)
-        per_member = max(1, -(-4096 // max(1, len(self.slots) * tiles)))
+        per_member = max(1, -(-_CG_WG_TARGET // max(1, len(self.slots) * tiles)))
         items = []
         for s, n in zip(self.slots, self.sizes):
             f = self.first[s]
             p_beg, p_end = f * hw_out * hw_out, (f + n) * hw_out * hw_out
-            chunk = max(512, -(-(p_end - p_beg) // per_member))
-            chunk = (chunk + 31) // 32 * 32
+            chunk = max(_CG_WG_MINCHUNK, -(-(p_end - p_beg) // per_member))
+            chunk = (chunk + 63) // 64 * 64
             for p0 in range(p_beg, p_end, chunk):
                 for o0 in range(0, co, 128):
                     for n0 in range(0, K, 128):
@@ -414,10 +425,10 @@ class _ImageNetPlan:
             trans = (1 if c.stride > 1 else 0) | 2  # | 2: A operand k-major from the forward layout
         a.log2ci = _log2(a.Ci)
         tc = 128 if a.Co >= 128 else 64
-        if a.Co >= 256 and os.environ.get("DTF_CG_TC256", "0") == "1":
-            # 128 x 64 per wave: more MFMA work per LDS byte, but one wave per SIMD -- measured slower (pop 8 x 128:
-            # 111.7 -> 123.4 ms/step, profiles/r2_imagenet_tc256_ab.log), so off
-            tc = 256
+        # (a 256-row tile, 128 x 64 per wave, measured slower: 111.7 -> 123.4 ms/step at pop 8 x 128,
+        # profiles/r2_imagenet_tc256_ab.log -- removed)
+        if _CG_BK == 64 and (not trans or a.Ci >= 64):
+            trans |= 4  # k depth 64 per LDS stage
         work = (self._pix_work(hw_in, a.Co, tc, classes=(0, 1, 2, 3)) if trans & 1
                 else self._pix_work(hw_out, a.Co, tc))
         a.work = _p(work)
@@ -443,7 +454,8 @@ class _ImageNetPlan:
         work = self._wgrad_work(hw_out, c.cout, c.k * c.k * cin)
         a.work = _p(work)
         self._hold(a)
-        self._add(ops.lib().dtf_convg_wgrad, ctypes.byref(a), mode_x, mode_dy, work.shape[0])
+        self._add(ops.lib().dtf_convg_wgrad, ctypes.byref(a), mode_x, mode_dy | (4 if _CG_WPK == 64 else 0),
+                  work.shape[0])
 
     def bn_final(self, bn, hw, backward):
         be, e = self.be, self.e

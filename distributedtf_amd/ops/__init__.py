@@ -113,6 +113,11 @@ class _DebugLib:
         return _CheckedLaunch(self, name, fn)
 
 
+def launcher_name(fn) -> str:
+    """Symbol name of a library launcher (a ctypes function or a debug-mode _CheckedLaunch)."""
+    return fn._o[1] if isinstance(fn, _CheckedLaunch) else fn.__name__
+
+
 class _CheckedLaunch:
     """A launcher of the debug library: calls through, then synchronises and checks (see _DebugLib).
     ``argtypes`` / ``restype`` read and write the underlying ctypes function."""

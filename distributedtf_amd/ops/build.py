@@ -54,7 +54,8 @@ def build(force: bool = False, verbose: bool = True, extra_flags=None, out: str 
     objs = []
     procs = []
     for src in sources():
-        obj = os.path.join(CSRC, os.path.basename(src) + ".%d.o" % os.getpid())
+        # per-process and per-library object names: the three libraries may build concurrently
+        obj = os.path.join(CSRC, "%s.%d.%s.o" % (os.path.basename(src), os.getpid(), os.path.basename(out)))
         cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
                "-Wno-unused-result", "-munsafe-fp-atomics"] + list(extra_flags or [])
         procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))

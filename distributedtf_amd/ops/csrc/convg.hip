@@ -58,7 +58,6 @@ struct CgArgs {
 };
 
 constexpr int TP = 128;   // pixels per workgroup tile
-constexpr int RP = 40;    // [rows][32] tile pitch (+16 B)
 
 // ---------------------------------------------------------------------------------------------- fwd / dgrad
 // MODE: 0 identity, 1 relu(x*s + t), 2 A*x + B*x2 + C.   EPI: bit0 residual, bit1 mask, bit2 stats (fwd: y, y^2;
@@ -66,13 +65,22 @@ constexpr int RP = 40;    // [rows][32] tile pitch (+16 B)
 // AKM (data gradient): the A operand (rows = dx channels i, k = (tap', dy channel o)) is read straight from the
 // FORWARD weight layout W[o][tap][i] (k-major: 8 consecutive i per 16-byte load, fragments via
 // ds_read_b64_tr_b16), so no transposed weight copy exists.
-template <int TC, int MODE, int EPI, bool TRANS, bool AKM = false>
+// BK: k depth per LDS stage (32 or 64).  BK = 64 halves the barriers and fragment-read restarts per MFMA and doubles
+// the bytes in flight per load batch; it needs Ci >= 64 on the incremental (one tap per k-step) gather path.
+template <int TC, int MODE, int EPI, bool TRANS, bool AKM = false, int BK = 32>
 __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
-  constexpr int KPA = TC + 8;  // [32][TC] k-major A tile pitch
-  constexpr int MT = TC / 32;  // MFMA row tiles per wave (wave covers TC/2 rows)
-  constexpr int SA = (TC * RP > 32 * KPA) ? TC * RP : 32 * KPA;
-  __shared__ __attribute__((aligned(16))) bf16_t sa[2][SA];
-  __shared__ __attribute__((aligned(16))) bf16_t sb[2][TP * RP];
+  constexpr int RP = BK + 8;        // [rows][BK] tile pitch (+16 B)
+  constexpr int CPR = BK / 8;       // 16-byte chunks per tile row
+  constexpr int RPT = 256 / CPR;    // tile rows covered per pass of the workgroup
+  constexpr int NJ = TP / RPT;      // B (pixel) rows per thread
+  constexpr int KPA = TC + 8;       // [BK][TC] k-major A tile pitch
+  constexpr int MT = TC / 32;       // MFMA row tiles per wave (wave covers TC/2 rows)
+  constexpr int SA = (TC * RP > BK * KPA) ? TC * RP : BK * KPA;
+  constexpr int CPF = TC + 4;  // epilogue staging row pitch (floats; 16-byte rows, conflict-free float4 stores)
+  constexpr int SOPS = 2 * SA + 2 * TP * RP, SEPI = 2 * TP * CPF;  // bf16 elements: operand buffers | staging
+  __shared__ __attribute__((aligned(16))) bf16_t smem_[SOPS > SEPI ? SOPS : SEPI];
+  bf16_t (*sa)[SA] = reinterpret_cast<bf16_t (*)[SA]>(smem_);
+  bf16_t (*sb)[TP * RP] = reinterpret_cast<bf16_t (*)[TP * RP]>(smem_ + 2 * SA);
   extern __shared__ float dyn[];  // transform coefficients: MODE 1: 2*Ci, MODE 2: 3*Ci
   __shared__ float acc_lds[2][TC];
   const int4 wk = a.work[blockIdx.x];
@@ -104,15 +112,15 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
     }
   }
   for (int i = tid; i < 2 * TC; i += 256) (&acc_lds[0][0])[i] = 0.f;
-  // per-thread B rows (pixels): r = (tid >> 2) + 64 j, chunk c = tid & 3
-  const int cB = tid & 3;
-  int pix_img[2], pix_y[2], pix_x[2];
-  bool pix_ok[2];
+  // per-thread B rows (pixels): r = tid / CPR + RPT j, chunk c = tid % CPR
+  const int cB = tid % CPR, rB = tid / CPR;
+  int pix_img[NJ], pix_y[NJ], pix_x[NJ];
+  bool pix_ok[NJ];
   const int GH = TRANS ? a.Hi : a.Ho, GW = TRANS ? a.Wi : a.Wo;  // pixel grid of the work items
   const int HWo = GH * GW;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int p = p0 + (tid >> 2) + 64 * j;
+  for (int j = 0; j < NJ; ++j) {
+    const int p = p0 + rB + RPT * j;
     pix_ok[j] = p < p1;
     const int pp = pix_ok[j] ? p : p0;
     pix_img[j] = pp / HWo;
@@ -122,10 +130,10 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   }
   const bf16_t* wbase = a.w + (long)slot * a.w_mstride + a.w_off;
   const long img_elems = (long)a.Hi * a.Wi * Ci;
-  // gather position of this thread's chunk: for Ci >= 32 a 32-wide k-step lies inside one tap, so the tap
+  // gather position of this thread's chunk: for Ci >= BK a BK-wide k-step lies inside one tap, so the tap
   // indices (ty, tx) along the (possibly parity-strided) tap grid and ci advance incrementally (no division in the
-  // loop); Ci < 32 (the channel-padded stem) decomposes k per step
-  const bool inc = Ci >= 32;
+  // loop); Ci < BK (the channel-padded stem) decomposes k per step
+  const bool inc = Ci >= BK;
   const int kstep = TRANS ? 2 : 1;
   int g_ty = 0, g_tx = 0, g_ci = 8 * cB;
   int cur_ky = 0, cur_kx = 0, cur_ci = 0;  // position of this thread's chunk in the current k-step
@@ -134,10 +142,10 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   // of the gathered image (forward: y0 = y*S - P; stride-2 data gradient: the class-grid origin), valid iff bit
   // ty of rmask and bit tx of cmask are set; pbase = element offset of (img, y0, x0) (may be negative: only used
   // when valid).  A k-step then costs one mask test and one add per pixel.
-  long pbase[2];
-  unsigned rmask[2], cmask[2];
+  long pbase[NJ];
+  unsigned rmask[NJ], cmask[NJ];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < NJ; ++j) {
     int y0, x0;
     if constexpr (TRANS) {  // class pixel (2*qy + py): dy row (py + ky - pad) / 2 + qy (even numerator)
       y0 = pix_y[j] + ((py + ky0 - a.pad) >> 1);
@@ -160,7 +168,7 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
       cur_ky = ky0 + kstep * g_ty;
       cur_kx = kx0 + kstep * g_tx;
       cur_ci = g_ci;
-      g_ci += 32;
+      g_ci += BK;
       if (g_ci >= Ci) {
         g_ci -= Ci;
         if (++g_tx >= nkx) {
@@ -168,7 +176,7 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
           ++g_ty;
         }
       }
-    } else {  // Ci < 32 only occurs for the (non-transposed) channel-padded stem
+    } else {  // Ci < BK only occurs for the (non-transposed) channel-padded stem
       const int k = k0 + 8 * cB;
       const int tap = k >> a.log2ci;
       cur_ci = k & (Ci - 1);
@@ -178,14 +186,14 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
       cur_tx = cur_kx;
     }
   };
-  auto load_b = [&](int k0, uint4 (&v)[2], uint4 (&v2)[2], int& cch, unsigned& okb) {
+  auto load_b = [&](int k0, uint4 (&v)[NJ], uint4 (&v2)[NJ], int& cch, unsigned& okb) {
     const int k = k0 + 8 * cB;
     const int ty = cur_ty, tx = cur_tx, ci0 = cur_ci;
     const int toff = (ty * a.Wi + tx) * Ci + ci0;
     cch = ci0;
     okb = 0;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const bool ok = ((rmask[j] >> ty) & (cmask[j] >> tx) & 1u) && k < K;
       v[j] = make_uint4(0, 0, 0, 0);
       v2[j] = make_uint4(0, 0, 0, 0);
@@ -197,9 +205,9 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
       }
     }
   };
-  auto xform_store = [&](bf16_t* dst, const uint4 (&v)[2], const uint4 (&v2)[2], int cch, unsigned okb) {
+  auto xform_store = [&](bf16_t* dst, const uint4 (&v)[NJ], const uint4 (&v2)[NJ], int cch, unsigned okb) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       uint4 t = v[j];
       if (!((okb >> j) & 1u)) {
         t = make_uint4(0, 0, 0, 0);
@@ -222,16 +230,16 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
         }
         t = make_uint4(w32[0], w32[1], w32[2], w32[3]);
       }
-      *reinterpret_cast<uint4*>(dst + ((tid >> 2) + 64 * j) * RP + 8 * cB) = t;
+      *reinterpret_cast<uint4*>(dst + (rB + RPT * j) * RP + 8 * cB) = t;
     }
   };
-  // A (weights): rows o0 + r, r = (tid >> 2) + 64 j (j < TC / 64)
-  constexpr int AJ = TC / 64;
+  // A (weights): rows o0 + r, r = tid / CPR + RPT j (j < TC / RPT); AKM: k rows kr = tid / ACH + (256 / ACH) j
+  constexpr int AJ = TC * BK / 2048;
   constexpr int ACH = TC / 8;  // AKM: 8-row chunks per k row
   auto load_a = [&](int k0, uint4 (&v)[AJ]) {
     const int k = k0 + 8 * cB;
     if constexpr (AKM) {
-      // k rows kr = tid / ACH + (256 / ACH) j; all 32 k of a step share one tap (Ci >= 32)
+      // all BK k of a step share one tap (Ci >= BK)
       const int kk = a.kh * a.kw;
       const int tapf = kk - 1 - (cur_ky * a.kw + cur_kx);  // forward tap of the flipped tap'
       const int obase = cur_ci - 8 * cB;                     // first dy channel of this k step
@@ -247,7 +255,7 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
       const int kcol = TRANS ? (cur_ky * a.kw + cur_kx) * Ci + cur_ci : k;  // column in the full [o][K] row
 #pragma unroll
       for (int j = 0; j < AJ; ++j) {
-        const int r = (tid >> 2) + 64 * j;
+        const int r = rB + RPT * j;
         v[j] = (o0 + r < a.Co && k < K) ? *reinterpret_cast<const uint4*>(wbase + (long)(o0 + r) * Kfull + kcol)
                                         : make_uint4(0, 0, 0, 0);
       }
@@ -259,7 +267,7 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
       if constexpr (AKM)
         *reinterpret_cast<uint4*>(dst + (tid / ACH + (256 / ACH) * j) * KPA + 8 * (tid % ACH)) = v[j];
       else
-        *reinterpret_cast<uint4*>(dst + ((tid >> 2) + 64 * j) * RP + 8 * cB) = v[j];
+        *reinterpret_cast<uint4*>(dst + (rB + RPT * j) * RP + 8 * cB) = v[j];
     }
   };
   f32x4_t acc[MT][4];
@@ -268,8 +276,8 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[m][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
   __syncthreads();  // coefficients in LDS
-  const int nk = (K + 31) / 32;
-  uint4 ra[AJ], rb[2], rb2[2];
+  const int nk = (K + BK - 1) / BK;
+  uint4 ra[AJ], rb[NJ], rb2[NJ];
   int cch;
   unsigned okb;
   next_pos(0);
@@ -283,115 +291,144 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
     const bool more = ks + 1 < nk;
     int ncch = 0;
     if (more) {
-      next_pos(32 * (ks + 1));
-      load_a(32 * (ks + 1), ra);
-      load_b(32 * (ks + 1), rb, rb2, ncch, okb);
+      next_pos(BK * (ks + 1));
+      load_a(BK * (ks + 1), ra);
+      load_b(BK * (ks + 1), rb, rb2, ncch, okb);
     }
-    bf16x8_t fa[MT], fb[4];
 #pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      if constexpr (AKM) {
-        const int g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
-        const int rb = wr * (TC / 2) + 16 * m + 4 * p4;
-        const s16x4_t lo = ds_read_tr(sa[cur] + (8 * g + q) * KPA + rb);
-        const s16x4_t hi = ds_read_tr(sa[cur] + (8 * g + 4 + q) * KPA + rb);
-        fa[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      } else {
-        fa[m] = *reinterpret_cast<const bf16x8_t*>(sa[cur] + (wr * (TC / 2) + 16 * m + (lane & 15)) * RP +
-                                                   8 * (lane >> 4));
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8_t fa[MT], fb[4];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        if constexpr (AKM) {
+          const int g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
+          const int rb_ = wr * (TC / 2) + 16 * m + 4 * p4;
+          const s16x4_t lo = ds_read_tr(sa[cur] + (32 * kk + 8 * g + q) * KPA + rb_);
+          const s16x4_t hi = ds_read_tr(sa[cur] + (32 * kk + 8 * g + 4 + q) * KPA + rb_);
+          fa[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        } else {
+          fa[m] = *reinterpret_cast<const bf16x8_t*>(sa[cur] + (wr * (TC / 2) + 16 * m + (lane & 15)) * RP +
+                                                     32 * kk + 8 * (lane >> 4));
+        }
       }
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+        fb[n] = *reinterpret_cast<const bf16x8_t*>(sb[cur] + (wc * 64 + 16 * n + (lane & 15)) * RP + 32 * kk +
+                                                   8 * (lane >> 4));
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(fa[m], fb[n], acc[m][n]);
     }
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-      fb[n] = *reinterpret_cast<const bf16x8_t*>(sb[cur] + (wc * 64 + 16 * n + (lane & 15)) * RP + 8 * (lane >> 4));
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(fa[m], fb[n], acc[m][n]);
     if (more) {
       store_a(sa[cur ^ 1], ra);
       xform_store(sb[cur ^ 1], rb, rb2, ncch, okb);
     }
     __syncthreads();
   }
-  // epilogue: lane holds pixel col (lane & 15), rows (output channels) 4*(lane>>4) + r
-  const float* ep = a.c_ep + (long)slot * 4 * a.cmax;
+  // ---- epilogue through LDS: the fp32 tile is staged as [pixel][channel] rows (the k loop ended with a barrier,
+  // so the operand buffers are free), then every thread owns one 16-byte channel chunk of a pixel row: the
+  // residual / mask loads and the bf16 store are whole contiguous row segments (TC * 2 bytes per pixel) instead
+  // of 8-byte pieces of 16 pixel rows per wave instruction
+  float* cst = reinterpret_cast<float*>(smem_);
 #pragma unroll
-  for (int m = 0; m < MT; ++m) {
-    const int oc = o0 + wr * (TC / 2) + 16 * m + 4 * (lane >> 4);
-    float ss[4] = {0.f, 0.f, 0.f, 0.f}, sq[4] = {0.f, 0.f, 0.f, 0.f};
-    float esc[4], esh[4], emu[4], eiv[4];
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+      *reinterpret_cast<f32x4_t*>(cst + (wc * 64 + 16 * n + (lane & 15)) * CPF + wr * (TC / 2) + 16 * m +
+                                  4 * (lane >> 4)) = acc[m][n];
+  __syncthreads();
+  constexpr int CH = TC / 8;     // 16-byte channel chunks per pixel row
+  constexpr int PPP = 256 / CH;  // pixel rows per pass of the workgroup
+  const int ch = tid % CH, pr = tid / CH;
+  const int oc = o0 + 8 * ch;
+  const bool cok = oc < a.Co;  // Co % 8 == 0 (host check)
+  float esc[8], esh[8], emu[8], eiv[8];
+  if constexpr (EPI & 2) {
+    const float* ep = a.c_ep + (long)slot * 4 * a.cmax + (cok ? oc : 0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float4 u0 = *reinterpret_cast<const float4*>(ep + 4 * h);
+      const float4 u1 = *reinterpret_cast<const float4*>(ep + a.cmax + 4 * h);
+      const float4 u2 = *reinterpret_cast<const float4*>(ep + 2 * a.cmax + 4 * h);
+      const float4 u3 = *reinterpret_cast<const float4*>(ep + 3 * a.cmax + 4 * h);
+      esc[4 * h] = u0.x; esc[4 * h + 1] = u0.y; esc[4 * h + 2] = u0.z; esc[4 * h + 3] = u0.w;
+      esh[4 * h] = u1.x; esh[4 * h + 1] = u1.y; esh[4 * h + 2] = u1.z; esh[4 * h + 3] = u1.w;
+      emu[4 * h] = u2.x; emu[4 * h + 1] = u2.y; emu[4 * h + 2] = u2.z; emu[4 * h + 3] = u2.w;
+      eiv[4 * h] = u3.x; eiv[4 * h + 1] = u3.y; eiv[4 * h + 2] = u3.z; eiv[4 * h + 3] = u3.w;
+    }
+  }
+  float ss[8], sq[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ss[i] = sq[i] = 0.f;
+#pragma unroll 2
+  for (int it = 0; it < TP / PPP; ++it) {
+    const int pl = pr + PPP * it;
+    const int p = p0 + pl;
+    if (p >= p1 || !cok) continue;
+    long pf = p;  // output pixel (full resolution)
+    if constexpr (TRANS) {
+      const int img = p / HWo, rem = p - img * HWo, qy = rem / GW, qx = rem - qy * GW;
+      pf = ((long)img * a.Ho + 2 * qy + py) * a.Wo + 2 * qx + px;
+    }
+    const long o = pf * a.Co + oc;
+    const float4 c0 = *reinterpret_cast<const float4*>(cst + pl * CPF + 8 * ch);
+    const float4 c1 = *reinterpret_cast<const float4*>(cst + pl * CPF + 8 * ch + 4);
+    float v[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    uint4 rr = make_uint4(0, 0, 0, 0), xr = make_uint4(0, 0, 0, 0);
+    if constexpr (EPI & 1) rr = *reinterpret_cast<const uint4*>(a.res + o);
+    if constexpr (EPI & 2) xr = *reinterpret_cast<const uint4*>(a.xm + o);
+    const uint32_t r32[4] = {rr.x, rr.y, rr.z, rr.w}, x32[4] = {xr.x, xr.y, xr.z, xr.w};
+    float xv[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      xv[2 * q] = __uint_as_float(x32[q] << 16);
+      xv[2 * q + 1] = __uint_as_float(x32[q] & 0xffff0000u);
+      if constexpr (EPI & 1) {
+        v[2 * q] += __uint_as_float(r32[q] << 16);
+        v[2 * q + 1] += __uint_as_float(r32[q] & 0xffff0000u);
+      }
+    }
     if constexpr (EPI & 2) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int c = min(oc + r, a.Co - 1);
-        esc[r] = ep[c];
-        esh[r] = ep[a.cmax + c];
-        emu[r] = ep[2 * a.cmax + c];
-        eiv[r] = ep[3 * a.cmax + c];
-      }
+      for (int i = 0; i < 8; ++i) v[i] = (xv[i] * esc[i] + esh[i] > 0.f) ? v[i] : 0.f;
     }
+    uint32_t pk[4];
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const int p = p0 + wc * 64 + 16 * n + (lane & 15);
-      if (p >= p1 || oc >= a.Co) continue;
-      long pf = p;  // output pixel (full resolution)
-      if constexpr (TRANS) {
-        const int img = p / HWo, rem = p - img * HWo, qy = rem / GW, qx = rem - qy * GW;
-        pf = ((long)img * a.Ho + 2 * qy + py) * a.Wo + 2 * qx + px;
-      }
-      const long o = pf * a.Co + oc;
-      float v[4] = {acc[m][n][0], acc[m][n][1], acc[m][n][2], acc[m][n][3]};
-      if constexpr (EPI & 1) {
-        const uint2 rr = *reinterpret_cast<const uint2*>(a.res + o);
-        v[0] += bf2f((bf16_t)(rr.x & 0xffff));
-        v[1] += bf2f((bf16_t)(rr.x >> 16));
-        v[2] += bf2f((bf16_t)(rr.y & 0xffff));
-        v[3] += bf2f((bf16_t)(rr.y >> 16));
-      }
-      float xv[4] = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (EPI & 2) {
-        const uint2 xr = *reinterpret_cast<const uint2*>(a.xm + o);
-        xv[0] = bf2f((bf16_t)(xr.x & 0xffff));
-        xv[1] = bf2f((bf16_t)(xr.x >> 16));
-        xv[2] = bf2f((bf16_t)(xr.y & 0xffff));
-        xv[3] = bf2f((bf16_t)(xr.y >> 16));
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (xv[r] * esc[r] + esh[r] > 0.f) ? v[r] : 0.f;
-      }
-      uint2 pk;
-      pk.x = pack2bf(v[0], v[1]);
-      pk.y = pack2bf(v[2], v[3]);
-      *reinterpret_cast<uint2*>(a.y + o) = pk;
-      if constexpr (EPI & 4) {
-        const float r4[4] = {bf2f((bf16_t)(pk.x & 0xffff)), bf2f((bf16_t)(pk.x >> 16)), bf2f((bf16_t)(pk.y & 0xffff)),
-                             bf2f((bf16_t)(pk.y >> 16))};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          ss[r] += r4[r];
-          if constexpr (EPI & 2) sq[r] += r4[r] * (xv[r] - emu[r]) * eiv[r];
-          else sq[r] += r4[r] * r4[r];
-        }
-      }
-    }
+    for (int q = 0; q < 4; ++q) pk[q] = pack2bf(v[2 * q], v[2 * q + 1]);
+    *reinterpret_cast<uint4*>(a.y + o) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
     if constexpr (EPI & 4) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float s = ss[r], q = sq[r];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          s += __shfl_xor(s, o, 64);
-          q += __shfl_xor(q, o, 64);
-        }
-        if ((lane & 15) == 0 && oc + r < a.Co) {
-          const int lc = oc + r - o0;
-          atomicAdd(&acc_lds[0][lc], s);
-          atomicAdd(&acc_lds[1][lc], q);
+      for (int q = 0; q < 4; ++q) {
+        const float r0 = __uint_as_float(pk[q] << 16), r1 = __uint_as_float(pk[q] & 0xffff0000u);
+        ss[2 * q] += r0;
+        ss[2 * q + 1] += r1;
+        if constexpr (EPI & 2) {
+          sq[2 * q] += r0 * (xv[2 * q] - emu[2 * q]) * eiv[2 * q];
+          sq[2 * q + 1] += r1 * (xv[2 * q + 1] - emu[2 * q + 1]) * eiv[2 * q + 1];
+        } else {
+          sq[2 * q] += r0 * r0;
+          sq[2 * q + 1] += r1 * r1;
         }
       }
     }
   }
   if constexpr (EPI & 4) {
+    // lanes l, l + CH, l + 2 CH, .. of a wave hold the same channel chunk: butterfly over them, then one LDS
+    // atomic per wave and channel, one global atomic per workgroup and channel
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float s_ = ss[i], q_ = sq[i];
+#pragma unroll
+      for (int o = CH; o < 64; o <<= 1) {
+        s_ += __shfl_xor(s_, o, 64);
+        q_ += __shfl_xor(q_, o, 64);
+      }
+      if (lane < CH && cok) {
+        atomicAdd(&acc_lds[0][8 * ch + i], s_);
+        atomicAdd(&acc_lds[1][8 * ch + i], q_);
+      }
+    }
     __syncthreads();
     if (tid < TC && o0 + tid < a.Co) {
       float* st = a.st_out + (long)slot * 2 * a.cmax;
@@ -402,14 +439,15 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------- wgrad
-// Tile: 128 output channels (rows) x 128 (tap, ci) columns, k = 32 output pixels per step.
+// Tile: 128 output channels (rows) x 128 (tap, ci) columns, k = PK output pixels per step (32 or 64).
 constexpr int WT = 128;
 constexpr int KP = WT + 8;
 
-template <int MODE_X, int MODE_DY>
+template <int MODE_X, int MODE_DY, int PK = 32>
 __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16_t sd[2][32 * KP];
-  __shared__ __attribute__((aligned(16))) bf16_t sx[2][32 * KP];
+  constexpr int NJ = PK / 16;  // pixel rows per thread per k-step
+  __shared__ __attribute__((aligned(16))) bf16_t sd[2][PK * KP];
+  __shared__ __attribute__((aligned(16))) bf16_t sx[2][PK * KP];
   extern __shared__ float dyn[];  // x coefficients (2*Ci) then dy coefficients (3*Co)
   const int4 wk = a.work[blockIdx.x];
   DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z >= wk.y);
@@ -457,12 +495,12 @@ __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
       r -= d;
     }
   };
-  // Pixel table of a k-step (32 output pixels), computed by the first 32 threads one k-step ahead and shared
+  // Pixel table of a k-step (PK output pixels), computed by the first PK threads one k-step ahead and shared
   // through LDS (every pixel used to be decomposed by all 16 column-chunk threads of its row):
   // {dy element offset, x image base, oy*S - P, ox*S - P}; an out-of-range pixel gets oy*S - P = -2^30.
-  __shared__ int4 pinfo[2][32];
+  __shared__ int4 pinfo[2][PK];
   auto make_pinfo = [&](int pk0) {
-    if (tid < 32) {
+    if (tid < PK) {
       const int p = pk0 + tid;
       int4 inf = make_int4(0, 0, -(1 << 30), 0);
       if (p < p1) {
@@ -472,14 +510,14 @@ __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
         inf = make_int4((int)((unsigned)p * (unsigned)Co), (int)((unsigned)img * (unsigned)img_x),
                         oy * a.stride - a.pad, ox * a.stride - a.pad);
       }
-      pinfo[(pk0 - p0) / 32 & 1][tid] = inf;
+      pinfo[(pk0 - p0) / PK & 1][tid] = inf;
     }
   };
-  auto load = [&](int pk0, uint4 (&dv)[2], uint4 (&dv2)[2], uint4 (&xv)[2], unsigned& okm) {
+  auto load = [&](int pk0, uint4 (&dv)[NJ], uint4 (&dv2)[NJ], uint4 (&xv)[NJ], unsigned& okm) {
     okm = 0;
-    const int par = (pk0 - p0) / 32 & 1;
+    const int par = (pk0 - p0) / PK & 1;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const int4 inf = pinfo[par][kr + 16 * j];
       const bool pin = inf.z > -(1 << 29);
       dv[j] = dv2[j] = xv[j] = make_uint4(0, 0, 0, 0);
@@ -492,14 +530,14 @@ __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
       const int gy = inf.z + xky, gx = inf.w + xkx;
       if (pin && xcol_ok && gy >= 0 && gy < a.Hi && gx >= 0 && gx < a.Wi) {
         xv[j] = *reinterpret_cast<const uint4*>(a.x + (unsigned)inf.y + (unsigned)((gy * a.Wi + gx) * Ci + xci));
-        okm |= 4u << j;
+        okm |= (1u << NJ) << j;
       }
     }
   };
-  auto store = [&](bf16_t* d, bf16_t* xx, const uint4 (&dv)[2], const uint4 (&dv2)[2], const uint4 (&xv)[2],
+  auto store = [&](bf16_t* d, bf16_t* xx, const uint4 (&dv)[NJ], const uint4 (&dv2)[NJ], const uint4 (&xv)[NJ],
                    unsigned okm) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       uint4 t = dv[j];
       if (MODE_DY != 0 && ((okm >> j) & 1u)) {
         uint32_t w32[4] = {t.x, t.y, t.z, t.w};
@@ -522,7 +560,7 @@ __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
       }
       *reinterpret_cast<uint4*>(d + (kr + 16 * j) * KP + 8 * cc) = t;
       uint4 u = xv[j];
-      if (MODE_X == 1 && ((okm >> (2 + j)) & 1u)) {
+      if (MODE_X == 1 && ((okm >> (NJ + j)) & 1u)) {
         uint32_t w32[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -540,11 +578,11 @@ __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
   for (int m = 0; m < 4; ++m)
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[m][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  const int nk = (p1 - p0 + 31) / 32;
+  const int nk = (p1 - p0 + PK - 1) / PK;
   make_pinfo(p0);
-  if (nk > 1) make_pinfo(p0 + 32);
+  if (nk > 1) make_pinfo(p0 + PK);
   __syncthreads();  // coefficients + the first two pixel tables
-  uint4 dv[2], dv2[2], xv[2];
+  uint4 dv[NJ], dv2[NJ], xv[NJ];
   unsigned okm;
   load(p0, dv, dv2, xv, okm);
   store(sd[0], sx[0], dv, dv2, xv, okm);
@@ -553,28 +591,31 @@ __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
   for (int ks = 0; ks < nk; ++ks) {
     const int cur = ks & 1;
     const bool more = ks + 1 < nk;
-    if (more) load(p0 + 32 * (ks + 1), dv, dv2, xv, okm);
+    if (more) load(p0 + PK * (ks + 1), dv, dv2, xv, okm);
     // table of k-step ks + 2 into the slot k-step ks read (its readers passed the previous barrier)
-    if (ks + 2 < nk) make_pinfo(p0 + 32 * (ks + 2));
-    bf16x8_t fa[4], fb[4];
+    if (ks + 2 < nk) make_pinfo(p0 + PK * (ks + 2));
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int cb = wr * 64 + 16 * m + 4 * p4;
-      const s16x4_t lo = ds_read_tr(sd[cur] + (8 * g + q) * KP + cb);
-      const s16x4_t hi = ds_read_tr(sd[cur] + (8 * g + 4 + q) * KP + cb);
-      fa[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    for (int kk = 0; kk < PK / 32; ++kk) {
+      bf16x8_t fa[4], fb[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int cb = wr * 64 + 16 * m + 4 * p4;
+        const s16x4_t lo = ds_read_tr(sd[cur] + (32 * kk + 8 * g + q) * KP + cb);
+        const s16x4_t hi = ds_read_tr(sd[cur] + (32 * kk + 8 * g + 4 + q) * KP + cb);
+        fa[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int cb = wc * 64 + 16 * n + 4 * p4;
+        const s16x4_t lo = ds_read_tr(sx[cur] + (32 * kk + 8 * g + q) * KP + cb);
+        const s16x4_t hi = ds_read_tr(sx[cur] + (32 * kk + 8 * g + 4 + q) * KP + cb);
+        fb[n] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(fa[m], fb[n], acc[m][n]);
     }
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const int cb = wc * 64 + 16 * n + 4 * p4;
-      const s16x4_t lo = ds_read_tr(sx[cur] + (8 * g + q) * KP + cb);
-      const s16x4_t hi = ds_read_tr(sx[cur] + (8 * g + 4 + q) * KP + cb);
-      fb[n] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    }
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(fa[m], fb[n], acc[m][n]);
     if (more) store(sd[cur ^ 1], sx[cur ^ 1], dv, dv2, xv, okm);
     __syncthreads();
   }
@@ -603,60 +644,69 @@ __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
 
 DTF_API int dtf_cg_args_size() { return (int)sizeof(CgArgs); }
 
-// flags: tc (64 | 128), mode (0..2), epi (0..7), trans (0/1)
+// flags: tc (64 | 128), mode (0..2), epi (0..7), trans: bit0 transposed gather, bit1 A operand k-major from the
+// forward weight layout (data gradient), bit2 BK = 64 (k depth per LDS stage; else 32)
 DTF_API int dtf_convg_fwd(const CgArgs* a, int tc, int mode, int epi, int trans, int nwork, hipStream_t stream) {
-  // trans bit1 (value 2): A operand from the forward weight layout (data gradient, AKM)
   const int akm = (trans >> 1) & 1;
+  const int bk64 = (trans >> 2) & 1;
   trans &= 1;
   if (nwork <= 0) return 0;
-  if ((a->Ci & (a->Ci - 1)) != 0 || a->Ci < 8 || (a->Co & 3) != 0) return -2;
+  if ((a->Ci & (a->Ci - 1)) != 0 || a->Ci < 8 || (a->Co & 7) != 0) return -2;
+  // the incremental one-tap-per-k-step gather of the dgrad (AKM / transposed) path needs Ci >= BK
+  if ((akm || trans) && a->Ci < (bk64 ? 64 : 32)) return -2;
   const size_t dyn = (size_t)(mode == 0 ? 0 : (mode == 1 ? 2 : 3)) * a->Ci * sizeof(float);
   dim3 grid(nwork), block(256);
-#define CG_CASE(TC_, M_, E_, T_)                                                                  \
-  if (tc == TC_ && mode == M_ && epi == E_ && trans == T_ && !akm) {                              \
-    hipLaunchKernelGGL((convg_fwd_kernel<TC_, M_, E_, T_>), grid, block, dyn, stream, *a);       \
-    return DTF_CHECK_LAUNCH();                                                                    \
-  }                                                                                               \
-  if (tc == TC_ && mode == M_ && epi == E_ && trans == T_ && akm) {                               \
-    hipLaunchKernelGGL((convg_fwd_kernel<TC_, M_, E_, T_, true>), grid, block, dyn, stream, *a); \
-    return DTF_CHECK_LAUNCH();                                                                    \
+#define CG_CASE(TC_, M_, E_, T_, AK_)                                                                      \
+  if (tc == TC_ && mode == M_ && epi == E_ && trans == T_ && akm == AK_) {                                 \
+    if (bk64)                                                                                              \
+      hipLaunchKernelGGL((convg_fwd_kernel<TC_, M_, E_, T_, AK_, 64>), grid, block, dyn, stream, *a);     \
+    else                                                                                                   \
+      hipLaunchKernelGGL((convg_fwd_kernel<TC_, M_, E_, T_, AK_, 32>), grid, block, dyn, stream, *a);     \
+    return DTF_CHECK_LAUNCH();                                                                             \
   }
-// TC = 256 (Co >= 256): a 128 x 64 tile per wave -- 1.33x the MFMA work per LDS byte of the 64 x 64 tile, whose
-// operand reads alone saturate the LDS bandwidth at the MFMA rate
-#define CG_ALL_TC(M_, E_, T_) CG_CASE(64, M_, E_, T_) CG_CASE(128, M_, E_, T_) CG_CASE(256, M_, E_, T_)
+#define CG_ALL_TC(M_, E_, T_, AK_) CG_CASE(64, M_, E_, T_, AK_) CG_CASE(128, M_, E_, T_, AK_)
   // forward: identity (stem / v1) or BN+ReLU prologue; stats epilogue; optional residual
-  CG_ALL_TC(0, 4, false)
-  CG_ALL_TC(0, 5, false)
-  CG_ALL_TC(0, 7, false)
-  CG_ALL_TC(1, 4, false)
-  CG_ALL_TC(1, 0, false)
-  CG_ALL_TC(1, 5, false)
-  CG_ALL_TC(1, 1, false)
-  CG_ALL_TC(0, 0, false)
-  // dgrad: dy plain or BN-backward prologue; [+res] mask + stats epilogue, or plain
-  CG_ALL_TC(0, 6, false)
-  CG_ALL_TC(2, 6, false)
-  CG_ALL_TC(2, 7, false)
-  CG_ALL_TC(0, 0, false)
-  CG_ALL_TC(2, 0, false)
-  CG_ALL_TC(0, 6, true)
-  CG_ALL_TC(2, 6, true)
-  CG_ALL_TC(2, 7, true)
-  CG_ALL_TC(0, 0, true)
-  CG_ALL_TC(2, 0, true)
+  CG_ALL_TC(0, 4, false, 0)
+  CG_ALL_TC(0, 5, false, 0)
+  CG_ALL_TC(0, 7, false, 0)
+  CG_ALL_TC(1, 4, false, 0)
+  CG_ALL_TC(1, 0, false, 0)
+  CG_ALL_TC(1, 5, false, 0)
+  CG_ALL_TC(1, 1, false, 0)
+  CG_ALL_TC(0, 0, false, 0)
+  // dgrad (A operand k-major from the forward layout): dy plain or BN-backward prologue; [+res] mask + stats
+  // epilogue, or plain
+  CG_ALL_TC(0, 6, false, 1)
+  CG_ALL_TC(2, 6, false, 1)
+  CG_ALL_TC(2, 7, false, 1)
+  CG_ALL_TC(0, 7, false, 1)
+  CG_ALL_TC(0, 0, false, 1)
+  CG_ALL_TC(2, 0, false, 1)
+  CG_ALL_TC(0, 6, true, 1)
+  CG_ALL_TC(2, 6, true, 1)
+  CG_ALL_TC(2, 7, true, 1)
+  CG_ALL_TC(0, 7, true, 1)
+  CG_ALL_TC(0, 0, true, 1)
+  CG_ALL_TC(2, 0, true, 1)
 #undef CG_ALL_TC
 #undef CG_CASE
   return -1;
 }
 
+// mode_dy bit 2 (value 4): 64 pixels per k-step (else 32)
 DTF_API int dtf_convg_wgrad(const CgArgs* a, int mode_x, int mode_dy, int nwork, hipStream_t stream) {
+  const int pk64 = (mode_dy >> 2) & 1;
+  mode_dy &= 3;
   if (nwork <= 0) return 0;
   if ((a->Ci & (a->Ci - 1)) != 0 || a->Ci < 8 || (a->Co & 7) != 0) return -2;
   const size_t dyn = (size_t)(2 * a->Ci + 3 * a->Co) * sizeof(float);
   dim3 grid(nwork), block(256);
 #define WG_CASE(MX, MD)                                                                     \
   if (mode_x == MX && mode_dy == MD) {                                                      \
-    hipLaunchKernelGGL((convg_wgrad_kernel<MX, MD>), grid, block, dyn, stream, *a);         \
+    if (pk64)                                                                               \
+      hipLaunchKernelGGL((convg_wgrad_kernel<MX, MD, 64>), grid, block, dyn, stream, *a);   \
+    else                                                                                    \
+      hipLaunchKernelGGL((convg_wgrad_kernel<MX, MD, 32>), grid, block, dyn, stream, *a);   \
     return DTF_CHECK_LAUNCH();                                                              \
   }
   WG_CASE(0, 0)

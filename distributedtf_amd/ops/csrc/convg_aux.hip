@@ -154,6 +154,18 @@ struct EwArgs {
   long nimg;
 };
 
+// 8 consecutive per-channel coefficients (c0 % 8 == 0: two 16-byte loads)
+__device__ __forceinline__ void coef8(const float* p, float (&v)[8]) {
+  const float4 u = *reinterpret_cast<const float4*>(p), w = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w; v[4] = w.x; v[5] = w.y; v[6] = w.z; v[7] = w.w;
+}
+
+// Channel of element 8*i of an image (32-bit: one image holds < 2^31 elements; a mask for power-of-two C).
+__device__ __forceinline__ int chan8(long i, int C) {
+  const int e = (int)i * 8;
+  return (C & (C - 1)) == 0 ? (e & (C - 1)) : e % C;
+}
+
 __global__ __launch_bounds__(256) void cg_bn_bwd_apply_kernel(EwArgs a) {
   const int img = blockIdx.x;
   const int slot = a.img_slot[img];
@@ -162,22 +174,25 @@ __global__ __launch_bounds__(256) void cg_bn_bwd_apply_kernel(EwArgs a) {
   const long n8 = a.hw * a.C / 8;
   for (long i = (long)blockIdx.y * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.y * blockDim.x) {
     const long o = base + i * 8;
-    const int c0 = (int)((i * 8) % a.C);
+    const int c0 = chan8(i, a.C);
     const uint4 dv = *reinterpret_cast<const uint4*>(a.dz + o);
     const uint4 hv = *reinterpret_cast<const uint4*>(a.h + o);
     uint4 av = make_uint4(0, 0, 0, 0);
     if (a.add) av = *reinterpret_cast<const uint4*>(a.add + o);
+    float ca[8], cbv[8], cc[8];
+    coef8(co + c0, ca);
+    coef8(co + a.cmax + c0, cbv);
+    coef8(co + 2 * a.cmax + c0, cc);
     const uint32_t d32[4] = {dv.x, dv.y, dv.z, dv.w}, h32[4] = {hv.x, hv.y, hv.z, hv.w},
                    a32[4] = {av.x, av.y, av.z, av.w};
     uint32_t r[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int c = c0 + 2 * q;
-      const float v0 = co[c] * bf2f((bf16_t)(d32[q] & 0xffff)) + co[a.cmax + c] * bf2f((bf16_t)(h32[q] & 0xffff)) +
-                       co[2 * a.cmax + c] + bf2f((bf16_t)(a32[q] & 0xffff));
-      const float v1 = co[c + 1] * bf2f((bf16_t)(d32[q] >> 16)) +
-                       co[a.cmax + c + 1] * bf2f((bf16_t)(h32[q] >> 16)) + co[2 * a.cmax + c + 1] +
-                       bf2f((bf16_t)(a32[q] >> 16));
+      const float v0 = ca[2 * q] * __uint_as_float(d32[q] << 16) + cbv[2 * q] * __uint_as_float(h32[q] << 16) +
+                       cc[2 * q] + __uint_as_float(a32[q] << 16);
+      const float v1 = ca[2 * q + 1] * __uint_as_float(d32[q] & 0xffff0000u) +
+                       cbv[2 * q + 1] * __uint_as_float(h32[q] & 0xffff0000u) + cc[2 * q + 1] +
+                       __uint_as_float(a32[q] & 0xffff0000u);
       r[q] = pack2bf(v0, v1);
     }
     *reinterpret_cast<uint4*>(a.out + o) = make_uint4(r[0], r[1], r[2], r[3]);
@@ -193,15 +208,17 @@ __global__ __launch_bounds__(256) void cg_bn_relu_apply_kernel(EwArgs a) {
   const long n8 = a.hw * a.C / 8;
   for (long i = (long)blockIdx.y * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.y * blockDim.x) {
     const long o = base + i * 8;
-    const int c0 = (int)((i * 8) % a.C);
+    const int c0 = chan8(i, a.C);
     const uint4 hv = *reinterpret_cast<const uint4*>(a.h + o);
+    float sc[8], sh[8];
+    coef8(co + c0, sc);
+    coef8(co + a.cmax + c0, sh);
     const uint32_t h32[4] = {hv.x, hv.y, hv.z, hv.w};
     uint32_t r[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int c = c0 + 2 * q;
-      const float v0 = fmaxf(bf2f((bf16_t)(h32[q] & 0xffff)) * co[c] + co[a.cmax + c], 0.f);
-      const float v1 = fmaxf(bf2f((bf16_t)(h32[q] >> 16)) * co[c + 1] + co[a.cmax + c + 1], 0.f);
+      const float v0 = fmaxf(__uint_as_float(h32[q] << 16) * sc[2 * q] + sh[2 * q], 0.f);
+      const float v1 = fmaxf(__uint_as_float(h32[q] & 0xffff0000u) * sc[2 * q + 1] + sh[2 * q + 1], 0.f);
       r[q] = pack2bf(v0, v1);
     }
     *reinterpret_cast<uint4*>(a.out + o) = make_uint4(r[0], r[1], r[2], r[3]);

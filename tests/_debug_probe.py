@@ -36,7 +36,8 @@ y = torch.zeros_like(x)
 w = torch.zeros(16 * 9 * 16, dtype=torch.bfloat16, device=dev)
 img_slot = torch.zeros(1, dtype=torch.int32, device=dev)
 cnt = torch.ones(1, dtype=torch.float32, device=dev)
-work = torch.tensor([[0, 0, 0, 0]], dtype=torch.int32, device=dev)  # nit = 0: invalid item
+# slot -1: an invalid item (an empty item, nit = 0, is legal since elastic plans generate them)
+work = torch.tensor([[0, 1, 0, -1]], dtype=torch.int32, device=dev)
 
 a = hr.ConvArgs()
 a.x, a.y, a.w = x.data_ptr(), y.data_ptr(), w.data_ptr()

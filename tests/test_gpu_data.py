@@ -62,8 +62,13 @@ def test_augment_kernel_matches_reference(augment):
         torch.testing.assert_close(o32, datasets.eval_cifar(x[idx]), rtol=1e-4, atol=1e-4)
 
 
-def test_hip_step_consumes_index_batches():
-    """Index batches through the in-graph augmentation == explicit float batches with the same draws."""
+def test_hip_step_consumes_index_batches(monkeypatch):
+    """Index batches through the in-graph augmentation == explicit float batches with the same draws.
+
+    Exact (packed) plans: the augmentation's per-image random draws are keyed on the image's position in the
+    plan's input buffer, and an elastic plan (mixed batch sizes, DTF_ELASTIC=auto) places member 1 at the
+    capacity offset instead of right after member 0 -- valid, but different, draws than the packed reference."""
+    monkeypatch.setenv("DTF_ELASTIC", "0")
     x, y = _data(400, seed=3)
     ds = datasets.DeviceDataset(x, y, x[:16], y[:16], "cuda", augment=datasets.augment_cifar, seed=99)
     assert ds.hip_augment

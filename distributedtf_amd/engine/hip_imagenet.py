@@ -33,9 +33,12 @@ c_void_p, c_int, c_long, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_long,
 CMAX = 2048
 NPAD_CLS = 1024
 # k depth per LDS stage of the convg forward / data-gradient kernel (32 or 64)
-_CG_BK = int(os.environ.get("DTF_CG_BK", "64"))
+_CG_BK = int(os.environ.get("DTF_CG_BK", "32"))
 # weight gradient: pixels per k-step (32 or 64), target items per launch, minimum pixels per split-K chunk
 _CG_WPK = int(os.environ.get("DTF_CG_WPK", "32"))
+_CG_WO64 = os.environ.get("DTF_CG_WO64", "1") == "1"
+_CG_TP256 = os.environ.get("DTF_CG_TP256", "1") == "1"  # 256-pixel forward / dgrad tiles for 64-channel outputs
+_CG_WPK_WO64 = int(os.environ.get("DTF_CG_WPK_WO64", "32"))  # pixels per k-step of the 64-row tiles
 _CG_WG_TARGET = int(os.environ.get("DTF_CG_WG_TARGET", "1024"))
 _CG_WG_MINCHUNK = int(os.environ.get("DTF_CG_WG_MINCHUNK", "2048"))
 
@@ -340,7 +343,7 @@ class _ImageNetPlan:
         self._keep.append(obj)
         return obj
 
-    def _pix_work(self, hw_grid, co, tc, classes=(0,)):
+    def _pix_work(self, hw_grid, co, tc, classes=(0,), tp=128):
         """(slot, p0, p1, o0 | class << 16) tiles of 128 grid pixels x tc output channels per member; a
         transposed (stride-2) dgrad runs every parity class (py*2 + px) over the dy-resolution grid."""
         items = []
@@ -348,18 +351,18 @@ class _ImageNetPlan:
             f = self.first[s]
             p_end = (f + n) * hw_grid * hw_grid
             for cls in classes:
-                for p0 in range(f * hw_grid * hw_grid, p_end, 128):
+                for p0 in range(f * hw_grid * hw_grid, p_end, tp):
                     for o0 in range(0, co, tc):
-                        items.append([s, p0, min(p0 + 128, p_end), o0 | (cls << 16)])
+                        items.append([s, p0, min(p0 + tp, p_end), o0 | (cls << 16)])
         return self._hold(torch.tensor(items, dtype=torch.int32, device=self.be.dev))
 
-    def _wgrad_work(self, hw_out, co, K):
+    def _wgrad_work(self, hw_out, co, K, wo=128):
         """(slot, p0, p1, o0 | n0/8 << 16) split-K items of the weight gradient: 128 x 128 dW tiles per member, the
         member's pixels split into chunks so that the launch has about ``_CG_WG_TARGET`` items.  Every item
         atomically adds its full fp32 tile into the member's gradient row, so the split count is a trade: more
         items fill the chip, but each split adds 64 KB of atomic traffic per tile (the chip absorbs about 1.3 TB/s
         of atomic adds).  The former 4096-item target moved ~14 GB of atomics per pop-8 ResNet-50 step."""
-        tiles = -(-co // 128) * -(-K // 128)
+        tiles = -(-co // wo) * -(-K // 128)
         per_member = max(1, -(-_CG_WG_TARGET // max(1, len(self.slots) * tiles)))
         items = []
         for s, n in zip(self.slots, self.sizes):
@@ -368,7 +371,7 @@ class _ImageNetPlan:
             chunk = max(_CG_WG_MINCHUNK, -(-(p_end - p_beg) // per_member))
             chunk = (chunk + 63) // 64 * 64
             for p0 in range(p_beg, p_end, chunk):
-                for o0 in range(0, co, 128):
+                for o0 in range(0, co, wo):
                     for n0 in range(0, K, 128):
                         items.append([s, p0, min(p0 + chunk, p_end), o0 | ((n0 // 8) << 16)])
         return self._hold(torch.tensor(items, dtype=torch.int32, device=self.be.dev))
@@ -427,10 +430,14 @@ class _ImageNetPlan:
         tc = 128 if a.Co >= 128 else 64
         # (a 256-row tile, 128 x 64 per wave, measured slower: 111.7 -> 123.4 ms/step at pop 8 x 128,
         # profiles/r2_imagenet_tc256_ab.log -- removed)
-        if _CG_BK == 64 and (not trans or a.Ci >= 64):
+        tp = 128
+        if tc == 64 and _CG_TP256:
+            trans |= 8  # 256-pixel tiles: 1 x 4 waves of 64 x 64 (BK = 32)
+            tp = 256
+        elif _CG_BK == 64 and (not trans or a.Ci >= 64):
             trans |= 4  # k depth 64 per LDS stage
-        work = (self._pix_work(hw_in, a.Co, tc, classes=(0, 1, 2, 3)) if trans & 1
-                else self._pix_work(hw_out, a.Co, tc))
+        work = (self._pix_work(hw_in, a.Co, tc, classes=(0, 1, 2, 3), tp=tp) if trans & 1
+                else self._pix_work(hw_out, a.Co, tc, tp=tp))
         a.work = _p(work)
         self._hold(a)
         self._add(ops.lib().dtf_convg_fwd, ctypes.byref(a), tc, mode, epi, trans, work.shape[0])
@@ -451,11 +458,12 @@ class _ImageNetPlan:
         a.stride, a.pad = c.stride, (c.k - 1) // 2
         a.log2ci = _log2(cin)
         a.cin_real = c.cin
-        work = self._wgrad_work(hw_out, c.cout, c.k * c.k * cin)
+        wo = 64 if (c.cout % 128 != 0 and _CG_WO64) else 128  # 64-row tiles: no padded half for Co = 64
+        work = self._wgrad_work(hw_out, c.cout, c.k * c.k * cin, wo)
         a.work = _p(work)
         self._hold(a)
-        self._add(ops.lib().dtf_convg_wgrad, ctypes.byref(a), mode_x, mode_dy | (4 if _CG_WPK == 64 else 0),
-                  work.shape[0])
+        flags = (4 if (_CG_WPK_WO64 if wo == 64 else _CG_WPK) == 64 else 0) | (8 if wo == 64 else 0)
+        self._add(ops.lib().dtf_convg_wgrad, ctypes.byref(a), mode_x, mode_dy | flags, work.shape[0])
 
     def bn_final(self, bn, hw, backward):
         be, e = self.be, self.e

@@ -57,7 +57,6 @@ struct CgArgs {
   int cin_real;       // wgrad: real input channels of a channel-padded operand (stem: 3 of 8); 0 = Ci
 };
 
-constexpr int TP = 128;   // pixels per workgroup tile
 
 // ---------------------------------------------------------------------------------------------- fwd / dgrad
 // MODE: 0 identity, 1 relu(x*s + t), 2 A*x + B*x2 + C.   EPI: bit0 residual, bit1 mask, bit2 stats (fwd: y, y^2;
@@ -67,17 +66,25 @@ constexpr int TP = 128;   // pixels per workgroup tile
 // ds_read_b64_tr_b16), so no transposed weight copy exists.
 // BK: k depth per LDS stage (32 or 64).  BK = 64 halves the barriers and fragment-read restarts per MFMA and doubles
 // the bytes in flight per load batch; it needs Ci >= 64 on the incremental (one tap per k-step) gather path.
-template <int TC, int MODE, int EPI, bool TRANS, bool AKM = false, int BK = 32>
+// TP: pixels per workgroup tile.  128: 2 x 2 waves of (TC/2 rows x 64 pixels); 256 (TC = 64 only): 1 x 4 waves of
+// 64 rows x 64 pixels -- twice the MFMA work per k-step and wave of the 32 x 64 wave tile a 64-row conv gets
+// otherwise.
+template <int TC, int MODE, int EPI, bool TRANS, bool AKM = false, int BK = 32, int TP = 128>
 __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
+  static_assert(TP == 128 || (TP == 256 && TC == 64), "pixel tile");
+  constexpr int WRN = TP == 256 ? 1 : 2;  // wave rows (the rest of the 4 waves split the pixels, 64 each)
   constexpr int RP = BK + 8;        // [rows][BK] tile pitch (+16 B)
   constexpr int CPR = BK / 8;       // 16-byte chunks per tile row
   constexpr int RPT = 256 / CPR;    // tile rows covered per pass of the workgroup
   constexpr int NJ = TP / RPT;      // B (pixel) rows per thread
   constexpr int KPA = TC + 8;       // [BK][TC] k-major A tile pitch
-  constexpr int MT = TC / 32;       // MFMA row tiles per wave (wave covers TC/2 rows)
+  constexpr int MT = TC / WRN / 16;  // MFMA row tiles per wave (wave covers TC/WRN rows)
   constexpr int SA = (TC * RP > BK * KPA) ? TC * RP : BK * KPA;
   constexpr int CPF = TC + 4;  // epilogue staging row pitch (floats; 16-byte rows, conflict-free float4 stores)
-  constexpr int SOPS = 2 * SA + 2 * TP * RP, SEPI = 2 * TP * CPF;  // bf16 elements: operand buffers | staging
+  // bf16 elements: operand buffers | fp32 epilogue staging of the whole tile; when the staging would exceed the
+  // operand buffers (BK = 32) the tile is staged in two 64-pixel halves so LDS (and occupancy) stays the same
+  constexpr int SOPS = 2 * SA + 2 * TP * RP, SEPI_FULL = 2 * TP * CPF;
+  constexpr int NHALF = SOPS >= SEPI_FULL ? 1 : 2, SEPI = SEPI_FULL / NHALF;
   __shared__ __attribute__((aligned(16))) bf16_t smem_[SOPS > SEPI ? SOPS : SEPI];
   bf16_t (*sa)[SA] = reinterpret_cast<bf16_t (*)[SA]>(smem_);
   bf16_t (*sb)[TP * RP] = reinterpret_cast<bf16_t (*)[TP * RP]>(smem_ + 2 * SA);
@@ -87,7 +94,7 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z >= wk.y);
   const int slot = wk.x, p0 = wk.y, p1 = wk.z;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int wr = wave & 1, wc = wave >> 1;
+  const int wr = wave % WRN, wc = wave / WRN;
   const int Ci = a.Ci, Kfull = a.kh * a.kw * Ci;
   // TRANS (stride-2 data gradient): the workgroup covers one output parity class (py, px); pixels are indexed on
   // the class grid (= the gathered dy grid) and only the taps with (parity + tap - pad) even contribute:
@@ -302,12 +309,12 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
       for (int m = 0; m < MT; ++m) {
         if constexpr (AKM) {
           const int g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
-          const int rb_ = wr * (TC / 2) + 16 * m + 4 * p4;
+          const int rb_ = wr * (TC / WRN) + 16 * m + 4 * p4;
           const s16x4_t lo = ds_read_tr(sa[cur] + (32 * kk + 8 * g + q) * KPA + rb_);
           const s16x4_t hi = ds_read_tr(sa[cur] + (32 * kk + 8 * g + 4 + q) * KPA + rb_);
           fa[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         } else {
-          fa[m] = *reinterpret_cast<const bf16x8_t*>(sa[cur] + (wr * (TC / 2) + 16 * m + (lane & 15)) * RP +
+          fa[m] = *reinterpret_cast<const bf16x8_t*>(sa[cur] + (wr * (TC / WRN) + 16 * m + (lane & 15)) * RP +
                                                      32 * kk + 8 * (lane >> 4));
         }
       }
@@ -331,13 +338,6 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   // residual / mask loads and the bf16 store are whole contiguous row segments (TC * 2 bytes per pixel) instead
   // of 8-byte pieces of 16 pixel rows per wave instruction
   float* cst = reinterpret_cast<float*>(smem_);
-#pragma unroll
-  for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-      *reinterpret_cast<f32x4_t*>(cst + (wc * 64 + 16 * n + (lane & 15)) * CPF + wr * (TC / 2) + 16 * m +
-                                  4 * (lane >> 4)) = acc[m][n];
-  __syncthreads();
   constexpr int CH = TC / 8;     // 16-byte channel chunks per pixel row
   constexpr int PPP = 256 / CH;  // pixel rows per pass of the workgroup
   const int ch = tid % CH, pr = tid / CH;
@@ -361,23 +361,46 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   float ss[8], sq[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) ss[i] = sq[i] = 0.f;
-#pragma unroll 2
-  for (int it = 0; it < TP / PPP; ++it) {
-    const int pl = pr + PPP * it;
-    const int p = p0 + pl;
-    if (p >= p1 || !cok) continue;
-    long pf = p;  // output pixel (full resolution)
-    if constexpr (TRANS) {
-      const int img = p / HWo, rem = p - img * HWo, qy = rem / GW, qx = rem - qy * GW;
-      pf = ((long)img * a.Ho + 2 * qy + py) * a.Wo + 2 * qx + px;
+  for (int h = 0; h < NHALF; ++h) {
+    if (h > 0) __syncthreads();  // the previous half's rows have been read
+    if (NHALF == 1 || (wc * 64) / (TP / NHALF) == h) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          *reinterpret_cast<f32x4_t*>(cst + (wc * 64 - h * (TP / NHALF) + 16 * n + (lane & 15)) * CPF +
+                                      wr * (TC / WRN) + 16 * m + 4 * (lane >> 4)) = acc[m][n];
     }
-    const long o = pf * a.Co + oc;
+    __syncthreads();
+    // all residual / mask rows of this half are loaded before the first store (the stores may alias them for the
+    // compiler), so a thread keeps NPASS 16-byte loads in flight instead of one per pass
+    constexpr int NPASS = TP / NHALF / PPP;
+    long orow[NPASS];
+    uint4 rrv[NPASS], xrv[NPASS];
+#pragma unroll
+    for (int it = 0; it < NPASS; ++it) {
+      const int p = p0 + h * (TP / NHALF) + pr + PPP * it;
+      long pf = p;  // output pixel (full resolution)
+      if constexpr (TRANS) {
+        const int img = p / HWo, rem = p - img * HWo, qy = rem / GW, qx = rem - qy * GW;
+        pf = ((long)img * a.Ho + 2 * qy + py) * a.Wo + 2 * qx + px;
+      }
+      orow[it] = (p < p1 && cok) ? pf * a.Co + oc : -1;
+      rrv[it] = xrv[it] = make_uint4(0, 0, 0, 0);
+      if (orow[it] >= 0) {
+        if constexpr (EPI & 1) rrv[it] = *reinterpret_cast<const uint4*>(a.res + orow[it]);
+        if constexpr (EPI & 2) xrv[it] = *reinterpret_cast<const uint4*>(a.xm + orow[it]);
+      }
+    }
+#pragma unroll
+  for (int it = 0; it < NPASS; ++it) {
+    const int pl = pr + PPP * it;  // staged row
+    if (orow[it] < 0) continue;
+    const long o = orow[it];
     const float4 c0 = *reinterpret_cast<const float4*>(cst + pl * CPF + 8 * ch);
     const float4 c1 = *reinterpret_cast<const float4*>(cst + pl * CPF + 8 * ch + 4);
     float v[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-    uint4 rr = make_uint4(0, 0, 0, 0), xr = make_uint4(0, 0, 0, 0);
-    if constexpr (EPI & 1) rr = *reinterpret_cast<const uint4*>(a.res + o);
-    if constexpr (EPI & 2) xr = *reinterpret_cast<const uint4*>(a.xm + o);
+    const uint4 rr = rrv[it], xr = xrv[it];
     const uint32_t r32[4] = {rr.x, rr.y, rr.z, rr.w}, x32[4] = {xr.x, xr.y, xr.z, xr.w};
     float xv[8];
 #pragma unroll
@@ -413,6 +436,7 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
       }
     }
   }
+  }
   if constexpr (EPI & 4) {
     // lanes l, l + CH, l + 2 CH, .. of a wave hold the same channel chunk: butterfly over them, then one LDS
     // atomic per wave and channel, one global atomic per workgroup and channel
@@ -443,9 +467,15 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
 constexpr int WT = 128;
 constexpr int KP = WT + 8;
 
-template <int MODE_X, int MODE_DY, int PK = 32>
-__global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
+// WO: output-channel rows per tile (128: 2 x 2 waves of 64 x 64; 64: 1 x 4 waves of 64 x 32, for Co = 64 layers
+// whose 128-row tile would be half padding)
+// occupancy matters more than anything else here (the k-step loads are latency-bound): ask for 4 workgroups per
+// CU (<= 128 registers); measured: the 140-register build at 3 per CU, and a prefetch-2 build at 2 per CU, slower
+template <int MODE_X, int MODE_DY, int PK = 32, int WO = 128>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void convg_wgrad_kernel(CgArgs a) {
   constexpr int NJ = PK / 16;  // pixel rows per thread per k-step
+  constexpr int WRN = WO / 64, WCN = 4 / WRN;  // wave grid (rows x columns)
+  constexpr int CWW = WT / WCN, NTN = CWW / 16;  // columns per wave, MFMA column tiles per wave
   __shared__ __attribute__((aligned(16))) bf16_t sd[2][PK * KP];
   __shared__ __attribute__((aligned(16))) bf16_t sx[2][PK * KP];
   extern __shared__ float dyn[];  // x coefficients (2*Ci) then dy coefficients (3*Co)
@@ -453,7 +483,7 @@ __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
   DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z >= wk.y);
   const int slot = wk.x, p0 = wk.y, p1 = wk.z, o0 = wk.w & 0xffff, n0 = (wk.w >> 16) * 8;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int wr = wave & 1, wc = wave >> 1;
+  const int wr = wave % WRN, wc = wave / WRN;
   const int Ci = a.Ci, Co = a.Co, K = a.kh * a.kw * Ci;
   float* cx = dyn;
   float* cd = dyn + 2 * Ci;
@@ -482,7 +512,7 @@ __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
   const int xky = xtap / a.kw, xkx = xtap - xky * a.kw;
   const bool xcol_ok = xcol < K;
   const int dcol = o0 + 8 * cc;
-  const bool dcol_ok = dcol < Co;
+  const bool dcol_ok = dcol < Co && 8 * cc < WO;
   const float r_hw = 1.0f / (float)HWo, r_w = 1.0f / (float)a.Wo;
   auto divmod = [](int n, int d, float rd, int& q, int& r) {  // exact for n < 2^24
     q = (int)((float)n * rd);
@@ -573,11 +603,13 @@ __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
       *reinterpret_cast<uint4*>(xx + (kr + 16 * j) * KP + 8 * cc) = u;
     }
   };
-  f32x4_t acc[4][4];
+  f32x4_t acc[4][NTN];
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < NTN; ++n) acc[m][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  // (A two-register-stage variant -- loads of k-step ks + 2 in flight while ks computes -- measured slower:
+  // 22.5 -> 27.3 ms of wgrad per pop-8 ResNet-50 step, occupancy 3 -> 2; profiles/r2_s3_imagenet_wgrad_pf2.log)
   const int nk = (p1 - p0 + PK - 1) / PK;
   make_pinfo(p0);
   if (nk > 1) make_pinfo(p0 + PK);
@@ -596,7 +628,7 @@ __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
     if (ks + 2 < nk) make_pinfo(p0 + PK * (ks + 2));
 #pragma unroll
     for (int kk = 0; kk < PK / 32; ++kk) {
-      bf16x8_t fa[4], fb[4];
+      bf16x8_t fa[4], fb[NTN];
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const int cb = wr * 64 + 16 * m + 4 * p4;
@@ -605,8 +637,8 @@ __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
         fa[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int cb = wc * 64 + 16 * n + 4 * p4;
+      for (int n = 0; n < NTN; ++n) {
+        const int cb = wc * CWW + 16 * n + 4 * p4;
         const s16x4_t lo = ds_read_tr(sx[cur] + (32 * kk + 8 * g + q) * KP + cb);
         const s16x4_t hi = ds_read_tr(sx[cur] + (32 * kk + 8 * g + 4 + q) * KP + cb);
         fb[n] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -614,7 +646,7 @@ __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(fa[m], fb[n], acc[m][n]);
+        for (int n = 0; n < NTN; ++n) acc[m][n] = mfma16(fa[m], fb[n], acc[m][n]);
     }
     if (more) store(sd[cur ^ 1], sx[cur ^ 1], dv, dv2, xv, okm);
     __syncthreads();
@@ -624,8 +656,8 @@ __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
   const int cr = a.cin_real > 0 ? a.cin_real : Ci;
   const int Kr = a.kh * a.kw * cr;
 #pragma unroll
-  for (int n = 0; n < 4; ++n) {
-    const int col = n0 + wc * 64 + 16 * n + (lane & 15);
+  for (int n = 0; n < NTN; ++n) {
+    const int col = n0 + wc * CWW + 16 * n + (lane & 15);
     const int tap = col >> a.log2ci, ci = col & (Ci - 1);
     if (col >= K || ci >= cr) continue;
     const int colr = tap * cr + ci;
@@ -645,10 +677,12 @@ __global__ __launch_bounds__(256) void convg_wgrad_kernel(CgArgs a) {
 DTF_API int dtf_cg_args_size() { return (int)sizeof(CgArgs); }
 
 // flags: tc (64 | 128), mode (0..2), epi (0..7), trans: bit0 transposed gather, bit1 A operand k-major from the
-// forward weight layout (data gradient), bit2 BK = 64 (k depth per LDS stage; else 32)
+// forward weight layout (data gradient), bit2 BK = 64 (k depth per LDS stage; else 32), bit3 256-pixel tiles (tc 64)
 DTF_API int dtf_convg_fwd(const CgArgs* a, int tc, int mode, int epi, int trans, int nwork, hipStream_t stream) {
   const int akm = (trans >> 1) & 1;
   const int bk64 = (trans >> 2) & 1;
+  const int tp256 = (trans >> 3) & 1;  // 256-pixel tiles (tc = 64, BK = 32)
+  if (tp256 && (tc != 64 || bk64)) return -2;
   trans &= 1;
   if (nwork <= 0) return 0;
   if ((a->Ci & (a->Ci - 1)) != 0 || a->Ci < 8 || (a->Co & 7) != 0) return -2;
@@ -658,7 +692,9 @@ DTF_API int dtf_convg_fwd(const CgArgs* a, int tc, int mode, int epi, int trans,
   dim3 grid(nwork), block(256);
 #define CG_CASE(TC_, M_, E_, T_, AK_)                                                                      \
   if (tc == TC_ && mode == M_ && epi == E_ && trans == T_ && akm == AK_) {                                 \
-    if (bk64)                                                                                              \
+    if (tp256 && TC_ == 64)                                                                                \
+      hipLaunchKernelGGL((convg_fwd_kernel<64, M_, E_, T_, AK_, 32, 256>), grid, block, dyn, stream, *a); \
+    else if (bk64)                                                                                         \
       hipLaunchKernelGGL((convg_fwd_kernel<TC_, M_, E_, T_, AK_, 64>), grid, block, dyn, stream, *a);     \
     else                                                                                                   \
       hipLaunchKernelGGL((convg_fwd_kernel<TC_, M_, E_, T_, AK_, 32>), grid, block, dyn, stream, *a);     \
@@ -693,9 +729,9 @@ DTF_API int dtf_convg_fwd(const CgArgs* a, int tc, int mode, int epi, int trans,
   return -1;
 }
 
-// mode_dy bit 2 (value 4): 64 pixels per k-step (else 32)
+// mode_dy bit 2 (value 4): 64 pixels per k-step (else 32); bit 3 (value 8): 64-row tiles (Co = 64 layers)
 DTF_API int dtf_convg_wgrad(const CgArgs* a, int mode_x, int mode_dy, int nwork, hipStream_t stream) {
-  const int pk64 = (mode_dy >> 2) & 1;
+  const int pk64 = (mode_dy >> 2) & 1, wo64 = (mode_dy >> 3) & 1;
   mode_dy &= 3;
   if (nwork <= 0) return 0;
   if ((a->Ci & (a->Ci - 1)) != 0 || a->Ci < 8 || (a->Co & 7) != 0) return -2;
@@ -703,8 +739,12 @@ DTF_API int dtf_convg_wgrad(const CgArgs* a, int mode_x, int mode_dy, int nwork,
   dim3 grid(nwork), block(256);
 #define WG_CASE(MX, MD)                                                                     \
   if (mode_x == MX && mode_dy == MD) {                                                      \
-    if (pk64)                                                                               \
+    if (pk64 && wo64)                                                                       \
+      hipLaunchKernelGGL((convg_wgrad_kernel<MX, MD, 64, 64>), grid, block, dyn, stream, *a); \
+    else if (pk64)                                                                          \
       hipLaunchKernelGGL((convg_wgrad_kernel<MX, MD, 64>), grid, block, dyn, stream, *a);   \
+    else if (wo64)                                                                          \
+      hipLaunchKernelGGL((convg_wgrad_kernel<MX, MD, 32, 64>), grid, block, dyn, stream, *a); \
     else                                                                                    \
       hipLaunchKernelGGL((convg_wgrad_kernel<MX, MD, 32>), grid, block, dyn, stream, *a);   \
     return DTF_CHECK_LAUNCH();                                                              \

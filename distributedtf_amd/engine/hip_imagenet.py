@@ -37,6 +37,10 @@ _CG_BK = int(os.environ.get("DTF_CG_BK", "32"))
 # weight gradient: pixels per k-step (32 or 64), target items per launch, minimum pixels per split-K chunk
 _CG_WPK = int(os.environ.get("DTF_CG_WPK", "32"))
 _CG_WO64 = os.environ.get("DTF_CG_WO64", "1") == "1"
+_CG_WIDE = os.environ.get("DTF_CG_WIDE", "1") == "1"  # wide-column 3x3 weight-gradient tiles
+_CG_WIDE128 = os.environ.get("DTF_CG_WIDE128", "1") == "1"
+_CG_WIDE7 = os.environ.get("DTF_CG_WIDE7", "1") == "1"  # one 64 x 416 tile for the 7x7 stem
+_CG_WIDE1 = os.environ.get("DTF_CG_WIDE1", "1") == "1"  # the wide tiles for 1x1 convs with Ci % 256 == 0
 _CG_TP256 = os.environ.get("DTF_CG_TP256", "1") == "1"  # 256-pixel forward / dgrad tiles for 64-channel outputs
 _CG_WPK_WO64 = int(os.environ.get("DTF_CG_WPK_WO64", "32"))  # pixels per k-step of the 64-row tiles
 _CG_WG_TARGET = int(os.environ.get("DTF_CG_WG_TARGET", "1024"))
@@ -87,6 +91,7 @@ def _register():
     reg = ops.register
     reg("dtf_convg_fwd", [P(CgArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
     reg("dtf_convg_wgrad", [P(CgArgs), c_int, c_int, c_int, c_void_p])
+    reg("dtf_convg_wgrad_wide", [P(CgArgs), c_int, c_int, c_int, c_void_p])
     reg("dtf_cg_weight_prep", [c_void_p, c_long, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_long,
                                c_void_p])
     reg("dtf_cg_dense_prep", [c_void_p, c_long, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_long,
@@ -356,13 +361,13 @@ class _ImageNetPlan:
                         items.append([s, p0, min(p0 + tp, p_end), o0 | (cls << 16)])
         return self._hold(torch.tensor(items, dtype=torch.int32, device=self.be.dev))
 
-    def _wgrad_work(self, hw_out, co, K, wo=128):
+    def _wgrad_work(self, hw_out, co, K, wo=128, wt=128):
         """(slot, p0, p1, o0 | n0/8 << 16) split-K items of the weight gradient: 128 x 128 dW tiles per member, the
         member's pixels split into chunks so that the launch has about ``_CG_WG_TARGET`` items.  Every item
         atomically adds its full fp32 tile into the member's gradient row, so the split count is a trade: more
         items fill the chip, but each split adds 64 KB of atomic traffic per tile (the chip absorbs about 1.3 TB/s
         of atomic adds).  The former 4096-item target moved ~14 GB of atomics per pop-8 ResNet-50 step."""
-        tiles = -(-co // wo) * -(-K // 128)
+        tiles = -(-co // wo) * -(-K // wt)
         per_member = max(1, -(-_CG_WG_TARGET // max(1, len(self.slots) * tiles)))
         items = []
         for s, n in zip(self.slots, self.sizes):
@@ -372,7 +377,7 @@ class _ImageNetPlan:
             chunk = (chunk + 63) // 64 * 64
             for p0 in range(p_beg, p_end, chunk):
                 for o0 in range(0, co, wo):
-                    for n0 in range(0, K, 128):
+                    for n0 in range(0, K, wt):
                         items.append([s, p0, min(p0 + chunk, p_end), o0 | ((n0 // 8) << 16)])
         return self._hold(torch.tensor(items, dtype=torch.int32, device=self.be.dev))
 
@@ -458,6 +463,20 @@ class _ImageNetPlan:
         a.stride, a.pad = c.stride, (c.k - 1) // 2
         a.log2ci = _log2(cin)
         a.cin_real = c.cin
+        K = c.k * c.k * cin
+        wide3 = c.k == 3 and cin % 64 == 0
+        wide1 = c.k == 1 and cin % 256 == 0 and _CG_WIDE1
+        wide7 = ci == be.prog.stem and c.k == 7 and cin == 8 and c.cout == 64 and _CG_WIDE7
+        if _CG_WIDE and (wide3 or wide1 or wide7) and mode_x == 0 and mode_dy == 0:
+            # 64 / 128 x 288 (3x3), x 256 (1x1) or 64 x 416 (stem) tiles: 18 / 36, 16 / 32, 26 MFMAs per wave and
+            # 32-pixel k-step (convg_wgrad_wide_kernel)
+            wo = 128 if c.cout % 128 == 0 and _CG_WIDE128 else 64
+            wt = 288 if wide3 else (256 if wide1 else 416)
+            work = self._wgrad_work(hw_out, c.cout, K, wo, wt)
+            a.work = _p(work)
+            self._hold(a)
+            self._add(ops.lib().dtf_convg_wgrad_wide, ctypes.byref(a), wo, wt, work.shape[0])
+            return
         wo = 64 if (c.cout % 128 != 0 and _CG_WO64) else 128  # 64-row tiles: no padded half for Co = 64
         work = self._wgrad_work(hw_out, c.cout, c.k * c.k * cin, wo)
         a.work = _p(work)

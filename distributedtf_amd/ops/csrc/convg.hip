@@ -472,7 +472,7 @@ constexpr int KP = WT + 8;
 // occupancy matters more than anything else here (the k-step loads are latency-bound): ask for 4 workgroups per
 // CU (<= 128 registers); measured: the 140-register build at 3 per CU, and a prefetch-2 build at 2 per CU, slower
 template <int MODE_X, int MODE_DY, int PK = 32, int WO = 128>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void convg_wgrad_kernel(CgArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PK == 32 ? 4 : 2))) void convg_wgrad_kernel(CgArgs a) {
   constexpr int NJ = PK / 16;  // pixel rows per thread per k-step
   constexpr int WRN = WO / 64, WCN = 4 / WRN;  // wave grid (rows x columns)
   constexpr int CWW = WT / WCN, NTN = CWW / 16;  // columns per wave, MFMA column tiles per wave
@@ -672,6 +672,170 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   }
 }
 
+// ---------------------------------------------------------------------------------------------- wide wgrad
+// Weight gradient of a 3x3 conv (plain operands, the default non-folded path) with WIDE column tiles: 64 output
+// channels x 288 (tap, ci) columns per workgroup (K = 9 * Ci is a multiple of 576 for Ci % 64 == 0), 2 x 2 waves of
+// 32 x 144 (18 MFMAs per wave and 32-pixel k-step instead of the 8 of a 64 x 128 tile): the per-k-step cost --
+// pixel table, dy / x gathers, LDS writes, the barrier -- is paid for 2.25x the MFMA work, and the dy tile is staged
+// once per 288 instead of 128 columns.
+
+// WWO = 64 (Co = 64) or 128 output-channel rows per tile: 2 x 2 waves of (WWO/2) x 144 -- the 128-row form reads
+// each B fragment for 4 instead of 2 MFMAs (the 64-row one is LDS-read-bound: 22 tr-reads per 18 MFMAs)
+// WWT: columns per tile, 288 (3x3 convs: K = 9 Ci), 256 (1x1 convs with Ci % 256 == 0) or 416 (the 7x7 stem:
+// 49 taps x 8 channels, one tile).
+template <int WWO, int WWT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ? 3 : 2))) void convg_wgrad_wide_kernel(CgArgs a) {
+  constexpr int WWOP = WWO + 8, MTW = WWO / 32, DJ = WWO / 64, WWP = WWT + 8;
+  constexpr int WXC = 32 * (WWT / 8);  // x chunks (8 columns) per k-step
+  constexpr int WXJ = (WXC + 255) / 256;
+  __shared__ __attribute__((aligned(16))) bf16_t sd[2][32 * WWOP];
+  __shared__ __attribute__((aligned(16))) bf16_t sx[2][32 * WWP];
+  __shared__ int4 pinfo[2][32];
+  const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z >= wk.y);
+  const int slot = wk.x, p0 = wk.y, p1 = wk.z, o0 = wk.w & 0xffff, n0 = (wk.w >> 16) * 8;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave & 1, wc = wave >> 1;
+  const int Ci = a.Ci, Co = a.Co, K = a.kh * a.kw * Ci;
+  const int HWo = a.Ho * a.Wo;
+  const long img_x = (long)a.Hi * a.Wi * Ci;
+  // dy: DJ 16-byte chunks per thread and k-step (row (tid + 256 j) / (WWO / 8), 8 channels)
+  int drow[DJ], dch[DJ];
+  bool dok[DJ];
+#pragma unroll
+  for (int j = 0; j < DJ; ++j) {
+    const int c = tid + 256 * j;
+    drow[j] = c / (WWO / 8);
+    dch[j] = 8 * (c % (WWO / 8));
+    dok[j] = o0 + dch[j] < Co;
+  }
+  // x: chunks c = tid + 256 j of the [32 rows][36 chunks] k-step tile; (row, tap, ci) fixed for the workgroup
+  int xrow[WXJ], xky[WXJ], xkx[WXJ], xoff[WXJ];
+  bool xok[WXJ];
+#pragma unroll
+  for (int j = 0; j < WXJ; ++j) {
+    const int c = tid + 256 * j;
+    const int r = c / (WWT / 8), ch = c - r * (WWT / 8);
+    const int col = n0 + 8 * ch;
+    const int tap = col >> a.log2ci, ci = col & (Ci - 1);
+    xrow[j] = r;
+    xky[j] = tap / a.kw;
+    xkx[j] = tap - xky[j] * a.kw;
+    xoff[j] = r * WWP + 8 * ch;  // LDS element offset in the k-step tile
+    xok[j] = c < WXC && col < K;
+    xoff[j] += ci << 16;         // ci in the high half (unpacked at use)
+  }
+  const float r_hw = 1.0f / (float)HWo, r_w = 1.0f / (float)a.Wo;
+  auto divmod = [](int n, int d, float rd, int& q, int& r) {  // exact for n < 2^24
+    q = (int)((float)n * rd);
+    r = n - q * d;
+    if (r < 0) {
+      --q;
+      r += d;
+    } else if (r >= d) {
+      ++q;
+      r -= d;
+    }
+  };
+  auto make_pinfo = [&](int pk0) {
+    if (tid < 32) {
+      const int p = pk0 + tid;
+      int4 inf = make_int4(0, 0, -(1 << 30), 0);
+      if (p < p1) {
+        int img, rem, oy, ox;
+        divmod(p, HWo, r_hw, img, rem);
+        divmod(rem, a.Wo, r_w, oy, ox);
+        inf = make_int4((int)((unsigned)p * (unsigned)Co), (int)((unsigned)img * (unsigned)img_x),
+                        oy * a.stride - a.pad, ox * a.stride - a.pad);
+      }
+      pinfo[(pk0 - p0) / 32 & 1][tid] = inf;
+    }
+  };
+  auto load = [&](int pk0, uint4 (&dv)[DJ], uint4 (&xv)[WXJ]) {
+    const int par = (pk0 - p0) / 32 & 1;
+#pragma unroll
+    for (int j = 0; j < DJ; ++j) {
+      const int4 di = pinfo[par][drow[j]];
+      dv[j] = (di.z > -(1 << 29) && dok[j]) ? *reinterpret_cast<const uint4*>(a.dy + (unsigned)di.x + o0 + dch[j])
+                                             : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < WXJ; ++j) {
+      const int4 inf = pinfo[par][xrow[j] & 31];
+      const int gy = inf.z + xky[j], gx = inf.w + xkx[j];
+      xv[j] = make_uint4(0, 0, 0, 0);
+      if (xok[j] && inf.z > -(1 << 29) && gy >= 0 && gy < a.Hi && gx >= 0 && gx < a.Wi)
+        xv[j] = *reinterpret_cast<const uint4*>(a.x + (unsigned)inf.y +
+                                                (unsigned)((gy * a.Wi + gx) * Ci + (xoff[j] >> 16)));
+    }
+  };
+  auto store = [&](bf16_t* d, bf16_t* xx, const uint4 (&dv)[DJ], const uint4 (&xv)[WXJ]) {
+#pragma unroll
+    for (int j = 0; j < DJ; ++j) *reinterpret_cast<uint4*>(d + drow[j] * WWOP + dch[j]) = dv[j];
+#pragma unroll
+    for (int j = 0; j < WXJ; ++j)
+      if (tid + 256 * j < WXC) *reinterpret_cast<uint4*>(xx + (xoff[j] & 0xffff)) = xv[j];
+  };
+  constexpr int NTN = WWT / 2 / 16;  // 9 column tiles per wave
+  f32x4_t acc[MTW][NTN];
+#pragma unroll
+  for (int m = 0; m < MTW; ++m)
+#pragma unroll
+    for (int n = 0; n < NTN; ++n) acc[m][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  const int nk = (p1 - p0 + 31) / 32;
+  make_pinfo(p0);
+  if (nk > 1) make_pinfo(p0 + 32);
+  __syncthreads();
+  uint4 dv[DJ], xv[WXJ];
+  load(p0, dv, xv);
+  store(sd[0], sx[0], dv, xv);
+  __syncthreads();
+  const int g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
+  for (int ks = 0; ks < nk; ++ks) {
+    const int cur = ks & 1;
+    const bool more = ks + 1 < nk;
+    if (more) load(p0 + 32 * (ks + 1), dv, xv);
+    if (ks + 2 < nk) make_pinfo(p0 + 32 * (ks + 2));
+    bf16x8_t fa[MTW];
+#pragma unroll
+    for (int m = 0; m < MTW; ++m) {
+      const int cb = wr * (WWO / 2) + 16 * m + 4 * p4;
+      const s16x4_t lo = ds_read_tr(sd[cur] + (8 * g + q) * WWOP + cb);
+      const s16x4_t hi = ds_read_tr(sd[cur] + (8 * g + 4 + q) * WWOP + cb);
+      fa[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+#pragma unroll
+    for (int n = 0; n < NTN; ++n) {
+      const int cb = wc * (WWT / 2) + 16 * n + 4 * p4;
+      const s16x4_t lo = ds_read_tr(sx[cur] + (8 * g + q) * WWP + cb);
+      const s16x4_t hi = ds_read_tr(sx[cur] + (8 * g + 4 + q) * WWP + cb);
+      const bf16x8_t fb = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+      for (int m = 0; m < MTW; ++m) acc[m][n] = mfma16(fa[m], fb, acc[m][n]);
+    }
+    if (more) store(sd[cur ^ 1], sx[cur ^ 1], dv, xv);
+    __syncthreads();
+  }
+  float* gr = a.grads + (long)slot * a.g_mstride + a.g_off;
+  const int cr = a.cin_real > 0 ? a.cin_real : Ci;  // real input channels of a channel-padded operand (stem)
+  const int Kr = a.kh * a.kw * cr;
+#pragma unroll
+  for (int n = 0; n < NTN; ++n) {
+    const int col0 = n0 + wc * (WWT / 2) + 16 * n + (lane & 15);
+    const int ci_ = col0 & (Ci - 1);
+    if (col0 >= K || ci_ >= cr) continue;
+    const int col = (col0 >> a.log2ci) * cr + ci_;
+#pragma unroll
+    for (int m = 0; m < MTW; ++m) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = o0 + wr * (WWO / 2) + 16 * m + 4 * (lane >> 4) + r;
+        if (o < Co) atomicAdd(gr + (long)o * Kr + col, acc[m][n][r]);
+      }
+    }
+  }
+}
+
 }  // namespace
 
 DTF_API int dtf_cg_args_size() { return (int)sizeof(CgArgs); }
@@ -755,6 +919,28 @@ DTF_API int dtf_convg_wgrad(const CgArgs* a, int mode_x, int mode_dy, int nwork,
   WG_CASE(0, 2)
 #undef WG_CASE
   return -1;
+}
+
+// wide-column weight gradient with plain operands (work: (slot, p0, p1, o0 | n0/8 << 16)): wo x 288 tiles for 3x3
+// convs, wo x 256 for 1x1 convs with Ci % 256 == 0
+DTF_API int dtf_convg_wgrad_wide(const CgArgs* a, int wo, int wt, int nwork, hipStream_t stream) {
+  if (nwork <= 0) return 0;
+  const int K = a->kh * a->kw * a->Ci;
+  if ((a->Ci & (a->Ci - 1)) != 0 || a->Ci < 8 || (a->Co & 7) != 0) return -2;
+  if (wt != 416 && (a->Ci < 64 || K % wt != 0)) return -2;
+  if (wo == 128 && wt == 288)
+    hipLaunchKernelGGL((convg_wgrad_wide_kernel<128, 288>), dim3(nwork), dim3(256), 0, stream, *a);
+  else if (wo == 64 && wt == 288)
+    hipLaunchKernelGGL((convg_wgrad_wide_kernel<64, 288>), dim3(nwork), dim3(256), 0, stream, *a);
+  else if (wo == 128 && wt == 256)
+    hipLaunchKernelGGL((convg_wgrad_wide_kernel<128, 256>), dim3(nwork), dim3(256), 0, stream, *a);
+  else if (wo == 64 && wt == 256)
+    hipLaunchKernelGGL((convg_wgrad_wide_kernel<64, 256>), dim3(nwork), dim3(256), 0, stream, *a);
+  else if (wo == 64 && wt == 416)  // the 7x7 stem: 49 taps x 8 (3 real) channels in one tile
+    hipLaunchKernelGGL((convg_wgrad_wide_kernel<64, 416>), dim3(nwork), dim3(256), 0, stream, *a);
+  else
+    return -2;
+  return DTF_CHECK_LAUNCH();
 }
 
 DTF_DEBUG_EXPORT(convg)

@@ -166,36 +166,56 @@ __device__ __forceinline__ int chan8(long i, int C) {
   return (C & (C - 1)) == 0 ? (e & (C - 1)) : e % C;
 }
 
+// Both apply kernels stream U 16-byte chunks per thread and outer iteration, all loads issued before the first
+// store (the output may alias an input for the compiler), so each thread keeps U (x 2-3 operands) loads in flight.
+constexpr int EW_U = 4;
+
 __global__ __launch_bounds__(256) void cg_bn_bwd_apply_kernel(EwArgs a) {
   const int img = blockIdx.x;
   const int slot = a.img_slot[img];
   const float* co = a.coef + (long)slot * 4 * a.cmax;
   const long base = (long)img * a.hw * a.C;
   const long n8 = a.hw * a.C / 8;
-  for (long i = (long)blockIdx.y * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.y * blockDim.x) {
-    const long o = base + i * 8;
-    const int c0 = chan8(i, a.C);
-    const uint4 dv = *reinterpret_cast<const uint4*>(a.dz + o);
-    const uint4 hv = *reinterpret_cast<const uint4*>(a.h + o);
-    uint4 av = make_uint4(0, 0, 0, 0);
-    if (a.add) av = *reinterpret_cast<const uint4*>(a.add + o);
-    float ca[8], cbv[8], cc[8];
-    coef8(co + c0, ca);
-    coef8(co + a.cmax + c0, cbv);
-    coef8(co + 2 * a.cmax + c0, cc);
-    const uint32_t d32[4] = {dv.x, dv.y, dv.z, dv.w}, h32[4] = {hv.x, hv.y, hv.z, hv.w},
-                   a32[4] = {av.x, av.y, av.z, av.w};
-    uint32_t r[4];
+  const long stride = (long)gridDim.y * blockDim.x;
+  const bf16_t* __restrict__ dz = a.dz + base;
+  const bf16_t* __restrict__ h = a.h + base;
+  const bf16_t* __restrict__ add = a.add ? a.add + base : nullptr;
+  bf16_t* __restrict__ out = a.out + base;
+  for (long i0 = (long)blockIdx.y * blockDim.x + threadIdx.x; i0 < n8; i0 += EW_U * stride) {
+    uint4 dv[EW_U], hv[EW_U], av[EW_U];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float v0 = ca[2 * q] * __uint_as_float(d32[q] << 16) + cbv[2 * q] * __uint_as_float(h32[q] << 16) +
-                       cc[2 * q] + __uint_as_float(a32[q] << 16);
-      const float v1 = ca[2 * q + 1] * __uint_as_float(d32[q] & 0xffff0000u) +
-                       cbv[2 * q + 1] * __uint_as_float(h32[q] & 0xffff0000u) + cc[2 * q + 1] +
-                       __uint_as_float(a32[q] & 0xffff0000u);
-      r[q] = pack2bf(v0, v1);
+    for (int u = 0; u < EW_U; ++u) {
+      const long i = i0 + u * stride;
+      dv[u] = hv[u] = av[u] = make_uint4(0, 0, 0, 0);
+      if (i < n8) {
+        dv[u] = *reinterpret_cast<const uint4*>(dz + i * 8);
+        hv[u] = *reinterpret_cast<const uint4*>(h + i * 8);
+        if (add) av[u] = *reinterpret_cast<const uint4*>(add + i * 8);
+      }
     }
-    *reinterpret_cast<uint4*>(a.out + o) = make_uint4(r[0], r[1], r[2], r[3]);
+#pragma unroll
+    for (int u = 0; u < EW_U; ++u) {
+      const long i = i0 + u * stride;
+      if (i >= n8) break;
+      const int c0 = chan8(i, a.C);
+      float ca[8], cbv[8], cc[8];
+      coef8(co + c0, ca);
+      coef8(co + a.cmax + c0, cbv);
+      coef8(co + 2 * a.cmax + c0, cc);
+      const uint32_t d32[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w}, h32[4] = {hv[u].x, hv[u].y, hv[u].z, hv[u].w},
+                     a32[4] = {av[u].x, av[u].y, av[u].z, av[u].w};
+      uint32_t r[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float v0 = ca[2 * q] * __uint_as_float(d32[q] << 16) + cbv[2 * q] * __uint_as_float(h32[q] << 16) +
+                         cc[2 * q] + __uint_as_float(a32[q] << 16);
+        const float v1 = ca[2 * q + 1] * __uint_as_float(d32[q] & 0xffff0000u) +
+                         cbv[2 * q + 1] * __uint_as_float(h32[q] & 0xffff0000u) + cc[2 * q + 1] +
+                         __uint_as_float(a32[q] & 0xffff0000u);
+        r[q] = pack2bf(v0, v1);
+      }
+      *reinterpret_cast<uint4*>(out + i * 8) = make_uint4(r[0], r[1], r[2], r[3]);
+    }
   }
 }
 
@@ -206,22 +226,34 @@ __global__ __launch_bounds__(256) void cg_bn_relu_apply_kernel(EwArgs a) {
   const float* co = a.coef + (long)slot * 4 * a.cmax;
   const long base = (long)img * a.hw * a.C;
   const long n8 = a.hw * a.C / 8;
-  for (long i = (long)blockIdx.y * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.y * blockDim.x) {
-    const long o = base + i * 8;
-    const int c0 = chan8(i, a.C);
-    const uint4 hv = *reinterpret_cast<const uint4*>(a.h + o);
-    float sc[8], sh[8];
-    coef8(co + c0, sc);
-    coef8(co + a.cmax + c0, sh);
-    const uint32_t h32[4] = {hv.x, hv.y, hv.z, hv.w};
-    uint32_t r[4];
+  const long stride = (long)gridDim.y * blockDim.x;
+  const bf16_t* __restrict__ h = a.h + base;
+  bf16_t* __restrict__ out = a.out + base;
+  for (long i0 = (long)blockIdx.y * blockDim.x + threadIdx.x; i0 < n8; i0 += EW_U * stride) {
+    uint4 hv[EW_U];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float v0 = fmaxf(__uint_as_float(h32[q] << 16) * sc[2 * q] + sh[2 * q], 0.f);
-      const float v1 = fmaxf(__uint_as_float(h32[q] & 0xffff0000u) * sc[2 * q + 1] + sh[2 * q + 1], 0.f);
-      r[q] = pack2bf(v0, v1);
+    for (int u = 0; u < EW_U; ++u) {
+      const long i = i0 + u * stride;
+      hv[u] = i < n8 ? *reinterpret_cast<const uint4*>(h + i * 8) : make_uint4(0, 0, 0, 0);
     }
-    *reinterpret_cast<uint4*>(a.out + o) = make_uint4(r[0], r[1], r[2], r[3]);
+#pragma unroll
+    for (int u = 0; u < EW_U; ++u) {
+      const long i = i0 + u * stride;
+      if (i >= n8) break;
+      const int c0 = chan8(i, a.C);
+      float sc[8], sh[8];
+      coef8(co + c0, sc);
+      coef8(co + a.cmax + c0, sh);
+      const uint32_t h32[4] = {hv[u].x, hv[u].y, hv[u].z, hv[u].w};
+      uint32_t r[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float v0 = fmaxf(__uint_as_float(h32[q] << 16) * sc[2 * q] + sh[2 * q], 0.f);
+        const float v1 = fmaxf(__uint_as_float(h32[q] & 0xffff0000u) * sc[2 * q + 1] + sh[2 * q + 1], 0.f);
+        r[q] = pack2bf(v0, v1);
+      }
+      *reinterpret_cast<uint4*>(out + i * 8) = make_uint4(r[0], r[1], r[2], r[3]);
+    }
   }
 }
 

@@ -32,6 +32,17 @@ __device__ __forceinline__ s16x4_t ds_read_tr(const bf16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p));
 }
 
+// Branch-free predicated 16-byte load: a masked-off lane reads a zero vector in global memory.  A conditional load
+// makes hipcc branch around it and wait vmcnt(0) per element, which serialises a thread's gathers (PMC before
+// the change: 5-12 VALU per MFMA in these kernels).
+__device__ const uint4 g_zero16 = {0u, 0u, 0u, 0u};  // what a masked-off lane loads
+
+__device__ __forceinline__ uint4 ld16(const bf16_t* base, long off, bool ok) {
+  // a pointer select (2 VALU), not `ok ? load : 0` (hipcc turns that into a branch) nor a value mask (4 VALU)
+  const uint4* p = ok ? reinterpret_cast<const uint4*>(base + off) : &g_zero16;
+  return *p;
+}
+
 struct CgArgs {
   const bf16_t* x;    // gathered operand (fwd: input activations; dgrad: output gradient; wgrad: input)
   const bf16_t* x2;   // second input of a BN-backward transform
@@ -202,14 +213,11 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const bool ok = ((rmask[j] >> ty) & (cmask[j] >> tx) & 1u) && k < K;
-      v[j] = make_uint4(0, 0, 0, 0);
+      const long off = pbase[j] + toff;
+      v[j] = ld16(a.x, off, ok);
       v2[j] = make_uint4(0, 0, 0, 0);
-      if (ok) {
-        const long off = pbase[j] + toff;
-        v[j] = *reinterpret_cast<const uint4*>(a.x + off);
-        if constexpr (MODE == 2) v2[j] = *reinterpret_cast<const uint4*>(a.x2 + off);
-        okb |= 1u << j;  // unset: zero padding (stays zero after the transform)
-      }
+      if constexpr (MODE == 2) v2[j] = ld16(a.x2, off, ok);
+      okb |= (unsigned)ok << j;  // unset: zero padding (stays zero after the transform)
     }
   };
   auto xform_store = [&](bf16_t* dst, const uint4 (&v)[NJ], const uint4 (&v2)[NJ], int cch, unsigned okb) {
@@ -254,17 +262,14 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
       for (int j = 0; j < AJ; ++j) {
         const int kr = tid / ACH + (256 / ACH) * j, ch = tid % ACH;
         const int oc = obase + kr;
-        v[j] = (k0 + kr < K && o0 + 8 * ch < a.Co)
-                   ? *reinterpret_cast<const uint4*>(wbase + ((long)oc * kk + tapf) * a.Co + o0 + 8 * ch)
-                   : make_uint4(0, 0, 0, 0);
+        v[j] = ld16(wbase, ((long)oc * kk + tapf) * a.Co + o0 + 8 * ch, k0 + kr < K && o0 + 8 * ch < a.Co);
       }
     } else {
       const int kcol = TRANS ? (cur_ky * a.kw + cur_kx) * Ci + cur_ci : k;  // column in the full [o][K] row
 #pragma unroll
       for (int j = 0; j < AJ; ++j) {
         const int r = rB + RPT * j;
-        v[j] = (o0 + r < a.Co && k < K) ? *reinterpret_cast<const uint4*>(wbase + (long)(o0 + r) * Kfull + kcol)
-                                        : make_uint4(0, 0, 0, 0);
+        v[j] = ld16(wbase, (long)(o0 + r) * Kfull + kcol, o0 + r < a.Co && k < K);
       }
     }
   };
@@ -387,10 +392,8 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
       }
       orow[it] = (p < p1 && cok) ? pf * a.Co + oc : -1;
       rrv[it] = xrv[it] = make_uint4(0, 0, 0, 0);
-      if (orow[it] >= 0) {
-        if constexpr (EPI & 1) rrv[it] = *reinterpret_cast<const uint4*>(a.res + orow[it]);
-        if constexpr (EPI & 2) xrv[it] = *reinterpret_cast<const uint4*>(a.xm + orow[it]);
-      }
+      if constexpr (EPI & 1) rrv[it] = ld16(a.res, orow[it], orow[it] >= 0);
+      if constexpr (EPI & 2) xrv[it] = ld16(a.xm, orow[it], orow[it] >= 0);
     }
 #pragma unroll
   for (int it = 0; it < NPASS; ++it) {
@@ -550,18 +553,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PK == 32 ? 
     for (int j = 0; j < NJ; ++j) {
       const int4 inf = pinfo[par][kr + 16 * j];
       const bool pin = inf.z > -(1 << 29);
-      dv[j] = dv2[j] = xv[j] = make_uint4(0, 0, 0, 0);
-      if (pin && dcol_ok) {
-        const bf16_t* dp = a.dy + (unsigned)inf.x + dcol;
-        dv[j] = *reinterpret_cast<const uint4*>(dp);
-        if constexpr (MODE_DY == 2) dv2[j] = *reinterpret_cast<const uint4*>(a.dy2 + (unsigned)inf.x + dcol);
-        okm |= 1u << j;
-      }
+      dv2[j] = make_uint4(0, 0, 0, 0);
+      const bool dok = pin && dcol_ok;
+      dv[j] = ld16(a.dy, (long)(unsigned)inf.x + dcol, dok);
+      if constexpr (MODE_DY == 2) dv2[j] = ld16(a.dy2, (long)(unsigned)inf.x + dcol, dok);
+      okm |= (unsigned)dok << j;
       const int gy = inf.z + xky, gx = inf.w + xkx;
-      if (pin && xcol_ok && gy >= 0 && gy < a.Hi && gx >= 0 && gx < a.Wi) {
-        xv[j] = *reinterpret_cast<const uint4*>(a.x + (unsigned)inf.y + (unsigned)((gy * a.Wi + gx) * Ci + xci));
-        okm |= (1u << NJ) << j;
-      }
+      const bool xok = pin && xcol_ok && gy >= 0 && gy < a.Hi && gx >= 0 && gx < a.Wi;
+      xv[j] = ld16(a.x, (long)(unsigned)inf.y + (unsigned)((gy * a.Wi + gx) * Ci + xci), xok);
+      okm |= ((unsigned)xok << NJ) << j;
     }
   };
   auto store = [&](bf16_t* d, bf16_t* xx, const uint4 (&dv)[NJ], const uint4 (&dv2)[NJ], const uint4 (&xv)[NJ],
@@ -756,17 +756,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ?
 #pragma unroll
     for (int j = 0; j < DJ; ++j) {
       const int4 di = pinfo[par][drow[j]];
-      dv[j] = (di.z > -(1 << 29) && dok[j]) ? *reinterpret_cast<const uint4*>(a.dy + (unsigned)di.x + o0 + dch[j])
-                                             : make_uint4(0, 0, 0, 0);
+      dv[j] = ld16(a.dy, (long)(unsigned)di.x + o0 + dch[j], di.z > -(1 << 29) && dok[j]);
     }
 #pragma unroll
     for (int j = 0; j < WXJ; ++j) {
       const int4 inf = pinfo[par][xrow[j] & 31];
       const int gy = inf.z + xky[j], gx = inf.w + xkx[j];
-      xv[j] = make_uint4(0, 0, 0, 0);
-      if (xok[j] && inf.z > -(1 << 29) && gy >= 0 && gy < a.Hi && gx >= 0 && gx < a.Wi)
-        xv[j] = *reinterpret_cast<const uint4*>(a.x + (unsigned)inf.y +
-                                                (unsigned)((gy * a.Wi + gx) * Ci + (xoff[j] >> 16)));
+      xv[j] = ld16(a.x, (long)(unsigned)inf.y + (unsigned)((gy * a.Wi + gx) * Ci + (xoff[j] >> 16)),
+                   xok[j] && inf.z > -(1 << 29) && gy >= 0 && gy < a.Hi && gx >= 0 && gx < a.Wi);
     }
   };
   auto store = [&](bf16_t* d, bf16_t* xx, const uint4 (&dv)[DJ], const uint4 (&xv)[WXJ]) {

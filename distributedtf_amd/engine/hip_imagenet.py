@@ -41,6 +41,7 @@ _CG_WIDE = os.environ.get("DTF_CG_WIDE", "1") == "1"  # wide-column 3x3 weight-g
 _CG_WIDE128 = os.environ.get("DTF_CG_WIDE128", "1") == "1"
 _CG_WIDE7 = os.environ.get("DTF_CG_WIDE7", "1") == "1"  # one 64 x 416 tile for the 7x7 stem
 _CG_WIDE1 = os.environ.get("DTF_CG_WIDE1", "1") == "1"  # the wide tiles for 1x1 convs with Ci % 256 == 0
+_CG_TP256_128 = os.environ.get("DTF_CG_TP256_128", "1") == "1"  # 128 x 256 tiles (2 x 2 waves of 64 x 128)
 _CG_TP256 = os.environ.get("DTF_CG_TP256", "1") == "1"  # 256-pixel forward / dgrad tiles for 64-channel outputs
 _CG_WPK_WO64 = int(os.environ.get("DTF_CG_WPK_WO64", "32"))  # pixels per k-step of the 64-row tiles
 _CG_WG_TARGET = int(os.environ.get("DTF_CG_WG_TARGET", "1024"))
@@ -436,8 +437,8 @@ class _ImageNetPlan:
         # (a 256-row tile, 128 x 64 per wave, measured slower: 111.7 -> 123.4 ms/step at pop 8 x 128,
         # profiles/r2_imagenet_tc256_ab.log -- removed)
         tp = 128
-        if tc == 64 and _CG_TP256:
-            trans |= 8  # 256-pixel tiles: 1 x 4 waves of 64 x 64 (BK = 32)
+        if (tc == 64 and _CG_TP256) or (tc == 128 and _CG_TP256_128):
+            trans |= 8  # 256-pixel tiles (BK = 32): 1 x 4 waves of 64 x 64, or 2 x 2 of 64 x 128 for tc 128
             tp = 256
         elif _CG_BK == 64 and (not trans or a.Ci >= 64):
             trans |= 4  # k depth 64 per LDS stage

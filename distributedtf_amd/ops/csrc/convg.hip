@@ -77,13 +77,15 @@ struct CgArgs {
 // ds_read_b64_tr_b16), so no transposed weight copy exists.
 // BK: k depth per LDS stage (32 or 64).  BK = 64 halves the barriers and fragment-read restarts per MFMA and doubles
 // the bytes in flight per load batch; it needs Ci >= 64 on the incremental (one tap per k-step) gather path.
-// TP: pixels per workgroup tile.  128: 2 x 2 waves of (TC/2 rows x 64 pixels); 256 (TC = 64 only): 1 x 4 waves of
-// 64 rows x 64 pixels -- twice the MFMA work per k-step and wave of the 32 x 64 wave tile a 64-row conv gets
-// otherwise.
+// TP: pixels per workgroup tile.  128: 2 x 2 waves of (TC/2 rows x 64 pixels); 256: with TC = 64 1 x 4 waves of
+// 64 x 64 (twice the MFMA work per k-step and wave of the 32 x 64 wave tile a 64-row conv gets otherwise), with
+// TC = 128 2 x 2 waves of 64 x 128 (32 MFMAs per wave and k-step; the epilogue is staged in 64-pixel quarters).
 template <int TC, int MODE, int EPI, bool TRANS, bool AKM = false, int BK = 32, int TP = 128>
 __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
-  static_assert(TP == 128 || (TP == 256 && TC == 64), "pixel tile");
-  constexpr int WRN = TP == 256 ? 1 : 2;  // wave rows (the rest of the 4 waves split the pixels, 64 each)
+  static_assert(TP == 128 || TP == 256, "pixel tile");
+  // wave grid: TC = 64 x TP = 256 -> 1 x 4 waves of 64 x 64; else 2 x 2 waves of (TC/2) x (TP/2)
+  constexpr int WRN = (TP == 256 && TC == 64) ? 1 : 2;
+  constexpr int PW = TP / (4 / WRN), NTP = PW / 16;  // pixels per wave, MFMA pixel tiles per wave
   constexpr int RP = BK + 8;        // [rows][BK] tile pitch (+16 B)
   constexpr int CPR = BK / 8;       // 16-byte chunks per tile row
   constexpr int RPT = 256 / CPR;    // tile rows covered per pass of the workgroup
@@ -95,7 +97,7 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   // bf16 elements: operand buffers | fp32 epilogue staging of the whole tile; when the staging would exceed the
   // operand buffers (BK = 32) the tile is staged in two 64-pixel halves so LDS (and occupancy) stays the same
   constexpr int SOPS = 2 * SA + 2 * TP * RP, SEPI_FULL = 2 * TP * CPF;
-  constexpr int NHALF = SOPS >= SEPI_FULL ? 1 : 2, SEPI = SEPI_FULL / NHALF;
+  constexpr int NHALF = SOPS >= SEPI_FULL ? 1 : (2 * SOPS >= SEPI_FULL ? 2 : 4), SEPI = SEPI_FULL / NHALF;
   __shared__ __attribute__((aligned(16))) bf16_t smem_[SOPS > SEPI ? SOPS : SEPI];
   bf16_t (*sa)[SA] = reinterpret_cast<bf16_t (*)[SA]>(smem_);
   bf16_t (*sb)[TP * RP] = reinterpret_cast<bf16_t (*)[TP * RP]>(smem_ + 2 * SA);
@@ -282,11 +284,11 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
         *reinterpret_cast<uint4*>(dst + (rB + RPT * j) * RP + 8 * cB) = v[j];
     }
   };
-  f32x4_t acc[MT][4];
+  f32x4_t acc[MT][NTP];
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < NTP; ++n) acc[m][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
   __syncthreads();  // coefficients in LDS
   const int nk = (K + BK - 1) / BK;
   uint4 ra[AJ], rb[NJ], rb2[NJ];
@@ -309,7 +311,7 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
     }
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
-      bf16x8_t fa[MT], fb[4];
+      bf16x8_t fa[MT], fb[NTP];
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         if constexpr (AKM) {
@@ -324,13 +326,13 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
         }
       }
 #pragma unroll
-      for (int n = 0; n < 4; ++n)
-        fb[n] = *reinterpret_cast<const bf16x8_t*>(sb[cur] + (wc * 64 + 16 * n + (lane & 15)) * RP + 32 * kk +
+      for (int n = 0; n < NTP; ++n)
+        fb[n] = *reinterpret_cast<const bf16x8_t*>(sb[cur] + (wc * PW + 16 * n + (lane & 15)) * RP + 32 * kk +
                                                    8 * (lane >> 4));
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(fa[m], fb[n], acc[m][n]);
+        for (int n = 0; n < NTP; ++n) acc[m][n] = mfma16(fa[m], fb[n], acc[m][n]);
     }
     if (more) {
       store_a(sa[cur ^ 1], ra);
@@ -368,13 +370,15 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   for (int i = 0; i < 8; ++i) ss[i] = sq[i] = 0.f;
   for (int h = 0; h < NHALF; ++h) {
     if (h > 0) __syncthreads();  // the previous half's rows have been read
-    if (NHALF == 1 || (wc * 64) / (TP / NHALF) == h) {
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
+    for (int n = 0; n < NTP; ++n) {
+      const int pl = wc * PW + 16 * n - h * (TP / NHALF);  // staged row of this 16-pixel tile (wave-uniform)
+      if (NHALF == 1 || (pl >= 0 && pl < TP / NHALF)) {
 #pragma unroll
-        for (int n = 0; n < 4; ++n)
-          *reinterpret_cast<f32x4_t*>(cst + (wc * 64 - h * (TP / NHALF) + 16 * n + (lane & 15)) * CPF +
-                                      wr * (TC / WRN) + 16 * m + 4 * (lane >> 4)) = acc[m][n];
+        for (int m = 0; m < MT; ++m)
+          *reinterpret_cast<f32x4_t*>(cst + (pl + (lane & 15)) * CPF + wr * (TC / WRN) + 16 * m + 4 * (lane >> 4)) =
+              acc[m][n];
+      }
     }
     __syncthreads();
     // all residual / mask rows of this half are loaded before the first store (the stores may alias them for the
@@ -843,7 +847,7 @@ DTF_API int dtf_convg_fwd(const CgArgs* a, int tc, int mode, int epi, int trans,
   const int akm = (trans >> 1) & 1;
   const int bk64 = (trans >> 2) & 1;
   const int tp256 = (trans >> 3) & 1;  // 256-pixel tiles (tc = 64, BK = 32)
-  if (tp256 && (tc != 64 || bk64)) return -2;
+  if (tp256 && bk64) return -2;
   trans &= 1;
   if (nwork <= 0) return 0;
   if ((a->Ci & (a->Ci - 1)) != 0 || a->Ci < 8 || (a->Co & 7) != 0) return -2;
@@ -853,8 +857,8 @@ DTF_API int dtf_convg_fwd(const CgArgs* a, int tc, int mode, int epi, int trans,
   dim3 grid(nwork), block(256);
 #define CG_CASE(TC_, M_, E_, T_, AK_)                                                                      \
   if (tc == TC_ && mode == M_ && epi == E_ && trans == T_ && akm == AK_) {                                 \
-    if (tp256 && TC_ == 64)                                                                                \
-      hipLaunchKernelGGL((convg_fwd_kernel<64, M_, E_, T_, AK_, 32, 256>), grid, block, dyn, stream, *a); \
+    if (tp256)                                                                                             \
+      hipLaunchKernelGGL((convg_fwd_kernel<TC_, M_, E_, T_, AK_, 32, 256>), grid, block, dyn, stream, *a); \
     else if (bk64)                                                                                         \
       hipLaunchKernelGGL((convg_fwd_kernel<TC_, M_, E_, T_, AK_, 64>), grid, block, dyn, stream, *a);     \
     else                                                                                                   \

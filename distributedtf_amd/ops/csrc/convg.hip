@@ -156,6 +156,11 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   const bool inc = Ci >= BK;
   const int kstep = TRANS ? 2 : 1;
   int g_ty = 0, g_tx = 0, g_ci = 8 * cB;
+  if (!inc) {  // stem: first tap of this thread's chunk
+    const int tap = (8 * cB) >> a.log2ci;
+    g_ty = tap / a.kw;
+    g_tx = tap - g_ty * a.kw;
+  }
   int cur_ky = 0, cur_kx = 0, cur_ci = 0;  // position of this thread's chunk in the current k-step
   int cur_ty = 0, cur_tx = 0;              // the same as indices into the tap grid (ky = ky0 + kstep * ty)
   // Per-pixel gather origin, hoisted out of the k loop: tap (ty, tx) of pixel j reads row y0 + ty, column x0 + tx
@@ -197,13 +202,18 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
         }
       }
     } else {  // Ci < BK only occurs for the (non-transposed) channel-padded stem
-      const int k = k0 + 8 * cB;
-      const int tap = k >> a.log2ci;
-      cur_ci = k & (Ci - 1);
-      cur_ky = tap / a.kw;
-      cur_kx = tap - cur_ky * a.kw;
+      // this thread's chunk keeps its channel offset; its tap advances by BK / Ci per k-step (kept as (ky, kx)
+      // incrementally: no integer division by kw in the loop)
+      cur_ci = g_ci & (Ci - 1);
+      cur_ky = g_ty;
+      cur_kx = g_tx;
       cur_ty = cur_ky;
       cur_tx = cur_kx;
+      g_tx += BK >> a.log2ci;
+      while (g_tx >= a.kw) {
+        g_tx -= a.kw;
+        ++g_ty;
+      }
     }
   };
   auto load_b = [&](int k0, uint4 (&v)[NJ], uint4 (&v2)[NJ], int& cch, unsigned& okb) {

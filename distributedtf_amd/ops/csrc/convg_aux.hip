@@ -272,12 +272,14 @@ __global__ __launch_bounds__(256) void cg_prep_input_kernel(const float* __restr
 __global__ __launch_bounds__(256) void cg_maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                               uint8_t* __restrict__ am, int H, int W, int Ho, int Wo,
                                                               int C, long total8) {
-  const long stride = (long)gridDim.x * blockDim.x;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total8; i += stride) {
-    const int c0 = (int)((i * 8) % C);
-    const long pix = (i * 8) / C;
-    const int ox = (int)(pix % Wo), oy = (int)((pix / Wo) % Ho);
-    const long img = pix / ((long)Wo * Ho);
+  // 32-bit index math (the host checks total8 < 2^31; 64-bit division per element cost more than the loads)
+  const unsigned stride = gridDim.x * blockDim.x, C8 = (unsigned)C / 8;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < (unsigned)total8; i += stride) {
+    const unsigned pix = i / C8;
+    const int c0 = (int)(i - pix * C8) * 8;
+    const unsigned pr = pix / (unsigned)Wo;
+    const int ox = (int)(pix - pr * Wo), oy = (int)(pr % (unsigned)Ho);
+    const long img = pr / (unsigned)Ho;
     float best[8];
     uint32_t arg[8];
 #pragma unroll
@@ -299,7 +301,7 @@ __global__ __launch_bounds__(256) void cg_maxpool_fwd_kernel(const bf16_t* __res
         }
       }
     }
-    const long o = pix * C + c0;
+    const long o = (long)pix * C + c0;
     *reinterpret_cast<uint4*>(y + o) = make_uint4(pack2bf(best[0], best[1]), pack2bf(best[2], best[3]),
                                                   pack2bf(best[4], best[5]), pack2bf(best[6], best[7]));
     *reinterpret_cast<uint2*>(am + o) = make_uint2(arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24),
@@ -310,12 +312,13 @@ __global__ __launch_bounds__(256) void cg_maxpool_fwd_kernel(const bf16_t* __res
 __global__ __launch_bounds__(256) void cg_maxpool_bwd_kernel(const bf16_t* __restrict__ g, const uint8_t* __restrict__ am,
                                                               bf16_t* __restrict__ dx, int H, int W, int Ho, int Wo,
                                                               int C, long total8) {
-  const long stride = (long)gridDim.x * blockDim.x;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total8; i += stride) {
-    const int c0 = (int)((i * 8) % C);
-    const long pix = (i * 8) / C;
-    const int ix = (int)(pix % W), iy = (int)((pix / W) % H);
-    const long img = pix / ((long)W * H);
+  const unsigned stride = gridDim.x * blockDim.x, C8 = (unsigned)C / 8;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < (unsigned)total8; i += stride) {
+    const unsigned pix = i / C8;
+    const int c0 = (int)(i - pix * C8) * 8;
+    const unsigned pr = pix / (unsigned)W;
+    const int ix = (int)(pix - pr * W), iy = (int)(pr % (unsigned)H);
+    const long img = pr / (unsigned)H;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     // windows containing iy: oy in {iy/2 - 1 .. iy/2} with 2*oy <= iy <= 2*oy + 2
     for (int oy = (iy - 2 + 1) / 2; oy <= iy / 2; ++oy) {
@@ -334,7 +337,7 @@ __global__ __launch_bounds__(256) void cg_maxpool_bwd_kernel(const bf16_t* __res
         }
       }
     }
-    *reinterpret_cast<uint4*>(dx + pix * C + c0) = make_uint4(pack2bf(acc[0], acc[1]), pack2bf(acc[2], acc[3]),
+    *reinterpret_cast<uint4*>(dx + (long)pix * C + c0) = make_uint4(pack2bf(acc[0], acc[1]), pack2bf(acc[2], acc[3]),
                                                               pack2bf(acc[4], acc[5]), pack2bf(acc[6], acc[7]));
   }
 }
@@ -585,6 +588,7 @@ DTF_API int dtf_cg_maxpool(const bf16_t* x, bf16_t* y, uint8_t* am, const bf16_t
                            int Ho, int Wo, int C, int backward, hipStream_t stream) {
   if (C % 8) return -2;
   const long total8 = (long)N * (backward ? H * W : Ho * Wo) * C / 8;
+  if (total8 >= (1L << 31)) return -2;  // 32-bit element indices in the kernels
   long blocks = (total8 + 255) / 256;
   if (blocks > 16384) blocks = 16384;
   if (backward)

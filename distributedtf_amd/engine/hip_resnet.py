@@ -617,7 +617,12 @@ class _StepPlan:
         self.dual_cs = frozenset(int(v) for v in os.environ.get("DTF_DUAL_CS", "32,64").split(",") if v) \
             if dm != "1" else frozenset((16, 32, 64))
         self.side_reduce = bool(self.side_cs) or self.split
-        self.side_stream = torch.cuda.Stream(device=dev) if self.side_reduce else None
+        # DTF_SIDE_DEFER64: the deferred C = 64 dW slab reduction forked onto the side stream as soon as the last
+        # C = 64 layer is done, overlapping the stage-2 / 1 backward (joined before the optimizer).  Off: the graph's
+        # cross-queue fork / join cost more than the 38 us reduction it hides (pop 1 1.21 -> 1.29 ms, pop 8 3.44 ->
+        # 3.55 ms; profiles/r2_s3_side_defer64_ab.log)
+        self.side64 = (dev.type == "cuda" and not self.split and os.environ.get("DTF_SIDE_DEFER64", "0") == "1")
+        self.side_stream = torch.cuda.Stream(device=dev) if (self.side_reduce or self.side64) else None
         self.launches = []
         self._pending_slab = None  # (slab ptr, reduce table, C, grad offset) of the last fused launch
         self._slab_flip = 0
@@ -1206,10 +1211,10 @@ class _StepPlan:
         t = int(os.environ.get("DTF_PIGGYBACK_C64_WGS", t))
         return max(1, min(nb, t // max(1, n_members)))
 
-    def _flush_deferred(self):
+    def _flush_deferred(self, side=False):
         """One reduction launch over every deferred C = 64 slab (dw_slab_reduce_multi_kernel) and one over every
-        dense wgrad slab (dense_slab_reduce_multi_kernel)."""
-        if self._deferred_dense:
+        dense wgrad slab (dense_slab_reduce_multi_kernel).  ``side``: only the C = 64 slabs, on the side stream."""
+        if self._deferred_dense and not side:
             jobs = (DenseJob * len(self._deferred_dense))()
             nmax = bmax = 0
             for i, (buf, red, goff, kel) in enumerate(self._deferred_dense):
@@ -1230,8 +1235,8 @@ class _StepPlan:
             nmax = max(nmax, red.shape[0])
         jt = torch.frombuffer(bytearray(bytes(jobs)), dtype=torch.uint8).to(self.be.dev)
         self._keep(jt)
-        self._add(ops.lib().dtf_dw_slab_reduce_multi, _p(jt), len(self._deferred), nmax, _p(self.e.grads),
-                  self.e.Pp, 64)
+        (self._side if side else self._add)(ops.lib().dtf_dw_slab_reduce_multi, _p(jt), len(self._deferred), nmax,
+                                            _p(self.e.grads), self.e.Pp, 64)
         self._deferred = []
 
     def _flush_slab(self):
@@ -1396,6 +1401,7 @@ class _StepPlan:
         fused = os.environ.get("DTF_FUSED_BWD", "1") == "1"
         fold = fused and os.environ.get("DTF_FOLD_BNBWD", "1") == "1"
         pend = None  # deferred BN1-backward of the block just processed: (dz1, x, add, out, bn1)
+        side64 = self.side64 and self.side_stream is not None
         for i in range(nblk - 1, -1, -1):
             blk = prog.blocks[i]
             bn1, bn2 = blk.bns
@@ -1403,6 +1409,10 @@ class _StepPlan:
             Hi, Ho = x.shape[1], h.shape[1]
             T = self._tmp_for(Ho)
             ca, cb = blk.convs
+            if side64 and self._deferred and prog.convs[cb].cout < 64:
+                # every C = 64 layer's dW slab is complete: reduce them on the side stream while the stage-2 / 1
+                # backward (which leaves CUs idle at small populations) runs; joined before the optimizer
+                self._flush_deferred(side=True)
             # conv_b: dgrad -> dz2 (mask by BN2(h), BN2 reductions); wgrad
             if fused and pend is not None:
                 # the previous block's g = BN1-backward(dz1, x) [+ g] is computed while staging conv_b's dY

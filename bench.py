@@ -48,6 +48,9 @@ def parse():
                    help="steps queued behind an exploit's loss readback before the host runs the cycle (metric "
                         "all-gather, plan, weight copies, explore): the GPU keeps that many steps of work while the "
                         "host gathers and plans, so the cycle does not drain the queue")
+    p.add_argument("--exploit_offset", type=int, default=None,
+                   help="exploit at steps k with (k + 1 + offset) %% exploit_every == 0; default exploit_every // 2 "
+                        "(mid-interval), 0 = on the interval's last step")
     p.add_argument("--seed", type=int, default=2024)
     p.add_argument("--graph", type=int, default=1, help="capture the population step in a HIP graph")
     p.add_argument("--profile_json", default=None)
@@ -59,6 +62,8 @@ def parse():
         a.resnet_size = 50 if a.model == "imagenet" else 56
     if a.exploit_every is None:
         a.exploit_every = min(25, max(1, a.steps // 2))
+    if a.exploit_offset is None:
+        a.exploit_offset = (a.exploit_every or 0) // 2
     return a
 
 
@@ -183,7 +188,10 @@ def main():
         losses = step()
         while pending and pending[0][0] <= k:
             exploit_cycle(pending.pop(0)[1])  # overlaps the steps queued since its readback
-        if args.exploit_every and (k + 1) % args.exploit_every == 0:
+        # exploit points sit mid-interval (steps every/2, every/2 + every, ..) rather than on the last step, so
+        # each cycle's host work (all-gather, plan, copies) overlaps steps still queued behind it -- as it does in
+        # a long run -- instead of being appended, fully exposed, after the final step
+        if args.exploit_every and (k + 1 + args.exploit_offset) % args.exploit_every == 0:
             pending.append((k + lag, exploit_start(losses)))
     for _, pend in pending:
         exploit_cycle(pend)  # an exploit due after the last step still runs inside the timed region

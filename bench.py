@@ -44,7 +44,7 @@ def parse():
     p.add_argument("--exploit_every", type=int, default=None,
                    help="steps between PBT exploit/explore cycles inside the timed region; default "
                         "min(25, max(1, steps // 2)) so every timed run holds at least one cycle; 0 = none")
-    p.add_argument("--exploit_lag", type=int, default=3,
+    p.add_argument("--exploit_lag", type=int, default=5,
                    help="steps queued behind an exploit's loss readback before the host runs the cycle (metric "
                         "all-gather, plan, weight copies, explore): the GPU keeps that many steps of work while the "
                         "host gathers and plans, so the cycle does not drain the queue")

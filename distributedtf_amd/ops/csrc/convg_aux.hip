@@ -14,6 +14,8 @@
 //   cg_gap_bwd_reduce / cg_gap_bwd_apply : backward of GAP + final BN + ReLU
 #include "common.h"
 
+#include <cstdlib>
+
 #define BN_EPS 1e-5f
 #define BN_MOM 0.997f
 
@@ -166,10 +168,26 @@ __device__ __forceinline__ int chan8(long i, int C) {
   return (C & (C - 1)) == 0 ? (e & (C - 1)) : e % C;
 }
 
+// 16-byte output store; NT: non-temporal (DTF_EW_NT=1; measured 86.7 vs 86.9 ms per ResNet-50 step, so off: the
+// next conv reads the output right away, partly from the caches; profiles/r2_s3_imagenet_ew_nt_ab.log)
+template <bool NT>
+__device__ __forceinline__ void ew_store(bf16_t* p, uint4 v) {
+  if constexpr (NT) {
+    uint32_t* q = reinterpret_cast<uint32_t*>(p);
+    __builtin_nontemporal_store(v.x, q);
+    __builtin_nontemporal_store(v.y, q + 1);
+    __builtin_nontemporal_store(v.z, q + 2);
+    __builtin_nontemporal_store(v.w, q + 3);
+  } else {
+    *reinterpret_cast<uint4*>(p) = v;
+  }
+}
+
 // Both apply kernels stream U 16-byte chunks per thread and outer iteration, all loads issued before the first
 // store (the output may alias an input for the compiler), so each thread keeps U (x 2-3 operands) loads in flight.
 constexpr int EW_U = 4;
 
+template <bool NT>
 __global__ __launch_bounds__(256) void cg_bn_bwd_apply_kernel(EwArgs a) {
   const int img = blockIdx.x;
   const int slot = a.img_slot[img];
@@ -214,12 +232,13 @@ __global__ __launch_bounds__(256) void cg_bn_bwd_apply_kernel(EwArgs a) {
                          __uint_as_float(a32[q] & 0xffff0000u);
         r[q] = pack2bf(v0, v1);
       }
-      *reinterpret_cast<uint4*>(out + i * 8) = make_uint4(r[0], r[1], r[2], r[3]);
+      ew_store<NT>(out + i * 8, make_uint4(r[0], r[1], r[2], r[3]));
     }
   }
 }
 
 // a = relu(BN(h)) with the member's forward coefficients (the activation every consumer conv stages as-is)
+template <bool NT>
 __global__ __launch_bounds__(256) void cg_bn_relu_apply_kernel(EwArgs a) {
   const int img = blockIdx.x;
   const int slot = a.img_slot[img];
@@ -252,7 +271,7 @@ __global__ __launch_bounds__(256) void cg_bn_relu_apply_kernel(EwArgs a) {
         const float v1 = fmaxf(__uint_as_float(h32[q] & 0xffff0000u) * sc[2 * q + 1] + sh[2 * q + 1], 0.f);
         r[q] = pack2bf(v0, v1);
       }
-      *reinterpret_cast<uint4*>(out + i * 8) = make_uint4(r[0], r[1], r[2], r[3]);
+      ew_store<NT>(out + i * 8, make_uint4(r[0], r[1], r[2], r[3]));
     }
   }
 }
@@ -562,7 +581,11 @@ DTF_API int dtf_cg_bn_bwd_apply(const EwArgs* a, hipStream_t stream) {
   const long ms = (n8 + 255) / 256;
   if (split > ms) split = ms;
   if (split < 1) split = 1;
-  hipLaunchKernelGGL(cg_bn_bwd_apply_kernel, dim3((unsigned)a->nimg, (unsigned)split), dim3(256), 0, stream, *a);
+  static const bool nt = getenv("DTF_EW_NT") != nullptr && atoi(getenv("DTF_EW_NT")) != 0;
+  if (nt)
+    hipLaunchKernelGGL(cg_bn_bwd_apply_kernel<true>, dim3((unsigned)a->nimg, (unsigned)split), dim3(256), 0, stream, *a);
+  else
+    hipLaunchKernelGGL(cg_bn_bwd_apply_kernel<false>, dim3((unsigned)a->nimg, (unsigned)split), dim3(256), 0, stream, *a);
   return DTF_CHECK_LAUNCH();
 }
 
@@ -573,7 +596,11 @@ DTF_API int dtf_cg_bn_relu_apply(const EwArgs* a, hipStream_t stream) {
   const long ms = (n8 + 255) / 256;
   if (split > ms) split = ms;
   if (split < 1) split = 1;
-  hipLaunchKernelGGL(cg_bn_relu_apply_kernel, dim3((unsigned)a->nimg, (unsigned)split), dim3(256), 0, stream, *a);
+  static const bool nt = getenv("DTF_EW_NT") != nullptr && atoi(getenv("DTF_EW_NT")) != 0;
+  if (nt)
+    hipLaunchKernelGGL(cg_bn_relu_apply_kernel<true>, dim3((unsigned)a->nimg, (unsigned)split), dim3(256), 0, stream, *a);
+  else
+    hipLaunchKernelGGL(cg_bn_relu_apply_kernel<false>, dim3((unsigned)a->nimg, (unsigned)split), dim3(256), 0, stream, *a);
   return DTF_CHECK_LAUNCH();
 }
 

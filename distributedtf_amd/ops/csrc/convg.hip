@@ -12,10 +12,16 @@
 //               gather q = p + tap - P', valid iff q % S == 0, then q / S).
 //               T_in: identity | BN+ReLU (fwd prologue) | BN-backward apply A*dz + B*h + C (dgrad prologue).
 //               Epilogue: [+ residual], [mask by BN(xm)+ReLU > 0], bf16 store, per-channel sum / second
-//               moment (BN forward statistics, or sum(dz) / sum(dz*xhat) for the BN backward).
+//               moment (BN forward statistics, or sum(dz) / sum(dz*xhat) for the BN backward); the fp32 tile is
+//               staged through LDS so residual / mask loads and stores are whole 16-byte row segments.
+//               Tiles: TC (64 | 128) output channels x TP (128 | 256) pixels, k depth BK (32 | 64) per stage.
 //  convg_wgrad: dW[o][tap][i] += sum_p T_dy(dy)[p][o] * T_x(x)[p*S + tap - P][i], split over pixel ranges,
 //               both operands "k = pixel" fragments via ds_read_b64_tr_b16 from K-major LDS tiles, fp32
-//               atomics into the member's gradient row.
+//               atomics into the member's gradient row (64- or 128-row tiles x 128 columns).
+//  convg_wgrad_wide: the same for plain operands with wide column tiles (x 288 for 3x3, x 256 for 1x1,
+//               one 64 x 416 tile for the 7x7 stem) -- more MFMA work per k-step and per staged dy tile.
+// Every gather is branch-free (ld16: a masked-off lane reads a zero vector), so a thread's loads stay in flight
+// together.  tools/imagenet_roofline.py prices each launch of the step against its HBM / MFMA floor.
 // Per-member BN coefficients are precomputed by bn_finalize (convg_aux.hip) into [cap][4][CMAX] tables and
 // staged into LDS per workgroup (a workgroup's pixels always belong to one member).
 #include "common.h"

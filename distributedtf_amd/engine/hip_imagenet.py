@@ -44,7 +44,7 @@ _CG_WIDE1 = os.environ.get("DTF_CG_WIDE1", "1") == "1"  # the wide tiles for 1x1
 _CG_TP256_128 = os.environ.get("DTF_CG_TP256_128", "1") == "1"  # 128 x 256 tiles (2 x 2 waves of 64 x 128)
 _CG_TP256 = os.environ.get("DTF_CG_TP256", "1") == "1"  # 256-pixel forward / dgrad tiles for 64-channel outputs
 _CG_WPK_WO64 = int(os.environ.get("DTF_CG_WPK_WO64", "32"))  # pixels per k-step of the 64-row tiles
-_CG_WG_TARGET = int(os.environ.get("DTF_CG_WG_TARGET", "1024"))
+_CG_WG_TARGET = int(os.environ.get("DTF_CG_WG_TARGET", "512"))
 _CG_WG_MINCHUNK = int(os.environ.get("DTF_CG_WG_MINCHUNK", "2048"))
 
 
@@ -367,7 +367,9 @@ class _ImageNetPlan:
         member's pixels split into chunks so that the launch has about ``_CG_WG_TARGET`` items.  Every item
         atomically adds its full fp32 tile into the member's gradient row, so the split count is a trade: more
         items fill the chip, but each split adds 64 KB of atomic traffic per tile (the chip absorbs about 1.3 TB/s
-        of atomic adds).  The former 4096-item target moved ~14 GB of atomics per pop-8 ResNet-50 step."""
+        of atomic adds).  The former 4096-item target moved ~14 GB of atomics per pop-8 ResNet-50 step; with the
+        wide-column tiles 512 items measured best (85.3 ms/step vs 87.2 at 1024, 93.5 at 256;
+        profiles/r2_s3_imagenet_wg_target_ab.log)."""
         tiles = -(-co // wo) * -(-K // wt)
         per_member = max(1, -(-_CG_WG_TARGET // max(1, len(self.slots) * tiles)))
         items = []

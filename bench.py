@@ -146,12 +146,13 @@ def main():
         tc = time.perf_counter()
         exploit_wait_s.append(tc - tw)  # GPU still running the steps queued before the readback
         ls = host.tolist()
-        vals = [[m.cluster_id, -ls[i], m.hparams] for i, m in enumerate(members)]
+        vals = [[m.cluster_id, -ls[i], m.hparams, m.global_step] for i, m in enumerate(members)]
         parts = comm.allgather(vals)
-        allv = [v for p in parts for v in p]
+        allv = [v[:3] for p in parts for v in p]
+        steps = {v[0]: v[3] for p in parts for v in p}  # winners' host steps travel with the scores
         plan = plan_exploit(allv)
         transfers = [(p.src_id, owner[p.src_id], p.dst_id, owner[p.dst_id]) for p in plan]
-        dataplane.execute(transfers, {m.cluster_id: m for m in members})
+        dataplane.execute(transfers, {m.cluster_id: m for m in members}, steps=steps)
         upd = apply_plan_to_values(allv, plan)
         for m in members:
             if m.cluster_id in upd:
@@ -173,12 +174,7 @@ def main():
 
     for _ in range(args.warmup):
         losses = step()
-    if args.exploit_every and world > 1 and args.warmup > 0:
-        # one untimed exploit cycle: RCCL P2P channels between GPU pairs are set up lazily on first use
-        exploit_cycle(exploit_start(losses))
-        exploits[0] = 0
-        exploit_s.clear()
-        exploit_wait_s.clear()
+    # (RCCL P2P connections of every GPU pair are opened by init_distributed: no timed exploit pays a lazy setup)
     barrier_sync()
     images_done[0] = 0
     t0 = time.perf_counter()

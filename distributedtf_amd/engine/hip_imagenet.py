@@ -207,13 +207,15 @@ class HipImageNetBackend:
         return self.correct[torch.as_tensor(list(slots), dtype=torch.long, device=self.dev)]
 
     def eval_plan(self, slots, m):
-        key = ("eval", tuple(slots), int(m))
-        p = self._plans.get(key)
+        """Eval plans live in their own bounded cache: an eval pass never evicts the captured training graph."""
+        key = (tuple(slots), int(m))
+        plans = self.__dict__.setdefault("_eval_plans", {})
+        p = plans.get(key)
         if p is None:
-            if len(self._plans) > 4:
-                self._plans.clear()
+            if len(plans) >= 4:
+                plans.pop(next(iter(plans)))  # oldest first
             p = _ImageNetPlan(self, list(slots), [int(m)] * len(slots), eval_mode=True)
-            self._plans[key] = p
+            plans[key] = p
         return p
 
     @torch.no_grad()

@@ -37,8 +37,9 @@ from ..data.datasets import IndexBatch, batch_len
 from ..models.resnet import BN_EPS
 
 def _nrep() -> int:
-    """BN statistic replicas: must match the loaded build (common.h DTF_NREP; 64 in the deterministic build)."""
-    return 64 if ops.deterministic_mode() else int(os.environ.get("DTF_NREP", "8"))
+    """BN statistic replicas, as compiled into the loaded library (common.h DTF_NREP; 64 in the deterministic
+    build)."""
+    return ops.build_nrep()
 
 
 DET_WG_PER_MEMBER = 64  # deterministic mode: statistic-producing launches use <= this many workgroups per member
@@ -346,7 +347,7 @@ class HipResNetBackend:
         self.wf = torch.zeros(cap, self.L.wtot, dtype=torch.bfloat16, device=self.dev)
         self.wd = torch.zeros(cap, self.L.wtot, dtype=torch.bfloat16, device=self.dev)
         nb = len(self.L.prog.bns)
-        self.det = ops.deterministic_mode()
+        self.det = ops.build_deterministic()  # what the loaded library was compiled as
         if self.det and self.L.cfg.version != 2:
             raise ValueError("the deterministic HIP build covers the ResNet v2 step; use --backend torch for v1")
         NREP = self.nrep = _nrep()

@@ -116,10 +116,11 @@ class PopulationEngine:
             self.free_slots.append(slot)
             self.free_slots.sort()
 
-    def on_state_imported(self, slot: int, step: Optional[int] = None) -> None:
-        """A member's state row was overwritten (exploit).  ``step``: the source's step counter when the caller
-        knows it (same-GPU copy) -- avoids a device sync; otherwise read back from the imported row."""
-        self.host_step[slot] = int(step) if step is not None else int(round(float(self.step_col()[slot].item())))
+    def on_state_imported(self, slot: int, step: int) -> None:
+        """A member's state row was overwritten (exploit / checkpoint import).  ``step``: the source's host step
+        counter -- always known on the host (all-gathered with the scores, or sent on the control plane), so an
+        import never reads the device row back (no sync that would drain the queued steps)."""
+        self.host_step[slot] = int(step)
         self.backend.on_params_changed([slot])
 
     # --------------------------------------------------------------- training

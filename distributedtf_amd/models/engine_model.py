@@ -155,11 +155,16 @@ class EngineModel(ModelBase):
     def export_state(self):
         return self.engine.state_row(self.slot)
 
-    def import_state(self, flat):
-        self.engine.state_row(self.slot).copy_(flat.to(self.engine.state.device, torch.float32))
-        self.on_state_imported()
+    def import_state(self, flat, step=None):
+        """Overwrite this member's state row with ``flat`` (a host or device row).  ``step``: the source's step
+        counter; if omitted it is taken from ``flat``'s step column (a host read for a host row)."""
+        e = self.engine
+        if step is None:
+            step = int(round(float(flat[3 * e.Pp + e.R])))
+        e.state_row(self.slot).copy_(flat.to(e.state.device, torch.float32))
+        self.on_state_imported(step)
 
-    def on_state_imported(self, step=None):
+    def on_state_imported(self, step):
         self.engine.on_state_imported(self.slot, step)
 
     def tf_variables(self):

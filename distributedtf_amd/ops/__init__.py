@@ -68,6 +68,20 @@ def lib():
     return _LIB
 
 
+def build_nrep() -> int:
+    """BatchNorm-statistic replicas compiled into the loaded library (``dtf_nrep``)."""
+    fn = lib().dtf_nrep
+    fn.argtypes, fn.restype = [], c_int
+    return int(fn())
+
+
+def build_deterministic() -> bool:
+    """True if the loaded library is the deterministic build (``dtf_build_deterministic``)."""
+    fn = lib().dtf_build_deterministic
+    fn.argtypes, fn.restype = [], c_int
+    return bool(fn())
+
+
 def deterministic_mode() -> bool:
     """DTF_DETERMINISTIC=1 (set by ``--deterministic``): the deterministic kernel build (64 statistic replicas) and
     workgroup caps that make every reduction order fixed (engine/hip_resnet.py)."""
@@ -108,7 +122,7 @@ class _DebugLib:
     def __getattr__(self, name):
         fn = getattr(self._L, name)
         if (not name.startswith("dtf_") or name.startswith("dtf_debug_") or name.endswith("_size")
-                or name == "dtf_crc32c" or not torch.cuda.is_available()):
+                or name in ("dtf_crc32c", "dtf_nrep", "dtf_build_deterministic") or not torch.cuda.is_available()):
             return fn
         return _CheckedLaunch(self, name, fn)
 

@@ -19,3 +19,18 @@ extern "C" __attribute__((visibility("default"), target("sse4.2"))) uint32_t dtf
   while (n--) c32 = _mm_crc32_u8(c32, *p++);
   return ~c32;
 }
+
+// Build configuration of the loaded library, so the Python side sizes its buffers from what was actually compiled
+// (not from environment variables that may disagree with it): BatchNorm-statistic replicas per member and BN
+// (common.h DTF_NREP) and whether this is the deterministic build (fixed-order reductions).
+#ifndef DTF_NREP
+#define DTF_NREP 8
+#endif
+extern "C" __attribute__((visibility("default"))) int dtf_nrep() { return DTF_NREP; }
+extern "C" __attribute__((visibility("default"))) int dtf_build_deterministic() {
+#ifdef DTF_DETERMINISTIC
+  return 1;
+#else
+  return 0;
+#endif
+}

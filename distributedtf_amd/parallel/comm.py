@@ -294,6 +294,8 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0) -
             # ranks (exploit copies) never trigger a lazy, partial-world communicator init
             t = torch.ones(1, device="cuda")
             dist.all_reduce(t)
+            if os.environ.get("DTF_RCCL_PRECONNECT", "1") == "1":
+                preconnect_p2p(world, rank)
             torch.cuda.synchronize()
     cpu_group = dist.new_group(backend="gloo", timeout=td) if backend != "gloo" else dist.group.WORLD
     try:
@@ -307,6 +309,32 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0) -
     _CTX["comm"] = comm
     _CTX["backend"] = backend
     return comm
+
+
+def preconnect_p2p(world: int, rank: int) -> None:
+    """Open the RCCL point-to-point connection of EVERY ordered rank pair now, in one ``batch_isend_irecv`` group
+    (each rank sends one element to and receives one from every peer).  RCCL sets P2P channels up lazily on a
+    pair's first send/recv; exploit winner/loser pairs change every cycle, so without this a pair's first copy
+    would pay the connection setup inside a (timed) training round."""
+    import torch
+    import torch.distributed as dist
+    if world <= 1:
+        return
+    dev = torch.device("cuda", torch.cuda.current_device())
+    out = [torch.full((1,), float(rank), device=dev) for _ in range(world)]
+    inp = [torch.empty(1, device=dev) for _ in range(world)]
+    ops = []
+    for peer in range(world):
+        if peer == rank:
+            continue
+        ops.append(dist.P2POp(dist.isend, out[peer], peer))
+        ops.append(dist.P2POp(dist.irecv, inp[peer], peer))
+    for r in dist.batch_isend_irecv(ops):
+        r.wait()
+    got = torch.stack([inp[p] for p in range(world) if p != rank]).cpu().tolist()
+    want = [[float(p)] for p in range(world) if p != rank]
+    if got != want:
+        raise RuntimeError("RCCL P2P pre-connect exchanged wrong values: %r" % (got,))
 
 
 def backend_name() -> str:

@@ -15,12 +15,18 @@ per exploit).  A transfer ``(src_id, src_rank, dst_id, dst_rank)`` is:
   possible.  The receive lands directly in the loser's state row (zero-copy).
 
 On CPU worlds (tests) the same code runs over gloo.
+
+The receiving member's host-side step counter (it drives the LR schedule of the
+next step) is never read back from the imported device row: the caller passes
+the winners' host steps (``steps``: all-gathered with the scores), or, when it
+has none (master/worker mode), each source rank posts its member's step to the
+destination rank on the control plane (a host message, no device sync).
 """
 
 from __future__ import annotations
 
 import time
-from typing import Dict, Iterable, List, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 Transfer = Tuple[int, int, int, int]  # (src_id, src_rank, dst_id, dst_rank)
 
@@ -33,13 +39,17 @@ class DataPlane:
         self.bytes_moved = 0
         self.seconds = 0.0
         self.transfers_done = 0
+        self.step_timeout = 600.0
 
     @staticmethod
     def _state_of(member):
         view = getattr(member, "state_view", None)
         return view() if view is not None else member.export_state()
 
-    def execute(self, transfers: Sequence[Transfer], local_members: Dict[int, object]) -> None:
+    def execute(self, transfers: Sequence[Transfer], local_members: Dict[int, object],
+                steps: Optional[Dict[int, int]] = None) -> None:
+        """Run one exploit's copies.  ``steps``: member id -> host step counter of every SOURCE (None: exchanged
+        over the control plane for cross-rank pairs)."""
         import torch
         t0 = time.time()
         ops = []
@@ -57,11 +67,7 @@ class DataPlane:
                         hook = getattr(dst_m, "on_state_imported", None)
                         if hook is not None:
                             # the winner's step counter is known on the host: no device round trip
-                            step = getattr(local_members[src_id], "global_step", None)
-                            if step is not None:
-                                hook(step)
-                            else:
-                                hook()
+                            hook(int(local_members[src_id].global_step))
                     else:
                         dst_m.import_state(src.clone())
                 self.bytes_moved += src.numel() * src.element_size()
@@ -71,12 +77,14 @@ class DataPlane:
                     src = src.contiguous()
                 ops.append(("send", src, dst_rank))
                 self.bytes_moved += src.numel() * src.element_size()
+                if steps is None and hasattr(local_members[src_id], "state_view"):
+                    self.comm.send(("dtf_step", src_id, int(local_members[src_id].global_step)), dst_rank)
             elif dst_rank == self.rank:
                 dst_m = local_members[dst_id]
                 inplace = hasattr(dst_m, "state_view")
                 buf = self._state_of(dst_m) if inplace else torch.empty_like(dst_m.export_state())
                 ops.append(("recv", buf, src_rank))
-                pending.append((dst_m, buf, inplace))
+                pending.append((dst_m, buf, inplace, src_id, src_rank))
         if ops:
             if hasattr(self.comm, "tensor_send"):
                 # in-process worlds (LocalComm): sends are buffered, so issue them first
@@ -92,13 +100,19 @@ class DataPlane:
                        for k, t, peer in ops]
                 for r in dist.batch_isend_irecv(p2p):
                     r.wait()
-        for dst_m, buf, inplace in pending:
+        for dst_m, buf, inplace, src_id, src_rank in pending:
             if not inplace:
                 dst_m.import_state(buf)
+                continue
+            hook = getattr(dst_m, "on_state_imported", None)
+            if hook is None:
+                continue
+            if steps is not None:
+                hook(int(steps[src_id]))
             else:
-                hook = getattr(dst_m, "on_state_imported", None)
-                if hook is not None:
-                    hook()
+                tag, sid, step = self.comm.recv(src_rank, timeout=self.step_timeout)
+                assert tag == "dtf_step" and sid == src_id, ("exploit step message out of order", tag, sid, src_id)
+                hook(int(step))
         self.transfers_done += len(transfers)
         self.seconds += time.time() - t0
 

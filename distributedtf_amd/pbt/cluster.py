@@ -354,9 +354,18 @@ class SPMDPopulation(_ReportMixin):
                     if not self.reseed_dead:
                         self.worker._cull(g, "injected nan")
 
+    def _steps(self):
+        """member id -> host step counter of this rank's members (sent with the scores: an exploit destination
+        learns its new step without reading the imported device row back)."""
+        return {int(g.cluster_id): int(getattr(g, "global_step", 0) or 0) for g in self.worker.worker_graphs}
+
     def exploit(self):
-        parts = self.comm.allgather(self._values())  # also the end-of-train barrier
+        gathered = self.comm.allgather([self._values(), self._steps()])  # also the end-of-train barrier
         t0 = time.time()
+        parts = [g[0] for g in gathered]
+        steps = {}
+        for g in gathered:
+            steps.update(g[1])
         values = [v for part in parts for v in part]
         owner = {int(v[0]): r // self.dp_size for r, part in enumerate(parts) for v in part}  # member group
         self.pop_size = len(values)
@@ -368,7 +377,7 @@ class SPMDPopulation(_ReportMixin):
         transfers = [(p.src_id, owner[p.src_id] * d + r, p.dst_id, owner[p.dst_id] * d + r)
                      for p in plan for r in range(d)]
         if transfers:
-            self.dataplane.execute(transfers, self.worker.members_by_id())
+            self.dataplane.execute(transfers, self.worker.members_by_id(), steps=steps)
         updates = apply_plan_to_values(values, plan)
         mine = [u for mid, u in updates.items() if owner[mid] == self.group_index]
         self.worker.set_values(mine)

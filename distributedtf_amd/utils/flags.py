@@ -225,6 +225,10 @@ def parse_main_args(argv=None, defaults=None) -> MainArgs:
     elif args.loss_scale is not None and args.loss_scale != 1 and args.backend != "torch" and args.model != "toy":
         p.error("--loss_scale applies to the fp16 / fp32 PyTorch path; bf16 needs no loss scaling "
                 "(pass --backend torch to scale anyway)")
+    if args.deterministic and args.debug_kernels:
+        # the debug kernel build keeps the release reductions (8 replicas, atomics): not replayable
+        p.error("--deterministic cannot be combined with --debug_kernels (the debug build is not the "
+                "deterministic one)")
     if args.benchmark_logger_type == "BenchmarkFileLogger" and not args.benchmark_log_dir:
         p.error("--benchmark_logger_type BenchmarkFileLogger needs --benchmark_log_dir")
     return args

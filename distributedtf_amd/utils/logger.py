@@ -144,8 +144,16 @@ class BenchmarkFileLogger(BaseBenchmarkLogger):
             f.write("\n")
 
 
-def config_benchmark_logger(flag_obj=None):
-    """``benchmark_logger_type`` in {BaseBenchmarkLogger, BenchmarkFileLogger} (+ ``benchmark_log_dir``)."""
+def rank_log_dir(log_dir: str, rank: int = 0) -> str:
+    """Where process ``rank`` of a multi-process run writes its benchmark files: rank 0 (and a single-process run)
+    the directory itself, rank k > 0 ``<dir>/rank_<k>`` -- every training process logs its own members' eval
+    results, as each reference worker process does (resnet_run_loop.py:466)."""
+    return log_dir if not rank else os.path.join(log_dir, "rank_%d" % int(rank))
+
+
+def config_benchmark_logger(flag_obj=None, rank: int = 0):
+    """``benchmark_logger_type`` in {BaseBenchmarkLogger, BenchmarkFileLogger} (+ ``benchmark_log_dir``);
+    ``rank`` picks the per-process directory (``rank_log_dir``)."""
     global _benchmark_logger
     with _logger_lock:
         kind = getattr(flag_obj, "benchmark_logger_type", "BaseBenchmarkLogger") if flag_obj else "BaseBenchmarkLogger"
@@ -155,7 +163,7 @@ def config_benchmark_logger(flag_obj=None):
             d = getattr(flag_obj, "benchmark_log_dir", None)
             if not d:
                 raise ValueError("BenchmarkFileLogger needs benchmark_log_dir")
-            _benchmark_logger = BenchmarkFileLogger(d)
+            _benchmark_logger = BenchmarkFileLogger(rank_log_dir(d, rank))
         else:
             raise ValueError("Unrecognized benchmark_logger_type: %s" % kind)
     return _benchmark_logger
@@ -168,11 +176,11 @@ def get_benchmark_logger():
 
 
 @contextlib.contextmanager
-def benchmark_context(flag_obj=None):
+def benchmark_context(flag_obj=None, rank: int = 0):
     """Configure the process-wide logger for one run; the previous logger is restored afterwards."""
     global _benchmark_logger
     prev = _benchmark_logger
-    bl = config_benchmark_logger(flag_obj)
+    bl = config_benchmark_logger(flag_obj, rank=rank)
     try:
         yield bl
         bl.on_finish(RUN_STATUS_SUCCESS)

@@ -60,6 +60,7 @@ def main(argv=None):
     comm.barrier()
 
     inject = args.inject_nan_schedule()
+    from distributedtf_amd.utils import logger as bench_logger
     if args.mode == "master_worker":
         if world < 2:
             raise SystemExit("master_worker mode needs >= 2 ranks (1 master + workers)")
@@ -72,7 +73,12 @@ def main(argv=None):
         else:
             worker = TrainingWorker(comm, master_rank, cls, save_base_dir=os.path.join(savedata, "model_"),
                                     seed=args.seed, model_kwargs=model_kwargs, dataplane=DataPlane(comm))
-            worker.main_loop()
+            # the worker process trains members: its eval results / hook metrics go to its own benchmark files
+            with bench_logger.benchmark_context(args, rank=rank):
+                worker.main_loop()
+            if world > 1:
+                from distributedtf_amd.parallel.comm import shutdown_distributed
+                shutdown_distributed()
             return 0
     else:
         cluster = SPMDPopulation(args.population_size, comm, cls, epochs_per_round=args.epochs_per_round,
@@ -80,11 +86,10 @@ def main(argv=None):
                                  savedata=savedata, model_kwargs=model_kwargs, inject_nan=inject,
                                  resume=args.resume, dp_size=args.dp_size, reseed_dead=args.reseed_dead)
 
-    from distributedtf_amd.utils import logger as bench_logger
     # benchmark logger (reference logger.benchmark_context / log_run_info, cifar10_main.py:314-318,
-    # resnet_run_loop.py:408-421): rank 0 owns the files, other ranks log through python logging
-    log_flags = args if rank == master_rank else None
-    with bench_logger.benchmark_context(log_flags) as blog:
+    # resnet_run_loop.py:408-421): configured in EVERY process (per-rank files, utils/logger.rank_log_dir), so the
+    # eval records of the members each rank trains are kept; rank 0 also writes the run info
+    with bench_logger.benchmark_context(args, rank=rank) as blog:
         if rank == master_rank:
             blog.log_run_info(args.model if args.model != "cifar10" else "resnet%s" % (args.resnet_size or 50),
                               {"toy": "toy", "mnist": "mnist", "cifar10": "cifar10", "imagenet": "imagenet"}.get(

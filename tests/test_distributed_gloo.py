@@ -46,6 +46,14 @@ def _worker(rank, world, port, tmp, q, pop=4):
         for d in gathered:
             allst.update(d)
         ok = all(torch.equal(allst[s], allst[d]) for s, d in plan)
+        # the loser's HOST step counter (LR schedule) equals the winner's: learnt from the score all-gather,
+        # never by reading the imported device row back
+        hsteps = {}
+        for d in comm.allgather({g.cluster_id: g.global_step for g in pop.worker.worker_graphs}):
+            hsteps.update(d)
+        e0 = pop.worker.worker_graphs[0].engine
+        col = 3 * e0.Pp + e0.R  # step column of a state row
+        ok = ok and all(hsteps[s] == hsteps[d] == int(allst[d][col].item()) for s, d in plan)
         q.put((rank, plan, ok, sorted(allst)))
         shutdown_distributed()
     except Exception as e:  # pragma: no cover

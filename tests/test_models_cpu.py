@@ -164,7 +164,7 @@ def test_population_engine_state_rows_and_import():
     assert eng.host_step[s0] == 1 and eng.step_col()[s0].item() == 1.0
     # exploit copy = one row copy; step counter travels with the state
     eng.state[s1].copy_(eng.state[s0])
-    eng.on_state_imported(s1)
+    eng.on_state_imported(s1, eng.host_step[s0])
     assert eng.host_step[s1] == 1 and torch.equal(eng.params[s1], eng.params[s0])
     assert eng.slot1[s0].abs().sum() > 0  # momentum slot populated
 

@@ -65,3 +65,28 @@ def test_main_manager_toy_master_worker_torchcomm(tmp_path):
         assert len(rows) == 1 + 3 * 2  # one row per toy step (toy_model.py:52-61)
     assert open(tmp_path / "test_results.txt").read().startswith("n = 2, pop_size = 4")
     assert "Copied:" in r.stdout
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("mode,world", [("spmd", 2), ("master_worker", 3)])
+def test_main_manager_per_rank_benchmark_logs(tmp_path, mode, world):
+    """Every training process logs its own members' eval results (resnet_run_loop.py:466) to its own
+    BenchmarkFileLogger directory: rank 0 -> <dir>, rank k -> <dir>/rank_k.  master_worker at world 3 also runs
+    the exploit copy between two worker ranks with the winner's step sent on the control plane."""
+    r = _torchrun(world, [os.path.join(REPO, "main_manager.py"), "4", "--model", "cifar10", "--resnet_size", "8",
+                          "--use_synthetic_data", "true", "--backend", "torch", "--max_train_steps", "2",
+                          "--rounds", "2", "--seed", "3", "--mode", mode, "--benchmark_logger_type",
+                          "BenchmarkFileLogger", "--benchmark_log_dir", "blog"], str(tmp_path), 540)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    acc = []
+    for k in range(world):
+        d = tmp_path / "blog" / ("rank_%d" % k if k else "")
+        p = d / "metric.log"
+        if mode == "master_worker" and k == 0:
+            assert not p.exists() or all(json.loads(l)["name"] != "accuracy" for l in open(p))  # master trains none
+            continue
+        assert p.is_file(), p
+        acc += [json.loads(l) for l in open(p) if json.loads(l)["name"] == "accuracy"]
+    assert len(acc) == 4 * 2  # every member's eval of both rounds, whichever rank trained it
+    assert json.load(open(tmp_path / "blog" / "benchmark_run.log"))["status"] == "success"
+    assert "Copied:" in r.stdout

@@ -33,19 +33,19 @@ c_void_p, c_int, c_long, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_long,
 CMAX = 2048
 NPAD_CLS = 1024
 # k depth per LDS stage of the convg forward / data-gradient kernel (32 or 64)
-_CG_BK = int(os.environ.get("DTF_CG_BK", "32"))
+_CG_BK = 32  # K depth of one LDS stage of the forward / dgrad tiles
 # weight gradient: pixels per k-step (32 or 64), target items per launch, minimum pixels per split-K chunk
-_CG_WPK = int(os.environ.get("DTF_CG_WPK", "32"))
-_CG_WO64 = os.environ.get("DTF_CG_WO64", "1") == "1"
-_CG_WIDE = os.environ.get("DTF_CG_WIDE", "1") == "1"  # wide-column 3x3 weight-gradient tiles
-_CG_WIDE128 = os.environ.get("DTF_CG_WIDE128", "1") == "1"
-_CG_WIDE7 = os.environ.get("DTF_CG_WIDE7", "1") == "1"  # one 64 x 416 tile for the 7x7 stem
-_CG_WIDE1 = os.environ.get("DTF_CG_WIDE1", "1") == "1"  # the wide tiles for 1x1 convs with Ci % 256 == 0
-_CG_TP256_128 = os.environ.get("DTF_CG_TP256_128", "1") == "1"  # 128 x 256 tiles (2 x 2 waves of 64 x 128)
-_CG_TP256 = os.environ.get("DTF_CG_TP256", "1") == "1"  # 256-pixel forward / dgrad tiles for 64-channel outputs
-_CG_WPK_WO64 = int(os.environ.get("DTF_CG_WPK_WO64", "32"))  # pixels per k-step of the 64-row tiles
-_CG_WG_TARGET = int(os.environ.get("DTF_CG_WG_TARGET", "512"))
-_CG_WG_MINCHUNK = int(os.environ.get("DTF_CG_WG_MINCHUNK", "2048"))
+_CG_WPK = 32
+_CG_WO64 = True
+_CG_WIDE = True  # wide-column 3x3 weight-gradient tiles
+_CG_WIDE128 = True
+_CG_WIDE7 = True  # one 64 x 416 tile for the 7x7 stem
+_CG_WIDE1 = True  # the wide tiles for 1x1 convs with Ci % 256 == 0
+_CG_TP256_128 = True  # 128 x 256 tiles (2 x 2 waves of 64 x 128)
+_CG_TP256 = True  # 256-pixel forward / dgrad tiles for 64-channel outputs
+_CG_WPK_WO64 = 32  # pixels per k-step of the 64-row tiles
+_CG_WG_TARGET = 512
+_CG_WG_MINCHUNK = 2048
 
 
 class CgArgs(ctypes.Structure):
@@ -296,11 +296,9 @@ class _ImageNetPlan:
         self.am0 = torch.empty(N, H2, H2, cfg.num_filters, dtype=torch.uint8, device=dev)
         self.xs, self.h1, self.h2, self.sc = [act("x", H2, cfg.num_filters, 0)], [], [], []
         # materialised BN+ReLU outputs (the operands every consumer conv stages as-is, and the weight-gradient
-        # inputs): ax = relu(BN1(x)), a1 = relu(BN2(h1)), a2 = relu(BN3(h2)) -- only without prologue folding
-        # (DTF_CG_FOLD=0) and in eval plans; folded, the consumers apply BN+ReLU / BN-backward while staging
-        # (off by default: folding measured slower, 114.7 -> 135.7 ms/step at pop 8 x 128 -- the transform is
-        # repeated for every output-channel tile and its coefficient LDS costs occupancy; profiles/r2_imagenet_fold_ab.log)
-        self.fold = (not self.eval) and os.environ.get("DTF_CG_FOLD", "0") == "1"
+        # inputs): ax = relu(BN1(x)), a1 = relu(BN2(h1)), a2 = relu(BN3(h2)).  (Applying BN+ReLU while each consumer
+        # stages its operand measured slower, 114.7 -> 135.7 ms/step at pop 8 x 128: the transform is repeated for
+        # every output-channel tile and its coefficient LDS costs occupancy; profiles/r2_imagenet_fold_ab.log)
         self.ax, self.a1, self.a2 = [], [], []
         hw, cin = H2, cfg.num_filters
         self.geo = []  # per block: (H_in, H_out, cin, f, fout)
@@ -309,10 +307,9 @@ class _ImageNetPlan:
             ho = hw // blk.stride
             self.h1.append(act("h1", hw, c1.cout))
             self.h2.append(act("h2", ho, c2.cout))
-            if not self.fold:
-                self.ax.append(act("ax", hw, cin))
-                self.a1.append(act("a1", hw, c1.cout))
-                self.a2.append(act("a2", ho, c2.cout))
+            self.ax.append(act("ax", hw, cin))
+            self.a1.append(act("a1", hw, c1.cout))
+            self.a2.append(act("a2", ho, c2.cout))
             self.sc.append(act("sc", ho, c3.cout) if blk.proj is not None else None)
             self.xs.append(act("x", ho, c3.cout, bi + 1))
             self.geo.append((hw, ho, cin, c1.cout, c3.cout))
@@ -535,7 +532,6 @@ class _ImageNetPlan:
         self._add(L.dtf_cg_chan_stats, _p(self.xs[0]), _p(self.img_slot), _p(self.sf(prog.blocks[0].bns[0])), N,
                   H2 * H2, cfg.num_filters, CMAX)
         nblk = len(prog.blocks)
-        fold = self.fold
         for i, blk in enumerate(prog.blocks):
             hi, ho, cin, f, fout = self.geo[i]
             b1, b2, b3 = blk.bns
@@ -545,17 +541,6 @@ class _ImageNetPlan:
             nxt = prog.blocks[i + 1].bns[0] if i + 1 < nblk else prog.final_bn
             res = self.sc[i] if blk.proj is not None else x
             self.bn_final(b1, hi, False)
-            if fold:
-                # BN+ReLU applied while each consumer stages its operand (convg MODE 1): no materialised activation
-                if blk.proj is not None:
-                    self.conv(blk.proj, x, self.sc[i], hi, mode=1, c_in=self.cf(b1), epi=0)
-                self.conv(c1, x, self.h1[i], hi, mode=1, c_in=self.cf(b1), epi=4, st=self.sf(b2))
-                self.bn_final(b2, hi, False)
-                self.conv(c2, self.h1[i], self.h2[i], hi, mode=1, c_in=self.cf(b2), epi=4, st=self.sf(b3))
-                self.bn_final(b3, ho, False)
-                self.conv(c3, self.h2[i], self.xs[i + 1], ho, mode=1, c_in=self.cf(b3), epi=5, res=res,
-                          st=self.sf(nxt))
-                continue
             self.ew(relu, x, self.ax[i], self.cf(b1), hi, cin)
             if blk.proj is not None:
                 self.conv(blk.proj, self.ax[i], self.sc[i], hi, mode=0, epi=0)
@@ -612,32 +597,6 @@ class _ImageNetPlan:
             c1, c2, c3 = blk.convs
             x, h1, h2 = self.xs[i], self.h1[i], self.h2[i]
             bwd = L.dtf_cg_bn_bwd_apply
-            if fold:
-                # BN-backward applied while the next dgrad / wgrad stage their dy operand (convg MODE 2); the
-                # forward BN+ReLU of each wgrad's x operand likewise (MODE_X 1)
-                dz3 = self.tmp("dz3", ho, f)
-                self.conv(c3, gcur, dz3, ho, mode=0, epi=6, xm=h2, c_ep=self.cf(b3), st=self.sb(b3), dgrad=True)
-                self.bn_final(b3, ho, True)
-                self.wgrad(c3, h2, gcur, ho, mode_x=1, c_x=self.cf(b3))
-                dz2 = self.tmp("dz2", hi, f)
-                self.conv(c2, dz3, dz2, ho, mode=2, c_in=self.cb(b3), x2=h2, epi=6, xm=h1, c_ep=self.cf(b2),
-                          st=self.sb(b2), dgrad=True)
-                self.bn_final(b2, hi, True)
-                self.wgrad(c2, h1, dz3, hi, mode_x=1, c_x=self.cf(b2), mode_dy=2, c_dy=self.cb(b3), dy2=h2)
-                pd = None
-                if blk.proj is not None:
-                    pd = self.tmp("pd", hi, cin)
-                    self.conv(blk.proj, gcur, pd, ho, mode=0, epi=0, dgrad=True)
-                    self.wgrad(blk.proj, x, gcur, hi, mode_x=1, c_x=self.cf(b1))
-                dz1 = self.tmp("dz1", hi, cin)
-                self.conv(c1, dz2, dz1, hi, mode=2, c_in=self.cb(b2), x2=h1, epi=6 | (1 if pd is not None else 0),
-                          res=pd, xm=x, c_ep=self.cf(b1), st=self.sb(b1), dgrad=True)
-                self.bn_final(b1, hi, True)
-                self.wgrad(c1, x, dz2, hi, mode_x=1, c_x=self.cf(b1), mode_dy=2, c_dy=self.cb(b2), dy2=h1)
-                gnext = self.tmp("gA" if (i % 2 == 0) else "gB", hi, cin)
-                self.ew(bwd, x, gnext, self.cb(b1), hi, cin, dz=dz1, add=None if blk.proj is not None else gcur)
-                gcur = gnext
-                continue
             # conv3: dz3 = dgrad(g) masked by BN3(h2) (+ BN3 reductions); dh2 = BN3-backward(dz3, h2)
             dz3 = self.tmp("dz3", ho, f)
             self.conv(c3, gcur, dz3, ho, mode=0, epi=6, xm=h2, c_ep=self.cf(b3), st=self.sb(b3), dgrad=True)

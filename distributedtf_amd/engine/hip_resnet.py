@@ -43,6 +43,18 @@ def _nrep() -> int:
 
 
 DET_WG_PER_MEMBER = 64  # deterministic mode: statistic-producing launches use <= this many workgroups per member
+# Work-split constants of the step plans (each the winner of an A/B in profiles/; the losing variants were deleted)
+DUAL_MAX_POP = 2          # dual (dgrad | wgrad role) backward launches up to this many members per GPU ...
+DUAL_CS = (32, 64)        # ... for these channel widths (C = 16 keeps the fused kernel)
+DUAL_WG = {16: 128, 32: 128, 64: 64}  # wgrad-role workgroups per member of a dual launch
+FWD_ITERS_PER_WG = 4      # forward: (image, band) iterations per workgroup (>= 256 workgroups kept)
+HEAD_ITEMS = 512          # head / GAP+dense+CE work items
+WGRAD_WG_PER_MEMBER = 128  # standalone wgrad launches: workgroups per member (bounds the dW partial traffic)
+DENSE_REDUCE_BLOCKS = 256  # dense_slab_reduce_multi: max 32-element blocks per job
+FUSED_SLAB_BYTES = {16: 16e6, 32: 16e6, 64: 48e6}  # fused backward: per-launch dW slab budget -> workgroup count
+FUSED_MIN_WG = 256        # ... at least this many workgroups (one member would leave CUs idle otherwise)
+FUSED_MAX_WG = {32: 128}  # ... at most this many per member (C = 32: fewer, fuller workgroups)
+PIGGYBACK_MAX_WG = 3000   # slab reductions ride on the next backward launch when they add <= this many workgroups
 c_void_p, c_int, c_long = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
 
 
@@ -119,7 +131,6 @@ def _register():
     ops.register("dtf_conv_fwd_s1", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_dw_slab_reduce", [c_void_p, c_void_p, c_int, c_void_p, c_long, c_long, c_int, c_void_p])
     ops.register("dtf_conv_bwd_fused", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
-    ops.register("dtf_conv_bwd_role", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_bwd_dual", [P(ConvArgs), P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_dw_slab_reduce_multi", [c_void_p, c_int, c_int, c_void_p, c_long, c_int, c_void_p])
     ops.register("dtf_slab_job_size", [])
@@ -167,8 +178,6 @@ def _register():
 
 def _cpad(c: int) -> int:
     """LDS pixel pitch (bf16 elements) of a C-channel tile: must match conv.hip ``cpad<C>()``."""
-    if os.environ.get("DTF_CPAD_OLD", "0") == "1":
-        return c + 8
     return {16: 16, 32: 48, 64: 80}.get(c, c + 8)
 
 
@@ -185,7 +194,7 @@ def _wpitch(c: int) -> int:
 
 def _cpad_fwd(c: int) -> int:
     """conv_fwd_s1 pitch (conv.hip ``cpad_fwd<C>()``)."""
-    return 24 if c == 16 and os.environ.get("DTF_CPAD_OLD", "0") != "1" else _cpad(c)
+    return 24 if c == 16 else _cpad(c)
 
 
 def _p(t):
@@ -507,8 +516,7 @@ class _StepPlan:
             cnt[s] = float(n)
         self.cnt = cnt.to(dev)
         # uniform population: work items of the stage kernels computed from blockIdx (ConvArgs.u_items)
-        self.uniform = (len(set(sizes)) == 1 and list(slots) == list(range(len(slots))) and not self.elastic
-                        and os.environ.get("DTF_UNIFORM_WORK", "1") == "1")
+        self.uniform = len(set(sizes)) == 1 and list(slots) == list(range(len(slots))) and not self.elastic
         if self.elastic:
             for s, n in zip(slots, self.real_sizes):
                 cnt[s] = float(n)
@@ -562,7 +570,6 @@ class _StepPlan:
             self.ev_acc = torch.zeros(2, cap, dtype=torch.float32, device=dev)  # [correct, summed mean CE] per slot
             self.logits = None  # [N, ncls] fp32 when requested (tests)
             self._work_cache, self._uniform_geo = {}, {}
-            self.side_cs, self.split, self.side_reduce, self.side_stream = frozenset(), False, False, None
             self.launches = []
             self._pending_slab = None
             self._build_eval()
@@ -588,53 +595,19 @@ class _StepPlan:
         self.dfeat = torch.zeros(N, cfg.final_size, dtype=torch.float32, device=dev)
         self._work_cache = {}
         self._uniform_geo = {}
-        # dW slab reductions on a forked stream (joined before the optimizer): off the critical path
-        # DTF_SIDE_REDUCE: "1" = every channel width, "0" = none, or a comma list of widths (e.g. "64")
-        sr = os.environ.get("DTF_SIDE_REDUCE", "0").strip()
-        if dev.type != "cuda" or sr in ("", "0"):
-            self.side_cs = frozenset()
-        elif sr == "1":
-            self.side_cs = frozenset((16, 32, 64))
-        else:
-            self.side_cs = frozenset(int(v) for v in sr.split(",") if v)
-        # Split backward (small populations: the step is latency-bound, one workgroup per CU): every stride-1 conv's
-        # dgrad runs on the main stream (the critical path) and its wgrad on a side stream, concurrently with the
-        # next layers' dgrads; backward temporaries are then never reused (the side stream reads them later).
-        # DTF_SPLIT_BWD: "auto" (populations of <= DTF_SPLIT_MAX_POP members, default 2), "1", "0" (default: on this
-        # ROCm the graph's cross-queue dependencies cost ~10 us each, pop 1 measured 2.30 vs 1.45 ms/step).
-        sp = os.environ.get("DTF_SPLIT_BWD", "0")
-        self.split = dev.type == "cuda" and not cfg.version == 1 and (
-            sp == "1" or (sp == "auto" and len(slots) <= int(os.environ.get("DTF_SPLIT_MAX_POP", "2"))))
-        # Dual backward (small populations): each stride-1 conv's dgrad and wgrad run as two workgroup roles of ONE
-        # launch (conv_bwd_dual_kernel) -- no cross-stream dependencies; the layer costs max(dgrad, wgrad) instead of
-        # their sum when the population leaves CUs idle.  DTF_DUAL_BWD: "auto" (<= DTF_DUAL_MAX_POP members,
-        # default 2), "1", "0".
-        # DTF_DUAL_CS: channel widths that use it (default 32, 64: at one member the C = 64 layers drop from 13.5 to
-        # 9.8 us, C = 32 from 12.2 to 11.4 us, C = 16 rises from 11.4 to 14 us -- its fused kernel already fills the
-        # GPU with single-band work items; profiles/r2_dual_pop1_breakdown.txt).
-        dm = os.environ.get("DTF_DUAL_BWD", "auto")
-        self.dual = (dev.type == "cuda" and not self.split and not cfg.version == 1 and (
-            dm == "1" or (dm == "auto" and len(slots) <= int(os.environ.get("DTF_DUAL_MAX_POP", "2")))))
-        self.dual_cs = frozenset(int(v) for v in os.environ.get("DTF_DUAL_CS", "32,64").split(",") if v) \
-            if dm != "1" else frozenset((16, 32, 64))
-        self.side_reduce = bool(self.side_cs) or self.split
-        # DTF_SIDE_DEFER64: the deferred C = 64 dW slab reduction forked onto the side stream as soon as the last
-        # C = 64 layer is done, overlapping the stage-2 / 1 backward (joined before the optimizer).  Off: the graph's
-        # cross-queue fork / join cost more than the 38 us reduction it hides (pop 1 1.21 -> 1.29 ms, pop 8 3.44 ->
-        # 3.55 ms; profiles/r2_s3_side_defer64_ab.log)
-        self.side64 = (dev.type == "cuda" and not self.split and os.environ.get("DTF_SIDE_DEFER64", "0") == "1")
-        self.side_stream = torch.cuda.Stream(device=dev) if (self.side_reduce or self.side64) else None
+        # Dual backward (small populations, <= DUAL_MAX_POP members): each stride-1 C = 32 / 64 conv's dgrad and wgrad
+        # run as two workgroup roles of ONE launch (conv_bwd_dual_kernel); the layer costs max(dgrad, wgrad) instead
+        # of their sum while the population leaves CUs idle (C = 16 keeps the fused kernel: its single-band work
+        # items already fill the GPU; profiles/r2_dual_pop1_breakdown.txt)
+        self.dual = dev.type == "cuda" and cfg.version == 2 and len(slots) <= DUAL_MAX_POP
         self.launches = []
         self._pending_slab = None  # (slab ptr, reduce table, C, grad offset) of the last fused launch
         self._slab_flip = 0
-        # C = 64 dW slabs reduced together by ONE launch after the backward (instead of 17 small reductions):
-        # every such layer keeps its own slab (DTF_DEFER_C64)
-        self.defer64 = dev.type == "cuda" and os.environ.get("DTF_DEFER_C64", "1") == "1"
+        # C = 64 dW slabs reduced together by ONE launch after the backward (instead of 17 small reductions)
         self._deferred = []
         # standalone wgrad launches (stem, projections, strided convs) write dense per-workgroup dW partials reduced
-        # in one launch after the backward (no contended fp32 atomics; fixed order).  Not with the side-stream split
-        # backward (its wgrads are joined only before the optimizer).
-        self.wslab = (dev.type == "cuda" and not self.split and os.environ.get("DTF_WGRAD_SLAB", "1") == "1")
+        # in one launch after the backward (no contended fp32 atomics; fixed order)
+        self.wslab = dev.type == "cuda"
         self._deferred_dense = []
         self._build()
         assert self._pending_slab is None and not self._deferred and not self._deferred_dense, \
@@ -715,28 +688,6 @@ class _StepPlan:
             self._cnt_stage = PinnedStager(self.e.capacity, torch.float32)
         self._cnt_stage.upload(self.cnt, vals)
 
-    @staticmethod
-    def _fwd_split(cin, n_items):
-        # DTF_FWD_SPLIT64: "auto" (split when fewer than 256 items), "1" always, "0" never (default: the split
-        # measured within run-to-run noise at pop 1/2/8, profiles/r1_s7_fwd_split64_ab.log)
-        mode = os.environ.get("DTF_FWD_SPLIT64", "0")
-        if cin != 64 or mode == "0":
-            return False
-        return mode == "1" or n_items < 256
-
-    def _split_work(self, work):
-        key = ("split", work.data_ptr())
-        w = self._work_cache.get(key)
-        if w is None and self.elastic:
-            per, bands, min_chunk = self._wgen_params[work.data_ptr()]
-            w = self._elastic_table(per, bands, min_chunk, split=True)
-            self._work_cache[key] = w
-        if w is None:
-            w = work.repeat_interleave(2, dim=0).contiguous()
-            w[1::2, 2] = 1
-            self._work_cache[key] = w
-        return w
-
     def _n_wg_iters(self, total_iters, per_wg=4, lo=256, hi=1024):
         """Enough (image, band) iterations per workgroup for the double-buffered pipeline,
         while keeping >= lo workgroups (fill 256 CUs) when the batch allows."""
@@ -752,7 +703,7 @@ class _StepPlan:
     def _head_items(self):
         # deterministic mode: one head workgroup per member (its dense-gradient / statistic atomics are then the
         # only writers)
-        return len(self.slots) if self.be.det else int(os.environ.get("DTF_HEAD_ITEMS", "512"))
+        return len(self.slots) if self.be.det else HEAD_ITEMS
 
     def _work_member(self, target_items=256, min_chunk=1):
         key = ("m", target_items)
@@ -811,8 +762,8 @@ class _StepPlan:
                 break
         assert rows is not None, ("no valid band for conv", ci)
         bands = Ho // rows
-        per_wg = int(os.environ.get("DTF_FWD_ITERS_%d" % c.cout, 4))
-        n_wg = self._n_wg_iters(self.N * bands, per_wg=per_wg, hi=max(1024, self.N * bands // per_wg))
+        n_wg = self._n_wg_iters(self.N * bands, per_wg=FWD_ITERS_PER_WG,
+                                hi=max(1024, self.N * bands // FWD_ITERS_PER_WG))
         work = self._work_iters(bands, n_wg)
         a = self._base_args()
         a.x, a.y, a.res = _p(x), _p(y), _p(res)
@@ -829,17 +780,9 @@ class _StepPlan:
         lds = 1280 + 2 * tsz * 2
         mode = 0 if in_bn is None else 1
         lib = ops.lib()
-        if (c.k == 3 and c.stride == 1 and cin == c.cout and Hi == 512 // cin and rows == 8
-                and stats_bn is not None and os.environ.get("DTF_FWD_S1", "1") == "1"):
+        if c.k == 3 and c.stride == 1 and cin == c.cout and Hi == 512 // cin and rows == 8 and stats_bn is not None:
             # compile-time-geometry kernel of the CIFAR stages (conv_fwd_s1_kernel)
-            if self._fwd_split(cin, work.shape[0]):
-                # C = 64 with few work items (one member: 128 images = 128 items): two workgroups per item,
-                # each computing half of the output channels (work.z), to fill the 256 CUs
-                work = self._split_work(work)
-                a.work = _p(work)
-                mode |= 4
-            else:
-                self._set_uniform(a, work)
+            self._set_uniform(a, work)
             a.cin_real = self._stamp_row("fwd", "fwd_s1 C=%d in=%d res=%d" % (cin, mode, res is not None))  # launch ordinal for DTF_STAMP diagnostic builds (unused otherwise)
             lds = 1280 + 2 * ((rows_in * _wpitch(cin) * _cpad_fwd(cin) + 8 + 63) // 64 * 64) * 2
             self._add(lib.dtf_conv_fwd_s1, ctypes.byref(a), cin, mode, int(res is not None), work.shape[0], lds)
@@ -882,11 +825,11 @@ class _StepPlan:
         self._add(lib.dtf_conv_dgrad, ctypes.byref(a), c.cin, c.cout, S, K, mode, epi, work.shape[0], lds)
         self._keep(a)
 
-    def _trans_multi(self, ca_spec):
-        """Combined stage-transition backward launch (conv_trans_multi_kernel): DTF_TRANS_MULTI (default on) for the
-        3x3 / 2 conv_a of a projection block with 16->32 or 32->64 channels; not with the side-stream split."""
-        return (os.environ.get("DTF_TRANS_MULTI", "1") == "1" and not self.split and ca_spec.stride == 2
-                and ca_spec.k == 3 and (ca_spec.cin, ca_spec.cout) in ((16, 32), (32, 64)))
+    @staticmethod
+    def _trans_multi(ca_spec):
+        """Combined stage-transition backward launch (conv_trans_multi_kernel) for the 3x3 / 2 conv_a of a projection
+        block with 16->32 or 32->64 channels."""
+        return ca_spec.stride == 2 and ca_spec.k == 3 and (ca_spec.cin, ca_spec.cout) in ((16, 32), (32, 64))
 
     def _add_trans_multi(self, grabbed, ca_spec):
         (f_c, args_c), (f_a, args_a), (f_b, args_b) = grabbed
@@ -925,8 +868,7 @@ class _StepPlan:
         # images per workgroup: bound the fp32 atomic traffic of the per-WG partial dW (~12 MB per launch)
         wn = c.cout * c.k * c.k * c.cin
         # bound fp32 atomic traffic (~12 MB / launch) and same-address contention (<= 128 WGs per member)
-        per_member = int(os.environ.get("DTF_WGRAD_WG_PER_MEMBER", "128"))
-        n_wg = max(64, min(per_member * len(self.slots), int(12e6 / (4.0 * wn))))
+        n_wg = max(64, min(WGRAD_WG_PER_MEMBER * len(self.slots), int(12e6 / (4.0 * wn))))
         if self.be.det and not self.wslab:
             n_wg = len(self.slots)  # one workgroup per member: every dW element is added once (fixed order)
         work = self._work_iters(Ho // rows, n_wg)
@@ -952,8 +894,7 @@ class _StepPlan:
             kel = c.cout * c.k * c.k * a.cin_real
             a.slab = _p(self._layer_slab(work.shape[0] * kel))
             self._deferred_dense.append((a.slab, self._slab_table(work), c.off, kel))
-        launch = self._side if self.split else self._add
-        launch(lib.dtf_conv_wgrad, ctypes.byref(a), cin, c.cout, c.stride, c.k, mode_x, mode_dy, work.shape[0], lds)
+        self._add(lib.dtf_conv_wgrad, ctypes.byref(a), cin, c.cout, c.stride, c.k, mode_x, mode_dy, work.shape[0], lds)
         self._keep(a)
 
     def _conv_bwd_fused(self, ci, dy, dz_out, x, mode_dy, dy2=None, dy_bn=None, x_bn=None, res=None, ident_x=False,
@@ -979,10 +920,7 @@ class _StepPlan:
         for t in (dy, dy2, dy3, dy_out, dz_out, x, res):
             assert t is None or tuple(t.shape) == (self.N, H, H, C), (t.shape, C, H)
         bands = H // rows
-        if self.split:
-            return self._conv_bwd_split(ci, c, C, H, rows, bands, dy, dz_out, x, mode_dy, dy2, dy_bn, x_bn, res,
-                                        ident_x, dy3, dy_out)
-        if self.dual and C in self.dual_cs:
+        if self.dual and C in DUAL_CS:
             return self._conv_bwd_dual(ci, c, C, H, rows, bands, dy, dz_out, x, mode_dy, dy2, dy_bn, x_bn, res,
                                        ident_x, dy3, dy_out)
         n_wg = self._fused_nwg(C, bands)
@@ -1004,114 +942,37 @@ class _StepPlan:
             a.st_out = _p(be.st_b(x_bn))
         a.Hi, a.Wi, a.Ho, a.Wo, a.rows = H, H, H, H, rows
         tsz = ((rows + 2) * _wpitch(C) * _cpad(C) + 8 + 63) // 64 * 64
-        raw = C >= 64 or os.environ.get("DTF_RAWX16", "0") == "1"  # must match the build (conv.hip RAWX)
-        sb = C == 16 and mode_dy != 3 and os.environ.get("DTF_FUSED_SB16", "1") == "1"  # must match conv.hip SB
+        raw = C >= 64  # must match conv.hip RAWX
+        sb = C == 16 and mode_dy != 3  # must match conv.hip SB
         nbuf = 2 if sb else 4
         lds = 2304 + (nbuf * tsz + (2 * rows * H * _cpad(C) if raw else 0)) * 2  # dY/X tiles [+ raw-x interiors]
         lib = ops.lib()
-        slab = os.environ.get("DTF_DW_SLAB", "1") == "1"
-        if C == 64 and os.environ.get("DTF_DW_SLAB_C64", "1") != "1":
-            slab = False  # fp32 atomics straight into the gradient row (no reduce launch)
-        side = slab and C in self.side_cs
-        defer = slab and not side and C == 64 and self.defer64
+        # dW partials: per-workgroup slabs.  C = 64: every layer its own slab, all reduced by ONE launch after the
+        # backward; C = 16 / 32: ping-pong slab buffers, each reduced by trailing workgroups of the next launch
         n_red = 0
-        if defer:
-            # own slab, reduced after the backward; the previous launch's pending slab still rides on this launch
-            pend = self._pending_slab
-            if pend is not None and self._piggyback(pend):
-                buf, red, rc, goff = pend
-                a.rslab, a.rtab, a.r_c, a.r_goff = buf, _p(red), rc, goff
-                a.r_nblk = self._reduce_wgs(rc, work.shape[0], red.shape[0])
-                n_red = a.r_nblk * red.shape[0]
-                self._pending_slab = None
-            else:
-                self._flush_slab()
+        pend = self._pending_slab
+        if pend is not None and self._piggyback(pend):
+            buf, red, rc, goff = pend
+            a.rslab, a.rtab, a.r_c, a.r_goff = buf, _p(red), rc, goff
+            a.r_nblk = self._reduce_wgs(rc)
+            n_red = a.r_nblk * red.shape[0]
+            self._pending_slab = None
+        else:
+            self._flush_slab()
+        if C == 64:
             a.slab = _p(self._layer_slab(work.shape[0] * self._slab_elems(C)))
-        elif slab and not side:
-            # ping-pong slab buffers: this launch writes one while its trailing workgroups reduce the other
-            pend = self._pending_slab
-            if pend is not None and self._piggyback(pend):
-                buf, red, rc, goff = pend
-                a.rslab, a.rtab, a.r_c, a.r_goff = buf, _p(red), rc, goff
-                a.r_nblk = self._reduce_wgs(rc, work.shape[0], red.shape[0])
-                n_red = a.r_nblk * red.shape[0]
-                self._pending_slab = None
-            else:
-                self._flush_slab()
+        else:
             a.slab = _p(self._slab(self._slab_floats())[self._slab_flip])
             self._slab_flip ^= 1
-        elif side:
-            # side-stream reductions run concurrently with later layers: every layer needs its own slab region
-            a.slab = _p(self._layer_slab(work.shape[0] * self._slab_elems(C)))
         epi = int(res is not None) | (2 if ident_x else 0)
         a.cin_real = self._stamp_row("fused", "fused C=%d mdy=%d epi=%d" % (C, mode_dy, epi))
         self._add(lib.dtf_conv_bwd_fused, ctypes.byref(a), C, mode_dy, epi, work.shape[0] + n_red, lds)
         self._keep(a)
-        if slab:
-            red = self._slab_table(work)
-            if side:
-                self._add("side", (lib.dtf_dw_slab_reduce, (a.slab, _p(red), red.shape[0], _p(self.e.grads),
-                                                            self.e.Pp, c.off, C)))
-            elif defer:
-                self._deferred.append((a.slab, red, c.off))
-            else:
-                self._pending_slab = (a.slab, red, C, c.off)
-
-    def _conv_bwd_split(self, ci, c, C, H, rows, bands, dy, dz_out, x, mode_dy, dy2, dy_bn, x_bn, res, ident_x, dy3,
-                        dy_out):
-        """Split backward of a stride-1 C->C conv: dgrad role on the main stream (one (image, band) item per
-        workgroup: the most workgroups a latency-bound small population can use), wgrad role on the side stream
-        reading the materialised dY (``dy`` itself, or the dgrad launch's ``xout``) and writing per-layer dW slabs
-        that a side-stream reduction adds into the gradient row."""
-        be, L = self.be, self.be.L
-        lib = ops.lib()
-        tsz = ((rows + 2) * _wpitch(C) * _cpad(C) + 8 + 63) // 64 * 64
-        epi = int(res is not None) | (2 if ident_x else 0)
-        # ---- dgrad role
-        nd = int(os.environ.get("DTF_SPLIT_DG_ITERS", "1"))
-        work = self._work_iters(bands, max(1, (self.N * bands) // nd))
-        a = self._base_args()
-        dmat = dy
-        if mode_dy >= 2:
-            dmat = dy_out if dy_out is not None else self._fresh_like(dz_out)
-        a.x, a.x2, a.y, a.xm, a.res = _p(dy), _p(dy2), _p(dz_out), _p(x), _p(res)
-        a.x3, a.xout = _p(dy3), _p(dmat if mode_dy >= 2 else None)
-        a.w, a.w_off = _p(be.wd), L.dgr_off[ci]
-        a.work = _p(work)
-        a.g_off = c.off
-        a.n_main = work.shape[0]
-        self._set_uniform(a, work)
-        if dy_bn is not None:
-            a.in_gamma, a.in_beta = self._bn(dy_bn)
-            a.st_in, a.st_in_b = _p(be.st_f(dy_bn)), _p(be.st_b(dy_bn))
-        if not ident_x:
-            a.ep_gamma, a.ep_beta = self._bn(x_bn)
-            a.st_ep = _p(be.st_f(x_bn))
-            a.st_out = _p(be.st_b(x_bn))
-        a.Hi, a.Wi, a.Ho, a.Wo, a.rows = H, H, H, H, rows
-        a.cin_real = self._stamp_row("fused", "dgrad C=%d mdy=%d epi=%d" % (C, mode_dy, epi))
-        self._keep(a)
-        self._add(lib.dtf_conv_bwd_role, ctypes.byref(a), C, mode_dy, epi, 1, work.shape[0], 2304 + 2 * tsz * 2)
-        # ---- wgrad role (side stream)
-        per = int(os.environ.get("DTF_SPLIT_WG_%d" % C, {16: "128", 32: "128", 64: "64"}[C]))
-        wwork = self._work_iters(bands, max(1, min(self.N * bands, per * len(self.slots))))
-        b = self._base_args()
-        b.x, b.xm = _p(dmat), _p(x)
-        b.work = _p(wwork)
-        b.g_off = c.off
-        b.n_main = wwork.shape[0]
-        self._set_uniform(b, wwork)
-        if not ident_x:
-            b.ep_gamma, b.ep_beta = self._bn(x_bn)
-            b.st_ep = _p(be.st_f(x_bn))
-        b.Hi, b.Wi, b.Ho, b.Wo, b.rows = H, H, H, H, rows
-        b.slab = _p(self._layer_slab(wwork.shape[0] * self._slab_elems(C)))
-        b.cin_real = -1
-        self._keep(b)
-        red = self._slab_table(wwork)
-        self._side(lib.dtf_conv_bwd_role, ctypes.byref(b), C, 0, 2 if ident_x else 0, 2, wwork.shape[0],
-                   2304 + 4 * tsz * 2)
-        self._side(lib.dtf_dw_slab_reduce, b.slab, _p(red), red.shape[0], _p(self.e.grads), self.e.Pp, c.off, C)
+        red = self._slab_table(work)
+        if C == 64:
+            self._deferred.append((a.slab, red, c.off))
+        else:
+            self._pending_slab = (a.slab, red, C, c.off)
 
     def _conv_bwd_dual(self, ci, c, C, H, rows, bands, dy, dz_out, x, mode_dy, dy2, dy_bn, x_bn, res, ident_x, dy3,
                        dy_out):
@@ -1123,9 +984,8 @@ class _StepPlan:
         lib = ops.lib()
         tsz = ((rows + 2) * _wpitch(C) * _cpad(C) + 8 + 63) // 64 * 64
         epi = int(res is not None) | (2 if ident_x else 0)
-        # ---- dgrad role
-        nd = int(os.environ.get("DTF_DUAL_DG_ITERS", "1"))
-        work = self._work_iters(bands, self._det_cap(max(1, (self.N * bands) // nd)))
+        # ---- dgrad role: one (image, band) iteration per workgroup
+        work = self._work_iters(bands, self._det_cap(max(1, self.N * bands)))
         a = self._base_args()
         a.x, a.x2, a.y, a.xm, a.res = _p(dy), _p(dy2), _p(dz_out), _p(x), _p(res)
         a.x3, a.xout = _p(dy3), _p(dy_out if mode_dy >= 2 else None)
@@ -1144,8 +1004,7 @@ class _StepPlan:
         a.Hi, a.Wi, a.Ho, a.Wo, a.rows = H, H, H, H, rows
         a.cin_real = self._stamp_row("fused", "fused-dg C=%d mdy=%d epi=%d" % (C, mode_dy, epi))
         # ---- wgrad role (same staging of dY / X; own work split)
-        per = int(os.environ.get("DTF_DUAL_WG_%d" % C, {16: "128", 32: "128", 64: "64"}[C]))
-        wwork = self._work_iters(bands, max(1, min(self.N * bands, per * len(self.slots))))
+        wwork = self._work_iters(bands, max(1, min(self.N * bands, DUAL_WG[C] * len(self.slots))))
         b = self._base_args()
         b.x, b.x2, b.x3, b.xm = _p(dy), _p(dy2), _p(dy3), _p(x)
         b.work = _p(wwork)
@@ -1167,7 +1026,7 @@ class _StepPlan:
         if pend is not None and self._piggyback(pend):
             buf, red, rc, goff = pend
             a.rslab, a.rtab, a.r_c, a.r_goff = buf, _p(red), rc, goff
-            a.r_nblk = self._reduce_wgs(rc, a.n_main + b.n_main, red.shape[0])
+            a.r_nblk = self._reduce_wgs(rc)
             n_red = a.r_nblk * red.shape[0]
             self._pending_slab = None
         else:
@@ -1177,45 +1036,27 @@ class _StepPlan:
         lds = 2304 + 4 * tsz * 2  # the wgrad role's dY + X tiles (double-buffered); the dgrad role uses half
         self._add(lib.dtf_conv_bwd_dual, ctypes.byref(a), ctypes.byref(b), C, mode_dy, epi,
                   a.n_main + b.n_main + n_red, lds)
-        if C == 64 and self.defer64:
+        if C == 64:
             self._deferred.append((b.slab, self._slab_table(wwork), c.off))
         else:
             self._pending_slab = (b.slab, self._slab_table(wwork), C, c.off)
 
     def _piggyback(self, pend):
-        """Reduce the previous launch's slabs inside the next fused launch when that adds few workgroups
-        (the trailing workgroups carry the fused kernel's register budget: low occupancy)."""
-        if os.environ.get("DTF_SLAB_PIGGYBACK", "1") != "1":
-            return False
+        """Reduce the previous launch's C = 16 / 32 slabs inside the next backward launch when that adds few
+        workgroups (the trailing workgroups carry the fused kernel's register budget: low occupancy).  C = 64 slabs
+        are deferred to one launch after the backward (a looping piggyback reduction measured slower:
+        profiles/r2_piggyback_c64_ab.log)."""
         _, red, rc, _ = pend
-        limit = int(os.environ.get("DTF_PIGGYBACK_MAX_WG", "3000"))
-        if rc == 64:
-            # C = 64: looping reduce workgroups that fill the carrier's last partial wave of CUs (_reduce_wgs).
-            # Off: measured slower (pop 1 1.39 -> 1.58 ms, pop 8 3.70 -> 4.30 ms; profiles/r2_piggyback_c64_ab.log):
-            # a looping workgroup's strided slab reads are latency-bound; one workgroup per 32 slab elements (1152
-            # per member) was also slower (pop 1: +0.1 ms)
-            return os.environ.get("DTF_PIGGYBACK_C64", "0") == "1"
-        return (self._slab_elems(rc) // 32) * red.shape[0] <= limit
+        return rc != 64 and (self._slab_elems(rc) // 32) * red.shape[0] <= PIGGYBACK_MAX_WG
 
-    def _reduce_wgs(self, rc, n_main, n_members):
-        """Reduce workgroups per member of a piggybacked slab reduction.  C = 16 / 32: one per 32 slab elements.
-        C = 64: as many as the CUs the carrier leaves idle in its last wave (>= 64 in total), each looping over
-        its share of the 1152 element blocks -- at one member the 128 carrier workgroups of a C = 64 layer
-        occupy half the GPU, the reduction runs on the other half."""
-        nb = self._slab_elems(rc) // 32
-        if rc != 64:
-            return nb
-        per_wave = int(os.environ.get("DTF_PIGGYBACK_WAVE", "256"))
-        t = -(-n_main // per_wave) * per_wave - n_main
-        if t < 64:
-            t += per_wave
-        t = int(os.environ.get("DTF_PIGGYBACK_C64_WGS", t))
-        return max(1, min(nb, t // max(1, n_members)))
+    def _reduce_wgs(self, rc):
+        """Reduce workgroups per member of a piggybacked slab reduction: one per 32 slab elements."""
+        return self._slab_elems(rc) // 32
 
-    def _flush_deferred(self, side=False):
+    def _flush_deferred(self):
         """One reduction launch over every deferred C = 64 slab (dw_slab_reduce_multi_kernel) and one over every
-        dense wgrad slab (dense_slab_reduce_multi_kernel).  ``side``: only the C = 64 slabs, on the side stream."""
-        if self._deferred_dense and not side:
+        dense wgrad slab (dense_slab_reduce_multi_kernel)."""
+        if self._deferred_dense:
             jobs = (DenseJob * len(self._deferred_dense))()
             nmax = bmax = 0
             for i, (buf, red, goff, kel) in enumerate(self._deferred_dense):
@@ -1225,7 +1066,7 @@ class _StepPlan:
             jt = torch.frombuffer(bytearray(bytes(jobs)), dtype=torch.uint8).to(self.be.dev)
             self._keep(jt)
             self._add(ops.lib().dtf_dense_slab_reduce_multi, _p(jt), len(self._deferred_dense), nmax,
-                      min(bmax, int(os.environ.get("DTF_DENSE_REDUCE_BLOCKS", "256"))), _p(self.e.grads), self.e.Pp)
+                      min(bmax, DENSE_REDUCE_BLOCKS), _p(self.e.grads), self.e.Pp)
             self._deferred_dense = []
         if not self._deferred:
             return
@@ -1236,8 +1077,8 @@ class _StepPlan:
             nmax = max(nmax, red.shape[0])
         jt = torch.frombuffer(bytearray(bytes(jobs)), dtype=torch.uint8).to(self.be.dev)
         self._keep(jt)
-        (self._side if side else self._add)(ops.lib().dtf_dw_slab_reduce_multi, _p(jt), len(self._deferred), nmax,
-                                            _p(self.e.grads), self.e.Pp, 64)
+        self._add(ops.lib().dtf_dw_slab_reduce_multi, _p(jt), len(self._deferred), nmax, _p(self.e.grads), self.e.Pp,
+                  64)
         self._deferred = []
 
     def _flush_slab(self):
@@ -1257,16 +1098,14 @@ class _StepPlan:
         # per-launch budget for the dW partials (bytes of slab stores, or of atomics without slabs): bounds the
         # workgroup count of the fused kernel
         wn = 9 * C * C
-        budget = float(os.environ.get("DTF_FUSED_ATOMIC_BYTES_%d" % C, {64: 48e6}.get(C, 16e6)))
-        n_wg = max(64, min(128 * len(self.slots), int(budget / (4.0 * wn))))
+        n_wg = max(64, min(128 * len(self.slots), int(FUSED_SLAB_BYTES[C] / (4.0 * wn))))
         # floor of 256 workgroups: a single member would otherwise run the C = 16 / 32 layers on 128 of the 256
         # CUs (pop 1: 1.54 -> 1.50 ms/step; larger populations already exceed it)
-        n_wg = max(n_wg, int(os.environ.get("DTF_FUSED_MIN_WG_%d" % C, os.environ.get("DTF_FUSED_MIN_WG", "256"))))
+        n_wg = max(n_wg, FUSED_MIN_WG)
         # per-member cap: fewer, fuller workgroups write fewer dW slab bytes.  C = 32 at 128 per member (2 bands
         # each): pop 1 1.52 -> 1.44-1.47 ms/step over two runs (profiles/r1_s7_variants.log); pop >= 2 unchanged
-        cap = int(os.environ.get("DTF_FUSED_MAX_WG_%d" % C, {32: "128"}.get(C, "0")))
-        if cap > 0:
-            n_wg = min(n_wg, cap * len(self.slots))
+        if C in FUSED_MAX_WG:
+            n_wg = min(n_wg, FUSED_MAX_WG[C] * len(self.slots))
         return self._det_cap(min(n_wg, self.N * bands))
 
     def _slab_floats(self):
@@ -1327,31 +1166,6 @@ class _StepPlan:
         self.stamp_rows = getattr(self, "stamp_rows", []) + [(row, label)]
         return row
 
-    def _tmp_for(self, hw):
-        """Backward temporaries at resolution ``hw``: the plan's shared ping-pong set, or (split mode) a fresh
-        lazily allocated set that no later layer overwrites."""
-        if not self.split:
-            return self.tmp[hw]
-        plan = self
-        proto = self.tmp[hw]
-
-        class _Fresh(dict):
-            def __missing__(self, key):
-                ref = proto[key]
-                v = [plan._fresh_like(t) for t in ref] if isinstance(ref, list) else plan._fresh_like(ref)
-                self[key] = v
-                return v
-        return _Fresh()
-
-    def _fresh_like(self, t):
-        u = torch.empty_like(t)
-        self._keep(u)
-        return u
-
-    def _side(self, fn, *args):
-        """Launch on the side stream (forked after everything queued so far on the main stream)."""
-        self._add("side", (fn, args))
-
     def _keep(self, obj):
         if not hasattr(self, "_keepalive"):
             self._keepalive = []
@@ -1399,35 +1213,25 @@ class _StepPlan:
         self._add(lib.dtf_head_bwd_apply, _p(self.xs[-1]), _p(self.dfeat), _p(g_cur), _p(self.img_slot), _p(e.state),
                   e.S, ha.gamma_off, ha.beta_off, _p(be.st_f(fb)), _p(be.st_b(fb)), _p(self.cnt), hw,
                   cfg.final_size, N)
-        fused = os.environ.get("DTF_FUSED_BWD", "1") == "1"
-        fold = fused and os.environ.get("DTF_FOLD_BNBWD", "1") == "1"
         pend = None  # deferred BN1-backward of the block just processed: (dz1, x, add, out, bn1)
-        side64 = self.side64 and self.side_stream is not None
         for i in range(nblk - 1, -1, -1):
             blk = prog.blocks[i]
             bn1, bn2 = blk.bns
             x, h = self.xs[i], self.hs[i]
             Hi, Ho = x.shape[1], h.shape[1]
-            T = self._tmp_for(Ho)
+            T = self.tmp[Ho]
             ca, cb = blk.convs
-            if side64 and self._deferred and prog.convs[cb].cout < 64:
-                # every C = 64 layer's dW slab is complete: reduce them on the side stream while the stage-2 / 1
-                # backward (which leaves CUs idle at small populations) runs; joined before the optimizer
-                self._flush_deferred(side=True)
             # conv_b: dgrad -> dz2 (mask by BN2(h), BN2 reductions); wgrad
-            if fused and pend is not None:
+            if pend is not None:
                 # the previous block's g = BN1-backward(dz1, x) [+ g] is computed while staging conv_b's dY
                 # and written out once (band interiors) for the projection / next BN-backward
                 dz1p, xp, addp, outp, bn1p = pend
                 self._conv_bwd_fused(cb, dz1p, T["dz2"], h, mode_dy=3 if addp is not None else 2, dy2=xp,
                                      dy3=addp, dy_out=outp, dy_bn=bn1p, x_bn=bn2)
                 g_cur, pend = outp, None
-            elif fused:
-                self._conv_bwd_fused(cb, g_cur, T["dz2"], h, mode_dy=0, x_bn=bn2)
             else:
-                self._conv_dgrad(cb, g_cur, T["dz2"], Ho, mode=0, epi=2, xm=h, ep_bn=bn2)
-                self._conv_wgrad(cb, h, g_cur, mode_x=1, mode_dy=0, x_bn=bn2)
-            Tin = self._tmp_for(Hi) if Hi != Ho else T
+                self._conv_bwd_fused(cb, g_cur, T["dz2"], h, mode_dy=0, x_bn=bn2)
+            Tin = self.tmp[Hi] if Hi != Ho else T
             pd = None
             ca_spec = prog.convs[ca]
             if blk.proj is not None and self._trans_multi(ca_spec):
@@ -1448,7 +1252,7 @@ class _StepPlan:
             # conv_a: dgrad of BN2-backward(dz2, h) [+ proj dgrad], mask by BN1(x), BN1 reductions
             if blk.proj is not None and self._trans_multi(ca_spec):
                 pass  # conv_a done above
-            elif fused and ca_spec.stride == 1 and ca_spec.cin == ca_spec.cout:
+            elif ca_spec.stride == 1 and ca_spec.cin == ca_spec.cout:
                 self._conv_bwd_fused(ca, T["dz2"], Tin["dz1"], x, mode_dy=2, dy2=h, dy_bn=bn2, x_bn=bn1, res=pd)
             else:
                 self._conv_dgrad(ca, T["dz2"], Tin["dz1"], Hi, mode=2, epi=2 | (1 if pd is not None else 0), dy2=h,
@@ -1457,7 +1261,7 @@ class _StepPlan:
             # g_in = BN1-backward(dz1, x) [+ g_out if identity shortcut]
             g_next = Tin["g"][1] if g_cur is Tin["g"][0] else Tin["g"][0]
             add = None if blk.proj is not None else g_cur
-            if fold and i > 0:
+            if i > 0:
                 pend = (Tin["dz1"], x, add, g_next, bn1)
             else:
                 self._bn_bwd_apply(Tin["dz1"], x, add, g_next, bn1)
@@ -1536,7 +1340,7 @@ class _StepPlan:
             self._forward_v1()
         else:
             self._forward_v2()
-        hwork = self._work_member(target_items=int(os.environ.get("DTF_HEAD_ITEMS", "512")))
+        hwork = self._work_member(target_items=HEAD_ITEMS)
         ha = HeadArgs()
         ha.x, ha.labels, ha.work = _p(self.xs[-1]), _p(self.labels), _p(hwork)
         ha.params, ha.p_mstride = _p(e.state), e.S
@@ -1573,12 +1377,9 @@ class _StepPlan:
         self.labels.view(k, m).copy_(y.reshape(1, m).expand(k, -1))
 
     def _zero_args(self):
-        """(buffer, n) zeroed by weight_prep; DTF_ZERO_IN_PREP=0 keeps a separate fill launch instead."""
+        """(buffer, n) zeroed by weight_prep: the statistic accumulators, losses and correct counts."""
         be = self.be
-        if os.environ.get("DTF_ZERO_IN_PREP", "1") == "1":
-            return _p(be.zbuf), be.zbuf.numel()
-        self._add("zero", be.zbuf)
-        return None, 0
+        return _p(be.zbuf), be.zbuf.numel()
 
     def _bn_bwd_apply(self, dz, x, add, out, bn):
         """out = BN-backward(dz, x) [+ add] (bn_bwd_apply_kernel)."""
@@ -1635,7 +1436,7 @@ class _StepPlan:
         self._forward_v1()
         # head: GAP + dense + CE on the last block output (no final BN: gamma_off = -1)
         hw = L.final_hw
-        hwork = self._work_member(target_items=int(os.environ.get("DTF_HEAD_ITEMS", "512")))
+        hwork = self._work_member(target_items=HEAD_ITEMS)
         ha_ = HeadArgs()
         ha_.x, ha_.labels, ha_.work = _p(self.xs[-1]), _p(self.labels), _p(hwork)
         ha_.params, ha_.p_mstride = _p(e.state), e.S
@@ -1713,24 +1514,8 @@ class _StepPlan:
 
     def _run_eager(self):
         e = self.e
-        main = torch.cuda.current_stream()
-        side = self.side_stream
-        forked = False
         for fn, args in self.launches:
-            if fn == "side":
-                kfn, kargs = args[0]
-                side.wait_stream(main)  # fork: the producing kernel has been enqueued on main
-                err = kfn(*kargs, ctypes.c_void_p(side.cuda_stream))
-                if err != 0:
-                    raise RuntimeError("side-stream launch failed with %d" % err)
-                forked = True
-                continue
-            if fn == "optim" and forked:
-                main.wait_stream(side)  # join before the optimizer reads the gradients
-                forked = False
-            if fn == "zero":
-                args[0].zero_()
-            elif fn == "augment":
+            if fn == "augment":
                 ops.augment_cifar(self.src.train_x, self.src.train_y, self.idx, self.rng, True, out16=self.xin16,
                                   lab32=self.labels)
             elif fn == "optim":
@@ -1751,7 +1536,7 @@ class _StepPlan:
 
     def run(self, train=True):
         be = self.be
-        if be.use_graph and self.graph is None and (os.environ.get("DTF_HIP_GRAPH", "1") == "1" and os.environ.get("DTF_DEBUG", "0") != "1"):
+        if be.use_graph and self.graph is None:
             # warm up once eagerly (allocator, lazy init), then capture
             self._run_eager()
             torch.cuda.synchronize()

@@ -26,25 +26,9 @@
 #include "common.h"
 
 #define BN_EPS 1e-5f
-#ifndef DTF_FUSED_WAVES
-#define DTF_FUSED_WAVES(C, M) ((C) <= 16 && (M) != 3 && DTF_FUSED_SB16 ? 3 : (C) <= 32 ? 2 : 1)  // min waves / SIMD the fused bwd kernel is register-capped for
-#endif
-#ifndef DTF_CPAD_OLD
-#define DTF_CPAD_OLD 0  // 1: the previous uniform C + 8 LDS pixel pitch (A/B builds)
-#endif
-#ifndef DTF_SLAB_STORE
-#define DTF_SLAB_STORE 2  // dW slab store form: 0 plain, 1 nontemporal, 2 write-through (sc1) buffer stores
-#endif
+// min waves / SIMD the fused backward kernel is register-capped for (C = 16 single-buffered: 3 WGs / CU)
+#define FUSED_WAVES(C, M) ((C) <= 16 && (M) != 3 ? 3 : (C) <= 32 ? 2 : 1)
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-#ifndef DTF_FUSED_SB16
-#define DTF_FUSED_SB16 1  // C = 16 fused bwd (MODE_DY != 3): single-buffered LDS tiles, 3 WGs / CU instead of 2
-#endif
-#ifndef DTF_RAWX16
-#define DTF_RAWX16 0
-#endif
-#ifndef DTF_ABL
-#define DTF_ABL 0  // timing-only ablation bits of conv_bwd_fused_kernel (tools/ablate.sh); 0 in real builds
-#endif
 #define NREP DTF_NREP
 #ifndef DTF_STAMP
 #define DTF_STAMP 0  // diagnostic build (tools/stamps.py): per-workgroup s_memrealtime stamps of the fwd_s1 / fused bwd
@@ -135,6 +119,24 @@ __device__ __forceinline__ int4 work_item_at(const ConvArgs& a, int b) {
 
 __device__ __forceinline__ int4 work_item(const ConvArgs& a) { return work_item_at(a, (int)blockIdx.x); }
 
+// Kernel-argument prologue.  A launch of these latency-bound layers is a chain of dependent memory round trips, and
+// hipcc places each kernarg s_load right before its first use -- behind branches and behind the previous
+// s_waitcnt -- so a kernel paid 4-6 sequential scalar round trips before its first tile load.  kpin() forces a
+// value into SGPRs at the point of the call: calling it for every field the prologue needs, straight after entry,
+// issues all their s_loads as one batch behind ONE lgkmcnt wait.
+template <typename T>
+__device__ __forceinline__ void kpin(T& v) {
+  asm volatile("" : "+s"(v));
+}
+// Pointers are pinned as global-address-space pointers and cast back, so the loads through them stay global_ /
+// s_load (not flat_) instructions.
+template <typename T>
+__device__ __forceinline__ void kpin(T*& p) {
+  auto g = (__attribute__((address_space(1))) T*)p;
+  asm volatile("" : "+s"(g));
+  p = (T*)g;
+}
+
 __device__ __forceinline__ const float* stats_row(const float* base, int slot) {
   return base + (long)slot * NREP * 128;
 }
@@ -181,14 +183,10 @@ __device__ __forceinline__ void bn_bwd_coef(const float* stf, const float* stb, 
 // function of the pixel index (no swizzle arithmetic in the inner loops).
 template <int C>
 __host__ __device__ constexpr int cpad() {
-#if DTF_CPAD_OLD
-  return C + 8;
-#else
   // pixel pitch in bf16: chosen with the gfx950 LDS lane-group banking of ds_read_b128 (4 x 16 lanes) /
   // ds_read_b64_tr_b16 / ds_write_b128 for the tiles' access patterns (tools/lds_banks.py): 16 -> no pad,
   // 32 -> +16, 64 -> +16 (the uniform +8 pad left 2-3-way conflicts on the MFMA operand gathers)
   return C == 16 ? 16 : C == 32 ? 48 : C == 64 ? 80 : C + 8;
-#endif
 }
 
 // LDS row pitch (pixels) of the stage kernels' [RT][WP][CP] tiles (conv_fwd_s1, fused / dual backward).  C = 64
@@ -196,19 +194,16 @@ __host__ __device__ constexpr int cpad() {
 // in disjoint bank halves of the ds_read_b128 lane groups (4 instead of 8 cycles per gather, tools/lds_banks.py;
 // the extra 6 columns are never staged).  Measured: no step-time change at pop 1 / pop 8 (these kernels wait on
 // global memory, not LDS; profiles/r2_wp64_ab.log), so the dense pitch (10) stays the default.
-#ifndef DTF_WP64
-#define DTF_WP64 10
-#endif
 template <int C>
 __host__ __device__ constexpr int wpitch() {
-  return C == 64 ? DTF_WP64 : 512 / C + 2;
+  return 512 / C + 2;
 }
 
 // Forward (conv_fwd_s1) pitch: the C = 16 forward measured faster with the +8 pad (1 vs 3 MFMA-operand
 // gathers per row pair, different occupancy) -- the fused backward keeps the unpadded pitch.
 template <int C>
 __host__ __device__ constexpr int cpad_fwd() {
-  return (C == 16 && !DTF_CPAD_OLD) ? 24 : cpad<C>();
+  return C == 16 ? 24 : cpad<C>();
 }
 
 template <int C>
@@ -420,11 +415,13 @@ struct CoefLd {
 };
 
 template <int C, int MODE>
-__device__ __forceinline__ void coef_issue(CoefLd<MODE>& L, const ConvArgs& a, int slot, const float* st_f,
-                                           const float* st_b, int g_off, int b_off) {
+__device__ __forceinline__ void coef_issue(CoefLd<MODE>& L, const float* params, long p_mstride, int slot,
+                                           const float* st_f, const float* st_b, int g_off, int b_off) {
   if constexpr (MODE == 0) return;
-  const int c = threadIdx.x;
-  if (c < C) {
+  // branch-free: every thread loads (channel threadIdx % C; the copies hit the same lines), so no exec-mask branch
+  // makes the compiler consume -- and wait for -- the first statistics before the tile loads are issued
+  const int c = (int)threadIdx.x & (C - 1);
+  {
     const float* rf = stats_row(st_f, slot) + c;
     if constexpr (CREP == NREP) {
 #pragma unroll
@@ -455,7 +452,7 @@ __device__ __forceinline__ void coef_issue(CoefLd<MODE>& L, const ConvArgs& a, i
         }
       }
     }
-    const float* prow = a.params + (long)slot * a.p_mstride;
+    const float* prow = params + (long)slot * p_mstride;
     L.g = prow[g_off + c];
     if constexpr (MODE == 1) L.b = prow[b_off + c];
   }
@@ -838,12 +835,11 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
 // Stride-1 3x3 C->C forward of the CIFAR stages (and the stem, C = 16 padded input) with compile-time
 // geometry (W = H = 512/C, 8-row bands), uniform-base + 32-bit lane offsets and packed epilogue math
 // (same scheme as conv_bwd_fused_kernel).
-// SPLIT = 2: the output channels are split over two workgroups per work item (work.z = which half), so a
 // single member's 8x8 C = 64 layer (one image per item) launches 256 workgroups instead of 128.
-template <int C, int MODE_IN, bool RESID, int SPLIT = 1>
+template <int C, int MODE_IN, bool RESID>
 __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
   constexpr int W = 512 / C, H = W, ROWS = 8, BANDS = H / ROWS;
-  constexpr int NT = C / 16 / SPLIT, WPT = 4 / NT;  // NT: output-channel tiles of this workgroup
+  constexpr int NT = C / 16, WPT = 4 / NT;  // NT: output-channel tiles
   constexpr int KTOT = 9 * C, KS = (KTOT + 31) / 32;
   constexpr int CP = cpad_fwd<C>(), RT = ROWS + 2, WP = wpitch<C>();
   constexpr int TSZ = (RT * WP * CP + 8 + 63) & ~63;  // + slack for inactive staging slots
@@ -861,15 +857,31 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
 #define SBUF(i) (tile0 + ((i) & 1) * TSZ)
   STAMP_DECL
   STAMP(0);
-  const int4 wk = work_item(a);
+  // every kernarg field of the prologue in one s_load batch (kpin)
+  int u_items = a.u_items, u_chunk = a.u_chunk, u_per = a.u_per, in_gamma = a.in_gamma, in_beta = a.in_beta;
+  const int4* work = a.work;
+  const float *params = a.params, *st_in = a.st_in, *cnt = a.cnt;
+  long p_mstride = a.p_mstride, w_mstride = a.w_mstride, w_off = a.w_off;
+  const bf16_t *xin = a.x, *wgt = a.w, *res = a.res;
+  kpin(u_items), kpin(u_chunk), kpin(u_per), kpin(in_gamma), kpin(in_beta), kpin(work), kpin(params), kpin(st_in);
+  kpin(cnt), kpin(p_mstride), kpin(w_mstride), kpin(w_off), kpin(xin), kpin(wgt), kpin(res);
+  int4 wk;
+  if (u_items > 0) {
+    const int b = (int)blockIdx.x, m = b / u_items, k = b - m * u_items, it0_ = k * u_chunk;
+    wk = make_int4(m * u_per + it0_, min(u_chunk, u_per - it0_), 0, m);
+  } else {
+    wk = work[blockIdx.x];
+    wk = make_int4(__builtin_amdgcn_readfirstlane(wk.x), __builtin_amdgcn_readfirstlane(wk.y),
+                   __builtin_amdgcn_readfirstlane(wk.z), __builtin_amdgcn_readfirstlane(wk.w));  // uniform (SGPRs)
+  }
   DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
   const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int ct = wave % NT + (SPLIT > 1 ? wk.z * NT : 0);
+  const int ct = wave % NT;
   // prologue loads in the order they are consumed: BN statistics -> input tile -> weights
   CoefLd<MODE_IN == 0 ? 0 : 1> cl;
-  coef_issue<C, MODE_IN == 0 ? 0 : 1>(cl, a, slot, a.st_in, a.st_in_b, a.in_gamma, a.in_beta);
-  const float n_in = a.cnt[slot] * (float)(H * W);
+  coef_issue<C, MODE_IN == 0 ? 0 : 1>(cl, params, p_mstride, slot, st_in, nullptr, in_gamma, in_beta);
+  const float n_in = cnt[slot] * (float)(H * W);
   St st;
   st.init();
   uint4 tv[MAXC], unused[MAXC];
@@ -877,11 +889,11 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
   {
     const int img = it0 / BANDS, gy0 = (it0 % BANDS) * ROWS - 1;
     tm = st.mask(gy0);
-    st.template load<LMODE>(tv, unused, tm, a.x + img * IMG, nullptr, gy0);
+    st.template load<LMODE>(tv, unused, tm, xin + img * IMG, nullptr, gy0);
   }
   bf16x8_t afr[KS];
   {
-    const bf16_t* wb = a.w + (long)slot * a.w_mstride + a.w_off + (long)(ct * 16 + (lane & 15)) * KTOT;
+    const bf16_t* wb = wgt + (long)slot * w_mstride + w_off + (long)(ct * 16 + (lane & 15)) * KTOT;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int k0 = 32 * s + 8 * (lane >> 4);
@@ -914,7 +926,7 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
   if constexpr (RESID) {
     const long band0 = (long)(it0 / BANDS) * IMG + (it0 % BANDS) * ROWS * ROW;
 #pragma unroll
-    for (int i = 0; i < MT; ++i) nres[i] = *reinterpret_cast<const uint2*>(a.res + band0 + pofs[i]);
+    for (int i = 0; i < MT; ++i) nres[i] = *reinterpret_cast<const uint2*>(res + band0 + pofs[i]);
   }
   __syncthreads();  // coefficients
   STAMP(1);
@@ -1442,9 +1454,9 @@ __device__ __forceinline__ void slab_reduce_wg(const float* __restrict__ slab, c
 // a 32-bit lane offset fixed for the workgroup, and the elementwise work uses
 // packed fp32 / bf16 math: the VALU budget per MFMA is what bounds these
 // small-channel layers.
-// ROLE (split backward of small populations, engine/hip_resnet.py DTF_SPLIT_BWD): 0 = dgrad + wgrad (fused),
+// ROLE (dual backward of small populations, conv_bwd_dual_kernel): 0 = dgrad + wgrad (fused),
 // 1 = dgrad only (critical path: no X tile, no wgrad; the transformed dY may be materialised via xout for the
-// wgrad), 2 = wgrad only (runs on a side stream beside the next layers' dgrads; no dgrad / stats / xout).
+// wgrad), 2 = wgrad only (the wgrad role of a dual launch; no dgrad / stats / xout).
 // Body of one workgroup; `bid` = the workgroup's index within its role (work item, stats replica, dW slab row).
 template <int C, int MODE_DY, int EPI, int ROLE>
 __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, char* smem) {
@@ -1470,19 +1482,59 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
   float* acc_lds = ecoef + 256;                    // 128
   bf16_t* t0 = reinterpret_cast<bf16_t*>(smem + 2304);
   // SB: single-buffered tiles (one extra barrier per iteration) so that C = 16 fits 3 workgroups per CU in LDS
-  constexpr bool SB = C == 16 && MODE_DY != 3 && DTF_FUSED_SB16 && ROLE == 0;
+  constexpr bool SB = C == 16 && MODE_DY != 3 && ROLE == 0;
   constexpr int BSTR = WG ? 2 * TSZ : TSZ;  // dgrad-only: dY tiles only
 #define FDBUF(i) (t0 + (SB ? 0 : ((i) & 1) * BSTR))
 #define FXBUF(i) (t0 + TSZ + (SB ? 0 : ((i) & 1) * BSTR))
   // raw (untransformed) x of the band interior, for the dgrad epilogue's mask / x-hat: read from LDS instead of
   // re-reading x from global memory (double-buffered like the tiles)
-  // (C <= 32 keeps the global re-read unless built with DTF_RAWX16: the extra LDS would cost its 2nd WG per CU)
-  constexpr bool RAWX = ROLE == 0 && (C >= 64 || DTF_RAWX16);
+  // (C <= 32 keeps the global re-read: the extra LDS would cost its 2nd WG per CU)
+  constexpr bool RAWX = ROLE == 0 && C >= 64;
   constexpr int RAWSZ = ROWS * W * CP;
 #define FXRAW(i) (t0 + 4 * TSZ + ((i) & 1) * RAWSZ)
   STAMP_DECL
   STAMP(0);
-  const int4 wk = work_item_at(a, bid);
+  // every kernarg field of the body in one s_load batch (kpin): one scalar round trip before the first load
+  const bf16_t* k_x = a.x;
+  const bf16_t* k_x2 = a.x2;
+  const bf16_t* k_x3 = a.x3;
+  const bf16_t* k_xm = a.xm;
+  const bf16_t* k_w = a.w;
+  const bf16_t* k_res = a.res;
+  bf16_t* k_xout = a.xout;
+  bf16_t* k_y = a.y;
+  const float* k_st_in = a.st_in;
+  const float* k_st_in_b = a.st_in_b;
+  const float* k_st_ep = a.st_ep;
+  const float* k_params = a.params;
+  const float* k_cnt = a.cnt;
+  float* k_st_out = a.st_out;
+  float* k_slab = a.slab;
+  float* k_grads = a.grads;
+  const int4* k_work = a.work;
+  long k_w_mstride = a.w_mstride;
+  long k_w_off = a.w_off;
+  int k_in_gamma = a.in_gamma;
+  int k_in_beta = a.in_beta;
+  int k_ep_gamma = a.ep_gamma;
+  int k_ep_beta = a.ep_beta;
+  long k_p_mstride = a.p_mstride;
+  long k_g_mstride = a.g_mstride;
+  long k_g_off = a.g_off;
+  int k_u_items = a.u_items;
+  int k_u_chunk = a.u_chunk;
+  int k_u_per = a.u_per;
+  kpin(k_x); kpin(k_x2); kpin(k_x3); kpin(k_xm); kpin(k_w); kpin(k_res); kpin(k_xout); kpin(k_y); kpin(k_st_in); kpin(k_st_in_b); kpin(k_st_ep); kpin(k_params); kpin(k_cnt); kpin(k_st_out); kpin(k_slab); kpin(k_grads); kpin(k_work);
+  kpin(k_w_mstride); kpin(k_w_off); kpin(k_in_gamma); kpin(k_in_beta); kpin(k_ep_gamma); kpin(k_ep_beta); kpin(k_p_mstride); kpin(k_g_mstride); kpin(k_g_off); kpin(k_u_items); kpin(k_u_chunk); kpin(k_u_per);
+  int4 wk;
+  if (k_u_items > 0) {
+    const int m = bid / k_u_items, kk = bid - m * k_u_items, it0_ = kk * k_u_chunk;
+    wk = make_int4(m * k_u_per + it0_, min(k_u_chunk, k_u_per - it0_), 0, m);
+  } else {
+    wk = k_work[bid];
+    wk = make_int4(__builtin_amdgcn_readfirstlane(wk.x), __builtin_amdgcn_readfirstlane(wk.y),
+                   __builtin_amdgcn_readfirstlane(wk.z), __builtin_amdgcn_readfirstlane(wk.w));  // uniform (SGPRs)
+  }
   DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
   const int it0 = wk.x, nit = wk.y, slot = wk.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1490,10 +1542,11 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
   STAMP_FINE(8);
   // prologue loads in the order they are consumed: BN statistics (dY transform, x BN) -> tiles -> weights
   CoefLd<MODE_DY == 0 ? 0 : 2> cld;
-  coef_issue<C, MODE_DY == 0 ? 0 : 2>(cld, a, slot, a.st_in, a.st_in_b, a.in_gamma, a.in_beta);
+  coef_issue<C, MODE_DY == 0 ? 0 : 2>(cld, k_params, k_p_mstride, slot, k_st_in, k_st_in_b, k_in_gamma, k_in_beta);
   CoefLd<1> cle;
-  if constexpr (!(EPI & 2)) coef_issue<C, 1>(cle, a, slot, a.st_ep, nullptr, a.ep_gamma, a.ep_beta);
-  const float n_hw = a.cnt[slot] * (float)(H * W);
+  if constexpr (!(EPI & 2))
+    coef_issue<C, 1>(cle, k_params, k_p_mstride, slot, k_st_ep, nullptr, k_ep_gamma, k_ep_beta);
+  const float n_hw = k_cnt[slot] * (float)(H * W);
   STAMP_FINE(9);
   St st;
   st.init();
@@ -1504,14 +1557,14 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
   int cimg = it0 / BANDS, cgy0 = (it0 % BANDS) * ROWS - 1;  // image / first tile row of the staged tile
   {
     dm = xm = st.mask(cgy0);
-    st.template load<MODE_DY == 3 ? 2 : MODE_DY>(dv, dv2, dm, a.x + cimg * IMG, a.x2 + cimg * IMG, cgy0);
-    if constexpr (MODE_DY == 3) st.template load<0>(dv3, unused, dm, a.x3 + cimg * IMG, nullptr, cgy0);
-    if constexpr (WG) st.template load<1>(xv_, unused, xm, a.xm + cimg * IMG, nullptr, cgy0);
+    st.template load<MODE_DY == 3 ? 2 : MODE_DY>(dv, dv2, dm, k_x + cimg * IMG, k_x2 + cimg * IMG, cgy0);
+    if constexpr (MODE_DY == 3) st.template load<0>(dv3, unused, dm, k_x3 + cimg * IMG, nullptr, cgy0);
+    if constexpr (WG) st.template load<1>(xv_, unused, xm, k_xm + cimg * IMG, nullptr, cgy0);
   }
   STAMP_FINE(10);
   bf16x8_t afr[KS];
   if constexpr (DG) {
-    const bf16_t* wb = a.w + (long)slot * a.w_mstride + a.w_off + (long)(ct * 16 + (lane & 15)) * KTOT;
+    const bf16_t* wb = k_w + (long)slot * k_w_mstride + k_w_off + (long)(ct * 16 + (lane & 15)) * KTOT;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int k0 = 32 * s + 8 * (lane >> 4);
@@ -1583,8 +1636,8 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
     const long b_ = (long)(it_ / BANDS) * IMG + (it_ % BANDS) * ROWS * ROW;
 #pragma unroll
     for (int i = 0; i < MAXT; ++i) {
-      if constexpr (EPI & 1) nres[i] = *reinterpret_cast<const uint2*>(a.res + b_ + pofs[i]);
-      if constexpr (!RAWX) nxres[i] = *reinterpret_cast<const uint2*>(a.xm + b_ + pofs[i]);
+      if constexpr (EPI & 1) nres[i] = *reinterpret_cast<const uint2*>(k_res + b_ + pofs[i]);
+      if constexpr (!RAWX) nxres[i] = *reinterpret_cast<const uint2*>(k_xm + b_ + pofs[i]);
     }
   };
   if constexpr (DG) epi_load(it0);
@@ -1593,7 +1646,7 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
   STAMP(1);
   if constexpr (XSTORE)  // (the wgrad role stages the same transform but never writes xout)
     st.template store_x<MODE_DY == 3 ? 3 : 2>(FDBUF(0), dv, dv2, dv3, dm, coef_d,
-                                              (DG && a.xout) ? a.xout + cimg * IMG : nullptr, cgy0);
+                                              (DG && k_xout) ? k_xout + cimg * IMG : nullptr, cgy0);
   else
     st.template store<MODE_DY>(FDBUF(0), dv, dv2, dm, coef_d);
   if constexpr (WG) st.template store<1>(FXBUF(0), xv_, unused, xm, ecoef);
@@ -1621,9 +1674,9 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
       cimg = (it + 1) / BANDS;
       cgy0 = ((it + 1) % BANDS) * ROWS - 1;
       dm = xm = st.mask(cgy0);
-      st.template load<MODE_DY == 3 ? 2 : MODE_DY>(dv, dv2, dm, a.x + cimg * IMG, a.x2 + cimg * IMG, cgy0);
-      if constexpr (MODE_DY == 3) st.template load<0>(dv3, unused, dm, a.x3 + cimg * IMG, nullptr, cgy0);
-      if constexpr (WG) st.template load<1>(xv_, unused, xm, a.xm + cimg * IMG, nullptr, cgy0);
+      st.template load<MODE_DY == 3 ? 2 : MODE_DY>(dv, dv2, dm, k_x + cimg * IMG, k_x2 + cimg * IMG, cgy0);
+      if constexpr (MODE_DY == 3) st.template load<0>(dv3, unused, dm, k_x3 + cimg * IMG, nullptr, cgy0);
+      if constexpr (WG) st.template load<1>(xv_, unused, xm, k_xm + cimg * IMG, nullptr, cgy0);
       if constexpr (DG) epi_load(it + 1);
     }
     const bf16_t* dcur = FDBUF(k);
@@ -1633,7 +1686,7 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
     const f32x2_t sh0 = lds2(ecoef + 64 + ci0), sh1 = lds2(ecoef + 64 + ci0 + 2);
     const f32x2_t nm0 = lds2(ecoef + 128 + ci0), nm1 = lds2(ecoef + 128 + ci0 + 2);
     const f32x2_t iv0 = lds2(ecoef + 192 + ci0), iv1 = lds2(ecoef + 192 + ci0 + 2);
-    if constexpr (DG && !(DTF_ABL & 4)) {  // timing-only ablation builds (tools/ablate.sh): skip the dgrad
+    if constexpr (DG) {
 #pragma unroll
     for (int i = 0; i < MAXT; ++i) {
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
@@ -1654,16 +1707,16 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
       uint2 pk;
       pk.x = pk2(v0);
       pk.y = pk2(v1);
-      *reinterpret_cast<uint2*>(a.y + band + pofs[i]) = pk;
+      *reinterpret_cast<uint2*>(k_y + band + pofs[i]) = pk;
       const f32x2_t dz0 = unpk2(pk.x), dz1 = unpk2(pk.y);
       ssum[0] += dz0;
       ssum[1] += dz1;
       ssq[0] += dz0 * (x0 * iv0 + nm0);
       ssq[1] += dz1 * (x1 * iv1 + nm1);
     }
-    }  // DTF_ABL & 4
+    }
     // ---- wgrad
-    if constexpr (WG && !(DTF_ABL & 2)) {  // ablation: skip the wgrad
+    if constexpr (WG) {
 #pragma unroll
     for (int ks = 0; ks < NK; ++ks) {
       bf16x8_t af[MT];
@@ -1685,12 +1738,12 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
 #pragma unroll
         for (int m = 0; m < MT; ++m) wacc[j][m] = mfma16(af[m], bfr[j], wacc[j][m]);
     }
-    }  // DTF_ABL & 2
+    }
     if (more) {
       if constexpr (SB) __syncthreads();  // every wave is done with the current tiles
       if constexpr (XSTORE)
         st.template store_x<MODE_DY == 3 ? 3 : 2>(FDBUF(k + 1), dv, dv2, dv3, dm, coef_d,
-                                                  (DG && a.xout) ? a.xout + cimg * IMG : nullptr, cgy0);
+                                                  (DG && k_xout) ? k_xout + cimg * IMG : nullptr, cgy0);
       else
         st.template store<MODE_DY>(FDBUF(k + 1), dv, dv2, dm, coef_d);
       if constexpr (WG) st.template store<1>(FXBUF(k + 1), xv_, unused, xm, ecoef);
@@ -1708,21 +1761,20 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
     reduce_stats_to_lds(acc_lds, s4, q4, ci0, lane);
     __syncthreads();
   }
-  if constexpr (DG && !(EPI & 2)) flush_stats_r(a.st_out, acc_lds, slot, C, bid);
+  if constexpr (DG && !(EPI & 2)) flush_stats_r(k_st_out, acc_lds, slot, C, bid);
   STAMP(4);
   if constexpr (!WG) {
     STAMP_DRAIN(5);
     STAMP_FLUSH(a.cin_real, nit);
     return;
   }
-  if (a.slab) {
+  if (k_slab) {
     // partial-sum slab [wg][j][m][256 threads][4]: one 16-byte store per lane per accumulator tile (a 1 KB
     // row per wave instruction; the store tail is issue-bound); dw_slab_reduce sums a member's slabs
-    f32x4_t* sb = reinterpret_cast<f32x4_t*>(a.slab + (long)bid * (NJ * MT * 4 * 256)) + threadIdx.x;
-    if constexpr (!(DTF_ABL & 1)) {
-#if DTF_SLAB_STORE == 2
+    f32x4_t* sb = reinterpret_cast<f32x4_t*>(k_slab + (long)bid * (NJ * MT * 4 * 256)) + threadIdx.x;
+    {
       // write-through (sc1) buffer stores: the slab does not sit dirty in L2 at the kernel boundary
-      const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(a.slab + (long)bid * (NJ * MT * 4 * 256), 0,
+      const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(k_slab + (long)bid * (NJ * MT * 4 * 256), 0,
                                                          NJ * MT * 4 * 256 * 4, 0x00020000);
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
@@ -1730,24 +1782,12 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
         for (int m = 0; m < MT; ++m)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, wacc[j][m]), rsrc,
                                                  (((j * MT + m) * 256) + (int)threadIdx.x) * 16, 0, 16);
-#else
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int m = 0; m < MT; ++m) {
-#if DTF_SLAB_STORE == 1
-          __builtin_nontemporal_store(wacc[j][m], &sb[(j * MT + m) * 256]);
-#else
-          sb[(j * MT + m) * 256] = wacc[j][m];
-#endif
-        }
-#endif
     }
     STAMP_DRAIN(5);
     STAMP_FLUSH(a.cin_real, nit);
     return;
   }
-  float* gb = a.grads + (long)slot * a.g_mstride + a.g_off;
+  float* gb = k_grads + (long)slot * k_g_mstride + k_g_off;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int nt = wave + 4 * j;
@@ -1777,14 +1817,14 @@ __device__ __forceinline__ void trailing_reduce(const ConvArgs& a, int r, char* 
   else if (a.r_c == 64) slab_reduce_wg<64>(a.rslab, a.rtab, a.grads, a.g_mstride, a.r_goff, bx, by, part, a.r_nblk);
 }
 
-template <int C, int MODE_DY, int EPI, int ROLE = 0>
-__global__ __launch_bounds__(256, ROLE == 1 ? 2 : DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_fused_kernel(ConvArgs a) {
+template <int C, int MODE_DY, int EPI>
+__global__ __launch_bounds__(256, FUSED_WAVES(C, MODE_DY)) void conv_bwd_fused_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if ((int)blockIdx.x >= a.n_main) {
     trailing_reduce(a, (int)blockIdx.x - a.n_main, smem);
     return;
   }
-  conv_bwd_body<C, MODE_DY, EPI, ROLE>(a, (int)blockIdx.x, smem);
+  conv_bwd_body<C, MODE_DY, EPI, 0>(a, (int)blockIdx.x, smem);
 }
 
 // Dual backward (small populations, engine/hip_resnet.py DTF_DUAL_BWD): ONE launch whose workgroups take
@@ -1794,12 +1834,14 @@ __global__ __launch_bounds__(256, ROLE == 1 ? 2 : DTF_FUSED_WAVES(C, MODE_DY)) v
 // launch (a.r_*).  The two roles run side by side on different CUs, so the layer costs max(dgrad, wgrad) instead
 // of their sum while a small population leaves most CUs idle.
 template <int C, int MODE_DY, int EPI>
-__global__ __launch_bounds__(256, DTF_FUSED_WAVES(C, MODE_DY)) void conv_bwd_dual_kernel(ConvArgs a, ConvArgs b) {
+__global__ __launch_bounds__(256, FUSED_WAVES(C, MODE_DY)) void conv_bwd_dual_kernel(ConvArgs a, ConvArgs b) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int bx = (int)blockIdx.x;
-  if (bx < a.n_main) {
+  int na = a.n_main, nb = b.n_main;
+  kpin(na), kpin(nb);  // both role bounds in one scalar round trip
+  if (bx < na) {
     conv_bwd_body<C, MODE_DY, EPI, 1>(a, bx, smem);
-  } else if (bx < a.n_main + b.n_main) {
+  } else if (bx < na + nb) {
     conv_bwd_body<C, MODE_DY, EPI & 2, 2>(b, bx - a.n_main, smem);
   } else {
     trailing_reduce(a, bx - a.n_main - b.n_main, smem);
@@ -1916,14 +1958,6 @@ DTF_API int dtf_conv_fwd_s1(const ConvArgs* args, int c, int mode, int resid, in
   S1_CASE(64, 1, false)
   S1_CASE(64, 1, true)
 #undef S1_CASE
-  // mode bit 2: output channels split over two workgroups per work item (C = 64)
-#define S1_SPLIT_CASE(CC, M, R)                   \
-  if (c == CC && mode == (M | 4) && resid == R) \
-    return launch(conv_fwd_s1_kernel<CC, M, R, 2>, nblocks, lds, stream, *args);
-  S1_SPLIT_CASE(64, 0, false)
-  S1_SPLIT_CASE(64, 1, false)
-  S1_SPLIT_CASE(64, 1, true)
-#undef S1_SPLIT_CASE
   return -1;
 }
 
@@ -2086,24 +2120,6 @@ DTF_API int dtf_conv_bwd_fused(const ConvArgs* args, int c, int mode_dy, int epi
   FUSED_CASE(16, 2, 3)  // v1 conv_a: identity-BN block input (+ shortcut grad)
   FUSED_CASE(32, 2, 3)
   FUSED_CASE(64, 2, 3)
-  return -1;
-}
-
-// Split backward roles (ROLE 1 dgrad / ROLE 2 wgrad of conv_bwd_fused_kernel).
-DTF_API int dtf_conv_bwd_role(const ConvArgs* args, int c, int mode_dy, int epi, int role, int nblocks, int lds,
-                              hipStream_t stream) {
-#define ROLE_CASE(CC, M, E, R)                                      \
-  if (c == CC && mode_dy == M && epi == E && role == R)            \
-    return launch(conv_bwd_fused_kernel<CC, M, E, R>, nblocks, lds, stream, *args);
-  ROLE_CASE(16, 0, 0, 1) ROLE_CASE(32, 0, 0, 1) ROLE_CASE(64, 0, 0, 1)
-  ROLE_CASE(16, 3, 0, 1) ROLE_CASE(32, 3, 0, 1) ROLE_CASE(64, 3, 0, 1)
-  ROLE_CASE(16, 2, 0, 1) ROLE_CASE(32, 2, 0, 1) ROLE_CASE(64, 2, 0, 1)
-  ROLE_CASE(16, 2, 1, 1)
-  ROLE_CASE(16, 2, 3, 1) ROLE_CASE(32, 2, 3, 1) ROLE_CASE(64, 2, 3, 1)
-  // wgrad role: dY is always a materialised tensor (MODE 0); EPI bit 1 = identity-BN x (v1)
-  ROLE_CASE(16, 0, 0, 2) ROLE_CASE(32, 0, 0, 2) ROLE_CASE(64, 0, 0, 2)
-  ROLE_CASE(16, 0, 2, 2) ROLE_CASE(32, 0, 2, 2) ROLE_CASE(64, 0, 2, 2)
-#undef ROLE_CASE
   return -1;
 }
 

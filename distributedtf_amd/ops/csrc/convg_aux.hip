@@ -168,8 +168,8 @@ __device__ __forceinline__ int chan8(long i, int C) {
   return (C & (C - 1)) == 0 ? (e & (C - 1)) : e % C;
 }
 
-// 16-byte output store; NT: non-temporal (DTF_EW_NT=1; measured 86.7 vs 86.9 ms per ResNet-50 step, so off: the
-// next conv reads the output right away, partly from the caches; profiles/r2_s3_imagenet_ew_nt_ab.log)
+// 16-byte output store; NT: non-temporal (measured 86.7 vs 86.9 ms per ResNet-50 step, so the launchers use plain
+// stores: the next conv reads the output right away, partly from the caches; profiles/r2_s3_imagenet_ew_nt_ab.log)
 template <bool NT>
 __device__ __forceinline__ void ew_store(bf16_t* p, uint4 v) {
   if constexpr (NT) {
@@ -581,11 +581,7 @@ DTF_API int dtf_cg_bn_bwd_apply(const EwArgs* a, hipStream_t stream) {
   const long ms = (n8 + 255) / 256;
   if (split > ms) split = ms;
   if (split < 1) split = 1;
-  static const bool nt = getenv("DTF_EW_NT") != nullptr && atoi(getenv("DTF_EW_NT")) != 0;
-  if (nt)
-    hipLaunchKernelGGL(cg_bn_bwd_apply_kernel<true>, dim3((unsigned)a->nimg, (unsigned)split), dim3(256), 0, stream, *a);
-  else
-    hipLaunchKernelGGL(cg_bn_bwd_apply_kernel<false>, dim3((unsigned)a->nimg, (unsigned)split), dim3(256), 0, stream, *a);
+  hipLaunchKernelGGL(cg_bn_bwd_apply_kernel<false>, dim3((unsigned)a->nimg, (unsigned)split), dim3(256), 0, stream, *a);
   return DTF_CHECK_LAUNCH();
 }
 
@@ -596,11 +592,7 @@ DTF_API int dtf_cg_bn_relu_apply(const EwArgs* a, hipStream_t stream) {
   const long ms = (n8 + 255) / 256;
   if (split > ms) split = ms;
   if (split < 1) split = 1;
-  static const bool nt = getenv("DTF_EW_NT") != nullptr && atoi(getenv("DTF_EW_NT")) != 0;
-  if (nt)
-    hipLaunchKernelGGL(cg_bn_relu_apply_kernel<true>, dim3((unsigned)a->nimg, (unsigned)split), dim3(256), 0, stream, *a);
-  else
-    hipLaunchKernelGGL(cg_bn_relu_apply_kernel<false>, dim3((unsigned)a->nimg, (unsigned)split), dim3(256), 0, stream, *a);
+  hipLaunchKernelGGL(cg_bn_relu_apply_kernel<false>, dim3((unsigned)a->nimg, (unsigned)split), dim3(256), 0, stream, *a);
   return DTF_CHECK_LAUNCH();
 }
 

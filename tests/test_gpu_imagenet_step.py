@@ -25,12 +25,16 @@ def _relerr(a, b):
     return float((a - b).norm() / (b.norm() + 1e-30))
 
 
-def test_hip_imagenet_step_matches_reference(monkeypatch):
-    monkeypatch.setenv("DTF_HIP_GRAPH", "1")
+@pytest.mark.parametrize("image,sizes,graph", [(64, (4, 6), "1"), (64, (4, 6), "0"), (224, (16, 16), "1")])
+def test_hip_imagenet_step_matches_reference(monkeypatch, image, sizes, graph):
+    """Step 1 (lr 0) is the eager warm-up that captures the graph; step 2 (lr 1) is the first graph REPLAY (graph
+    "1") or a second eager run ("0") -- its parameter delta is compared.  224 x 224 at 2 x 16 runs the benchmark's
+    tile / split-K choices."""
+    monkeypatch.setenv("DTF_HIP_GRAPH", graph)
     torch.manual_seed(0)
-    arch = ResNetArch(imagenet_config(50, 2, num_classes=1001, image_size=64))
+    arch = ResNetArch(imagenet_config(50, 2, num_classes=1001, image_size=image))
     dev = torch.device("cuda")
-    sizes = [4, 6]
+    sizes = list(sizes)
     ref = PopulationEngine(arch, 2, dev, backend="torch", compute_dtype=torch.float32, optimizer_impl="hip")
     r16 = PopulationEngine(arch, 2, dev, backend="torch", compute_dtype=torch.bfloat16, optimizer_impl="hip")
     hip = PopulationEngine(arch, 2, dev, backend="hip")
@@ -48,10 +52,16 @@ def test_hip_imagenet_step_matches_reference(monkeypatch):
         for st in (ref.state, hip.state, r16.state):
             st[:, b.gamma_off:b.gamma_off + b.c] = ng.to(dev)
             st[:, b.beta_off:b.beta_off + b.c] = nb.to(dev)
-    batches = [(torch.randn(bs, 64, 64, 3, generator=g).to(dev), torch.randint(0, 1001, (bs,), generator=g).to(dev))
-               for bs in sizes]
+    batches = [(torch.randn(bs, image, image, 3, generator=g).to(dev),
+                torch.randint(0, 1001, (bs,), generator=g).to(dev)) for bs in sizes]
     before = hip.params.clone()
     hps = [_hp(bs) for bs in sizes]
+    for e in (ref, r16, hip):
+        e.train_step(slots, batches, hps, [0.0, 0.0])
+    torch.cuda.synchronize()
+    assert torch.equal(hip.params, before)
+    plan = next(iter(hip.backend._plans.values()))
+    assert (plan.graph is not None) == (graph == "1")
     l_ref = ref.train_step(slots, batches, hps, [1.0, 1.0])
     r16.train_step(slots, batches, hps, [1.0, 1.0])
     l_hip = hip.train_step(slots, batches, hps, [1.0, 1.0])

@@ -100,6 +100,13 @@ def test_hip_mnist_step_matches_reference(graph, monkeypatch):
     batches = [((torch.rand(bs, 28, 28, 1, generator=g) * 255.0).to(dev), torch.randint(0, 10, (bs,), generator=g).to(dev))
                for bs in sizes]
     before = hip.params.clone()
+    # step 1 (lr 0): the eager warm-up that also captures the step graph; step 2 (lr 1): with DTF_HIP_GRAPH=1 the
+    # first graph REPLAY (device-side step advance, hyper table, dropout counter), else a second eager run
+    hip.train_step(slots, batches, [_hp(bs) for bs in sizes], [0.0, 0.0])
+    torch.cuda.synchronize()
+    assert torch.equal(hip.params, before)
+    plan = next(iter(hip.backend._plans.values()))
+    assert (plan.graph is not None) == (graph == "1")
     losses = hip.train_step(slots, batches, [_hp(bs) for bs in sizes], [1.0, 1.0])
     torch.cuda.synchronize()
     seed, ctr = hip.backend.last_rng

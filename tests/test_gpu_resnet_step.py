@@ -109,32 +109,16 @@ def _compare_step(arch, sizes, floor=0.06, seed=0, warm_sizes=None, check=None):
     return max(r[3] for r in report)
 
 
-@pytest.mark.parametrize("size,graph,fused,version,fold,split", [
-    (8, "1", "1", 2, "1", "0"), (14, "1", "1", 2, "1", "0"), (14, "0", "1", 2, "1", "0"),
-    (14, "1", "1", 2, "0", "0"), (14, "1", "0", 2, "1", "0"), (8, "0", "0", 2, "1", "0"),
-    (8, "1", "1", 1, "1", "0"), (14, "0", "1", 1, "1", "0"), (20, "1", "1", 1, "1", "0"),
-    (14, "1", "1", 2, "1", "1"), (20, "0", "1", 2, "1", "1")])
-def test_hip_step_matches_reference(size, graph, fused, version, fold, split, monkeypatch):
-    """fold=1: BN1-backward folded into the next conv_b staging + dW slab reductions carried by the next fused
-    launch (hip_resnet._conv_bwd_fused); fold=0: standalone bn_bwd_apply / dw_slab_reduce launches;
-    split=1: dgrad on the main stream, wgrad on a side stream (small-population mode)."""
+@pytest.mark.parametrize("size,graph,version,sizes", [
+    (8, "1", 2, [8, 12, 6]), (14, "1", 2, [8, 12, 6]), (14, "0", 2, [8, 12, 6]),
+    (14, "1", 2, [8, 12]), (20, "0", 2, [8, 12]), (14, "1", 2, [16]),
+    (8, "1", 1, [8, 12]), (14, "0", 1, [8, 12]), (20, "1", 1, [8, 12])])
+def test_hip_step_matches_reference(size, graph, version, sizes, monkeypatch):
+    """Three members: the fused backward launches (BN1-backward folded into the next conv_b staging, dW slab
+    reductions carried by the next launch); one or two members: the dual backward (dgrad and wgrad roles of one
+    launch, conv_bwd_dual_kernel) -- with and without graphs, ragged and single-member populations, v2 and v1."""
     monkeypatch.setenv("DTF_HIP_GRAPH", graph)
-    monkeypatch.setenv("DTF_FUSED_BWD", fused)
-    monkeypatch.setenv("DTF_FOLD_BNBWD", fold)
-    monkeypatch.setenv("DTF_SLAB_PIGGYBACK", fold)
-    monkeypatch.setenv("DTF_SPLIT_BWD", split)
-    _compare_step(ResNetArch(cifar_config(size, version=version)), [8, 12])
-
-
-@pytest.mark.parametrize("size,graph,dual,sizes", [(14, "1", "1", [8, 12]), (20, "0", "1", [8, 12]),
-                                                   (14, "1", "1", [16]), (8, "1", "0", [16])])
-def test_hip_step_dual_backward(size, graph, dual, sizes, monkeypatch):
-    """Dual backward (dgrad and wgrad roles of one launch, conv_bwd_dual_kernel; the default for populations of
-    <= 2 members) vs the fp32 oracle, with and without graphs, ragged and single-member populations."""
-    monkeypatch.setenv("DTF_HIP_GRAPH", graph)
-    monkeypatch.setenv("DTF_DUAL_BWD", dual)
-    monkeypatch.setenv("DTF_SPLIT_BWD", "0")
-    _compare_step(ResNetArch(cifar_config(size, version=2)), sizes)
+    _compare_step(ResNetArch(cifar_config(size, version=version)), sizes)
 
 
 @pytest.mark.parametrize("elastic", ["auto", "0"])
@@ -159,14 +143,12 @@ def test_hip_step_elastic_plan(elastic, monkeypatch):
     _compare_step(ResNetArch(cifar_config(14, version=2)), [12, 17, 6], warm_sizes=[20, 9, 14], check=check)
 
 
-@pytest.mark.parametrize("size,sizes,split", [(56, [128] * 8, "0"), (56, [128], "auto"), (56, [128], "0"),
-                                              (110, [128, 128], "auto")])
-def test_hip_step_benchmark_shapes(size, sizes, split, monkeypatch):
+@pytest.mark.parametrize("size,sizes", [(56, [128] * 8), (56, [128]), (110, [128, 128])])
+def test_hip_step_benchmark_shapes(size, sizes, monkeypatch):
     """The shapes bench.py times (ResNet-56 v2 at pop 8 x 128 and pop 1 x 128; ResNet-110 at pop 2 x 128): the
     workgroup splits, dW slab budgets and piggyback reductions chosen there (hip_resnet._fused_nwg) and the
-    small-population split backward are checked numerically, on the graph-replayed step."""
+    small-population dual backward are checked numerically, on the graph-replayed step."""
     monkeypatch.setenv("DTF_HIP_GRAPH", "1")
-    monkeypatch.setenv("DTF_SPLIT_BWD", split)
     worst = _compare_step(ResNetArch(cifar_config(size, version=2)), sizes, floor=0.04)
     print("worst per-layer relative error %.4f" % worst)
 

@@ -32,7 +32,7 @@ import torch
 
 from .. import ops
 from ..data.datasets import IndexBatch, batch_len
-from .hip_resnet import PinnedStager, advance_steps, note_step_advanced, same_batches, upload_hyper
+from .hip_resnet import PinnedStager, advance_steps, note_step_advanced, run_captured, same_batches, upload_hyper
 
 c_void_p, c_int, c_long, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float
 
@@ -405,21 +405,4 @@ class _MnistPlan:
         advance_steps(e, self.slots_long, self.slots_t, be.loss, self.loss_sel)
 
     def run(self):
-        be = self.be
-        if be.use_graph and self.graph is None:
-            self._run_eager()
-            torch.cuda.synchronize()
-            g = torch.cuda.CUDAGraph()
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                g.capture_begin()
-                self._run_eager()
-                g.capture_end()
-            torch.cuda.current_stream().wait_stream(s)
-            self.graph = g
-            return
-        if self.graph is not None:
-            self.graph.replay()
-        else:
-            self._run_eager()
+        run_captured(self)

@@ -332,6 +332,44 @@ def advance_steps(e, slots_long, slots_i32=None, loss=None, loss_sel=None):
         torch.index_select(loss, 0, slots_long, out=loss_sel)
 
 
+def run_captured(plan) -> None:
+    """Run one step of ``plan``: the first call executes it eagerly (allocator / lazy init warm-up) and then
+    captures the launch list into a HIP graph; later calls replay the graph.  A data-parallel step captures its
+    RCCL gradient all-reduce with the rest of the step; if this RCCL build refuses a collective inside a capture,
+    the plan falls back to eager launches (the warm-up already ran this step)."""
+    be = plan.be
+    if be.use_graph and plan.graph is None and not getattr(plan, "_no_graph", False):
+        plan._run_eager()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        ok = False
+        try:
+            with torch.cuda.stream(s):
+                g.capture_begin()
+                try:
+                    plan._run_eager()
+                finally:
+                    g.capture_end()
+            ok = True
+        except RuntimeError as err:
+            if plan.e.dp is None:
+                raise
+            import warnings
+            warnings.warn("step graph capture with the data-parallel all-reduce failed (%s): eager launches" % err)
+            torch.cuda.synchronize()
+            plan._no_graph = True
+        torch.cuda.current_stream().wait_stream(s)
+        if ok:
+            plan.graph = g
+        return
+    if plan.graph is not None:
+        plan.graph.replay()
+    else:
+        plan._run_eager()
+
+
 def same_batches(plan, batches) -> bool:
     """True if ``batches`` are the very (x, y) storages staged last step and unmodified since (tensor version
     counters); a reference to them is held so their memory cannot be recycled into a different batch."""
@@ -390,20 +428,34 @@ class HipResNetBackend:
     # --- plans ------------------------------------------------------------------------
     accepts_index_batches = True
 
-    def _elastic_cap(self, sizes):
+    def _elastic_cap(self, sizes, force=False):
         """Per-member capacity of an elastic plan for these batch sizes, or None for an exact plan.  Mixed batch
         sizes (PBT samples and perturbs them, constants.py:91-93) run on one capacity-keyed plan whose work tables
-        are regenerated on the device every step (DTF_ELASTIC: "auto" = mixed sizes only, "1", "0")."""
+        are regenerated on the device every step (DTF_ELASTIC: "auto" = mixed sizes only (or ``force``: a
+        shrinking active set), "1", "0")."""
         mode = os.environ.get("DTF_ELASTIC", "auto")
         cap = int(os.environ.get("DTF_ELASTIC_MAXB", "256"))
         if (mode == "0" or self.dev.type != "cuda" or self.L.cfg.version == 1 or self.e.dp is not None
-                or max(sizes) > cap or (mode == "auto" and len(set(sizes)) == 1)):
+                or max(sizes) > cap or (mode == "auto" and len(set(sizes)) == 1 and not force)):
             return None
         return cap
 
     def plan(self, slots: Sequence[int], sizes: Sequence[int], src=None) -> "_StepPlan":
+        """The step plan (buffers + captured graph) for this batch composition.  Elastic plans are keyed on the
+        capacity and the member set; a step of a SUBSET of an elastic plan's members (members that finished their
+        epoch drop out of the active set: engine_model._train_cycle) replays that plan with zero images for the
+        others -- their optimizer rows are inactive (hyper table), their step counters and BN moving statistics do
+        not move (step_advance / bn_running_update) -- instead of building and capturing a new plan."""
+        src_id = id(src) if src is not None else None
+        shrink = self._covering_plan(slots, sizes, src_id)
+        if shrink is not None:
+            by = dict(zip(slots, sizes))
+            shrink.set_sizes([by.get(s, 0) for s in shrink.slots])
+            return shrink
         cap = self._elastic_cap(sizes) if sizes else None
-        key = (tuple(slots), ("elastic", cap) if cap else tuple(sizes), id(src) if src is not None else None)
+        if cap is None and self._subset_of_known(slots, src_id):
+            cap = self._elastic_cap(sizes, force=True)  # a shrinking active set: go elastic once, reuse after
+        key = (tuple(slots), ("elastic", cap) if cap else tuple(sizes), src_id)
         p = self._plans.get(key)
         if p is None:
             if len(self._plans) > 16:
@@ -413,6 +465,19 @@ class HipResNetBackend:
         if cap:
             p.set_sizes(list(sizes))
         return p
+
+    def _covering_plan(self, slots, sizes, src_id):
+        """An elastic plan whose members strictly include ``slots`` (and whose capacity fits ``sizes``)."""
+        want = set(slots)
+        for key, p in self._plans.items():
+            if (p.elastic and key[2] == src_id and want < set(p.slots) and sizes
+                    and max(sizes) <= p.sizes[0]):
+                return p
+        return None
+
+    def _subset_of_known(self, slots, src_id):
+        want = set(slots)
+        return any(key[2] == src_id and want < set(key[0]) for key in self._plans)
 
     def train_step(self, slots, batches, hparams, lrs):
         e = self.e
@@ -425,9 +490,15 @@ class HipResNetBackend:
         sizes = [batch_len(b) for b in batches]
         p = self.plan(slots, sizes, src)
         upload_hyper(e, slots, hparams, lrs)
-        p.load_batch(batches)
+        if list(p.slots) != list(slots):  # a subset of an elastic plan's members (idle members: no images)
+            by = dict(zip(slots, batches))
+            p.load_batch([by[s] for s in p.slots if s in by], slots=list(slots))
+        else:
+            p.load_batch(batches)
         p.run(train=True)
         note_step_advanced(e, slots)
+        if list(p.slots) != list(slots):
+            return p.loss_view()[p.slot_index(slots)]
         return p.loss_view()
 
     def forward_backward(self, slots, batches):
@@ -1495,19 +1566,30 @@ class _StepPlan:
         self._add("step", None)
 
     # -------------------------------------------------------------------- execution
-    def load_batch(self, batches):
+    def slot_index(self, slots):
+        """Positions of ``slots`` in this plan's member list (device tensor, cached)."""
+        key = tuple(slots)
+        cache = self.__dict__.setdefault("_slot_index", {})
+        if key not in cache:
+            pos = {s: i for i, s in enumerate(self.slots)}
+            cache[key] = torch.tensor([pos[s] for s in slots], dtype=torch.long, device=self.be.dev)
+        return cache[key]
+
+    def load_batch(self, batches, slots=None):
+        """Stage the members' batches (``slots``: the members they belong to, default every plan member)."""
+        slots = list(self.slots) if slots is None else [s for s in self.slots if s in set(slots)]
         # member regions start at self.first[slot] (packed for exact plans, capacity-strided for elastic ones)
         if self.src is None and same_batches(self, batches):
             return  # the staged copy is still current (same unmodified source storage)
         if self.src is not None:
-            for s, b in zip(self.slots, batches):
+            for s, b in zip(slots, batches):
                 n, off = len(b), self.first[s]
                 self.idx[off:off + n].copy_(b.idx, non_blocking=True)
             if getattr(self, "_rng_stage", None) is None:
                 self._rng_stage = PinnedStager(2, torch.int32)
             self._rng_stage.upload(self.rng, self.src.next_rng())
             return
-        for s, (x, y) in zip(self.slots, batches):
+        for s, (x, y) in zip(slots, batches):
             n, off = x.shape[0], self.first[s]
             self.x_in[off:off + n].copy_(x.reshape(n, *self.x_in.shape[1:]), non_blocking=True)
             self.labels[off:off + n].copy_(y, non_blocking=True)
@@ -1535,26 +1617,7 @@ class _StepPlan:
         self._run_eager()
 
     def run(self, train=True):
-        be = self.be
-        if be.use_graph and self.graph is None:
-            # warm up once eagerly (allocator, lazy init), then capture
-            self._run_eager()
-            torch.cuda.synchronize()
-            g = torch.cuda.CUDAGraph()
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                g.capture_begin()
-                self._run_eager()
-                g.capture_end()
-            torch.cuda.current_stream().wait_stream(s)
-            self.graph = g
-            self._captured_once = True
-            return  # the warm-up executed this step
-        if self.graph is not None:
-            self.graph.replay()
-        else:
-            self._run_eager()
+        run_captured(self)
 
     def loss_view(self):
         # a copy: callers keep per-step losses across later replays (engine_model.loss_acc)

@@ -62,6 +62,9 @@ class PopulationEngine:
             self.compute_dtype = torch.float32
         self.loss_scale = float(loss_scale)  # static loss scaling of the PyTorch path (fp16; resnet_run_loop.py:284)
         self.dp = None  # parallel.dataparallel.DPContext when a member is trained by a group of ranks
+        # data parallelism: this replica's gradient weight per member row (local shard / member batch), a device
+        # buffer so the captured step graph reads the current step's weights
+        self.dp_weight = torch.zeros(self.capacity, dtype=torch.float32, device=self.device)
         self.backend = make_backend(self, backend)
         if optimizer_impl == "auto":
             optimizer_impl = "hip" if self.device.type == "cuda" else "reference"
@@ -135,6 +138,8 @@ class PopulationEngine:
         per-member cross-entropy losses (device tensor)."""
         if not getattr(self.backend, "accepts_index_batches", False):
             batches = [b.materialize() if isinstance(b, IndexBatch) else b for b in batches]
+        if self.dp is not None:
+            self._set_dp_weights(slots, batches, hparams)
         if hasattr(self.backend, "train_step"):
             # whole step (fwd, bwd, optimizer, step counters) inside one HIP graph
             losses = self.backend.train_step(slots, batches, hparams, lrs)
@@ -160,16 +165,30 @@ class PopulationEngine:
     # ------------------------------------------------------- data parallelism
     def set_data_parallel(self, dp) -> None:
         self.dp = dp
-        if dp is not None and hasattr(self.backend, "use_graph"):
-            self.backend.use_graph = False  # collectives run eagerly between the backward and the optimizer
+        self._dp_idx = {}
+
+    def _set_dp_weights(self, slots, batches, hparams) -> None:
+        """This replica's share of each member's batch: local images / member batch size (the hparam)."""
+        from ..data.datasets import batch_len
+        w = [0.0] * self.capacity
+        for s, b, hp in zip(slots, batches, hparams):
+            w[s] = batch_len(b) / float(max(1, int(hp["batch_size"])))
+        key = tuple(w)
+        if getattr(self, "_dp_w_host", None) != key:
+            self.dp_weight.copy_(torch.tensor(w, dtype=torch.float32))
+            self._dp_w_host = key
 
     def dp_sync_grads(self, slots: Sequence[int]) -> None:
-        """Mean of the members' gradient rows over the member group (before the optimizer)."""
+        """Gradient rows of the members summed over the member group, each replica's row weighted by its share of
+        the member batch (before the optimizer; inside the captured step on the HIP backends)."""
         if self.dp is None or not slots:
             return
-        idx = torch.tensor(sorted(slots), device=self.device, dtype=torch.long)
+        key = tuple(sorted(slots))
+        idx = self._dp_idx.get(key)
+        if idx is None:
+            idx = self._dp_idx[key] = torch.tensor(key, device=self.device, dtype=torch.long)
         g = self.grads.index_select(0, idx)
-        self.dp.allreduce_mean_(g)
+        self.dp.allreduce_weighted_(g, self.dp_weight.index_select(0, idx))
         self.grads.index_copy_(0, idx, g)
 
     def dp_sync_running(self, slots: Sequence[int]) -> None:

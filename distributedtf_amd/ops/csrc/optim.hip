@@ -134,16 +134,18 @@ __global__ __launch_bounds__(256) void shadow_refresh_kernel(const float* __rest
   }
 }
 
-// Per-member step counters after a captured step: state[slot][col] += 1 and hyper[slot][h_step] += 1; optionally
-// the step's per-member losses gathered in slot-list order (loss_sel[i] = loss[slots[i]]).
+// Per-member step counters after a captured step: state[slot][col] += 1 and hyper[slot][h_step] += 1 for every
+// ACTIVE listed member (hyper column 7; an elastic plan replayed for a subset of its members leaves the others
+// untouched); optionally the step's per-member losses gathered in slot-list order (loss_sel[i] = loss[slots[i]]).
 __global__ void step_advance_kernel(float* __restrict__ state, long S, long col, float* __restrict__ hyper,
                                     int h_step, const int* __restrict__ slots, int n, const float* __restrict__ loss,
                                     float* __restrict__ loss_sel) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
     const int s = slots[i];
-    state[(long)s * S + col] += 1.f;
-    hyper[s * 8 + h_step] += 1.f;
+    const float inc = hyper[s * 8 + 7] != 0.f ? 1.f : 0.f;
+    state[(long)s * S + col] += inc;
+    hyper[s * 8 + h_step] += inc;
     if (loss_sel != nullptr) loss_sel[i] = loss[s];
   }
 }

@@ -119,7 +119,7 @@ __global__ __launch_bounds__(64) void bn_running_update_kernel(float* __restrict
   const int slot = slots[blockIdx.y];
   const int c = threadIdx.x;
   const int C = t[1];
-  if (c >= C) return;
+  if (c >= C || cnt[slot] <= 0.f) return;  // (a member without images this step: an elastic plan's idle slot)
   if (blockIdx.z == 1) {  // combined launch: z = 1 is the moving-statistics update from the forward statistics
     stats = stats_fwd;
     grads = nullptr;

@@ -5,9 +5,13 @@ all-reduce), which the reference's main path hard-wires off (``resnet_run_loop.p
 C19).  Here it is the optional extension for ``population < #GPUs``: ``--dp_size k`` splits the world into
 ``world / k`` member groups of ``k`` consecutive ranks.  Every rank of a group holds a replica of the group's
 members (same ids, same initialisation, same exploit/explore decisions) and trains on its own shard of each
-batch; before every optimizer step the gradient rows of the members are all-reduced (mean) over the group --
-RCCL over xGMI on GPUs, gloo on CPU -- so the replicas stay bit-identical.  BatchNorm normalises with the
-replica's own batch statistics (as MirroredStrategy's per-replica BN did); the running statistics are averaged
+batch; before every optimizer step the gradient rows of the members are all-reduced over the group -- RCCL over
+xGMI on GPUs, gloo on CPU -- so the replicas stay bit-identical.  Each replica's gradient is the mean over its own
+shard, so it is weighted by ``local batch / member batch`` before the sum: an uneven split (a member batch of 129
+over 2 replicas = 65 + 64 images) then yields exactly the gradient of the mean loss over the whole member batch
+(equal weights would over-count the larger shard).  The weighting and the all-reduce are device ops on the step's
+stream, so the HIP backends capture them in the step graph with the rest of the step.  BatchNorm normalises with
+the replica's own batch statistics (as MirroredStrategy's per-replica BN did); the running statistics are averaged
 over the group at the end of every round.
 """
 
@@ -34,6 +38,12 @@ class DPContext:
         import torch.distributed as dist
         dist.all_reduce(t, group=self.group)
         t.div_(self.size)
+
+    def allreduce_weighted_(self, t, w) -> None:
+        """``t[i] <- sum over replicas of w_r[i] * t_r[i]`` (rows ``t[i]``, per-row replica weights ``w[i]``)."""
+        import torch.distributed as dist
+        t.mul_(w.reshape(-1, *([1] * (t.dim() - 1))))
+        dist.all_reduce(t, group=self.group)
 
 
 def make_dp_context(comm, dp_size: int) -> Optional[DPContext]:

@@ -85,3 +85,53 @@ def test_dp_groups_world4_dp2(tmp_path):
     for mid in range(4):
         rows = open(os.path.join(tmp_path, "savedata", "model_%d" % mid, "learning_curve.csv")).read().splitlines()
         assert len(rows) == 1 + 2, rows
+
+
+def _weighted_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    try:
+        from distributedtf_amd.parallel.comm import init_distributed, shutdown_distributed
+        from distributedtf_amd.parallel.dataparallel import make_dp_context
+        from distributedtf_amd.engine.population import PopulationEngine
+        from distributedtf_amd.models.mnist import MnistArch
+        comm = init_distributed(backend="gloo")
+        dp = make_dp_context(comm, world)
+        eng = PopulationEngine(MnistArch(), 2, "cpu")
+        eng.set_data_parallel(dp)
+        # member 0: batch 9 split 5 / 4; member 1: batch 8 split 4 / 4
+        shard = [torch.zeros(dp.local_batch(9)), torch.zeros(dp.local_batch(8))]
+        eng._set_dp_weights([0, 1], [(x, x) for x in shard], [{"batch_size": 9}, {"batch_size": 8}])
+        eng.grads[0, :4] = torch.tensor([1.0, 2.0, 3.0, 4.0]) * (rank + 1)
+        eng.grads[1, :4] = torch.tensor([1.0, 1.0, 1.0, 1.0]) * (rank + 1)
+        eng.dp_sync_grads([0, 1])
+        q.put((rank, eng.grads[:, :4].clone().numpy(), eng.dp_weight.clone().numpy()))
+        shutdown_distributed()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, "ERR", traceback.format_exc()))
+
+
+@pytest.mark.timeout(120)
+def test_dp_gradient_weighted_by_shard():
+    """An uneven split of a member batch (9 = 5 + 4) weights each replica's shard-mean gradient by its share:
+    sum_r (n_r / N) * g_r is the gradient of the mean loss over the whole member batch (reference
+    distribution_utils.py:24-78: MirroredStrategy averages equal per-replica batches)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_weighted_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=100) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(30)
+    for r in res:
+        assert not isinstance(r[1], str), r[2]
+    g = torch.tensor([1.0, 2.0, 3.0, 4.0])
+    want0 = g * (5 / 9.0) * 1 + g * (4 / 9.0) * 2      # rank 0 holds 5 images, rank 1 holds 4
+    want1 = torch.ones(4) * 0.5 * 1 + torch.ones(4) * 0.5 * 2
+    for _, grads, w in res:
+        torch.testing.assert_close(torch.from_numpy(grads[0]), want0)
+        torch.testing.assert_close(torch.from_numpy(grads[1]), want1)
+    assert abs(res[0][2][0] - 5 / 9.0) < 1e-6 and abs(res[1][2][0] - 4 / 9.0) < 1e-6

@@ -178,3 +178,42 @@ def test_hip_step_repeat_and_population_capacity():
     assert torch.isfinite(L).all()
     assert (L[-1] < L[0]).all(), L  # memorising one fixed batch must reduce the loss
     assert eng.host_step[:4] == [12] * 4
+
+
+def test_hip_step_shrinking_active_set(monkeypatch):
+    """Members that finish their epoch drop out of the active set (engine_model._train_cycle): the elastic plan of
+    the full set is replayed with zero images for them -- no new plan or capture.  The idle member's parameters,
+    optimizer slots, BN moving statistics and step counter stay untouched; the active members' step-2 gradients
+    match the fp32 oracle (reference training_worker.py:64-69: members train independently)."""
+    monkeypatch.setenv("DTF_HIP_GRAPH", "1")
+    torch.manual_seed(0)
+    arch = ResNetArch(cifar_config(14, version=2))
+    dev = torch.device("cuda")
+    sizes = [20, 9, 14]
+    ref = PopulationEngine(arch, 3, dev, backend="torch", compute_dtype=torch.float32, optimizer_impl="hip")
+    hip = PopulationEngine(arch, 3, dev, backend="hip")
+    for i, bs in enumerate(sizes):
+        ref.add_member(None, _hp(bs), seed=10 + i)
+        hip.add_member(None, _hp(bs), seed=10 + i)
+    g = torch.Generator().manual_seed(5)
+    _perturb_bn(arch, (ref, hip), 3, g)
+    batches = [(torch.randn(bs, 32, 32, 3, generator=g).to(dev), torch.randint(0, 10, (bs,), generator=g).to(dev))
+               for bs in sizes]
+    for e in (ref, hip):
+        e.train_step([0, 1, 2], batches, [_hp(bs) for bs in sizes], [0.0] * 3)
+    plans0 = dict(hip.backend._plans)
+    assert len(plans0) == 1 and next(iter(plans0.values())).elastic
+    before = hip.state.clone()
+    active = [0, 2]
+    l_ref = ref.train_step(active, [batches[0], batches[2]], [_hp(20), _hp(14)], [1.0, 1.0])
+    l_hip = hip.train_step(active, [batches[0], batches[2]], [_hp(20), _hp(14)], [1.0, 1.0])
+    torch.cuda.synchronize()
+    assert dict(hip.backend._plans) == plans0  # the captured plan was replayed, nothing new built
+    assert torch.equal(hip.state[1], before[1])  # idle member: params, slots, running stats, step
+    assert hip.host_step == ref.host_step and hip.host_step[1] == 1
+    torch.testing.assert_close(l_hip.float(), l_ref.float(), rtol=3e-2, atol=3e-2)
+    for s in active:
+        a, b = before[s, :arch.n_params] - hip.params[s], before[s, :arch.n_params] - ref.params[s]
+        assert _relerr(a, b) < 0.06, (s, _relerr(a, b))
+    torch.testing.assert_close(hip.running[active], ref.running[active], rtol=2e-2, atol=2e-3)
+    torch.testing.assert_close(hip.step_col(), ref.step_col())

@@ -314,12 +314,17 @@ class _MnistPlan:
         if self.eval:  # counts accumulate over the eval chunks in the plan's own buffers
             a.loss, a.correct = _p(self.ev_acc[1]), _p(self.ev_acc[0])
         self.args = a
-        # work lists (img0, nimg, 0, slot): image chunks of one member
+        # work lists (img0, nimg, 0, slot): image chunks of one member.  Deterministic build: ONE chunk per member
+        # for every launch that adds into per-member accumulators (dense / conv weight gradients, bias gradients,
+        # loss, correct count) -- each address then receives a single add onto zero, and every partial sum is
+        # formed in a fixed order inside its workgroup, so the step replays bitwise (the GEMMs own their tiles)
+        det = ops.build_deterministic()
+        whole = 1 << 30
         self.w_fwd = self._chunks(max(1, -(-N // 512)))
-        self.w_head = self._chunks(16)
+        self.w_head = self._chunks(whole if det else 16)
         self.w_dgrad = self._chunks(max(1, -(-N // 512)))
-        self.w_c2w = self._chunks(max(4, -(-N * 5 // 320)))
-        self.w_c1w = self._chunks(max(4, -(-N // 256)))
+        self.w_c2w = self._chunks(whole if det else max(4, -(-N * 5 // 320)))
+        self.w_c1w = self._chunks(whole if det else max(4, -(-N // 256)))
         Pp, S = e.Pp, e.S
         d1 = o["dense1_w"]
         fwd, dgr, wgr = [], [], []

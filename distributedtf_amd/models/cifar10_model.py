@@ -20,6 +20,8 @@ for the dataset); bf16 compute with fp32 master weights and BN statistics.
 
 from __future__ import annotations
 
+import torch
+
 from .engine_model import EngineModel
 from .resnet import ResNetArch, cifar_config
 from ..data import datasets
@@ -43,7 +45,10 @@ class Cifar10Model(EngineModel):
         if synthetic is None:
             synthetic = not datasets.cifar10_available(self.data_dir)
         if synthetic:
-            return datasets.SyntheticDataset((32, 32, 3), 10, device, max_batch=256, n_eval=1000)
+            # the reference evaluates on the full 10k-image test set every epoch (resnet_run_loop.py:463-466,
+            # mnist_model.py:167-172): a synthetic eval set of the same size on the GPU (1k on CPU test runs)
+            n_eval = datasets.CIFAR_NUM_TEST if torch.device(device).type == "cuda" else 1000
+            return datasets.SyntheticDataset((32, 32, 3), 10, device, max_batch=256, n_eval=n_eval)
         trx, tr_y, tex, te_y = datasets.load_cifar10(self.data_dir)
         return datasets.DeviceDataset(trx, tr_y, tex, te_y, device, augment=datasets.augment_cifar,
                                       eval_transform=datasets.eval_cifar)

@@ -13,6 +13,8 @@ epoch, Appendix A4) or ``max_train_steps`` is given; data is synthetic when
 
 from __future__ import annotations
 
+import torch
+
 from .engine_model import EngineModel
 from .mnist import MnistArch
 from ..data import datasets
@@ -34,7 +36,10 @@ class MNISTModel(EngineModel):
         if synthetic is None:
             synthetic = not datasets.mnist_available(self.data_dir)
         if synthetic:
-            return datasets.SyntheticDataset((28, 28, 1), 10, device, max_batch=256, n_eval=1000)
+            # the reference evaluates on the full 10k-image test set every epoch (resnet_run_loop.py:463-466,
+            # mnist_model.py:167-172): a synthetic eval set of the same size on the GPU (1k on CPU test runs)
+            n_eval = datasets.MNIST_NUM_TEST if torch.device(device).type == "cuda" else 1000
+            return datasets.SyntheticDataset((28, 28, 1), 10, device, max_batch=256, n_eval=n_eval)
         trx, tr_y, tex, te_y = datasets.load_mnist(self.data_dir, self.normalize)
         return datasets.DeviceDataset(trx, tr_y, tex, te_y, device)
 

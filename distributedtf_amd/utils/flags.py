@@ -197,9 +197,8 @@ class MainArgs(argparse.Namespace):
             torch.backends.cudnn.benchmark = False
             torch.backends.cudnn.deterministic = True
             os.environ["DTF_DETERMINISTIC"] = "1"  # ops.lib() loads the deterministic build
-            hip_det = self.model == "cifar10" and int(getattr(self, "resnet_version", 2)) == 2
-            if self.backend == "auto" and not hip_det:
-                self.backend = "torch"  # the MNIST / ImageNet / v1 HIP paths keep atomic reductions
+            if self.backend == "auto" and not hip_deterministic(self):
+                self.backend = "torch"  # this family's HIP path still has order-dependent reductions
 
     def inject_nan_schedule(self) -> Dict[int, List[int]]:
         out: Dict[int, List[int]] = {}
@@ -207,6 +206,14 @@ class MainArgs(argparse.Namespace):
             mid, rnd = spec.split("@")
             out.setdefault(int(rnd), []).append(int(mid))
         return out
+
+
+def hip_deterministic(args) -> bool:
+    """Model families whose HIP step has a deterministic (bitwise-replayable) build: CIFAR ResNet v2 (64 statistic
+    replicas, capped workgroups) and MNIST (one workgroup per member for every accumulation)."""
+    if args.model == "mnist":
+        return True
+    return args.model == "cifar10" and int(getattr(args, "resnet_version", 2) or 2) == 2
 
 
 def parse_main_args(argv=None, defaults=None) -> MainArgs:
@@ -225,6 +232,9 @@ def parse_main_args(argv=None, defaults=None) -> MainArgs:
     elif args.loss_scale is not None and args.loss_scale != 1 and args.backend != "torch" and args.model != "toy":
         p.error("--loss_scale applies to the fp16 / fp32 PyTorch path; bf16 needs no loss scaling "
                 "(pass --backend torch to scale anyway)")
+    if args.deterministic and args.backend == "hip" and args.model != "toy" and not hip_deterministic(args):
+        p.error("--deterministic with --backend hip: the %s HIP step has no deterministic build yet; use --backend "
+                "auto (deterministic PyTorch algorithms) or torch" % args.model)
     if args.deterministic and args.debug_kernels:
         # the debug kernel build keeps the release reductions (8 replicas, atomics): not replayable
         p.error("--deterministic cannot be combined with --debug_kernels (the debug build is not the "

@@ -97,8 +97,9 @@ def test_fp16_loss_scaled_training_is_finite(tmp_path, monkeypatch):
 
 
 def test_deterministic_flag_selects_det_build(monkeypatch):
-    """--deterministic keeps the HIP backend for the CIFAR ResNet v2 step (deterministic kernel build, selected by
-    DTF_DETERMINISTIC) and moves the families whose HIP kernels keep atomic reductions to the torch backend."""
+    """--deterministic keeps the HIP backend for the CIFAR ResNet v2 and MNIST steps (deterministic kernel build,
+    selected by DTF_DETERMINISTIC) and moves the families whose HIP kernels keep atomic reductions to the torch
+    backend; an explicit --backend hip for those is an error."""
     from distributedtf_amd import ops
     from distributedtf_amd.ops import build as kb
     from distributedtf_amd.utils.flags import parse_main_args
@@ -110,7 +111,14 @@ def test_deterministic_flag_selects_det_build(monkeypatch):
         assert a.backend == "auto" and a.seed == 0
         b = parse_main_args(["--model", "mnist", "--deterministic"])
         b.apply_runtime_modes()
-        assert b.backend == "torch"
+        assert b.backend == "auto"  # MNIST has a deterministic HIP build too
+        c = parse_main_args(["--model", "imagenet", "--deterministic"])
+        c.apply_runtime_modes()
+        assert c.backend == "torch"  # ImageNet keeps order-dependent split-K reductions on the HIP path
+        with pytest.raises(SystemExit):  # an explicit --backend hip must not silently lose the guarantee
+            parse_main_args(["--model", "imagenet", "--deterministic", "--backend", "hip"])
+        with pytest.raises(SystemExit):  # the debug kernel build is not the deterministic one
+            parse_main_args(["--model", "cifar10", "--deterministic", "--debug_kernels"])
         assert kb.LIB_DET.endswith("libdtf_kernels_det.so") and "-DDTF_NREP=64" in kb.DET_FLAGS
     finally:
         os.environ.pop("DTF_DETERMINISTIC", None)

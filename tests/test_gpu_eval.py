@@ -158,5 +158,5 @@ def test_deterministic_build_is_bitwise_replayable():
     # and the deterministic step matches the fp32 oracle like the regular build (ResNet-14, ragged pop 2, graphs)
     r = subprocess.run([_sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
                         os.path.join(root, "tests", "test_gpu_resnet_step.py") + "::test_hip_step_matches_reference",
-                        "-k", "14-1-1-2-1-0"], env=env, capture_output=True, text=True, timeout=240, cwd=root)
+                        "-k", "v2-r14-g1-pop2"], env=env, capture_output=True, text=True, timeout=240, cwd=root)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]

@@ -109,10 +109,13 @@ def _compare_step(arch, sizes, floor=0.06, seed=0, warm_sizes=None, check=None):
     return max(r[3] for r in report)
 
 
-@pytest.mark.parametrize("size,graph,version,sizes", [
-    (8, "1", 2, [8, 12, 6]), (14, "1", 2, [8, 12, 6]), (14, "0", 2, [8, 12, 6]),
-    (14, "1", 2, [8, 12]), (20, "0", 2, [8, 12]), (14, "1", 2, [16]),
-    (8, "1", 1, [8, 12]), (14, "0", 1, [8, 12]), (20, "1", 1, [8, 12])])
+_STEP_CASES = [(8, "1", 2, [8, 12, 6]), (14, "1", 2, [8, 12, 6]), (14, "0", 2, [8, 12, 6]),
+               (14, "1", 2, [8, 12]), (20, "0", 2, [8, 12]), (14, "1", 2, [16]),
+               (8, "1", 1, [8, 12]), (14, "0", 1, [8, 12]), (20, "1", 1, [8, 12])]
+
+
+@pytest.mark.parametrize("size,graph,version,sizes", _STEP_CASES,
+                         ids=["v%d-r%d-g%s-pop%d" % (v, n, g, len(z)) for n, g, v, z in _STEP_CASES])
 def test_hip_step_matches_reference(size, graph, version, sizes, monkeypatch):
     """Three members: the fused backward launches (BN1-backward folded into the next conv_b staging, dW slab
     reductions carried by the next launch); one or two members: the dual backward (dgrad and wgrad roles of one

@@ -1,6 +1,6 @@
 """Deterministic HIP build check (run with DTF_DETERMINISTIC=1): two identically initialised engines train the same
-steps on the same batches (graph replay, ragged two-member population) and must hold bitwise-identical state
-rows; the step also stays close to the fp32 PyTorch oracle.  Prints DET_OK."""
+steps on the same batches (graph replay, ragged populations) and must hold bitwise-identical state rows -- the
+CIFAR ResNet v2 and MNIST families.  Prints DET_OK."""
 import os
 import sys
 
@@ -40,6 +40,33 @@ def run(size, sizes, steps, opt="Momentum"):
     return same
 
 
-ok = all([run(20, [16, 24], 4), run(56, [128], 3), run(56, [128] * 4, 2)])
+def run_mnist(sizes, steps):
+    """The MNIST HIP step (deterministic work splits: one accumulation workgroup per member, hip_mnist.py)."""
+    from distributedtf_amd.models.mnist import MnistArch
+    arch = MnistArch()
+    dev = torch.device("cuda")
+    out = []
+    for rep in range(2):
+        e = PopulationEngine(arch, len(sizes), dev, backend="hip")
+        hps = []
+        for i, bs in enumerate(sizes):
+            hp = {"opt_case": {"optimizer": "Adam", "lr": 1e-3}, "batch_size": bs, "initializer": "he_init"}
+            e.add_member(None, hp, seed=7 + i)
+            hps.append(hp)
+        g = torch.Generator().manual_seed(3)
+        batches = [((torch.rand(bs, 28, 28, 1, generator=g) * 255).to(dev),
+                    torch.randint(0, 10, (bs,), generator=g).to(dev)) for bs in sizes]
+        slots = list(range(len(sizes)))
+        for _ in range(steps):
+            losses = e.train_step(slots, batches, hps, [1e-3] * len(sizes))
+        torch.cuda.synchronize()
+        out.append((e.state.clone(), losses.cpu()))
+    same = torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    print("mnist sizes %s steps %d: bitwise identical %s, losses %s" % (sizes, steps, same, out[0][1].tolist()),
+          flush=True)
+    return same
+
+
+ok = all([run(20, [16, 24], 4), run(56, [128], 3), run(56, [128] * 4, 2), run_mnist([40, 72], 4)])
 print("DET_OK" if ok else "DET_FAIL")
 sys.exit(0 if ok else 1)

@@ -41,7 +41,7 @@ def _perturb_bn(arch, engines, n, g):
             e.state[:n, b.beta_off:b.beta_off + b.c] = noise_b.to(dev)
 
 
-def _compare_step(arch, sizes, floor=0.06, seed=0, warm_sizes=None, check=None):
+def _compare_step(arch, sizes, floor=0.06, seed=0, warm_sizes=None, check=None, active=None):
     """Two optimizer steps on the same batches: step 1 with lr = 0 (the eager warm-up that also captures the HIP
     graph), step 2 with lr = 1 (the first graph REPLAY: device-side step advance, hyper-table refresh, in-graph
     loss gather).  Step 2's parameter delta is its gradient, compared per layer with the fp32 oracle."""
@@ -81,10 +81,22 @@ def _compare_step(arch, sizes, floor=0.06, seed=0, warm_sizes=None, check=None):
         check(hip, plans0 if warm_sizes is not None else None)
     before = hip.params.clone()
     assert torch.equal(before, ref.params)
-    l_ref = ref.train_step(slots, batches, hps, [1.0] * n)
-    r16.train_step(slots, batches, hps, [1.0] * n)
-    l_hip = hip.train_step(slots, batches, hps, [1.0] * n)
+    full = slots
+    if active is not None:  # the compared step trains only these members (an elastic plan's subset replay)
+        plans0 = dict(hip.backend._plans)
+        state0 = hip.state.clone()
+        pos = [slots.index(s) for s in active]
+        slots, batches, hps = list(active), [batches[i] for i in pos], [hps[i] for i in pos]
+    l_ref = ref.train_step(slots, batches, hps, [1.0] * len(slots))
+    r16.train_step(slots, batches, hps, [1.0] * len(slots))
+    l_hip = hip.train_step(slots, batches, hps, [1.0] * len(slots))
     torch.cuda.synchronize()
+    if active is not None:
+        assert dict(hip.backend._plans) == plans0, "a subset step must replay the existing elastic plan"
+        for s in full:
+            if s not in active:  # idle member: parameters, optimizer slots, BN moving statistics, step counter
+                assert torch.equal(hip.state[s], state0[s]), s
+        assert hip.host_step == ref.host_step
     torch.testing.assert_close(l_hip.float(), l_ref.float(), rtol=3e-2, atol=3e-2)
     g_ref = before - ref.params
     g_hip = before - hip.params
@@ -189,34 +201,5 @@ def test_hip_step_shrinking_active_set(monkeypatch):
     optimizer slots, BN moving statistics and step counter stay untouched; the active members' step-2 gradients
     match the fp32 oracle (reference training_worker.py:64-69: members train independently)."""
     monkeypatch.setenv("DTF_HIP_GRAPH", "1")
-    torch.manual_seed(0)
-    arch = ResNetArch(cifar_config(14, version=2))
-    dev = torch.device("cuda")
-    sizes = [20, 9, 14]
-    ref = PopulationEngine(arch, 3, dev, backend="torch", compute_dtype=torch.float32, optimizer_impl="hip")
-    hip = PopulationEngine(arch, 3, dev, backend="hip")
-    for i, bs in enumerate(sizes):
-        ref.add_member(None, _hp(bs), seed=10 + i)
-        hip.add_member(None, _hp(bs), seed=10 + i)
-    g = torch.Generator().manual_seed(5)
-    _perturb_bn(arch, (ref, hip), 3, g)
-    batches = [(torch.randn(bs, 32, 32, 3, generator=g).to(dev), torch.randint(0, 10, (bs,), generator=g).to(dev))
-               for bs in sizes]
-    for e in (ref, hip):
-        e.train_step([0, 1, 2], batches, [_hp(bs) for bs in sizes], [0.0] * 3)
-    plans0 = dict(hip.backend._plans)
-    assert len(plans0) == 1 and next(iter(plans0.values())).elastic
-    before = hip.state.clone()
-    active = [0, 2]
-    l_ref = ref.train_step(active, [batches[0], batches[2]], [_hp(20), _hp(14)], [1.0, 1.0])
-    l_hip = hip.train_step(active, [batches[0], batches[2]], [_hp(20), _hp(14)], [1.0, 1.0])
-    torch.cuda.synchronize()
-    assert dict(hip.backend._plans) == plans0  # the captured plan was replayed, nothing new built
-    assert torch.equal(hip.state[1], before[1])  # idle member: params, slots, running stats, step
-    assert hip.host_step == ref.host_step and hip.host_step[1] == 1
-    torch.testing.assert_close(l_hip.float(), l_ref.float(), rtol=3e-2, atol=3e-2)
-    for s in active:
-        a, b = before[s, :arch.n_params] - hip.params[s], before[s, :arch.n_params] - ref.params[s]
-        assert _relerr(a, b) < 0.06, (s, _relerr(a, b))
-    torch.testing.assert_close(hip.running[active], ref.running[active], rtol=2e-2, atol=2e-3)
-    torch.testing.assert_close(hip.step_col(), ref.step_col())
+    _compare_step(ResNetArch(cifar_config(14, version=2)), [20, 9, 14], active=[0, 2])
+

@@ -55,6 +55,7 @@ FUSED_SLAB_BYTES = {16: 16e6, 32: 16e6, 64: 48e6}  # fused backward: per-launch 
 FUSED_MIN_WG = 256        # ... at least this many workgroups (one member would leave CUs idle otherwise)
 FUSED_MAX_WG = {32: 128}  # ... at most this many per member (C = 32: fewer, fuller workgroups)
 PIGGYBACK_MAX_WG = 3000   # slab reductions ride on the next backward launch when they add <= this many workgroups
+DEFER_WG = {16: 64, 32: 32, 64: 16}  # deferred wgrad (small populations): workgroups per member and layer
 c_void_p, c_int, c_long = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
 
 
@@ -132,6 +133,7 @@ def _register():
     ops.register("dtf_dw_slab_reduce", [c_void_p, c_void_p, c_int, c_void_p, c_long, c_long, c_int, c_void_p])
     ops.register("dtf_conv_bwd_fused", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_bwd_dual", [P(ConvArgs), P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
+    ops.register("dtf_conv_wgrad_multi", [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_dw_slab_reduce_multi", [c_void_p, c_int, c_int, c_void_p, c_long, c_int, c_void_p])
     ops.register("dtf_slab_job_size", [])
     ops.register("dtf_dense_job_size", [])
@@ -671,11 +673,17 @@ class _StepPlan:
         # of their sum while the population leaves CUs idle (C = 16 keeps the fused kernel: its single-band work
         # items already fill the GPU; profiles/r2_dual_pop1_breakdown.txt)
         self.dual = dev.type == "cuda" and cfg.version == 2 and len(slots) <= DUAL_MAX_POP
+        # Deferred weight gradients (the same small populations): each stride-1 layer's backward launch runs only
+        # its dgrad role -- the critical path, serialised by the BatchNorm statistics -- and the wgrad work of all
+        # those layers runs afterwards in a few wide launches (conv_wgrad_multi_kernel), one per (C, dY mode).
+        # Their dY / x operands stay alive for the whole backward (per-block buffers instead of ping-pong ones).
+        self.defer_wg = self.dual
+        self._wg_jobs = {}  # (C, wgrad dY mode) -> [(ConvArgs, work table, grad offset)]
         self.launches = []
         self._pending_slab = None  # (slab ptr, reduce table, C, grad offset) of the last fused launch
         self._slab_flip = 0
         # C = 64 dW slabs reduced together by ONE launch after the backward (instead of 17 small reductions)
-        self._deferred = []
+        self._deferred = []  # (slab, reduce table, grad offset, C): reduced by one launch per C after the backward
         # standalone wgrad launches (stem, projections, strided convs) write dense per-workgroup dW partials reduced
         # in one launch after the backward (no contended fp32 atomics; fixed order)
         self.wslab = dev.type == "cuda"
@@ -991,7 +999,7 @@ class _StepPlan:
         for t in (dy, dy2, dy3, dy_out, dz_out, x, res):
             assert t is None or tuple(t.shape) == (self.N, H, H, C), (t.shape, C, H)
         bands = H // rows
-        if self.dual and C in DUAL_CS:
+        if self.dual and (C in DUAL_CS or self.defer_wg):
             return self._conv_bwd_dual(ci, c, C, H, rows, bands, dy, dz_out, x, mode_dy, dy2, dy_bn, x_bn, res,
                                        ident_x, dy3, dy_out)
         n_wg = self._fused_nwg(C, bands)
@@ -1041,7 +1049,7 @@ class _StepPlan:
         self._keep(a)
         red = self._slab_table(work)
         if C == 64:
-            self._deferred.append((a.slab, red, c.off))
+            self._deferred.append((a.slab, red, c.off, 64))
         else:
             self._pending_slab = (a.slab, red, C, c.off)
 
@@ -1089,8 +1097,11 @@ class _StepPlan:
             b.ep_gamma, b.ep_beta = self._bn(x_bn)
             b.st_ep = _p(be.st_f(x_bn))
         b.Hi, b.Wi, b.Ho, b.Wo, b.rows = H, H, H, H, rows
-        b.slab = _p(self._layer_slab(wwork.shape[0] * self._slab_elems(C)))
         b.cin_real = self._stamp_row("fused", "fused-wg C=%d mdy=%d epi=%d" % (C, mode_dy, epi))
+        if self.defer_wg:
+            return self._defer_wgrad(ci, c, C, H, rows, bands, a, b, dy, x, mode_dy, dy2, dy_bn, x_bn, dy_out,
+                                     tsz, epi)
+        b.slab = _p(self._layer_slab(wwork.shape[0] * self._slab_elems(C)))
         # ---- trailing reduction of the previous backward launch's slabs
         n_red = 0
         pend = self._pending_slab
@@ -1108,9 +1119,64 @@ class _StepPlan:
         self._add(lib.dtf_conv_bwd_dual, ctypes.byref(a), ctypes.byref(b), C, mode_dy, epi,
                   a.n_main + b.n_main + n_red, lds)
         if C == 64:
-            self._deferred.append((b.slab, self._slab_table(wwork), c.off))
+            self._deferred.append((b.slab, self._slab_table(wwork), c.off, 64))
         else:
             self._pending_slab = (b.slab, self._slab_table(wwork), C, c.off)
+
+    def _defer_wgrad(self, ci, c, C, H, rows, bands, a, b, dy, x, mode_dy, dy2, dy_bn, x_bn, dy_out, tsz, epi):
+        """Deferred-wgrad form of a dual launch: the launch holds the dgrad role only; the wgrad job (the role's
+        arguments with its own work split) is queued for conv_wgrad_multi_kernel.  Its dY operand: the dY the
+        dgrad role materialises (``dy_out``) or the plain incoming gradient (mode 0), read as-is; else (conv_a)
+        BN2-backward(dz2, h) recomputed while staging, as the dgrad role does."""
+        lib = ops.lib()
+        nb = b.n_main
+        b.n_main = 0
+        self._keep(a)
+        self._keep(b)
+        self._add(lib.dtf_conv_bwd_dual, ctypes.byref(a), ctypes.byref(b), C, mode_dy, epi, a.n_main,
+                  2304 + 2 * tsz * 2)
+        b.n_main = nb
+        w = self._base_args()
+        ctypes.memmove(ctypes.addressof(w), ctypes.addressof(b), ctypes.sizeof(ConvArgs))
+        if dy_out is not None or mode_dy == 0:
+            wmode = 0
+            w.x, w.x2, w.x3 = _p(dy_out if dy_out is not None else dy), None, None
+            w.in_gamma = w.in_beta = 0
+            w.st_in = w.st_in_b = None
+        else:
+            wmode = 2
+            assert mode_dy == 2 and dy2 is not None and dy_bn is not None
+        wwork = self._work_iters(bands, max(1, min(self.N * bands, DEFER_WG[C] * len(self.slots))))
+        w.work = _p(wwork)
+        w.n_main = wwork.shape[0]
+        self._set_uniform(w, wwork)
+        w.slab = _p(self._layer_slab(wwork.shape[0] * self._slab_elems(C)))
+        w.cin_real = -1
+        self._wg_jobs.setdefault((C, wmode), []).append((w, wwork, c.off))
+
+    def _emit_deferred_wgrad(self):
+        """One conv_wgrad_multi launch per (C, dY mode) over every queued layer; their slabs join the per-C
+        reductions of _flush_deferred."""
+        lib = ops.lib()
+        for (C, wmode), jobs in sorted(self._wg_jobs.items()):
+            arr = (ConvArgs * len(jobs))()
+            wmap = []
+            for j, (w, work, goff) in enumerate(jobs):
+                arr[j] = w
+                wmap += [(j, k) for k in range(w.n_main)]
+                self._deferred.append((w.slab, self._slab_table(work), goff, C))
+            jt = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.be.dev)
+            mt = torch.tensor(wmap, dtype=torch.int32, device=self.be.dev)
+            self._keep(jt)
+            self._keep(mt)
+            tsz = ((8 + 2) * _wpitch(C) * _cpad(C) + 8 + 63) // 64 * 64
+            self._add(lib.dtf_conv_wgrad_multi, _p(jt), _p(mt), len(wmap), C, wmode, 2304 + 4 * tsz * 2)
+        self._wg_jobs = {}
+
+    def _fresh_like(self, t):
+        u = torch.empty_like(t)
+        self._keep(u)
+        return u
 
     def _piggyback(self, pend):
         """Reduce the previous launch's C = 16 / 32 slabs inside the next backward launch when that adds few
@@ -1139,17 +1205,16 @@ class _StepPlan:
             self._add(ops.lib().dtf_dense_slab_reduce_multi, _p(jt), len(self._deferred_dense), nmax,
                       min(bmax, DENSE_REDUCE_BLOCKS), _p(self.e.grads), self.e.Pp)
             self._deferred_dense = []
-        if not self._deferred:
-            return
-        jobs = (SlabJob * len(self._deferred))()
-        nmax = 0
-        for i, (buf, red, goff) in enumerate(self._deferred):
-            jobs[i] = SlabJob(buf, _p(red), goff, red.shape[0], 0)
-            nmax = max(nmax, red.shape[0])
-        jt = torch.frombuffer(bytearray(bytes(jobs)), dtype=torch.uint8).to(self.be.dev)
-        self._keep(jt)
-        self._add(ops.lib().dtf_dw_slab_reduce_multi, _p(jt), len(self._deferred), nmax, _p(self.e.grads), self.e.Pp,
-                  64)
+        for C in sorted({d[3] for d in self._deferred}):
+            sel = [d for d in self._deferred if d[3] == C]
+            jobs = (SlabJob * len(sel))()
+            nmax = 0
+            for i, (buf, red, goff, _) in enumerate(sel):
+                jobs[i] = SlabJob(buf, _p(red), goff, red.shape[0], 0)
+                nmax = max(nmax, red.shape[0])
+            jt = torch.frombuffer(bytearray(bytes(jobs)), dtype=torch.uint8).to(self.be.dev)
+            self._keep(jt)
+            self._add(ops.lib().dtf_dw_slab_reduce_multi, _p(jt), len(sel), nmax, _p(self.e.grads), self.e.Pp, C)
         self._deferred = []
 
     def _flush_slab(self):
@@ -1291,6 +1356,8 @@ class _StepPlan:
             x, h = self.xs[i], self.hs[i]
             Hi, Ho = x.shape[1], h.shape[1]
             T = self.tmp[Ho]
+            if self.defer_wg:  # deferred wgrad: this block's dz2 is read again after the backward
+                T = dict(T, dz2=self._fresh_like(T["dz2"]))
             ca, cb = blk.convs
             # conv_b: dgrad -> dz2 (mask by BN2(h), BN2 reductions); wgrad
             if pend is not None:
@@ -1331,6 +1398,8 @@ class _StepPlan:
                 self._conv_wgrad(ca, x, T["dz2"], mode_x=1, mode_dy=2, x_bn=bn1, dy_bn=bn2, dy2=h)
             # g_in = BN1-backward(dz1, x) [+ g_out if identity shortcut]
             g_next = Tin["g"][1] if g_cur is Tin["g"][0] else Tin["g"][0]
+            if self.defer_wg:  # every block's g stays alive for the deferred wgrad
+                g_next = self._fresh_like(Tin["g"][0])
             add = None if blk.proj is not None else g_cur
             if i > 0:
                 pend = (Tin["dz1"], x, add, g_next, bn1)
@@ -1339,6 +1408,7 @@ class _StepPlan:
             g_cur = g_next
         # stem wgrad (input = padded image, real channels 3)
         self._conv_wgrad(prog.stem, self.xin16, g_cur, mode_x=0, mode_dy=0, cin_real=cfg.in_channels)
+        self._emit_deferred_wgrad()
         # BN parameter gradients from the backward reductions
         self._flush_slab()
         self._flush_deferred()

@@ -1848,6 +1848,21 @@ __global__ __launch_bounds__(256, FUSED_WAVES(C, MODE_DY)) void conv_bwd_dual_ke
   }
 }
 
+// Deferred weight gradients of small populations (engine/hip_resnet.py: one or two members per GPU).  The backward
+// launches of the stride-1 3x3 layers run only their dgrad role (the critical path: every layer waits for the
+// previous one's BatchNorm statistics), and the wgrad work of ALL the layers of one (C, MODE_DY) class runs here,
+// afterwards, as ONE wide launch -- hundreds of independent workgroups instead of a wgrad role that stretched every
+// latency-bound backward launch.  jobs[j]: the wgrad-role arguments of layer j (dY / x operands kept alive for the
+// whole backward, own dW slab); map[block] = (job, workgroup index within the job).
+template <int C, int MODE_DY>
+__global__ __launch_bounds__(256, 1) void conv_wgrad_multi_kernel(const ConvArgs* __restrict__ jobs,
+                                                                    const int2* __restrict__ map) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int2 m = map[blockIdx.x];
+  const int j = __builtin_amdgcn_readfirstlane(m.x), bid = __builtin_amdgcn_readfirstlane(m.y);
+  conv_bwd_body<C, MODE_DY, 0, 2>(jobs[j], bid, smem);
+}
+
 // Sum of one member's per-workgroup dW slabs (written by conv_bwd_fused_kernel) into its gradient row.
 // grid (E/32, members), 256 threads = 32 slab elements x 8 workgroup groups (each thread strides over the
 // member's slabs, then an LDS reduction across the 8 groups); red[y] = (first wg, n wgs, -, slot).  Element
@@ -2139,6 +2154,22 @@ DTF_API int dtf_conv_bwd_dual(const ConvArgs* a, const ConvArgs* b, int c, int m
   DUAL_CASE(16, 2, 0) DUAL_CASE(32, 2, 0) DUAL_CASE(64, 2, 0)
   DUAL_CASE(16, 2, 1)
 #undef DUAL_CASE
+  return -1;
+}
+
+DTF_API int dtf_conv_wgrad_multi(const void* jobs, const void* map, int nblocks, int c, int mode_dy, int lds,
+                                 hipStream_t stream) {
+  if (nblocks <= 0) return 0;
+  DTF_HOST_CHECK(jobs != nullptr && map != nullptr && lds <= 160 * 1024);
+#define WM_CASE(CC, M)                                                                                          \
+  if (c == CC && mode_dy == M) {                                                                               \
+    hipLaunchKernelGGL((conv_wgrad_multi_kernel<CC, M>), dim3(nblocks), dim3(256), lds, stream,                \
+                       reinterpret_cast<const ConvArgs*>(jobs), reinterpret_cast<const int2*>(map));            \
+    return DTF_CHECK_LAUNCH();                                                                                 \
+  }
+  WM_CASE(16, 0) WM_CASE(32, 0) WM_CASE(64, 0)
+  WM_CASE(16, 2) WM_CASE(32, 2) WM_CASE(64, 2)
+#undef WM_CASE
   return -1;
 }
 

@@ -1129,13 +1129,15 @@ class _StepPlan:
         dgrad role materialises (``dy_out``) or the plain incoming gradient (mode 0), read as-is; else (conv_a)
         BN2-backward(dz2, h) recomputed while staging, as the dgrad role does."""
         lib = ops.lib()
-        nb = b.n_main
-        b.n_main = 0
+        # the launch's copy of the wgrad-role arguments has no workgroups (the launch is read when the plan runs,
+        # not here, so it must not share b, whose n_main the queued job keeps)
+        b0 = self._base_args()
+        ctypes.memmove(ctypes.addressof(b0), ctypes.addressof(b), ctypes.sizeof(ConvArgs))
+        b0.n_main = 0
         self._keep(a)
-        self._keep(b)
-        self._add(lib.dtf_conv_bwd_dual, ctypes.byref(a), ctypes.byref(b), C, mode_dy, epi, a.n_main,
+        self._keep(b0)
+        self._add(lib.dtf_conv_bwd_dual, ctypes.byref(a), ctypes.byref(b0), C, mode_dy, epi, a.n_main,
                   2304 + 2 * tsz * 2)
-        b.n_main = nb
         w = self._base_args()
         ctypes.memmove(ctypes.addressof(w), ctypes.addressof(b), ctypes.sizeof(ConvArgs))
         if dy_out is not None or mode_dy == 0:

@@ -20,7 +20,7 @@ def test_debug_kernels_sets_hip_serialisation(monkeypatch):
 
 
 def test_deterministic_mode_seeds_and_selects_backend(monkeypatch):
-    """--deterministic seeds every RNG; the CIFAR ResNet v2 step keeps the HIP backend (deterministic kernel build),
+    """--deterministic seeds every RNG; CIFAR ResNet v2 and MNIST keep the HIP backend (deterministic kernel builds),
     families whose HIP kernels keep atomic reductions fall back to deterministic torch algorithms."""
     monkeypatch.delenv("DTF_DETERMINISTIC", raising=False)
     try:
@@ -31,7 +31,10 @@ def test_deterministic_mode_seeds_and_selects_backend(monkeypatch):
         assert torch.are_deterministic_algorithms_enabled()
         b = parse_main_args(["4", "--model", "mnist", "--deterministic"])
         b.apply_runtime_modes()
-        assert b.backend == "torch" and b.model_kwargs()["backend"] == "torch"
+        assert b.backend == "auto"
+        c = parse_main_args(["4", "--model", "imagenet", "--deterministic"])
+        c.apply_runtime_modes()
+        assert c.backend == "torch" and c.model_kwargs()["backend"] == "torch"
     finally:
         torch.use_deterministic_algorithms(False)
         os.environ.pop("DTF_DETERMINISTIC", None)

@@ -572,6 +572,23 @@ __device__ __forceinline__ uint32_t relu_pk2(uint32_t w) {
 }
 __device__ __forceinline__ f32x2_t lds2(const float* p) { return *reinterpret_cast<const f32x2_t*>(p); }
 
+// Activation outputs of the stage kernels are stored write-through (sc1): the line leaves the XCD's L2 while the
+// kernel still runs, so the dependent kernel boundary does not first write back megabytes of dirty L2 lines
+// (MI355X_MICROARCH.md, price row "boundary": + B / 6 TB/s for B dirty bytes).  The consumer is always the next
+// launch, which reads from MALL/HBM either way (its L2 is not coherent with the producer XCD's).
+#ifndef DTF_WT_ACT
+#define DTF_WT_ACT 1
+#endif
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+__device__ __forceinline__ void st_act8(bf16_t* p, uint2 v) {
+#if DTF_WT_ACT
+  __hip_atomic_store((gu64_t*)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+#else
+  *reinterpret_cast<uint2*>(p) = v;
+#endif
+}
+
 // T(8 channels c0..c0+7): MODE 1 relu(x*coef[c] + coef[64+c]); MODE 2 coef[c]*x + coef[64+c]*h + coef[128+c]
 template <int MODE>
 __device__ __forceinline__ uint4 xform8(uint4 v, uint4 v2, int c0, const float* __restrict__ coef) {
@@ -683,13 +700,21 @@ struct Stage {
                                           int gy0) const {
     const unsigned interior = m & ~top & ~bot;
     const int rb = gy0 * ROW * 2;
+#if DTF_WT_ACT
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(out, 0, H * ROW * 2, 0x00020000);  // one image
+#endif
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
       uint4 t = make_uint4(0, 0, 0, 0);
       if ((m >> j) & 1u) t = xform8r<MODE>(v[j], v2[j], v3[j], c0, coef);
       *reinterpret_cast<uint4*>(buf + loff[j]) = t;
-      if (out != nullptr && ((interior >> j) & 1u))
+      if (out != nullptr && ((interior >> j) & 1u)) {
+#if DTF_WT_ACT
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, t), rsrc, rb + goff[j], 0, 16);  // sc1
+#else
         *reinterpret_cast<uint4*>(reinterpret_cast<char*>(out) + (uint32_t)(rb + goff[j])) = t;
+#endif
+      }
     }
   }
 };
@@ -968,7 +993,7 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
       uint2 pk;
       pk.x = pk2(v0);
       pk.y = pk2(v1);
-      *reinterpret_cast<uint2*>(a.y + band + pofs[i]) = pk;
+      st_act8(a.y + band + pofs[i], pk);
       const f32x2_t r0v = unpk2(pk.x), r1v = unpk2(pk.y);
       ssum[0] += r0v;
       ssum[1] += r1v;
@@ -1707,7 +1732,7 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
       uint2 pk;
       pk.x = pk2(v0);
       pk.y = pk2(v1);
-      *reinterpret_cast<uint2*>(k_y + band + pofs[i]) = pk;
+      st_act8(k_y + band + pofs[i], pk);
       const f32x2_t dz0 = unpk2(pk.x), dz1 = unpk2(pk.y);
       ssum[0] += dz0;
       ssum[1] += dz1;

@@ -56,6 +56,8 @@ FUSED_MIN_WG = 256        # ... at least this many workgroups (one member would 
 FUSED_MAX_WG = {32: 128}  # ... at most this many per member (C = 32: fewer, fuller workgroups)
 PIGGYBACK_MAX_WG = 3000   # slab reductions ride on the next backward launch when they add <= this many workgroups
 DEFER_WG = {16: 64, 32: 32, 64: 16}  # deferred wgrad (small populations): workgroups per member and layer
+DEFER_LARGE_CS = (64,)    # larger populations defer the wgrad of these channel widths only ...
+DEFER_LARGE_WG = {16: 16, 32: 8, 64: 8}  # ... with this many workgroups per member and layer
 c_void_p, c_int, c_long = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
 
 
@@ -133,6 +135,7 @@ def _register():
     ops.register("dtf_dw_slab_reduce", [c_void_p, c_void_p, c_int, c_void_p, c_long, c_long, c_int, c_void_p])
     ops.register("dtf_conv_bwd_fused", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_bwd_dual", [P(ConvArgs), P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
+    ops.register("dtf_conv_bwd_dg", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_wgrad_multi", [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_dw_slab_reduce_multi", [c_void_p, c_int, c_int, c_void_p, c_long, c_int, c_void_p])
     ops.register("dtf_slab_job_size", [])
@@ -678,6 +681,11 @@ class _StepPlan:
         # those layers runs afterwards in a few wide launches (conv_wgrad_multi_kernel), one per (C, dY mode).
         # Their dY / x operands stay alive for the whole backward (per-block buffers instead of ping-pong ones).
         self.defer_wg = self.dual
+        # channel widths whose stride-1 wgrad is deferred: every width at small populations; at larger ones the
+        # C = 64 layers only (1 workgroup per CU of the fused kernel left the MFMA pipe idle, and its 147 KB dW slab
+        # per workgroup cost more than re-reading dY / x once in the wide wgrad launch)
+        v2gpu = dev.type == "cuda" and cfg.version == 2
+        self.defer_cs = {16, 32, 64} if self.defer_wg else (set(DEFER_LARGE_CS) if v2gpu else set())
         self._wg_jobs = {}  # (C, wgrad dY mode) -> [(ConvArgs, work table, grad offset)]
         self.launches = []
         self._pending_slab = None  # (slab ptr, reduce table, C, grad offset) of the last fused launch
@@ -999,7 +1007,7 @@ class _StepPlan:
         for t in (dy, dy2, dy3, dy_out, dz_out, x, res):
             assert t is None or tuple(t.shape) == (self.N, H, H, C), (t.shape, C, H)
         bands = H // rows
-        if self.dual and (C in DUAL_CS or self.defer_wg):
+        if (self.dual and (C in DUAL_CS or self.defer_wg)) or C in self.defer_cs:
             return self._conv_bwd_dual(ci, c, C, H, rows, bands, dy, dz_out, x, mode_dy, dy2, dy_bn, x_bn, res,
                                        ident_x, dy3, dy_out)
         n_wg = self._fused_nwg(C, bands)
@@ -1098,7 +1106,7 @@ class _StepPlan:
             b.st_ep = _p(be.st_f(x_bn))
         b.Hi, b.Wi, b.Ho, b.Wo, b.rows = H, H, H, H, rows
         b.cin_real = self._stamp_row("fused", "fused-wg C=%d mdy=%d epi=%d" % (C, mode_dy, epi))
-        if self.defer_wg:
+        if C in self.defer_cs:
             return self._defer_wgrad(ci, c, C, H, rows, bands, a, b, dy, x, mode_dy, dy2, dy_bn, x_bn, dy_out,
                                      tsz, epi)
         b.slab = _p(self._layer_slab(wwork.shape[0] * self._slab_elems(C)))
@@ -1129,15 +1137,8 @@ class _StepPlan:
         dgrad role materialises (``dy_out``) or the plain incoming gradient (mode 0), read as-is; else (conv_a)
         BN2-backward(dz2, h) recomputed while staging, as the dgrad role does."""
         lib = ops.lib()
-        # the launch's copy of the wgrad-role arguments has no workgroups (the launch is read when the plan runs,
-        # not here, so it must not share b, whose n_main the queued job keeps)
-        b0 = self._base_args()
-        ctypes.memmove(ctypes.addressof(b0), ctypes.addressof(b), ctypes.sizeof(ConvArgs))
-        b0.n_main = 0
         self._keep(a)
-        self._keep(b0)
-        self._add(lib.dtf_conv_bwd_dual, ctypes.byref(a), ctypes.byref(b0), C, mode_dy, epi, a.n_main,
-                  2304 + 2 * tsz * 2)
+        self._add(lib.dtf_conv_bwd_dg, ctypes.byref(a), C, mode_dy, epi, a.n_main, 2304 + 2 * tsz * 2)
         w = self._base_args()
         ctypes.memmove(ctypes.addressof(w), ctypes.addressof(b), ctypes.sizeof(ConvArgs))
         if dy_out is not None or mode_dy == 0:
@@ -1148,7 +1149,8 @@ class _StepPlan:
         else:
             wmode = 2
             assert mode_dy == 2 and dy2 is not None and dy_bn is not None
-        wwork = self._work_iters(bands, max(1, min(self.N * bands, DEFER_WG[C] * len(self.slots))))
+        per = DEFER_WG[C] if self.defer_wg else DEFER_LARGE_WG[C]
+        wwork = self._work_iters(bands, max(1, min(self.N * bands, per * len(self.slots))))
         w.work = _p(wwork)
         w.n_main = wwork.shape[0]
         self._set_uniform(w, wwork)
@@ -1358,7 +1360,7 @@ class _StepPlan:
             x, h = self.xs[i], self.hs[i]
             Hi, Ho = x.shape[1], h.shape[1]
             T = self.tmp[Ho]
-            if self.defer_wg:  # deferred wgrad: this block's dz2 is read again after the backward
+            if h.shape[3] in self.defer_cs:  # deferred wgrad: this block's dz2 is read again after the backward
                 T = dict(T, dz2=self._fresh_like(T["dz2"]))
             ca, cb = blk.convs
             # conv_b: dgrad -> dz2 (mask by BN2(h), BN2 reductions); wgrad
@@ -1400,7 +1402,7 @@ class _StepPlan:
                 self._conv_wgrad(ca, x, T["dz2"], mode_x=1, mode_dy=2, x_bn=bn1, dy_bn=bn2, dy2=h)
             # g_in = BN1-backward(dz1, x) [+ g_out if identity shortcut]
             g_next = Tin["g"][1] if g_cur is Tin["g"][0] else Tin["g"][0]
-            if self.defer_wg:  # every block's g stays alive for the deferred wgrad
+            if x.shape[3] in self.defer_cs:  # g (read by the previous block's deferred conv_b wgrad) stays alive
                 g_next = self._fresh_like(Tin["g"][0])
             add = None if blk.proj is not None else g_cur
             if i > 0:

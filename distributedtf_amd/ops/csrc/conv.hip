@@ -835,7 +835,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
       uint2 pk;
       pk.x = pack2bf(v[0], v[1]);
       pk.y = pack2bf(v[2], v[3]);
-      *reinterpret_cast<uint2*>(a.y + o) = pk;
+      st_act8(a.y + o, pk);
       if constexpr (STATS) {
         const float r0 = bf2f((bf16_t)(pk.x & 0xffff)), r1 = bf2f((bf16_t)(pk.x >> 16));
         const float r2 = bf2f((bf16_t)(pk.y & 0xffff)), r3 = bf2f((bf16_t)(pk.y >> 16));
@@ -1178,7 +1178,7 @@ __device__ __forceinline__ void conv_dgrad_body(const ConvArgs& a, const int bid
       uint2 pk;
       pk.x = pack2bf(v[0], v[1]);
       pk.y = pack2bf(v[2], v[3]);
-      *reinterpret_cast<uint2*>(a.y + o) = pk;
+      st_act8(a.y + o, pk);
       if constexpr (STATS) {
         const float dz[4] = {bf2f((bf16_t)(pk.x & 0xffff)), bf2f((bf16_t)(pk.x >> 16)), bf2f((bf16_t)(pk.y & 0xffff)),
                              bf2f((bf16_t)(pk.y >> 16))};
@@ -1873,6 +1873,14 @@ __global__ __launch_bounds__(256, FUSED_WAVES(C, MODE_DY)) void conv_bwd_dual_ke
   }
 }
 
+// dgrad role alone (the backward launch of a layer whose wgrad is deferred to conv_wgrad_multi_kernel): without the
+// wgrad role's accumulators the kernel fits two waves per SIMD (the dual kernel is register-capped at one).
+template <int C, int MODE_DY, int EPI>
+__global__ __launch_bounds__(256, 2) void conv_bwd_dg_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  conv_bwd_body<C, MODE_DY, EPI, 1>(a, (int)blockIdx.x, smem);
+}
+
 // Deferred weight gradients of small populations (engine/hip_resnet.py: one or two members per GPU).  The backward
 // launches of the stride-1 3x3 layers run only their dgrad role (the critical path: every layer waits for the
 // previous one's BatchNorm statistics), and the wgrad work of ALL the layers of one (C, MODE_DY) class runs here,
@@ -2179,6 +2187,23 @@ DTF_API int dtf_conv_bwd_dual(const ConvArgs* a, const ConvArgs* b, int c, int m
   DUAL_CASE(16, 2, 0) DUAL_CASE(32, 2, 0) DUAL_CASE(64, 2, 0)
   DUAL_CASE(16, 2, 1)
 #undef DUAL_CASE
+  return -1;
+}
+
+DTF_API int dtf_conv_bwd_dg(const ConvArgs* a, int c, int mode_dy, int epi, int nblocks, int lds, hipStream_t stream) {
+  if (nblocks <= 0) return 0;
+  DTF_HOST_CHECK(lds <= 160 * 1024);
+  DTF_HOST_CHECK(a->work != nullptr && nblocks == a->n_main);
+#define DG_CASE(CC, M, E)                                                                                    \
+  if (c == CC && mode_dy == M && epi == E) {                                                                \
+    hipLaunchKernelGGL((conv_bwd_dg_kernel<CC, M, E>), dim3(nblocks), dim3(256), lds, stream, *a);          \
+    return DTF_CHECK_LAUNCH();                                                                              \
+  }
+  DG_CASE(16, 0, 0) DG_CASE(32, 0, 0) DG_CASE(64, 0, 0)
+  DG_CASE(16, 3, 0) DG_CASE(32, 3, 0) DG_CASE(64, 3, 0)
+  DG_CASE(16, 2, 0) DG_CASE(32, 2, 0) DG_CASE(64, 2, 0)
+  DG_CASE(16, 2, 1)
+#undef DG_CASE
   return -1;
 }
 

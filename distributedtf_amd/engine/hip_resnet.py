@@ -58,6 +58,8 @@ PIGGYBACK_MAX_WG = 3000   # slab reductions ride on the next backward launch whe
 DEFER_WG = {16: 64, 32: 32, 64: 16}  # deferred wgrad (small populations): workgroups per member and layer
 DEFER_LARGE_CS = (64,)    # larger populations defer the wgrad of these channel widths only ...
 DEFER_LARGE_WG = {16: 16, 32: 8, 64: 8}  # ... with this many workgroups per member and layer
+DG_ITERS_LARGE = 2        # ... and (image, band) iterations per dgrad workgroup (the weights load once per workgroup)
+DG_MIN_WG = 512           # ... keeping at least this many dgrad workgroups
 c_void_p, c_int, c_long = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
 
 
@@ -1071,8 +1073,11 @@ class _StepPlan:
         lib = ops.lib()
         tsz = ((rows + 2) * _wpitch(C) * _cpad(C) + 8 + 63) // 64 * 64
         epi = int(res is not None) | (2 if ident_x else 0)
-        # ---- dgrad role: one (image, band) iteration per workgroup
-        work = self._work_iters(bands, self._det_cap(max(1, self.N * bands)))
+        # ---- dgrad role: one (image, band) iteration per workgroup (larger populations: DG_ITERS_LARGE)
+        n_dg = max(1, self.N * bands)
+        if not self.dual:
+            n_dg = min(n_dg, max(DG_MIN_WG, -(-n_dg // DG_ITERS_LARGE)))
+        work = self._work_iters(bands, self._det_cap(n_dg))
         a = self._base_args()
         a.x, a.x2, a.y, a.xm, a.res = _p(dy), _p(dy2), _p(dz_out), _p(x), _p(res)
         a.x3, a.xout = _p(dy3), _p(dy_out if mode_dy >= 2 else None)

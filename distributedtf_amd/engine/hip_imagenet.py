@@ -44,6 +44,8 @@ _CG_WIDE1 = True  # the wide tiles for 1x1 convs with Ci % 256 == 0
 _CG_TP256_128 = True  # 128 x 256 tiles (2 x 2 waves of 64 x 128)
 _CG_TP256 = True  # 256-pixel forward / dgrad tiles for 64-channel outputs
 _CG_WPK_WO64 = 32  # pixels per k-step of the 64-row tiles
+# stride-1 3x3 forward / data gradient with LDS-resident input rows (convg_t3_kernel): image width -> rows per tile
+_CG_T3 = {56: 8, 28: 7, 14: 14}  # must match dtf_convg_t3 (rows divide the image height)
 _CG_WG_TARGET = 512
 _CG_WG_MINCHUNK = 2048
 
@@ -91,6 +93,7 @@ def _register():
     P = ctypes.POINTER
     reg = ops.register
     reg("dtf_convg_fwd", [P(CgArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
+    reg("dtf_convg_t3", [P(CgArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
     reg("dtf_convg_wgrad", [P(CgArgs), c_int, c_int, c_int, c_void_p])
     reg("dtf_convg_wgrad_wide", [P(CgArgs), c_int, c_int, c_int, c_void_p])
     reg("dtf_cg_weight_prep", [c_void_p, c_long, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_long,
@@ -361,6 +364,17 @@ class _ImageNetPlan:
                         items.append([s, p0, min(p0 + tp, p_end), o0 | (cls << 16)])
         return self._hold(torch.tensor(items, dtype=torch.int32, device=self.be.dev))
 
+    def _band_work(self, hw, rows, co, tc):
+        """(slot, p0, p1, o0) tiles of `rows` whole image rows x tc output channels (convg_t3_kernel)."""
+        items = []
+        for s, n in zip(self.slots, self.sizes):
+            for img in range(self.first[s], self.first[s] + n):
+                for y0 in range(0, hw, rows):
+                    p0 = (img * hw + y0) * hw
+                    for o0 in range(0, co, tc):
+                        items.append([s, p0, p0 + min(rows, hw - y0) * hw, o0])
+        return self._hold(torch.tensor(items, dtype=torch.int32, device=self.be.dev))
+
     def _wgrad_work(self, hw_out, co, K, wo=128, wt=128):
         """(slot, p0, p1, o0 | n0/8 << 16) split-K items of the weight gradient: 128 x 128 dW tiles per member, the
         member's pixels split into chunks so that the launch has about ``_CG_WG_TARGET`` items.  Every item
@@ -435,6 +449,15 @@ class _ImageNetPlan:
             trans = (1 if c.stride > 1 else 0) | 2  # | 2: A operand k-major from the forward layout
         a.log2ci = _log2(a.Ci)
         tc = 128 if a.Co >= 128 else 64
+        if (k == 3 and c.stride == 1 and mode == 0 and hw_in in _CG_T3 and ci != be.prog.stem
+                and epi == (6 if dgrad else 4) and a.Ci % 32 == 0):
+            rows = _CG_T3[hw_in]
+            tc = 64 if hw_in == 56 else 128  # must match dtf_convg_t3's instantiations
+            work = self._band_work(hw_in, rows, a.Co, tc)
+            a.work = _p(work)
+            self._hold(a)
+            self._add(ops.lib().dtf_convg_t3, ctypes.byref(a), tc, epi, int(dgrad), hw_in, work.shape[0])
+            return
         # (a 256-row tile, 128 x 64 per wave, measured slower: 111.7 -> 123.4 ms/step at pop 8 x 128,
         # profiles/r2_imagenet_tc256_ab.log -- removed)
         tp = 128

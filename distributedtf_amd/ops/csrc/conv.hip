@@ -1401,7 +1401,8 @@ struct DenseJob {
 __global__ __launch_bounds__(256) void dense_slab_reduce_multi_kernel(const DenseJob* __restrict__ jobs,
                                                                       float* __restrict__ grads, long g_mstride) {
   __shared__ float part[8 * 33];
-  const DenseJob j = jobs[blockIdx.z];
+  DenseJob j = jobs[blockIdx.z];
+  kpin(j.slab), kpin(j.red);  // global (not flat) loads through the job's pointers
   if ((int)blockIdx.y >= j.nmem) return;  // workgroup-uniform
   const int el = threadIdx.x & 31, gg = threadIdx.x >> 5;
   const int4 rd = j.red[blockIdx.y];
@@ -1928,7 +1929,8 @@ __global__ __launch_bounds__(256) void dw_slab_reduce_multi_kernel(const SlabJob
   constexpr int MT = C / 16, NTN = 9 * C / 16, NJ = (NTN + 3) / 4, E = NJ * MT * 4 * 256;
   static_assert(E % 256 == 0, "whole 256-element blocks");
   __shared__ float4 part[4][64];
-  const SlabJob j = jobs[blockIdx.z];
+  SlabJob j = jobs[blockIdx.z];
+  kpin(j.slab), kpin(j.red);  // global (not flat) loads through the job's pointers
   if ((int)blockIdx.y >= j.nmem) return;  // workgroup-uniform
   const int4 rd = j.red[blockIdx.y];
   const int q = threadIdx.x & 63, gg = threadIdx.x >> 6;

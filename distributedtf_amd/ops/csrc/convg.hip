@@ -41,12 +41,18 @@ __device__ __forceinline__ s16x4_t ds_read_tr(const bf16_t* p) {
 // Branch-free predicated 16-byte load: a masked-off lane reads a zero vector in global memory.  A conditional load
 // makes hipcc branch around it and wait vmcnt(0) per element, which serialises a thread's gathers (PMC before
 // the change: 5-12 VALU per MFMA in these kernels).
-__device__ const uint4 g_zero16 = {0u, 0u, 0u, 0u};  // what a masked-off lane loads
+__device__ uint4 g_zero16 = {0u, 0u, 0u, 0u};  // what a masked-off lane loads (never written; not const: a const
+// __device__ variable lives in the constant address space, and a select with it made every gather a flat_load)
 
+typedef unsigned int u32x4v_t __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4v_t guint4_t;
 __device__ __forceinline__ uint4 ld16(const bf16_t* base, long off, bool ok) {
-  // a pointer select (2 VALU), not `ok ? load : 0` (hipcc turns that into a branch) nor a value mask (4 VALU)
-  const uint4* p = ok ? reinterpret_cast<const uint4*>(base + off) : &g_zero16;
-  return *p;
+  // a pointer select (2 VALU), not `ok ? load : 0` (hipcc turns that into a branch) nor a value mask (4 VALU).
+  // Both arms are GLOBAL-address-space pointers: a select between a generic pointer and a __device__ variable is a
+  // generic pointer, i.e. a flat_load -- which also counts in lgkmcnt, so every LDS-read wait of the k-loop
+  // drained the whole global prefetch behind it
+  guint4_t* p = ok ? (guint4_t*)(base + off) : (guint4_t*)&g_zero16;
+  return __builtin_bit_cast(uint4, *p);
 }
 
 struct CgArgs {
@@ -74,6 +80,145 @@ struct CgArgs {
   int cin_real;       // wgrad: real input channels of a channel-padded operand (stem: 3 of 8); 0 = Ci
 };
 
+
+// Epilogue shared by the forward / data-gradient kernels: the fp32 accumulator tile (wave grid WRN x 4/WRN of
+// (TC/WRN) x (TP/(4/WRN)) per wave) goes through LDS (cst, NHALF passes), then [+ residual], [mask by BN(xm)+ReLU],
+// bf16 store and per-channel statistics.
+template <int TC, int EPI, bool TRANS, int TP, int WRN, int NHALF>
+__device__ __forceinline__ void convg_epilogue(const CgArgs& a, f32x4_t (&acc)[TC / WRN / 16][TP / (4 / WRN) / 16],
+                                               float* cst, float (&acc_lds)[2][TC], int slot, int o0, int p0, int p1,
+                                               int HWo, int GW, int py, int px) {
+  constexpr int PW = TP / (4 / WRN), NTP = PW / 16, MT = TC / WRN / 16;
+  constexpr int CPF = TC + 4;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave % WRN, wc = wave / WRN;
+  // ---- epilogue through LDS: the fp32 tile is staged as [pixel][channel] rows (the k loop ended with a barrier,
+  // so the operand buffers are free), then every thread owns one 16-byte channel chunk of a pixel row: the
+  // residual / mask loads and the bf16 store are whole contiguous row segments (TC * 2 bytes per pixel) instead
+  // of 8-byte pieces of 16 pixel rows per wave instruction
+  constexpr int CH = TC / 8;     // 16-byte channel chunks per pixel row
+  constexpr int PPP = 256 / CH;  // pixel rows per pass of the workgroup
+  const int ch = tid % CH, pr = tid / CH;
+  const int oc = o0 + 8 * ch;
+  const bool cok = oc < a.Co;  // Co % 8 == 0 (host check)
+  float esc[8], esh[8], emu[8], eiv[8];
+  if constexpr (EPI & 2) {
+    const float* ep = a.c_ep + (long)slot * 4 * a.cmax + (cok ? oc : 0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float4 u0 = *reinterpret_cast<const float4*>(ep + 4 * h);
+      const float4 u1 = *reinterpret_cast<const float4*>(ep + a.cmax + 4 * h);
+      const float4 u2 = *reinterpret_cast<const float4*>(ep + 2 * a.cmax + 4 * h);
+      const float4 u3 = *reinterpret_cast<const float4*>(ep + 3 * a.cmax + 4 * h);
+      esc[4 * h] = u0.x; esc[4 * h + 1] = u0.y; esc[4 * h + 2] = u0.z; esc[4 * h + 3] = u0.w;
+      esh[4 * h] = u1.x; esh[4 * h + 1] = u1.y; esh[4 * h + 2] = u1.z; esh[4 * h + 3] = u1.w;
+      emu[4 * h] = u2.x; emu[4 * h + 1] = u2.y; emu[4 * h + 2] = u2.z; emu[4 * h + 3] = u2.w;
+      eiv[4 * h] = u3.x; eiv[4 * h + 1] = u3.y; eiv[4 * h + 2] = u3.z; eiv[4 * h + 3] = u3.w;
+    }
+  }
+  float ss[8], sq[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ss[i] = sq[i] = 0.f;
+  for (int h = 0; h < NHALF; ++h) {
+    if (h > 0) __syncthreads();  // the previous half's rows have been read
+#pragma unroll
+    for (int n = 0; n < NTP; ++n) {
+      const int pl = wc * PW + 16 * n - h * (TP / NHALF);  // staged row of this 16-pixel tile (wave-uniform)
+      if (NHALF == 1 || (pl >= 0 && pl < TP / NHALF)) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          *reinterpret_cast<f32x4_t*>(cst + (pl + (lane & 15)) * CPF + wr * (TC / WRN) + 16 * m + 4 * (lane >> 4)) =
+              acc[m][n];
+      }
+    }
+    __syncthreads();
+    // all residual / mask rows of this half are loaded before the first store (the stores may alias them for the
+    // compiler), so a thread keeps NPASS 16-byte loads in flight instead of one per pass
+    constexpr int NPASS = TP / NHALF / PPP;
+    long orow[NPASS];
+    uint4 rrv[NPASS], xrv[NPASS];
+#pragma unroll
+    for (int it = 0; it < NPASS; ++it) {
+      const int p = p0 + h * (TP / NHALF) + pr + PPP * it;
+      long pf = p;  // output pixel (full resolution)
+      if constexpr (TRANS) {
+        const int img = p / HWo, rem = p - img * HWo, qy = rem / GW, qx = rem - qy * GW;
+        pf = ((long)img * a.Ho + 2 * qy + py) * a.Wo + 2 * qx + px;
+      }
+      orow[it] = (p < p1 && cok) ? pf * a.Co + oc : -1;
+      rrv[it] = xrv[it] = make_uint4(0, 0, 0, 0);
+      if constexpr (EPI & 1) rrv[it] = ld16(a.res, orow[it], orow[it] >= 0);
+      if constexpr (EPI & 2) xrv[it] = ld16(a.xm, orow[it], orow[it] >= 0);
+    }
+#pragma unroll
+  for (int it = 0; it < NPASS; ++it) {
+    const int pl = pr + PPP * it;  // staged row
+    if (orow[it] < 0) continue;
+    const long o = orow[it];
+    const float4 c0 = *reinterpret_cast<const float4*>(cst + pl * CPF + 8 * ch);
+    const float4 c1 = *reinterpret_cast<const float4*>(cst + pl * CPF + 8 * ch + 4);
+    float v[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    const uint4 rr = rrv[it], xr = xrv[it];
+    const uint32_t r32[4] = {rr.x, rr.y, rr.z, rr.w}, x32[4] = {xr.x, xr.y, xr.z, xr.w};
+    float xv[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      xv[2 * q] = __uint_as_float(x32[q] << 16);
+      xv[2 * q + 1] = __uint_as_float(x32[q] & 0xffff0000u);
+      if constexpr (EPI & 1) {
+        v[2 * q] += __uint_as_float(r32[q] << 16);
+        v[2 * q + 1] += __uint_as_float(r32[q] & 0xffff0000u);
+      }
+    }
+    if constexpr (EPI & 2) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = (xv[i] * esc[i] + esh[i] > 0.f) ? v[i] : 0.f;
+    }
+    uint32_t pk[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pk[q] = pack2bf(v[2 * q], v[2 * q + 1]);
+    *reinterpret_cast<uint4*>(a.y + o) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    if constexpr (EPI & 4) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float r0 = __uint_as_float(pk[q] << 16), r1 = __uint_as_float(pk[q] & 0xffff0000u);
+        ss[2 * q] += r0;
+        ss[2 * q + 1] += r1;
+        if constexpr (EPI & 2) {
+          sq[2 * q] += r0 * (xv[2 * q] - emu[2 * q]) * eiv[2 * q];
+          sq[2 * q + 1] += r1 * (xv[2 * q + 1] - emu[2 * q + 1]) * eiv[2 * q + 1];
+        } else {
+          sq[2 * q] += r0 * r0;
+          sq[2 * q + 1] += r1 * r1;
+        }
+      }
+    }
+  }
+  }
+  if constexpr (EPI & 4) {
+    // lanes l, l + CH, l + 2 CH, .. of a wave hold the same channel chunk: butterfly over them, then one LDS
+    // atomic per wave and channel, one global atomic per workgroup and channel
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float s_ = ss[i], q_ = sq[i];
+#pragma unroll
+      for (int o = CH; o < 64; o <<= 1) {
+        s_ += __shfl_xor(s_, o, 64);
+        q_ += __shfl_xor(q_, o, 64);
+      }
+      if (lane < CH && cok) {
+        atomicAdd(&acc_lds[0][8 * ch + i], s_);
+        atomicAdd(&acc_lds[1][8 * ch + i], q_);
+      }
+    }
+    __syncthreads();
+    if (tid < TC && o0 + tid < a.Co) {
+      float* st = a.st_out + (long)slot * 2 * a.cmax;
+      atomicAdd(st + o0 + tid, acc_lds[0][tid]);
+      atomicAdd(st + a.cmax + o0 + tid, acc_lds[1][tid]);
+    }
+  }
+}
 
 // ---------------------------------------------------------------------------------------------- fwd / dgrad
 // MODE: 0 identity, 1 relu(x*s + t), 2 A*x + B*x2 + C.   EPI: bit0 residual, bit1 mask, bit2 stats (fwd: y, y^2;
@@ -356,133 +501,200 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
     }
     __syncthreads();
   }
-  // ---- epilogue through LDS: the fp32 tile is staged as [pixel][channel] rows (the k loop ended with a barrier,
-  // so the operand buffers are free), then every thread owns one 16-byte channel chunk of a pixel row: the
-  // residual / mask loads and the bf16 store are whole contiguous row segments (TC * 2 bytes per pixel) instead
-  // of 8-byte pieces of 16 pixel rows per wave instruction
-  float* cst = reinterpret_cast<float*>(smem_);
-  constexpr int CH = TC / 8;     // 16-byte channel chunks per pixel row
-  constexpr int PPP = 256 / CH;  // pixel rows per pass of the workgroup
-  const int ch = tid % CH, pr = tid / CH;
-  const int oc = o0 + 8 * ch;
-  const bool cok = oc < a.Co;  // Co % 8 == 0 (host check)
-  float esc[8], esh[8], emu[8], eiv[8];
-  if constexpr (EPI & 2) {
-    const float* ep = a.c_ep + (long)slot * 4 * a.cmax + (cok ? oc : 0);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const float4 u0 = *reinterpret_cast<const float4*>(ep + 4 * h);
-      const float4 u1 = *reinterpret_cast<const float4*>(ep + a.cmax + 4 * h);
-      const float4 u2 = *reinterpret_cast<const float4*>(ep + 2 * a.cmax + 4 * h);
-      const float4 u3 = *reinterpret_cast<const float4*>(ep + 3 * a.cmax + 4 * h);
-      esc[4 * h] = u0.x; esc[4 * h + 1] = u0.y; esc[4 * h + 2] = u0.z; esc[4 * h + 3] = u0.w;
-      esh[4 * h] = u1.x; esh[4 * h + 1] = u1.y; esh[4 * h + 2] = u1.z; esh[4 * h + 3] = u1.w;
-      emu[4 * h] = u2.x; emu[4 * h + 1] = u2.y; emu[4 * h + 2] = u2.z; emu[4 * h + 3] = u2.w;
-      eiv[4 * h] = u3.x; eiv[4 * h + 1] = u3.y; eiv[4 * h + 2] = u3.z; eiv[4 * h + 3] = u3.w;
-    }
+  convg_epilogue<TC, EPI, TRANS, TP, WRN, NHALF>(a, acc, reinterpret_cast<float*>(smem_), acc_lds, slot, o0, p0, p1,
+                                                  HWo, GW, py, px);
+}
+
+// ------------------------------------------------------------------------ stride-1 3x3: LDS-resident input rows
+// The generic kernel above gathers every (tap, channel-chunk) k-step of B from global memory: a 3x3 conv re-reads
+// each input row 9 times through L1 and spends 5-14 VALU per MFMA on per-tap gather addressing
+// (profiles/r2_s3_pmc_imagenet_after.txt).  Here a work item is R whole rows of one image (TP >= R*W pixels); for
+// each BK-channel chunk the (R+2) x (W+2) halo tile is staged in LDS ONCE (loads issued a whole chunk -- 9 k-steps
+// -- ahead) and the 9 taps read their B fragments from it at a constant offset.  A (weights) is staged per k-step
+// as in the generic kernel (AKM: data gradient straight from the forward layout, taps flipped).
+// k order: chunk c outer, tap t inner.  Forward: A columns t*Ci + c*BK; gathered rows y + t/3 - 1, x + t%3 - 1.
+template <int TP, int TC, int SOPS>
+__host__ __device__ constexpr int t3_nhalf() {
+  // smallest split of the fp32 epilogue staging (TP * (TC + 4) floats) that fits the operand buffers, with whole
+  // 16-pixel tiles and whole workgroup passes (256 / (TC / 8) pixel rows) per part
+  for (int n = 1; n <= TP / 16; ++n) {
+    if (TP % n != 0 || (TP / n) % 16 != 0 || (TP / n) % (2048 / TC) != 0) continue;
+    if (2 * TP * (TC + 4) / n <= SOPS) return n;
   }
-  float ss[8], sq[8];
+  return -1;
+}
+
+#ifndef DTF_T3_AD
+#define DTF_T3_AD 1
+#endif
+template <int TC, int EPI, bool AKM, int W, int R, int TP, int WRN, int AD = DTF_T3_AD>
+__global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
+  constexpr int BK = 32;
+  constexpr int PW = TP / (4 / WRN), NTP = PW / 16, MT = TC / WRN / 16;
+  static_assert(PW % 16 == 0 && TP >= R * W && W % R == 0, "pixel tile: whole rows, bands divide the image");
+  constexpr int RP = BK + 8;  // A row / staged-pixel pitch (bf16; +16 B)
+  constexpr int CPR = BK / 8, RPT = 256 / CPR;
+  constexpr int KPA = TC + 8;
+  constexpr int SA = (TC * RP > BK * KPA) ? TC * RP : BK * KPA;
+  constexpr int WT = W + 2, RT = R + 2, NBP = RT * WT;
+  constexpr int NBC = NBP * CPR, MAXB = (NBC + 255) / 256;
+  constexpr int SBT = NBP * RP + 8;  // + slack for the inactive staging slots
+  constexpr int SOPS = 2 * SA + SBT;
+  constexpr int NHALF = t3_nhalf<TP, TC, SOPS>();
+  static_assert(NHALF > 0, "epilogue staging split");
+  constexpr int SEPI = 2 * TP * (TC + 4) / NHALF;
+  __shared__ __attribute__((aligned(16))) bf16_t smem_[SOPS > SEPI ? SOPS : SEPI];
+  __shared__ float acc_lds[2][TC];
+  bf16_t (*sa)[SA] = reinterpret_cast<bf16_t (*)[SA]>(smem_);
+  bf16_t* sbt = smem_ + 2 * SA;
+  const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z > wk.y && wk.z - wk.y <= R * W && a.Wi == W && a.Hi % R == 0);
+  const int slot = wk.x, p0 = wk.y, p1 = wk.z, o0 = wk.w;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave % WRN, wc = wave / WRN;
+  const int Ci = a.Ci, H = a.Hi;
+  const int img = p0 / (H * W), y0 = (p0 - img * H * W) / W;
+  for (int i = tid; i < 2 * TC; i += 256) (&acc_lds[0][0])[i] = 0.f;
+  // B staging slots: chunk idx = tid + 256 j -> staged pixel (r, col), 8-channel piece c8
+  const bf16_t* xb = a.x + (long)img * H * W * Ci;
+  int bl[MAXB], bg[MAXB];
+  unsigned bok = 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) ss[i] = sq[i] = 0.f;
-  for (int h = 0; h < NHALF; ++h) {
-    if (h > 0) __syncthreads();  // the previous half's rows have been read
+  for (int j = 0; j < MAXB; ++j) {
+    const int idx = tid + 256 * j;
+    const int pix = idx / CPR, c8 = idx % CPR, r = pix / WT, col = pix % WT;
+    const int gy = y0 - 1 + r, gx = col - 1;
+    const bool ok = idx < NBC && gy >= 0 && gy < H && gx >= 0 && gx < W;
+    bl[j] = idx < NBC ? pix * RP + 8 * c8 : NBP * RP;
+    bg[j] = ok ? (gy * W + gx) * Ci + 8 * c8 : 0;
+    bok |= (unsigned)ok << j;
+  }
+  auto load_b = [&](int c, uint4 (&v)[MAXB]) {
 #pragma unroll
-    for (int n = 0; n < NTP; ++n) {
-      const int pl = wc * PW + 16 * n - h * (TP / NHALF);  // staged row of this 16-pixel tile (wave-uniform)
-      if (NHALF == 1 || (pl >= 0 && pl < TP / NHALF)) {
+    for (int j = 0; j < MAXB; ++j) v[j] = ld16(xb, bg[j] + c * BK, (bok >> j) & 1u);
+  };
+  auto store_b = [&](const uint4 (&v)[MAXB]) {
 #pragma unroll
-        for (int m = 0; m < MT; ++m)
-          *reinterpret_cast<f32x4_t*>(cst + (pl + (lane & 15)) * CPF + wr * (TC / WRN) + 16 * m + 4 * (lane >> 4)) =
-              acc[m][n];
+    for (int j = 0; j < MAXB; ++j) *reinterpret_cast<uint4*>(sbt + bl[j]) = v[j];
+  };
+  // A (weights), one k-step = (chunk c, tap t)
+  const bf16_t* wbase = a.w + (long)slot * a.w_mstride + a.w_off;
+  constexpr int AJ = TC * BK / 2048, ACH = TC / 8;
+  const int cB = tid % CPR, rB = tid / CPR;
+  auto load_a = [&](int c, int t, uint4 (&v)[AJ]) {
+    if constexpr (AKM) {  // rows of the k-major tile: dy channels c*BK + kr of forward tap 8 - t
+#pragma unroll
+      for (int j = 0; j < AJ; ++j) {
+        const int kr = tid / ACH + (256 / ACH) * j, ch = tid % ACH;
+        v[j] = ld16(wbase, ((long)(c * BK + kr) * 9 + (8 - t)) * a.Co + o0 + 8 * ch, o0 + 8 * ch < a.Co);
       }
+    } else {
+#pragma unroll
+      for (int j = 0; j < AJ; ++j) {
+        const int r = rB + RPT * j;
+        v[j] = ld16(wbase, (long)(o0 + r) * 9 * Ci + t * Ci + c * BK + 8 * cB, o0 + r < a.Co);
+      }
+    }
+  };
+  auto store_a = [&](bf16_t* dst, const uint4 (&v)[AJ]) {
+#pragma unroll
+    for (int j = 0; j < AJ; ++j) {
+      if constexpr (AKM)
+        *reinterpret_cast<uint4*>(dst + (tid / ACH + (256 / ACH) * j) * KPA + 8 * (tid % ACH)) = v[j];
+      else
+        *reinterpret_cast<uint4*>(dst + (rB + RPT * j) * RP + 8 * cB) = v[j];
+    }
+  };
+  // this lane's B fragment rows: pixel p = wc * PW + 16 n + lane % 16 of the tile -> staged pixel (y, x)
+  int bpo[NTP];
+#pragma unroll
+  for (int n = 0; n < NTP; ++n) {
+    int p = wc * PW + 16 * n + (lane & 15);
+    p = p < R * W ? p : 0;  // padding pixels (discarded by the epilogue) read pixel 0
+    bpo[n] = ((p / W) * WT + p % W) * RP + 8 * (lane >> 4);
+  }
+  f32x4_t acc[MT][NTP];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < NTP; ++n) acc[m][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  const int nch = Ci / BK, nk = 9 * nch;
+  // A (weights) is prefetched AD k-steps ahead: with AD = 2 the loop is unrolled by two over a pair of register
+  // sets, so every load / store names a fixed register set (a set picked by a runtime parity makes hipcc drain the
+  // prefetch with vmcnt(0) at the merge)
+  uint4 ra0[AJ], ra1[AJ], rb[MAXB];
+  load_b(0, rb);
+  load_a(0, 0, ra0);
+  if constexpr (AD == 2) load_a(0, 1, ra1);  // nk >= 9
+  store_b(rb);
+  store_a(sa[0], ra0);
+  __syncthreads();
+  // one k-step (chunk c, tap t): r_next holds A(ks + 1) (AD 2), r_free receives A(ks + AD)
+  auto kstep = [&](int ks, int c, int t, bf16_t* sa_cur, bf16_t* sa_nxt, uint4 (&r_next)[AJ], uint4 (&r_free)[AJ]) {
+    const bool more = ks + 1 < nk;
+    if constexpr (AD == 1) {
+      if (more) load_a(t == 8 ? c + 1 : c, t == 8 ? 0 : t + 1, r_free);
+    } else {
+      if (ks + 2 < nk) load_a(t >= 7 ? c + 1 : c, t >= 7 ? t - 7 : t + 2, r_free);
+    }
+    if (t == 0 && c + 1 < nch) load_b(c + 1, rb);  // next chunk's rows: 9 k-steps of latency cover
+    const int tapo = ((t / 3) * WT + t % 3) * RP;
+    bf16x8_t fa[MT], fb[NTP];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      if constexpr (AKM) {
+        const int g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
+        const int rb_ = wr * (TC / WRN) + 16 * m + 4 * p4;
+        const s16x4_t lo = ds_read_tr(sa_cur + (8 * g + q) * KPA + rb_);
+        const s16x4_t hi = ds_read_tr(sa_cur + (8 * g + 4 + q) * KPA + rb_);
+        fa[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      } else {
+        fa[m] = *reinterpret_cast<const bf16x8_t*>(sa_cur + (wr * (TC / WRN) + 16 * m + (lane & 15)) * RP +
+                                                   8 * (lane >> 4));
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NTP; ++n) fb[n] = *reinterpret_cast<const bf16x8_t*>(sbt + bpo[n] + tapo);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < NTP; ++n) acc[m][n] = mfma16(fa[m], fb[n], acc[m][n]);
+    if (more) {
+      if (t == 8) {  // chunk boundary: every wave is done with the staged rows
+        __syncthreads();
+        store_b(rb);
+      }
+      if constexpr (AD == 1)
+        store_a(sa_nxt, r_free);
+      else
+        store_a(sa_nxt, r_next);
     }
     __syncthreads();
-    // all residual / mask rows of this half are loaded before the first store (the stores may alias them for the
-    // compiler), so a thread keeps NPASS 16-byte loads in flight instead of one per pass
-    constexpr int NPASS = TP / NHALF / PPP;
-    long orow[NPASS];
-    uint4 rrv[NPASS], xrv[NPASS];
-#pragma unroll
-    for (int it = 0; it < NPASS; ++it) {
-      const int p = p0 + h * (TP / NHALF) + pr + PPP * it;
-      long pf = p;  // output pixel (full resolution)
-      if constexpr (TRANS) {
-        const int img = p / HWo, rem = p - img * HWo, qy = rem / GW, qx = rem - qy * GW;
-        pf = ((long)img * a.Ho + 2 * qy + py) * a.Wo + 2 * qx + px;
-      }
-      orow[it] = (p < p1 && cok) ? pf * a.Co + oc : -1;
-      rrv[it] = xrv[it] = make_uint4(0, 0, 0, 0);
-      if constexpr (EPI & 1) rrv[it] = ld16(a.res, orow[it], orow[it] >= 0);
-      if constexpr (EPI & 2) xrv[it] = ld16(a.xm, orow[it], orow[it] >= 0);
+  };
+  int c = 0, t = 0;
+  auto adv = [&]() {
+    if (++t == 9) {
+      t = 0;
+      ++c;
     }
-#pragma unroll
-  for (int it = 0; it < NPASS; ++it) {
-    const int pl = pr + PPP * it;  // staged row
-    if (orow[it] < 0) continue;
-    const long o = orow[it];
-    const float4 c0 = *reinterpret_cast<const float4*>(cst + pl * CPF + 8 * ch);
-    const float4 c1 = *reinterpret_cast<const float4*>(cst + pl * CPF + 8 * ch + 4);
-    float v[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-    const uint4 rr = rrv[it], xr = xrv[it];
-    const uint32_t r32[4] = {rr.x, rr.y, rr.z, rr.w}, x32[4] = {xr.x, xr.y, xr.z, xr.w};
-    float xv[8];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      xv[2 * q] = __uint_as_float(x32[q] << 16);
-      xv[2 * q + 1] = __uint_as_float(x32[q] & 0xffff0000u);
-      if constexpr (EPI & 1) {
-        v[2 * q] += __uint_as_float(r32[q] << 16);
-        v[2 * q + 1] += __uint_as_float(r32[q] & 0xffff0000u);
-      }
+  };
+  if constexpr (AD == 1) {
+    for (int ks = 0; ks < nk; ++ks) {
+      kstep(ks, c, t, sa[ks & 1], sa[(ks & 1) ^ 1], ra0, ra0);
+      adv();
     }
-    if constexpr (EPI & 2) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = (xv[i] * esc[i] + esh[i] > 0.f) ? v[i] : 0.f;
-    }
-    uint32_t pk[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) pk[q] = pack2bf(v[2 * q], v[2 * q + 1]);
-    *reinterpret_cast<uint4*>(a.y + o) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-    if constexpr (EPI & 4) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float r0 = __uint_as_float(pk[q] << 16), r1 = __uint_as_float(pk[q] & 0xffff0000u);
-        ss[2 * q] += r0;
-        ss[2 * q + 1] += r1;
-        if constexpr (EPI & 2) {
-          sq[2 * q] += r0 * (xv[2 * q] - emu[2 * q]) * eiv[2 * q];
-          sq[2 * q + 1] += r1 * (xv[2 * q + 1] - emu[2 * q + 1]) * eiv[2 * q + 1];
-        } else {
-          sq[2 * q] += r0 * r0;
-          sq[2 * q + 1] += r1 * r1;
-        }
+  } else {
+    for (int ks = 0; ks < nk; ks += 2) {
+      kstep(ks, c, t, sa[0], sa[1], ra1, ra0);
+      adv();
+      if (ks + 1 < nk) {
+        kstep(ks + 1, c, t, sa[1], sa[0], ra0, ra1);
+        adv();
       }
     }
   }
-  }
-  if constexpr (EPI & 4) {
-    // lanes l, l + CH, l + 2 CH, .. of a wave hold the same channel chunk: butterfly over them, then one LDS
-    // atomic per wave and channel, one global atomic per workgroup and channel
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float s_ = ss[i], q_ = sq[i];
-#pragma unroll
-      for (int o = CH; o < 64; o <<= 1) {
-        s_ += __shfl_xor(s_, o, 64);
-        q_ += __shfl_xor(q_, o, 64);
-      }
-      if (lane < CH && cok) {
-        atomicAdd(&acc_lds[0][8 * ch + i], s_);
-        atomicAdd(&acc_lds[1][8 * ch + i], q_);
-      }
-    }
-    __syncthreads();
-    if (tid < TC && o0 + tid < a.Co) {
-      float* st = a.st_out + (long)slot * 2 * a.cmax;
-      atomicAdd(st + o0 + tid, acc_lds[0][tid]);
-      atomicAdd(st + a.cmax + o0 + tid, acc_lds[1][tid]);
-    }
-  }
+  convg_epilogue<TC, EPI, false, TP, WRN, NHALF>(a, acc, reinterpret_cast<float*>(smem_), acc_lds, slot, o0, p0, p1,
+                                                 0, 0, 0, 0);
 }
 
 // ---------------------------------------------------------------------------------------------- wgrad
@@ -907,6 +1119,29 @@ DTF_API int dtf_convg_fwd(const CgArgs* a, int tc, int mode, int epi, int trans,
   CG_ALL_TC(2, 0, true, 1)
 #undef CG_ALL_TC
 #undef CG_CASE
+  return -1;
+}
+
+// Stride-1 3x3 conv / data gradient with LDS-resident input rows (convg_t3_kernel).  w: image width (56: 8-row
+// tiles of 448 pixels, 64-channel tiles; 28: 7 rows, 14: whole 14-row images, 224-pixel tiles of 128 channels);
+// epi 4 (forward, statistics) or 6 (data gradient: mask + statistics, akm = 1).
+DTF_API int dtf_convg_t3(const CgArgs* a, int tc, int epi, int akm, int w, int nwork, hipStream_t stream) {
+  if (nwork <= 0) return 0;
+  if (a->kh != 3 || a->kw != 3 || a->stride != 1 || a->pad != 1 || a->Wi != w || a->Hi != w || a->Ho != w ||
+      a->Ci % 32 != 0 || (a->Co & 7) != 0)
+    return -2;
+  dim3 grid(nwork), block(256);
+#define T3_CASE(TC_, E_, AK_, W_, R_, TP_, WRN_)                                                              \
+  if (tc == TC_ && epi == E_ && akm == AK_ && w == W_) {                                                    \
+    hipLaunchKernelGGL((convg_t3_kernel<TC_, E_, AK_, W_, R_, TP_, WRN_>), grid, block, 0, stream, *a);     \
+    return DTF_CHECK_LAUNCH();                                                                              \
+  }
+#define T3_GEO(E_, AK_) T3_CASE(64, E_, AK_, 56, 8, 448, 1) T3_CASE(128, E_, AK_, 28, 7, 224, 2) \
+  T3_CASE(128, E_, AK_, 14, 14, 224, 2)
+  T3_GEO(4, false)
+  T3_GEO(6, true)
+#undef T3_GEO
+#undef T3_CASE
   return -1;
 }
 

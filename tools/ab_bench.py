@@ -3,7 +3,8 @@
     python tools/ab_bench.py --set FWD_ITERS_PER_WG=1 --set DUAL_WG.64=32 --set DUAL_CS=32:64 -- --pop 8 --steps 60
 
 Each ``--set`` overrides one module constant of ``engine/hip_resnet.py`` in this process only: ``NAME=int``,
-``NAME.key=int`` for a dict constant, ``NAME=a:b:c`` for a tuple of ints.  Everything after ``--`` goes to
+``NAME.key=int`` for a dict constant, ``NAME=a:b:c`` for a tuple of ints, ``NAME=`` empties a dict constant;
+``imagenet:NAME...`` addresses ``engine/hip_imagenet.py`` instead.  Everything after ``--`` goes to
 ``bench.py``.  Values are parsed as integers (no evaluation of the text).
 """
 import os
@@ -14,10 +15,15 @@ sys.path.insert(0, os.path.dirname(HERE))
 
 
 def apply(sets):
-    from distributedtf_amd.engine import hip_resnet as hr
+    from distributedtf_amd.engine import hip_imagenet, hip_resnet
     for item in sets:
         name, val = item.split("=", 1)
-        if "." in name:
+        hr = hip_resnet
+        if name.startswith("imagenet:"):  # a constant of engine/hip_imagenet.py
+            hr, name = hip_imagenet, name[len("imagenet:"):]
+        if isinstance(getattr(hr, name, None), dict) and val == "":
+            getattr(hr, name).clear()  # NAME= empties a dict constant (e.g. switches a per-shape path off)
+        elif "." in name:
             base, key = name.split(".", 1)
             d = getattr(hr, base)
             assert isinstance(d, dict), base

@@ -107,7 +107,7 @@ class BnEwArgs(ctypes.Structure):
         ("img_slot", c_void_p), ("params", c_void_p), ("p_mstride", c_long),
         ("g1", c_int), ("b1", c_int), ("g2", c_int), ("b2", c_int),
         ("st1", c_void_p), ("st2", c_void_p), ("sb1", c_void_p), ("sb2", c_void_p), ("cnt", c_void_p),
-        ("hw", c_int), ("C", c_int), ("nimg", c_long),
+        ("hw", c_int), ("C", c_int), ("nimg", c_long), ("cap", c_int), ("pad_", c_int),
     ]
 
 
@@ -442,7 +442,7 @@ class HipResNetBackend:
         shrinking active set), "1", "0")."""
         mode = os.environ.get("DTF_ELASTIC", "auto")
         cap = int(os.environ.get("DTF_ELASTIC_MAXB", "256"))
-        if (mode == "0" or self.dev.type != "cuda" or self.L.cfg.version == 1 or self.e.dp is not None
+        if (mode == "0" or self.dev.type != "cuda" or self.e.dp is not None
                 or max(sizes) > cap or (mode == "auto" and len(set(sizes)) == 1 and not force)):
             return None
         return cap
@@ -1556,6 +1556,7 @@ class _StepPlan:
             a.g2, a.b2 = self._bn(bn2)
             a.st2, a.sb2 = _p(self._st_r(bn2)), _p(be.st_b(bn2))
         a.cnt, a.hw, a.C, a.nimg = _p(self.cnt), hw, C, self.N
+        a.cap = self.sizes[0] if self.elastic else 0  # elastic: skip each member's capacity padding
         self._keep(a)
         self._add(fn, ctypes.byref(a))
 

@@ -536,9 +536,12 @@ __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
   constexpr int CPR = BK / 8, RPT = 256 / CPR;
   constexpr int KPA = TC + 8;
   constexpr int SA = (TC * RP > BK * KPA) ? TC * RP : BK * KPA;
-  constexpr int WT = W + 2, RT = R + 2, NBP = RT * WT;
+  // staged tile: RT rows x WS columns (halo), LDS row pitch WT = W + 16 pixels: a 16-pixel fragment that wraps to
+  // the next image row then shifts by 16 pixel pitches (80 B = 20 banks each, 5 x 16 = 0 mod 16 bank quads), so
+  // its 16 lanes still hit 16 distinct bank quads (with pitch W + 2 every wrapping fragment had 2-way conflicts)
+  constexpr int WS = W + 2, WT = W + 16, RT = R + 2, NBP = RT * WS;
   constexpr int NBC = NBP * CPR, MAXB = (NBC + 255) / 256;
-  constexpr int SBT = NBP * RP + 8;  // + slack for the inactive staging slots
+  constexpr int SBT = RT * WT * RP + 8;  // + slack for the inactive staging slots
   constexpr int SOPS = 2 * SA + SBT;
   constexpr int NHALF = t3_nhalf<TP, TC, SOPS>();
   static_assert(NHALF > 0, "epilogue staging split");
@@ -562,10 +565,10 @@ __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
 #pragma unroll
   for (int j = 0; j < MAXB; ++j) {
     const int idx = tid + 256 * j;
-    const int pix = idx / CPR, c8 = idx % CPR, r = pix / WT, col = pix % WT;
+    const int pix = idx / CPR, c8 = idx % CPR, r = pix / WS, col = pix % WS;
     const int gy = y0 - 1 + r, gx = col - 1;
     const bool ok = idx < NBC && gy >= 0 && gy < H && gx >= 0 && gx < W;
-    bl[j] = idx < NBC ? pix * RP + 8 * c8 : NBP * RP;
+    bl[j] = idx < NBC ? (r * WT + col) * RP + 8 * c8 : RT * WT * RP;
     bg[j] = ok ? (gy * W + gx) * Ci + 8 * c8 : 0;
     bok |= (unsigned)ok << j;
   }

@@ -596,7 +596,15 @@ struct BnEwArgs {
   const float* cnt;
   int hw, C;
   long nimg;
+  int cap;            // elastic plan: images per member region (an image is real iff img % cap < cnt[slot]); 0: exact
+  int pad_;
 };
+
+// Elastic plans lay member k's images at [k * cap, (k + 1) * cap) and only the first cnt[slot] of them are real:
+// the per-image BN kernels skip the rest (a capacity-padded image must not enter the BatchNorm reductions)
+__device__ __forceinline__ bool idle_image(const BnEwArgs& a, int img, int slot) {
+  return a.cap > 0 && (float)(img % a.cap) >= a.cnt[slot];
+}
 
 __device__ __forceinline__ void fwd_coef2(const float* st, float n, float gamma, float beta, int c, float& scale,
                                           float& shift, float& mean, float& inv) {
@@ -613,6 +621,7 @@ __global__ __launch_bounds__(256) void bn_add_relu_kernel(BnEwArgs a) {
   __shared__ float co[4 * 64];
   const int img = blockIdx.x;
   const int slot = a.img_slot[img];
+  if (idle_image(a, img, slot)) return;  // workgroup-uniform
   const int C = a.C;
   if (threadIdx.x < C) {
     const int c = threadIdx.x;
@@ -667,6 +676,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnEwArgs a) {
   __shared__ float acc[3 * 64];
   const int img = blockIdx.x;
   const int slot = a.img_slot[img];
+  if (idle_image(a, img, slot)) return;  // workgroup-uniform
   const int C = a.C;
   if (threadIdx.x < C) {
     const int c = threadIdx.x;

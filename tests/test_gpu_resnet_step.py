@@ -136,12 +136,14 @@ def test_hip_step_matches_reference(size, graph, version, sizes, monkeypatch):
     _compare_step(ResNetArch(cifar_config(size, version=version)), sizes)
 
 
+@pytest.mark.parametrize("version", [2, 1])
 @pytest.mark.parametrize("elastic", ["auto", "0"])
-def test_hip_step_elastic_plan(elastic, monkeypatch):
+def test_hip_step_elastic_plan(elastic, version, monkeypatch):
     """Mixed batch sizes run on ONE capacity-keyed plan (DTF_ELASTIC): the work tables are regenerated on the device
     from the per-member sizes each step, so a batch-size change (PBT explore of batch_size) reuses the captured
     graph.  Warm-up with sizes (20, 9, 14), then the compared graph replay with (12, 17, 6) vs the fp32 oracle;
-    DTF_ELASTIC=0 (exact plans, one per size tuple) as the control."""
+    DTF_ELASTIC=0 (exact plans, one per size tuple) as the control.  v1: the per-image BN kernels (bn_add_relu,
+    bn_bwd_reduce) skip each member's capacity padding."""
     monkeypatch.setenv("DTF_HIP_GRAPH", "1")
     monkeypatch.setenv("DTF_ELASTIC", elastic)
     monkeypatch.setenv("DTF_ELASTIC_MAXB", "24")
@@ -155,7 +157,7 @@ def test_hip_step_elastic_plan(elastic, monkeypatch):
         else:
             assert len(plans) == 2 and not any(p.elastic for p in plans.values())
 
-    _compare_step(ResNetArch(cifar_config(14, version=2)), [12, 17, 6], warm_sizes=[20, 9, 14], check=check)
+    _compare_step(ResNetArch(cifar_config(14, version=version)), [12, 17, 6], warm_sizes=[20, 9, 14], check=check)
 
 
 @pytest.mark.parametrize("size,sizes", [(56, [128] * 8), (56, [128]), (110, [128, 128])])

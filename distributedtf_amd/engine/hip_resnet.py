@@ -50,7 +50,7 @@ DUAL_WG = {16: 128, 32: 128, 64: 64}  # wgrad-role workgroups per member of a du
 FWD_ITERS_PER_WG = 4      # forward: (image, band) iterations per workgroup (>= 256 workgroups kept)
 HEAD_ITEMS = 512          # head / GAP+dense+CE work items
 WGRAD_WG_PER_MEMBER = 128  # standalone wgrad launches: workgroups per member (bounds the dW partial traffic)
-DENSE_REDUCE_BLOCKS = 256  # dense_slab_reduce_multi: max 32-element blocks per job
+DENSE_REDUCE_BLOCKS = 256  # slab_reduce_all, dense jobs: max 32-element blocks per job
 FUSED_SLAB_BYTES = {16: 16e6, 32: 16e6, 64: 48e6}  # fused backward: per-launch dW slab budget -> workgroup count
 FUSED_MIN_WG = 256        # ... at least this many workgroups (one member would leave CUs idle otherwise)
 FUSED_MAX_WG = {32: 128}  # ... at most this many per member (C = 32: fewer, fuller workgroups)
@@ -138,11 +138,10 @@ def _register():
     ops.register("dtf_conv_bwd_fused", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_bwd_dual", [P(ConvArgs), P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_bwd_dg", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
-    ops.register("dtf_conv_wgrad_multi", [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p])
-    ops.register("dtf_dw_slab_reduce_multi", [c_void_p, c_int, c_int, c_void_p, c_long, c_int, c_void_p])
+    ops.register("dtf_conv_wgrad_all", [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p])
+    ops.register("dtf_slab_reduce_all", [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_void_p])
     ops.register("dtf_slab_job_size", [])
     ops.register("dtf_dense_job_size", [])
-    ops.register("dtf_dense_slab_reduce_multi", [c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_void_p])
     ops.register("dtf_conv_args_size", [])
     ops.register("dtf_bnbwd_args_size", [])
     ops.register("dtf_head_args_size", [])
@@ -680,7 +679,7 @@ class _StepPlan:
         self.dual = dev.type == "cuda" and cfg.version == 2 and len(slots) <= DUAL_MAX_POP
         # Deferred weight gradients (the same small populations): each stride-1 layer's backward launch runs only
         # its dgrad role -- the critical path, serialised by the BatchNorm statistics -- and the wgrad work of all
-        # those layers runs afterwards in a few wide launches (conv_wgrad_multi_kernel), one per (C, dY mode).
+        # those layers runs afterwards in two wide launches (conv_wgrad_all_kernel: widths 64 + 32, width 16).
         # Their dY / x operands stay alive for the whole backward (per-block buffers instead of ping-pong ones).
         self.defer_wg = self.dual
         # channel widths whose stride-1 wgrad is deferred: every width at small populations; at larger ones the
@@ -1138,7 +1137,7 @@ class _StepPlan:
 
     def _defer_wgrad(self, ci, c, C, H, rows, bands, a, b, dy, x, mode_dy, dy2, dy_bn, x_bn, dy_out, tsz, epi):
         """Deferred-wgrad form of a dual launch: the launch holds the dgrad role only; the wgrad job (the role's
-        arguments with its own work split) is queued for conv_wgrad_multi_kernel.  Its dY operand: the dY the
+        arguments with its own work split) is queued for conv_wgrad_all_kernel.  Its dY operand: the dY the
         dgrad role materialises (``dy_out``) or the plain incoming gradient (mode 0), read as-is; else (conv_a)
         BN2-backward(dz2, h) recomputed while staging, as the dgrad role does."""
         lib = ops.lib()
@@ -1164,22 +1163,30 @@ class _StepPlan:
         self._wg_jobs.setdefault((C, wmode), []).append((w, wwork, c.off))
 
     def _emit_deferred_wgrad(self):
-        """One conv_wgrad_multi launch per (C, dY mode) over every queued layer; their slabs join the per-C
-        reductions of _flush_deferred."""
+        """Every queued layer's wgrad job in two launches (conv_wgrad_all_kernel: widths 64 + 32 -- one wave per SIMD
+        -- and width 16, kept apart at its higher occupancy); their slabs join the reduction of _flush_deferred.
+        One launch per (C, dY mode) measured 18 us slower at pop 1 (profiles/r3_merged_launches_ab.log)."""
         lib = ops.lib()
-        for (C, wmode), jobs in sorted(self._wg_jobs.items()):
-            arr = (ConvArgs * len(jobs))()
-            wmap = []
-            for j, (w, work, goff) in enumerate(jobs):
-                arr[j] = w
-                wmap += [(j, k) for k in range(w.n_main)]
-                self._deferred.append((w.slab, self._slab_table(work), goff, C))
+        for cset, widths in ((0, (64, 32)), (1, (16,))):  # must match dtf_conv_wgrad_all's instantiations
+            arr_l, wmap, lds = [], [], 0
+            for (C, wmode), jobs in sorted(self._wg_jobs.items(), key=lambda kv: (-kv[0][0], -kv[0][1])):
+                if C not in widths:
+                    continue
+                tsz = ((8 + 2) * _wpitch(C) * _cpad(C) + 8 + 63) // 64 * 64
+                lds = max(lds, 2304 + 4 * tsz * 2)
+                for (w, work, goff) in jobs:
+                    j = len(arr_l)
+                    arr_l.append(w)
+                    wmap += [(j, k, C, wmode) for k in range(w.n_main)]
+                    self._deferred.append((w.slab, self._slab_table(work), goff, C))
+            if not arr_l:
+                continue
+            arr = (ConvArgs * len(arr_l))(*arr_l)
             jt = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.be.dev)
             mt = torch.tensor(wmap, dtype=torch.int32, device=self.be.dev)
             self._keep(jt)
             self._keep(mt)
-            tsz = ((8 + 2) * _wpitch(C) * _cpad(C) + 8 + 63) // 64 * 64
-            self._add(lib.dtf_conv_wgrad_multi, _p(jt), _p(mt), len(wmap), C, wmode, 2304 + 4 * tsz * 2)
+            self._add(lib.dtf_conv_wgrad_all, _p(jt), _p(mt), len(wmap), cset, lds)
         self._wg_jobs = {}
 
     def _fresh_like(self, t):
@@ -1200,31 +1207,28 @@ class _StepPlan:
         return self._slab_elems(rc) // 32
 
     def _flush_deferred(self):
-        """One reduction launch over every deferred C = 64 slab (dw_slab_reduce_multi_kernel) and one over every
-        dense wgrad slab (dense_slab_reduce_multi_kernel)."""
-        if self._deferred_dense:
-            jobs = (DenseJob * len(self._deferred_dense))()
-            nmax = bmax = 0
-            for i, (buf, red, goff, kel) in enumerate(self._deferred_dense):
-                jobs[i] = DenseJob(buf, _p(red), goff, kel, red.shape[0])
-                nmax = max(nmax, red.shape[0])
-                bmax = max(bmax, -(-kel // 32))
-            jt = torch.frombuffer(bytearray(bytes(jobs)), dtype=torch.uint8).to(self.be.dev)
-            self._keep(jt)
-            self._add(ops.lib().dtf_dense_slab_reduce_multi, _p(jt), len(self._deferred_dense), nmax,
-                      min(bmax, DENSE_REDUCE_BLOCKS), _p(self.e.grads), self.e.Pp)
-            self._deferred_dense = []
-        for C in sorted({d[3] for d in self._deferred}):
-            sel = [d for d in self._deferred if d[3] == C]
-            jobs = (SlabJob * len(sel))()
-            nmax = 0
-            for i, (buf, red, goff, _) in enumerate(sel):
-                jobs[i] = SlabJob(buf, _p(red), goff, red.shape[0], 0)
-                nmax = max(nmax, red.shape[0])
-            jt = torch.frombuffer(bytearray(bytes(jobs)), dtype=torch.uint8).to(self.be.dev)
-            self._keep(jt)
-            self._add(ops.lib().dtf_dw_slab_reduce_multi, _p(jt), len(sel), nmax, _p(self.e.grads), self.e.Pp, C)
-        self._deferred = []
+        """Every deferred dW slab (conv slabs of each width, dense wgrad slabs) reduced by one launch
+        (slab_reduce_all_kernel; one launch per width plus one for the dense slabs measured 10 us slower)."""
+        if not (self._deferred or self._deferred_dense):
+            return
+        sj = (SlabJob * max(1, len(self._deferred)))()
+        dj = (DenseJob * max(1, len(self._deferred_dense)))()
+        nmax = bmax = 0
+        for i, (buf, red, goff, C) in enumerate(self._deferred):
+            sj[i] = SlabJob(buf, _p(red), goff, red.shape[0], C)
+            nmax = max(nmax, red.shape[0])
+            bmax = max(bmax, self._slab_elems(C) // 256)
+        for i, (buf, red, goff, kel) in enumerate(self._deferred_dense):
+            dj[i] = DenseJob(buf, _p(red), goff, kel, red.shape[0])
+            nmax = max(nmax, red.shape[0])
+            bmax = max(bmax, min(-(-kel // 32), DENSE_REDUCE_BLOCKS))
+        st = torch.frombuffer(bytearray(bytes(sj)), dtype=torch.uint8).to(self.be.dev)
+        dt = torch.frombuffer(bytearray(bytes(dj)), dtype=torch.uint8).to(self.be.dev)
+        self._keep(st)
+        self._keep(dt)
+        self._add(ops.lib().dtf_slab_reduce_all, _p(st), len(self._deferred), _p(dt), len(self._deferred_dense),
+                  nmax, bmax, _p(self.e.grads), self.e.Pp)
+        self._deferred, self._deferred_dense = [], []
 
     def _flush_slab(self):
         """Standalone reduction of a pending slab (no later fused launch can take it)."""

@@ -1338,7 +1338,7 @@ __device__ __forceinline__ void conv_wgrad_body(const ConvArgs& a, const int bid
   }
   // epilogue: D[co][n] with co = m*16 + 4*(lane>>4) + r, n-col = lane & 15.  With a slab: this workgroup's dense
   // partial dW (every element of [co][tap][ci < cin_real] written once, plain stores), summed in workgroup order by
-  // dense_slab_reduce_multi_kernel; else fp32 atomics into the gradient row.
+  // slab_reduce_all_kernel; else fp32 atomics into the gradient row.
   const int KK = K * K;
   const long kel = (long)COUT * KK * a.cin_real;
   float* gb = a.slab ? a.slab + (long)bid * kel : a.grads + (long)slot * a.g_mstride + a.g_off;
@@ -1397,38 +1397,6 @@ struct DenseJob {
   int kel;
   int nmem;
 };
-
-__global__ __launch_bounds__(256) void dense_slab_reduce_multi_kernel(const DenseJob* __restrict__ jobs,
-                                                                      float* __restrict__ grads, long g_mstride) {
-  __shared__ float part[8 * 33];
-  DenseJob j = jobs[blockIdx.z];
-  kpin(j.slab), kpin(j.red);  // global (not flat) loads through the job's pointers
-  if ((int)blockIdx.y >= j.nmem) return;  // workgroup-uniform
-  const int el = threadIdx.x & 31, gg = threadIdx.x >> 5;
-  const int4 rd = j.red[blockIdx.y];
-  for (int bx = blockIdx.x; bx * 32 < j.kel; bx += gridDim.x) {
-    const int e = bx * 32 + el;
-    const bool ok = e < j.kel;
-    float s0 = 0.f, s1 = 0.f;
-    int g = gg;
-    for (; g + 8 < rd.y; g += 16) {
-      if (ok) {
-        s0 += j.slab[(long)(rd.x + g) * j.kel + e];
-        s1 += j.slab[(long)(rd.x + g + 8) * j.kel + e];
-      }
-    }
-    if (g < rd.y && ok) s0 += j.slab[(long)(rd.x + g) * j.kel + e];
-    part[gg * 33 + el] = s0 + s1;
-    __syncthreads();
-    if (gg == 0 && ok) {
-      float sum = 0.f;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) sum += part[i * 33 + el];
-      grads[(long)rd.w * g_mstride + j.g_off + e] += sum;
-    }
-    __syncthreads();
-  }
-}
 
 // One workgroup of the dW slab reduction (see dw_slab_reduce_kernel): 32 slab elements of member row `by`.
 // Blocks bx0, bx0 + bstride, ... of 32 slab elements (workgroup-uniform loop: every thread reaches each barrier).
@@ -1874,7 +1842,7 @@ __global__ __launch_bounds__(256, FUSED_WAVES(C, MODE_DY)) void conv_bwd_dual_ke
   }
 }
 
-// dgrad role alone (the backward launch of a layer whose wgrad is deferred to conv_wgrad_multi_kernel): without the
+// dgrad role alone (the backward launch of a layer whose wgrad is deferred to conv_wgrad_all_kernel): without the
 // wgrad role's accumulators the kernel fits two waves per SIMD (the dual kernel is register-capped at one).
 template <int C, int MODE_DY, int EPI>
 __global__ __launch_bounds__(256, 2) void conv_bwd_dg_kernel(ConvArgs a) {
@@ -1882,19 +1850,26 @@ __global__ __launch_bounds__(256, 2) void conv_bwd_dg_kernel(ConvArgs a) {
   conv_bwd_body<C, MODE_DY, EPI, 1>(a, (int)blockIdx.x, smem);
 }
 
-// Deferred weight gradients of small populations (engine/hip_resnet.py: one or two members per GPU).  The backward
-// launches of the stride-1 3x3 layers run only their dgrad role (the critical path: every layer waits for the
-// previous one's BatchNorm statistics), and the wgrad work of ALL the layers of one (C, MODE_DY) class runs here,
-// afterwards, as ONE wide launch -- hundreds of independent workgroups instead of a wgrad role that stretched every
-// latency-bound backward launch.  jobs[j]: the wgrad-role arguments of layer j (dY / x operands kept alive for the
-// whole backward, own dW slab); map[block] = (job, workgroup index within the job).
-template <int C, int MODE_DY>
-__global__ __launch_bounds__(256, 1) void conv_wgrad_multi_kernel(const ConvArgs* __restrict__ jobs,
-                                                                    const int2* __restrict__ map) {
+// Deferred weight gradients (engine/hip_resnet.py): the backward launches of a deferred layer run only their dgrad
+// role (the critical path: every layer waits for the previous one's BatchNorm statistics), and the wgrad work of
+// all those layers runs afterwards as wide launches (conv_wgrad_all_kernel) -- hundreds of independent workgroups
+// instead of a wgrad role that stretched every latency-bound backward launch.  jobs[j]: the wgrad-role arguments
+// of layer j (dY / x operands kept alive for the whole backward, own dW slab).
+// The deferred wgrad jobs of the channel widths CA and CB (both dY modes) in ONE launch: map[block] = (job,
+// workgroup index, C, mode); the jobs of different layers / widths overlap instead of each launch draining its own
+// tail.  <64, 32> (register-heavy, one wave per SIMD) and <16, 16> (kept apart: it runs at several waves per SIMD).
+template <int CA, int CB>
+__global__ __launch_bounds__(256, 1) void conv_wgrad_all_kernel(const ConvArgs* __restrict__ jobs,
+                                                                const int4* __restrict__ map) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int2 m = map[blockIdx.x];
+  const int4 m = map[blockIdx.x];
   const int j = __builtin_amdgcn_readfirstlane(m.x), bid = __builtin_amdgcn_readfirstlane(m.y);
-  conv_bwd_body<C, MODE_DY, 0, 2>(jobs[j], bid, smem);
+  const int c = __builtin_amdgcn_readfirstlane(m.z), mode = __builtin_amdgcn_readfirstlane(m.w);
+  if (c == CA) {
+    if (mode == 0) conv_bwd_body<CA, 0, 0, 2>(jobs[j], bid, smem); else conv_bwd_body<CA, 2, 0, 2>(jobs[j], bid, smem);
+  } else if constexpr (CB != CA) {
+    if (mode == 0) conv_bwd_body<CB, 0, 0, 2>(jobs[j], bid, smem); else conv_bwd_body<CB, 2, 0, 2>(jobs[j], bid, smem);
+  }
 }
 
 // Sum of one member's per-workgroup dW slabs (written by conv_bwd_fused_kernel) into its gradient row.
@@ -1920,49 +1895,81 @@ struct SlabJob {
   int pad;
 };
 
-// blockIdx.z = job (one layer), y = member row of its reduce table, x = block of 256 slab elements.  Thread t reads
-// elements 4*(t%64)..+3 (float4) of every 4th slab starting at t/64, four loads in flight; the 4 partial sums meet
-// in LDS and thread t finishes element t (fixed summation order).
-template <int C>
-__global__ __launch_bounds__(256) void dw_slab_reduce_multi_kernel(const SlabJob* __restrict__ jobs,
-                                                                   float* __restrict__ grads, long g_mstride) {
-  constexpr int MT = C / 16, NTN = 9 * C / 16, NJ = (NTN + 3) / 4, E = NJ * MT * 4 * 256;
-  static_assert(E % 256 == 0, "whole 256-element blocks");
-  __shared__ float4 part[4][64];
-  SlabJob j = jobs[blockIdx.z];
-  kpin(j.slab), kpin(j.red);  // global (not flat) loads through the job's pointers
-  if ((int)blockIdx.y >= j.nmem) return;  // workgroup-uniform
+// Every deferred dW reduction of a step in ONE launch (x = block of 256 slab elements, y = member row of the job's
+// reduce table, z = job).  z < nsj: a conv slab job (channel width C in SlabJob.pad): thread t reads elements
+// 4*(t%64)..+3 (float4) of every 4th slab starting at t/64, four loads in flight; the partial sums meet in LDS and
+// thread t finishes element t (fixed summation order).  Else dense job z - nsj: 32 elements x 8 slab groups per
+// block, LDS reduction across the groups.  Blocks past a job's extent exit (workgroup-uniform).
+__global__ __launch_bounds__(256) void slab_reduce_all_kernel(const SlabJob* __restrict__ sjobs, int nsj,
+                                                              const DenseJob* __restrict__ djobs,
+                                                              float* __restrict__ grads, long g_mstride) {
+  __shared__ float4 part4[4][64];
+  if ((int)blockIdx.z < nsj) {
+    SlabJob j = sjobs[blockIdx.z];
+    kpin(j.slab), kpin(j.red);
+    const int C = j.pad, MT = C / 16, NTN = 9 * C / 16, NJ = (NTN + 3) / 4, E = NJ * MT * 4 * 256;
+    if ((int)blockIdx.y >= j.nmem || (int)blockIdx.x * 256 >= E) return;
+    const int4 rd = j.red[blockIdx.y];
+    const int q = threadIdx.x & 63, gg = threadIdx.x >> 6;
+    const int e0 = blockIdx.x * 256;
+    const float4* p = reinterpret_cast<const float4*>(j.slab + (long)rd.x * E + e0) + q;
+    const long E4 = E / 4;
+    float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0, s3 = s0;
+    int g = gg;
+    for (; g + 12 < rd.y; g += 16) {
+      const float4 a0 = p[(long)g * E4], a1 = p[(long)(g + 4) * E4], a2 = p[(long)(g + 8) * E4],
+                   a3 = p[(long)(g + 12) * E4];
+      s0.x += a0.x; s0.y += a0.y; s0.z += a0.z; s0.w += a0.w;
+      s1.x += a1.x; s1.y += a1.y; s1.z += a1.z; s1.w += a1.w;
+      s2.x += a2.x; s2.y += a2.y; s2.z += a2.z; s2.w += a2.w;
+      s3.x += a3.x; s3.y += a3.y; s3.z += a3.z; s3.w += a3.w;
+    }
+    for (; g < rd.y; g += 4) {
+      const float4 a0 = p[(long)g * E4];
+      s0.x += a0.x; s0.y += a0.y; s0.z += a0.z; s0.w += a0.w;
+    }
+    part4[gg][q] = make_float4((s0.x + s1.x) + (s2.x + s3.x), (s0.y + s1.y) + (s2.y + s3.y),
+                               (s0.z + s1.z) + (s2.z + s3.z), (s0.w + s1.w) + (s2.w + s3.w));
+    __syncthreads();
+    const float* pf = reinterpret_cast<const float*>(part4);
+    const int t0 = threadIdx.x;
+    const float sum = (pf[t0] + pf[256 + t0]) + (pf[512 + t0] + pf[768 + t0]);
+    const int e = e0 + t0;
+    const int r = e & 3, t = (e >> 2) & 255, m = (e >> 10) % MT, jj = (e >> 10) / MT;  // slab [j][m][t][r]
+    const int wave = t >> 6, lane = t & 63, nt = wave + 4 * jj;
+    if (nt < NTN) {
+      const int tap = (nt * 16) / C, ci = (nt * 16) % C + (lane & 15), co = m * 16 + 4 * (lane >> 4) + r;
+      grads[(long)rd.w * g_mstride + j.g_off + ((long)co * 9 + tap) * C + ci] += sum;
+    }
+    return;
+  }
+  float* part = reinterpret_cast<float*>(part4);  // [8][33]
+  DenseJob j = djobs[blockIdx.z - nsj];
+  kpin(j.slab), kpin(j.red);
+  if ((int)blockIdx.y >= j.nmem) return;
+  const int el = threadIdx.x & 31, gg = threadIdx.x >> 5;
   const int4 rd = j.red[blockIdx.y];
-  const int q = threadIdx.x & 63, gg = threadIdx.x >> 6;
-  const int e0 = blockIdx.x * 256;
-  const float4* p = reinterpret_cast<const float4*>(j.slab + (long)rd.x * E + e0) + q;
-  constexpr long E4 = E / 4;
-  float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0, s3 = s0;
-  int g = gg;
-  for (; g + 12 < rd.y; g += 16) {
-    const float4 a0 = p[(long)g * E4], a1 = p[(long)(g + 4) * E4], a2 = p[(long)(g + 8) * E4],
-                 a3 = p[(long)(g + 12) * E4];
-    s0.x += a0.x; s0.y += a0.y; s0.z += a0.z; s0.w += a0.w;
-    s1.x += a1.x; s1.y += a1.y; s1.z += a1.z; s1.w += a1.w;
-    s2.x += a2.x; s2.y += a2.y; s2.z += a2.z; s2.w += a2.w;
-    s3.x += a3.x; s3.y += a3.y; s3.z += a3.z; s3.w += a3.w;
-  }
-  for (; g < rd.y; g += 4) {
-    const float4 a0 = p[(long)g * E4];
-    s0.x += a0.x; s0.y += a0.y; s0.z += a0.z; s0.w += a0.w;
-  }
-  part[gg][q] = make_float4((s0.x + s1.x) + (s2.x + s3.x), (s0.y + s1.y) + (s2.y + s3.y),
-                            (s0.z + s1.z) + (s2.z + s3.z), (s0.w + s1.w) + (s2.w + s3.w));
-  __syncthreads();
-  const float* pf = reinterpret_cast<const float*>(part);
-  const int t0 = threadIdx.x;
-  const float sum = (pf[t0] + pf[256 + t0]) + (pf[512 + t0] + pf[768 + t0]);
-  const int e = e0 + t0;
-  const int r = e & 3, t = (e >> 2) & 255, m = (e >> 10) % MT, jj = (e >> 10) / MT;  // slab [j][m][t][r]
-  const int wave = t >> 6, lane = t & 63, nt = wave + 4 * jj;
-  if (nt < NTN) {
-    const int tap = (nt * 16) / C, ci = (nt * 16) % C + (lane & 15), co = m * 16 + 4 * (lane >> 4) + r;
-    grads[(long)rd.w * g_mstride + j.g_off + ((long)co * 9 + tap) * C + ci] += sum;
+  for (int bx = blockIdx.x; bx * 32 < j.kel; bx += gridDim.x) {
+    const int e = bx * 32 + el;
+    const bool ok = e < j.kel;
+    float s0 = 0.f, s1 = 0.f;
+    int g = gg;
+    for (; g + 8 < rd.y; g += 16) {
+      if (ok) {
+        s0 += j.slab[(long)(rd.x + g) * j.kel + e];
+        s1 += j.slab[(long)(rd.x + g + 8) * j.kel + e];
+      }
+    }
+    if (g < rd.y && ok) s0 += j.slab[(long)(rd.x + g) * j.kel + e];
+    part[gg * 33 + el] = s0 + s1;
+    __syncthreads();
+    if (gg == 0 && ok) {
+      float sum = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sum += part[i * 33 + el];
+      grads[(long)rd.w * g_mstride + j.g_off + e] += sum;
+    }
+    __syncthreads();
   }
 }
 
@@ -2031,31 +2038,14 @@ DTF_API int dtf_dw_slab_reduce(const float* slab, const int4* red, int nmembers,
 DTF_API int dtf_slab_job_size() { return (int)sizeof(SlabJob); }
 DTF_API int dtf_dense_job_size() { return (int)sizeof(DenseJob); }
 
-DTF_API int dtf_dense_slab_reduce_multi(const void* jobs, int njobs, int max_members, int max_blocks, float* grads,
-                                        long g_mstride, hipStream_t stream) {
-  if (njobs <= 0 || max_members <= 0 || max_blocks <= 0) return 0;
-  DTF_HOST_CHECK(jobs != nullptr && njobs <= 65535);
-  hipLaunchKernelGGL(dense_slab_reduce_multi_kernel, dim3(max_blocks, max_members, njobs), dim3(256), 0, stream,
-                     reinterpret_cast<const DenseJob*>(jobs), grads, g_mstride);
+DTF_API int dtf_slab_reduce_all(const void* sjobs, int nsj, const void* djobs, int ndj, int max_members, int max_blocks,
+                                float* grads, long g_mstride, hipStream_t stream) {
+  if (nsj + ndj <= 0 || max_members <= 0 || max_blocks <= 0) return 0;
+  DTF_HOST_CHECK((nsj == 0 || sjobs != nullptr) && (ndj == 0 || djobs != nullptr) && nsj + ndj <= 65535);
+  hipLaunchKernelGGL(slab_reduce_all_kernel, dim3(max_blocks, max_members, nsj + ndj), dim3(256), 0, stream,
+                     reinterpret_cast<const SlabJob*>(sjobs), nsj, reinterpret_cast<const DenseJob*>(djobs), grads,
+                     g_mstride);
   return DTF_CHECK_LAUNCH();
-}
-
-DTF_API int dtf_dw_slab_reduce_multi(const void* jobs, int njobs, int max_members, float* grads, long g_mstride, int c,
-                                     hipStream_t stream) {
-  if (njobs <= 0 || max_members <= 0) return 0;
-  DTF_HOST_CHECK(jobs != nullptr && njobs <= 65535);
-#define REDM_CASE(CC)                                                                                        \
-  if (c == CC) {                                                                                            \
-    constexpr int E = ((9 * CC / 16 + 3) / 4) * (CC / 16) * 4 * 256;                                         \
-    hipLaunchKernelGGL(dw_slab_reduce_multi_kernel<CC>, dim3(E / 256, max_members, njobs), dim3(256), 0,    \
-                       stream, reinterpret_cast<const SlabJob*>(jobs), grads, g_mstride);                   \
-    return DTF_CHECK_LAUNCH();                                                                              \
-  }
-  REDM_CASE(16)
-  REDM_CASE(32)
-  REDM_CASE(64)
-#undef REDM_CASE
-  return -1;
 }
 
 DTF_DEBUG_EXPORT(conv)
@@ -2209,20 +2199,17 @@ DTF_API int dtf_conv_bwd_dg(const ConvArgs* a, int c, int mode_dy, int epi, int 
   return -1;
 }
 
-DTF_API int dtf_conv_wgrad_multi(const void* jobs, const void* map, int nblocks, int c, int mode_dy, int lds,
-                                 hipStream_t stream) {
+// cset 0: widths 64 and 32; 1: width 16
+DTF_API int dtf_conv_wgrad_all(const void* jobs, const void* map, int nblocks, int cset, int lds, hipStream_t stream) {
   if (nblocks <= 0) return 0;
-  DTF_HOST_CHECK(jobs != nullptr && map != nullptr && lds <= 160 * 1024);
-#define WM_CASE(CC, M)                                                                                          \
-  if (c == CC && mode_dy == M) {                                                                               \
-    hipLaunchKernelGGL((conv_wgrad_multi_kernel<CC, M>), dim3(nblocks), dim3(256), lds, stream,                \
-                       reinterpret_cast<const ConvArgs*>(jobs), reinterpret_cast<const int2*>(map));            \
-    return DTF_CHECK_LAUNCH();                                                                                 \
-  }
-  WM_CASE(16, 0) WM_CASE(32, 0) WM_CASE(64, 0)
-  WM_CASE(16, 2) WM_CASE(32, 2) WM_CASE(64, 2)
-#undef WM_CASE
-  return -1;
+  DTF_HOST_CHECK(jobs != nullptr && map != nullptr && lds <= 160 * 1024 && (cset == 0 || cset == 1));
+  if (cset == 0)
+    hipLaunchKernelGGL((conv_wgrad_all_kernel<64, 32>), dim3(nblocks), dim3(256), lds, stream,
+                       reinterpret_cast<const ConvArgs*>(jobs), reinterpret_cast<const int4*>(map));
+  else
+    hipLaunchKernelGGL((conv_wgrad_all_kernel<16, 16>), dim3(nblocks), dim3(256), lds, stream,
+                       reinterpret_cast<const ConvArgs*>(jobs), reinterpret_cast<const int4*>(map));
+  return DTF_CHECK_LAUNCH();
 }
 
 DTF_API int dtf_conv_wgrad(const ConvArgs* args, int cin, int cout, int s, int k, int mode_x, int mode_dy,

@@ -120,6 +120,11 @@ def test_hip_mnist_step_matches_reference(graph, monkeypatch):
         logits = arch.forward(p, None, x, training=True, dtype=torch.float32, dropout_mask=mask[first:first + n])
         loss = torch.nn.functional.cross_entropy(logits, y)
         gref, = torch.autograd.grad(loss, p)
+        # the same step through PyTorch in bf16: its distance from the fp32 oracle is the scale of the bf16 rounding
+        # (max-pool argmax / ReLU decisions flipped by bf16 activations reroute whole gradient entries)
+        p16 = before[s].detach().clone().requires_grad_(True)
+        logits16 = arch.forward(p16, None, x, training=True, dtype=torch.bfloat16, dropout_mask=mask[first:first + n])
+        g16, = torch.autograd.grad(torch.nn.functional.cross_entropy(logits16.float(), y), p16)
         assert abs(float(losses[slots.index(s)]) - float(loss)) < 3e-2 * max(1.0, abs(float(loss)))
         for name, (off, shp) in arch.offsets.items():
             numel = 1
@@ -127,11 +132,8 @@ def test_hip_mnist_step_matches_reference(graph, monkeypatch):
                 numel *= d
             a, b = g_hip[s, off:off + numel], gref[off:off + numel]
             err = _relerr(a, b)
-            # conv parameters: the bf16 forward flips some max-pool argmax / ReLU decisions against the fp32 oracle,
-            # which reroutes whole entries of the conv output gradient (3-6 % observed for conv2_w / conv2_b at
-            # these ragged batch sizes)
-            tol = 0.08 if name.startswith("conv") else 0.05
-            assert err < tol, "%s member %d rel err %.4f" % (name, s, err)
+            tol = max(0.05, 2.5 * _relerr(g16[off:off + numel], b))  # as the ResNet / ImageNet tests
+            assert err < tol, "%s member %d rel err %.4f (tol %.4f)" % (name, s, err, tol)
         first += n
 
 

@@ -56,6 +56,8 @@ FUSED_MIN_WG = 256        # ... at least this many workgroups (one member would 
 FUSED_MAX_WG = {32: 128}  # ... at most this many per member (C = 32: fewer, fuller workgroups)
 PIGGYBACK_MAX_WG = 3000   # slab reductions ride on the next backward launch when they add <= this many workgroups
 DEFER_WG = {16: 64, 32: 32, 64: 16}  # deferred wgrad (small populations): workgroups per member and layer
+DEFER_MID_POP = 4         # up to this many members: defer the wgrad of DEFER_MID_CS ...
+DEFER_MID_CS = (32, 64)
 DEFER_LARGE_CS = (64,)    # larger populations defer the wgrad of these channel widths only ...
 DEFER_LARGE_WG = {16: 16, 32: 8, 64: 8}  # ... with this many workgroups per member and layer
 DG_ITERS_LARGE = 2        # ... and (image, band) iterations per dgrad workgroup (the weights load once per workgroup)
@@ -682,11 +684,13 @@ class _StepPlan:
         # those layers runs afterwards in two wide launches (conv_wgrad_all_kernel: widths 64 + 32, width 16).
         # Their dY / x operands stay alive for the whole backward (per-block buffers instead of ping-pong ones).
         self.defer_wg = self.dual
-        # channel widths whose stride-1 wgrad is deferred: every width at small populations; at larger ones the
-        # C = 64 layers only (1 workgroup per CU of the fused kernel left the MFMA pipe idle, and its 147 KB dW slab
-        # per workgroup cost more than re-reading dY / x once in the wide wgrad launch)
+        # channel widths whose stride-1 wgrad is deferred: every width at small populations; up to 4 members C = 32
+        # and 64, at larger ones the C = 64 layers only (1 workgroup per CU of the fused kernel left the MFMA pipe
+        # idle, and its 147 KB dW slab per workgroup cost more than re-reading dY / x once in the wide wgrad
+        # launch; profiles/r3_defer_ab.log)
         v2gpu = dev.type == "cuda" and cfg.version == 2
-        self.defer_cs = {16, 32, 64} if self.defer_wg else (set(DEFER_LARGE_CS) if v2gpu else set())
+        large = DEFER_MID_CS if len(slots) <= DEFER_MID_POP else DEFER_LARGE_CS
+        self.defer_cs = {16, 32, 64} if self.defer_wg else (set(large) if v2gpu else set())
         self._wg_jobs = {}  # (C, wgrad dY mode) -> [(ConvArgs, work table, grad offset)]
         self.launches = []
         self._pending_slab = None  # (slab ptr, reduce table, C, grad offset) of the last fused launch

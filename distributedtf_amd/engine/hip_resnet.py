@@ -109,7 +109,7 @@ class BnEwArgs(ctypes.Structure):
         ("img_slot", c_void_p), ("params", c_void_p), ("p_mstride", c_long),
         ("g1", c_int), ("b1", c_int), ("g2", c_int), ("b2", c_int),
         ("st1", c_void_p), ("st2", c_void_p), ("sb1", c_void_p), ("sb2", c_void_p), ("cnt", c_void_p),
-        ("hw", c_int), ("C", c_int), ("nimg", c_long), ("cap", c_int), ("pad_", c_int),
+        ("hw", c_int), ("C", c_int), ("nimg", c_long), ("cap", c_int), ("pad_", c_int), ("slab", c_void_p),
     ]
 
 
@@ -163,6 +163,7 @@ def _register():
     ops.register("dtf_bn_bwd_apply", [P(BnBwdArgs), c_void_p])
     ops.register("dtf_bn_add_relu", [P(BnEwArgs), c_void_p])
     ops.register("dtf_bn_bwd_reduce", [P(BnEwArgs), c_void_p])
+    ops.register("dtf_bn_bwd_reduce_finish", [P(BnEwArgs), c_void_p, c_void_p, c_int, c_void_p])
     ops.register("dtf_bnew_args_size", [])
     ops.register("dtf_head", [P(HeadArgs), c_int, c_void_p])
     ops.register("dtf_head_bwd_apply", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_int,
@@ -403,8 +404,6 @@ class HipResNetBackend:
         self.wd = torch.zeros(cap, self.L.wtot, dtype=torch.bfloat16, device=self.dev)
         nb = len(self.L.prog.bns)
         self.det = ops.build_deterministic()  # what the loaded library was compiled as
-        if self.det and self.L.cfg.version != 2:
-            raise ValueError("the deterministic HIP build covers the ResNet v2 step; use --backend torch for v1")
         NREP = self.nrep = _nrep()
         self.stats_bn_stride = cap * NREP * 128
         # [fwd | bwd] statistic accumulators: zeroed by ONE memset per step
@@ -1565,8 +1564,18 @@ class _StepPlan:
             a.st2, a.sb2 = _p(self._st_r(bn2)), _p(be.st_b(bn2))
         a.cnt, a.hw, a.C, a.nimg = _p(self.cnt), hw, C, self.N
         a.cap = self.sizes[0] if self.elastic else 0  # elastic: skip each member's capacity padding
+        det_reduce = self.be.det and d is not None
+        if det_reduce:  # deterministic build: per-image partial rows, added per member in image order
+            if getattr(self, "_det_rows", None) is None:
+                self._det_rows = torch.zeros(self.N * 192, dtype=torch.float32, device=self.be.dev)
+                self._first_t = torch.tensor([self.first[s] for s in self.slots], dtype=torch.int32,
+                                             device=self.be.dev)
+            a.slab = _p(self._det_rows)
         self._keep(a)
         self._add(fn, ctypes.byref(a))
+        if det_reduce:
+            self._add(ops.lib().dtf_bn_bwd_reduce_finish, ctypes.byref(a), _p(self._first_t), _p(self.slots_t),
+                      len(self.slots))
 
     def _build_v1(self):
         """ResNet v1 (``_building_block_v1``, resnet_model.py:127-168): conv -> BN -> ReLU -> conv -> BN

@@ -598,6 +598,7 @@ struct BnEwArgs {
   long nimg;
   int cap;            // elastic plan: images per member region (an image is real iff img % cap < cnt[slot]); 0: exact
   int pad_;
+  float* slab;        // deterministic build, bn_bwd_reduce: per-image partial sums [nimg][3][64]
 };
 
 // Elastic plans lay member k's images at [k * cap, (k + 1) * cap) and only the first cnt[slot] of them are real:
@@ -722,6 +723,33 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnEwArgs a) {
       }
     }
   }
+#ifdef DTF_DETERMINISTIC
+  // fixed order: every thread's 8-channel partials to LDS, thread c sums its channel's owners in thread order and
+  // stores the image's partial row; bn_bwd_reduce_finish_kernel adds a member's rows in image order (one launch
+  // per image: gridDim.y == 1)
+  __shared__ float part[3][256][8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    part[0][threadIdx.x][k] = i0 < n8 ? sd[k] : 0.f;
+    part[1][threadIdx.x][k] = i0 < n8 ? s1[k] : 0.f;
+    part[2][threadIdx.x][k] = i0 < n8 ? s2[k] : 0.f;
+  }
+  __syncthreads();
+  if (threadIdx.x < C) {
+    const int c = threadIdx.x, g = C / 8;
+    float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+    for (int t = c / 8; t < 256; t += g) {
+      t0 += part[0][t][c & 7];
+      t1 += part[1][t][c & 7];
+      t2 += part[2][t][c & 7];
+    }
+    float* row = a.slab + (long)img * 192;
+    row[c] = t0;
+    row[64 + c] = t1;
+    row[128 + c] = t2;
+  }
+  (void)acc;
+#else
   if (i0 < n8) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -742,6 +770,31 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnEwArgs a) {
       atomicAdd(&r2[c], acc[c]);
       atomicAdd(&r2[64 + c], acc[128 + c]);
     }
+  }
+#endif
+}
+
+// Deterministic build: a member's BN-backward reductions = its images' partial rows (bn_bwd_reduce_kernel) added in
+// image order, stored in replica 0 of the member's accumulators (the others stay zero).  grid = members.
+__global__ __launch_bounds__(64) void bn_bwd_reduce_finish_kernel(BnEwArgs a, const int* __restrict__ first,
+                                                                  const int* __restrict__ slots) {
+  const int s = slots[blockIdx.x], f = first[blockIdx.x], n = (int)a.cnt[s];
+  const int c = threadIdx.x;
+  if (c >= a.C) return;
+  float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+  for (int i = 0; i < n; ++i) {
+    const float* row = a.slab + (long)(f + i) * 192;
+    t0 += row[c];
+    t1 += row[64 + c];
+    t2 += row[128 + c];
+  }
+  float* r1 = a.sb1 + (long)s * NREP * 128;
+  r1[c] += t0;
+  r1[64 + c] += t1;
+  if (a.h2) {
+    float* r2 = a.sb2 + (long)s * NREP * 128;
+    r2[c] += t0;
+    r2[64 + c] += t2;
   }
 }
 
@@ -837,6 +890,9 @@ DTF_API int dtf_head_bwd_apply(const bf16_t* x, const float* dfeat, bf16_t* out,
 }
 
 static int ew_split(const BnEwArgs* a) {
+#ifdef DTF_DETERMINISTIC
+  if (a->slab != nullptr) return 1;  // bn_bwd_reduce: one workgroup (one partial row) per image
+#endif
   const int n8 = a->hw * a->C / 8;
   int split = (int)((2048 + a->nimg - 1) / a->nimg);
   const int max_split = (n8 + 255) / 256;
@@ -856,6 +912,19 @@ DTF_API int dtf_bn_bwd_reduce(const BnEwArgs* a, hipStream_t stream) {
   if (a->nimg <= 0) return 0;
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((unsigned)a->nimg, ew_split(a)), dim3(256), 0, stream, *a);
   return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_bn_bwd_reduce_finish(const BnEwArgs* a, const int* first, const int* slots, int nslots,
+                                     hipStream_t stream) {
+#ifdef DTF_DETERMINISTIC
+  if (nslots <= 0) return 0;
+  DTF_HOST_CHECK(a->slab != nullptr && a->C <= 64);
+  hipLaunchKernelGGL(bn_bwd_reduce_finish_kernel, dim3(nslots), dim3(64), 0, stream, *a, first, slots);
+  return DTF_CHECK_LAUNCH();
+#else
+  (void)a, (void)first, (void)slots, (void)nslots, (void)stream;
+  return -1;  // release builds reduce with replicated atomics inside bn_bwd_reduce_kernel
+#endif
 }
 
 DTF_DEBUG_EXPORT(resnet_aux)

@@ -209,11 +209,10 @@ class MainArgs(argparse.Namespace):
 
 
 def hip_deterministic(args) -> bool:
-    """Model families whose HIP step has a deterministic (bitwise-replayable) build: CIFAR ResNet v2 (64 statistic
-    replicas, capped workgroups) and MNIST (one workgroup per member for every accumulation)."""
-    if args.model == "mnist":
-        return True
-    return args.model == "cifar10" and int(getattr(args, "resnet_version", 2) or 2) == 2
+    """Model families whose HIP step has a deterministic (bitwise-replayable) build: CIFAR ResNet v2 and v1 (64
+    statistic replicas, capped workgroups; v1's BN-backward reductions as per-image rows added in image order) and
+    MNIST (one workgroup per member for every accumulation)."""
+    return args.model in ("mnist", "cifar10")
 
 
 def parse_main_args(argv=None, defaults=None) -> MainArgs:

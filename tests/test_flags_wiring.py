@@ -97,7 +97,7 @@ def test_fp16_loss_scaled_training_is_finite(tmp_path, monkeypatch):
 
 
 def test_deterministic_flag_selects_det_build(monkeypatch):
-    """--deterministic keeps the HIP backend for the CIFAR ResNet v2 and MNIST steps (deterministic kernel build,
+    """--deterministic keeps the HIP backend for the CIFAR ResNet v1/v2 and MNIST steps (deterministic kernel build,
     selected by DTF_DETERMINISTIC) and moves the families whose HIP kernels keep atomic reductions to the torch
     backend; an explicit --backend hip for those is an error."""
     from distributedtf_amd import ops
@@ -112,6 +112,8 @@ def test_deterministic_flag_selects_det_build(monkeypatch):
         b = parse_main_args(["--model", "mnist", "--deterministic"])
         b.apply_runtime_modes()
         assert b.backend == "auto"  # MNIST has a deterministic HIP build too
+        v1 = parse_main_args(["--model", "cifar10", "--resnet_version", "1", "--deterministic", "--backend", "hip"])
+        assert v1.backend == "hip"  # so does ResNet v1 (per-image BN-backward rows added in image order)
         c = parse_main_args(["--model", "imagenet", "--deterministic"])
         c.apply_runtime_modes()
         assert c.backend == "torch"  # ImageNet keeps order-dependent split-K reductions on the HIP path

@@ -1,6 +1,6 @@
 """Deterministic HIP build check (run with DTF_DETERMINISTIC=1): two identically initialised engines train the same
 steps on the same batches (graph replay, ragged populations) and must hold bitwise-identical state rows -- the
-CIFAR ResNet v2 and MNIST families.  Prints DET_OK."""
+CIFAR ResNet v2, ResNet v1 and MNIST families.  Prints DET_OK."""
 import os
 import sys
 
@@ -14,8 +14,8 @@ from distributedtf_amd.models.resnet import ResNetArch, cifar_config  # noqa: E4
 assert ops.deterministic_mode(), "run with DTF_DETERMINISTIC=1"
 
 
-def run(size, sizes, steps, opt="Momentum"):
-    arch = ResNetArch(cifar_config(size))
+def run(size, sizes, steps, opt="Momentum", version=2):
+    arch = ResNetArch(cifar_config(size, version=version))
     dev = torch.device("cuda")
     out = []
     for rep in range(2):
@@ -35,7 +35,7 @@ def run(size, sizes, steps, opt="Momentum"):
         torch.cuda.synchronize()
         out.append((e.state.clone(), losses.cpu()))
     same = torch.equal(out[0][0], out[1][0])
-    print("size %d sizes %s steps %d: bitwise identical %s, losses %s" % (size, sizes, steps, same,
+    print("v%d size %d sizes %s steps %d: bitwise identical %s, losses %s" % (version, size, sizes, steps, same,
                                                                          out[0][1].tolist()), flush=True)
     return same
 
@@ -67,6 +67,7 @@ def run_mnist(sizes, steps):
     return same
 
 
-ok = all([run(20, [16, 24], 4), run(56, [128], 3), run(56, [128] * 4, 2), run_mnist([40, 72], 4)])
+ok = all([run(20, [16, 24], 4), run(56, [128], 3), run(56, [128] * 4, 2), run(20, [16, 24], 4, version=1),
+          run(56, [128] * 2, 2, version=1), run_mnist([40, 72], 4)])
 print("DET_OK" if ok else "DET_FAIL")
 sys.exit(0 if ok else 1)

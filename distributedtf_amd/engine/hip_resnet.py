@@ -60,6 +60,8 @@ DEFER_MID_POP = 4         # up to this many members: defer the wgrad of DEFER_MI
 DEFER_MID_CS = (32, 64)
 DEFER_LARGE_CS = (64,)    # larger populations defer the wgrad of these channel widths only ...
 DEFER_LARGE_WG = {16: 16, 32: 8, 64: 8}  # ... with this many workgroups per member and layer
+HALF_BANDS_MAX_IMGS = 128  # C = 64 stage (8x8): 4-row half-image bands for the forward / dgrad launches up to this many
+#                            images per step (one member: whole-image items left half the CUs idle; pop 2 is slower)
 DG_ITERS_LARGE = 2        # ... and (image, band) iterations per dgrad workgroup (the weights load once per workgroup)
 DG_MIN_WG = 512           # ... keeping at least this many dgrad workgroups
 c_void_p, c_int, c_long = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
@@ -135,11 +137,11 @@ def _register():
                                   c_void_p])
     ops.register("dtf_conv_dgrad", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_wgrad", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
-    ops.register("dtf_conv_fwd_s1", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
+    ops.register("dtf_conv_fwd_s1", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_dw_slab_reduce", [c_void_p, c_void_p, c_int, c_void_p, c_long, c_long, c_int, c_void_p])
     ops.register("dtf_conv_bwd_fused", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_bwd_dual", [P(ConvArgs), P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
-    ops.register("dtf_conv_bwd_dg", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
+    ops.register("dtf_conv_bwd_dg", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_wgrad_all", [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_slab_reduce_all", [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_void_p])
     ops.register("dtf_slab_job_size", [])
@@ -852,6 +854,9 @@ class _StepPlan:
                 rows = r
                 break
         assert rows is not None, ("no valid band for conv", ci)
+        s1 = c.k == 3 and c.stride == 1 and cin == c.cout and Hi == 512 // cin and stats_bn is not None
+        if s1 and cin == 64 and self.N <= HALF_BANDS_MAX_IMGS and in_bn is not None:
+            rows = 4  # conv_fwd_s1_kernel<64, ., ., 4>
         bands = Ho // rows
         n_wg = self._n_wg_iters(self.N * bands, per_wg=FWD_ITERS_PER_WG,
                                 hi=max(1024, self.N * bands // FWD_ITERS_PER_WG))
@@ -871,12 +876,12 @@ class _StepPlan:
         lds = 1280 + 2 * tsz * 2
         mode = 0 if in_bn is None else 1
         lib = ops.lib()
-        if c.k == 3 and c.stride == 1 and cin == c.cout and Hi == 512 // cin and rows == 8 and stats_bn is not None:
+        if s1 and (rows == 8 or (rows == 4 and cin == 64)):
             # compile-time-geometry kernel of the CIFAR stages (conv_fwd_s1_kernel)
             self._set_uniform(a, work)
             a.cin_real = self._stamp_row("fwd", "fwd_s1 C=%d in=%d res=%d" % (cin, mode, res is not None))  # launch ordinal for DTF_STAMP diagnostic builds (unused otherwise)
             lds = 1280 + 2 * ((rows_in * _wpitch(cin) * _cpad_fwd(cin) + 8 + 63) // 64 * 64) * 2
-            self._add(lib.dtf_conv_fwd_s1, ctypes.byref(a), cin, mode, int(res is not None), work.shape[0], lds)
+            self._add(lib.dtf_conv_fwd_s1, ctypes.byref(a), cin, mode, int(res is not None), rows, work.shape[0], lds)
         else:
             self._add(lib.dtf_conv_fwd, ctypes.byref(a), cin, c.cout, c.stride, c.k, mode, int(res is not None),
                       int(stats_bn is not None), work.shape[0], lds)
@@ -1075,11 +1080,14 @@ class _StepPlan:
         lib = ops.lib()
         tsz = ((rows + 2) * _wpitch(C) * _cpad(C) + 8 + 63) // 64 * 64
         epi = int(res is not None) | (2 if ident_x else 0)
-        # ---- dgrad role: one (image, band) iteration per workgroup (larger populations: DG_ITERS_LARGE)
-        n_dg = max(1, self.N * bands)
+        # ---- dgrad role: one (image, band) iteration per workgroup (larger populations: DG_ITERS_LARGE); the
+        # deferred-wgrad dgrad launch of the C = 64 stage takes half-image bands at small populations
+        rows_dg = 4 if (C == 64 and C in self.defer_cs and self.N <= HALF_BANDS_MAX_IMGS) else rows
+        bands_dg = H // rows_dg
+        n_dg = max(1, self.N * bands_dg)
         if not self.dual:
             n_dg = min(n_dg, max(DG_MIN_WG, -(-n_dg // DG_ITERS_LARGE)))
-        work = self._work_iters(bands, self._det_cap(n_dg))
+        work = self._work_iters(bands_dg, self._det_cap(n_dg))
         a = self._base_args()
         a.x, a.x2, a.y, a.xm, a.res = _p(dy), _p(dy2), _p(dz_out), _p(x), _p(res)
         a.x3, a.xout = _p(dy3), _p(dy_out if mode_dy >= 2 else None)
@@ -1095,7 +1103,7 @@ class _StepPlan:
             a.ep_gamma, a.ep_beta = self._bn(x_bn)
             a.st_ep = _p(be.st_f(x_bn))
             a.st_out = _p(be.st_b(x_bn))
-        a.Hi, a.Wi, a.Ho, a.Wo, a.rows = H, H, H, H, rows
+        a.Hi, a.Wi, a.Ho, a.Wo, a.rows = H, H, H, H, rows_dg
         a.cin_real = self._stamp_row("fused", "fused-dg C=%d mdy=%d epi=%d" % (C, mode_dy, epi))
         # ---- wgrad role (same staging of dY / X; own work split)
         wwork = self._work_iters(bands, max(1, min(self.N * bands, DUAL_WG[C] * len(self.slots))))
@@ -1145,7 +1153,8 @@ class _StepPlan:
         BN2-backward(dz2, h) recomputed while staging, as the dgrad role does."""
         lib = ops.lib()
         self._keep(a)
-        self._add(lib.dtf_conv_bwd_dg, ctypes.byref(a), C, mode_dy, epi, a.n_main, 2304 + 2 * tsz * 2)
+        tsz_dg = ((a.rows + 2) * _wpitch(C) * _cpad(C) + 8 + 63) // 64 * 64
+        self._add(lib.dtf_conv_bwd_dg, ctypes.byref(a), C, mode_dy, epi, a.rows, a.n_main, 2304 + 2 * tsz_dg * 2)
         w = self._base_args()
         ctypes.memmove(ctypes.addressof(w), ctypes.addressof(b), ctypes.sizeof(ConvArgs))
         if dy_out is not None or mode_dy == 0:

@@ -861,9 +861,9 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
 // geometry (W = H = 512/C, 8-row bands), uniform-base + 32-bit lane offsets and packed epilogue math
 // (same scheme as conv_bwd_fused_kernel).
 // single member's 8x8 C = 64 layer (one image per item) launches 256 workgroups instead of 128.
-template <int C, int MODE_IN, bool RESID>
+template <int C, int MODE_IN, bool RESID, int ROWS = 8>
 __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
-  constexpr int W = 512 / C, H = W, ROWS = 8, BANDS = H / ROWS;
+  constexpr int W = 512 / C, H = W, BANDS = H / ROWS;
   constexpr int NT = C / 16, WPT = 4 / NT;  // NT: output-channel tiles
   constexpr int KTOT = 9 * C, KS = (KTOT + 31) / 32;
   constexpr int CP = cpad_fwd<C>(), RT = ROWS + 2, WP = wpitch<C>();
@@ -1452,10 +1452,11 @@ __device__ __forceinline__ void slab_reduce_wg(const float* __restrict__ slab, c
 // 1 = dgrad only (critical path: no X tile, no wgrad; the transformed dY may be materialised via xout for the
 // wgrad), 2 = wgrad only (the wgrad role of a dual launch; no dgrad / stats / xout).
 // Body of one workgroup; `bid` = the workgroup's index within its role (work item, stats replica, dW slab row).
-template <int C, int MODE_DY, int EPI, int ROLE>
+template <int C, int MODE_DY, int EPI, int ROLE, int ROWS = 8>
 __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, char* smem) {
   constexpr bool DG = ROLE != 2, WG = ROLE != 1;
-  constexpr int W = 512 / C, H = W, ROWS = 8, BANDS = H / ROWS;
+  static_assert(ROWS == 8 || ROLE == 1, "half-image bands: dgrad role only");
+  constexpr int W = 512 / C, H = W, BANDS = H / ROWS;
   constexpr int NT = C / 16;           // dgrad output-channel tiles
   constexpr int WPT = 4 / NT;
   constexpr int KTOT = 9 * C;
@@ -1466,7 +1467,8 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
   constexpr int CP = cpad<C>(), RT = ROWS + 2, WP = wpitch<C>();
   constexpr int TSZ = (RT * WP * CP + 8 + 63) & ~63;  // + slack for inactive staging slots
   constexpr int NTILES = ROWS * W / 16;
-  static_assert(NTILES == WPT * MAXT, "every wave owns MAXT dgrad tiles");
+  constexpr int MTD = NTILES / WPT;  // dgrad tiles per wave (MAXT for 8-row bands)
+  static_assert(NTILES == WPT * MTD && MTD <= MAXT, "every wave owns MTD dgrad tiles");
   constexpr int ROW = W * C, IMG = H * ROW;
   constexpr int NK = ROWS * W / 32, RSTEP = 32 / W, KINC = RSTEP * WP * CP;
   using St = Stage<C, RT, W, H, CP, WP>;
@@ -1596,10 +1598,10 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
     tapoff[s] = k0 < KTOT ? -((tap / 3) * WP + (tap % 3)) * CP + c0 : 0;
   }
   const int ci0 = ct * 16 + (lane >> 4) * 4;
-  int tbo[MAXT], rpo[MAXT];
-  uint32_t pofs[MAXT];
+  int tbo[MTD], rpo[MTD];
+  uint32_t pofs[MTD];
 #pragma unroll
-  for (int i = 0; i < MAXT; ++i) {
+  for (int i = 0; i < MTD; ++i) {
     const int p = (wave / NT + WPT * i) * 16 + (lane & 15);
     tbo[i] = ((p / W + 2) * WP + p % W + 2) * CP;
     pofs[i] = p * C + ci0;
@@ -1625,11 +1627,11 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
     for (int m = 0; m < MT; ++m) wacc[j][m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
   f32x2_t ssum[2] = {{0.f, 0.f}, {0.f, 0.f}}, ssq[2] = {{0.f, 0.f}, {0.f, 0.f}};
   // dgrad epilogue operands from global memory one iteration ahead (software-pipelined)
-  uint2 nres[MAXT], nxres[MAXT];
+  uint2 nres[MTD], nxres[MTD];
   auto epi_load = [&](int it_) {
     const long b_ = (long)(it_ / BANDS) * IMG + (it_ % BANDS) * ROWS * ROW;
 #pragma unroll
-    for (int i = 0; i < MAXT; ++i) {
+    for (int i = 0; i < MTD; ++i) {
       if constexpr (EPI & 1) nres[i] = *reinterpret_cast<const uint2*>(k_res + b_ + pofs[i]);
       if constexpr (!RAWX) nxres[i] = *reinterpret_cast<const uint2*>(k_xm + b_ + pofs[i]);
     }
@@ -1653,10 +1655,10 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
     const bool more = k + 1 < nit;
     const long band = (long)img * IMG + r0 * ROW;
     // epilogue operands before the prefetch (counted vmcnt)
-    uint2 rres[MAXT], xres[MAXT];
+    uint2 rres[MTD], xres[MTD];
     if constexpr (DG) {
 #pragma unroll
-    for (int i = 0; i < MAXT; ++i) {
+    for (int i = 0; i < MTD; ++i) {
       if constexpr (EPI & 1) rres[i] = nres[i];
       if constexpr (RAWX)
         xres[i] = *reinterpret_cast<const uint2*>(FXRAW(k) + rpo[i]);
@@ -1682,7 +1684,7 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
     const f32x2_t iv0 = lds2(ecoef + 192 + ci0), iv1 = lds2(ecoef + 192 + ci0 + 2);
     if constexpr (DG) {
 #pragma unroll
-    for (int i = 0; i < MAXT; ++i) {
+    for (int i = 0; i < MTD; ++i) {
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < KS; ++s)
@@ -1844,10 +1846,10 @@ __global__ __launch_bounds__(256, FUSED_WAVES(C, MODE_DY)) void conv_bwd_dual_ke
 
 // dgrad role alone (the backward launch of a layer whose wgrad is deferred to conv_wgrad_all_kernel): without the
 // wgrad role's accumulators the kernel fits two waves per SIMD (the dual kernel is register-capped at one).
-template <int C, int MODE_DY, int EPI>
+template <int C, int MODE_DY, int EPI, int ROWS = 8>
 __global__ __launch_bounds__(256, 2) void conv_bwd_dg_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  conv_bwd_body<C, MODE_DY, EPI, 1>(a, (int)blockIdx.x, smem);
+  conv_bwd_body<C, MODE_DY, EPI, 1, ROWS>(a, (int)blockIdx.x, smem);
 }
 
 // Deferred weight gradients (engine/hip_resnet.py): the backward launches of a deferred layer run only their dgrad
@@ -2001,8 +2003,15 @@ int launch(KernelT k, int nblocks, size_t lds, hipStream_t st, const ConvArgs& a
   if (cin == CI && cout == CO && s == S && k == K && mode_x == MX && mode_dy == MD)                  \
     return launch(conv_wgrad_kernel<CI, CO, S, K, MX, MD>, nblocks, lds, stream, *args);
 
-DTF_API int dtf_conv_fwd_s1(const ConvArgs* args, int c, int mode, int resid, int nblocks, int lds,
+// rows: band height (8; 4: half-image bands of the C = 64 layer, twice the workgroups of a small population)
+DTF_API int dtf_conv_fwd_s1(const ConvArgs* args, int c, int mode, int resid, int rows, int nblocks, int lds,
                             hipStream_t stream) {
+  DTF_HOST_CHECK(args->rows == rows);
+  if (rows == 4) {
+    if (c == 64 && mode == 1 && resid == 0) return launch(conv_fwd_s1_kernel<64, 1, false, 4>, nblocks, lds, stream, *args);
+    if (c == 64 && mode == 1 && resid == 1) return launch(conv_fwd_s1_kernel<64, 1, true, 4>, nblocks, lds, stream, *args);
+    return -1;
+  }
 #define S1_CASE(CC, M, R) \
   if (c == CC && mode == M && resid == R) return launch(conv_fwd_s1_kernel<CC, M, R>, nblocks, lds, stream, *args);
   S1_CASE(16, 0, false)  // stem (input padded to 16 channels); v1 conv_a (identity input)
@@ -2182,10 +2191,22 @@ DTF_API int dtf_conv_bwd_dual(const ConvArgs* a, const ConvArgs* b, int c, int m
   return -1;
 }
 
-DTF_API int dtf_conv_bwd_dg(const ConvArgs* a, int c, int mode_dy, int epi, int nblocks, int lds, hipStream_t stream) {
+// rows: band height (8 = whole 8x8 image for C = 64; 4: half-image bands for C = 64, twice the workgroups)
+DTF_API int dtf_conv_bwd_dg(const ConvArgs* a, int c, int mode_dy, int epi, int rows, int nblocks, int lds,
+                            hipStream_t stream) {
   if (nblocks <= 0) return 0;
   DTF_HOST_CHECK(lds <= 160 * 1024);
-  DTF_HOST_CHECK(a->work != nullptr && nblocks == a->n_main);
+  DTF_HOST_CHECK(a->work != nullptr && nblocks == a->n_main && a->rows == rows);
+  if (rows == 4) {
+#define DG4_CASE(M)                                                                                          \
+    if (c == 64 && mode_dy == M && epi == 0) {                                                              \
+      hipLaunchKernelGGL((conv_bwd_dg_kernel<64, M, 0, 4>), dim3(nblocks), dim3(256), lds, stream, *a);     \
+      return DTF_CHECK_LAUNCH();                                                                            \
+    }
+    DG4_CASE(0) DG4_CASE(2) DG4_CASE(3)
+#undef DG4_CASE
+    return -1;
+  }
 #define DG_CASE(CC, M, E)                                                                                    \
   if (c == CC && mode_dy == M && epi == E) {                                                                \
     hipLaunchKernelGGL((conv_bwd_dg_kernel<CC, M, E>), dim3(nblocks), dim3(256), lds, stream, *a);          \

@@ -43,11 +43,11 @@ a = hr.ConvArgs()
 a.x, a.y, a.w = x.data_ptr(), y.data_ptr(), w.data_ptr()
 a.img_slot, a.cnt, a.work = img_slot.data_ptr(), cnt.data_ptr(), work.data_ptr()
 # 1) host-side argument check: zero spatial dims never reach the GPU
-expect_error(lambda: L.dtf_conv_fwd_s1(ctypes.byref(a), 16, 0, 0, 1, 65536, st), "host-side argument check")
+expect_error(lambda: L.dtf_conv_fwd_s1(ctypes.byref(a), 16, 0, 0, 0, 1, 65536, st), "host-side argument check")
 # 2) device-side workgroup check: the item is rejected before any tensor access, recorded and reported
 a.Hi = a.Wi = a.Ho = a.Wo = 32
-a.rows = 4
-expect_error(lambda: L.dtf_conv_fwd_s1(ctypes.byref(a), 16, 0, 0, 1, 65536, st), "device check failed in conv.hip")
+a.rows = 8
+expect_error(lambda: L.dtf_conv_fwd_s1(ctypes.byref(a), 16, 0, 0, 8, 1, 65536, st), "device check failed in conv.hip")
 torch.cuda.synchronize()
 # 3) a real population step with every launch checked
 import __graft_entry__  # noqa: E402

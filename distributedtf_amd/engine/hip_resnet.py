@@ -60,8 +60,9 @@ DEFER_MID_POP = 4         # up to this many members: defer the wgrad of DEFER_MI
 DEFER_MID_CS = (32, 64)
 DEFER_LARGE_CS = (64,)    # larger populations defer the wgrad of these channel widths only ...
 DEFER_LARGE_WG = {16: 16, 32: 8, 64: 8}  # ... with this many workgroups per member and layer
-HALF_BANDS_MAX_IMGS = 128  # 4-row bands for the forward / dgrad launches of the HALF_BANDS_CS stages up to this many
-HALF_BANDS_CS = (64,)      # images per step (one member: 8-row items left half the CUs idle; pop 2 is slower)
+HALF_BANDS_MAX_IMGS = 128  # C = 64 stage (8x8): 4-row half-image bands for the forward / dgrad launches up to this many
+#                            images per step (one member: whole-image items left half the CUs idle; pop 2 and the
+#                            C = 32 stage are slower with half bands: profiles/r3_half_bands_ab.log)
 DG_ITERS_LARGE = 2        # ... and (image, band) iterations per dgrad workgroup (the weights load once per workgroup)
 DG_MIN_WG = 512           # ... keeping at least this many dgrad workgroups
 c_void_p, c_int, c_long = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
@@ -855,7 +856,7 @@ class _StepPlan:
                 break
         assert rows is not None, ("no valid band for conv", ci)
         s1 = c.k == 3 and c.stride == 1 and cin == c.cout and Hi == 512 // cin and stats_bn is not None
-        if s1 and cin in HALF_BANDS_CS and self.N <= HALF_BANDS_MAX_IMGS and in_bn is not None:
+        if s1 and cin == 64 and self.N <= HALF_BANDS_MAX_IMGS and in_bn is not None:
             rows = 4  # conv_fwd_s1_kernel<64, ., ., 4>
         bands = Ho // rows
         n_wg = self._n_wg_iters(self.N * bands, per_wg=FWD_ITERS_PER_WG,
@@ -1082,7 +1083,7 @@ class _StepPlan:
         epi = int(res is not None) | (2 if ident_x else 0)
         # ---- dgrad role: one (image, band) iteration per workgroup (larger populations: DG_ITERS_LARGE); the
         # deferred-wgrad dgrad launch of the C = 64 stage takes half-image bands at small populations
-        rows_dg = 4 if (C in HALF_BANDS_CS and C in self.defer_cs and self.N <= HALF_BANDS_MAX_IMGS) else rows
+        rows_dg = 4 if (C == 64 and C in self.defer_cs and self.N <= HALF_BANDS_MAX_IMGS) else rows
         bands_dg = H // rows_dg
         n_dg = max(1, self.N * bands_dg)
         if not self.dual:

@@ -2003,15 +2003,13 @@ int launch(KernelT k, int nblocks, size_t lds, hipStream_t st, const ConvArgs& a
   if (cin == CI && cout == CO && s == S && k == K && mode_x == MX && mode_dy == MD)                  \
     return launch(conv_wgrad_kernel<CI, CO, S, K, MX, MD>, nblocks, lds, stream, *args);
 
-// rows: band height (8; 4: half-height bands for C = 64 / 32, twice the workgroups of a small population)
+// rows: band height (8; 4: half-image bands for C = 64, twice the workgroups of one member; C = 32 measured slower)
 DTF_API int dtf_conv_fwd_s1(const ConvArgs* args, int c, int mode, int resid, int rows, int nblocks, int lds,
                             hipStream_t stream) {
   DTF_HOST_CHECK(args->rows == rows);
   if (rows == 4) {
     if (c == 64 && mode == 1 && resid == 0) return launch(conv_fwd_s1_kernel<64, 1, false, 4>, nblocks, lds, stream, *args);
     if (c == 64 && mode == 1 && resid == 1) return launch(conv_fwd_s1_kernel<64, 1, true, 4>, nblocks, lds, stream, *args);
-    if (c == 32 && mode == 1 && resid == 0) return launch(conv_fwd_s1_kernel<32, 1, false, 4>, nblocks, lds, stream, *args);
-    if (c == 32 && mode == 1 && resid == 1) return launch(conv_fwd_s1_kernel<32, 1, true, 4>, nblocks, lds, stream, *args);
     return -1;
   }
 #define S1_CASE(CC, M, R) \
@@ -2193,7 +2191,7 @@ DTF_API int dtf_conv_bwd_dual(const ConvArgs* a, const ConvArgs* b, int c, int m
   return -1;
 }
 
-// rows: band height (8; 4: half-height bands for C = 64 / 32, twice the workgroups of a small population)
+// rows: band height (8; 4: half-image bands for C = 64, twice the workgroups of one member; C = 32 measured slower)
 DTF_API int dtf_conv_bwd_dg(const ConvArgs* a, int c, int mode_dy, int epi, int rows, int nblocks, int lds,
                             hipStream_t stream) {
   if (nblocks <= 0) return 0;
@@ -2205,7 +2203,7 @@ DTF_API int dtf_conv_bwd_dg(const ConvArgs* a, int c, int mode_dy, int epi, int 
       hipLaunchKernelGGL((conv_bwd_dg_kernel<CC, M, 0, 4>), dim3(nblocks), dim3(256), lds, stream, *a);     \
       return DTF_CHECK_LAUNCH();                                                                            \
     }
-    DG4_CASE(64, 0) DG4_CASE(64, 2) DG4_CASE(64, 3) DG4_CASE(32, 0) DG4_CASE(32, 2) DG4_CASE(32, 3)
+    DG4_CASE(64, 0) DG4_CASE(64, 2) DG4_CASE(64, 3)
 #undef DG4_CASE
     return -1;
   }

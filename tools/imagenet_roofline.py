@@ -75,6 +75,8 @@ KERNEL_FAMILY = [("cg_bn_relu_apply", "bn_relu_apply"), ("cg_bn_bwd_apply", "bn_
 def kernel_family(k: str):
     if "convg_fwd_kernel" in k:
         return "conv dgrad" if k.split(",")[4].strip().startswith("true") else "conv fwd"
+    if "convg_t3_kernel" in k:  # <TC, EPI, AKM, ...>: AKM = data gradient
+        return "conv dgrad" if k.split(",")[2].strip().startswith("true") else "conv fwd"
     for pre, f in KERNEL_FAMILY:
         if pre in k:
             return f

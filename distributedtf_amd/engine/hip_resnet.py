@@ -47,7 +47,8 @@ DET_WG_PER_MEMBER = 64  # deterministic mode: statistic-producing launches use <
 DUAL_MAX_POP = 2          # dual (dgrad | wgrad role) backward launches up to this many members per GPU ...
 DUAL_CS = (32, 64)        # ... for these channel widths (C = 16 keeps the fused kernel)
 DUAL_WG = {16: 128, 32: 128, 64: 64}  # wgrad-role workgroups per member of a dual launch
-FWD_ITERS_PER_WG = 4      # forward: (image, band) iterations per workgroup (>= 256 workgroups kept)
+FWD_ITERS_PER_WG = 4      # forward: (image, band) iterations per workgroup (>= FWD_MIN_WG workgroups kept)
+FWD_MIN_WG = 256
 HEAD_ITEMS = 512          # head / GAP+dense+CE work items
 WGRAD_WG_PER_MEMBER = 128  # standalone wgrad launches: workgroups per member (bounds the dW partial traffic)
 DENSE_REDUCE_BLOCKS = 256  # slab_reduce_all, dense jobs: max 32-element blocks per job
@@ -859,7 +860,7 @@ class _StepPlan:
         if s1 and cin == 64 and self.N <= HALF_BANDS_MAX_IMGS and in_bn is not None:
             rows = 4  # conv_fwd_s1_kernel<64, ., ., 4>
         bands = Ho // rows
-        n_wg = self._n_wg_iters(self.N * bands, per_wg=FWD_ITERS_PER_WG,
+        n_wg = self._n_wg_iters(self.N * bands, per_wg=FWD_ITERS_PER_WG, lo=FWD_MIN_WG,
                                 hi=max(1024, self.N * bands // FWD_ITERS_PER_WG))
         work = self._work_iters(bands, n_wg)
         a = self._base_args()

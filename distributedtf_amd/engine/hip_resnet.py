@@ -47,8 +47,9 @@ DET_WG_PER_MEMBER = 64  # deterministic mode: statistic-producing launches use <
 DUAL_MAX_POP = 2          # dual (dgrad | wgrad role) backward launches up to this many members per GPU ...
 DUAL_CS = (32, 64)        # ... for these channel widths (C = 16 keeps the fused kernel)
 DUAL_WG = {16: 128, 32: 128, 64: 64}  # wgrad-role workgroups per member of a dual launch
-FWD_ITERS_PER_WG = 4      # forward: (image, band) iterations per workgroup (>= FWD_MIN_WG workgroups kept)
-FWD_MIN_WG = 256
+FWD_ITERS_PER_WG = 4      # forward: (image, band) iterations per workgroup (>= FWD_MIN_WG workgroups kept;
+FWD_MIN_WG = 256          # 512 for up to DUAL_MAX_POP members: pop 1 1.059 -> 1.055, pop 2 1.427 -> 1.398 ms)
+FWD_MIN_WG_SMALL = 512
 HEAD_ITEMS = 512          # head / GAP+dense+CE work items
 WGRAD_WG_PER_MEMBER = 128  # standalone wgrad launches: workgroups per member (bounds the dW partial traffic)
 DENSE_REDUCE_BLOCKS = 256  # slab_reduce_all, dense jobs: max 32-element blocks per job
@@ -860,7 +861,8 @@ class _StepPlan:
         if s1 and cin == 64 and self.N <= HALF_BANDS_MAX_IMGS and in_bn is not None:
             rows = 4  # conv_fwd_s1_kernel<64, ., ., 4>
         bands = Ho // rows
-        n_wg = self._n_wg_iters(self.N * bands, per_wg=FWD_ITERS_PER_WG, lo=FWD_MIN_WG,
+        lo = FWD_MIN_WG_SMALL if len(self.slots) <= DUAL_MAX_POP else FWD_MIN_WG
+        n_wg = self._n_wg_iters(self.N * bands, per_wg=FWD_ITERS_PER_WG, lo=lo,
                                 hi=max(1024, self.N * bands // FWD_ITERS_PER_WG))
         work = self._work_iters(bands, n_wg)
         a = self._base_args()
@@ -1075,7 +1077,7 @@ class _StepPlan:
     def _conv_bwd_dual(self, ci, c, C, H, rows, bands, dy, dz_out, x, mode_dy, dy2, dy_bn, x_bn, res, ident_x, dy3,
                        dy_out):
         """Dual backward of a stride-1 C->C conv (conv_bwd_dual_kernel): dgrad-role workgroups (one (image, band)
-        iteration each by default: the critical path) and wgrad-role workgroups (DTF_DUAL_WG_<C> per member, each
+        iteration each by default: the critical path) and wgrad-role workgroups (DUAL_WG[C] per member, each
         over a run of iterations, writing a dW slab) in one launch; both stage the same transformed dY.  The
         slabs are reduced by the trailing workgroups of the next backward launch (or a standalone reduction)."""
         be, L = self.be, self.be.L

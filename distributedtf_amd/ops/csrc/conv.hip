@@ -1823,7 +1823,7 @@ __global__ __launch_bounds__(256, FUSED_WAVES(C, MODE_DY)) void conv_bwd_fused_k
   conv_bwd_body<C, MODE_DY, EPI, 0>(a, (int)blockIdx.x, smem);
 }
 
-// Dual backward (small populations, engine/hip_resnet.py DTF_DUAL_BWD): ONE launch whose workgroups take
+// Dual backward (engine/hip_resnet.py _conv_bwd_dual): ONE launch whose workgroups take
 // different roles of the same layer -- [0, a.n_main): dgrad role (args a: staging, dgrad MFMAs, mask / stats
 // epilogue, dz out); [a.n_main, + b.n_main): wgrad role (args b: its own work split over the same (image, band)
 // iterations, the same dY / X staging, wgrad MFMAs, dW slab); then the trailing slab reduction of the previous
@@ -1887,7 +1887,7 @@ __global__ __launch_bounds__(256) void dw_slab_reduce_kernel(const float* __rest
   slab_reduce_wg<C>(slab, red, grads, g_mstride, g_off, blockIdx.x, blockIdx.y, part, gridDim.x);
 }
 
-// One launch for the dW slabs of several layers (deferred C = 64 reductions, engine/hip_resnet.py DTF_DEFER_C64):
+// Slab reduction job (slab_reduce_all_kernel): the dW slabs of one deferred layer
 // blockIdx.z = layer, y = member row of that layer's reduce table, x = 32-element block.
 struct SlabJob {
   const float* slab;

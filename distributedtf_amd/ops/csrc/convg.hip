@@ -524,10 +524,7 @@ __host__ __device__ constexpr int t3_nhalf() {
   return -1;
 }
 
-#ifndef DTF_T3_AD
-#define DTF_T3_AD 1
-#endif
-template <int TC, int EPI, bool AKM, int W, int R, int TP, int WRN, int AD = DTF_T3_AD>
+template <int TC, int EPI, bool AKM, int W, int R, int TP, int WRN>
 __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
   constexpr int BK = 32;
   constexpr int PW = TP / (4 / WRN), NTP = PW / 16, MT = TC / WRN / 16;
@@ -622,24 +619,19 @@ __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
 #pragma unroll
     for (int n = 0; n < NTP; ++n) acc[m][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
   const int nch = Ci / BK, nk = 9 * nch;
-  // A (weights) is prefetched AD k-steps ahead: with AD = 2 the loop is unrolled by two over a pair of register
-  // sets, so every load / store names a fixed register set (a set picked by a runtime parity makes hipcc drain the
-  // prefetch with vmcnt(0) at the merge)
-  uint4 ra0[AJ], ra1[AJ], rb[MAXB];
+  // A (weights) is prefetched one k-step ahead (a two-deep register ring, loop unrolled by two, measured the same:
+  // profiles/r3_imagenet_t3_ab.log); the input rows of the next channel chunk a whole chunk (9 k-steps) ahead
+  uint4 ra[AJ], rb[MAXB];
   load_b(0, rb);
-  load_a(0, 0, ra0);
-  if constexpr (AD == 2) load_a(0, 1, ra1);  // nk >= 9
+  load_a(0, 0, ra);
   store_b(rb);
-  store_a(sa[0], ra0);
+  store_a(sa[0], ra);
   __syncthreads();
-  // one k-step (chunk c, tap t): r_next holds A(ks + 1) (AD 2), r_free receives A(ks + AD)
-  auto kstep = [&](int ks, int c, int t, bf16_t* sa_cur, bf16_t* sa_nxt, uint4 (&r_next)[AJ], uint4 (&r_free)[AJ]) {
+  int c = 0, t = 0;
+  for (int ks = 0; ks < nk; ++ks) {
     const bool more = ks + 1 < nk;
-    if constexpr (AD == 1) {
-      if (more) load_a(t == 8 ? c + 1 : c, t == 8 ? 0 : t + 1, r_free);
-    } else {
-      if (ks + 2 < nk) load_a(t >= 7 ? c + 1 : c, t >= 7 ? t - 7 : t + 2, r_free);
-    }
+    bf16_t* sa_cur = sa[ks & 1];
+    if (more) load_a(t == 8 ? c + 1 : c, t == 8 ? 0 : t + 1, ra);
     if (t == 0 && c + 1 < nch) load_b(c + 1, rb);  // next chunk's rows: 9 k-steps of latency cover
     const int tapo = ((t / 3) * WT + t % 3) * RP;
     bf16x8_t fa[MT], fb[NTP];
@@ -667,33 +659,12 @@ __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
         __syncthreads();
         store_b(rb);
       }
-      if constexpr (AD == 1)
-        store_a(sa_nxt, r_free);
-      else
-        store_a(sa_nxt, r_next);
+      store_a(sa[(ks & 1) ^ 1], ra);
     }
     __syncthreads();
-  };
-  int c = 0, t = 0;
-  auto adv = [&]() {
     if (++t == 9) {
       t = 0;
       ++c;
-    }
-  };
-  if constexpr (AD == 1) {
-    for (int ks = 0; ks < nk; ++ks) {
-      kstep(ks, c, t, sa[ks & 1], sa[(ks & 1) ^ 1], ra0, ra0);
-      adv();
-    }
-  } else {
-    for (int ks = 0; ks < nk; ks += 2) {
-      kstep(ks, c, t, sa[0], sa[1], ra1, ra0);
-      adv();
-      if (ks + 1 < nk) {
-        kstep(ks + 1, c, t, sa[1], sa[0], ra0, ra1);
-        adv();
-      }
     }
   }
   convg_epilogue<TC, EPI, false, TP, WRN, NHALF>(a, acc, reinterpret_cast<float*>(smem_), acc_lds, slot, o0, p0, p1,

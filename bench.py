@@ -174,7 +174,17 @@ def main():
 
     for _ in range(args.warmup):
         losses = step()
-    # (RCCL P2P connections of every GPU pair are opened by init_distributed: no timed exploit pays a lazy setup)
+    # RCCL P2P connections of every GPU pair are opened by init_distributed (DTF_RCCL_PRECONNECT=1, the default):
+    # no timed exploit pays a lazy setup.  Without that pre-connect (env off, or gloo), one untimed exploit cycle
+    # opens the connections of this plan's pairs instead, so the timed cycles do not include the setup.
+    from distributedtf_amd.parallel.comm import preconnected
+    from distributedtf_amd.engine.hip_resnet import graph_state
+    warm_exploit = world > 1 and args.exploit_every and not preconnected()
+    if warm_exploit:
+        exploit_cycle(exploit_start(losses))
+        exploit_s.clear()
+        exploit_wait_s.clear()
+        exploits[0] = 0
     barrier_sync()
     images_done[0] = 0
     t0 = time.perf_counter()
@@ -222,7 +232,10 @@ def main():
                        "population": args.pop, "seq_len": None,
                        "parallelism": "pbt_pop%d_%dmembers_per_gpu" % (args.pop, cnt),
                        "backend": eng.backend.name, "exploit_every": args.exploit_every,
-                       "exploits_timed": exploits[0]},
+                       "exploits_timed": exploits[0],
+                       "p2p_preconnected": preconnected() if world > 1 else None,
+                       "untimed_warmup_exploit": bool(warm_exploit),
+                       "step_graph": graph_state(eng.backend)},
             "exploit_ms_mean": round(1000.0 * sum(exploit_s) / len(exploit_s), 3) if exploit_s else None,
             "exploit_readback_wait_ms_mean": (round(1000.0 * sum(exploit_wait_s) / len(exploit_wait_s), 3)
                                               if exploit_wait_s else None),

@@ -124,6 +124,36 @@ def synthetic_images(n: int, shape, num_classes: int, seed: int, device, dtype=t
     return x.to(device), y.to(device)
 
 
+def learnable_cifar(n_train: int = 10000, n_test: int = 2000, seed: int = 7, noise: float = 0.9,
+                    num_classes: int = 10):
+    """A learnable CIFAR-shaped dataset that needs no download (the real CIFAR-10 is not on these machines):
+    uint8 NHWC 32x32x3 images with labels, so it runs through the real input path (on-device gather, pad-4 random
+    crop, flip, per-image standardisation: data.hip / cifar10_main.py:98-108).
+
+    Each class has a fixed smooth random template (an 8x8x3 Gaussian field upsampled bilinearly to 32x32, so a
+    random crop and a flip keep most of it) and every image is ``template[label] * contrast + noise`` with a
+    per-image random contrast in [0.6, 1.4], brightness shift and i.i.d. pixel noise of ``noise`` template
+    standard deviations.  Chance accuracy is 1/num_classes; a ResNet-20 reaches well above it within a few hundred
+    steps, so loss / accuracy trajectories of two implementations can be compared (tests/test_gpu_trajectory.py).
+    Returns (train_x, train_y, test_x, test_y) as numpy arrays."""
+    g = torch.Generator().manual_seed(int(seed))
+    base = torch.randn(num_classes, 3, 8, 8, generator=g)
+    tmpl = torch.nn.functional.interpolate(base, size=(32, 32), mode="bilinear", align_corners=False)
+    tmpl = tmpl / tmpl.flatten(1).std(dim=1).view(-1, 1, 1, 1)
+
+    def make(n):
+        y = torch.randint(0, num_classes, (n,), generator=g)
+        contrast = 0.6 + 0.8 * torch.rand(n, 1, 1, 1, generator=g)
+        shift = 0.3 * torch.randn(n, 1, 1, 1, generator=g)
+        x = tmpl[y] * contrast + shift + noise * torch.randn(n, 3, 32, 32, generator=g)
+        x = (x * 40.0 + 128.0).round().clamp(0, 255).to(torch.uint8)
+        return x.permute(0, 2, 3, 1).contiguous().numpy(), y.numpy().astype(np.int64)
+
+    trx, tr_y = make(n_train)
+    tex, te_y = make(n_test)
+    return trx, tr_y, tex, te_y
+
+
 def _idx(path, offset, dtype=np.uint8):
     with gzip.open(path, "rb") as f:
         return np.frombuffer(f.read(), dtype, offset=offset)

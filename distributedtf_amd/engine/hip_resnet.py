@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 from typing import Dict, List, Sequence, Tuple
 
 import torch
@@ -346,6 +347,22 @@ def advance_steps(e, slots_long, slots_i32=None, loss=None, loss_sel=None):
         torch.index_select(loss, 0, slots_long, out=loss_sel)
 
 
+_LIVE_GRAPH_PLANS = weakref.WeakSet()  # plans holding a captured step graph (released before RCCL teardown)
+
+
+def release_graphs() -> int:
+    """Drop every captured step graph (they are re-captured on the next step).  A graph that recorded an RCCL
+    collective keeps that communicator busy: ``destroy_process_group`` then blocks forever (measured with the
+    data-parallel step on the GPU box), so ``parallel.comm.shutdown_distributed`` calls this first."""
+    n = 0
+    for plan in list(_LIVE_GRAPH_PLANS):
+        if plan.graph is not None:
+            plan.graph = None
+            n += 1
+    _LIVE_GRAPH_PLANS.clear()
+    return n
+
+
 def run_captured(plan) -> None:
     """Run one step of ``plan``: the first call executes it eagerly (allocator / lazy init warm-up) and then
     captures the launch list into a HIP graph; later calls replay the graph.  A data-parallel step captures its
@@ -361,7 +378,7 @@ def run_captured(plan) -> None:
         ok = False
         try:
             with torch.cuda.stream(s):
-                g.capture_begin()
+                g.capture_begin(capture_error_mode="thread_local")
                 try:
                     plan._run_eager()
                 finally:
@@ -370,18 +387,37 @@ def run_captured(plan) -> None:
         except RuntimeError as err:
             if plan.e.dp is None:
                 raise
+            import sys
             import warnings
-            warnings.warn("step graph capture with the data-parallel all-reduce failed (%s): eager launches" % err)
+            msg = "step graph capture with the data-parallel all-reduce failed (%s): eager launches" % err
+            warnings.warn(msg)
+            print("DTF WARNING: " + msg, file=sys.stderr, flush=True)
             torch.cuda.synchronize()
             plan._no_graph = True
+            be.graph_fallbacks = getattr(be, "graph_fallbacks", 0) + 1
         torch.cuda.current_stream().wait_stream(s)
         if ok:
             plan.graph = g
+            be.graphs_captured = getattr(be, "graphs_captured", 0) + 1
+            _LIVE_GRAPH_PLANS.add(plan)
         return
     if plan.graph is not None:
         plan.graph.replay()
     else:
         plan._run_eager()
+
+
+def graph_state(be):
+    """How a HIP backend's steps run: "captured" (HIP-graph replay), "eager_fallback" (a data-parallel capture was
+    refused and at least one plan runs its launches eagerly -- slow, recorded in the bench JSON and metrics.jsonl),
+    "disabled" (DTF_HIP_GRAPH=0 / debug), "none" (nothing captured yet), or None (not a HIP backend)."""
+    if not hasattr(be, "use_graph"):
+        return None
+    if not be.use_graph:
+        return "disabled"
+    if getattr(be, "graph_fallbacks", 0):
+        return "eager_fallback"
+    return "captured" if getattr(be, "graphs_captured", 0) else "none"
 
 
 def same_batches(plan, batches) -> bool:

@@ -44,6 +44,14 @@ class Cifar10Model(EngineModel):
         synthetic = self.use_synthetic_data
         if synthetic is None:
             synthetic = not datasets.cifar10_available(self.data_dir)
+        if synthetic == "learnable":
+            # class-template images through the real input path (augmentation, per-image standardisation): eval
+            # accuracy can climb above chance without the real dataset (--use_synthetic_data learnable)
+            on_gpu = torch.device(device).type == "cuda"
+            trx, tr_y, tex, te_y = datasets.learnable_cifar(n_train=20000 if on_gpu else 2000,
+                                                            n_test=datasets.CIFAR_NUM_TEST if on_gpu else 500)
+            return datasets.DeviceDataset(trx, tr_y, tex, te_y, device, augment=datasets.augment_cifar,
+                                          eval_transform=datasets.eval_cifar)
         if synthetic:
             # the reference evaluates on the full 10k-image test set every epoch (resnet_run_loop.py:463-466,
             # mnist_model.py:167-172): a synthetic eval set of the same size on the GPU (1k on CPU test runs)

@@ -280,14 +280,17 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0) -
     rank = int(os.environ["RANK"])
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
+    device_index = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend == "nccl" and os.environ.get("DTF_SHARE_GPU", "0") == "1":
+        device_index = configure_shared_gpu(rank, device_index)
     if backend == "nccl":
-        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(local_rank)
+        torch.cuda.set_device(device_index)
     td = datetime.timedelta(seconds=timeout_s)
+    _CTX["preconnected"] = False
     if not dist.is_initialized():
         kw = dict(backend=backend, timeout=td)
         if backend == "nccl":
-            kw["device_id"] = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+            kw["device_id"] = torch.device("cuda", device_index)
         dist.init_process_group(**kw)
         if backend == "nccl":
             # create the RCCL communicator now (all ranks), so later P2P batches that involve only some
@@ -296,6 +299,7 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0) -
             dist.all_reduce(t)
             if os.environ.get("DTF_RCCL_PRECONNECT", "1") == "1":
                 preconnect_p2p(world, rank)
+                _CTX["preconnected"] = True
             torch.cuda.synchronize()
     cpu_group = dist.new_group(backend="gloo", timeout=td) if backend != "gloo" else dist.group.WORLD
     try:
@@ -309,6 +313,29 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0) -
     _CTX["comm"] = comm
     _CTX["backend"] = backend
     return comm
+
+
+def configure_shared_gpu(rank: int, local_rank: int) -> int:
+    """``DTF_SHARE_GPU=1``: rehearse a multi-rank RCCL job on fewer GPUs than ranks (the 1-GPU test box).
+
+    RCCL refuses two ranks of one communicator on one device ("Duplicate GPU detected") when they share a host
+    hash.  Giving every rank its own ``NCCL_HOSTID`` makes each rank a one-GPU "node": the communicator then forms,
+    and ranks exchange data through RCCL's network (socket, loopback) transport instead of xGMI P2P.  Every RCCL
+    call of the product -- the exploit ``send``/``recv`` of state rows, the data-parallel all-reduce captured in the
+    step graph, the pre-connect -- then really executes RCCL kernels and proxy progress on the GPU, only over a
+    slower wire.  Must run before the communicator is created.  Returns the device index (local rank modulo the
+    visible devices)."""
+    import torch
+    os.environ["NCCL_HOSTID"] = "dtf-shared-gpu-rank%d" % rank
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    os.environ.setdefault("NCCL_IB_DISABLE", "1")
+    n = max(1, torch.cuda.device_count())
+    return local_rank % n
+
+
+def preconnected() -> bool:
+    """True when init_distributed opened every RCCL P2P pair (exploit copies then pay no lazy connection setup)."""
+    return bool(_CTX.get("preconnected", False))
 
 
 def preconnect_p2p(world: int, rank: int) -> None:
@@ -342,7 +369,17 @@ def backend_name() -> str:
 
 
 def shutdown_distributed():
+    """Tear the process groups down.  Captured HIP step graphs that recorded RCCL collectives (the data-parallel
+    all-reduce) are released first: ``destroy_process_group`` blocks forever while such a graph is alive."""
+    import sys
     import torch.distributed as dist
     _CTX.clear()
+    hr = sys.modules.get("distributedtf_amd.engine.hip_resnet")
+    if hr is not None and hr.release_graphs():
+        import gc
+        import torch
+        gc.collect()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()

@@ -391,6 +391,14 @@ class SPMDPopulation(_ReportMixin):
         return [sum(int(getattr(g, "images_trained", 0)) for g in self.worker.worker_graphs), self.worker.train_time,
                 self.worker.explore_time, float(dp.bytes_moved), dp.seconds, dp.transfers_done]
 
+    def _graph_state(self):
+        from ..engine.hip_resnet import graph_state
+        for g in self.worker.worker_graphs:
+            eng = getattr(g, "engine", None)
+            if eng is not None:
+                return graph_state(eng.backend)
+        return None
+
     def log_round_metrics(self, rnd, round_s):
         """Append one JSON line per round to ``savedata/metrics.jsonl``: throughput (images/s of
         the whole job), per-phase times (train / exploit / explore, max over ranks), exploit data-plane bytes and
@@ -402,7 +410,7 @@ class SPMDPopulation(_ReportMixin):
         delta = [c - p for c, p in zip(cur, prev)]
         phases = PHASES.since(getattr(self, "_prev_phases", {}))
         self._prev_phases = PHASES.snapshot()
-        parts = self.comm.allgather([delta, [float(v[1]) for v in self._values()], phases])
+        parts = self.comm.allgather([delta, [float(v[1]) for v in self._values()], phases, self._graph_state()])
         if self.rank != 0:
             return
         d = [p[0] for p in parts]
@@ -419,7 +427,10 @@ class SPMDPopulation(_ReportMixin):
                "exploit_transfers": int(max(x[5] for x in d)), "exploit_bytes": int(sum(x[3] for x in d)),
                "exploit_dataplane_s": max(x[4] for x in d), "population": len(accs),
                "best_acc": max(accs) if accs else None, "mean_acc": sum(accs) / len(accs) if accs else None,
-               "world_size": self.world, "phases_s": phase_s}
+               "world_size": self.world, "phases_s": phase_s,
+               # how the HIP step ran on each rank ("captured" graph replay / "eager_fallback" when a data-parallel
+               # capture was refused / "disabled" / None for torch backends): a silent eager cliff shows up here
+               "step_graph": sorted({str(p[3]) for p in parts})}
         self._prev_exploit = self.exploit_time
         import json
         os.makedirs(self.savedata, exist_ok=True)

@@ -124,7 +124,7 @@ def synthetic_images(n: int, shape, num_classes: int, seed: int, device, dtype=t
     return x.to(device), y.to(device)
 
 
-def learnable_cifar(n_train: int = 10000, n_test: int = 2000, seed: int = 7, noise: float = 0.9,
+def learnable_cifar(n_train: int = 10000, n_test: int = 2000, seed: int = 7, noise: float = 2.5,
                     num_classes: int = 10):
     """A learnable CIFAR-shaped dataset that needs no download (the real CIFAR-10 is not on these machines):
     uint8 NHWC 32x32x3 images with labels, so it runs through the real input path (on-device gather, pad-4 random
@@ -134,7 +134,9 @@ def learnable_cifar(n_train: int = 10000, n_test: int = 2000, seed: int = 7, noi
     random crop and a flip keep most of it) and every image is ``template[label] * contrast + noise`` with a
     per-image random contrast in [0.6, 1.4], brightness shift and i.i.d. pixel noise of ``noise`` template
     standard deviations.  Chance accuracy is 1/num_classes; a ResNet-20 reaches well above it within a few hundred
-    steps, so loss / accuracy trajectories of two implementations can be compared (tests/test_gpu_trajectory.py).
+    steps (ResNet-8 fp32 on CPU at noise 2.5: training loss 2.1 -> 0.05 in 500 steps of batch 64; eval accuracy with the
+    reference's 0.997-momentum moving BN statistics 0.58 / 0.77 after 600 steps, still rising), so loss / accuracy
+    trajectories of two implementations can be compared (tests/test_gpu_trajectory.py).
     Returns (train_x, train_y, test_x, test_y) as numpy arrays."""
     g = torch.Generator().manual_seed(int(seed))
     base = torch.randn(num_classes, 3, 8, 8, generator=g)

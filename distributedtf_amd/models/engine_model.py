@@ -236,7 +236,12 @@ class EngineModel(ModelBase):
     def _batch(self, ds, gen):
         b = int(self.hparams["batch_size"])
         if self.dp is not None:
-            b = max(1, self.dp.local_batch(b))  # this replica's shard of the member's batch
+            if b < self.dp.size:
+                # an empty shard would still train on one image and the replica weights (local / member batch)
+                # would sum to more than 1, scaling the all-reduced gradient up
+                raise ValueError("member %d: batch_size %d < --dp_size %d (every replica needs >= 1 image)"
+                                 % (self.cluster_id, b, self.dp.size))
+            b = self.dp.local_batch(b)  # this replica's shard of the member's batch
         if hasattr(ds, "batch_slice"):
             return ds.batch_slice(b)
         if not hasattr(self, "_perm") or self._perm_pos + b > self._perm.numel():

@@ -77,8 +77,11 @@ class DataPlane:
                     src = src.contiguous()
                 ops.append(("send", src, dst_rank))
                 self.bytes_moved += src.numel() * src.element_size()
-                if steps is None and hasattr(local_members[src_id], "state_view"):
-                    self.comm.send(("dtf_step", src_id, int(local_members[src_id].global_step)), dst_rank)
+                if steps is None:
+                    # always posted for a cross-rank pair (and always consumed below), whatever the two members'
+                    # types: a condition only one side can evaluate would leave a message unread or a recv hanging
+                    self.comm.send(("dtf_step", src_id, int(getattr(local_members[src_id], "global_step", 0) or 0)),
+                                   dst_rank)
             elif dst_rank == self.rank:
                 dst_m = local_members[dst_id]
                 inplace = hasattr(dst_m, "state_view")
@@ -101,17 +104,16 @@ class DataPlane:
                 for r in dist.batch_isend_irecv(p2p):
                     r.wait()
         for dst_m, buf, inplace, src_id, src_rank in pending:
+            if steps is not None:
+                step = int(steps.get(src_id, 0))
+            else:
+                tag, sid, step = self.comm.recv(src_rank, timeout=self.step_timeout)
+                assert tag == "dtf_step" and sid == src_id, ("exploit step message out of order", tag, sid, src_id)
             if not inplace:
                 dst_m.import_state(buf)
                 continue
             hook = getattr(dst_m, "on_state_imported", None)
-            if hook is None:
-                continue
-            if steps is not None:
-                hook(int(steps[src_id]))
-            else:
-                tag, sid, step = self.comm.recv(src_rank, timeout=self.step_timeout)
-                assert tag == "dtf_step" and sid == src_id, ("exploit step message out of order", tag, sid, src_id)
+            if hook is not None:
                 hook(int(step))
         self.transfers_done += len(transfers)
         self.seconds += time.time() - t0

@@ -50,6 +50,14 @@ def _str2bool(v):
     return str(v).lower() in ("1", "true", "yes", "y", "t")
 
 
+def _synthetic(v):
+    """--use_synthetic_data: a boolean (reference flag), or ``learnable`` -- class-template CIFAR-shaped images
+    through the real input path, so eval accuracy can climb without the dataset (datasets.learnable_cifar)."""
+    if isinstance(v, str) and v.lower() == "learnable":
+        return "learnable"
+    return _str2bool(v)
+
+
 @dataclass
 class MemberConfig:
     """Per-member training settings derived from one hparam dict (no global flags)."""
@@ -100,7 +108,8 @@ def build_parser(defaults: Optional[Dict[str, Any]] = None) -> argparse.Argument
     p.add_argument("--resnet_size", type=int, default=None)
     p.add_argument("--resnet_version", type=int, default=2, choices=[1, 2])
     p.add_argument("--data_dir", default=None)
-    p.add_argument("--use_synthetic_data", type=_str2bool, default=None)
+    p.add_argument("--use_synthetic_data", type=_synthetic, default=None,
+                   help="true / false (reference flag) or 'learnable' (CIFAR: class-template images, real input path)")
     p.add_argument("--max_train_steps", type=int, default=None)
     p.add_argument("--debug_steps", type=int, default=None, help="MNIST: steps per 'epoch' (reference used 10)")
     p.add_argument("--batch_size", type=int, default=None, help="override every member's batch_size")

@@ -135,3 +135,21 @@ def test_dp_gradient_weighted_by_shard():
         torch.testing.assert_close(torch.from_numpy(grads[0]), want0)
         torch.testing.assert_close(torch.from_numpy(grads[1]), want1)
     assert abs(res[0][2][0] - 5 / 9.0) < 1e-6 and abs(res[1][2][0] - 4 / 9.0) < 1e-6
+
+
+def test_dp_rejects_batch_smaller_than_group():
+    """A member batch smaller than --dp_size would give some replica an empty shard: rejected."""
+    from distributedtf_amd.parallel.dataparallel import DPContext
+    from distributedtf_amd.models.cifar10_model import Cifar10Model
+    from distributedtf_amd.pbt.hparams import generate_random_hparam
+    import random
+    h = generate_random_hparam(random.Random(0))
+    h["batch_size"] = 3
+    m = Cifar10Model(0, h, "/tmp/dtf_dp_small/model_", seed=0, resnet_size=8, device="cpu", use_synthetic_data=True,
+                     checkpoint_every_round=False)
+    m.dp = DPContext(group=None, size=4, rank=0, group_index=0, n_groups=1)
+    with pytest.raises(ValueError, match="dp_size"):
+        m._batch(m.dataset(), None)
+    m.hparams["batch_size"] = 9
+    x, y = m._batch(m.dataset(), None)
+    assert x.shape[0] == 3  # 9 = 3 + 2 + 2 + 2

@@ -9,7 +9,7 @@ rc=$?; tail -25 gpurun_out/pbt_run/pytest.log
 [ $rc -ne 0 ] && { echo "pytest rc=$rc"; exit 1; }
 [ "${PBT:-1}" = "0" ] && { echo PBT_OK; exit 0; }
 rm -rf /tmp/pbt_run && mkdir -p /tmp/pbt_run && cd /tmp/pbt_run
-timeout -k 10 600 python -u $GRAFT_REPO_ROOT/main_manager.py 8 --model cifar10 --resnet_size 56 --use_synthetic_data true \
+timeout -k 10 600 python -u $GRAFT_REPO_ROOT/main_manager.py 8 --model cifar10 --resnet_size 56 --use_synthetic_data ${SYN:-true} \
   --max_train_steps ${STEPS:-200} --rounds ${ROUNDS:-4} --seed 1 --backend hip $PBT_ARGS > $GRAFT_REPO_ROOT/gpurun_out/pbt_run/main_manager.log 2>&1
 rc=$?
 cp savedata/metrics.jsonl savedata/best_model.json test_results.txt $GRAFT_REPO_ROOT/gpurun_out/pbt_run/ 2>/dev/null

@@ -95,7 +95,8 @@ def main():
                                     use_synthetic_data=True, checkpoint_every_round=False)
     elif args.model == "imagenet":
         make = lambda i: ImageNetModel(begin + i, hps[begin + i], "/tmp/bench_savedata_%d/model_" % rank,  # noqa: E731
-                                       seed=args.seed, resnet_size=args.resnet_size, device=dev, backend=args.backend,
+                                       seed=args.seed, resnet_size=args.resnet_size,
+                                       resnet_version=args.resnet_version, device=dev, backend=args.backend,
                                        capacity=max(1, cnt), use_synthetic_data=True, checkpoint_every_round=False)
     else:
         make = lambda i: Cifar10Model(begin + i, hps[begin + i], "/tmp/bench_savedata_%d/model_" % rank,  # noqa: E731

@@ -81,6 +81,17 @@ class GapArgs(ctypes.Structure):
                 ("hw", c_int), ("C", c_int), ("cmax", c_int)]
 
 
+class BnAddArgs(ctypes.Structure):
+    _fields_ = [("h", c_void_p), ("s", c_void_p), ("out", c_void_p), ("coef_h", c_void_p), ("coef_s", c_void_p),
+                ("img_slot", c_void_p), ("hw", c_long), ("C", c_int), ("cmax", c_int), ("nimg", c_long)]
+
+
+class BnSumArgs(ctypes.Structure):
+    _fields_ = [("dz", c_void_p), ("h", c_void_p), ("h2", c_void_p), ("fc", c_void_p), ("fc2", c_void_p),
+                ("sums", c_void_p), ("sums2", c_void_p), ("img_slot", c_void_p), ("hw", c_int), ("C", c_int),
+                ("cmax", c_int), ("pad", c_int)]
+
+
 _REGISTERED = False
 
 
@@ -110,7 +121,10 @@ def _register():
     reg("dtf_cg_softmax_ce", [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_long,
                               c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p])
     reg("dtf_cg_chan_stats", [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p])
-    for n in ("dtf_cg_args_size", "dtf_bnfin_args_size", "dtf_ew_args_size", "dtf_gap_args_size"):
+    reg("dtf_cg_bn_add_relu", [P(BnAddArgs), c_void_p])
+    reg("dtf_cg_bn_bwd_sums", [P(BnSumArgs), c_int, c_void_p])
+    for n in ("dtf_cg_args_size", "dtf_bnfin_args_size", "dtf_ew_args_size", "dtf_gap_args_size",
+              "dtf_bnadd_args_size", "dtf_bnsum_args_size"):
         reg(n, [])
     L = ops.lib()
     for name, args in ops._SIGNATURES.items():
@@ -119,7 +133,8 @@ def _register():
             fn.argtypes = args
             fn.restype = c_int
     for st, fn in ((CgArgs, "dtf_cg_args_size"), (BnFinArgs, "dtf_bnfin_args_size"), (EwArgs, "dtf_ew_args_size"),
-                   (GapArgs, "dtf_gap_args_size")):
+                   (GapArgs, "dtf_gap_args_size"), (BnAddArgs, "dtf_bnadd_args_size"),
+                   (BnSumArgs, "dtf_bnsum_args_size")):
         assert getattr(L, fn)() == ctypes.sizeof(st), "%s ABI mismatch" % st.__name__
     _REGISTERED = True
 
@@ -143,9 +158,9 @@ class HipImageNetBackend:
         self.dev = engine.device
         prog = engine.arch.prog
         cfg = prog.cfg
-        if not (cfg.bottleneck and cfg.version == 2 and cfg.first_pool_size == 3 and cfg.first_pool_stride == 2
+        if not (cfg.bottleneck and cfg.version in (1, 2) and cfg.first_pool_size == 3 and cfg.first_pool_stride == 2
                 and cfg.kernel_size == 7 and cfg.conv_stride == 2):
-            raise ValueError("HIP ImageNet backend supports the v2 bottleneck ImageNet configuration")
+            raise ValueError("HIP ImageNet backend supports the v1 / v2 bottleneck ImageNet configurations")
         if cfg.image_size % 32:
             raise ValueError("image size must be a multiple of 32")
         self.prog, self.cfg = prog, cfg
@@ -169,6 +184,13 @@ class HipImageNetBackend:
         self.coef = torch.zeros(2, nb, cap, 4, CMAX, dtype=torch.float32, device=self.dev)   # [fwd|bwd]
         self.loss = torch.zeros(cap, dtype=torch.float32, device=self.dev)
         self.correct = torch.zeros(cap, dtype=torch.float32, device=self.dev)
+        self.v1 = cfg.version == 1
+        if self.v1:
+            # identity "BN" coefficients (scale 1, shift 0): the convg epilogue's ReLU mask by BN(xm) > 0 then masks by
+            # xm > 0 -- the v1 block input is a ReLU output
+            self.ident = torch.zeros(cap, 4, CMAX, dtype=torch.float32, device=self.dev)
+            self.ident[:, 0].fill_(1.0)
+            self.ident[:, 3].fill_(1.0)
         self._plans: Dict[tuple, "_ImageNetPlan"] = {}
         self.use_graph = (os.environ.get("DTF_HIP_GRAPH", "1") == "1" and os.environ.get("DTF_DEBUG", "0") != "1")
 
@@ -303,6 +325,11 @@ class _ImageNetPlan:
         # stages its operand measured slower, 114.7 -> 135.7 ms/step at pop 8 x 128: the transform is repeated for
         # every output-channel tile and its coefficient LDS costs occupancy; profiles/r2_imagenet_fold_ab.log)
         self.ax, self.a1, self.a2 = [], [], []
+        # v1 (post-activation): h3 = conv3 output (BN3 input), sc = raw projection output (BN_p input), a0 = the
+        # stem's relu(BN(y0)); no ax (the block input IS a ReLU output)
+        self.v1 = be.v1
+        self.h3 = []
+        self.a0 = torch.empty(N, H1, H1, cfg.num_filters, dtype=bf, device=dev) if self.v1 else None
         hw, cin = H2, cfg.num_filters
         self.geo = []  # per block: (H_in, H_out, cin, f, fout)
         for bi, blk in enumerate(prog.blocks):
@@ -310,7 +337,8 @@ class _ImageNetPlan:
             ho = hw // blk.stride
             self.h1.append(act("h1", hw, c1.cout))
             self.h2.append(act("h2", ho, c2.cout))
-            self.ax.append(act("ax", hw, cin))
+            self.ax.append(act("ax", hw, cin) if not self.v1 else None)
+            self.h3.append(act("h3", ho, c3.cout) if self.v1 else None)
             self.a1.append(act("a1", hw, c1.cout))
             self.a2.append(act("a2", ho, c2.cout))
             self.sc.append(act("sc", ho, c3.cout) if blk.proj is not None else None)
@@ -330,9 +358,9 @@ class _ImageNetPlan:
             self.ev_coef = torch.zeros(nb, e.capacity, 4, CMAX, dtype=torch.float32, device=dev)
             self.ev_sink = torch.zeros(e.capacity, 2, CMAX, dtype=torch.float32, device=dev)  # conv-epilogue stats
             self.ev_acc = torch.zeros(2, e.capacity, dtype=torch.float32, device=dev)  # [correct, summed CE]
-            self._build_eval()
+            self._build_eval_v1() if self.v1 else self._build_eval()
         else:
-            self._build()
+            self._build_v1() if self.v1 else self._build()
         self.graph = None
 
     # ----------------------------------------------------------------------------------------- helpers
@@ -702,6 +730,204 @@ class _ImageNetPlan:
         self._add(L.dtf_cg_gap, ctypes.byref(g), 0, N)
         from .hip_mnist import GEMM_OUT_F32, GroupedGemm
         C = cfg.final_size
+        Dstride = NPAD_CLS * C
+        fwd = [(self.first[s] * C, s * Dstride, self.first[s] * NPAD_CLS, n, NPAD_CLS, C)
+               for s, n in zip(self.slots, self.sizes)]
+        self.g_fwd = GroupedGemm(self.feat, be.dense, self.logits, C, C, NPAD_CLS, fwd, False, False, GEMM_OUT_F32,
+                                 be.dev)
+        self._add("gemm", self.g_fwd)
+        self._add(L.dtf_cg_softmax_ce, _p(self.logits), NPAD_CLS, be.ncls, _p(self.labels), _p(self.img_slot),
+                  _p(e.state), e.S, prog.dense_b_off, None, e.Pp, _p(self.cnt), _p(self.ev_acc[1]),
+                  _p(self.ev_acc[0]), None, N)
+
+    # ------------------------------------------------------------------------------------ ResNet v1 program
+    def bn_add_relu(self, h, s, out, coef_h, coef_s, hw, C):
+        """v1 block output: out = relu(BN3(h) + (BN_p(s) if coef_s else s))."""
+        a = BnAddArgs()
+        a.h, a.s, a.out, a.coef_h, a.coef_s = _p(h), _p(s), _p(out), _p(coef_h), _p(coef_s)
+        a.img_slot, a.hw, a.C, a.cmax, a.nimg = _p(self.img_slot), hw * hw, C, CMAX, self.N
+        self._hold(a)
+        self._add(ops.lib().dtf_cg_bn_add_relu, ctypes.byref(a))
+
+    def bwd_sums(self, dz, h, bn, hw, C, h2=None, bn2=None):
+        """sum dz, sum dz * xhat of the post-activation BN `bn` (input h) [and of `bn2` (input h2), same dz]."""
+        a = BnSumArgs()
+        a.dz, a.h, a.h2 = _p(dz), _p(h), _p(h2)
+        a.fc, a.sums = _p(self.cf(bn)), _p(self.sb(bn))
+        if bn2 is not None:
+            a.fc2, a.sums2 = _p(self.cf(bn2)), _p(self.sb(bn2))
+        a.img_slot, a.hw, a.C, a.cmax = _p(self.img_slot), hw * hw, C, CMAX
+        self._hold(a)
+        self._add(ops.lib().dtf_cg_bn_bwd_sums, ctypes.byref(a), self.N)
+
+    def _forward_v1(self, sink=None):
+        """Forward of the v1 bottleneck net (reference resnet_model.py:215-264, 504-510): stem conv -> BN -> ReLU ->
+        max-pool; per block conv -> BN -> ReLU twice, conv -> BN, + shortcut (identity, or projection conv -> BN),
+        ReLU; no final BN.  Training: statistics epilogues + bn_final per BN; eval (``sink``): every BN's
+        coefficients come from the moving statistics (bn_final mode 2, issued by the caller)."""
+        be, prog, cfg = self.be, self.be.prog, self.be.cfg
+        L = ops.lib()
+        N, H = self.N, self.H
+        H1, H2 = H // 2, self.xs[0].shape[1]
+        train = sink is None
+        relu = L.dtf_cg_bn_relu_apply
+        sb = prog.stem_bn
+        self.conv(prog.stem, self.xin8, self.y0, H, mode=0, epi=4, st=self.sf(sb) if train else sink)
+        if train:
+            self.bn_final(sb, H1, False)
+        self.ew(relu, self.y0, self.a0, self.cf(sb), H1, cfg.num_filters)
+        self._add(L.dtf_cg_maxpool, _p(self.a0), _p(self.xs[0]), _p(self.am0), None, None, N, H1, H1, H2, H2,
+                  cfg.num_filters, 0)
+        for i, blk in enumerate(prog.blocks):
+            hi, ho, cin, f, fout = self.geo[i]
+            b1, b2, b3 = blk.bns
+            c1, c2, c3 = blk.convs
+            x = self.xs[i]
+            if blk.proj is not None:
+                self.conv(blk.proj, x, self.sc[i], hi, mode=0, epi=4, st=self.sf(blk.proj_bn) if train else sink)
+            self.conv(c1, x, self.h1[i], hi, mode=0, epi=4, st=self.sf(b1) if train else sink)
+            if train:
+                self.bn_final(b1, hi, False)
+            self.ew(relu, self.h1[i], self.a1[i], self.cf(b1), hi, f)
+            self.conv(c2, self.a1[i], self.h2[i], hi, mode=0, epi=4, st=self.sf(b2) if train else sink)
+            if train:
+                self.bn_final(b2, ho, False)
+            self.ew(relu, self.h2[i], self.a2[i], self.cf(b2), ho, f)
+            self.conv(c3, self.a2[i], self.h3[i], ho, mode=0, epi=4, st=self.sf(b3) if train else sink)
+            if train:
+                self.bn_final(b3, ho, False)
+                if blk.proj is not None:
+                    self.bn_final(blk.proj_bn, ho, False)
+            if blk.proj is not None:
+                self.bn_add_relu(self.h3[i], self.sc[i], self.xs[i + 1], self.cf(b3), self.cf(blk.proj_bn), ho, fout)
+            else:
+                self.bn_add_relu(self.h3[i], x, self.xs[i + 1], self.cf(b3), None, ho, fout)
+
+    def _build_v1(self):
+        be, e, prog, cfg = self.be, self.e, self.be.prog, self.be.cfg
+        L = ops.lib()
+        N, H = self.N, self.H
+        ns = len(self.slots)
+        self._add(L.dtf_cg_weight_prep, _p(e.state), e.S, _p(be.conv_table), 1, _p(self.slots_t), ns,
+                  _p(be.w), _p(be.w), be.wtot)
+        self._add(L.dtf_cg_dense_prep, _p(e.state), e.S, prog.dense_w_off, be.ncls, NPAD_CLS, cfg.final_size,
+                  _p(self.slots_t), ns, _p(be.dense), NPAD_CLS * cfg.final_size)
+        self._add("zero", be.sums)
+        self._add("zero", be.loss)
+        self._add("zero", be.correct)
+        self._add(L.dtf_cg_prep_input, _p(self.x_in), _p(self.xin8), N * H * H, cfg.in_channels)
+        self._forward_v1()
+        H1, H2, HL = H // 2, self.xs[0].shape[1], self.HL
+        C = cfg.final_size
+        # GAP of the last block output (already a ReLU output: no final BN in v1), dense, softmax CE
+        g = GapArgs()
+        g.x, g.coef, g.img_slot, g.feat = _p(self.xs[-1]), None, _p(self.img_slot), _p(self.feat)
+        g.dfeat, g.sums, g.bcoef = _p(self.dfeat), None, None
+        g.hw, g.C, g.cmax = HL * HL, C, CMAX
+        self._hold(g)
+        self._add(L.dtf_cg_gap, ctypes.byref(g), 0, N)
+        from .hip_mnist import GEMM_OUT_ACC, GEMM_OUT_F32, GroupedGemm
+        Dstride = NPAD_CLS * C
+        fwd, dgr, wgr = [], [], []
+        for s, n in zip(self.slots, self.sizes):
+            f0 = self.first[s]
+            fwd.append((f0 * C, s * Dstride, f0 * NPAD_CLS, n, NPAD_CLS, C))
+            dgr.append((f0 * NPAD_CLS, s * Dstride, f0 * C, n, C, NPAD_CLS))
+            wgr.append((f0 * NPAD_CLS, f0 * C, s * e.Pp + prog.dense_w_off, NPAD_CLS, C, n, be.ncls))
+        dev = be.dev
+        self.g_fwd = GroupedGemm(self.feat, be.dense, self.logits, C, C, NPAD_CLS, fwd, False, False, GEMM_OUT_F32, dev)
+        self.g_dgr = GroupedGemm(self.dlog, be.dense, self.dfeat, NPAD_CLS, C, C, dgr, False, True, GEMM_OUT_F32, dev)
+        self.g_wgr = GroupedGemm(self.dlog, self.feat, e.grads, NPAD_CLS, C, C, wgr, True, True, GEMM_OUT_ACC, dev)
+        self._add("gemm", self.g_fwd)
+        self._add(L.dtf_cg_softmax_ce, _p(self.logits), NPAD_CLS, be.ncls, _p(self.labels), _p(self.img_slot),
+                  _p(e.state), e.S, prog.dense_b_off, _p(e.grads), e.Pp, _p(self.cnt), _p(be.loss), _p(be.correct),
+                  _p(self.dlog), N)
+        self._add("gemm", self.g_dgr)
+        self._add("gemm", self.g_wgr)
+        # GAP backward: the gradient at the last block output, masked by its ReLU (cg_gap_bwd_apply, coef = null)
+        gz = self.tmp("gA" if (len(prog.blocks) % 2 == 0) else "gB", HL, C)
+        g2 = GapArgs()
+        ctypes.memmove(ctypes.addressof(g2), ctypes.addressof(g), ctypes.sizeof(GapArgs))
+        g2.out = _p(gz)
+        self._hold(g2)
+        self._add(L.dtf_cg_gap, ctypes.byref(g2), 2, N)
+        bwd = L.dtf_cg_bn_bwd_apply
+        # ---- blocks, reversed.  gz = dL/d(BN3(h3) + shortcut), already ReLU-masked (by the GAP backward, or by the
+        # next block's conv1 data-gradient epilogue)
+        for i in range(len(prog.blocks) - 1, -1, -1):
+            blk = prog.blocks[i]
+            hi, ho, cin, f, fout = self.geo[i]
+            b1, b2, b3 = blk.bns
+            c1, c2, c3 = blk.convs
+            x, h1, h2, h3 = self.xs[i], self.h1[i], self.h2[i], self.h3[i]
+            pbn = blk.proj_bn
+            # BN3 (and the projection BN: same dz) backward sums -> coefficients; dh3 = A3 gz + B3 h3 + C3
+            self.bwd_sums(gz, h3, b3, ho, fout, h2=self.sc[i] if pbn is not None else None, bn2=pbn)
+            self.bn_final(b3, ho, True)
+            dh3 = self.tmp("dh3", ho, fout)
+            self.ew(bwd, h3, dh3, self.cb(b3), ho, fout, dz=gz)
+            ds = None
+            if pbn is not None:
+                self.bn_final(pbn, ho, True)
+                ds = self.tmp("ds", ho, fout)
+                self.ew(bwd, self.sc[i], ds, self.cb(pbn), ho, fout, dz=gz)
+            # conv3: dz2 = dgrad(dh3) masked by relu(BN2(h2)) + BN2 backward sums
+            dz2 = self.tmp("dz3", ho, f)
+            self.conv(c3, dh3, dz2, ho, mode=0, epi=6, xm=h2, c_ep=self.cf(b2), st=self.sb(b2), dgrad=True)
+            self.bn_final(b2, ho, True)
+            dh2 = self.tmp("dh2", ho, f)
+            self.ew(bwd, h2, dh2, self.cb(b2), ho, f, dz=dz2)
+            self.wgrad(c3, self.a2[i], dh3, ho)
+            # conv2 (3x3 / s): dz1 = dgrad(dh2) masked by relu(BN1(h1)) + BN1 sums
+            dz1 = self.tmp("dz2", hi, f)
+            self.conv(c2, dh2, dz1, ho, mode=0, epi=6, xm=h1, c_ep=self.cf(b1), st=self.sb(b1), dgrad=True)
+            self.bn_final(b1, hi, True)
+            dh1 = self.tmp("dh1", hi, f)
+            self.ew(bwd, h1, dh1, self.cb(b1), hi, f, dz=dz1)
+            self.wgrad(c2, self.a1[i], dh2, hi)
+            res = gz
+            if blk.proj is not None:
+                res = self.tmp("pd", hi, cin)
+                self.conv(blk.proj, ds, res, ho, mode=0, epi=0, dgrad=True)
+                self.wgrad(blk.proj, x, ds, hi)
+            # conv1: g = dgrad(dh1) + shortcut gradient, masked by the block input's ReLU (x > 0) -> the previous
+            # block's gz (block 0: the pooled stem activation's)
+            gnext = self.tmp("gA" if (i % 2 == 0) else "gB", hi, cin)
+            self.conv(c1, dh1, gnext, hi, mode=0, epi=3, res=res, xm=x, c_ep=be.ident, dgrad=True)
+            self.wgrad(c1, x, dh1, hi)
+            gz = gnext
+        # ---- stem: max-pool backward (gz is masked by the pooled ReLU output > 0), BN_stem backward, stem wgrad
+        sbn = prog.stem_bn
+        dz0 = self.tmp("dz0", H1, cfg.num_filters)
+        self._add(L.dtf_cg_maxpool, None, None, _p(self.am0), _p(gz), _p(dz0), N, H1, H1, H2, H2, cfg.num_filters, 1)
+        self.bwd_sums(dz0, self.y0, sbn, H1, cfg.num_filters)
+        self.bn_final(sbn, H1, True)
+        dy0 = self.tmp("dy0", H1, cfg.num_filters)
+        self.ew(bwd, self.y0, dy0, self.cb(sbn), H1, cfg.num_filters, dz=dz0)
+        self.wgrad(prog.stem, self.xin8, dy0, H, mode_x=0, mode_dy=0)
+        self._add("optim", None)
+        self._add("step", None)
+
+    def _build_eval_v1(self):
+        be, e, prog, cfg = self.be, self.e, self.be.prog, self.be.cfg
+        L = ops.lib()
+        N, H = self.N, self.H
+        ns = len(self.slots)
+        self._add(L.dtf_cg_weight_prep, _p(e.state), e.S, _p(be.conv_table), 1, _p(self.slots_t), ns,
+                  _p(be.w), _p(be.w), be.wtot)
+        self._add(L.dtf_cg_dense_prep, _p(e.state), e.S, prog.dense_w_off, be.ncls, NPAD_CLS, cfg.final_size,
+                  _p(self.slots_t), ns, _p(be.dense), NPAD_CLS * cfg.final_size)
+        for b in range(len(prog.bns)):
+            self.bn_final(b, 1, 2)
+        self._add(L.dtf_cg_prep_input, _p(self.x_in), _p(self.xin8), N * H * H, cfg.in_channels)
+        self._forward_v1(sink=self.ev_sink)
+        HL, C = self.HL, cfg.final_size
+        g = GapArgs()
+        g.x, g.coef, g.img_slot, g.feat = _p(self.xs[-1]), None, _p(self.img_slot), _p(self.feat)
+        g.hw, g.C, g.cmax = HL * HL, C, CMAX
+        self._hold(g)
+        self._add(L.dtf_cg_gap, ctypes.byref(g), 0, N)
+        from .hip_mnist import GEMM_OUT_F32, GroupedGemm
         Dstride = NPAD_CLS * C
         fwd = [(self.first[s] * C, s * Dstride, self.first[s] * NPAD_CLS, n, NPAD_CLS, C)
                for s, n in zip(self.slots, self.sizes)]

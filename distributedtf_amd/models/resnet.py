@@ -459,9 +459,9 @@ class ResNetArch:
         self.num_classes = cfg.num_classes
         self.input_shape = (cfg.image_size, cfg.image_size, cfg.in_channels)
         # population-batched HIP kernels: CIFAR-shape building-block nets (v1 and v2, engine/hip_resnet.py) and
-        # the ImageNet-shape v2 bottleneck nets (engine/hip_imagenet.py)
+        # the ImageNet-shape v1 / v2 bottleneck nets (engine/hip_imagenet.py)
         self.hip_supported = ((cfg.image_size == 32 and not cfg.bottleneck and cfg.version in (1, 2))
-                              or (cfg.bottleneck and cfg.version == 2 and cfg.first_pool_size == 3
+                              or (cfg.bottleneck and cfg.version in (1, 2) and cfg.first_pool_size == 3
                                   and cfg.image_size % 32 == 0))
 
     @property

@@ -1085,6 +1085,7 @@ DTF_API int dtf_convg_fwd(const CgArgs* a, int tc, int mode, int epi, int trans,
   CG_ALL_TC(0, 7, false, 1)
   CG_ALL_TC(0, 0, false, 1)
   CG_ALL_TC(2, 0, false, 1)
+  CG_ALL_TC(0, 3, false, 1)  // v1 bottleneck conv1: + shortcut gradient, masked by the block input's ReLU
   CG_ALL_TC(0, 6, true, 1)
   CG_ALL_TC(2, 6, true, 1)
   CG_ALL_TC(2, 7, true, 1)

@@ -532,7 +532,173 @@ __global__ __launch_bounds__(256) void cg_chan_stats_kernel(const bf16_t* __rest
   }
 }
 
+// ---- ResNet v1 (post-activation) bottleneck blocks (reference resnet_model.py:215-264)
+// Block output y = relu(BN3(h3) + shortcut), shortcut = BN_p(s) (projection conv output s) or the block input.
+struct BnAddArgs {
+  const bf16_t* h;       // conv3 output (BN3 input)
+  const bf16_t* s;       // projection conv output (coef_s) or the block input (coef_s == null: identity)
+  bf16_t* out;
+  const float* coef_h;   // [cap][4][cmax] forward coefficients of BN3
+  const float* coef_s;   // ... of the projection BN, or null
+  const int* img_slot;
+  long hw;
+  int C, cmax;
+  long nimg;
+};
+
+__global__ __launch_bounds__(256) void cg_bn_add_relu_kernel(BnAddArgs a) {
+  const int img = blockIdx.x;
+  const int slot = a.img_slot[img];
+  const float* ch = a.coef_h + (long)slot * 4 * a.cmax;
+  const float* cs = a.coef_s ? a.coef_s + (long)slot * 4 * a.cmax : nullptr;
+  const long base = (long)img * a.hw * a.C;
+  const long n8 = a.hw * a.C / 8;
+  const long stride = (long)gridDim.y * blockDim.x;
+  const bf16_t* __restrict__ h = a.h + base;
+  const bf16_t* __restrict__ s = a.s + base;
+  bf16_t* __restrict__ out = a.out + base;
+  for (long i0 = (long)blockIdx.y * blockDim.x + threadIdx.x; i0 < n8; i0 += EW_U * stride) {
+    uint4 hv[EW_U], sv[EW_U];
+#pragma unroll
+    for (int u = 0; u < EW_U; ++u) {
+      const long i = i0 + u * stride;
+      hv[u] = sv[u] = make_uint4(0, 0, 0, 0);
+      if (i < n8) {
+        hv[u] = *reinterpret_cast<const uint4*>(h + i * 8);
+        sv[u] = *reinterpret_cast<const uint4*>(s + i * 8);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < EW_U; ++u) {
+      const long i = i0 + u * stride;
+      if (i >= n8) break;
+      const int c0 = chan8(i, a.C);
+      float sc[8], sh[8], ps[8], pt[8];
+      coef8(ch + c0, sc);
+      coef8(ch + a.cmax + c0, sh);
+      if (cs) {
+        coef8(cs + c0, ps);
+        coef8(cs + a.cmax + c0, pt);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) ps[k] = 1.f, pt[k] = 0.f;
+      }
+      const uint32_t h32[4] = {hv[u].x, hv[u].y, hv[u].z, hv[u].w}, s32[4] = {sv[u].x, sv[u].y, sv[u].z, sv[u].w};
+      uint32_t r[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float v0 = __uint_as_float(h32[q] << 16) * sc[2 * q] + sh[2 * q] +
+                         __uint_as_float(s32[q] << 16) * ps[2 * q] + pt[2 * q];
+        const float v1 = __uint_as_float(h32[q] & 0xffff0000u) * sc[2 * q + 1] + sh[2 * q + 1] +
+                         __uint_as_float(s32[q] & 0xffff0000u) * ps[2 * q + 1] + pt[2 * q + 1];
+        r[q] = pack2bf(fmaxf(v0, 0.f), fmaxf(v1, 0.f));
+      }
+      *reinterpret_cast<uint4*>(out + i * 8) = make_uint4(r[0], r[1], r[2], r[3]);
+    }
+  }
+}
+
+// BN-backward sums of post-activation BNs whose output gradient dz is already ReLU-masked (v1: the block output's
+// mask is applied by the consumer's data-gradient epilogue): sum dz and sum dz * xhat into [cap][2][cmax], for
+// the BN of h and optionally a second BN of h2 that received the same dz (v1 projection BN of the shortcut).
+// Layout as cg_chan_stats: thread = 8 fixed channels, LDS accumulators, one global atomic per workgroup+channel.
+struct BnSumArgs {
+  const bf16_t* dz;
+  const bf16_t* h;
+  const bf16_t* h2;     // null: one BN
+  const float* fc;      // forward coefficients of h's BN (mean at 2*cmax, inv at 3*cmax)
+  const float* fc2;
+  float* sums;
+  float* sums2;
+  const int* img_slot;
+  int hw, C, cmax, pad;
+};
+
+__global__ __launch_bounds__(256) void cg_bn_bwd_sums_kernel(BnSumArgs a) {
+  __shared__ float acc[3][2048];
+  const int img = blockIdx.x, slot = a.img_slot[img];
+  const bool two = a.h2 != nullptr;
+  for (int i = threadIdx.x; i < 3 * a.C; i += blockDim.x) (&acc[0][0])[(i / a.C) * 2048 + i % a.C] = 0.f;
+  __syncthreads();
+  const long n8 = (long)a.hw * a.C / 8;
+  const long i0 = (long)blockIdx.y * blockDim.x + threadIdx.x, st = (long)gridDim.y * blockDim.x;
+  if (i0 < n8 && (st * 8) % a.C == 0) {
+    const int c0 = (int)((i0 * 8) % a.C);
+    const float* f1 = a.fc + (long)slot * 4 * a.cmax;
+    float mu[8], iv[8], mu2[8], iv2[8];
+    coef8(f1 + 2 * a.cmax + c0, mu);
+    coef8(f1 + 3 * a.cmax + c0, iv);
+    if (two) {
+      const float* f2 = a.fc2 + (long)slot * 4 * a.cmax;
+      coef8(f2 + 2 * a.cmax + c0, mu2);
+      coef8(f2 + 3 * a.cmax + c0, iv2);
+    }
+    float s[8], q[8], q2[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] = q[k] = q2[k] = 0.f;
+    const long base = (long)img * a.hw * a.C;
+    for (long i = i0; i < n8; i += st) {
+      const uint4 dv = *reinterpret_cast<const uint4*>(a.dz + base + i * 8);
+      const uint4 hv = *reinterpret_cast<const uint4*>(a.h + base + i * 8);
+      const uint4 gv = two ? *reinterpret_cast<const uint4*>(a.h2 + base + i * 8) : make_uint4(0, 0, 0, 0);
+      const uint32_t d32[4] = {dv.x, dv.y, dv.z, dv.w}, h32[4] = {hv.x, hv.y, hv.z, hv.w},
+                     g32[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int sh = 16 * (k & 1);
+        const float d = bf2f((bf16_t)((d32[k >> 1] >> sh) & 0xffff));
+        const float hx = bf2f((bf16_t)((h32[k >> 1] >> sh) & 0xffff));
+        s[k] += d;
+        q[k] += d * (hx - mu[k]) * iv[k];
+        if (two) {
+          const float gx = bf2f((bf16_t)((g32[k >> 1] >> sh) & 0xffff));
+          q2[k] += d * (gx - mu2[k]) * iv2[k];
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      atomicAdd(&acc[0][c0 + k], s[k]);
+      atomicAdd(&acc[1][c0 + k], q[k]);
+      if (two) atomicAdd(&acc[2][c0 + k], q2[k]);
+    }
+  }
+  __syncthreads();
+  float* su = a.sums + (long)slot * 2 * a.cmax;
+  float* su2 = two ? a.sums2 + (long)slot * 2 * a.cmax : nullptr;
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+    atomicAdd(su + c, acc[0][c]);
+    atomicAdd(su + a.cmax + c, acc[1][c]);
+    if (two) {
+      atomicAdd(su2 + c, acc[0][c]);
+      atomicAdd(su2 + a.cmax + c, acc[2][c]);
+    }
+  }
+}
+
 }  // namespace
+
+DTF_API int dtf_bnadd_args_size() { return (int)sizeof(BnAddArgs); }
+DTF_API int dtf_bnsum_args_size() { return (int)sizeof(BnSumArgs); }
+
+DTF_API int dtf_cg_bn_add_relu(const BnAddArgs* a, hipStream_t stream) {
+  if (a->nimg <= 0) return 0;
+  if (a->C % 8) return -2;
+  const long n8 = a->hw * a->C / 8;
+  long split = (4096 + a->nimg - 1) / a->nimg;
+  const long ms = (n8 + 255) / 256;
+  if (split > ms) split = ms;
+  if (split < 1) split = 1;
+  hipLaunchKernelGGL(cg_bn_add_relu_kernel, dim3((unsigned)a->nimg, (unsigned)split), dim3(256), 0, stream, *a);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_cg_bn_bwd_sums(const BnSumArgs* a, int nimg, hipStream_t stream) {
+  if (nimg <= 0) return 0;
+  if (a->C > 2048 || a->C % 8 || 2048 % a->C) return -2;
+  hipLaunchKernelGGL(cg_bn_bwd_sums_kernel, dim3(nimg, 8), dim3(256), 0, stream, *a);
+  return DTF_CHECK_LAUNCH();
+}
 
 DTF_API int dtf_cg_chan_stats(const bf16_t* x, const int* img_slot, float* sums, int nimg, int hw, int C, int cmax,
                               hipStream_t stream) {

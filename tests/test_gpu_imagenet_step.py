@@ -25,14 +25,17 @@ def _relerr(a, b):
     return float((a - b).norm() / (b.norm() + 1e-30))
 
 
-@pytest.mark.parametrize("image,sizes,graph", [(64, (4, 6), "1"), (64, (4, 6), "0"), (224, (16, 16), "1")])
-def test_hip_imagenet_step_matches_reference(monkeypatch, image, sizes, graph):
+@pytest.mark.parametrize("image,sizes,graph,version", [(64, (4, 6), "1", 2), (64, (4, 6), "0", 2),
+                                                       (224, (16, 16), "1", 2), (64, (4, 6), "1", 1),
+                                                       (64, (4, 6), "0", 1), (224, (16, 16), "1", 1)])
+def test_hip_imagenet_step_matches_reference(monkeypatch, image, sizes, graph, version):
     """Step 1 (lr 0) is the eager warm-up that captures the graph; step 2 (lr 1) is the first graph REPLAY (graph
     "1") or a second eager run ("0") -- its parameter delta is compared.  224 x 224 at 2 x 16 runs the benchmark's
-    tile / split-K choices."""
+    tile / split-K choices.  Version 1: the post-activation bottleneck (reference resnet_model.py:215-264; stem
+    BN+ReLU, projection BN on the shortcut, ReLU after the residual add, no final BN)."""
     monkeypatch.setenv("DTF_HIP_GRAPH", graph)
     torch.manual_seed(0)
-    arch = ResNetArch(imagenet_config(50, 2, num_classes=1001, image_size=image))
+    arch = ResNetArch(imagenet_config(50, version, num_classes=1001, image_size=image))
     dev = torch.device("cuda")
     sizes = list(sizes)
     ref = PopulationEngine(arch, 2, dev, backend="torch", compute_dtype=torch.float32, optimizer_impl="hip")

@@ -41,6 +41,8 @@ def parse():
     p.add_argument("--resnet_size", type=int, default=None, help="default 56 (CIFAR) / 50 (imagenet)")
     p.add_argument("--resnet_version", type=int, default=2, choices=[1, 2])
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                   help="compute dtype; fp32 = the reference's default (CIFAR ResNets: the fp32 HIP step)")
     p.add_argument("--exploit_every", type=int, default=None,
                    help="steps between PBT exploit/explore cycles inside the timed region; default "
                         "min(25, max(1, steps // 2)) so every timed run holds at least one cycle; 0 = none")
@@ -101,7 +103,7 @@ def main():
     else:
         make = lambda i: Cifar10Model(begin + i, hps[begin + i], "/tmp/bench_savedata_%d/model_" % rank,  # noqa: E731
                                       seed=args.seed, resnet_size=args.resnet_size, resnet_version=args.resnet_version,
-                                      device=dev, backend=args.backend,
+                                      device=dev, backend=args.backend, dtype=args.dtype,
                                       capacity=max(1, cnt), use_synthetic_data=True, checkpoint_every_round=False)
     members = [make(i) for i in range(cnt)]
     eng = members[0].engine
@@ -224,7 +226,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": args.dtype,
             "data": "synthetic (device-resident random-normal %s, uniform labels), random-init weights"
                     % "x".join(str(d) for d in members[0].arch.input_shape),
             "config": {"model": members[0].arch.name,

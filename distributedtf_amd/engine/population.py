@@ -273,14 +273,26 @@ class TorchBackend:
         return e.arch.forward(e.params[slot], e.running[slot], x, training=False, dtype=e.compute_dtype)
 
 
+def _hip_f32_ok(engine) -> bool:
+    """fp32 HIP step (engine/hip_f32.py): CIFAR-shape building-block ResNets."""
+    if engine.compute_dtype != torch.float32:
+        return False
+    from .hip_f32 import supports
+    return supports(engine.arch)
+
+
 def make_backend(engine: PopulationEngine, name: str):
     if name == "auto":
         name = "hip" if (engine.device.type == "cuda" and getattr(engine.arch, "hip_supported", False)
-                         and engine.compute_dtype == torch.bfloat16) else "torch"
-    if name == "hip" and engine.compute_dtype != torch.bfloat16:
-        raise ValueError("the HIP kernels compute in bf16 (got %s): use the torch backend" % engine.compute_dtype)
+                         and (engine.compute_dtype == torch.bfloat16 or _hip_f32_ok(engine))) else "torch"
+    if name == "hip" and engine.compute_dtype != torch.bfloat16 and not _hip_f32_ok(engine):
+        raise ValueError("the HIP kernels of this model compute in bf16 (got %s; fp32 HIP runs the CIFAR ResNets): "
+                         "use the torch backend" % engine.compute_dtype)
     if name == "torch":
         return TorchBackend(engine)
+    if name == "hip" and engine.compute_dtype == torch.float32:
+        from .hip_f32 import HipResNetF32Backend
+        return HipResNetF32Backend(engine)
     if name == "hip":
         if getattr(engine.arch, "name", "") == "mnist_cnn":
             from .hip_mnist import HipMnistBackend

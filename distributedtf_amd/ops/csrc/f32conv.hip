@@ -1,0 +1,712 @@
+// fp32 population-batched CIFAR ResNet kernels (gfx950): the --dtype fp32 path (the reference's default dtype,
+// resnet/official/utils/flags/_performance.py:30-33), accurate to fp32 rounding instead of bf16.
+//
+// Tensors are NHWC fp32 with the images of every member packed along N; weights are read straight from the fp32
+// master state rows (OHWI at the conv's offset) -- no weight-prep pass, no bf16 shadow.  Matrix products run on
+// v_mfma_f32_16x16x4_f32 (fp32 inputs, fp32 accumulation): A = 16 rows x 4 k (one float per lane: row lane % 16,
+// k lane / 16), B = 4 k x 16 columns (k lane / 16, column lane % 16), D = 16 x 16 (lane holds rows
+// 4 (lane / 16) + i, column lane % 16).
+//
+//  f32conv  : out[p][o] = sum_k A[k][o] * T(gathered)[p][k], forward (k = (tap, ci), any stride) or data gradient
+//             (k = (tap, o) over dy; dx pixel (y, x) reads dy at ((y + P - ky) / S, (x + P - kx) / S) when
+//             divisible -- the transposed convolution without a flipped weight copy).  T: identity | relu(x s + t)
+//             | A dz + B h + C (BN backward).  Epilogue: [+ residual] [mask by BN(xm) + ReLU > 0] [per-channel
+//             statistics: y, y^2 (forward) or dz, dz * xhat (with the mask)] -> fp32 sums [cap][2][cmax] that the
+//             shared bn_final kernel (convg_aux.hip) turns into coefficients.
+//  f32wgrad : dW[o][k] += sum_p T_dy(dy)[p][o] * T_x(gather(x))[p][k], split over pixel chunks, fp32 atomics into
+//             the member's gradient row.
+//  elementwise / head: BN-backward apply, ReLU(BN) apply, v1 block output and BN-backward sums, global average
+//             pool (+ final BN + ReLU), dense + softmax CE, dense gradient (fixed-order per member), GAP backward.
+#include "common.h"
+
+namespace {
+
+__device__ __forceinline__ f32x4_t mfma4(float a, float b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+struct F32Args {
+  const float* x;     // gathered operand (fwd: input; dgrad: dy; wgrad: x)
+  const float* x2;    // MODE 2: the BN input h of the gathered operand's BN-backward transform
+  const float* dy;    // wgrad: output-side operand
+  const float* dy2;   // wgrad: BN input of dy's BN-backward transform
+  const float* w;     // fp32 master rows; OHWI weights at w_off
+  long w_mstride, w_off;
+  float* y;
+  const float* res;   // residual added in the epilogue
+  const float* xm;    // epilogue mask source
+  float* grads;
+  long g_mstride, g_off;
+  const float* c_in;  // [cap][4][cmax] transform coefficients of the gathered operand
+  const float* c_dy;  // wgrad: of dy
+  const float* c_ep;  // epilogue mask BN (scale, shift, mean, inv)
+  float* st_out;      // [cap][2][cmax] statistics (atomics)
+  const int4* work;   // (slot, p0, p1, o0 [| n0 / 16 << 16 for wgrad])
+  int Hi, Wi, Ci;     // gathered tensor (fwd: x, dgrad: dy)
+  int Ho, Wo, Co;     // output tensor (wgrad: dy)
+  int kh, kw, stride, pad;  // FORWARD conv geometry
+  int cmax, log2ci;
+  int wci;            // input channels of the weight row (the stem's 3; Ci is its 4-channel padded gather)
+  int pad_;
+};
+
+constexpr int F_TP = 64;  // output pixels per conv workgroup
+constexpr int F_BK = 16;  // k per LDS stage
+constexpr int f_pitch(int n) { return n == 64 ? 80 : (n == 32 ? 48 : 16); }  // LDS row pitch: 4 row groups of a
+// fragment read land 16 banks apart
+
+// ------------------------------------------------------------------------------------------------ fwd / dgrad
+template <int TC, int MODE, int EPI, bool DGRAD>
+__global__ __launch_bounds__(256) void f32conv_kernel(F32Args a) {
+  constexpr int MT = TC / 16;
+  constexpr int PA = f_pitch(TC), PB = f_pitch(F_TP);
+  constexpr int AE = TC * F_BK / 256;  // A elements per thread per stage
+  __shared__ __attribute__((aligned(16))) float sA[2][F_BK * PA];
+  __shared__ __attribute__((aligned(16))) float sB[2][F_BK * PB];
+  __shared__ float acc_lds[2][TC];
+  extern __shared__ float dyn[];  // transform coefficients: MODE 1: 2 * Ci, MODE 2: 3 * Ci
+  const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z >= wk.y && wk.z - wk.y <= F_TP);
+  const int slot = wk.x, p0 = wk.y, p1 = wk.z, o0 = wk.w;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int Ci = a.Ci, kk = a.kh * a.kw;
+  const int K = kk * Ci;
+  if constexpr (MODE != 0) {
+    const float* cb = a.c_in + (long)slot * 4 * a.cmax;
+    for (int i = tid; i < Ci; i += 256) {
+      dyn[i] = cb[i];
+      dyn[Ci + i] = cb[a.cmax + i];
+      if constexpr (MODE == 2) dyn[2 * Ci + i] = cb[2 * a.cmax + i];
+    }
+  }
+  for (int i = tid; i < 2 * TC; i += 256) (&acc_lds[0][0])[i] = 0.f;
+  // this thread's B row (pixel) and k chunk (4 consecutive k of one tap: Ci % 4 == 0)
+  const int rB = tid >> 2, cB = tid & 3;
+  const int pB = p0 + rB;
+  const bool okp = pB < p1;
+  const int HWo = a.Ho * a.Wo;
+  const int pp = okp ? pB : p0;
+  const int img = pp / HWo, rem = pp - img * HWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
+  const int by = DGRAD ? oy + a.pad : oy * a.stride - a.pad;
+  const int bx = DGRAD ? ox + a.pad : ox * a.stride - a.pad;
+  const long ibase = (long)img * a.Hi * a.Wi * Ci;
+  const float* wrow = a.w + (long)slot * a.w_mstride + a.w_off;
+  float4 rb, rb2;
+  bool okb;
+  int cb_;
+  auto load_b = [&](int k0) {
+    const int k = k0 + 4 * cB;
+    const int tap = k >> a.log2ci, ci = k & (Ci - 1);
+    const int ky = a.kw == 1 ? tap : tap / a.kw, kx = tap - ky * a.kw;
+    int iy, ix;
+    bool ok;
+    if constexpr (DGRAD) {
+      const int ny = by - ky, nx = bx - kx;
+      iy = ny / a.stride;
+      ix = nx / a.stride;
+      ok = ny >= 0 && nx >= 0 && iy * a.stride == ny && ix * a.stride == nx && iy < a.Hi && ix < a.Wi;
+    } else {
+      iy = by + ky;
+      ix = bx + kx;
+      ok = iy >= 0 && ix >= 0 && iy < a.Hi && ix < a.Wi;
+    }
+    ok = ok && okp && k < K;
+    const long off = ibase + ((long)iy * a.Wi + ix) * Ci + ci;
+    rb = ok ? *reinterpret_cast<const float4*>(a.x + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (MODE == 2) rb2 = ok ? *reinterpret_cast<const float4*>(a.x2 + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+    okb = ok;
+    cb_ = ci;
+  };
+  auto store_b = [&](float* dst) {
+    float v[4] = {rb.x, rb.y, rb.z, rb.w};
+    if constexpr (MODE != 0) {
+      const float h[4] = {rb2.x, rb2.y, rb2.z, rb2.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = cb_ + j;
+        float t;
+        if constexpr (MODE == 1)
+          t = fmaxf(v[j] * dyn[c] + dyn[Ci + c], 0.f);
+        else
+          t = dyn[c] * v[j] + dyn[Ci + c] * h[j] + dyn[2 * Ci + c];
+        v[j] = okb ? t : 0.f;  // zero padding stays zero after the transform
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dst[(4 * cB + j) * PB + rB] = v[j];
+  };
+  float ra[AE];
+  auto load_a = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < AE; ++j) {
+      const int idx = tid + 256 * j;
+      int m, kl;
+      if constexpr (DGRAD) {  // A[k = (tap, o)][m = dx channel i] = W[o][tap][o0 + m]: contiguous in m
+        m = idx % TC;
+        kl = idx / TC;
+      } else {                // A[k][m = o] = W[o0 + m][k]: contiguous in k
+        m = idx / F_BK;
+        kl = idx % F_BK;
+      }
+      const int k = k0 + kl;
+      bool ok = k < K && o0 + m < a.Co;
+      long off;
+      const int tap = k >> a.log2ci, ci = k & (Ci - 1);
+      if constexpr (DGRAD) {  // ci = dy channel o
+        off = ((long)ci * kk + tap) * a.Co + o0 + m;
+      } else {
+        ok = ok && ci < a.wci;
+        off = ((long)(o0 + m) * kk + tap) * a.wci + ci;
+      }
+      ra[j] = ok ? wrow[off] : 0.f;
+    }
+  };
+  auto store_a = [&](float* dst) {
+#pragma unroll
+    for (int j = 0; j < AE; ++j) {
+      const int idx = tid + 256 * j;
+      const int m = DGRAD ? idx % TC : idx / F_BK, kl = DGRAD ? idx / TC : idx % F_BK;
+      dst[kl * PA + m] = ra[j];
+    }
+  };
+  f32x4_t acc[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acc[m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  __syncthreads();  // coefficients
+  const int nk = (K + F_BK - 1) / F_BK;
+  load_a(0);
+  load_b(0);
+  store_a(sA[0]);
+  store_b(sB[0]);
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    const int cur = ks & 1;
+    const bool more = ks + 1 < nk;
+    if (more) {
+      load_a(F_BK * (ks + 1));
+      load_b(F_BK * (ks + 1));
+    }
+    const float* A = sA[cur];
+    const float* B = sB[cur];
+#pragma unroll
+    for (int q = 0; q < F_BK / 4; ++q) {
+      const int kr = 4 * q + (lane >> 4);
+      const float bv = B[kr * PB + 16 * wave + (lane & 15)];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[m] = mfma4(A[kr * PA + 16 * m + (lane & 15)], bv, acc[m]);
+    }
+    if (more) {
+      store_a(sA[cur ^ 1]);
+      store_b(sB[cur ^ 1]);
+    }
+    __syncthreads();
+  }
+  // ---- epilogue: lane holds channels o0 + 16 m + 4 (lane / 16) + i of pixel p0 + 16 wave + lane % 16
+  const int p = p0 + 16 * wave + (lane & 15);
+  const bool pok = p < p1;
+  float ss[MT][4], sq[MT][4];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int co = o0 + 16 * m + 4 * (lane >> 4);
+    const bool ok = pok && co < a.Co;
+    const long o = (long)p * a.Co + co;
+    float v[4] = {acc[m][0], acc[m][1], acc[m][2], acc[m][3]};
+    float xv[4] = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPI & 1) {
+      if (ok) {
+        const float4 r = *reinterpret_cast<const float4*>(a.res + o);
+        v[0] += r.x, v[1] += r.y, v[2] += r.z, v[3] += r.w;
+      }
+    }
+    const float* ep = (EPI & 2) ? a.c_ep + (long)slot * 4 * a.cmax + (ok ? co : 0) : nullptr;
+    if constexpr (EPI & 2) {
+      if (ok) {
+        const float4 xr = *reinterpret_cast<const float4*>(a.xm + o);
+        xv[0] = xr.x, xv[1] = xr.y, xv[2] = xr.z, xv[3] = xr.w;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = (xv[i] * ep[i] + ep[a.cmax + i] > 0.f) ? v[i] : 0.f;
+    }
+    if (ok) *reinterpret_cast<float4*>(a.y + o) = make_float4(v[0], v[1], v[2], v[3]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float vv = ok ? v[i] : 0.f;
+      ss[m][i] = vv;
+      if constexpr (EPI & 2)
+        sq[m][i] = ok ? vv * (xv[i] - ep[2 * a.cmax + i]) * ep[3 * a.cmax + i] : 0.f;
+      else
+        sq[m][i] = vv * vv;
+    }
+  }
+  if constexpr (EPI & 4) {
+    // the 16 lanes of one lane / 16 group hold the same 4 channels (16 pixels): butterfly, one LDS atomic per
+    // group and channel, one global atomic per workgroup and channel
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float s_ = ss[m][i], q_ = sq[m][i];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s_ += __shfl_xor(s_, o, 64);
+          q_ += __shfl_xor(q_, o, 64);
+        }
+        if ((lane & 15) == 0) {
+          atomicAdd(&acc_lds[0][16 * m + 4 * (lane >> 4) + i], s_);
+          atomicAdd(&acc_lds[1][16 * m + 4 * (lane >> 4) + i], q_);
+        }
+      }
+    __syncthreads();
+    if (tid < TC && o0 + tid < a.Co) {
+      float* st = a.st_out + (long)slot * 2 * a.cmax;
+      atomicAdd(st + o0 + tid, acc_lds[0][tid]);
+      atomicAdd(st + a.cmax + o0 + tid, acc_lds[1][tid]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------ wgrad
+// work: (slot, p0, p1, o0 | (n0 / 16) << 16); rows o0 .. o0 + TC of dW, columns n0 .. n0 + 64 of K; pixels p0..p1 of
+// the OUTPUT grid (dy), 16 per stage.  Each wave owns 16 columns and every row tile.
+template <int TC, int MODE_X, int MODE_DY>
+__global__ __launch_bounds__(256) void f32wgrad_kernel(F32Args a) {
+  constexpr int MT = TC / 16, TN = 64, BP = 16;  // pixels per stage
+  constexpr int PA = f_pitch(TC), PB = f_pitch(TN);
+  constexpr int DE = TC / 16;                    // dy floats per thread per stage
+  __shared__ __attribute__((aligned(16))) float sA[2][BP * PA];  // [pixel][o]
+  __shared__ __attribute__((aligned(16))) float sB[2][BP * PB];  // [pixel][k]
+  extern __shared__ float dyn[];  // x coefficients (2 Ci) | dy coefficients (3 Co)
+  const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z >= wk.y);
+  const int slot = wk.x, p0 = wk.y, p1 = wk.z, o0 = wk.w & 0xffff, n0 = (wk.w >> 16) * 16;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int Ci = a.Ci, K = a.kh * a.kw * Ci;
+  float* cx = dyn;
+  float* cd = dyn + 2 * Ci;
+  if constexpr (MODE_X != 0) {
+    const float* cb = a.c_in + (long)slot * 4 * a.cmax;
+    for (int i = tid; i < Ci; i += 256) {
+      cx[i] = cb[i];
+      cx[Ci + i] = cb[a.cmax + i];
+    }
+  }
+  if constexpr (MODE_DY != 0) {
+    const float* cb = a.c_dy + (long)slot * 4 * a.cmax;
+    for (int i = tid; i < a.Co; i += 256) {
+      cd[i] = cb[i];
+      cd[a.Co + i] = cb[a.cmax + i];
+      cd[2 * a.Co + i] = cb[2 * a.cmax + i];
+    }
+  }
+  const int HWo = a.Ho * a.Wo;
+  // dy stage: pixel tid / 16, channels o0 + (tid % 16) * DE ..
+  const int pD = tid >> 4, oD = o0 + (tid & 15) * DE;
+  // x stage: pixel tid / 16, columns n0 + 4 (tid % 16) ..
+  const int pX = tid >> 4, kX = n0 + 4 * (tid & 15);
+  const int tapX = kX >> a.log2ci, ciX = kX & (Ci - 1);
+  const int kyX = a.kw == 1 ? tapX : tapX / a.kw, kxX = tapX - kyX * a.kw;
+  const bool kok = kX < K;
+  float rd[DE], rd2[DE];
+  float4 rx;
+  bool okx, okd;
+  auto load = [&](int s0) {
+    const int p = s0 + pD;
+    okd = p < p1 && oD < a.Co;
+    const long o = (long)p * a.Co + oD;
+#pragma unroll
+    for (int j = 0; j < DE; ++j) {
+      rd[j] = okd ? a.dy[o + j] : 0.f;
+      if constexpr (MODE_DY == 2) rd2[j] = okd ? a.dy2[o + j] : 0.f;
+    }
+    const int px = s0 + pX;
+    const int pp = px < p1 ? px : p0;
+    const int img = pp / HWo, rem = pp - img * HWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
+    const int iy = oy * a.stride - a.pad + kyX, ix = ox * a.stride - a.pad + kxX;
+    okx = px < p1 && kok && iy >= 0 && ix >= 0 && iy < a.Hi && ix < a.Wi;
+    const long xo = (((long)img * a.Hi + iy) * a.Wi + ix) * Ci + ciX;
+    rx = okx ? *reinterpret_cast<const float4*>(a.x + xo) : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto store = [&](float* A, float* B) {
+#pragma unroll
+    for (int j = 0; j < DE; ++j) {
+      float v = rd[j];
+      if constexpr (MODE_DY == 2) {
+        const int c = oD + j;
+        v = okd ? cd[c] * rd[j] + cd[a.Co + c] * rd2[j] + cd[2 * a.Co + c] : 0.f;
+      }
+      A[pD * PA + (tid & 15) * DE + j] = v;
+    }
+    float v[4] = {rx.x, rx.y, rx.z, rx.w};
+    if constexpr (MODE_X == 1) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = okx ? fmaxf(v[j] * cx[ciX + j] + cx[Ci + ciX + j], 0.f) : 0.f;
+    }
+    *reinterpret_cast<float4*>(B + pX * PB + 4 * (tid & 15)) = make_float4(v[0], v[1], v[2], v[3]);
+  };
+  f32x4_t acc[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acc[m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  __syncthreads();  // coefficients
+  const int ns = (p1 - p0 + BP - 1) / BP;
+  load(p0);
+  store(sA[0], sB[0]);
+  __syncthreads();
+  for (int s = 0; s < ns; ++s) {
+    const int cur = s & 1;
+    const bool more = s + 1 < ns;
+    if (more) load(p0 + BP * (s + 1));
+    const float* A = sA[cur];
+    const float* B = sB[cur];
+#pragma unroll
+    for (int q = 0; q < BP / 4; ++q) {
+      const int pr = 4 * q + (lane >> 4);
+      const float bv = B[pr * PB + 16 * wave + (lane & 15)];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[m] = mfma4(A[pr * PA + 16 * m + (lane & 15)], bv, acc[m]);
+    }
+    if (more) store(sA[cur ^ 1], sB[cur ^ 1]);
+    __syncthreads();
+  }
+  const int kcol = n0 + 16 * wave + (lane & 15);
+  const int tapc = kcol >> a.log2ci, cic = kcol & (Ci - 1);
+  if (kcol < K && cic < a.wci) {  // the stem's padded 4th channel has no weight
+    float* g = a.grads + (long)slot * a.g_mstride + a.g_off;
+    const long Kw = (long)a.kh * a.kw * a.wci;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int o = o0 + 16 * m + 4 * (lane >> 4) + i;
+        if (o < a.Co) atomicAdd(g + (long)o * Kw + (long)tapc * a.wci + cic, acc[m][i]);
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ elementwise
+struct F32Ew {
+  const float* dz;
+  const float* h;
+  const float* add;    // bwd apply: added; add_relu: the shortcut
+  float* out;
+  const float* coef;   // [cap][4][cmax]
+  const float* coef2;  // add_relu: shortcut BN (null: identity shortcut)
+  const int* img_slot;
+  long hw;
+  int C, cmax;
+  long nimg;
+};
+
+// which: 0 out = A dz + B h + C (+ add); 1 out = relu(h s + t); 2 out = relu(BN(h) + BN2(add) | add)
+template <int WHICH>
+__global__ __launch_bounds__(256) void f32_ew_kernel(F32Ew a) {
+  const long n4 = a.nimg * a.hw * a.C / 4;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const long e = 4 * i;
+    const long img = e / (a.hw * a.C);
+    const int c0 = (int)(e % a.C);
+    const int slot = a.img_slot[img];
+    const float* co = a.coef + (long)slot * 4 * a.cmax + c0;
+    const float4 hv = *reinterpret_cast<const float4*>(a.h + e);
+    const float h[4] = {hv.x, hv.y, hv.z, hv.w};
+    float r[4];
+    if constexpr (WHICH == 0) {
+      const float4 dv = *reinterpret_cast<const float4*>(a.dz + e);
+      const float d[4] = {dv.x, dv.y, dv.z, dv.w};
+      float4 av = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (a.add) av = *reinterpret_cast<const float4*>(a.add + e);
+      const float ad[4] = {av.x, av.y, av.z, av.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = co[j] * d[j] + co[a.cmax + j] * h[j] + co[2 * a.cmax + j] + ad[j];
+    } else if constexpr (WHICH == 1) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = fmaxf(h[j] * co[j] + co[a.cmax + j], 0.f);
+    } else {
+      const float4 sv = *reinterpret_cast<const float4*>(a.add + e);
+      const float s[4] = {sv.x, sv.y, sv.z, sv.w};
+      const float* c2 = a.coef2 ? a.coef2 + (long)slot * 4 * a.cmax + c0 : nullptr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        r[j] = fmaxf(h[j] * co[j] + co[a.cmax + j] + (c2 ? s[j] * c2[j] + c2[a.cmax + j] : s[j]), 0.f);
+    }
+    *reinterpret_cast<float4*>(a.out + e) = make_float4(r[0], r[1], r[2], r[3]);
+  }
+}
+
+// v1 BN-backward sums of a post-activation BN (dz already ReLU-masked): sum dz, sum dz * xhat of h [and of h2 for
+// a second BN fed the same dz].  One workgroup per image, thread = channel (C <= 256), LDS-free.
+struct F32Sum {
+  const float* dz;
+  const float* h;
+  const float* h2;
+  const float* fc;
+  const float* fc2;
+  float* sums;
+  float* sums2;
+  const int* img_slot;
+  int hw, C, cmax, pad;
+};
+
+__global__ __launch_bounds__(256) void f32_bwd_sums_kernel(F32Sum a) {
+  const int img = blockIdx.x, slot = a.img_slot[img];
+  const int c = threadIdx.x;
+  if (c >= a.C) return;
+  const float* f1 = a.fc + (long)slot * 4 * a.cmax;
+  const float mu = f1[2 * a.cmax + c], iv = f1[3 * a.cmax + c];
+  float mu2 = 0.f, iv2 = 0.f;
+  if (a.h2) {
+    const float* f2 = a.fc2 + (long)slot * 4 * a.cmax;
+    mu2 = f2[2 * a.cmax + c];
+    iv2 = f2[3 * a.cmax + c];
+  }
+  float s = 0.f, q = 0.f, q2 = 0.f;
+  const long base = (long)img * a.hw * a.C + c;
+  for (int p = 0; p < a.hw; ++p) {
+    const float d = a.dz[base + (long)p * a.C];
+    s += d;
+    q += d * (a.h[base + (long)p * a.C] - mu) * iv;
+    if (a.h2) q2 += d * (a.h2[base + (long)p * a.C] - mu2) * iv2;
+  }
+  float* su = a.sums + (long)slot * 2 * a.cmax;
+  atomicAdd(su + c, s);
+  atomicAdd(su + a.cmax + c, q);
+  if (a.h2) {
+    float* s2 = a.sums2 + (long)slot * 2 * a.cmax;
+    atomicAdd(s2 + c, s);
+    atomicAdd(s2 + a.cmax + c, q2);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------- head
+struct F32Head {
+  const float* x;       // [N][hw][C] last block output
+  const float* coef;    // final BN forward coefficients (v2) or null (v1: x is already a ReLU output)
+  const int* img_slot;
+  const int* labels;
+  const float* state;   // master rows: dense W [ncls][C] at w_off, bias at b_off
+  long s_mstride;
+  int w_off, b_off;
+  float* feat;          // [N][C]
+  float* dlog;          // [N][ncls]
+  float* dfeat;         // [N][C]
+  const float* cnt;     // images per member
+  float* loss;
+  float* correct;
+  float* sums;          // final-BN backward sums [cap][2][cmax]
+  const float* bcoef;   // final-BN backward coefficients
+  float* gout;          // gradient at x
+  int hw, C, ncls, cmax;
+  int train, pad;
+};
+
+// one workgroup per image: feat = mean_p T(x); logits = W feat + b; softmax CE -> loss / correct (/ member batch),
+// dlogits, dfeat = W^T dlogits (train)
+__global__ __launch_bounds__(256) void f32_head_kernel(F32Head a) {
+  __shared__ float f[256];
+  __shared__ float lg[64];
+  const int img = blockIdx.x, slot = a.img_slot[img];
+  const int t = threadIdx.x;
+  if (t < a.C) {
+    const float* co = a.coef ? a.coef + (long)slot * 4 * a.cmax : nullptr;
+    float s = 0.f;
+    for (int p = 0; p < a.hw; ++p) {
+      float v = a.x[((long)img * a.hw + p) * a.C + t];
+      if (co) v = fmaxf(v * co[t] + co[a.cmax + t], 0.f);
+      s += v;
+    }
+    f[t] = s / (float)a.hw;
+    a.feat[(long)img * a.C + t] = f[t];
+  }
+  __syncthreads();
+  const float* row = a.state + (long)slot * a.s_mstride;
+  if (t < a.ncls) {
+    float z = row[a.b_off + t];
+    for (int c = 0; c < a.C; ++c) z += row[a.w_off + t * a.C + c] * f[c];
+    lg[t] = z;
+  }
+  __syncthreads();
+  if (t == 0) {
+    float mx = lg[0];
+    int arg = 0;
+    for (int j = 1; j < a.ncls; ++j)
+      if (lg[j] > mx) mx = lg[j], arg = j;
+    float se = 0.f;
+    for (int j = 0; j < a.ncls; ++j) se += expf(lg[j] - mx);
+    const float lse = mx + logf(se);
+    const int lab = a.labels[img];
+    const float bsz = a.cnt[slot];
+    atomicAdd(a.loss + slot, (lse - lg[lab]) / bsz);
+    atomicAdd(a.correct + slot, arg == lab ? 1.f : 0.f);
+    for (int j = 0; j < a.ncls; ++j) lg[j] = (expf(lg[j] - lse) - (j == lab ? 1.f : 0.f)) / bsz;
+  }
+  __syncthreads();
+  if (!a.train) return;
+  if (t < a.ncls) a.dlog[(long)img * a.ncls + t] = lg[t];
+  if (t < a.C) {
+    float d = 0.f;
+    for (int j = 0; j < a.ncls; ++j) d += row[a.w_off + j * a.C + t] * lg[j];
+    a.dfeat[(long)img * a.C + t] = d;
+  }
+}
+
+// dense gradient, fixed summation order: workgroup = (member, 256 elements of [ncls][C] + ncls bias)
+__global__ __launch_bounds__(256) void f32_dense_grad_kernel(F32Head a, const int* slots, const int* first,
+                                                             float* grads, long g_mstride) {
+  const int m = blockIdx.y, slot = slots[m], i0 = first[m];
+  const int n = (int)a.cnt[slot];
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int nw = a.ncls * a.C;
+  if (e >= nw + a.ncls) return;
+  float s = 0.f;
+  if (e < nw) {
+    const int j = e / a.C, c = e - j * a.C;
+    for (int i = i0; i < i0 + n; ++i) s += a.dlog[(long)i * a.ncls + j] * a.feat[(long)i * a.C + c];
+    grads[(long)slot * g_mstride + a.w_off + e] += s;
+  } else {
+    const int j = e - nw;
+    for (int i = i0; i < i0 + n; ++i) s += a.dlog[(long)i * a.ncls + j];
+    grads[(long)slot * g_mstride + a.b_off + j] += s;
+  }
+}
+
+// GAP backward: which 0 -> final-BN backward sums (dz = dfeat / hw masked by BN(x) + ReLU > 0); which 1 -> gradient
+// at x: A dz + B x + C (v2) or dfeat / hw masked by x > 0 (v1: coef null)
+template <int WHICH>
+__global__ __launch_bounds__(256) void f32_gap_bwd_kernel(F32Head a) {
+  const int img = blockIdx.x, slot = a.img_slot[img];
+  const float* co = a.coef ? a.coef + (long)slot * 4 * a.cmax : nullptr;
+  const float inv_hw = 1.f / (float)a.hw;
+  if constexpr (WHICH == 0) {
+    const int c = threadIdx.x;
+    if (c >= a.C) return;
+    const float g = a.dfeat[(long)img * a.C + c] * inv_hw;
+    const float sc = co[c], sh = co[a.cmax + c], mu = co[2 * a.cmax + c], iv = co[3 * a.cmax + c];
+    float s = 0.f, q = 0.f;
+    for (int p = 0; p < a.hw; ++p) {
+      const float xv = a.x[((long)img * a.hw + p) * a.C + c];
+      if (xv * sc + sh > 0.f) {
+        s += g;
+        q += g * (xv - mu) * iv;
+      }
+    }
+    float* su = a.sums + (long)slot * 2 * a.cmax;
+    atomicAdd(su + c, s);
+    atomicAdd(su + a.cmax + c, q);
+  } else {
+    const float* bc = a.bcoef ? a.bcoef + (long)slot * 4 * a.cmax : nullptr;
+    const long n = (long)a.hw * a.C;
+    for (long i = threadIdx.x; i < n; i += blockDim.x) {
+      const int c = (int)(i % a.C);
+      const long o = (long)img * n + i;
+      const float xv = a.x[o];
+      const float g = a.dfeat[(long)img * a.C + c] * inv_hw;
+      float r;
+      if (co) {
+        const float dz = (xv * co[c] + co[a.cmax + c] > 0.f) ? g : 0.f;
+        r = bc[c] * dz + bc[a.cmax + c] * xv + bc[2 * a.cmax + c];
+      } else {
+        r = xv > 0.f ? g : 0.f;
+      }
+      a.gout[o] = r;
+    }
+  }
+}
+
+// [N][hw][3] fp32 -> [N][hw][4] (channel 3 zero: the stem gathers 4-channel chunks)
+__global__ __launch_bounds__(256) void f32_prep_input_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                             long npix) {
+  for (long p = (long)blockIdx.x * 256 + threadIdx.x; p < npix; p += (long)gridDim.x * 256)
+    *reinterpret_cast<float4*>(y + 4 * p) = make_float4(x[3 * p], x[3 * p + 1], x[3 * p + 2], 0.f);
+}
+
+}  // namespace
+
+DTF_API int dtf_f32_args_size() { return (int)sizeof(F32Args); }
+DTF_API int dtf_f32_ew_size() { return (int)sizeof(F32Ew); }
+DTF_API int dtf_f32_sum_size() { return (int)sizeof(F32Sum); }
+DTF_API int dtf_f32_head_size() { return (int)sizeof(F32Head); }
+
+// conv / data gradient: tc (16 | 32 | 64), mode (0 | 1 | 2), epi (bits: 1 residual, 2 mask, 4 statistics)
+DTF_API int dtf_f32_conv(const F32Args* a, int tc, int mode, int epi, int dgrad, int nwork, hipStream_t stream) {
+  if (nwork <= 0) return 0;
+  if ((a->Ci & (a->Ci - 1)) != 0 || a->Ci < 4 || (a->Co & 3) != 0 || (1 << a->log2ci) != a->Ci) return -2;
+  DTF_HOST_CHECK(DTF_ALIGNED16(a->x) && DTF_ALIGNED16(a->y));
+  const size_t dyn = (size_t)(mode == 0 ? 1 : (mode == 1 ? 2 : 3)) * a->Ci * sizeof(float);
+#define F_CASE(TC_, M_, E_, D_)                                                                          \
+  if (tc == TC_ && mode == M_ && epi == E_ && dgrad == D_) {                                             \
+    hipLaunchKernelGGL((f32conv_kernel<TC_, M_, E_, D_>), dim3(nwork), dim3(256), dyn, stream, *a);      \
+    return DTF_CHECK_LAUNCH();                                                                           \
+  }
+#define F_TCS(M_, E_, D_) F_CASE(16, M_, E_, D_) F_CASE(32, M_, E_, D_) F_CASE(64, M_, E_, D_)
+  // forward: stem / v1 (identity), v2 BN+ReLU prologue; statistics; + residual
+  F_TCS(0, 4, false) F_TCS(0, 0, false) F_TCS(1, 4, false) F_TCS(1, 0, false) F_TCS(1, 5, false)
+  // data gradient: mask + statistics [+ residual], plain, residual + mask (v1)
+  F_TCS(0, 6, true) F_TCS(0, 7, true) F_TCS(0, 0, true) F_TCS(2, 3, true) F_TCS(2, 6, true) F_TCS(2, 7, true)
+  F_TCS(2, 0, true)
+#undef F_TCS
+#undef F_CASE
+  return -1;
+}
+
+DTF_API int dtf_f32_wgrad(const F32Args* a, int tc, int mode_x, int mode_dy, int nwork, hipStream_t stream) {
+  if (nwork <= 0) return 0;
+  if ((a->Ci & (a->Ci - 1)) != 0 || a->Ci < 4 || (a->Co % tc) != 0 || (1 << a->log2ci) != a->Ci) return -2;
+  const size_t dyn = (size_t)(2 * a->Ci + 3 * a->Co) * sizeof(float);
+#define W_CASE(TC_, MX, MD)                                                                              \
+  if (tc == TC_ && mode_x == MX && mode_dy == MD) {                                                      \
+    hipLaunchKernelGGL((f32wgrad_kernel<TC_, MX, MD>), dim3(nwork), dim3(256), dyn, stream, *a);         \
+    return DTF_CHECK_LAUNCH();                                                                           \
+  }
+#define W_TCS(MX, MD) W_CASE(16, MX, MD) W_CASE(32, MX, MD) W_CASE(64, MX, MD)
+  W_TCS(0, 0) W_TCS(1, 0) W_TCS(0, 2) W_TCS(1, 2)
+#undef W_TCS
+#undef W_CASE
+  return -1;
+}
+
+DTF_API int dtf_f32_ew(const F32Ew* a, int which, hipStream_t stream) {
+  if (a->nimg <= 0) return 0;
+  if (a->C % 4) return -2;
+  const long n4 = a->nimg * a->hw * a->C / 4;
+  long blocks = (n4 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (which == 0)
+    hipLaunchKernelGGL(f32_ew_kernel<0>, dim3((unsigned)blocks), dim3(256), 0, stream, *a);
+  else if (which == 1)
+    hipLaunchKernelGGL(f32_ew_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, stream, *a);
+  else
+    hipLaunchKernelGGL(f32_ew_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, stream, *a);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_f32_bwd_sums(const F32Sum* a, int nimg, hipStream_t stream) {
+  if (nimg <= 0) return 0;
+  if (a->C > 256) return -2;
+  hipLaunchKernelGGL(f32_bwd_sums_kernel, dim3(nimg), dim3(256), 0, stream, *a);
+  return DTF_CHECK_LAUNCH();
+}
+
+// which 0: GAP + dense + CE (+ dlogits / dfeat when train); 1: dense gradient; 2: GAP-backward sums; 3: gradient at x
+DTF_API int dtf_f32_head(const F32Head* a, int which, int nimg, const int* slots, const int* first, int nslots,
+                         float* grads, long g_mstride, hipStream_t stream) {
+  if (nimg <= 0) return 0;
+  if (a->C > 256 || a->ncls > 64) return -2;
+  if (which == 0)
+    hipLaunchKernelGGL(f32_head_kernel, dim3(nimg), dim3(256), 0, stream, *a);
+  else if (which == 1)
+    hipLaunchKernelGGL(f32_dense_grad_kernel, dim3((a->ncls * a->C + a->ncls + 255) / 256, nslots), dim3(256), 0,
+                       stream, *a, slots, first, grads, g_mstride);
+  else if (which == 2)
+    hipLaunchKernelGGL(f32_gap_bwd_kernel<0>, dim3(nimg), dim3(256), 0, stream, *a);
+  else
+    hipLaunchKernelGGL(f32_gap_bwd_kernel<1>, dim3(nimg), dim3(256), 0, stream, *a);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_f32_prep_input(const float* x, float* y, long npix, hipStream_t stream) {
+  long blocks = (npix + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(f32_prep_input_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, y, npix);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_DEBUG_EXPORT(f32conv)

@@ -221,7 +221,7 @@ def hip_deterministic(args) -> bool:
     """Model families whose HIP step has a deterministic (bitwise-replayable) build: CIFAR ResNet v2 and v1 (64
     statistic replicas, capped workgroups; v1's BN-backward reductions as per-image rows added in image order) and
     MNIST (one workgroup per member for every accumulation)."""
-    return args.model in ("mnist", "cifar10")
+    return args.model in ("mnist", "cifar10") and getattr(args, "dtype", "bf16") == "bf16"  # the fp32 step: atomics
 
 
 def parse_main_args(argv=None, defaults=None) -> MainArgs:
@@ -231,11 +231,19 @@ def parse_main_args(argv=None, defaults=None) -> MainArgs:
         args.population_size = args.pop_size
     if args.resnet_version == 1 and args.dtype == "fp16":
         p.error("ResNet version 1 is not currently supported with fp16. Please use version 2 instead.")
-    if args.dtype != "bf16" and args.model != "toy":
-        # the hand-written MI355X kernels compute in bf16 (fp32 master weights / statistics); fp32 and fp16 (static
-        # loss scaling) run on the PyTorch backend
+    if args.dtype == "fp32" and args.model == "cifar10":
+        # fp32 CIFAR ResNets run the fp32 HIP step (engine/hip_f32.py: v_mfma_f32_16x16x4_f32, fp32 tensors); a
+        # static loss scale is a PyTorch-path feature
+        if args.loss_scale is not None and args.loss_scale != 1:
+            if args.backend == "hip":
+                p.error("--loss_scale with --dtype fp32: the fp32 HIP step does not scale the loss; use --backend torch")
+            args.backend = "torch"
+    elif args.dtype != "bf16" and args.model != "toy":
+        # the other families' kernels compute in bf16 (fp32 master weights / statistics); their fp32 and fp16
+        # (static loss scaling) run on the PyTorch backend
         if args.backend == "hip":
-            p.error("--dtype %s: the HIP kernels compute in bf16; use --backend torch (or auto)" % args.dtype)
+            p.error("--dtype %s: the %s HIP kernels compute in bf16; use --backend torch (or auto)"
+                    % (args.dtype, args.model))
         args.backend = "torch"
     elif args.loss_scale is not None and args.loss_scale != 1 and args.backend != "torch" and args.model != "toy":
         p.error("--loss_scale applies to the fp16 / fp32 PyTorch path; bf16 needs no loss scaling "

@@ -79,9 +79,14 @@ def test_ready_steps_and_batch_size(tmp_path, monkeypatch):
 def test_dtype_routing():
     from distributedtf_amd.utils.flags import parse_main_args
     a = parse_main_args(["--model", "cifar10", "--dtype", "fp32"])
-    assert a.backend == "torch" and a.model_kwargs()["dtype"] == "fp32"
+    assert a.backend == "auto" and a.model_kwargs()["dtype"] == "fp32"  # the fp32 HIP step on a GPU
+    assert parse_main_args(["--model", "cifar10", "--dtype", "fp32", "--backend", "hip"]).backend == "hip"
+    assert parse_main_args(["--model", "cifar10", "--dtype", "fp32", "--loss_scale", "8"]).backend == "torch"
     with pytest.raises(SystemExit):
-        parse_main_args(["--model", "cifar10", "--dtype", "fp32", "--backend", "hip"])
+        parse_main_args(["--model", "cifar10", "--dtype", "fp32", "--loss_scale", "8", "--backend", "hip"])
+    with pytest.raises(SystemExit):
+        parse_main_args(["--model", "imagenet", "--dtype", "fp32", "--backend", "hip"])
+    assert parse_main_args(["--model", "mnist", "--dtype", "fp32"]).backend == "torch"
     with pytest.raises(SystemExit):
         parse_main_args(["--model", "cifar10", "--loss_scale", "8"])  # bf16 HIP path: no loss scaling
     a = parse_main_args(["--model", "cifar10", "--dtype", "fp16"])

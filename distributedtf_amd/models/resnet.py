@@ -272,6 +272,12 @@ def _conv(prog, params, x, i, dtype):
     return F.conv2d(x, w, stride=c.stride, padding=(c.k - 1) // 2)
 
 
+def _acc(t):
+    """Accumulation precision of the oracle: fp32, or fp64 for a float64 run (the fp32 HIP step's tests compare
+    against an fp64 evaluation of the same step)."""
+    return t if t.dtype == torch.float64 else t.float()
+
+
 def _bn(prog, params, running, x, i, training, update_running=True):
     b = prog.bns[i]
     g = params[b.gamma_off:b.gamma_off + b.c]
@@ -279,7 +285,7 @@ def _bn(prog, params, running, x, i, training, update_running=True):
     rm = running[b.run_off:b.run_off + b.c]
     rv = running[b.run_off + b.c:b.run_off + 2 * b.c]
     if training:
-        xf = x.float()
+        xf = _acc(x)
         mean = xf.mean(dim=(0, 2, 3))
         var = xf.var(dim=(0, 2, 3), unbiased=False)
         if update_running:
@@ -290,7 +296,7 @@ def _bn(prog, params, running, x, i, training, update_running=True):
     else:
         mean, var = rm, rv
     inv = torch.rsqrt(var + BN_EPS)
-    y = (x.float() - mean[None, :, None, None]) * (inv * g)[None, :, None, None] + be[None, :, None, None]
+    y = (_acc(x) - mean[None, :, None, None]) * (inv * g)[None, :, None, None] + be[None, :, None, None]
     return y.to(x.dtype)
 
 
@@ -397,7 +403,7 @@ def forward_reference(prog: ResNetProgram, params: torch.Tensor, running: torch.
         x = block_forward(prog, params, running, x, blk, training, dtype, update_running)
     if cfg.version == 2:
         x = F.relu(bn(x, prog.final_bn))
-    feat = x.float().mean(dim=(2, 3))
+    feat = _acc(x).mean(dim=(2, 3))
     w = params[prog.dense_w_off:prog.dense_w_off + cfg.num_classes * cfg.final_size].view(cfg.num_classes, cfg.final_size)
     b = params[prog.dense_b_off:prog.dense_b_off + cfg.num_classes]
     return feat @ w.t() + b

@@ -446,10 +446,21 @@ struct F32Sum {
   int hw, C, cmax, pad;
 };
 
+__device__ __forceinline__ void kahan_add(float& s, float& c, float v) {
+  const float y = v - c;
+  const float t = s + y;
+  c = (t - s) - y;
+  s = t;
+}
+
+// One workgroup per image: thread (channel c, part) sums the pixels part, part + P, .. (P = 256 / C parts) with
+// compensated (Kahan) accumulation, then the parts combine in LDS: a long serial fp32 sum over the image's pixels
+// loses ~1e-3 of these cancellation-heavy BN-backward sums.
 __global__ __launch_bounds__(256) void f32_bwd_sums_kernel(F32Sum a) {
+  __shared__ float red[3][256];
   const int img = blockIdx.x, slot = a.img_slot[img];
-  const int c = threadIdx.x;
-  if (c >= a.C) return;
+  const int P = 256 / a.C;
+  const int c = threadIdx.x % a.C, part = threadIdx.x / a.C;
   const float* f1 = a.fc + (long)slot * 4 * a.cmax;
   const float mu = f1[2 * a.cmax + c], iv = f1[3 * a.cmax + c];
   float mu2 = 0.f, iv2 = 0.f;
@@ -458,21 +469,36 @@ __global__ __launch_bounds__(256) void f32_bwd_sums_kernel(F32Sum a) {
     mu2 = f2[2 * a.cmax + c];
     iv2 = f2[3 * a.cmax + c];
   }
-  float s = 0.f, q = 0.f, q2 = 0.f;
+  float s = 0.f, q = 0.f, q2 = 0.f, cs = 0.f, cq = 0.f, cq2 = 0.f;
   const long base = (long)img * a.hw * a.C + c;
-  for (int p = 0; p < a.hw; ++p) {
-    const float d = a.dz[base + (long)p * a.C];
-    s += d;
-    q += d * (a.h[base + (long)p * a.C] - mu) * iv;
-    if (a.h2) q2 += d * (a.h2[base + (long)p * a.C] - mu2) * iv2;
+  if (part < P) {
+    for (int p = part; p < a.hw; p += P) {
+      const float d = a.dz[base + (long)p * a.C];
+      kahan_add(s, cs, d);
+      kahan_add(q, cq, d * (a.h[base + (long)p * a.C] - mu) * iv);
+      if (a.h2) kahan_add(q2, cq2, d * (a.h2[base + (long)p * a.C] - mu2) * iv2);
+    }
   }
+  red[0][threadIdx.x] = s;
+  red[1][threadIdx.x] = q;
+  red[2][threadIdx.x] = q2;
+  __syncthreads();
+  for (int w = P / 2; w >= 1; w >>= 1) {  // pairwise over the parts (P is a power of two)
+    if (part < w) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + w * a.C];
+      red[1][threadIdx.x] += red[1][threadIdx.x + w * a.C];
+      red[2][threadIdx.x] += red[2][threadIdx.x + w * a.C];
+    }
+    __syncthreads();
+  }
+  if (part != 0) return;
   float* su = a.sums + (long)slot * 2 * a.cmax;
-  atomicAdd(su + c, s);
-  atomicAdd(su + a.cmax + c, q);
+  atomicAdd(su + c, red[0][c]);
+  atomicAdd(su + a.cmax + c, red[1][c]);
   if (a.h2) {
     float* s2 = a.sums2 + (long)slot * 2 * a.cmax;
-    atomicAdd(s2 + c, s);
-    atomicAdd(s2 + a.cmax + c, q2);
+    atomicAdd(s2 + c, red[0][c]);
+    atomicAdd(s2 + a.cmax + c, red[2][c]);
   }
 }
 
@@ -680,7 +706,7 @@ DTF_API int dtf_f32_ew(const F32Ew* a, int which, hipStream_t stream) {
 
 DTF_API int dtf_f32_bwd_sums(const F32Sum* a, int nimg, hipStream_t stream) {
   if (nimg <= 0) return 0;
-  if (a->C > 256) return -2;
+  if (a->C > 256 || 256 % a->C) return -2;
   hipLaunchKernelGGL(f32_bwd_sums_kernel, dim3(nimg), dim3(256), 0, stream, *a);
   return DTF_CHECK_LAUNCH();
 }

@@ -23,7 +23,10 @@ struct Big {  // the size of the conv kernels' ConvArgs (~0.4 KB)
   uint4* out;
   float* st;
   const float* st_in;
-  long pad[44];
+  unsigned* ticket;     // last-arriver finalize: arrival counter of this launch's statistics
+  float* coef_out;      // ... the finalized coefficients it writes
+  const float* coef_in; // ... the coefficients the previous launch finalized
+  long pad[41];
   int per_thread;
   int mode;
 };
@@ -68,7 +71,9 @@ __global__ __launch_bounds__(256) void k_chain(Big a) {
 
 template <int PT>
 __device__ void body(const Big& a, float* coef, float* acc, int t) {
-  if (a.mode & 1) {
+  if (a.mode & 32) {  // coefficients finalized by the previous launch's last arriver: one load per channel
+    if (t < 128) coef[t] = __hip_atomic_load(a.coef_in + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1.f;
+  } else if (a.mode & 1) {
     if (t < 128) {
       float s = 0.f;
 #pragma unroll
@@ -97,6 +102,97 @@ __device__ void body(const Big& a, float* coef, float* acc, int t) {
     __syncthreads();
     if (t < 128) atomicAdd(&a.st[(blockIdx.x & 7) * 128 + t], acc[t]);
   }
+  if (a.mode & 16) {  // producer-side finalize: the last-arriving workgroup sums the replicas into coefficients
+    __shared__ int last;
+    __syncthreads();  // every wave's statistic atomics are issued
+    if (t == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      const unsigned tk = atomicAdd(a.ticket, 1u);  // returning: the arrival order
+      last = tk == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (t < 128) {
+        float s = 0.f;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) s += __hip_atomic_load(a.st + r * 128 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.coef_out + t, s * 1e-12f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (t == 0) __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Persistent variant: NPH phases of the "1 MB + stats read + atomic flush" body in ONE launch of nwg workgroups (one
+// per CU), separated by a software grid barrier instead of a kernel boundary.  xcd = 0: one flat arrival counter;
+// xcd = 1: hierarchical (per-XCC counter, the XCC's last arriver then arrives at the top counter).  Spins are bounded
+// (a broken barrier ends the kernel instead of hanging the GPU; *fail counts such exits).
+__device__ unsigned long long g_ph[2][1024];  // phase 0 start / last phase end per workgroup
+__device__ __forceinline__ bool spin_until_changed(unsigned* gen, unsigned g) {
+  for (long it = 0; it < (1L << 16); ++it) {  // ~0.1 s: far above any real barrier wait
+    if (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != g) return true;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return false;
+}
+
+__device__ bool grid_barrier(unsigned* bar, int nwg, int xcd, unsigned* fail) {
+  // bar: [0] top counter, [1] generation, [2..9] per-XCC counters; XCC of this workgroup from the hardware register
+  __shared__ int ok;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ok = 1;
+    const unsigned g = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bool top = true;
+    if (xcd) {
+      const int xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & 7;  // HW_REG_XCC_ID bits 0..2
+      const unsigned per = nwg / 8;
+      const unsigned tk = atomicAdd(bar + 2 + xcc, 1u);
+      top = tk == per - 1;
+      if (top) __hip_atomic_store(bar + 2 + xcc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (top) {
+      const unsigned want = xcd ? 8u : (unsigned)nwg;
+      const unsigned tk = atomicAdd(bar, 1u);
+      if (tk == want - 1) {
+        __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(bar + 1, g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else if (!spin_until_changed(bar + 1, g)) {
+        ok = 0;
+      }
+    } else if (!spin_until_changed(bar + 1, g)) {
+      ok = 0;
+    }
+    if (!ok) atomicAdd(fail, 1u);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  return ok;
+}
+
+__global__ __launch_bounds__(256) void k_persist(Big a, int nph, int xcd, unsigned* bar, unsigned* fail,
+                                                 const uint4* b0, uint4* b1, float* s0, float* s1) {
+  __shared__ float coef[128];
+  __shared__ float acc[128];
+  const int t = threadIdx.x;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (int k = 0; k < nph; ++k) {
+    Big p = a;
+    p.in = (k & 1) ? reinterpret_cast<const uint4*>(b1) : b0;
+    p.out = (k & 1) ? const_cast<uint4*>(b0) : b1;
+    p.st = (k & 1) ? s0 : s1;
+    p.st_in = (k & 1) ? s1 : s0;
+    body<1>(p, coef, acc, t);
+    __builtin_amdgcn_s_waitcnt(0);
+    if (!grid_barrier(bar, gridDim.x, xcd, fail)) break;  // a broken barrier ends the kernel (bounded)
+  }
+  if (t == 0) {
+    g_ph[0][blockIdx.x & 1023] = t0;
+    g_ph[1][blockIdx.x & 1023] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
 int main() {
@@ -111,13 +207,28 @@ int main() {
   CHECK(hipMemset(b1, 0, 64 << 20));
   CHECK(hipMemset(st0, 0, 1 << 20));
   CHECK(hipMemset(st1, 0, 1 << 20));
+  unsigned *ticket, *bar, *fail;
+  float *coef0, *coef1;
+  CHECK(hipMalloc(&ticket, 4096));
+  CHECK(hipMalloc(&bar, 4096));
+  CHECK(hipMalloc(&fail, 4096));
+  CHECK(hipMalloc(&coef0, 4096));
+  CHECK(hipMalloc(&coef1, 4096));
+  CHECK(hipMemset(ticket, 0, 4096));
+  CHECK(hipMemset(bar, 0, 4096));
+  CHECK(hipMemset(fail, 0, 4096));
+  CHECK(hipMemset(coef0, 0, 4096));
+  CHECK(hipMemset(coef1, 0, 4096));
   hipStream_t s;
   CHECK(hipStreamCreate(&s));
   const char* names[] = {"empty (tiny kernarg)", "empty, 0.4 KB kernarg read", "1 MB read+write",
                          "1 MB + BN stats read", "1 MB + stats read + atomic flush", "4 MB + stats + atomics",
                          "1 WG/CU x 4: 1024 WG, 1 MB + stats + atomics", "1 MB loads only", "1 MB stores only",
-                         "1 MB read+write, eager launches (no graph)"};
-  for (int variant = 0; variant < 10; ++variant) {
+                         "1 MB read+write, eager launches (no graph)",
+                         "1 MB + atomics + last-arriver finalize (ticket)",
+                         "persistent: flat grid barrier per phase",
+                         "persistent: XCD-hierarchical barrier per phase"};
+  for (int variant = 0; variant < 13; ++variant) {
     const bool eager = variant == 9;
     auto enqueue = [&]() {
       for (int k = 0; k < NK; ++k) {
@@ -128,7 +239,17 @@ int main() {
         a.st_in = (k & 1) ? st1 : st0;
         a.per_thread = 1;
         a.pad[0] = k;
+        a.ticket = ticket + (k & 1) * 64;
+        a.coef_out = (k & 1) ? coef1 : coef0;
+        a.coef_in = (k & 1) ? coef0 : coef1;
         int nwg = NWG;
+        if (variant >= 11) {  // one persistent launch holds all NK phases
+          if (k == 0) {
+            a.mode = 3;
+            k_persist<<<NWG, 256, 0, s>>>(a, NK, variant == 12, bar, fail, b0, b1, st0, st1);
+          }
+          continue;
+        }
         switch (variant) {
           case 0: k_empty<<<NWG, 256, 0, s>>>(k); continue;
           case 1: k_bigarg<<<NWG, 256, 0, s>>>(a); continue;
@@ -140,6 +261,7 @@ int main() {
           case 7: a.mode = 4; break;
           case 8: a.mode = 8; break;
           case 9: a.mode = 0; break;
+          case 10: a.mode = 2 | 16 | 32; break;
         }
         if (a.per_thread == 4)
           k_chain<4><<<nwg, 256, 0, s>>>(a);
@@ -161,6 +283,16 @@ int main() {
       else
         CHECK(hipGraphLaunch(ge, s));
     };
+    if (variant >= 11) {  // one checked run first: a persistent kernel with a broken barrier must not be replayed
+      run();
+      CHECK(hipStreamSynchronize(s));
+      unsigned nf = 0;
+      CHECK(hipMemcpy(&nf, fail, 4, hipMemcpyDeviceToHost));
+      if (nf) {
+        printf("%-48s barrier timeouts on the first run (%u): stopping\n", names[variant], nf);
+        return 2;
+      }
+    }
     for (int w = 0; w < 300; ++w) run();  // >= 0.5 s: clocks ramped up
     CHECK(hipStreamSynchronize(s));
     hipEvent_t e0, e1;
@@ -173,6 +305,13 @@ int main() {
     float ms = 0.f;
     CHECK(hipEventElapsedTime(&ms, e0, e1));
     printf("%-48s %6.2f us/launch", names[variant], 1000.f * ms / (REPS * NK));
+    if (variant >= 11) {
+      unsigned nf = 0;
+      CHECK(hipMemcpy(&nf, fail, 4, hipMemcpyDeviceToHost));
+      printf("   (per phase; barrier timeouts: %u)\n", nf);
+      if (nf) return 2;  // a broken barrier: stop here
+      continue;
+    }
     if (variant >= 2) {  // one more run with stamps: kernel execution span vs launch gap, mean workgroup duration
       static unsigned long long st[128][1024][2];
       run();

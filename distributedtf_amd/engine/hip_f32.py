@@ -33,7 +33,7 @@ from .hip_resnet import advance_steps, note_step_advanced, run_captured, same_ba
 
 c_void_p, c_int, c_long = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
 CMAX = 64
-TP = 64           # output pixels per conv workgroup (f32conv.hip F_TP)
+TP = {16: 256, 32: 128, 64: 64}  # output pixels per conv workgroup by channel tile (f32conv.hip f_tp)
 WG_CHUNK = 2048   # pixels per weight-gradient work item
 
 
@@ -340,9 +340,10 @@ class _F32Plan:
         hwo = a.Ho * a.Wo
         for s, n in zip(self.slots, self.sizes):
             f = self.first[s]
-            for p0 in range(f * hwo, (f + n) * hwo, TP):
+            tp = TP[tc]
+            for p0 in range(f * hwo, (f + n) * hwo, tp):
                 for o0 in range(0, a.Co, tc):
-                    items.append([s, p0, min(p0 + TP, (f + n) * hwo), o0])
+                    items.append([s, p0, min(p0 + tp, (f + n) * hwo), o0])
         work = self._hold(torch.tensor(items, dtype=torch.int32, device=self.be.dev))
         a.work = _p(work)
         self._hold(a)

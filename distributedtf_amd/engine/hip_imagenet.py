@@ -123,6 +123,8 @@ def _register():
     reg("dtf_cg_chan_stats", [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p])
     reg("dtf_cg_bn_add_relu", [P(BnAddArgs), c_void_p])
     reg("dtf_cg_bn_bwd_sums", [P(BnSumArgs), c_int, c_void_p])
+    reg("dtf_cg_det_finish", [c_void_p, c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_void_p, c_void_p])
+    reg("dtf_fixed_acc", [])
     for n in ("dtf_cg_args_size", "dtf_bnfin_args_size", "dtf_ew_args_size", "dtf_gap_args_size",
               "dtf_bnadd_args_size", "dtf_bnsum_args_size"):
         reg(n, [])
@@ -180,10 +182,20 @@ class HipImageNetBackend:
         assert self.ncls <= NPAD_CLS and cfg.final_size % 32 == 0
         self.dense = torch.zeros(cap, NPAD_CLS * cfg.final_size, dtype=torch.bfloat16, device=self.dev)
         nb = len(prog.bns)
-        self.sums = torch.zeros(2, nb, cap, 2, CMAX, dtype=torch.float32, device=self.dev)   # [fwd|bwd]
+        # deterministic build (common.h DTF_FIXED_ACC): every cross-workgroup sum -- BN statistics, BN-backward sums,
+        # conv weight gradients, dense bias gradient, loss -- accumulates as int64 fixed point (order-free integer
+        # atomics); cg_det_finish folds the gradient / loss accumulators into the fp32 rows before the optimizer
+        self.det = bool(ops.lib().dtf_fixed_acc())
+        self.acc_dtype = torch.int64 if self.det else torch.float32
+        self.sums = torch.zeros(2, nb, cap, 2, CMAX, dtype=self.acc_dtype, device=self.dev)   # [fwd|bwd]
         self.coef = torch.zeros(2, nb, cap, 4, CMAX, dtype=torch.float32, device=self.dev)   # [fwd|bwd]
         self.loss = torch.zeros(cap, dtype=torch.float32, device=self.dev)
         self.correct = torch.zeros(cap, dtype=torch.float32, device=self.dev)
+        if self.det:
+            self.gacc = torch.zeros(cap, engine.Pp, dtype=torch.int64, device=self.dev)
+            self.loss64 = torch.zeros(cap, dtype=torch.int64, device=self.dev)
+        self.acc_grads = self.gacc if self.det else engine.grads  # where the convg / softmax kernels accumulate
+        self.acc_loss = self.loss64 if self.det else self.loss
         self.v1 = cfg.version == 1
         if self.v1:
             # identity "BN" coefficients (scale 1, shift 0): the convg epilogue's ReLU mask by BN(xm) > 0 then masks by
@@ -356,8 +368,9 @@ class _ImageNetPlan:
         if self.eval:
             nb = len(prog.bns)
             self.ev_coef = torch.zeros(nb, e.capacity, 4, CMAX, dtype=torch.float32, device=dev)
-            self.ev_sink = torch.zeros(e.capacity, 2, CMAX, dtype=torch.float32, device=dev)  # conv-epilogue stats
+            self.ev_sink = torch.zeros(e.capacity, 2, CMAX, dtype=be.acc_dtype, device=dev)  # conv-epilogue stats
             self.ev_acc = torch.zeros(2, e.capacity, dtype=torch.float32, device=dev)  # [correct, summed CE]
+            self.ev_loss = torch.zeros(e.capacity, dtype=be.acc_dtype, device=dev)  # summed CE (accumulator words)
             self._build_eval_v1() if self.v1 else self._build_eval()
         else:
             self._build_v1() if self.v1 else self._build()
@@ -429,7 +442,7 @@ class _ImageNetPlan:
         be, e = self.be, self.e
         a = CgArgs()
         a.w_mstride = e.Pp
-        a.grads, a.g_mstride = _p(e.grads), e.Pp
+        a.grads, a.g_mstride = _p(be.acc_grads), e.Pp
         a.cmax = CMAX
         return a
 
@@ -561,6 +574,12 @@ class _ImageNetPlan:
         self._hold(a)
         self._add(fn, ctypes.byref(a))
 
+    def det_finish(self):
+        be, e = self.be, self.e
+        if be.det:
+            self._add(ops.lib().dtf_cg_det_finish, _p(be.gacc), _p(e.grads), e.Pp, e.Pp, _p(self.slots_t),
+                      len(self.slots), _p(be.loss64), _p(be.loss))
+
     # ------------------------------------------------------------------------------------------ program
     def _build(self):
         be, e, prog, cfg = self.be, self.e, self.be.prog, self.be.cfg
@@ -627,7 +646,8 @@ class _ImageNetPlan:
         self.g_wgr = GroupedGemm(self.dlog, self.feat, e.grads, NPAD_CLS, C, C, wgr, True, True, GEMM_OUT_ACC, dev)
         self._add("gemm", self.g_fwd)
         self._add(L.dtf_cg_softmax_ce, _p(self.logits), NPAD_CLS, be.ncls, _p(self.labels), _p(self.img_slot),
-                  _p(e.state), e.S, prog.dense_b_off, _p(e.grads), e.Pp, _p(self.cnt), _p(be.loss), _p(be.correct),
+                  _p(e.state), e.S, prog.dense_b_off, _p(be.acc_grads), e.Pp, _p(self.cnt), _p(be.acc_loss),
+                  _p(be.correct),
                   _p(self.dlog), N)
         self._add("gemm", self.g_dgr)
         self._add("gemm", self.g_wgr)
@@ -680,6 +700,7 @@ class _ImageNetPlan:
         dy0 = self.tmp("dy0", H1, cfg.num_filters)
         self._add(L.dtf_cg_maxpool, None, None, _p(self.am0), _p(gcur), _p(dy0), N, H1, H1, H2, H2, cfg.num_filters, 1)
         self.wgrad(prog.stem, self.xin8, dy0, H, mode_x=0, mode_dy=0)
+        self.det_finish()
         self._add("optim", None)
         self._add("step", None)
 
@@ -737,7 +758,7 @@ class _ImageNetPlan:
                                  be.dev)
         self._add("gemm", self.g_fwd)
         self._add(L.dtf_cg_softmax_ce, _p(self.logits), NPAD_CLS, be.ncls, _p(self.labels), _p(self.img_slot),
-                  _p(e.state), e.S, prog.dense_b_off, None, e.Pp, _p(self.cnt), _p(self.ev_acc[1]),
+                  _p(e.state), e.S, prog.dense_b_off, None, e.Pp, _p(self.cnt), _p(self.ev_loss),
                   _p(self.ev_acc[0]), None, N)
 
     # ------------------------------------------------------------------------------------ ResNet v1 program
@@ -840,7 +861,8 @@ class _ImageNetPlan:
         self.g_wgr = GroupedGemm(self.dlog, self.feat, e.grads, NPAD_CLS, C, C, wgr, True, True, GEMM_OUT_ACC, dev)
         self._add("gemm", self.g_fwd)
         self._add(L.dtf_cg_softmax_ce, _p(self.logits), NPAD_CLS, be.ncls, _p(self.labels), _p(self.img_slot),
-                  _p(e.state), e.S, prog.dense_b_off, _p(e.grads), e.Pp, _p(self.cnt), _p(be.loss), _p(be.correct),
+                  _p(e.state), e.S, prog.dense_b_off, _p(be.acc_grads), e.Pp, _p(self.cnt), _p(be.acc_loss),
+                  _p(be.correct),
                   _p(self.dlog), N)
         self._add("gemm", self.g_dgr)
         self._add("gemm", self.g_wgr)
@@ -905,6 +927,7 @@ class _ImageNetPlan:
         dy0 = self.tmp("dy0", H1, cfg.num_filters)
         self.ew(bwd, self.y0, dy0, self.cb(sbn), H1, cfg.num_filters, dz=dz0)
         self.wgrad(prog.stem, self.xin8, dy0, H, mode_x=0, mode_dy=0)
+        self.det_finish()
         self._add("optim", None)
         self._add("step", None)
 
@@ -935,7 +958,7 @@ class _ImageNetPlan:
                                  be.dev)
         self._add("gemm", self.g_fwd)
         self._add(L.dtf_cg_softmax_ce, _p(self.logits), NPAD_CLS, be.ncls, _p(self.labels), _p(self.img_slot),
-                  _p(e.state), e.S, prog.dense_b_off, None, e.Pp, _p(self.cnt), _p(self.ev_acc[1]),
+                  _p(e.state), e.S, prog.dense_b_off, None, e.Pp, _p(self.cnt), _p(self.ev_loss),
                   _p(self.ev_acc[0]), None, N)
 
     def load_eval(self, x, y):

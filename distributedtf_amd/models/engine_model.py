@@ -347,18 +347,24 @@ class EngineModel(ModelBase):
     def _train_cycle(cls, eng, ds, gen, by_slot, todo, hooks):
         """``todo[slot]`` population steps of every listed member (members drop out of the active set when their
         count is reached), then one readback of the members' last losses."""
+        from ..utils.profiling import PHASES
         done = 0
         loss_acc = {s: None for s in todo}
         ms = [by_slot[s] for s in todo]
+        t_enq = t_prep = 0.0  # host time enqueueing steps / preparing their inputs (metrics.jsonl phases_s)
         with timed_phase("train_steps"):
             while True:
+                t0 = time.perf_counter()
                 active = [s for s in sorted(todo) if todo[s] > done]
                 if not active:
                     break
                 batches = [by_slot[s]._batch(ds, gen) for s in active]
                 hps = [by_slot[s].hparams for s in active]
                 lrs = [by_slot[s].learning_rate(eng.host_step[s]) for s in active]
+                t1 = time.perf_counter()
                 losses = eng.train_step(active, batches, hps, lrs)
+                t_enq += time.perf_counter() - t1
+                t_prep += t1 - t0
                 n_img = 0
                 for i, s in enumerate(active):
                     b = datasets.batch_len(batches[i])
@@ -381,9 +387,14 @@ class EngineModel(ModelBase):
             present = [m for m in ms if loss_acc[m.slot] is not None]
             if present:
                 # every member's last loss in one readback (also where the host waits for the queued steps)
+                t2 = time.perf_counter()
                 vals = torch.stack([loss_acc[m.slot].float().reshape(()) for m in present]).cpu().tolist()
+                PHASES.total["train_drain"] += time.perf_counter() - t2
                 for m, v in zip(present, vals):
                     m.last_loss = float(v)
+        PHASES.total["host_step_enqueue"] += t_enq
+        PHASES.total["host_step_prep"] += t_prep
+        PHASES.total["train_step_count"] += done
 
     @staticmethod
     def _run_hooks(eng, hooks, active, losses, lrs, n_img):

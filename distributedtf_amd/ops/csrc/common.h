@@ -89,3 +89,51 @@ static __device__ int dtf_debug_err;
 #define DTF_NREP 8
 #endif
 #define DTF_ALIGNED16(p) ((((uintptr_t)(p)) & 15) == 0)
+
+// Order-independent accumulation for the large-channel (ImageNet) kernels of the deterministic build: a float
+// partial is rounded to a signed 64-bit multiple of 2^-SHIFT and added with an integer atomic.  Integer addition is
+// associative, so the total is the same whatever order the workgroups (and, in LDS, the waves) arrive in.  Buffers
+// accumulated this way hold int64 words with the float layout's element indexing; the consumers (bn_final,
+// cg_det_finish) convert back.  Scales: BN forward sums 2^24 (sum of y^2 over a member's 1.6M pixels stays below
+// 2^39 for |y| < 30); gradients, BN-backward sums and the loss 2^36 (|value| < 1.3e8, resolution 1.5e-11).
+#define DTF_FX_STAT 24
+#define DTF_FX_GRAD 36
+__device__ __forceinline__ long long dtf_fx(float v, int shift) { return __float2ll_rn(ldexpf(v, shift)); }
+__device__ __forceinline__ float dtf_unfx(long long v, int shift) { return (float)ldexp((double)v, -shift); }
+__device__ __forceinline__ void dtf_fx_add(long long* p, float v, int shift) {
+  atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)dtf_fx(v, shift));
+}
+__device__ __forceinline__ void dtf_fx_addi(long long* p, long long v) {
+  atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v);
+}
+#ifdef DTF_DETERMINISTIC
+#define DTF_FIXED_ACC 1
+typedef long long dtf_acc_t;  // accumulator word of the ImageNet statistics / gradient sums
+#else
+#define DTF_FIXED_ACC 0
+typedef float dtf_acc_t;
+#endif
+// acc += v (float partial) / acc += w (an accumulated word, LDS -> global)
+__device__ __forceinline__ void dtf_acc_add(dtf_acc_t* p, float v, int shift) {
+#if DTF_FIXED_ACC
+  dtf_fx_add(p, v, shift);
+#else
+  (void)shift;
+  atomicAdd(p, v);
+#endif
+}
+__device__ __forceinline__ void dtf_acc_addw(dtf_acc_t* p, dtf_acc_t w) {
+#if DTF_FIXED_ACC
+  dtf_fx_addi(p, w);
+#else
+  atomicAdd(p, w);
+#endif
+}
+__device__ __forceinline__ float dtf_acc_get(const dtf_acc_t* p, int shift) {
+#if DTF_FIXED_ACC
+  return dtf_unfx(*p, shift);
+#else
+  (void)shift;
+  return *p;
+#endif
+}

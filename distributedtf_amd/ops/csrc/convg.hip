@@ -65,12 +65,12 @@ struct CgArgs {
   bf16_t* y;          // output NHWC
   const bf16_t* res;  // residual added in the epilogue
   const bf16_t* xm;   // epilogue mask source
-  float* grads;       // wgrad output rows
+  dtf_acc_t* grads;   // wgrad output rows (deterministic build: int64 fixed-point accumulators, common.h)
   long g_mstride, g_off;
   const float* c_in;  // transform coefficients of the gathered operand [cap][4][cmax]
   const float* c_dy;  // wgrad: transform coefficients of dy
   const float* c_ep;  // epilogue mask BN: scale, shift, mean, inv [cap][4][cmax]
-  float* st_out;      // per-channel sums [cap][2][cmax] (atomics)
+  dtf_acc_t* st_out;  // per-channel sums [cap][2][cmax] (atomics)
   const int4* work;   // fwd: (slot, p0, p1, o0); wgrad: (slot, p0, p1, o0 | n0 << 16 (in 8-col units))
   int Hi, Wi, Ci;     // gathered tensor geometry
   int Ho, Wo, Co;     // output geometry (Co = GEMM rows)
@@ -86,7 +86,7 @@ struct CgArgs {
 // bf16 store and per-channel statistics.
 template <int TC, int EPI, bool TRANS, int TP, int WRN, int NHALF>
 __device__ __forceinline__ void convg_epilogue(const CgArgs& a, f32x4_t (&acc)[TC / WRN / 16][TP / (4 / WRN) / 16],
-                                               float* cst, float (&acc_lds)[2][TC], int slot, int o0, int p0, int p1,
+                                               float* cst, dtf_acc_t (&acc_lds)[2][TC], int slot, int o0, int p0, int p1,
                                                int HWo, int GW, int py, int px) {
   constexpr int PW = TP / (4 / WRN), NTP = PW / 16, MT = TC / WRN / 16;
   constexpr int CPF = TC + 4;
@@ -207,15 +207,17 @@ __device__ __forceinline__ void convg_epilogue(const CgArgs& a, f32x4_t (&acc)[T
         q_ += __shfl_xor(q_, o, 64);
       }
       if (lane < CH && cok) {
-        atomicAdd(&acc_lds[0][8 * ch + i], s_);
-        atomicAdd(&acc_lds[1][8 * ch + i], q_);
+        // forward statistics (y, y^2) or BN-backward sums (dz, dz*xhat): fixed-point scales of the deterministic build
+        constexpr int FX = (EPI & 2) ? DTF_FX_GRAD : DTF_FX_STAT;
+        dtf_acc_add(&acc_lds[0][8 * ch + i], s_, FX);
+        dtf_acc_add(&acc_lds[1][8 * ch + i], q_, FX);
       }
     }
     __syncthreads();
     if (tid < TC && o0 + tid < a.Co) {
-      float* st = a.st_out + (long)slot * 2 * a.cmax;
-      atomicAdd(st + o0 + tid, acc_lds[0][tid]);
-      atomicAdd(st + a.cmax + o0 + tid, acc_lds[1][tid]);
+      dtf_acc_t* st = a.st_out + (long)slot * 2 * a.cmax;
+      dtf_acc_addw(st + o0 + tid, acc_lds[0][tid]);
+      dtf_acc_addw(st + a.cmax + o0 + tid, acc_lds[1][tid]);
     }
   }
 }
@@ -253,7 +255,7 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   bf16_t (*sa)[SA] = reinterpret_cast<bf16_t (*)[SA]>(smem_);
   bf16_t (*sb)[TP * RP] = reinterpret_cast<bf16_t (*)[TP * RP]>(smem_ + 2 * SA);
   extern __shared__ float dyn[];  // transform coefficients: MODE 1: 2*Ci, MODE 2: 3*Ci
-  __shared__ float acc_lds[2][TC];
+  __shared__ dtf_acc_t acc_lds[2][TC];
   const int4 wk = a.work[blockIdx.x];
   DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z >= wk.y);
   const int slot = wk.x, p0 = wk.y, p1 = wk.z;
@@ -282,7 +284,7 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
       if constexpr (MODE == 2) dyn[2 * Ci + i] = cb[2 * a.cmax + i];
     }
   }
-  for (int i = tid; i < 2 * TC; i += 256) (&acc_lds[0][0])[i] = 0.f;
+  for (int i = tid; i < 2 * TC; i += 256) (&acc_lds[0][0])[i] = 0;
   // per-thread B rows (pixels): r = tid / CPR + RPT j, chunk c = tid % CPR
   const int cB = tid % CPR, rB = tid / CPR;
   int pix_img[NJ], pix_y[NJ], pix_x[NJ];
@@ -544,7 +546,7 @@ __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
   static_assert(NHALF > 0, "epilogue staging split");
   constexpr int SEPI = 2 * TP * (TC + 4) / NHALF;
   __shared__ __attribute__((aligned(16))) bf16_t smem_[SOPS > SEPI ? SOPS : SEPI];
-  __shared__ float acc_lds[2][TC];
+  __shared__ dtf_acc_t acc_lds[2][TC];
   bf16_t (*sa)[SA] = reinterpret_cast<bf16_t (*)[SA]>(smem_);
   bf16_t* sbt = smem_ + 2 * SA;
   const int4 wk = a.work[blockIdx.x];
@@ -554,7 +556,7 @@ __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
   const int wr = wave % WRN, wc = wave / WRN;
   const int Ci = a.Ci, H = a.Hi;
   const int img = p0 / (H * W), y0 = (p0 - img * H * W) / W;
-  for (int i = tid; i < 2 * TC; i += 256) (&acc_lds[0][0])[i] = 0.f;
+  for (int i = tid; i < 2 * TC; i += 256) (&acc_lds[0][0])[i] = 0;
   // B staging slots: chunk idx = tid + 256 j -> staged pixel (r, col), 8-channel piece c8
   const bf16_t* xb = a.x + (long)img * H * W * Ci;
   int bl[MAXB], bg[MAXB];
@@ -858,7 +860,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PK == 32 ? 
     __syncthreads();
   }
   // D: lane holds column n = lane & 15 ((tap, ci) index), rows (o) 4*(lane>>4) + r
-  float* gr = a.grads + (long)slot * a.g_mstride + a.g_off;
+  dtf_acc_t* gr = a.grads + (long)slot * a.g_mstride + a.g_off;
   const int cr = a.cin_real > 0 ? a.cin_real : Ci;
   const int Kr = a.kh * a.kw * cr;
 #pragma unroll
@@ -872,7 +874,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PK == 32 ? 
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int o = o0 + wr * 64 + 16 * m + 4 * (lane >> 4) + r;
-        if (o < Co) atomicAdd(gr + (long)o * Kr + colr, acc[m][n][r]);
+        if (o < Co) dtf_acc_add(gr + (long)o * Kr + colr, acc[m][n][r], DTF_FX_GRAD);
       }
     }
   }
@@ -1019,7 +1021,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ?
     if (more) store(sd[cur ^ 1], sx[cur ^ 1], dv, xv);
     __syncthreads();
   }
-  float* gr = a.grads + (long)slot * a.g_mstride + a.g_off;
+  dtf_acc_t* gr = a.grads + (long)slot * a.g_mstride + a.g_off;
   const int cr = a.cin_real > 0 ? a.cin_real : Ci;  // real input channels of a channel-padded operand (stem)
   const int Kr = a.kh * a.kw * cr;
 #pragma unroll
@@ -1033,7 +1035,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ?
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int o = o0 + wr * (WWO / 2) + 16 * m + 4 * (lane >> 4) + r;
-        if (o < Co) atomicAdd(gr + (long)o * Kr + col, acc[m][n][r]);
+        if (o < Co) dtf_acc_add(gr + (long)o * Kr + col, acc[m][n][r], DTF_FX_GRAD);
       }
     }
   }

@@ -74,7 +74,7 @@ __global__ __launch_bounds__(256) void cg_dense_prep_kernel(const float* __restr
 struct BnFinArgs {
   float* state;        // fp32 state rows (gamma/beta in params, running stats at run_base)
   long s_mstride;
-  const float* sums;   // [cap][2][cmax]
+  const dtf_acc_t* sums;  // [cap][2][cmax]
   float* coef;         // [cap][4][cmax] out
   const float* fcoef;  // bwd: forward coefficients of the same BN
   float* grads;        // bwd: dgamma / dbeta
@@ -89,10 +89,10 @@ __global__ __launch_bounds__(256) void cg_bn_fwd_final_kernel(BnFinArgs a) {
   const int slot = a.slots[blockIdx.y];
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= a.C) return;
-  const float* su = a.sums + (long)slot * 2 * a.cmax;
+  const dtf_acc_t* su = a.sums + (long)slot * 2 * a.cmax;
   const float n = a.cnt[slot] * (float)a.hw;
-  const float mean = su[c] / n;
-  const float var = fmaxf(su[a.cmax + c] / n - mean * mean, 0.f);
+  const float mean = dtf_acc_get(su + c, DTF_FX_STAT) / n;
+  const float var = fmaxf(dtf_acc_get(su + a.cmax + c, DTF_FX_STAT) / n - mean * mean, 0.f);
   const float inv = rsqrtf(var + BN_EPS);
   float* row = a.state + (long)slot * a.s_mstride;
   const float scale = row[a.gamma_off + c] * inv;
@@ -127,10 +127,10 @@ __global__ __launch_bounds__(256) void cg_bn_bwd_final_kernel(BnFinArgs a) {
   const int slot = a.slots[blockIdx.y];
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= a.C) return;
-  const float* su = a.sums + (long)slot * 2 * a.cmax;
+  const dtf_acc_t* su = a.sums + (long)slot * 2 * a.cmax;
   const float* fc = a.fcoef + (long)slot * 4 * a.cmax;
   const float n = a.cnt[slot] * (float)a.hw;
-  const float sdz = su[c], sdzx = su[a.cmax + c];
+  const float sdz = dtf_acc_get(su + c, DTF_FX_GRAD), sdzx = dtf_acc_get(su + a.cmax + c, DTF_FX_GRAD);
   const float mean = fc[2 * a.cmax + c], inv = fc[3 * a.cmax + c];
   const float* row = a.state + (long)slot * a.s_mstride;
   const float scale = row[a.gamma_off + c] * inv;
@@ -367,7 +367,7 @@ struct GapArgs {
   const int* img_slot;
   bf16_t* feat;         // [N][C] bf16
   const float* dfeat;   // bwd: [N][C] fp32 (dL/dfeat)
-  float* sums;          // bwd: final-BN backward sums [cap][2][cmax]
+  dtf_acc_t* sums;      // bwd: final-BN backward sums [cap][2][cmax]
   const float* bcoef;   // bwd apply: A, B, C
   bf16_t* out;          // bwd apply: gradient at x
   int hw, C, cmax;
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(256) void cg_gap_kernel(GapArgs a) {
 __global__ __launch_bounds__(256) void cg_gap_bwd_reduce_kernel(GapArgs a) {
   const int img = blockIdx.x, slot = a.img_slot[img];
   const float* co = a.coef + (long)slot * 4 * a.cmax;
-  float* su = a.sums + (long)slot * 2 * a.cmax;
+  dtf_acc_t* su = a.sums + (long)slot * 2 * a.cmax;
   const float inv_hw = 1.f / (float)a.hw;
   for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
     const float g = a.dfeat[(long)img * a.C + c] * inv_hw;
@@ -415,8 +415,8 @@ __global__ __launch_bounds__(256) void cg_gap_bwd_reduce_kernel(GapArgs a) {
         q += g * (xv - mu) * iv;
       }
     }
-    atomicAdd(su + c, s);
-    atomicAdd(su + a.cmax + c, q);
+    dtf_acc_add(su + c, s, DTF_FX_GRAD);
+    dtf_acc_add(su + a.cmax + c, q, DTF_FX_GRAD);
   }
 }
 
@@ -447,8 +447,8 @@ __global__ __launch_bounds__(256) void cg_softmax_ce_kernel(const float* __restr
                                                              const int* __restrict__ labels,
                                                              const int* __restrict__ img_slot,
                                                              const float* __restrict__ state, long s_mstride, int b_off,
-                                                             float* __restrict__ grads, long g_mstride,
-                                                             const float* __restrict__ cnt, float* __restrict__ loss,
+                                                             dtf_acc_t* __restrict__ grads, long g_mstride,
+                                                             const float* __restrict__ cnt, dtf_acc_t* __restrict__ loss,
                                                              float* __restrict__ correct, bf16_t* __restrict__ dl,
                                                              long nimg) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -480,28 +480,28 @@ __global__ __launch_bounds__(256) void cg_softmax_ce_kernel(const float* __restr
   const float lse = mx + __logf(se);
   const int lab = labels[img];
   const float bsz = cnt[slot];
-  float* gb = grads != nullptr ? grads + (long)slot * g_mstride + b_off : nullptr;
+  dtf_acc_t* gb = grads != nullptr ? grads + (long)slot * g_mstride + b_off : nullptr;
   for (int j = lane; j < ld; j += 64) {
     float d = 0.f;
     if (j < ncls) {
       d = (__expf(lr[j] + bias[j] - lse) - (j == lab ? 1.f : 0.f)) / bsz;
-      if (grads != nullptr) atomicAdd(gb + j, d);
+      if (grads != nullptr) dtf_acc_add(gb + j, d, DTF_FX_GRAD);
     }
     if (dl != nullptr) dl[img * ld + j] = f2bf(d);  // eval (no grads / dlogits): loss and correct count only
   }
   if (lane == 0) {
-    atomicAdd(loss + slot, (lse - (lr[lab] + bias[lab])) / bsz);
-    atomicAdd(correct + slot, arg == lab ? 1.f : 0.f);
+    dtf_acc_add(loss + slot, (lse - (lr[lab] + bias[lab])) / bsz, DTF_FX_GRAD);
+    atomicAdd(correct + slot, arg == lab ? 1.f : 0.f);  // integer-valued: exact in any order
   }
 }
 
 // per-channel sum / second moment of a [N][hw][C] tensor into [cap][2][cmax] (BN statistics of a tensor no conv
 // epilogue produced, e.g. the max-pool output); thread = 8 fixed channels, LDS reduction, one atomic per WG
 __global__ __launch_bounds__(256) void cg_chan_stats_kernel(const bf16_t* __restrict__ x, const int* __restrict__ img_slot,
-                                                             float* __restrict__ sums, int hw, int C, int cmax) {
-  __shared__ float acc[2][2048];
+                                                             dtf_acc_t* __restrict__ sums, int hw, int C, int cmax) {
+  __shared__ dtf_acc_t acc[2][2048];
   const int img = blockIdx.x, slot = img_slot[img];
-  for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) (&acc[0][0])[(i / C) * 2048 + i % C] = 0.f;
+  for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) (&acc[0][0])[(i / C) * 2048 + i % C] = 0;
   __syncthreads();
   const long n8 = (long)hw * C / 8;
   const long i0 = (long)blockIdx.y * blockDim.x + threadIdx.x, st = (long)gridDim.y * blockDim.x;
@@ -520,15 +520,15 @@ __global__ __launch_bounds__(256) void cg_chan_stats_kernel(const bf16_t* __rest
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      atomicAdd(&acc[0][c0 + k], s[k]);
-      atomicAdd(&acc[1][c0 + k], q[k]);
+      dtf_acc_add(&acc[0][c0 + k], s[k], DTF_FX_STAT);
+      dtf_acc_add(&acc[1][c0 + k], q[k], DTF_FX_STAT);
     }
   }
   __syncthreads();
-  float* su = sums + (long)slot * 2 * cmax;
+  dtf_acc_t* su = sums + (long)slot * 2 * cmax;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    atomicAdd(su + c, acc[0][c]);
-    atomicAdd(su + cmax + c, acc[1][c]);
+    dtf_acc_addw(su + c, acc[0][c]);
+    dtf_acc_addw(su + cmax + c, acc[1][c]);
   }
 }
 
@@ -608,17 +608,17 @@ struct BnSumArgs {
   const bf16_t* h2;     // null: one BN
   const float* fc;      // forward coefficients of h's BN (mean at 2*cmax, inv at 3*cmax)
   const float* fc2;
-  float* sums;
-  float* sums2;
+  dtf_acc_t* sums;
+  dtf_acc_t* sums2;
   const int* img_slot;
   int hw, C, cmax, pad;
 };
 
 __global__ __launch_bounds__(256) void cg_bn_bwd_sums_kernel(BnSumArgs a) {
-  __shared__ float acc[3][2048];
+  __shared__ dtf_acc_t acc[3][2048];
   const int img = blockIdx.x, slot = a.img_slot[img];
   const bool two = a.h2 != nullptr;
-  for (int i = threadIdx.x; i < 3 * a.C; i += blockDim.x) (&acc[0][0])[(i / a.C) * 2048 + i % a.C] = 0.f;
+  for (int i = threadIdx.x; i < 3 * a.C; i += blockDim.x) (&acc[0][0])[(i / a.C) * 2048 + i % a.C] = 0;
   __syncthreads();
   const long n8 = (long)a.hw * a.C / 8;
   const long i0 = (long)blockIdx.y * blockDim.x + threadIdx.x, st = (long)gridDim.y * blockDim.x;
@@ -658,25 +658,59 @@ __global__ __launch_bounds__(256) void cg_bn_bwd_sums_kernel(BnSumArgs a) {
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      atomicAdd(&acc[0][c0 + k], s[k]);
-      atomicAdd(&acc[1][c0 + k], q[k]);
-      if (two) atomicAdd(&acc[2][c0 + k], q2[k]);
+      dtf_acc_add(&acc[0][c0 + k], s[k], DTF_FX_GRAD);
+      dtf_acc_add(&acc[1][c0 + k], q[k], DTF_FX_GRAD);
+      if (two) dtf_acc_add(&acc[2][c0 + k], q2[k], DTF_FX_GRAD);
     }
   }
   __syncthreads();
-  float* su = a.sums + (long)slot * 2 * a.cmax;
-  float* su2 = two ? a.sums2 + (long)slot * 2 * a.cmax : nullptr;
+  dtf_acc_t* su = a.sums + (long)slot * 2 * a.cmax;
+  dtf_acc_t* su2 = two ? a.sums2 + (long)slot * 2 * a.cmax : nullptr;
   for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
-    atomicAdd(su + c, acc[0][c]);
-    atomicAdd(su + a.cmax + c, acc[1][c]);
+    dtf_acc_addw(su + c, acc[0][c]);
+    dtf_acc_addw(su + a.cmax + c, acc[1][c]);
     if (two) {
-      atomicAdd(su2 + c, acc[0][c]);
-      atomicAdd(su2 + a.cmax + c, acc[2][c]);
+      dtf_acc_addw(su2 + c, acc[0][c]);
+      dtf_acc_addw(su2 + a.cmax + c, acc[2][c]);
     }
   }
 }
 
+// Deterministic build: fold the fixed-point gradient accumulators of the step into the fp32 gradient rows (which
+// already hold the order-free contributions: the dense-layer GEMM and the BN gamma / beta sums) and the loss, and
+// clear the accumulators for the next step.  grid (chunks, members)
+__global__ __launch_bounds__(256) void cg_det_finish_kernel(long long* __restrict__ gacc, float* __restrict__ grads,
+                                                             long stride, long n, const int* __restrict__ slots,
+                                                             long long* __restrict__ loss64, float* __restrict__ loss) {
+  const int slot = slots[blockIdx.y];
+  long long* ga = gacc + (long)slot * stride;
+  float* g = grads + (long)slot * stride;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long long v = ga[i];
+    if (v != 0) {
+      g[i] += dtf_unfx(v, DTF_FX_GRAD);
+      ga[i] = 0;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    loss[slot] = dtf_unfx(loss64[slot], DTF_FX_GRAD);
+    loss64[slot] = 0;
+  }
+}
+
 }  // namespace
+
+DTF_API int dtf_cg_det_finish(long long* gacc, float* grads, long stride, long n, const int* slots, int nslots,
+                              long long* loss64, float* loss, hipStream_t stream) {
+  if (nslots <= 0) return 0;
+  long blocks = (n + 255) / 256;
+  if (blocks > 512) blocks = 512;
+  hipLaunchKernelGGL(cg_det_finish_kernel, dim3((unsigned)blocks, nslots), dim3(256), 0, stream, gacc, grads, stride, n,
+                     slots, loss64, loss);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_fixed_acc() { return DTF_FIXED_ACC; }
 
 DTF_API int dtf_bnadd_args_size() { return (int)sizeof(BnAddArgs); }
 DTF_API int dtf_bnsum_args_size() { return (int)sizeof(BnSumArgs); }
@@ -700,7 +734,7 @@ DTF_API int dtf_cg_bn_bwd_sums(const BnSumArgs* a, int nimg, hipStream_t stream)
   return DTF_CHECK_LAUNCH();
 }
 
-DTF_API int dtf_cg_chan_stats(const bf16_t* x, const int* img_slot, float* sums, int nimg, int hw, int C, int cmax,
+DTF_API int dtf_cg_chan_stats(const bf16_t* x, const int* img_slot, dtf_acc_t* sums, int nimg, int hw, int C, int cmax,
                               hipStream_t stream) {
   if (nimg <= 0) return 0;
   if (C > 2048 || C % 8 || 2048 % C) return -2;
@@ -797,8 +831,8 @@ DTF_API int dtf_cg_gap(const GapArgs* a, int which, int nimg, hipStream_t stream
 }
 
 DTF_API int dtf_cg_softmax_ce(const float* logits, int ld, int ncls, const int* labels, const int* img_slot,
-                              const float* state, long s_mstride, int b_off, float* grads, long g_mstride,
-                              const float* cnt, float* loss, float* correct, bf16_t* dl, long nimg,
+                              const float* state, long s_mstride, int b_off, dtf_acc_t* grads, long g_mstride,
+                              const float* cnt, dtf_acc_t* loss, float* correct, bf16_t* dl, long nimg,
                               hipStream_t stream) {
   if (nimg <= 0) return 0;
   hipLaunchKernelGGL(cg_softmax_ce_kernel, dim3((unsigned)((nimg + 3) / 4)), dim3(256), 0, stream, logits, ld, ncls,

@@ -50,23 +50,25 @@ struct F32Args {
   int pad_;
 };
 
-constexpr int F_TP = 64;  // output pixels per conv workgroup
 constexpr int F_BK = 16;  // k per LDS stage
-constexpr int f_pitch(int n) { return n == 64 ? 80 : (n == 32 ? 48 : 16); }  // LDS row pitch: 4 row groups of a
-// fragment read land 16 banks apart
+// LDS row pitch (floats): the 4 row groups (lane / 16) of a fragment read land 16 banks apart
+constexpr int f_pitch(int n) { return n == 16 ? 16 : (n == 32 ? 48 : n + 16); }
+// conv tile: TC output channels x TP = 16 * 4 * NT pixels, NT = 64 / TC pixel tiles per wave -- every wave runs
+// MT x NT = 4 MFMA tiles per k-step whatever the channel width (a C = 16 layer would otherwise get one)
+constexpr int f_tp(int tc) { return 64 * (64 / tc); }
 
 // ------------------------------------------------------------------------------------------------ fwd / dgrad
 template <int TC, int MODE, int EPI, bool DGRAD>
 __global__ __launch_bounds__(256) void f32conv_kernel(F32Args a) {
-  constexpr int MT = TC / 16;
-  constexpr int PA = f_pitch(TC), PB = f_pitch(F_TP);
+  constexpr int MT = TC / 16, NT = 64 / TC, TP = f_tp(TC);
+  constexpr int PA = f_pitch(TC), PB = f_pitch(TP);
   constexpr int AE = TC * F_BK / 256;  // A elements per thread per stage
   __shared__ __attribute__((aligned(16))) float sA[2][F_BK * PA];
   __shared__ __attribute__((aligned(16))) float sB[2][F_BK * PB];
   __shared__ float acc_lds[2][TC];
   extern __shared__ float dyn[];  // transform coefficients: MODE 1: 2 * Ci, MODE 2: 3 * Ci
   const int4 wk = a.work[blockIdx.x];
-  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z >= wk.y && wk.z - wk.y <= F_TP);
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z >= wk.y && wk.z - wk.y <= TP);
   const int slot = wk.x, p0 = wk.y, p1 = wk.z, o0 = wk.w;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int Ci = a.Ci, kk = a.kh * a.kw;
@@ -80,60 +82,75 @@ __global__ __launch_bounds__(256) void f32conv_kernel(F32Args a) {
     }
   }
   for (int i = tid; i < 2 * TC; i += 256) (&acc_lds[0][0])[i] = 0.f;
-  // this thread's B row (pixel) and k chunk (4 consecutive k of one tap: Ci % 4 == 0)
+  // this thread's B rows (pixels rB + 64 j) and k chunk (4 consecutive k of one tap: Ci % 4 == 0)
   const int rB = tid >> 2, cB = tid & 3;
-  const int pB = p0 + rB;
-  const bool okp = pB < p1;
   const int HWo = a.Ho * a.Wo;
-  const int pp = okp ? pB : p0;
-  const int img = pp / HWo, rem = pp - img * HWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
-  const int by = DGRAD ? oy + a.pad : oy * a.stride - a.pad;
-  const int bx = DGRAD ? ox + a.pad : ox * a.stride - a.pad;
-  const long ibase = (long)img * a.Hi * a.Wi * Ci;
+  int by[NT], bx[NT];
+  long ibase[NT];
+  bool okp[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int pB = p0 + rB + 64 * j;
+    okp[j] = pB < p1;
+    const int pp = okp[j] ? pB : p0;
+    const int img = pp / HWo, rem = pp - img * HWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
+    by[j] = DGRAD ? oy + a.pad : oy * a.stride - a.pad;
+    bx[j] = DGRAD ? ox + a.pad : ox * a.stride - a.pad;
+    ibase[j] = (long)img * a.Hi * a.Wi * Ci;
+  }
   const float* wrow = a.w + (long)slot * a.w_mstride + a.w_off;
-  float4 rb, rb2;
-  bool okb;
+  float4 rb[NT], rb2[NT];
+  unsigned okb;
   int cb_;
   auto load_b = [&](int k0) {
     const int k = k0 + 4 * cB;
     const int tap = k >> a.log2ci, ci = k & (Ci - 1);
     const int ky = a.kw == 1 ? tap : tap / a.kw, kx = tap - ky * a.kw;
-    int iy, ix;
-    bool ok;
-    if constexpr (DGRAD) {
-      const int ny = by - ky, nx = bx - kx;
-      iy = ny / a.stride;
-      ix = nx / a.stride;
-      ok = ny >= 0 && nx >= 0 && iy * a.stride == ny && ix * a.stride == nx && iy < a.Hi && ix < a.Wi;
-    } else {
-      iy = by + ky;
-      ix = bx + kx;
-      ok = iy >= 0 && ix >= 0 && iy < a.Hi && ix < a.Wi;
+    okb = 0;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      int iy, ix;
+      bool ok;
+      if constexpr (DGRAD) {
+        const int ny = by[j] - ky, nx = bx[j] - kx;
+        iy = ny / a.stride;
+        ix = nx / a.stride;
+        ok = ny >= 0 && nx >= 0 && iy * a.stride == ny && ix * a.stride == nx && iy < a.Hi && ix < a.Wi;
+      } else {
+        iy = by[j] + ky;
+        ix = bx[j] + kx;
+        ok = iy >= 0 && ix >= 0 && iy < a.Hi && ix < a.Wi;
+      }
+      ok = ok && okp[j] && k < K;
+      const long off = ibase[j] + ((long)iy * a.Wi + ix) * Ci + ci;
+      rb[j] = ok ? *reinterpret_cast<const float4*>(a.x + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (MODE == 2)
+        rb2[j] = ok ? *reinterpret_cast<const float4*>(a.x2 + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+      okb |= (unsigned)ok << j;
     }
-    ok = ok && okp && k < K;
-    const long off = ibase + ((long)iy * a.Wi + ix) * Ci + ci;
-    rb = ok ? *reinterpret_cast<const float4*>(a.x + off) : make_float4(0.f, 0.f, 0.f, 0.f);
-    if constexpr (MODE == 2) rb2 = ok ? *reinterpret_cast<const float4*>(a.x2 + off) : make_float4(0.f, 0.f, 0.f, 0.f);
-    okb = ok;
     cb_ = ci;
   };
   auto store_b = [&](float* dst) {
-    float v[4] = {rb.x, rb.y, rb.z, rb.w};
-    if constexpr (MODE != 0) {
-      const float h[4] = {rb2.x, rb2.y, rb2.z, rb2.w};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = cb_ + j;
-        float t;
-        if constexpr (MODE == 1)
-          t = fmaxf(v[j] * dyn[c] + dyn[Ci + c], 0.f);
-        else
-          t = dyn[c] * v[j] + dyn[Ci + c] * h[j] + dyn[2 * Ci + c];
-        v[j] = okb ? t : 0.f;  // zero padding stays zero after the transform
+    for (int j = 0; j < NT; ++j) {
+      float v[4] = {rb[j].x, rb[j].y, rb[j].z, rb[j].w};
+      if constexpr (MODE != 0) {
+        const float h[4] = {rb2[j].x, rb2[j].y, rb2[j].z, rb2[j].w};
+        const bool ok = (okb >> j) & 1u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = cb_ + q;
+          float t;
+          if constexpr (MODE == 1)
+            t = fmaxf(v[q] * dyn[c] + dyn[Ci + c], 0.f);
+          else
+            t = dyn[c] * v[q] + dyn[Ci + c] * h[q] + dyn[2 * Ci + c];
+          v[q] = ok ? t : 0.f;  // zero padding stays zero after the transform
+        }
       }
-    }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) dst[(4 * cB + j) * PB + rB] = v[j];
+      for (int q = 0; q < 4; ++q) dst[(4 * cB + q) * PB + rB + 64 * j] = v[q];
+    }
   };
   float ra[AE];
   auto load_a = [&](int k0) {
@@ -169,9 +186,11 @@ __global__ __launch_bounds__(256) void f32conv_kernel(F32Args a) {
       dst[kl * PA + m] = ra[j];
     }
   };
-  f32x4_t acc[MT];
+  f32x4_t acc[MT][NT];
 #pragma unroll
-  for (int m = 0; m < MT; ++m) acc[m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[m][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
   __syncthreads();  // coefficients
   const int nk = (K + F_BK - 1) / F_BK;
   load_a(0);
@@ -191,9 +210,15 @@ __global__ __launch_bounds__(256) void f32conv_kernel(F32Args a) {
 #pragma unroll
     for (int q = 0; q < F_BK / 4; ++q) {
       const int kr = 4 * q + (lane >> 4);
-      const float bv = B[kr * PB + 16 * wave + (lane & 15)];
+      float av[MT], bv[NT];
 #pragma unroll
-      for (int m = 0; m < MT; ++m) acc[m] = mfma4(A[kr * PA + 16 * m + (lane & 15)], bv, acc[m]);
+      for (int m = 0; m < MT; ++m) av[m] = A[kr * PA + 16 * m + (lane & 15)];
+#pragma unroll
+      for (int n = 0; n < NT; ++n) bv[n] = B[kr * PB + 16 * (wave * NT + n) + (lane & 15)];
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[m][n] = mfma4(av[m], bv[n], acc[m][n]);
     }
     if (more) {
       store_a(sA[cur ^ 1]);
@@ -201,46 +226,53 @@ __global__ __launch_bounds__(256) void f32conv_kernel(F32Args a) {
     }
     __syncthreads();
   }
-  // ---- epilogue: lane holds channels o0 + 16 m + 4 (lane / 16) + i of pixel p0 + 16 wave + lane % 16
-  const int p = p0 + 16 * wave + (lane & 15);
-  const bool pok = p < p1;
+  // ---- epilogue: lane holds channels o0 + 16 m + 4 (lane / 16) + i of pixel p0 + 16 (wave NT + n) + lane % 16
   float ss[MT][4], sq[MT][4];
 #pragma unroll
-  for (int m = 0; m < MT; ++m) {
-    const int co = o0 + 16 * m + 4 * (lane >> 4);
-    const bool ok = pok && co < a.Co;
-    const long o = (long)p * a.Co + co;
-    float v[4] = {acc[m][0], acc[m][1], acc[m][2], acc[m][3]};
-    float xv[4] = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (EPI & 1) {
-      if (ok) {
-        const float4 r = *reinterpret_cast<const float4*>(a.res + o);
-        v[0] += r.x, v[1] += r.y, v[2] += r.z, v[3] += r.w;
-      }
-    }
-    const float* ep = (EPI & 2) ? a.c_ep + (long)slot * 4 * a.cmax + (ok ? co : 0) : nullptr;
-    if constexpr (EPI & 2) {
-      if (ok) {
-        const float4 xr = *reinterpret_cast<const float4*>(a.xm + o);
-        xv[0] = xr.x, xv[1] = xr.y, xv[2] = xr.z, xv[3] = xr.w;
-      }
+  for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = (xv[i] * ep[i] + ep[a.cmax + i] > 0.f) ? v[i] : 0.f;
-    }
-    if (ok) *reinterpret_cast<float4*>(a.y + o) = make_float4(v[0], v[1], v[2], v[3]);
+    for (int i = 0; i < 4; ++i) ss[m][i] = sq[m][i] = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float vv = ok ? v[i] : 0.f;
-      ss[m][i] = vv;
-      if constexpr (EPI & 2)
-        sq[m][i] = ok ? vv * (xv[i] - ep[2 * a.cmax + i]) * ep[3 * a.cmax + i] : 0.f;
-      else
-        sq[m][i] = vv * vv;
+  for (int n = 0; n < NT; ++n) {
+    const int p = p0 + 16 * (wave * NT + n) + (lane & 15);
+    const bool pok = p < p1;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int co = o0 + 16 * m + 4 * (lane >> 4);
+      const bool ok = pok && co < a.Co;
+      const long o = (long)p * a.Co + co;
+      float v[4] = {acc[m][n][0], acc[m][n][1], acc[m][n][2], acc[m][n][3]};
+      float xv[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI & 1) {
+        if (ok) {
+          const float4 r = *reinterpret_cast<const float4*>(a.res + o);
+          v[0] += r.x, v[1] += r.y, v[2] += r.z, v[3] += r.w;
+        }
+      }
+      const float* ep = (EPI & 2) ? a.c_ep + (long)slot * 4 * a.cmax + (ok ? co : 0) : nullptr;
+      if constexpr (EPI & 2) {
+        if (ok) {
+          const float4 xr = *reinterpret_cast<const float4*>(a.xm + o);
+          xv[0] = xr.x, xv[1] = xr.y, xv[2] = xr.z, xv[3] = xr.w;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = (xv[i] * ep[i] + ep[a.cmax + i] > 0.f) ? v[i] : 0.f;
+      }
+      if (ok) *reinterpret_cast<float4*>(a.y + o) = make_float4(v[0], v[1], v[2], v[3]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float vv = ok ? v[i] : 0.f;
+        ss[m][i] += vv;
+        if constexpr (EPI & 2)
+          sq[m][i] += ok ? vv * (xv[i] - ep[2 * a.cmax + i]) * ep[3 * a.cmax + i] : 0.f;
+        else
+          sq[m][i] += vv * vv;
+      }
     }
   }
   if constexpr (EPI & 4) {
-    // the 16 lanes of one lane / 16 group hold the same 4 channels (16 pixels): butterfly, one LDS atomic per
-    // group and channel, one global atomic per workgroup and channel
+    // the 16 lanes of one lane / 16 group hold the same 4 channels: butterfly, one LDS atomic per group and
+    // channel, one global atomic per workgroup and channel
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -267,12 +299,15 @@ __global__ __launch_bounds__(256) void f32conv_kernel(F32Args a) {
 
 // ------------------------------------------------------------------------------------------------------ wgrad
 // work: (slot, p0, p1, o0 | (n0 / 16) << 16); rows o0 .. o0 + TC of dW, columns n0 .. n0 + 64 of K; pixels p0..p1 of
-// the OUTPUT grid (dy), 16 per stage.  Each wave owns 16 columns and every row tile.
+// the OUTPUT grid (dy), BP per stage.  Each wave owns 16 columns and every row tile: BP / 4 x MT MFMAs per stage.
+constexpr int W_BP = 32;
 template <int TC, int MODE_X, int MODE_DY>
 __global__ __launch_bounds__(256) void f32wgrad_kernel(F32Args a) {
-  constexpr int MT = TC / 16, TN = 64, BP = 16;  // pixels per stage
+  constexpr int MT = TC / 16, TN = 64, BP = W_BP;
   constexpr int PA = f_pitch(TC), PB = f_pitch(TN);
-  constexpr int DE = TC / 16;                    // dy floats per thread per stage
+  constexpr int DCH = BP * TC / 4;               // dy float4 chunks per stage
+  constexpr int DQ = (DCH + 255) / 256;          // ... per thread
+  constexpr int XQ = BP * TN / 1024;   // x float4 chunks per thread per stage
   __shared__ __attribute__((aligned(16))) float sA[2][BP * PA];  // [pixel][o]
   __shared__ __attribute__((aligned(16))) float sB[2][BP * PB];  // [pixel][k]
   extern __shared__ float dyn[];  // x coefficients (2 Ci) | dy coefficients (3 Co)
@@ -299,49 +334,69 @@ __global__ __launch_bounds__(256) void f32wgrad_kernel(F32Args a) {
     }
   }
   const int HWo = a.Ho * a.Wo;
-  // dy stage: pixel tid / 16, channels o0 + (tid % 16) * DE ..
-  const int pD = tid >> 4, oD = o0 + (tid & 15) * DE;
-  // x stage: pixel tid / 16, columns n0 + 4 (tid % 16) ..
-  const int pX = tid >> 4, kX = n0 + 4 * (tid & 15);
+  // dy chunk q = tid + 256 j: pixel q / (TC / 4), channels o0 + 4 (q % (TC / 4)) ..
+  // x chunk q = tid + 256 j: pixel q / 16, columns n0 + 4 (tid % 16) .. (the same columns for every j)
+  const int kX = n0 + 4 * (tid & 15);
   const int tapX = kX >> a.log2ci, ciX = kX & (Ci - 1);
   const int kyX = a.kw == 1 ? tapX : tapX / a.kw, kxX = tapX - kyX * a.kw;
   const bool kok = kX < K;
-  float rd[DE], rd2[DE];
-  float4 rx;
-  bool okx, okd;
+  float4 rd[DQ], rd2[DQ], rx[XQ];
+  unsigned okd, okx;
   auto load = [&](int s0) {
-    const int p = s0 + pD;
-    okd = p < p1 && oD < a.Co;
-    const long o = (long)p * a.Co + oD;
+    okd = 0;
 #pragma unroll
-    for (int j = 0; j < DE; ++j) {
-      rd[j] = okd ? a.dy[o + j] : 0.f;
-      if constexpr (MODE_DY == 2) rd2[j] = okd ? a.dy2[o + j] : 0.f;
+    for (int j = 0; j < DQ; ++j) {
+      const int q = tid + 256 * j;
+      const int p = s0 + q / (TC / 4), oc = o0 + 4 * (q % (TC / 4));
+      const bool ok = q < DCH && p < p1 && oc < a.Co;
+      const long o = (long)p * a.Co + oc;
+      rd[j] = ok ? *reinterpret_cast<const float4*>(a.dy + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (MODE_DY == 2)
+        rd2[j] = ok ? *reinterpret_cast<const float4*>(a.dy2 + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+      okd |= (unsigned)ok << j;
     }
-    const int px = s0 + pX;
-    const int pp = px < p1 ? px : p0;
-    const int img = pp / HWo, rem = pp - img * HWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
-    const int iy = oy * a.stride - a.pad + kyX, ix = ox * a.stride - a.pad + kxX;
-    okx = px < p1 && kok && iy >= 0 && ix >= 0 && iy < a.Hi && ix < a.Wi;
-    const long xo = (((long)img * a.Hi + iy) * a.Wi + ix) * Ci + ciX;
-    rx = okx ? *reinterpret_cast<const float4*>(a.x + xo) : make_float4(0.f, 0.f, 0.f, 0.f);
+    okx = 0;
+#pragma unroll
+    for (int j = 0; j < XQ; ++j) {
+      const int px = s0 + (tid >> 4) + 16 * j;
+      const int pp = px < p1 ? px : p0;
+      const int img = pp / HWo, rem = pp - img * HWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
+      const int iy = oy * a.stride - a.pad + kyX, ix = ox * a.stride - a.pad + kxX;
+      const bool ok = px < p1 && kok && iy >= 0 && ix >= 0 && iy < a.Hi && ix < a.Wi;
+      const long xo = (((long)img * a.Hi + iy) * a.Wi + ix) * Ci + ciX;
+      rx[j] = ok ? *reinterpret_cast<const float4*>(a.x + xo) : make_float4(0.f, 0.f, 0.f, 0.f);
+      okx |= (unsigned)ok << j;
+    }
   };
   auto store = [&](float* A, float* B) {
 #pragma unroll
-    for (int j = 0; j < DE; ++j) {
-      float v = rd[j];
+    for (int j = 0; j < DQ; ++j) {
+      const int q = tid + 256 * j;
+      if (q >= DCH) break;
+      const int pr = q / (TC / 4), oc = 4 * (q % (TC / 4));
+      float v[4] = {rd[j].x, rd[j].y, rd[j].z, rd[j].w};
       if constexpr (MODE_DY == 2) {
-        const int c = oD + j;
-        v = okd ? cd[c] * rd[j] + cd[a.Co + c] * rd2[j] + cd[2 * a.Co + c] : 0.f;
-      }
-      A[pD * PA + (tid & 15) * DE + j] = v;
-    }
-    float v[4] = {rx.x, rx.y, rx.z, rx.w};
-    if constexpr (MODE_X == 1) {
+        const float h[4] = {rd2[j].x, rd2[j].y, rd2[j].z, rd2[j].w};
+        const bool ok = (okd >> j) & 1u;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = okx ? fmaxf(v[j] * cx[ciX + j] + cx[Ci + ciX + j], 0.f) : 0.f;
+        for (int i = 0; i < 4; ++i) {
+          const int c = o0 + oc + i;
+          v[i] = ok ? cd[c] * v[i] + cd[a.Co + c] * h[i] + cd[2 * a.Co + c] : 0.f;
+        }
+      }
+      *reinterpret_cast<float4*>(A + pr * PA + oc) = make_float4(v[0], v[1], v[2], v[3]);
     }
-    *reinterpret_cast<float4*>(B + pX * PB + 4 * (tid & 15)) = make_float4(v[0], v[1], v[2], v[3]);
+#pragma unroll
+    for (int j = 0; j < XQ; ++j) {
+      float v[4] = {rx[j].x, rx[j].y, rx[j].z, rx[j].w};
+      if constexpr (MODE_X == 1) {
+        const bool ok = (okx >> j) & 1u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = ok ? fmaxf(v[i] * cx[ciX + i] + cx[Ci + ciX + i], 0.f) : 0.f;
+      }
+      *reinterpret_cast<float4*>(B + ((tid >> 4) + 16 * j) * PB + 4 * (tid & 15)) = make_float4(v[0], v[1], v[2],
+                                                                                               v[3]);
+    }
   };
   f32x4_t acc[MT];
 #pragma unroll

@@ -502,7 +502,13 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   __syncthreads();
   if (wave == 0) {
     if (lane == 0) {
+#ifdef DTF_DETERMINISTIC
+      // partials rounded to multiples of 2^-16: their float sum is exact (so order-free) while the member's loss
+      // stays below 2^8
+      atomicAdd(&a.loss[slot], rintf(ldexpf(loss_acc / bsz, 16)) * (1.f / 65536.f));
+#else
       atomicAdd(&a.loss[slot], loss_acc / bsz);
+#endif
       atomicAdd(&a.correct[slot], corr);
     }
     if (a.train) {

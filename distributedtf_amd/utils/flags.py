@@ -219,9 +219,10 @@ class MainArgs(argparse.Namespace):
 
 def hip_deterministic(args) -> bool:
     """Model families whose HIP step has a deterministic (bitwise-replayable) build: CIFAR ResNet v2 and v1 (64
-    statistic replicas, capped workgroups; v1's BN-backward reductions as per-image rows added in image order) and
-    MNIST (one workgroup per member for every accumulation)."""
-    return args.model in ("mnist", "cifar10") and getattr(args, "dtype", "bf16") == "bf16"  # the fp32 step: atomics
+    statistic replicas, capped workgroups; v1's BN-backward reductions as per-image rows added in image order),
+    MNIST (one workgroup per member for every accumulation) and the ImageNet bottleneck nets (every cross-workgroup
+    sum as int64 fixed point with integer atomics, common.h DTF_FIXED_ACC)."""
+    return args.model in ("mnist", "cifar10", "imagenet") and getattr(args, "dtype", "bf16") == "bf16"  # fp32: atomics
 
 
 def parse_main_args(argv=None, defaults=None) -> MainArgs:

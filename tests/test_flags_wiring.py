@@ -121,9 +121,10 @@ def test_deterministic_flag_selects_det_build(monkeypatch):
         assert v1.backend == "hip"  # so does ResNet v1 (per-image BN-backward rows added in image order)
         c = parse_main_args(["--model", "imagenet", "--deterministic"])
         c.apply_runtime_modes()
-        assert c.backend == "torch"  # ImageNet keeps order-dependent split-K reductions on the HIP path
+        assert c.backend == "auto"  # ImageNet: fixed-point (int64) accumulation in the deterministic build
+        assert parse_main_args(["--model", "imagenet", "--deterministic", "--backend", "hip"]).backend == "hip"
         with pytest.raises(SystemExit):  # an explicit --backend hip must not silently lose the guarantee
-            parse_main_args(["--model", "imagenet", "--deterministic", "--backend", "hip"])
+            parse_main_args(["--model", "cifar10", "--dtype", "fp32", "--deterministic", "--backend", "hip"])
         with pytest.raises(SystemExit):  # the debug kernel build is not the deterministic one
             parse_main_args(["--model", "cifar10", "--deterministic", "--debug_kernels"])
         assert kb.LIB_DET.endswith("libdtf_kernels_det.so") and "-DDTF_NREP=64" in kb.DET_FLAGS

@@ -160,3 +160,18 @@ def test_deterministic_build_is_bitwise_replayable():
                         os.path.join(root, "tests", "test_gpu_resnet_step.py") + "::test_hip_step_matches_reference",
                         "-k", "v2-r14-g1-pop2"], env=env, capture_output=True, text=True, timeout=240, cwd=root)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def test_deterministic_imagenet_matches_reference():
+    """The ImageNet step of the deterministic build (every cross-workgroup sum as int64 fixed point, common.h
+    DTF_FIXED_ACC; its bitwise replay is checked by tools/det_check.py above) against the same fp32 oracle as the
+    regular build: 64 x 64 v2 / v1, graph replay and eager, and the 224 x 224 benchmark tiles."""
+    import subprocess
+    import sys as _sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DTF_DETERMINISTIC="1")
+    r = subprocess.run([_sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
+                        os.path.join(root, "tests", "test_gpu_imagenet_step.py")],
+                       env=env, capture_output=True, text=True, timeout=400, cwd=root)
+    print(r.stdout[-1500:])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]

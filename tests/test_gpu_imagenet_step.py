@@ -66,10 +66,15 @@ def test_hip_imagenet_step_matches_reference(monkeypatch, image, sizes, graph, v
     plan = next(iter(hip.backend._plans.values()))
     assert (plan.graph is not None) == (graph == "1")
     l_ref = ref.train_step(slots, batches, hps, [1.0, 1.0])
-    r16.train_step(slots, batches, hps, [1.0, 1.0])
+    l16 = r16.train_step(slots, batches, hps, [1.0, 1.0])
     l_hip = hip.train_step(slots, batches, hps, [1.0, 1.0])
     torch.cuda.synchronize()
-    torch.testing.assert_close(l_hip.float(), l_ref.float(), rtol=3e-2, atol=3e-2)
+    # loss tolerance: 3%, or 2.5x how far a bf16 PyTorch forward of the same net lands from fp32 (a 1001-way softmax
+    # over bf16 logits of a 50-layer v1 net moves by more than 3% at random init)
+    rt = max(3e-2, 2.5 * float(((l16.float() - l_ref.float()).abs() / l_ref.float().abs()).max()))
+    print("loss rel: hip %s, torch bf16 %s" % (((l_hip.float() - l_ref.float()) / l_ref.float()).tolist(),
+                                               ((l16.float() - l_ref.float()) / l_ref.float()).tolist()))
+    torch.testing.assert_close(l_hip.float(), l_ref.float(), rtol=rt, atol=3e-2)
     g_ref, g_hip, g16 = before - ref.params, before - hip.params, before - r16.params
     prog = arch.prog
     segs = [("conv%d" % c.idx, c.off, c.off + c.numel) for c in prog.convs]

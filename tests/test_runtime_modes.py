@@ -34,7 +34,7 @@ def test_deterministic_mode_seeds_and_selects_backend(monkeypatch):
         assert b.backend == "auto"
         c = parse_main_args(["4", "--model", "imagenet", "--deterministic"])
         c.apply_runtime_modes()
-        assert c.backend == "torch" and c.model_kwargs()["backend"] == "torch"
+        assert c.backend == "auto" and c.model_kwargs()["backend"] == "auto"
     finally:
         torch.use_deterministic_algorithms(False)
         os.environ.pop("DTF_DETERMINISTIC", None)

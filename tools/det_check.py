@@ -1,6 +1,7 @@
 """Deterministic HIP build check (run with DTF_DETERMINISTIC=1): two identically initialised engines train the same
 steps on the same batches (graph replay, ragged populations) and must hold bitwise-identical state rows -- the
-CIFAR ResNet v2, ResNet v1 and MNIST families.  Prints DET_OK."""
+CIFAR ResNet v2, ResNet v1, ImageNet ResNet-50 v2 / v1 (fixed-point accumulation) and MNIST families.  Prints
+DET_OK."""
 import os
 import sys
 
@@ -9,13 +10,16 @@ import torch  # noqa: E402
 
 from distributedtf_amd import ops  # noqa: E402
 from distributedtf_amd.engine.population import PopulationEngine  # noqa: E402
-from distributedtf_amd.models.resnet import ResNetArch, cifar_config  # noqa: E402
+from distributedtf_amd.models.resnet import ResNetArch, cifar_config, imagenet_config  # noqa: E402
 
 assert ops.deterministic_mode(), "run with DTF_DETERMINISTIC=1"
 
 
-def run(size, sizes, steps, opt="Momentum", version=2):
-    arch = ResNetArch(cifar_config(size, version=version))
+def run(size, sizes, steps, opt="Momentum", version=2, image=32):
+    if image == 32:
+        arch = ResNetArch(cifar_config(size, version=version))
+    else:
+        arch = ResNetArch(imagenet_config(size, version, num_classes=1001, image_size=image))
     dev = torch.device("cuda")
     out = []
     for rep in range(2):
@@ -27,16 +31,18 @@ def run(size, sizes, steps, opt="Momentum", version=2):
             e.add_member(None, hp, seed=7 + i)
             hps.append(hp)
         g = torch.Generator().manual_seed(3)
-        batches = [(torch.randn(bs, 32, 32, 3, generator=g).to(dev), torch.randint(0, 10, (bs,), generator=g).to(dev))
-                   for bs in sizes]
+        ncls = arch.cfg.num_classes
+        batches = [(torch.randn(bs, image, image, 3, generator=g).to(dev),
+                    torch.randint(0, ncls, (bs,), generator=g).to(dev)) for bs in sizes]
         slots = list(range(len(sizes)))
         for _ in range(steps):
             losses = e.train_step(slots, batches, hps, [0.05] * len(sizes))
         torch.cuda.synchronize()
         out.append((e.state.clone(), losses.cpu()))
-    same = torch.equal(out[0][0], out[1][0])
-    print("v%d size %d sizes %s steps %d: bitwise identical %s, losses %s" % (version, size, sizes, steps, same,
-                                                                         out[0][1].tolist()), flush=True)
+    st, ls = torch.equal(out[0][0], out[1][0]), torch.equal(out[0][1], out[1][1])
+    same = st and ls
+    print("image %d v%d size %d sizes %s steps %d: bitwise identical %s (state %s, losses %s), losses %s"
+          % (image, version, size, sizes, steps, same, st, ls, out[0][1].tolist()), flush=True)
     return same
 
 
@@ -68,6 +74,7 @@ def run_mnist(sizes, steps):
 
 
 ok = all([run(20, [16, 24], 4), run(56, [128], 3), run(56, [128] * 4, 2), run(20, [16, 24], 4, version=1),
-          run(56, [128] * 2, 2, version=1), run_mnist([40, 72], 4)])
+          run(56, [128] * 2, 2, version=1), run_mnist([40, 72], 4),
+          run(50, [4, 6], 3, image=64), run(50, [8, 8], 2, version=1, image=64)])
 print("DET_OK" if ok else "DET_FAIL")
 sys.exit(0 if ok else 1)

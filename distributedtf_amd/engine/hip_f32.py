@@ -35,6 +35,8 @@ c_void_p, c_int, c_long = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
 CMAX = 64
 TP = {16: 256, 32: 128, 64: 64}  # output pixels per conv workgroup by channel tile (f32conv.hip f_tp)
 WG_CHUNK = 2048   # pixels per weight-gradient work item
+BAND_WGRAD = os.environ.get("DTF_F32_BAND_WGRAD", "1") == "1"  # stride-1 3x3 wgrad on the LDS row-band kernel
+BAND_WG_TARGET = int(os.environ.get("DTF_F32_BAND_WG", "768"))  # workgroups per band-wgrad launch
 
 
 class F32Args(ctypes.Structure):
@@ -81,6 +83,8 @@ def _register():
     reg = ops.register
     reg("dtf_f32_conv", [P(F32Args), c_int, c_int, c_int, c_int, c_int, c_void_p])
     reg("dtf_f32_wgrad", [P(F32Args), c_int, c_int, c_int, c_int, c_void_p])
+    reg("dtf_f32_wgrad_band", [P(F32Args), c_int, c_int, c_int, c_void_p])
+    reg("dtf_f32_wgrad_band_ok", [c_int, c_int])
     reg("dtf_f32_ew", [P(F32Ew), c_int, c_void_p])
     reg("dtf_f32_bwd_sums", [P(F32Sum), c_int, c_void_p])
     reg("dtf_f32_head", [P(F32Head), c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_long, c_void_p])
@@ -363,6 +367,26 @@ class _F32Plan:
         a.kh = a.kw = c.k
         a.stride, a.pad = c.stride, (c.k - 1) // 2
         a.log2ci = _log2(a.Ci)
+        L = ops.lib()
+        if (BAND_WGRAD and not stem and c.k == 3 and c.stride == 1 and c.cin == c.cout
+                and L.dtf_f32_wgrad_band_ok(c.cin, hw_in)):
+            # LDS row-band kernel: x / dy staged once per band, all 9 taps from the same tile
+            R = min(hw_in, 128 // hw_in)
+            bpi = hw_in // R
+            nct = c.cin // 16
+            total = sum(self.sizes) * bpi * nct
+            chunk = max(1, int(round(total / float(BAND_WG_TARGET))))
+            items = []
+            for s, n in zip(self.slots, self.sizes):
+                f = self.first[s]
+                for b0 in range(f * bpi, (f + n) * bpi, chunk):
+                    for ct in range(nct):
+                        items.append([s, b0, min(b0 + chunk, (f + n) * bpi), ct])
+            work = self._hold(torch.tensor(items, dtype=torch.int32, device=self.be.dev))
+            a.work = _p(work)
+            self._hold(a)
+            self._add(L.dtf_f32_wgrad_band, ctypes.byref(a), mode_x, mode_dy, work.shape[0])
+            return
         K = c.k * c.k * a.Ci
         tc = min(64, c.cout)
         items = []

@@ -277,6 +277,9 @@ def _hip_f32_ok(engine) -> bool:
     """fp32 HIP step (engine/hip_f32.py): CIFAR-shape building-block ResNets."""
     if engine.compute_dtype != torch.float32:
         return False
+    from .. import ops
+    if ops.deterministic_mode():  # the deterministic build's shared bn_final reads int64 fixed-point sums
+        return False
     from .hip_f32 import supports
     return supports(engine.arch)
 

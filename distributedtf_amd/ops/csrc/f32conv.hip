@@ -437,6 +437,180 @@ __global__ __launch_bounds__(256) void f32wgrad_kernel(F32Args a) {
   }
 }
 
+// --------------------------------------------------------------------------------------------- band wgrad
+// Weight gradient of the stride-1 3x3 convs with Ci = Co = C (every CIFAR ResNet conv but the stem and the stride-2
+// / projection convs) from LDS-resident row bands: a band of R output rows of one image stages dy (all C channels,
+// BN-backward transform applied once) and x (one 16-channel tile `ct`, R + 2 rows x W + 2 columns with the zero
+// halo, ReLU(BN) applied once), and all 9 taps read their B fragments from the same x tile at a (ky, kx) offset.
+// The gather kernel above re-reads x from memory once per tap and per 64-column tile (9-27x the bytes) and
+// re-applies the transforms per read.
+// MFMA: A = dy^T (16 o x 4 pixels), B = x (4 pixels x 16 ci of tap t), acc[m][t] = dW[16 m .. +16][t][16 ct .. +16].
+// The 4 waves split each band's 4-pixel groups and are summed through LDS at the end; then one fp32 atomic per
+// weight and workgroup.  work: (slot, first band, end band, ct); band b = image b / (W / R), rows (b % (W / R)) R ..
+template <int C, int W, int MODE_X, int MODE_DY>
+__global__ __launch_bounds__(256) void f32wgrad_band_kernel(F32Args a) {
+  constexpr int R = (128 / W < W) ? 128 / W : W;  // output rows per band: W 32 -> 4, 16 -> 8, 8 -> 8
+  constexpr int BPI = W / R;                      // bands per image
+  constexpr int NPX = R * W;                      // output pixels per band
+  constexpr int XW = W + 2, XR = R + 2;
+  constexpr int XCH = XR * XW * 4;                // x float4 chunks per band (16 channels)
+  constexpr int XQ = (XCH + 255) / 256;
+  constexpr int DP = f_pitch(C);                  // dy pixel pitch (floats): A-fragment reads conflict-free
+  constexpr int DCH = NPX * C / 4;
+  constexpr int DQ = (DCH + 255) / 256;
+  constexpr int MT = C / 16;
+  constexpr int GPW = NPX / 16;                   // 4-pixel groups per wave and band
+  constexpr int SX = XR * XW * 16, SD = NPX * DP, SRED = MT * 9 * 256;
+  constexpr int SM = (SX + SD > SRED) ? SX + SD : SRED;
+  static_assert(NPX % 16 == 0 && W % 4 == 0, "band geometry");
+  __shared__ __attribute__((aligned(16))) float smem[SM];
+  __shared__ float cx[32];
+  __shared__ float cd[3 * C];
+  float* xL = smem;
+  float* dL = smem + SX;
+  const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z >= wk.y && wk.w >= 0 && wk.w < MT);
+  const int slot = wk.x, b0 = wk.y, b1 = wk.z, ct = wk.w;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if constexpr (MODE_X != 0) {
+    const float* cb = a.c_in + (long)slot * 4 * a.cmax + 16 * ct;
+    if (tid < 16) {
+      cx[tid] = cb[tid];
+      cx[16 + tid] = cb[a.cmax + tid];
+    }
+  }
+  if constexpr (MODE_DY != 0) {
+    const float* cb = a.c_dy + (long)slot * 4 * a.cmax;
+    for (int i = tid; i < C; i += 256) {
+      cd[i] = cb[i];
+      cd[C + i] = cb[a.cmax + i];
+      cd[2 * C + i] = cb[2 * a.cmax + i];
+    }
+  }
+  float4 rx[XQ], rd[DQ], rd2[DQ];
+  unsigned okx = 0;
+  auto load = [&](int b) {
+    const int img = b / BPI, y0 = (b - img * BPI) * R;
+    okx = 0;
+#pragma unroll
+    for (int j = 0; j < XQ; ++j) {
+      const int q = tid + 256 * j;
+      const int pix = q >> 2, c4 = q & 3;
+      const int r = pix / XW, c = pix - r * XW;
+      const int iy = y0 - 1 + r, ix = c - 1;
+      const bool ok = q < XCH && iy >= 0 && iy < W && ix >= 0 && ix < W;
+      const long off = (((long)img * W + iy) * W + ix) * C + 16 * ct + 4 * c4;
+      rx[j] = ok ? *reinterpret_cast<const float4*>(a.x + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+      okx |= (unsigned)ok << j;
+    }
+    const long dbase = ((long)img * W + y0) * W * C;  // the band's rows are contiguous in NHWC
+#pragma unroll
+    for (int j = 0; j < DQ; ++j) {
+      const int q = tid + 256 * j;
+      const bool ok = q < DCH;
+      const long off = dbase + 4L * (ok ? q : 0);
+      rd[j] = ok ? *reinterpret_cast<const float4*>(a.dy + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (MODE_DY == 2)
+        rd2[j] = ok ? *reinterpret_cast<const float4*>(a.dy2 + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int j = 0; j < XQ; ++j) {
+      const int q = tid + 256 * j;
+      if (q >= XCH) break;
+      const int pix = q >> 2, c4 = q & 3;
+      float v[4] = {rx[j].x, rx[j].y, rx[j].z, rx[j].w};
+      if constexpr (MODE_X == 1) {
+        const bool ok = (okx >> j) & 1u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = ok ? fmaxf(v[i] * cx[4 * c4 + i] + cx[16 + 4 * c4 + i], 0.f) : 0.f;
+      }
+      *reinterpret_cast<float4*>(xL + pix * 16 + 4 * c4) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+#pragma unroll
+    for (int j = 0; j < DQ; ++j) {
+      const int q = tid + 256 * j;
+      if (q >= DCH) break;
+      const int pix = q / (C / 4), oc = 4 * (q % (C / 4));
+      float v[4] = {rd[j].x, rd[j].y, rd[j].z, rd[j].w};
+      if constexpr (MODE_DY == 2) {
+        const float h[4] = {rd2[j].x, rd2[j].y, rd2[j].z, rd2[j].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = cd[oc + i] * v[i] + cd[C + oc + i] * h[i] + cd[2 * C + oc + i];
+      }
+      *reinterpret_cast<float4*>(dL + pix * DP + oc) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  f32x4_t acc[MT][9];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[m][t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  const int j4 = lane >> 4, i16 = lane & 15;
+  __syncthreads();  // coefficients
+  if (b0 < b1) load(b0);
+  for (int b = b0; b < b1; ++b) {
+    store();
+    __syncthreads();
+    if (b + 1 < b1) load(b + 1);  // next band's loads in flight under this band's MFMAs
+#pragma unroll 2
+    for (int gi = 0; gi < GPW; ++gi) {
+      const int pb = 4 * (wave * GPW + gi);  // first pixel of the group (one output row: W % 4 == 0)
+      const int row = pb / W, col = pb - row * W;
+      float av[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) av[m] = dL[(pb + j4) * DP + 16 * m + i16];
+      const float* xb = xL + (row * XW + col + j4) * 16 + i16;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const float bv = xb[((t / 3) * XW + t % 3) * 16];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m][t] = mfma4(av[m], bv, acc[m][t]);
+      }
+    }
+    __syncthreads();
+  }
+  // ---- sum the 4 waves' partials through LDS (the band buffers are free), then one atomic per weight
+  float* red = smem;
+  for (int w = 1; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) red[((m * 9 + t) * 4 + r) * 64 + lane] = acc[m][t][r];
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[m][t][r] += red[((m * 9 + t) * 4 + r) * 64 + lane];
+    }
+    __syncthreads();
+  }
+  if (wave == 0) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[((m * 9 + t) * 4 + r) * 64 + lane] = acc[m][t][r];
+  }
+  __syncthreads();
+  float* g = a.grads + (long)slot * a.g_mstride + a.g_off;
+  for (int idx = tid; idx < SRED; idx += 256) {
+    const int l = idx & 63, r = (idx >> 6) & 3, mt = idx >> 8;
+    const int m = mt / 9, t = mt - m * 9;
+    const int o = 16 * m + 4 * (l >> 4) + r, ci = 16 * ct + (l & 15);
+    atomicAdd(g + (long)o * 9 * C + t * C + ci, red[idx]);
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ elementwise
 struct F32Ew {
   const float* dz;
@@ -742,6 +916,29 @@ DTF_API int dtf_f32_wgrad(const F32Args* a, int tc, int mode_x, int mode_dy, int
 #undef W_TCS
 #undef W_CASE
   return -1;
+}
+
+// band wgrad of a stride-1 3x3 conv with Ci = Co = C on W x W images: (C, W) in (16, 32) (32, 16) (64, 8)
+DTF_API int dtf_f32_wgrad_band(const F32Args* a, int mode_x, int mode_dy, int nwork, hipStream_t stream) {
+  if (nwork <= 0) return 0;
+  if (a->Ci != a->Co || a->kh != 3 || a->kw != 3 || a->stride != 1 || a->pad != 1 || a->Hi != a->Wi ||
+      a->Ho != a->Hi || a->Wo != a->Wi || a->wci != a->Ci)
+    return -2;
+  DTF_HOST_CHECK(DTF_ALIGNED16(a->x) && DTF_ALIGNED16(a->dy));
+#define B_CASE(C_, W_, MX, MD)                                                                           \
+  if (a->Ci == C_ && a->Wi == W_ && mode_x == MX && mode_dy == MD) {                                     \
+    hipLaunchKernelGGL((f32wgrad_band_kernel<C_, W_, MX, MD>), dim3(nwork), dim3(256), 0, stream, *a);   \
+    return DTF_CHECK_LAUNCH();                                                                           \
+  }
+#define B_CWS(MX, MD) B_CASE(16, 32, MX, MD) B_CASE(32, 16, MX, MD) B_CASE(64, 8, MX, MD)
+  B_CWS(0, 0) B_CWS(1, 0) B_CWS(0, 2) B_CWS(1, 2)
+#undef B_CWS
+#undef B_CASE
+  return -1;
+}
+
+DTF_API int dtf_f32_wgrad_band_ok(int C, int W) {
+  return (C == 16 && W == 32) || (C == 32 && W == 16) || (C == 64 && W == 8);
 }
 
 DTF_API int dtf_f32_ew(const F32Ew* a, int which, hipStream_t stream) {

@@ -37,6 +37,8 @@ TP = {16: 256, 32: 128, 64: 64}  # output pixels per conv workgroup by channel t
 WG_CHUNK = 2048   # pixels per weight-gradient work item
 BAND_WGRAD = os.environ.get("DTF_F32_BAND_WGRAD", "1") == "1"  # stride-1 3x3 wgrad on the LDS row-band kernel
 BAND_WG_TARGET = int(os.environ.get("DTF_F32_BAND_WG", "768"))  # workgroups per band-wgrad launch
+BAND_CONV = os.environ.get("DTF_F32_BAND_CONV", "1") == "1"  # stride-1 3x3 fwd / dgrad on the row-band kernel
+BAND_CONV_WG_TARGET = int(os.environ.get("DTF_F32_BAND_CONV_WG", "1024"))
 
 
 class F32Args(ctypes.Structure):
@@ -85,6 +87,8 @@ def _register():
     reg("dtf_f32_wgrad", [P(F32Args), c_int, c_int, c_int, c_int, c_void_p])
     reg("dtf_f32_wgrad_band", [P(F32Args), c_int, c_int, c_int, c_void_p])
     reg("dtf_f32_wgrad_band_ok", [c_int, c_int])
+    reg("dtf_f32_conv_band", [P(F32Args), c_int, c_int, c_int, c_int, c_void_p])
+    reg("dtf_f32_conv_band_rows", [c_int])
     reg("dtf_f32_ew", [P(F32Ew), c_int, c_void_p])
     reg("dtf_f32_bwd_sums", [P(F32Sum), c_int, c_void_p])
     reg("dtf_f32_head", [P(F32Head), c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_long, c_void_p])
@@ -339,6 +343,13 @@ class _F32Plan:
             a.Ho = a.Wo = hw_in * c.stride
             a.Co = c.cin
         a.log2ci = _log2(a.Ci)
+        L = ops.lib()
+        if (BAND_CONV and not stem and c.k == 3 and c.stride == 1 and c.cin == c.cout
+                and L.dtf_f32_wgrad_band_ok(c.cin, hw_in)):
+            # LDS row-band kernel: weights staged once per workgroup, the operand band once for all 9 taps
+            self._add_band(a, c.cin, hw_in, BAND_CONV_WG_TARGET, L.dtf_f32_conv_band_rows(c.cin),
+                           L.dtf_f32_conv_band, mode, epi, int(dgrad))
+            return
         tc = min(64, a.Co)
         items = []
         hwo = a.Ho * a.Wo
@@ -352,6 +363,26 @@ class _F32Plan:
         a.work = _p(work)
         self._hold(a)
         self._add(ops.lib().dtf_f32_conv, ctypes.byref(a), tc, mode, epi, int(dgrad), work.shape[0])
+
+    def _add_band(self, a, C, hw, target, rows, fn, *mode_args):
+        """Work items (slot, first band, end band, tile) of a row-band kernel: bands of R = min(hw, 128 / hw) output
+        rows, ``tile`` = output-row offset (conv: multiples of ``rows``) or 16-channel tile index (wgrad: rows = 1,
+        C / 16 tiles); bands per item chosen for about ``target`` workgroups."""
+        R = min(hw, 128 // hw)
+        bpi = hw // R
+        tiles = list(range(0, C, rows)) if rows > 1 else list(range(C // 16))
+        total = sum(self.sizes) * bpi * len(tiles)
+        chunk = max(1, int(round(total / float(target))))
+        items = []
+        for s, n in zip(self.slots, self.sizes):
+            f = self.first[s]
+            for b0 in range(f * bpi, (f + n) * bpi, chunk):
+                for t in tiles:
+                    items.append([s, b0, min(b0 + chunk, (f + n) * bpi), t])
+        work = self._hold(torch.tensor(items, dtype=torch.int32, device=self.be.dev))
+        a.work = _p(work)
+        self._hold(a)
+        self._add(fn, ctypes.byref(a), *mode_args, work.shape[0])
 
     def wgrad(self, ci, x, dy, hw_in, mode_x=0, c_x=None, mode_dy=0, c_dy=None, dy2=None):
         c = self.be.prog.convs[ci]
@@ -371,21 +402,7 @@ class _F32Plan:
         if (BAND_WGRAD and not stem and c.k == 3 and c.stride == 1 and c.cin == c.cout
                 and L.dtf_f32_wgrad_band_ok(c.cin, hw_in)):
             # LDS row-band kernel: x / dy staged once per band, all 9 taps from the same tile
-            R = min(hw_in, 128 // hw_in)
-            bpi = hw_in // R
-            nct = c.cin // 16
-            total = sum(self.sizes) * bpi * nct
-            chunk = max(1, int(round(total / float(BAND_WG_TARGET))))
-            items = []
-            for s, n in zip(self.slots, self.sizes):
-                f = self.first[s]
-                for b0 in range(f * bpi, (f + n) * bpi, chunk):
-                    for ct in range(nct):
-                        items.append([s, b0, min(b0 + chunk, (f + n) * bpi), ct])
-            work = self._hold(torch.tensor(items, dtype=torch.int32, device=self.be.dev))
-            a.work = _p(work)
-            self._hold(a)
-            self._add(L.dtf_f32_wgrad_band, ctypes.byref(a), mode_x, mode_dy, work.shape[0])
+            self._add_band(a, c.cin, hw_in, BAND_WG_TARGET, 1, L.dtf_f32_wgrad_band, mode_x, mode_dy)
             return
         K = c.k * c.k * a.Ci
         tc = min(64, c.cout)

@@ -57,6 +57,72 @@ constexpr int f_pitch(int n) { return n == 16 ? 16 : (n == 32 ? 48 : n + 16); }
 // MT x NT = 4 MFMA tiles per k-step whatever the channel width (a C = 16 layer would otherwise get one)
 constexpr int f_tp(int tc) { return 64 * (64 / tc); }
 
+// ---- shared epilogue of the conv kernels: one lane's 4 output channels co .. co + 3 of pixel p (MFMA D layout):
+// [+ residual] [mask by BN(xm) + ReLU > 0], fp32 store, per-channel statistics (y, y^2; with the mask dz, dz * xhat)
+template <int EPI>
+__device__ __forceinline__ void f32_epi4(const F32Args& a, int slot, long p, int co, bool ok, const f32x4_t& acc,
+                                         float (&ss)[4], float (&sq)[4]) {
+  const long o = p * a.Co + co;
+  float v[4] = {acc[0], acc[1], acc[2], acc[3]};
+  float xv[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (EPI & 1) {
+    if (ok) {
+      const float4 r = *reinterpret_cast<const float4*>(a.res + o);
+      v[0] += r.x, v[1] += r.y, v[2] += r.z, v[3] += r.w;
+    }
+  }
+  const float* ep = (EPI & 2) ? a.c_ep + (long)slot * 4 * a.cmax + (ok ? co : 0) : nullptr;
+  if constexpr (EPI & 2) {
+    if (ok) {
+      const float4 xr = *reinterpret_cast<const float4*>(a.xm + o);
+      xv[0] = xr.x, xv[1] = xr.y, xv[2] = xr.z, xv[3] = xr.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = (xv[i] * ep[i] + ep[a.cmax + i] > 0.f) ? v[i] : 0.f;
+  }
+  if (ok) *reinterpret_cast<float4*>(a.y + o) = make_float4(v[0], v[1], v[2], v[3]);
+  if constexpr (EPI & 4) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float vv = ok ? v[i] : 0.f;
+      ss[i] += vv;
+      if constexpr (EPI & 2)
+        sq[i] += ok ? vv * (xv[i] - ep[2 * a.cmax + i]) * ep[3 * a.cmax + i] : 0.f;
+      else
+        sq[i] += vv * vv;
+    }
+  }
+}
+
+// Workgroup statistics: the 16 lanes of one lane / 16 group hold the same 4 channels -- butterfly, one LDS atomic
+// per group and channel, one global atomic per workgroup and channel.  acc_lds [2][TC] zeroed before the k loop.
+template <int TC, int MT>
+__device__ __forceinline__ void f32_stats_flush(const F32Args& a, int slot, int o0, float (&ss)[MT][4],
+                                                float (&sq)[MT][4], float (&acc_lds)[2][TC]) {
+  const int tid = threadIdx.x, lane = tid & 63;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float s_ = ss[m][i], q_ = sq[m][i];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s_ += __shfl_xor(s_, o, 64);
+        q_ += __shfl_xor(q_, o, 64);
+      }
+      if ((lane & 15) == 0) {
+        atomicAdd(&acc_lds[0][16 * m + 4 * (lane >> 4) + i], s_);
+        atomicAdd(&acc_lds[1][16 * m + 4 * (lane >> 4) + i], q_);
+      }
+    }
+  __syncthreads();
+  if (tid < TC && o0 + tid < a.Co) {
+    float* st = a.st_out + (long)slot * 2 * a.cmax;
+    atomicAdd(st + o0 + tid, acc_lds[0][tid]);
+    atomicAdd(st + a.cmax + o0 + tid, acc_lds[1][tid]);
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ fwd / dgrad
 template <int TC, int MODE, int EPI, bool DGRAD>
 __global__ __launch_bounds__(256) void f32conv_kernel(F32Args a) {
@@ -235,66 +301,168 @@ __global__ __launch_bounds__(256) void f32conv_kernel(F32Args a) {
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
     const int p = p0 + 16 * (wave * NT + n) + (lane & 15);
-    const bool pok = p < p1;
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       const int co = o0 + 16 * m + 4 * (lane >> 4);
-      const bool ok = pok && co < a.Co;
-      const long o = (long)p * a.Co + co;
-      float v[4] = {acc[m][n][0], acc[m][n][1], acc[m][n][2], acc[m][n][3]};
-      float xv[4] = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (EPI & 1) {
-        if (ok) {
-          const float4 r = *reinterpret_cast<const float4*>(a.res + o);
-          v[0] += r.x, v[1] += r.y, v[2] += r.z, v[3] += r.w;
-        }
-      }
-      const float* ep = (EPI & 2) ? a.c_ep + (long)slot * 4 * a.cmax + (ok ? co : 0) : nullptr;
-      if constexpr (EPI & 2) {
-        if (ok) {
-          const float4 xr = *reinterpret_cast<const float4*>(a.xm + o);
-          xv[0] = xr.x, xv[1] = xr.y, xv[2] = xr.z, xv[3] = xr.w;
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = (xv[i] * ep[i] + ep[a.cmax + i] > 0.f) ? v[i] : 0.f;
-      }
-      if (ok) *reinterpret_cast<float4*>(a.y + o) = make_float4(v[0], v[1], v[2], v[3]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float vv = ok ? v[i] : 0.f;
-        ss[m][i] += vv;
-        if constexpr (EPI & 2)
-          sq[m][i] += ok ? vv * (xv[i] - ep[2 * a.cmax + i]) * ep[3 * a.cmax + i] : 0.f;
-        else
-          sq[m][i] += vv * vv;
-      }
+      f32_epi4<EPI>(a, slot, p, co, p < p1 && co < a.Co, acc[m][n], ss[m], sq[m]);
     }
   }
-  if constexpr (EPI & 4) {
-    // the 16 lanes of one lane / 16 group hold the same 4 channels: butterfly, one LDS atomic per group and
-    // channel, one global atomic per workgroup and channel
+  if constexpr (EPI & 4) f32_stats_flush<TC>(a, slot, o0, ss, sq, acc_lds);
+}
+
+// ------------------------------------------------------------------------------------------ band fwd / dgrad
+// Forward or data gradient of a stride-1 3x3 conv with Ci = Co = C on W x W images from LDS-resident row bands: the
+// workgroup stages its TCB output rows of the weights once ([tap][row][k], k contiguous; the data gradient's
+// transposed operand W[o][t][i] -> [t][i][o] is transposed while staging), then per band of R output rows the
+// gathered operand (x, or dy) with its zero halo, transform applied once; all 9 taps read B fragments from that tile
+// at a (ky, kx) offset (data gradient: the flipped (2 - ky, 2 - kx) offset).  The gather kernel above re-reads the
+// operand from memory per tap and per output-channel tile.
+// Both operands are read as float4 along k: lane l takes k = base + 4 (l / 16) .. + 3, and MFMA q of the four uses
+// element q -- the 4 MFMAs cover k = base .. base + 15 in a permuted order that A and B share.  Pitches C + 8
+// (k rows of one pixel / one weight row) make those ds_read_b128 conflict-free (the W = 8 tile: 2-way).
+// work: (slot, first band, end band, o0); band b = image b / (W / R), rows (b % (W / R)) R ..
+template <int C, int W, int TCB, int MODE, int EPI, bool DGRAD>
+__global__ __launch_bounds__(256) void f32conv_band_kernel(F32Args a) {
+  constexpr int R = (128 / W < W) ? 128 / W : W;
+  constexpr int BPI = W / R;
+  constexpr int NPX = R * W;
+  constexpr int XW = W + 2, XR = R + 2, XP = C + 8, WP = C + 8;
+  constexpr int MT = TCB / 16, NT = NPX / 64;     // row tiles; 16-pixel tiles per wave
+  constexpr int XCH = XR * XW * C / 4;
+  constexpr int XQ = (XCH + 255) / 256;
+  constexpr int SW = 9 * TCB * WP, SX = XR * XW * XP;
+  static_assert(NPX % 64 == 0 && W % 4 == 0 && C % 16 == 0 && TCB % 16 == 0, "band geometry");
+  __shared__ __attribute__((aligned(16))) float wL[SW];
+  __shared__ __attribute__((aligned(16))) float xL[SX];
+  __shared__ float acc_lds[2][TCB];
+  __shared__ float cf[3 * C];
+  const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z >= wk.y && wk.w >= 0 && wk.w + TCB <= C);
+  const int slot = wk.x, b0 = wk.y, b1 = wk.z, o0 = wk.w;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int j4 = lane >> 4, i16 = lane & 15;
+  if constexpr (MODE != 0) {
+    const float* cb = a.c_in + (long)slot * 4 * a.cmax;
+    for (int i = tid; i < C; i += 256) {
+      cf[i] = cb[i];
+      cf[C + i] = cb[a.cmax + i];
+      if constexpr (MODE == 2) cf[2 * C + i] = cb[2 * a.cmax + i];
+    }
+  }
+  for (int i = tid; i < 2 * TCB; i += 256) (&acc_lds[0][0])[i] = 0.f;
+  // ---- weights: wL[t][r][k] (r = output row o0 + r, k = reduction channel)
+  const float* wrow = a.w + (long)slot * a.w_mstride + a.w_off;
+  if constexpr (!DGRAD) {
+    for (int q = tid; q < 9 * TCB * C / 4; q += 256) {  // (r, t, k4): global W[o0 + r][t][4 k4 ..] contiguous
+      const int k4 = q % (C / 4), rt = q / (C / 4), t = rt % 9, r = rt / 9;
+      const float4 v = *reinterpret_cast<const float4*>(wrow + ((long)(o0 + r) * 9 + t) * C + 4 * k4);
+      *reinterpret_cast<float4*>(wL + (t * TCB + r) * WP + 4 * k4) = v;
+    }
+  } else {
+    for (int q = tid; q < 9 * TCB * C; q += 256) {  // (o, t, r): global W[o][t][o0 + r], r fastest
+      const int r = q % TCB, ot = q / TCB, t = ot % 9, o = ot / 9;
+      wL[(t * TCB + r) * WP + o] = wrow[((long)o * 9 + t) * C + o0 + r];
+    }
+  }
+  // ---- per-lane pixel of each of the wave's 16-pixel tiles (band-relative) and its halo-tile index
+  int pxl[NT], xb[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    pxl[n] = 16 * (wave * NT + n) + i16;
+    const int r = pxl[n] / W, c = pxl[n] - r * W;
+    xb[n] = (r * XW + c) * XP + 4 * j4;
+  }
+  float4 rx[XQ], rx2[XQ];
+  unsigned okx = 0;
+  auto load = [&](int b) {
+    const int img = b / BPI, y0 = (b - img * BPI) * R;
+    okx = 0;
+#pragma unroll
+    for (int j = 0; j < XQ; ++j) {
+      const int q = tid + 256 * j;
+      const int pix = q / (C / 4), c4 = q - pix * (C / 4);
+      const int r = pix / XW, c = pix - r * XW;
+      const int iy = y0 - 1 + r, ix = c - 1;
+      const bool ok = q < XCH && iy >= 0 && iy < W && ix >= 0 && ix < W;
+      const long off = (((long)img * W + iy) * W + ix) * C + 4 * c4;
+      rx[j] = ok ? *reinterpret_cast<const float4*>(a.x + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (MODE == 2)
+        rx2[j] = ok ? *reinterpret_cast<const float4*>(a.x2 + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+      okx |= (unsigned)ok << j;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int j = 0; j < XQ; ++j) {
+      const int q = tid + 256 * j;
+      if (q >= XCH) break;
+      const int pix = q / (C / 4), c4 = q - pix * (C / 4);
+      float v[4] = {rx[j].x, rx[j].y, rx[j].z, rx[j].w};
+      if constexpr (MODE != 0) {
+        const float h[4] = {rx2[j].x, rx2[j].y, rx2[j].z, rx2[j].w};
+        const bool ok = (okx >> j) & 1u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ch = 4 * c4 + i;
+          float t;
+          if constexpr (MODE == 1)
+            t = fmaxf(v[i] * cf[ch] + cf[C + ch], 0.f);
+          else
+            t = cf[ch] * v[i] + cf[C + ch] * h[i] + cf[2 * C + ch];
+          v[i] = ok ? t : 0.f;  // the zero padding stays zero after the transform
+        }
+      }
+      *reinterpret_cast<float4*>(xL + pix * XP + 4 * c4) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  float ss[MT][4], sq[MT][4];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ss[m][i] = sq[m][i] = 0.f;
+  if (b0 < b1) load(b0);
+  for (int b = b0; b < b1; ++b) {
+    __syncthreads();  // (first band: weights / coefficients staged) the previous band's tile is consumed
+    store();
+    __syncthreads();
+    if (b + 1 < b1) load(b + 1);  // the next band's loads stay in flight under this band's MFMAs
+    f32x4_t acc[MT][NT];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float s_ = ss[m][i], q_ = sq[m][i];
+      for (int n = 0; n < NT; ++n) acc[m][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll 3
+    for (int t = 0; t < 9; ++t) {
+      const int ky = t / 3, kx = t - 3 * (t / 3);
+      const int boff = DGRAD ? ((2 - ky) * XW + 2 - kx) * XP : (ky * XW + kx) * XP;
+      const float* wt = wL + (t * TCB + i16) * WP + 4 * j4;
 #pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          s_ += __shfl_xor(s_, o, 64);
-          q_ += __shfl_xor(q_, o, 64);
-        }
-        if ((lane & 15) == 0) {
-          atomicAdd(&acc_lds[0][16 * m + 4 * (lane >> 4) + i], s_);
-          atomicAdd(&acc_lds[1][16 * m + 4 * (lane >> 4) + i], q_);
-        }
+      for (int kc = 0; kc < C / 16; ++kc) {
+        float4 av[MT], bv[NT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) av[m] = *reinterpret_cast<const float4*>(wt + 16 * m * WP + 16 * kc);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) bv[n] = *reinterpret_cast<const float4*>(xL + xb[n] + boff + 16 * kc);
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int n = 0; n < NT; ++n) {
+            acc[m][n] = mfma4(av[m].x, bv[n].x, acc[m][n]);
+            acc[m][n] = mfma4(av[m].y, bv[n].y, acc[m][n]);
+            acc[m][n] = mfma4(av[m].z, bv[n].z, acc[m][n]);
+            acc[m][n] = mfma4(av[m].w, bv[n].w, acc[m][n]);
+          }
       }
-    __syncthreads();
-    if (tid < TC && o0 + tid < a.Co) {
-      float* st = a.st_out + (long)slot * 2 * a.cmax;
-      atomicAdd(st + o0 + tid, acc_lds[0][tid]);
-      atomicAdd(st + a.cmax + o0 + tid, acc_lds[1][tid]);
     }
+    const int img = b / BPI, y0 = (b - img * BPI) * R;
+    const long pbase = ((long)img * W + y0) * W;
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        f32_epi4<EPI>(a, slot, pbase + pxl[n], o0 + 16 * m + 4 * j4, true, acc[m][n], ss[m], sq[m]);
   }
+  if constexpr (EPI & 4) f32_stats_flush<TCB>(a, slot, o0, ss, sq, acc_lds);
 }
 
 // ------------------------------------------------------------------------------------------------------ wgrad
@@ -915,6 +1083,31 @@ DTF_API int dtf_f32_wgrad(const F32Args* a, int tc, int mode_x, int mode_dy, int
   W_TCS(0, 0) W_TCS(1, 0) W_TCS(0, 2) W_TCS(1, 2)
 #undef W_TCS
 #undef W_CASE
+  return -1;
+}
+
+// band fwd / dgrad of a stride-1 3x3 conv with Ci = Co = C on W x W images (the dtf_f32_conv modes / epilogues);
+// rows per workgroup: C (C <= 32) or 16 (C = 64: the 9 x 64 x 72 weight tile of all 64 rows would not fit twice)
+DTF_API int dtf_f32_conv_band_rows(int C) { return C <= 32 ? C : 16; }
+
+DTF_API int dtf_f32_conv_band(const F32Args* a, int mode, int epi, int dgrad, int nwork, hipStream_t stream) {
+  if (nwork <= 0) return 0;
+  if (a->Ci != a->Co || a->kh != 3 || a->kw != 3 || a->stride != 1 || a->pad != 1 || a->Hi != a->Wi ||
+      a->Ho != a->Hi || a->Wo != a->Wi || a->wci != a->Ci)
+    return -2;
+  DTF_HOST_CHECK(DTF_ALIGNED16(a->x) && DTF_ALIGNED16(a->y));
+#define CB_CASE(C_, W_, M_, E_, D_)                                                                                \
+  if (a->Ci == C_ && a->Wi == W_ && mode == M_ && epi == E_ && dgrad == D_) {                                      \
+    hipLaunchKernelGGL((f32conv_band_kernel<C_, W_, (C_ <= 32 ? C_ : 16), M_, E_, D_>), dim3(nwork), dim3(256), 0, \
+                       stream, *a);                                                                               \
+    return DTF_CHECK_LAUNCH();                                                                                     \
+  }
+#define CB_CWS(M_, E_, D_) CB_CASE(16, 32, M_, E_, D_) CB_CASE(32, 16, M_, E_, D_) CB_CASE(64, 8, M_, E_, D_)
+  CB_CWS(0, 4, false) CB_CWS(0, 0, false) CB_CWS(1, 4, false) CB_CWS(1, 0, false) CB_CWS(1, 5, false)
+  CB_CWS(0, 6, true) CB_CWS(0, 7, true) CB_CWS(0, 0, true) CB_CWS(2, 3, true) CB_CWS(2, 6, true) CB_CWS(2, 7, true)
+  CB_CWS(2, 0, true)
+#undef CB_CWS
+#undef CB_CASE
   return -1;
 }
 

@@ -59,6 +59,9 @@ def parse():
     p.add_argument("--ragged", action="store_true",
                    help="keep the sampled per-member batch sizes (65..255) and let explore perturb them (real PBT: "
                         "a new batch composition after every exploit); default pins every member to --batch")
+    p.add_argument("--batch_sizes", default=None,
+                   help="with --ragged: comma-separated per-member batch sizes (e.g. a PBT round's mix from "
+                        "metrics.jsonl 'batch_sizes') instead of the sampled ones")
     a = p.parse_args()
     if a.resnet_size is None:
         a.resnet_size = 50 if a.model == "imagenet" else 56
@@ -90,6 +93,11 @@ def main():
     if not args.ragged:
         for h in hps:
             h["batch_size"] = args.batch
+    elif args.batch_sizes:
+        bs = [int(v) for v in args.batch_sizes.split(",")]
+        assert len(bs) == args.pop, "--batch_sizes needs one size per member (--pop %d)" % args.pop
+        for h, b in zip(hps, bs):
+            h["batch_size"] = b
     begin, cnt = partition(args.pop, world)[rank]
     if args.model == "mnist":
         make = lambda i: MNISTModel(begin + i, hps[begin + i], "/tmp/bench_savedata_%d/model_" % rank,  # noqa: E731

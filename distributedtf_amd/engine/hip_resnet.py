@@ -59,6 +59,13 @@ FUSED_MIN_WG = 256        # ... at least this many workgroups (one member would 
 FUSED_MAX_WG = {32: 128}  # ... at most this many per member (C = 32: fewer, fuller workgroups)
 PIGGYBACK_MAX_WG = 3000   # slab reductions ride on the next backward launch when they add <= this many workgroups
 DEFER_WG = {16: 64, 32: 32, 64: 16}  # deferred wgrad (small populations): workgroups per member and layer
+# deferred wgrad launches issued on a side stream (a parallel branch of the step graph) as soon as a stage's layers
+# -- or OVERLAP_CHUNK of them -- are queued, so they run under the serial dgrad chain of the earlier stages instead
+# of as a tail after it.  Off by default: the two-branch step graph measured SLOWER (pop 1: 1.051 -> 1.272 ms, stage
+# chunks 1.394 ms; pop 2: 1.389 -> 1.577 ms; profiles/r4_wg_overlap_ab.log) -- the branch's cross-stream
+# dependencies cost more than the idle CUs it fills
+WG_OVERLAP = os.environ.get("DTF_WG_OVERLAP", "0") == "1"  # measured slower: profiles/r4_wg_overlap_ab.log
+OVERLAP_CHUNK = int(os.environ.get("DTF_WG_OVERLAP_CHUNK", "0"))  # 0: stage boundaries only
 DEFER_MID_POP = 4         # up to this many members: defer the wgrad of DEFER_MID_CS ...
 DEFER_MID_CS = (32, 64)
 DEFER_LARGE_CS = (64,)    # larger populations defer the wgrad of these channel widths only ...
@@ -724,6 +731,7 @@ class _StepPlan:
         # those layers runs afterwards in two wide launches (conv_wgrad_all_kernel: widths 64 + 32, width 16).
         # Their dY / x operands stay alive for the whole backward (per-block buffers instead of ping-pong ones).
         self.defer_wg = self.dual
+        self.overlap_wg = self.defer_wg and WG_OVERLAP and dev.type == "cuda"
         # channel widths whose stride-1 wgrad is deferred: every width at small populations; up to 4 members C = 32
         # and 64, at larger ones the C = 64 layers only (1 workgroup per CU of the fused kernel left the MFMA pipe
         # idle, and its 147 KB dW slab per workgroup cost more than re-reading dY / x once in the wide wgrad
@@ -1214,15 +1222,20 @@ class _StepPlan:
         w.cin_real = -1
         self._wg_jobs.setdefault((C, wmode), []).append((w, wwork, c.off))
 
-    def _emit_deferred_wgrad(self):
+    def _emit_deferred_wgrad(self, only_c=None, side=False):
         """Every queued layer's wgrad job in two launches (conv_wgrad_all_kernel: widths 64 + 32 -- one wave per SIMD
         -- and width 16, kept apart at its higher occupancy); their slabs join the reduction of _flush_deferred.
-        One launch per (C, dY mode) measured 18 us slower at pop 1 (profiles/r3_merged_launches_ab.log)."""
+        One launch per (C, dY mode) measured 18 us slower at pop 1 (profiles/r3_merged_launches_ab.log).
+        ``only_c``: just the jobs of that width; ``side``: on the side stream (a parallel graph branch, joined before
+        the slab reduction)."""
         lib = ops.lib()
+        if side and any(C == only_c or only_c is None for (C, _) in self._wg_jobs):
+            self._add("fork", None)
+            self._forked = True
         for cset, widths in ((0, (64, 32)), (1, (16,))):  # must match dtf_conv_wgrad_all's instantiations
             arr_l, wmap, lds = [], [], 0
             for (C, wmode), jobs in sorted(self._wg_jobs.items(), key=lambda kv: (-kv[0][0], -kv[0][1])):
-                if C not in widths:
+                if C not in widths or (only_c is not None and C != only_c):
                     continue
                 tsz = ((8 + 2) * _wpitch(C) * _cpad(C) + 8 + 63) // 64 * 64
                 lds = max(lds, 2304 + 4 * tsz * 2)
@@ -1239,7 +1252,20 @@ class _StepPlan:
             self._keep(jt)
             self._keep(mt)
             self._add(lib.dtf_conv_wgrad_all, _p(jt), _p(mt), len(wmap), cset, lds)
-        self._wg_jobs = {}
+        if side and getattr(self, "_forked", False):
+            self._add("endfork", None)
+        self._wg_jobs = {k: v for k, v in self._wg_jobs.items() if only_c is not None and k[0] != only_c}
+
+    def _maybe_overlap_wgrad(self, i):
+        """After block i's backward: issue the queued deferred wgrad jobs of its width on the side stream when the
+        next block to process has another width (stage boundary) or OVERLAP_CHUNK jobs are queued."""
+        if not (self.overlap_wg and self._wg_jobs):
+            return
+        C = self.hs[i].shape[3]
+        nxt = self.hs[i - 1].shape[3] if i > 0 else None
+        queued = sum(len(v) for (c, _), v in self._wg_jobs.items() if c == C)
+        if nxt != C or (OVERLAP_CHUNK and queued >= OVERLAP_CHUNK):
+            self._emit_deferred_wgrad(only_c=C, side=True)
 
     def _fresh_like(self, t):
         u = torch.empty_like(t)
@@ -1471,9 +1497,12 @@ class _StepPlan:
             else:
                 self._bn_bwd_apply(Tin["dz1"], x, add, g_next, bn1)
             g_cur = g_next
+            self._maybe_overlap_wgrad(i)
         # stem wgrad (input = padded image, real channels 3)
         self._conv_wgrad(prog.stem, self.xin16, g_cur, mode_x=0, mode_dy=0, cin_real=cfg.in_channels)
         self._emit_deferred_wgrad()
+        if getattr(self, "_forked", False):
+            self._add("join", None)  # the side-stream wgrad branch ends before the slab reduction
         # BN parameter gradients from the backward reductions
         self._flush_slab()
         self._flush_deferred()
@@ -1742,8 +1771,23 @@ class _StepPlan:
 
     def _run_eager(self):
         e = self.e
+        main = torch.cuda.current_stream() if self.be.dev.type == "cuda" else None
+        target = None  # None: the current stream; else the side stream of a fork
         for fn, args in self.launches:
-            if fn == "augment":
+            if fn == "fork":  # the side stream waits for everything issued so far on the main stream
+                if getattr(self, "_side", None) is None:
+                    self._side = torch.cuda.Stream(device=self.be.dev)
+                self._side.wait_stream(main)
+                target = self._side
+            elif fn == "endfork":
+                target = None
+            elif fn == "join":
+                main.wait_stream(self._side)
+            elif target is not None:
+                err = fn(*args, target.cuda_stream)
+                if err != 0:
+                    raise RuntimeError("kernel launch %s failed with %d" % (getattr(fn, "__name__", fn), err))
+            elif fn == "augment":
                 ops.augment_cifar(self.src.train_x, self.src.train_y, self.idx, self.rng, True, out16=self.xin16,
                                   lab32=self.labels)
             elif fn == "optim":

@@ -346,6 +346,9 @@ class SPMDPopulation(_ReportMixin):
         return [v for part in parts for v in part]
 
     def train_one_round(self, rnd, total_rounds):
+        # the batch sizes this round trains with (explore may change them before the round's metrics line)
+        self._round_bs = [[int(getattr(g, "cluster_id", -1)), int(g.hparams.get("batch_size", 0))]
+                          for g in self.worker.worker_graphs if self.is_group_leader and hasattr(g, "hparams")]
         self.worker.train(self.epochs_per_round, self.epochs_per_round * total_rounds)
         for mid in self.inject_nan.get(rnd, []):
             for g in list(self.worker.worker_graphs):
@@ -410,7 +413,8 @@ class SPMDPopulation(_ReportMixin):
         delta = [c - p for c, p in zip(cur, prev)]
         phases = PHASES.since(getattr(self, "_prev_phases", {}))
         self._prev_phases = PHASES.snapshot()
-        parts = self.comm.allgather([delta, [float(v[1]) for v in self._values()], phases, self._graph_state()])
+        parts = self.comm.allgather([delta, [float(v[1]) for v in self._values()], phases, self._graph_state(),
+                                     getattr(self, "_round_bs", [])])
         if self.rank != 0:
             return
         d = [p[0] for p in parts]
@@ -430,7 +434,9 @@ class SPMDPopulation(_ReportMixin):
                "world_size": self.world, "phases_s": phase_s,
                # how the HIP step ran on each rank ("captured" graph replay / "eager_fallback" when a data-parallel
                # capture was refused / "disabled" / None for torch backends): a silent eager cliff shows up here
-               "step_graph": sorted({str(p[3]) for p in parts})}
+               "step_graph": sorted({str(p[3]) for p in parts}),
+               # member id -> batch size trained this round (bench.py --ragged --batch_sizes reproduces the mix)
+               "batch_sizes": {str(i): b for p in parts for i, b in sorted(p[4])}}
         self._prev_exploit = self.exploit_time
         import json
         os.makedirs(self.savedata, exist_ok=True)

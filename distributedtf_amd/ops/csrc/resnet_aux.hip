@@ -708,24 +708,41 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnEwArgs a) {
   for (int k = 0; k < 8; ++k) sd[k] = s1[k] = s2[k] = 0.f;
   const int i0 = blockIdx.y * blockDim.x + threadIdx.x;
   const int c0 = (i0 * 8) % C;
-  for (int i = i0; i < n8; i += gridDim.y * blockDim.x) {
-    const long o = base + (long)i * 8;
-    const uint4 dv = *reinterpret_cast<const uint4*>(a.d + o);
-    const uint4 hv = *reinterpret_cast<const uint4*>(a.h1 + o);
-    uint4 pv = make_uint4(0, 0, 0, 0);
-    if (a.h2) pv = *reinterpret_cast<const uint4*>(a.h2 + o);
-    const uint32_t d32[4] = {dv.x, dv.y, dv.z, dv.w}, h32[4] = {hv.x, hv.y, hv.z, hv.w},
-                   p32[4] = {pv.x, pv.y, pv.z, pv.w};
+  const int stride = gridDim.y * blockDim.x;
+  float mi1[8], iv1[8], mi2[8], iv2[8];  // this thread's 8 channels' coefficients in registers
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int c = c0 + k;
-      const float dd = bf2f((bf16_t)((d32[k >> 1] >> (16 * (k & 1))) & 0xffff));
-      const float hh = bf2f((bf16_t)((h32[k >> 1] >> (16 * (k & 1))) & 0xffff));
-      sd[k] += dd;
-      s1[k] += dd * (hh * co[64 + c] + co[c]);
-      if (a.h2) {
-        const float pp = bf2f((bf16_t)((p32[k >> 1] >> (16 * (k & 1))) & 0xffff));
-        s2[k] += dd * (pp * co[192 + c] + co[128 + c]);
+  for (int k = 0; k < 8; ++k) {
+    mi1[k] = co[c0 + k];
+    iv1[k] = co[64 + c0 + k];
+    mi2[k] = co[128 + c0 + k];
+    iv2[k] = co[192 + c0 + k];
+  }
+  // two 16-byte chunks per operand in flight per thread and trip (the loop was load-latency bound)
+  for (int i = i0; i < n8; i += 2 * stride) {
+    const bool two = i + stride < n8;
+    uint4 dv[2], hv[2], pv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const long o = base + (long)(u && two ? i + stride : i) * 8;
+      dv[u] = *reinterpret_cast<const uint4*>(a.d + o);
+      hv[u] = *reinterpret_cast<const uint4*>(a.h1 + o);
+      pv[u] = a.h2 ? *reinterpret_cast<const uint4*>(a.h2 + o) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (u == 1 && !two) break;
+      const uint32_t d32[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w}, h32[4] = {hv[u].x, hv[u].y, hv[u].z, hv[u].w},
+                     p32[4] = {pv[u].x, pv[u].y, pv[u].z, pv[u].w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float dd = bf2f((bf16_t)((d32[k >> 1] >> (16 * (k & 1))) & 0xffff));
+        const float hh = bf2f((bf16_t)((h32[k >> 1] >> (16 * (k & 1))) & 0xffff));
+        sd[k] += dd;
+        s1[k] += dd * (hh * iv1[k] + mi1[k]);
+        if (a.h2) {
+          const float pp = bf2f((bf16_t)((p32[k >> 1] >> (16 * (k & 1))) & 0xffff));
+          s2[k] += dd * (pp * iv2[k] + mi2[k]);
+        }
       }
     }
   }
@@ -756,7 +773,19 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnEwArgs a) {
   }
   (void)acc;
 #else
-  if (i0 < n8) {
+  // lanes l and l ^ (G j) hold the same 8 channels (c0 = 8 (lane % G), G = C / 8): butterfly over them first, so the
+  // LDS atomics are 4-way (one per wave) instead of 256 / G-way contended (the contention made this kernel 4x its
+  // HBM time)
+  const int G = C / 8, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    for (int o = G; o < 64; o <<= 1) {
+      sd[k] += __shfl_xor(sd[k], o, 64);
+      s1[k] += __shfl_xor(s1[k], o, 64);
+      if (a.h2) s2[k] += __shfl_xor(s2[k], o, 64);
+    }
+  }
+  if (lane < G) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       atomicAdd(&acc[c0 + k], sd[k]);

@@ -70,6 +70,7 @@ DEFER_MID_POP = 4         # up to this many members: defer the wgrad of DEFER_MI
 DEFER_MID_CS = (32, 64)
 DEFER_LARGE_CS = (64,)    # larger populations defer the wgrad of these channel widths only ...
 DEFER_LARGE_WG = {16: 16, 32: 8, 64: 8}  # ... with this many workgroups per member and layer
+V1_CHAIN_BN = os.environ.get("DTF_V1_CHAIN_BN", "1") == "1"  # v1: BN_b backward sums in the next conv_a epilogue
 HALF_BANDS_MAX_IMGS = 128  # C = 64 stage (8x8): 4-row half-image bands for the forward / dgrad launches up to this many
 #                            images per step (one member: whole-image items left half the CUs idle; pop 2 and the
 #                            C = 32 stage are slower with half bands: profiles/r3_half_bands_ab.log)
@@ -1042,13 +1043,16 @@ class _StepPlan:
         self._keep(a)
 
     def _conv_bwd_fused(self, ci, dy, dz_out, x, mode_dy, dy2=None, dy_bn=None, x_bn=None, res=None, ident_x=False,
-                        dy3=None, dy_out=None):
+                        dy3=None, dy_out=None, chain_bn=None, chain_h=None):
         """dgrad + wgrad of a stride-1 3x3 C->C conv in one launch (see conv_bwd_fused_kernel).
 
         ``mode_dy`` 3: dY = BN-backward(dy, dy2) + dy3 (the previous block's BN1 backward and the identity
         shortcut folded into the staging); ``dy_out`` materialises that dY (needed downstream).  The dW slabs
         of the PREVIOUS fused launch are reduced by trailing workgroups of this one when small enough
-        (``_piggyback``); the rest by a standalone dw_slab_reduce."""
+        (``_piggyback``); the rest by a standalone dw_slab_reduce.
+        ``chain_bn`` / ``chain_h`` (v1 conv_a, identity mask): the epilogue also takes the backward sums of BN
+        ``chain_bn`` whose input is ``chain_h`` -- sum(dz), sum(dz * x-hat) of the output gradient this launch
+        produces (EPI bit 8), instead of a standalone bn_bwd_reduce pass over it."""
         be, L = self.be, self.be.L
         c = L.prog.convs[ci]
         assert c.stride == 1 and c.k == 3 and c.cin == c.cout
@@ -1084,6 +1088,12 @@ class _StepPlan:
             a.ep_gamma, a.ep_beta = self._bn(x_bn)
             a.st_ep = _p(be.st_f(x_bn))
             a.st_out = _p(be.st_b(x_bn))
+        if chain_bn is not None:
+            assert ident_x and mode_dy == 2 and tuple(chain_h.shape) == (self.N, H, H, C)
+            a.x3 = _p(chain_h)
+            a.ep_gamma, a.ep_beta = self._bn(chain_bn)
+            a.st_ep = _p(self._st_r(chain_bn))
+            a.st_out = _p(be.st_b(chain_bn))
         a.Hi, a.Wi, a.Ho, a.Wo, a.rows = H, H, H, H, rows
         tsz = ((rows + 2) * _wpitch(C) * _cpad(C) + 8 + 63) // 64 * 64
         raw = C >= 64  # must match conv.hip RAWX
@@ -1108,7 +1118,7 @@ class _StepPlan:
         else:
             a.slab = _p(self._slab(self._slab_floats())[self._slab_flip])
             self._slab_flip ^= 1
-        epi = int(res is not None) | (2 if ident_x else 0)
+        epi = int(res is not None) | (2 if ident_x else 0) | (8 if chain_bn is not None else 0)
         a.cin_real = self._stamp_row("fused", "fused C=%d mdy=%d epi=%d" % (C, mode_dy, epi))
         self._add(lib.dtf_conv_bwd_fused, ctypes.byref(a), C, mode_dy, epi, work.shape[0] + n_red, lds)
         self._keep(a)
@@ -1702,6 +1712,7 @@ class _StepPlan:
         d = self.tmp[hwL]["g"][0]
         self._add(lib.dtf_head_bwd_apply, _p(self.xs[-1]), _p(self.dfeat), _p(d), _p(self.img_slot), _p(e.state),
                   e.S, -1, -1, _p(be.stats), _p(be.stats), _p(self.cnt), hw, cfg.final_size, N)
+        chained = set()  # blocks whose BN_b backward sums the next block's conv_a epilogue already took
         for i in range(len(prog.blocks) - 1, -1, -1):
             blk = prog.blocks[i]
             bna, bnb = blk.bns
@@ -1710,8 +1721,9 @@ class _StepPlan:
             Hi, Ho = x.shape[1], ha.shape[1]
             T, Tin = self.tmp[Ho], self.tmp[Hi]
             hp = self.scs[i]
-            self._bn_ew(lib.dtf_bn_bwd_reduce, (Ho * Ho, ha.shape[3]), bnb, hb,
-                        bn2=blk.proj_bn if hp is not None else None, h2=hp, d=d)
+            if i not in chained:
+                self._bn_ew(lib.dtf_bn_bwd_reduce, (Ho * Ho, ha.shape[3]), bnb, hb,
+                            bn2=blk.proj_bn if hp is not None else None, h2=hp, d=d)
             # conv_b: dy = BN_b-backward(d, hb); dz_a = dgrad masked by BN_a(ha) + BN_a reductions; dW_b
             self._conv_bwd_fused(cb, d, T["dz2"], ha, mode_dy=2, dy2=hb, dy_bn=bnb, x_bn=bna)
             res = d
@@ -1723,7 +1735,15 @@ class _StepPlan:
             d_next = Tin["g"][1] if d is Tin["g"][0] else Tin["g"][0]
             ca_spec = prog.convs[ca]
             if ca_spec.stride == 1 and ca_spec.cin == ca_spec.cout:
-                self._conv_bwd_fused(ca, T["dz2"], d_next, x, mode_dy=2, dy2=ha, dy_bn=bna, res=res, ident_x=True)
+                # d_next = dL/d(block i-1's pre-ReLU sum): block i-1's BN_b sums ride in this epilogue when that
+                # block has no projection BN (which would need a second x-hat) and the build is not deterministic
+                # (whose BN_b reduction is the per-image fixed-order pass)
+                chain = (i > 0 and prog.blocks[i - 1].proj is None and not self.be.det and V1_CHAIN_BN)
+                if chain:
+                    chained.add(i - 1)
+                self._conv_bwd_fused(ca, T["dz2"], d_next, x, mode_dy=2, dy2=ha, dy_bn=bna, res=res, ident_x=True,
+                                     chain_bn=prog.blocks[i - 1].bns[1] if chain else None,
+                                     chain_h=self.hb[i - 1] if chain else None)
             else:
                 self._conv_dgrad(ca, T["dz2"], d_next, Hi, mode=2, epi=1 | 4, dy2=ha, in_bn=bna, res=res, xm=x)
                 self._conv_wgrad(ca, x, T["dz2"], mode_x=0, mode_dy=2, dy_bn=bna, dy2=ha)

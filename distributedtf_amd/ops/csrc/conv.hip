@@ -1539,8 +1539,11 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
   // prologue loads in the order they are consumed: BN statistics (dY transform, x BN) -> tiles -> weights
   CoefLd<MODE_DY == 0 ? 0 : 2> cld;
   coef_issue<C, MODE_DY == 0 ? 0 : 2>(cld, k_params, k_p_mstride, slot, k_st_in, k_st_in_b, k_in_gamma, k_in_beta);
+  // EPI bit 8 (v1 chain): the statistics' x-hat comes from x3 = the BN input h of the NEXT BN in the backward (the
+  // previous block's BN_b), normalised with that BN's batch statistics (st_ep); the mask stays the identity BN
+  static_assert(!(EPI & 8) || ((EPI & 2) && MODE_DY != 3 && ROLE != 2), "EPI 8: identity mask, x3 free, dgrad");
   CoefLd<1> cle;
-  if constexpr (!(EPI & 2))
+  if constexpr (!(EPI & 2) || (EPI & 8))
     coef_issue<C, 1>(cle, k_params, k_p_mstride, slot, k_st_ep, nullptr, k_ep_gamma, k_ep_beta);
   const float n_hw = k_cnt[slot] * (float)(H * W);
   STAMP_FINE(9);
@@ -1580,6 +1583,8 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
         coef_moments<1>(cle, n_hw, mean, inv);
         scale = cle.g * inv;
         shift = cle.b - mean * scale;
+      } else if constexpr ((EPI & 8) != 0) {
+        coef_moments<1>(cle, n_hw, mean, inv);  // x-hat of x3 only; the mask keeps scale 1, shift 0
       }
       ecoef[c] = scale;
       ecoef[64 + c] = shift;
@@ -1627,13 +1632,14 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
     for (int m = 0; m < MT; ++m) wacc[j][m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
   f32x2_t ssum[2] = {{0.f, 0.f}, {0.f, 0.f}}, ssq[2] = {{0.f, 0.f}, {0.f, 0.f}};
   // dgrad epilogue operands from global memory one iteration ahead (software-pipelined)
-  uint2 nres[MTD], nxres[MTD];
+  uint2 nres[MTD], nxres[MTD], nhres[MTD];
   auto epi_load = [&](int it_) {
     const long b_ = (long)(it_ / BANDS) * IMG + (it_ % BANDS) * ROWS * ROW;
 #pragma unroll
     for (int i = 0; i < MTD; ++i) {
       if constexpr (EPI & 1) nres[i] = *reinterpret_cast<const uint2*>(k_res + b_ + pofs[i]);
       if constexpr (!RAWX) nxres[i] = *reinterpret_cast<const uint2*>(k_xm + b_ + pofs[i]);
+      if constexpr ((EPI & 8) != 0) nhres[i] = *reinterpret_cast<const uint2*>(k_x3 + b_ + pofs[i]);
     }
   };
   if constexpr (DG) epi_load(it0);
@@ -1655,11 +1661,12 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
     const bool more = k + 1 < nit;
     const long band = (long)img * IMG + r0 * ROW;
     // epilogue operands before the prefetch (counted vmcnt)
-    uint2 rres[MTD], xres[MTD];
+    uint2 rres[MTD], xres[MTD], hres[MTD];
     if constexpr (DG) {
 #pragma unroll
     for (int i = 0; i < MTD; ++i) {
       if constexpr (EPI & 1) rres[i] = nres[i];
+      if constexpr ((EPI & 8) != 0) hres[i] = nhres[i];
       if constexpr (RAWX)
         xres[i] = *reinterpret_cast<const uint2*>(FXRAW(k) + rpo[i]);
       else
@@ -1707,8 +1714,13 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
       const f32x2_t dz0 = unpk2(pk.x), dz1 = unpk2(pk.y);
       ssum[0] += dz0;
       ssum[1] += dz1;
-      ssq[0] += dz0 * (x0 * iv0 + nm0);
-      ssq[1] += dz1 * (x1 * iv1 + nm1);
+      if constexpr ((EPI & 8) != 0) {  // x-hat of the chained BN's input x3
+        ssq[0] += dz0 * (unpk2(hres[i].x) * iv0 + nm0);
+        ssq[1] += dz1 * (unpk2(hres[i].y) * iv1 + nm1);
+      } else {
+        ssq[0] += dz0 * (x0 * iv0 + nm0);
+        ssq[1] += dz1 * (x1 * iv1 + nm1);
+      }
     }
     }
     // ---- wgrad
@@ -1757,7 +1769,7 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
     reduce_stats_to_lds(acc_lds, s4, q4, ci0, lane);
     __syncthreads();
   }
-  if constexpr (DG && !(EPI & 2)) flush_stats_r(k_st_out, acc_lds, slot, C, bid);
+  if constexpr (DG && (!(EPI & 2) || (EPI & 8))) flush_stats_r(k_st_out, acc_lds, slot, C, bid);
   STAMP(4);
   if constexpr (!WG) {
     STAMP_DRAIN(5);
@@ -2169,6 +2181,9 @@ DTF_API int dtf_conv_bwd_fused(const ConvArgs* args, int c, int mode_dy, int epi
   FUSED_CASE(16, 2, 3)  // v1 conv_a: identity-BN block input (+ shortcut grad)
   FUSED_CASE(32, 2, 3)
   FUSED_CASE(64, 2, 3)
+  FUSED_CASE(16, 2, 11)  // v1 conv_a + the previous block's BN_b backward sums (x-hat of x3) in the epilogue
+  FUSED_CASE(32, 2, 11)
+  FUSED_CASE(64, 2, 11)
   return -1;
 }
 

@@ -246,7 +246,10 @@ def main():
                        "exploits_timed": exploits[0],
                        "p2p_preconnected": preconnected() if world > 1 else None,
                        "untimed_warmup_exploit": bool(warm_exploit),
-                       "step_graph": graph_state(eng.backend)},
+                       "step_graph": graph_state(eng.backend),
+                       # persistent forward segments whose grid barrier timed out (must be 0; see hip_resnet)
+                       "persist_barrier_failures": (eng.backend.persist_failures()
+                                                    if hasattr(eng.backend, "persist_failures") else None)},
             "exploit_ms_mean": round(1000.0 * sum(exploit_s) / len(exploit_s), 3) if exploit_s else None,
             "exploit_readback_wait_ms_mean": (round(1000.0 * sum(exploit_wait_s) / len(exploit_wait_s), 3)
                                               if exploit_wait_s else None),

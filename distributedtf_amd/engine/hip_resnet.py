@@ -70,7 +70,12 @@ DEFER_MID_POP = 4         # up to this many members: defer the wgrad of DEFER_MI
 DEFER_MID_CS = (32, 64)
 DEFER_LARGE_CS = (64,)    # larger populations defer the wgrad of these channel widths only ...
 DEFER_LARGE_WG = {16: 16, 32: 8, 64: 8}  # ... with this many workgroups per member and layer
-V1_CHAIN_BN = os.environ.get("DTF_V1_CHAIN_BN", "1") == "1"  # v1: BN_b backward sums in the next conv_a epilogue
+V1_CHAIN_BN = os.environ.get("DTF_V1_CHAIN_BN", "1") == "1"
+# small populations: each stage's run of stride-1 forward convs in one persistent launch with a software grid
+# barrier between layers instead of a kernel boundary (conv_fwd_s1_persist_kernel); up to PERSIST_MAX_POP members
+PERSIST_FWD = os.environ.get("DTF_PERSIST_FWD", "0") == "1"
+PERSIST_MAX_POP = int(os.environ.get("DTF_PERSIST_MAX_POP", "2"))
+PERSIST_FENCE = int(os.environ.get("DTF_PERSIST_FENCE", "0"))  # conv.hip persist_barrier fence bits  # v1: BN_b backward sums in the next conv_a epilogue
 HALF_BANDS_MAX_IMGS = 128  # C = 64 stage (8x8): 4-row half-image bands for the forward / dgrad launches up to this many
 #                            images per step (one member: whole-image items left half the CUs idle; pop 2 and the
 #                            C = 32 stage are slower with half bands: profiles/r3_half_bands_ab.log)
@@ -155,6 +160,8 @@ def _register():
     ops.register("dtf_conv_bwd_dual", [P(ConvArgs), P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_bwd_dg", [P(ConvArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_conv_wgrad_all", [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p])
+    ops.register("dtf_conv_fwd_s1_persist", [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                                             c_void_p, c_int, c_int, c_void_p])
     ops.register("dtf_slab_reduce_all", [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_long, c_void_p])
     ops.register("dtf_slab_job_size", [])
     ops.register("dtf_dense_job_size", [])
@@ -469,6 +476,12 @@ class HipResNetBackend:
         self.use_graph = (os.environ.get("DTF_HIP_GRAPH", "1") == "1" and os.environ.get("DTF_DEBUG", "0") != "1")
 
     # --- engine hooks --------------------------------------------------------------
+    def persist_failures(self) -> int:
+        """Software grid barriers of the persistent forward segments that timed out (their step is wrong; 0 on a
+        healthy run: every workgroup of such a launch is co-resident by construction).  Reads the device."""
+        t = getattr(self, "persist_fail", None)
+        return 0 if t is None else int(t.item())
+
     def on_params_changed(self, slots):
         pass  # weight_prep runs at the start of every step (inside the graph)
 
@@ -732,6 +745,8 @@ class _StepPlan:
         # those layers runs afterwards in two wide launches (conv_wgrad_all_kernel: widths 64 + 32, width 16).
         # Their dY / x operands stay alive for the whole backward (per-block buffers instead of ping-pong ones).
         self.defer_wg = self.dual
+        self.persist_fwd = (PERSIST_FWD and dev.type == "cuda" and len(slots) <= PERSIST_MAX_POP
+                            and not self.be.det and not self.eval)
         self.overlap_wg = self.defer_wg and WG_OVERLAP and dev.type == "cuda"
         # channel widths whose stride-1 wgrad is deferred: every width at small populations; up to 4 members C = 32
         # and 64, at larger ones the C = 64 layers only (1 workgroup per CU of the fused kernel left the MFMA pipe
@@ -883,10 +898,53 @@ class _StepPlan:
         return b.gamma_off, b.beta_off
 
     def _add(self, fn, *args):
+        if getattr(self, "_pseg", None):
+            self._flush_pseg()  # a pending persistent forward segment precedes every other launch
         if getattr(self, "_grab", None) is not None:
             self._grab.append((fn, args))  # collected for a combined multi-role launch
             return
         self.launches.append((fn, args))
+
+    def _pseg_add(self, a, cin, mode, resid, rows, nwg, lds):
+        """Queue a conv_fwd_s1 launch into the pending persistent segment (same C / bands / workgroup count)."""
+        seg = getattr(self, "_pseg", None)
+        if seg and (seg[0][1], seg[0][4], seg[0][5]) != (cin, rows, nwg):
+            self._flush_pseg()
+            seg = None
+        if not seg:
+            self._pseg = seg = []
+        seg.append((a, cin, mode, resid, rows, nwg, lds))
+
+    def _flush_pseg(self):
+        """Emit the pending segment: one persistent launch (2+ layers whose workgroups are all co-resident), else
+        the ordinary per-layer launches."""
+        seg, self._pseg = self._pseg, None
+        lib = ops.lib()
+        if not seg:
+            return
+        cin, rows, nwg = seg[0][1], seg[0][4], seg[0][5]
+        lds = max(t[6] for t in seg)
+        be = self.be
+        if len(seg) >= 2:
+            if getattr(be, "persist_bar", None) is None:
+                be.persist_bar = torch.zeros(64 + 1024, dtype=torch.int32, device=be.dev)  # [0] gen, [64+b] flags
+                be.persist_fail = torch.zeros(1, dtype=torch.int32, device=be.dev)
+            arr = (ConvArgs * len(seg))(*[t[0] for t in seg])
+            tbl = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(be.dev)
+            kinds = torch.tensor([0 if t[2] == 0 else (2 if t[3] else 1) for t in seg], dtype=torch.int32,
+                                 device=be.dev)
+            ok = lib.dtf_conv_fwd_s1_persist(_p(tbl), _p(kinds), len(seg), cin, rows, nwg, lds, _p(be.persist_bar),
+                                             _p(be.persist_fail), PERSIST_FENCE, 1, None)
+            if ok == 1 and nwg <= 1024 and all(t[2] != 0 or rows == 8 for t in seg):
+                self._keep(tbl)
+                self._keep(kinds)
+                self.launches.append((lib.dtf_conv_fwd_s1_persist,
+                                      (_p(tbl), _p(kinds), len(seg), cin, rows, nwg, lds, _p(be.persist_bar),
+                                       _p(be.persist_fail), PERSIST_FENCE, 0)))
+                self.persist_segments = getattr(self, "persist_segments", 0) + 1
+                return
+        for a, cin, mode, resid, rows, nwg, lds in seg:
+            self.launches.append((lib.dtf_conv_fwd_s1, (ctypes.byref(a), cin, mode, int(resid), rows, nwg, lds)))
 
     def _conv_fwd(self, ci, x, y, stats_bn, in_bn, res=None):
         be, L = self.be, self.be.L
@@ -930,7 +988,11 @@ class _StepPlan:
             self._set_uniform(a, work)
             a.cin_real = self._stamp_row("fwd", "fwd_s1 C=%d in=%d res=%d" % (cin, mode, res is not None))  # launch ordinal for DTF_STAMP diagnostic builds (unused otherwise)
             lds = 1280 + 2 * ((rows_in * _wpitch(cin) * _cpad_fwd(cin) + 8 + 63) // 64 * 64) * 2
-            self._add(lib.dtf_conv_fwd_s1, ctypes.byref(a), cin, mode, int(res is not None), rows, work.shape[0], lds)
+            if self.persist_fwd and getattr(self, "_grab", None) is None:
+                self._pseg_add(a, cin, mode, res is not None, rows, work.shape[0], lds)
+            else:
+                self._add(lib.dtf_conv_fwd_s1, ctypes.byref(a), cin, mode, int(res is not None), rows,
+                          work.shape[0], lds)
         else:
             self._add(lib.dtf_conv_fwd, ctypes.byref(a), cin, c.cout, c.stride, c.k, mode, int(res is not None),
                       int(stats_bn is not None), work.shape[0], lds)

@@ -862,7 +862,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvArgs a) {
 // (same scheme as conv_bwd_fused_kernel).
 // single member's 8x8 C = 64 layer (one image per item) launches 256 workgroups instead of 128.
 template <int C, int MODE_IN, bool RESID, int ROWS = 8>
-__global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
+__device__ __forceinline__ void conv_fwd_s1_body(const ConvArgs& a, const int bid, char* smem) {
   constexpr int W = 512 / C, H = W, BANDS = H / ROWS;
   constexpr int NT = C / 16, WPT = 4 / NT;  // NT: output-channel tiles
   constexpr int KTOT = 9 * C, KS = (KTOT + 31) / 32;
@@ -875,7 +875,6 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
   using St = Stage<C, RT, W, H, CP, WP>;
   constexpr int MAXC = St::MAXC;
   constexpr int LMODE = MODE_IN == 0 ? 0 : 1;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   float* coef = reinterpret_cast<float*>(smem);  // 192 floats
   float* acc_lds = coef + 192;                   // 128 floats
   bf16_t* tile0 = reinterpret_cast<bf16_t*>(smem + 1280);
@@ -892,10 +891,10 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
   kpin(cnt), kpin(p_mstride), kpin(w_mstride), kpin(w_off), kpin(xin), kpin(wgt), kpin(res);
   int4 wk;
   if (u_items > 0) {
-    const int b = (int)blockIdx.x, m = b / u_items, k = b - m * u_items, it0_ = k * u_chunk;
+    const int b = bid, m = b / u_items, k = b - m * u_items, it0_ = k * u_chunk;
     wk = make_int4(m * u_per + it0_, min(u_chunk, u_per - it0_), 0, m);
   } else {
-    wk = work[blockIdx.x];
+    wk = work[bid];
     wk = make_int4(__builtin_amdgcn_readfirstlane(wk.x), __builtin_amdgcn_readfirstlane(wk.y),
                    __builtin_amdgcn_readfirstlane(wk.z), __builtin_amdgcn_readfirstlane(wk.w));  // uniform (SGPRs)
   }
@@ -1009,9 +1008,91 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
   const float q4[4] = {ssq[0].x, ssq[0].y, ssq[1].x, ssq[1].y};
   reduce_stats_to_lds(acc_lds, s4, q4, co0, lane);
   __syncthreads();
-  flush_stats(a.st_out, acc_lds, slot, C);
+  flush_stats_r(a.st_out, acc_lds, slot, C, bid);
   STAMP_DRAIN(4);
   STAMP_FLUSH(a.cin_real, nit);
+}
+
+template <int C, int MODE_IN, bool RESID, int ROWS = 8>
+__global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  conv_fwd_s1_body<C, MODE_IN, RESID, ROWS>(a, (int)blockIdx.x, smem);
+}
+
+// ------------------------------------------------------------------ persistent forward segment (small populations)
+// A run of conv_fwd_s1 layers of one stage (stem / conv_a / conv_b, the same C and band geometry and the same
+// workgroup count) in ONE launch: each workgroup runs its work item of layer l, then a software grid barrier
+// replaces the kernel boundary before layer l + 1 (whose BatchNorm prologue needs layer l's complete statistics).
+// The barrier: release fence (this workgroup's activation stores / statistic atomics visible at agent scope), one
+// arrival atomic on a flat counter, the last arriver resets it and bumps the generation word the others spin on
+// (bounded: a barrier that does not complete within ~50 ms counts a failure and ends the kernel -- the step's
+// result is then wrong and the host reports it -- instead of hanging the GPU), acquire fence (drops this XCD's
+// stale L2 lines of the next layer's inputs).  The host launches it only when every workgroup is co-resident
+// (occupancy check in dtf_conv_fwd_s1_persist).  kinds[l]: 0 stem (identity input), 1 BN+ReLU input, 2 + residual.
+// fence bits: 1 agent release (else only this wave's counters drained), 2 agent acquire (L2 invalidate).
+// bar[64 + b]: arrival counter of workgroup b (never reset; a workgroup's k-th barrier writes its k-th value).
+// Arrival is a store to the workgroup's own word (no single-address atomic: 512 serialised arrivals on one counter
+// measured ~8 us per barrier), and every workgroup's first wave polls all the words until each has reached this
+// barrier's value (no central release: one memory round trip less than a master that publishes a generation).
+// A workgroup can run ahead by at most one barrier, hence the wrap-safe ">=" test.
+__device__ __forceinline__ bool persist_barrier(unsigned* bar, unsigned nwg, unsigned* fail, int fence) {
+  __shared__ int ok;
+  __syncthreads();
+  const unsigned bid = blockIdx.x;
+  const int t = threadIdx.x;
+  if (t < 64) {
+    unsigned* flags = bar + 64;
+    const unsigned want = __hip_atomic_load(flags + bid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    if (t == 0) {
+      ok = 1;
+      // Release: activation stores are write-through (st_act8) and the statistics agent-scope atomics, so
+      // completing this workgroup's outstanding memory operations is enough (fence bit 1 adds the agent fence's L2
+      // write-back).  Acquire: every buffer a layer reads was first written inside this launch (distinct
+      // activation buffers per layer; statistics rows read only after their layer) and the L2 was clean at
+      // launch, so no stale line exists (fence bit 2 adds the agent acquire's L2 invalidate).
+      if (fence & 1)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      else
+        __builtin_amdgcn_s_waitcnt(0);
+      __hip_atomic_store(flags + bid, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    bool all = false;
+    for (int it = 0; it < (1 << 20) && !all; ++it) {
+      bool mine = true;
+      for (unsigned w = t; w < nwg; w += 64)
+        mine = mine && (int)(__hip_atomic_load(flags + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) >= 0;
+      all = __all(mine);
+      if (!all) __builtin_amdgcn_s_sleep(1);
+    }
+    if (t == 0) {
+      if (!all) {
+        ok = 0;
+        atomicAdd(fail, 1u);
+      }
+      if (fence & 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+  }
+  __syncthreads();
+  return ok != 0;
+}
+
+template <int C, int ROWS>
+__global__ __launch_bounds__(256) void conv_fwd_s1_persist_kernel(const ConvArgs* __restrict__ layers,
+                                                                  const int* __restrict__ kinds, int nlayers,
+                                                                  unsigned* bar, unsigned* fail, int fence) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int bid = (int)blockIdx.x;
+  for (int l = 0; l < nlayers; ++l) {
+    const int kind = kinds[l];
+    if (kind == 0) {
+      if constexpr (ROWS == 8) conv_fwd_s1_body<C, 0, false, ROWS>(layers[l], bid, smem);
+    } else if (kind == 1) {
+      conv_fwd_s1_body<C, 1, false, ROWS>(layers[l], bid, smem);
+    } else {
+      conv_fwd_s1_body<C, 1, true, ROWS>(layers[l], bid, smem);
+    }
+    if (l + 1 < nlayers && !persist_barrier(bar, gridDim.x, fail, fence)) return;
+  }
 }
 
 // ---------------------------------------------------------------------------------- dgrad
@@ -2036,6 +2117,31 @@ DTF_API int dtf_conv_fwd_s1(const ConvArgs* args, int c, int mode, int resid, in
   S1_CASE(64, 1, false)
   S1_CASE(64, 1, true)
 #undef S1_CASE
+  return -1;
+}
+
+// Persistent forward segment (conv_fwd_s1_persist_kernel): layers = device ConvArgs table, kinds[l] as above.
+// check_only: return 1 if nblocks workgroups of this instantiation are co-resident on the device (0 otherwise)
+// without launching.  Returns -3 (no launch) when they are not: the caller must not rely on the barrier then.
+DTF_API int dtf_conv_fwd_s1_persist(const ConvArgs* layers, const int* kinds, int nlayers, int c, int rows,
+                                    int nblocks, int lds, unsigned* bar, unsigned* fail, int fence,
+                                    int check_only, hipStream_t stream) {
+  if (nblocks <= 0 || nlayers <= 0) return 0;
+  DTF_HOST_CHECK(lds <= 160 * 1024);
+  auto go = [&](auto kern) -> int {
+    int per_cu = 0, dev = 0, ncu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds) != hipSuccess) return -3;
+    if (hipGetDevice(&dev) != hipSuccess) return -3;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -3;
+    if ((long)per_cu * ncu < nblocks) return check_only ? 0 : -3;
+    if (check_only) return 1;
+    hipLaunchKernelGGL(kern, dim3(nblocks), dim3(256), lds, stream, layers, kinds, nlayers, bar, fail, fence);
+    return DTF_CHECK_LAUNCH();
+  };
+  if (rows == 8 && c == 16) return go(conv_fwd_s1_persist_kernel<16, 8>);
+  if (rows == 8 && c == 32) return go(conv_fwd_s1_persist_kernel<32, 8>);
+  if (rows == 8 && c == 64) return go(conv_fwd_s1_persist_kernel<64, 8>);
+  if (rows == 4 && c == 64) return go(conv_fwd_s1_persist_kernel<64, 4>);
   return -1;
 }
 

@@ -170,6 +170,25 @@ def test_hip_step_benchmark_shapes(size, sizes, monkeypatch):
     print("worst per-layer relative error %.4f" % worst)
 
 
+@pytest.mark.parametrize("size,sizes,version", [(56, [128], 2), (20, [16, 24], 2), (14, [8, 12], 1)])
+def test_persistent_forward_segments(size, sizes, version, monkeypatch):
+    """Small populations run each stage's stride-1 forward convs in one persistent launch with a software grid
+    barrier between layers (hip_resnet PERSIST_FWD, conv_fwd_s1_persist_kernel): the graph-replayed step matches the
+    fp32 oracle per layer, the plan really holds persistent segments, and no barrier timed out."""
+    monkeypatch.setenv("DTF_HIP_GRAPH", "1")
+    from distributedtf_amd.engine import hip_resnet
+    monkeypatch.setattr(hip_resnet, "PERSIST_FWD", True)  # off by default (measured; BASELINE.md)
+    seen = {}
+
+    def check(hip, plans0):
+        seen["segments"] = sum(getattr(p, "persist_segments", 0) for p in hip.backend._plans.values())
+        seen["fail"] = hip.backend.persist_failures()
+
+    _compare_step(ResNetArch(cifar_config(size, version=version)), sizes, floor=0.04 if size == 56 else 0.06,
+                  check=check)
+    assert seen["segments"] >= 1 and seen["fail"] == 0, seen
+
+
 def test_hip_step_repeat_and_population_capacity():
     """Several graph replays with members on different optimizers stay finite and learn."""
     arch = ResNetArch(cifar_config(20))

@@ -70,12 +70,12 @@ DEFER_MID_POP = 4         # up to this many members: defer the wgrad of DEFER_MI
 DEFER_MID_CS = (32, 64)
 DEFER_LARGE_CS = (64,)    # larger populations defer the wgrad of these channel widths only ...
 DEFER_LARGE_WG = {16: 16, 32: 8, 64: 8}  # ... with this many workgroups per member and layer
-V1_CHAIN_BN = os.environ.get("DTF_V1_CHAIN_BN", "1") == "1"
+V1_CHAIN_BN = os.environ.get("DTF_V1_CHAIN_BN", "1") == "1"  # v1: BN_b backward sums in the next conv_a epilogue
 # small populations: each stage's run of stride-1 forward convs in one persistent launch with a software grid
 # barrier between layers instead of a kernel boundary (conv_fwd_s1_persist_kernel); up to PERSIST_MAX_POP members
 PERSIST_FWD = os.environ.get("DTF_PERSIST_FWD", "0") == "1"
 PERSIST_MAX_POP = int(os.environ.get("DTF_PERSIST_MAX_POP", "2"))
-PERSIST_FENCE = int(os.environ.get("DTF_PERSIST_FENCE", "0"))  # conv.hip persist_barrier fence bits  # v1: BN_b backward sums in the next conv_a epilogue
+PERSIST_FENCE = int(os.environ.get("DTF_PERSIST_FENCE", "0"))  # conv.hip persist_barrier fence bits
 HALF_BANDS_MAX_IMGS = 128  # C = 64 stage (8x8): 4-row half-image bands for the forward / dgrad launches up to this many
 #                            images per step (one member: whole-image items left half the CUs idle; pop 2 and the
 #                            C = 32 stage are slower with half bands: profiles/r3_half_bands_ab.log)
@@ -926,20 +926,23 @@ class _StepPlan:
         lds = max(t[6] for t in seg)
         be = self.be
         if len(seg) >= 2:
-            if getattr(be, "persist_bar", None) is None:
-                be.persist_bar = torch.zeros(64 + 1024, dtype=torch.int32, device=be.dev)  # [0] gen, [64+b] flags
+            if getattr(be, "persist_fail", None) is None:
                 be.persist_fail = torch.zeros(1, dtype=torch.int32, device=be.dev)
+            # this segment's own arrival-flag words (conv.hip persist_barrier: [64 + b]): every launch of the segment
+            # has the same workgroup count and barrier count, so its flags stay in lockstep across replays
+            bar = torch.zeros(64 + 1024, dtype=torch.int32, device=be.dev)
+            self._keep(bar)
             arr = (ConvArgs * len(seg))(*[t[0] for t in seg])
             tbl = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(be.dev)
             kinds = torch.tensor([0 if t[2] == 0 else (2 if t[3] else 1) for t in seg], dtype=torch.int32,
                                  device=be.dev)
-            ok = lib.dtf_conv_fwd_s1_persist(_p(tbl), _p(kinds), len(seg), cin, rows, nwg, lds, _p(be.persist_bar),
+            ok = lib.dtf_conv_fwd_s1_persist(_p(tbl), _p(kinds), len(seg), cin, rows, nwg, lds, _p(bar),
                                              _p(be.persist_fail), PERSIST_FENCE, 1, None)
             if ok == 1 and nwg <= 1024 and all(t[2] != 0 or rows == 8 for t in seg):
                 self._keep(tbl)
                 self._keep(kinds)
                 self.launches.append((lib.dtf_conv_fwd_s1_persist,
-                                      (_p(tbl), _p(kinds), len(seg), cin, rows, nwg, lds, _p(be.persist_bar),
+                                      (_p(tbl), _p(kinds), len(seg), cin, rows, nwg, lds, _p(bar),
                                        _p(be.persist_fail), PERSIST_FENCE, 0)))
                 self.persist_segments = getattr(self, "persist_segments", 0) + 1
                 return

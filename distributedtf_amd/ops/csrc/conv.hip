@@ -1030,48 +1030,60 @@ __global__ __launch_bounds__(256) void conv_fwd_s1_kernel(ConvArgs a) {
 // stale L2 lines of the next layer's inputs).  The host launches it only when every workgroup is co-resident
 // (occupancy check in dtf_conv_fwd_s1_persist).  kinds[l]: 0 stem (identity input), 1 BN+ReLU input, 2 + residual.
 // fence bits: 1 agent release (else only this wave's counters drained), 2 agent acquire (L2 invalidate).
-// bar[64 + b]: arrival counter of workgroup b (never reset; a workgroup's k-th barrier writes its k-th value).
-// Arrival is a store to the workgroup's own word (no single-address atomic: 512 serialised arrivals on one counter
-// measured ~8 us per barrier), and every workgroup's first wave polls all the words until each has reached this
-// barrier's value (no central release: one memory round trip less than a master that publishes a generation).
-// A workgroup can run ahead by at most one barrier, hence the wrap-safe ">=" test.
+// bar: [0] generation, [64 + b] arrival flag of workgroup b (generation-stamped: never reset; one bar array per
+// persistent segment).  Arrival is a store to the workgroup's own word -- a single arrival counter (512 serialised
+// same-address atomics) measured ~8 us per barrier; workgroup 0's first wave polls every flag, then publishes the
+// next generation, which the others poll.  (Every workgroup polling all flags itself instead measured slower:
+// profiles/r4_persist_ab.log.)
 __device__ __forceinline__ bool persist_barrier(unsigned* bar, unsigned nwg, unsigned* fail, int fence) {
   __shared__ int ok;
   __syncthreads();
   const unsigned bid = blockIdx.x;
   const int t = threadIdx.x;
-  if (t < 64) {
-    unsigned* flags = bar + 64;
-    const unsigned want = __hip_atomic_load(flags + bid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-    if (t == 0) {
-      ok = 1;
-      // Release: activation stores are write-through (st_act8) and the statistics agent-scope atomics, so
-      // completing this workgroup's outstanding memory operations is enough (fence bit 1 adds the agent fence's L2
-      // write-back).  Acquire: every buffer a layer reads was first written inside this launch (distinct
-      // activation buffers per layer; statistics rows read only after their layer) and the L2 was clean at
-      // launch, so no stale line exists (fence bit 2 adds the agent acquire's L2 invalidate).
-      if (fence & 1)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      else
-        __builtin_amdgcn_s_waitcnt(0);
-      __hip_atomic_store(flags + bid, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+  unsigned g = 0;
+  if (t < 64) g = __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t == 0) {
+    ok = 1;
+    // Release: activation stores are write-through (st_act8) and the statistics agent-scope atomics, so completing
+    // this workgroup's outstanding memory operations is enough (fence bit 1 adds the agent fence's L2 write-back).
+    // Acquire: every buffer a layer reads was first written inside this launch (distinct activation buffers per
+    // layer; statistics rows read only after their layer) and the L2 was clean at launch, so no stale line exists
+    // (fence bit 2 adds the agent acquire's L2 invalidate).
+    if (fence & 1)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    else
+      __builtin_amdgcn_s_waitcnt(0);
+    __hip_atomic_store(bar + 64 + bid, g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (bid == 0 && t < 64) {
     bool all = false;
     for (int it = 0; it < (1 << 20) && !all; ++it) {
       bool mine = true;
       for (unsigned w = t; w < nwg; w += 64)
-        mine = mine && (int)(__hip_atomic_load(flags + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) >= 0;
+        mine = mine && __hip_atomic_load(bar + 64 + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g + 1;
       all = __all(mine);
       if (!all) __builtin_amdgcn_s_sleep(1);
     }
     if (t == 0) {
-      if (!all) {
+      if (all) {
+        __hip_atomic_store(bar, g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
         ok = 0;
         atomicAdd(fail, 1u);
       }
-      if (fence & 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+  } else if (t == 0) {
+    bool done = false;
+    for (int it = 0; it < (1 << 20) && !done; ++it) {
+      done = __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != g;
+      if (!done) __builtin_amdgcn_s_sleep(1);
+    }
+    if (!done) {
+      ok = 0;
+      atomicAdd(fail, 1u);
     }
   }
+  if (t == 0 && (fence & 2)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   __syncthreads();
   return ok != 0;
 }

@@ -639,6 +639,7 @@ class _StepPlan:
         self.sizes = sizes
         self._wgen = []
         self.eval = bool(eval_mode)
+        self.persist_fwd = False  # (training plans of small populations may enable it below)
         dev = be.dev
         L = be.L
         prog = L.prog

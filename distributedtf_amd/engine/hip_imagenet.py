@@ -46,6 +46,8 @@ _CG_TP256 = True  # 256-pixel forward / dgrad tiles for 64-channel outputs
 _CG_WPK_WO64 = 32  # pixels per k-step of the 64-row tiles
 # stride-1 3x3 forward / data gradient with LDS-resident input rows (convg_t3_kernel): image width -> rows per tile
 _CG_T3 = {56: 8, 28: 7, 14: 14}  # must match dtf_convg_t3 (rows divide the image height)
+# convg_t3 forward: bit 0 = LDS-staged weights (the pre-round-4 form) instead of direct fragment loads (A/B switch)
+T3_FLAGS = int(os.environ.get("DTF_T3_FLAGS", "1"))  # direct: 81.61 vs staged 80.92 ms (profiles/r4_imagenet_t3_ab.log)
 _CG_WG_TARGET = 512
 _CG_WG_MINCHUNK = 2048
 
@@ -58,7 +60,7 @@ class CgArgs(ctypes.Structure):
         ("c_ep", c_void_p), ("st_out", c_void_p), ("work", c_void_p),
         ("Hi", c_int), ("Wi", c_int), ("Ci", c_int), ("Ho", c_int), ("Wo", c_int), ("Co", c_int),
         ("kh", c_int), ("kw", c_int), ("stride", c_int), ("pad", c_int), ("cmax", c_int), ("log2ci", c_int),
-        ("cin_real", c_int),
+        ("cin_real", c_int), ("flags", c_int),
     ]
 
 
@@ -444,6 +446,7 @@ class _ImageNetPlan:
         a.w_mstride = e.Pp
         a.grads, a.g_mstride = _p(be.acc_grads), e.Pp
         a.cmax = CMAX
+        a.flags = T3_FLAGS
         return a
 
     def cf(self, bn):  # forward coefficients of BN `bn` (eval: from the moving statistics, the plan's own buffer)

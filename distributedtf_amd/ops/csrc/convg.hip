@@ -78,6 +78,7 @@ struct CgArgs {
   int cmax;
   int log2ci;
   int cin_real;       // wgrad: real input channels of a channel-padded operand (stem: 3 of 8); 0 = Ci
+  int flags;          // convg_t3 forward: bit 0 keeps the LDS-staged weights (A/B of the direct fragment loads)
 };
 
 
@@ -526,19 +527,24 @@ __host__ __device__ constexpr int t3_nhalf() {
   return -1;
 }
 
+#ifndef T3_DIRECT_A
+#define T3_DIRECT_A 1  // forward t3: A fragments loaded directly from the weight rows (no LDS staging of A)
+#endif
 template <int TC, int EPI, bool AKM, int W, int R, int TP, int WRN>
 __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
   constexpr int BK = 32;
   constexpr int PW = TP / (4 / WRN), NTP = PW / 16, MT = TC / WRN / 16;
   static_assert(PW % 16 == 0 && TP >= R * W && W % R == 0, "pixel tile: whole rows, bands divide the image");
-  constexpr int RP = BK + 8;  // A row / staged-pixel pitch (bf16; +16 B)
+  constexpr int RP = BK + 16;  // A row / staged-pixel pitch (bf16; 96 B = 6 bank quads per pixel)
   constexpr int CPR = BK / 8, RPT = 256 / CPR;
   constexpr int KPA = TC + 8;
   constexpr int SA = (TC * RP > BK * KPA) ? TC * RP : BK * KPA;
-  // staged tile: RT rows x WS columns (halo), LDS row pitch WT = W + 16 pixels: a 16-pixel fragment that wraps to
-  // the next image row then shifts by 16 pixel pitches (80 B = 20 banks each, 5 x 16 = 0 mod 16 bank quads), so
-  // its 16 lanes still hit 16 distinct bank quads (with pitch W + 2 every wrapping fragment had 2-way conflicts)
-  constexpr int WS = W + 2, WT = W + 16, RT = R + 2, NBP = RT * WS;
+  // staged tile: RT rows x WS columns (halo), LDS row pitch WT = W + 8 pixels, pixel pitch 96 B: every B fragment
+  // read (ds_read_b128: its lane groups are {0-3,12-15,20-27}, {4-11,16-19,28-31}, .. -- pixel i with k-chunk j
+  // against pixels i' with chunk j + 1) hits 16 distinct bank quads for every tap offset and for fragments that
+  // wrap to the next image row (the former 80 B / W + 16 pitches were 2-way: 1,193-4,432 conflicts per wave,
+  // profiles/r3_pmc_imagenet_t3.txt; exhaustive check over tap offsets / fragment starts in tools/t3_bank_check.py)
+  constexpr int WS = W + 2, WT = W + 8, RT = R + 2, NBP = RT * WS;
   constexpr int NBC = NBP * CPR, MAXB = (NBC + 255) / 256;
   constexpr int SBT = RT * WT * RP + 8;  // + slack for the inactive staging slots
   constexpr int SOPS = 2 * SA + SBT;
@@ -621,6 +627,54 @@ __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
 #pragma unroll
     for (int n = 0; n < NTP; ++n) acc[m][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
   const int nch = Ci / BK, nk = 9 * nch;
+  // (the 64-channel 56-wide instance keeps LDS-staged A: its 28 accumulator tiles plus two fragment sets spill)
+  if (!AKM && T3_DIRECT_A && TC == 128 && !(a.flags & 1)) {
+    // Forward: A fragments straight from the OHWI weight rows (lane: row o, 8 consecutive channels of one tap = one
+    // 16-byte load) into registers one k-step ahead -- no LDS staging of A, so no barrier per k-step: the workgroup
+    // synchronises only when the next channel chunk's input rows replace the staged tile (every 9 k-steps)
+    uint4 rb[MAXB];
+    load_b(0, rb);
+    store_b(rb);
+    const int orow0 = o0 + wr * (TC / WRN) + (lane & 15);
+    const bf16_t* wl = wbase + (long)orow0 * 9 * Ci + 8 * (lane >> 4);
+    auto load_fa = [&](int c_, int t_, bf16x8_t (&f)[MT]) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        f[m] = __builtin_bit_cast(bf16x8_t, ld16(wl, (long)16 * m * 9 * Ci + t_ * Ci + c_ * BK, orow0 + 16 * m < a.Co));
+    };
+    bf16x8_t fa[MT], fan[MT];
+    load_fa(0, 0, fa);
+    __syncthreads();
+    int c = 0, t = 0;
+    for (int ks = 0; ks < nk; ++ks) {
+      const bool more = ks + 1 < nk;
+      if (more) load_fa(t == 8 ? c + 1 : c, t == 8 ? 0 : t + 1, fan);
+      if (t == 0 && c + 1 < nch) load_b(c + 1, rb);  // next chunk's rows: 9 k-steps of latency cover
+      const int tapo = ((t / 3) * WT + t % 3) * RP;
+      bf16x8_t fb[NTP];
+#pragma unroll
+      for (int n = 0; n < NTP; ++n) fb[n] = *reinterpret_cast<const bf16x8_t*>(sbt + bpo[n] + tapo);
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NTP; ++n) acc[m][n] = mfma16(fa[m], fb[n], acc[m][n]);
+      if (t == 8 && more) {  // chunk boundary: every wave is done with the staged rows
+        __syncthreads();
+        store_b(rb);
+        __syncthreads();
+      }
+#pragma unroll
+      for (int m = 0; m < MT; ++m) fa[m] = fan[m];
+      if (++t == 9) {
+        t = 0;
+        ++c;
+      }
+    }
+    __syncthreads();  // the epilogue reuses the operand LDS
+    convg_epilogue<TC, EPI, false, TP, WRN, NHALF>(a, acc, reinterpret_cast<float*>(smem_), acc_lds, slot, o0, p0,
+                                                   p1, 0, 0, 0, 0);
+    return;
+  }
   // A (weights) is prefetched one k-step ahead (a two-deep register ring, loop unrolled by two, measured the same:
   // profiles/r3_imagenet_t3_ab.log); the input rows of the next channel chunk a whole chunk (9 k-steps) ahead
   uint4 ra[AJ], rb[MAXB];

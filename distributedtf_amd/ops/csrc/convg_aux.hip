@@ -328,6 +328,9 @@ __global__ __launch_bounds__(256) void cg_maxpool_fwd_kernel(const bf16_t* __res
   }
 }
 
+__device__ uint4 g_mp_zero16 = {0u, 0u, 0u, 0u};  // what a masked-off candidate window reads (never written)
+__device__ uint2 g_mp_ff8 = {0xffffffffu, 0xffffffffu};  // ... and its argmax (matches no tap)
+
 __global__ __launch_bounds__(256) void cg_maxpool_bwd_kernel(const bf16_t* __restrict__ g, const uint8_t* __restrict__ am,
                                                               bf16_t* __restrict__ dx, int H, int W, int Ho, int Wo,
                                                               int C, long total8) {
@@ -339,21 +342,33 @@ __global__ __launch_bounds__(256) void cg_maxpool_bwd_kernel(const bf16_t* __res
     const int ix = (int)(pix - pr * W), iy = (int)(pr % (unsigned)H);
     const long img = pr / (unsigned)H;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    // windows containing iy: oy in {iy/2 - 1 .. iy/2} with 2*oy <= iy <= 2*oy + 2
-    for (int oy = (iy - 2 + 1) / 2; oy <= iy / 2; ++oy) {
-      if (oy < 0 || oy >= Ho || iy - 2 * oy > 2 || iy < 2 * oy) continue;
-      for (int ox = (ix - 2 + 1) / 2; ox <= ix / 2; ++ox) {
-        if (ox < 0 || ox >= Wo || ix - 2 * ox > 2 || ix < 2 * ox) continue;
-        const uint32_t t = (uint32_t)((iy - 2 * oy) * 3 + (ix - 2 * ox));
-        const long o = ((img * Ho + oy) * Wo + ox) * C + c0;
-        const uint2 av = *reinterpret_cast<const uint2*>(am + o);
-        const uint4 gv = *reinterpret_cast<const uint4*>(g + o);
-        const uint32_t g32[4] = {gv.x, gv.y, gv.z, gv.w};
+    // the (at most 2 x 2) windows containing (iy, ix): oy = iy / 2 (tap row iy % 2) and, for even iy >= 2,
+    // oy = iy / 2 - 1 (tap row 2); likewise in x.  All four candidates' loads are issued before any is used
+    // (branch-free: a missing window reads a zero vector / an argmax that matches no tap) -- the former loop
+    // issued one window's loads at a time (2.9 TB/s, profiles/r3_s2_imagenet_roofline.txt)
+    const int oyA = iy >> 1, oxA = ix >> 1;
+    const bool yA = oyA < Ho, xA = oxA < Wo, yB = !(iy & 1) && iy >= 2, xB = !(ix & 1) && ix >= 2;
+    const int oy_[2] = {oyA, oyA - 1}, ox_[2] = {oxA, oxA - 1};
+    const uint32_t ty_[2] = {(uint32_t)(iy & 1), 2u}, tx_[2] = {(uint32_t)(ix & 1), 2u};
+    const bool oky[2] = {yA, yB}, okx[2] = {xA, xB};
+    uint2 av[4];
+    uint4 gv[4];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const uint32_t ak = ((k < 4 ? av.x : av.y) >> (8 * (k & 3))) & 0xffu;
-          if (ak == t) acc[k] += bf2f((bf16_t)((g32[k >> 1] >> (16 * (k & 1))) & 0xffff));
-        }
+    for (int w = 0; w < 4; ++w) {
+      const int a_ = w >> 1, b_ = w & 1;
+      const bool ok = oky[a_] && okx[b_];
+      const long o = ok ? ((img * Ho + oy_[a_]) * Wo + ox_[b_]) * C + c0 : 0;
+      av[w] = *(ok ? reinterpret_cast<const uint2*>(am + o) : &g_mp_ff8);
+      gv[w] = *(ok ? reinterpret_cast<const uint4*>(g + o) : &g_mp_zero16);
+    }
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t t = ty_[w >> 1] * 3 + tx_[w & 1];
+      const uint32_t g32[4] = {gv[w].x, gv[w].y, gv[w].z, gv[w].w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t ak = ((k < 4 ? av[w].x : av[w].y) >> (8 * (k & 3))) & 0xffu;
+        if (ak == t) acc[k] += bf2f((bf16_t)((g32[k >> 1] >> (16 * (k & 1))) & 0xffff));
       }
     }
     *reinterpret_cast<uint4*>(dx + (long)pix * C + c0) = make_uint4(pack2bf(acc[0], acc[1]), pack2bf(acc[2], acc[3]),

@@ -47,6 +47,10 @@ _CG_WPK_WO64 = 32  # pixels per k-step of the 64-row tiles
 # stride-1 3x3 forward / data gradient with LDS-resident input rows (convg_t3_kernel): image width -> rows per tile
 _CG_T3 = {56: 8, 28: 7, 14: 14}  # must match dtf_convg_t3 (rows divide the image height)
 # convg_t3 forward: bit 0 = LDS-staged weights (the pre-round-4 form) instead of direct fragment loads (A/B switch)
+# Folded forward (v2 training): every BN+ReLU is applied while the consuming convolution -- and, in the backward, its
+# weight gradient -- stages its input (convg MODE 1, convg_t3 XF, convg_wgrad_wide MX 1), so no relu(BN(.)) tensor
+# (ax / a1 / a2) is materialised: 3 elementwise passes per block fewer
+CG_FOLD = os.environ.get("DTF_CG_FOLD", "0") == "1"
 T3_FLAGS = int(os.environ.get("DTF_T3_FLAGS", "1"))  # direct: 81.61 vs staged 80.92 ms (profiles/r4_imagenet_t3_ab.log)
 _CG_WG_TARGET = 512
 _CG_WG_MINCHUNK = 2048
@@ -106,9 +110,9 @@ def _register():
     P = ctypes.POINTER
     reg = ops.register
     reg("dtf_convg_fwd", [P(CgArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
-    reg("dtf_convg_t3", [P(CgArgs), c_int, c_int, c_int, c_int, c_int, c_void_p])
+    reg("dtf_convg_t3", [P(CgArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
     reg("dtf_convg_wgrad", [P(CgArgs), c_int, c_int, c_int, c_void_p])
-    reg("dtf_convg_wgrad_wide", [P(CgArgs), c_int, c_int, c_int, c_void_p])
+    reg("dtf_convg_wgrad_wide", [P(CgArgs), c_int, c_int, c_int, c_int, c_void_p])
     reg("dtf_cg_weight_prep", [c_void_p, c_long, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_long,
                                c_void_p])
     reg("dtf_cg_dense_prep", [c_void_p, c_long, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_long,
@@ -339,6 +343,8 @@ class _ImageNetPlan:
         # stages its operand measured slower, 114.7 -> 135.7 ms/step at pop 8 x 128: the transform is repeated for
         # every output-channel tile and its coefficient LDS costs occupancy; profiles/r2_imagenet_fold_ab.log)
         self.ax, self.a1, self.a2 = [], [], []
+        # folded forward (CG_FOLD): v2 training plans keep no relu(BN(.)) tensors
+        self.fold = CG_FOLD and not self.eval and not be.v1
         # v1 (post-activation): h3 = conv3 output (BN3 input), sc = raw projection output (BN_p input), a0 = the
         # stem's relu(BN(y0)); no ax (the block input IS a ReLU output)
         self.v1 = be.v1
@@ -351,10 +357,10 @@ class _ImageNetPlan:
             ho = hw // blk.stride
             self.h1.append(act("h1", hw, c1.cout))
             self.h2.append(act("h2", ho, c2.cout))
-            self.ax.append(act("ax", hw, cin) if not self.v1 else None)
+            self.ax.append(act("ax", hw, cin) if not (self.v1 or self.fold) else None)
             self.h3.append(act("h3", ho, c3.cout) if self.v1 else None)
-            self.a1.append(act("a1", hw, c1.cout))
-            self.a2.append(act("a2", ho, c2.cout))
+            self.a1.append(act("a1", hw, c1.cout) if not self.fold else None)
+            self.a2.append(act("a2", ho, c2.cout) if not self.fold else None)
             self.sc.append(act("sc", ho, c3.cout) if blk.proj is not None else None)
             self.xs.append(act("x", ho, c3.cout, bi + 1))
             self.geo.append((hw, ho, cin, c1.cout, c3.cout))
@@ -493,14 +499,14 @@ class _ImageNetPlan:
             trans = (1 if c.stride > 1 else 0) | 2  # | 2: A operand k-major from the forward layout
         a.log2ci = _log2(a.Ci)
         tc = 128 if a.Co >= 128 else 64
-        if (k == 3 and c.stride == 1 and mode == 0 and hw_in in _CG_T3 and ci != be.prog.stem
-                and epi == (6 if dgrad else 4) and a.Ci % 32 == 0):
+        if (k == 3 and c.stride == 1 and (mode == 0 or (mode == 1 and not dgrad)) and hw_in in _CG_T3
+                and ci != be.prog.stem and epi == (6 if dgrad else 4) and a.Ci % 32 == 0 and a.Ci <= 512):
             rows = _CG_T3[hw_in]
             tc = 64 if hw_in == 56 else 128  # must match dtf_convg_t3's instantiations
             work = self._band_work(hw_in, rows, a.Co, tc)
             a.work = _p(work)
             self._hold(a)
-            self._add(ops.lib().dtf_convg_t3, ctypes.byref(a), tc, epi, int(dgrad), hw_in, work.shape[0])
+            self._add(ops.lib().dtf_convg_t3, ctypes.byref(a), tc, epi, int(dgrad), hw_in, work.shape[0], mode)
             return
         # (a 256-row tile, 128 x 64 per wave, measured slower: 111.7 -> 123.4 ms/step at pop 8 x 128,
         # profiles/r2_imagenet_tc256_ab.log -- removed)
@@ -536,7 +542,7 @@ class _ImageNetPlan:
         wide3 = c.k == 3 and cin % 64 == 0
         wide1 = c.k == 1 and cin % 256 == 0 and _CG_WIDE1
         wide7 = ci == be.prog.stem and c.k == 7 and cin == 8 and c.cout == 64 and _CG_WIDE7
-        if _CG_WIDE and (wide3 or wide1 or wide7) and mode_x == 0 and mode_dy == 0:
+        if _CG_WIDE and (wide3 or wide1 or wide7) and mode_x in (0, 1) and mode_dy == 0 and not (wide7 and mode_x):
             # 64 / 128 x 288 (3x3), x 256 (1x1) or 64 x 416 (stem) tiles: 18 / 36, 16 / 32, 26 MFMAs per wave and
             # 32-pixel k-step (convg_wgrad_wide_kernel)
             wo = 128 if c.cout % 128 == 0 and _CG_WIDE128 else 64
@@ -544,7 +550,7 @@ class _ImageNetPlan:
             work = self._wgrad_work(hw_out, c.cout, K, wo, wt)
             a.work = _p(work)
             self._hold(a)
-            self._add(ops.lib().dtf_convg_wgrad_wide, ctypes.byref(a), wo, wt, work.shape[0])
+            self._add(ops.lib().dtf_convg_wgrad_wide, ctypes.byref(a), wo, wt, work.shape[0], mode_x)
             return
         wo = 64 if (c.cout % 128 != 0 and _CG_WO64) else 128  # 64-row tiles: no padded half for Co = 64
         work = self._wgrad_work(hw_out, c.cout, c.k * c.k * cin, wo)
@@ -614,6 +620,16 @@ class _ImageNetPlan:
             nxt = prog.blocks[i + 1].bns[0] if i + 1 < nblk else prog.final_bn
             res = self.sc[i] if blk.proj is not None else x
             self.bn_final(b1, hi, False)
+            if self.fold:
+                if blk.proj is not None:
+                    self.conv(blk.proj, x, self.sc[i], hi, mode=1, c_in=self.cf(b1), epi=0)
+                self.conv(c1, x, self.h1[i], hi, mode=1, c_in=self.cf(b1), epi=4, st=self.sf(b2))
+                self.bn_final(b2, hi, False)
+                self.conv(c2, self.h1[i], self.h2[i], hi, mode=1, c_in=self.cf(b2), epi=4, st=self.sf(b3))
+                self.bn_final(b3, ho, False)
+                self.conv(c3, self.h2[i], self.xs[i + 1], ho, mode=1, c_in=self.cf(b3), epi=5, res=res,
+                          st=self.sf(nxt))
+                continue
             self.ew(relu, x, self.ax[i], self.cf(b1), hi, cin)
             if blk.proj is not None:
                 self.conv(blk.proj, self.ax[i], self.sc[i], hi, mode=0, epi=0)
@@ -677,25 +693,28 @@ class _ImageNetPlan:
             self.bn_final(b3, ho, True)
             dh2 = self.tmp("dh2", ho, f)
             self.ew(bwd, h2, dh2, self.cb(b3), ho, f, dz=dz3)
-            self.wgrad(c3, self.a2[i], gcur, ho)
+            self.wgrad(c3, h2, gcur, ho, mode_x=1, c_x=self.cf(b3)) if self.fold else self.wgrad(c3, self.a2[i], gcur, ho)
             # conv2 (3x3 / s): dz2 = dgrad(dh2) masked by BN2(h1); dh1 = BN2-backward(dz2, h1)
             dz2 = self.tmp("dz2", hi, f)
             self.conv(c2, dh2, dz2, ho, mode=0, epi=6, xm=h1, c_ep=self.cf(b2), st=self.sb(b2), dgrad=True)
             self.bn_final(b2, hi, True)
             dh1 = self.tmp("dh1", hi, f)
             self.ew(bwd, h1, dh1, self.cb(b2), hi, f, dz=dz2)
-            self.wgrad(c2, self.a1[i], dh2, hi)
+            self.wgrad(c2, h1, dh2, hi, mode_x=1, c_x=self.cf(b2)) if self.fold else self.wgrad(c2, self.a1[i], dh2, hi)
             pd = None
             if blk.proj is not None:
                 pd = self.tmp("pd", hi, cin)
                 self.conv(blk.proj, gcur, pd, ho, mode=0, epi=0, dgrad=True)
-                self.wgrad(blk.proj, self.ax[i], gcur, hi)
+                if self.fold:
+                    self.wgrad(blk.proj, x, gcur, hi, mode_x=1, c_x=self.cf(b1))
+                else:
+                    self.wgrad(blk.proj, self.ax[i], gcur, hi)
             # conv1: dz1 = (dgrad(dh1) [+ projection dgrad]) masked by BN1(x); g_in = BN1-backward(dz1, x) [+ g]
             dz1 = self.tmp("dz1", hi, cin)
             self.conv(c1, dh1, dz1, hi, mode=0, epi=6 | (1 if pd is not None else 0), res=pd, xm=x,
                       c_ep=self.cf(b1), st=self.sb(b1), dgrad=True)
             self.bn_final(b1, hi, True)
-            self.wgrad(c1, self.ax[i], dh1, hi)
+            self.wgrad(c1, x, dh1, hi, mode_x=1, c_x=self.cf(b1)) if self.fold else self.wgrad(c1, self.ax[i], dh1, hi)
             gnext = self.tmp("gA" if (i % 2 == 0) else "gB", hi, cin)
             self.ew(bwd, x, gnext, self.cb(b1), hi, cin, dz=dz1, add=None if blk.proj is not None else gcur)
             gcur = gnext

@@ -55,6 +55,19 @@ __device__ __forceinline__ uint4 ld16(const bf16_t* base, long off, bool ok) {
   return __builtin_bit_cast(uint4, *p);
 }
 
+// relu(x * sc + sh) of 8 bf16 channels (BN + ReLU applied while an operand is staged: the folded forward)
+__device__ __forceinline__ uint4 bnrelu8(uint4 v, const float (&sc)[8], const float (&sh)[8]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t r[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float lo = fmaxf(__uint_as_float(w[q] << 16) * sc[2 * q] + sh[2 * q], 0.f);
+    const float hi = fmaxf(__uint_as_float(w[q] & 0xffff0000u) * sc[2 * q + 1] + sh[2 * q + 1], 0.f);
+    r[q] = pack2bf(lo, hi);
+  }
+  return make_uint4(r[0], r[1], r[2], r[3]);
+}
+
 struct CgArgs {
   const bf16_t* x;    // gathered operand (fwd: input activations; dgrad: output gradient; wgrad: input)
   const bf16_t* x2;   // second input of a BN-backward transform
@@ -530,7 +543,8 @@ __host__ __device__ constexpr int t3_nhalf() {
 #ifndef T3_DIRECT_A
 #define T3_DIRECT_A 1  // forward t3: A fragments loaded directly from the weight rows (no LDS staging of A)
 #endif
-template <int TC, int EPI, bool AKM, int W, int R, int TP, int WRN>
+// XF: the staged input rows get BN + ReLU (coefficients c_in: scale / shift of the input's BN) -- the folded forward
+template <int TC, int EPI, bool AKM, int W, int R, int TP, int WRN, bool XF = false>
 __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
   constexpr int BK = 32;
   constexpr int PW = TP / (4 / WRN), NTP = PW / 16, MT = TC / WRN / 16;
@@ -577,13 +591,39 @@ __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
     bg[j] = ok ? (gy * W + gx) * Ci + 8 * c8 : 0;
     bok |= (unsigned)ok << j;
   }
+  // XF: the input BN's scale / shift of every channel in LDS (Ci <= 512), read at staging time (held in registers
+  // across the 9 k-steps of a chunk they made the kernel spill)
+  __shared__ float xcf[XF ? 2 * 512 : 1];
+  if constexpr (XF) {
+    const float* cb = a.c_in + (long)slot * 4 * a.cmax;
+    for (int i = tid; i < Ci; i += 256) {
+      xcf[i] = cb[i];
+      xcf[512 + i] = cb[a.cmax + i];
+    }
+    __syncthreads();  // the first staging (before the k loop's first barrier) reads them
+  }
+  int cur_c = 0;  // XF: channel chunk of the rows last loaded by load_b
   auto load_b = [&](int c, uint4 (&v)[MAXB]) {
 #pragma unroll
     for (int j = 0; j < MAXB; ++j) v[j] = ld16(xb, bg[j] + c * BK, (bok >> j) & 1u);
+    cur_c = c;
   };
   auto store_b = [&](const uint4 (&v)[MAXB]) {
+    float sc[8], sh[8];
+    if constexpr (XF) {
+      const int c0 = cur_c * BK + 8 * (tid % CPR);  // the same 8 channels for every slot j of this thread
 #pragma unroll
-    for (int j = 0; j < MAXB; ++j) *reinterpret_cast<uint4*>(sbt + bl[j]) = v[j];
+      for (int k = 0; k < 8; ++k) {
+        sc[k] = xcf[c0 + k];
+        sh[k] = xcf[512 + c0 + k];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < MAXB; ++j) {
+      uint4 t = v[j];
+      if constexpr (XF) t = ((bok >> j) & 1u) ? bnrelu8(t, sc, sh) : make_uint4(0, 0, 0, 0);  // halo stays 0
+      *reinterpret_cast<uint4*>(sbt + bl[j]) = t;
+    }
   };
   // A (weights), one k-step = (chunk c, tap t)
   const bf16_t* wbase = a.w + (long)slot * a.w_mstride + a.w_off;
@@ -945,7 +985,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PK == 32 ? 
 // each B fragment for 4 instead of 2 MFMAs (the 64-row one is LDS-read-bound: 22 tr-reads per 18 MFMAs)
 // WWT: columns per tile, 288 (3x3 convs: K = 9 Ci), 256 (1x1 convs with Ci % 256 == 0) or 416 (the 7x7 stem:
 // 49 taps x 8 channels, one tile).
-template <int WWO, int WWT>
+// MX 1: x operand = relu(BN(x)) applied while staging (c_in scale / shift per channel, staged in LDS; the folded
+// forward keeps no materialised BN+ReLU output)
+template <int WWO, int WWT, int MX = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ? 3 : 2))) void convg_wgrad_wide_kernel(CgArgs a) {
   constexpr int WWOP = WWO + 8, MTW = WWO / 32, DJ = WWO / 64, WWP = WWT + 8;
   constexpr int WXC = 32 * (WWT / 8);  // x chunks (8 columns) per k-step
@@ -953,12 +995,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ?
   __shared__ __attribute__((aligned(16))) bf16_t sd[2][32 * WWOP];
   __shared__ __attribute__((aligned(16))) bf16_t sx[2][32 * WWP];
   __shared__ int4 pinfo[2][32];
+  extern __shared__ float xcoef[];  // MX 1: scale [Ci] | shift [Ci]
   const int4 wk = a.work[blockIdx.x];
   DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z >= wk.y);
   const int slot = wk.x, p0 = wk.y, p1 = wk.z, o0 = wk.w & 0xffff, n0 = (wk.w >> 16) * 8;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wr = wave & 1, wc = wave >> 1;
   const int Ci = a.Ci, Co = a.Co, K = a.kh * a.kw * Ci;
+  if constexpr (MX == 1) {
+    const float* cb = a.c_in + (long)slot * 4 * a.cmax;
+    for (int i = tid; i < Ci; i += 256) {
+      xcoef[i] = cb[i];
+      xcoef[Ci + i] = cb[a.cmax + i];
+    }
+  }
   const int HWo = a.Ho * a.Wo;
   const long img_x = (long)a.Hi * a.Wi * Ci;
   // dy: DJ 16-byte chunks per thread and k-step (row (tid + 256 j) / (WWO / 8), 8 channels)
@@ -1013,6 +1063,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ?
       pinfo[(pk0 - p0) / 32 & 1][tid] = inf;
     }
   };
+  bool xval[WXJ];  // MX 1: the chunk of xv holds real pixels (not padding)
   auto load = [&](int pk0, uint4 (&dv)[DJ], uint4 (&xv)[WXJ]) {
     const int par = (pk0 - p0) / 32 & 1;
 #pragma unroll
@@ -1024,16 +1075,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ?
     for (int j = 0; j < WXJ; ++j) {
       const int4 inf = pinfo[par][xrow[j] & 31];
       const int gy = inf.z + xky[j], gx = inf.w + xkx[j];
-      xv[j] = ld16(a.x, (long)(unsigned)inf.y + (unsigned)((gy * a.Wi + gx) * Ci + (xoff[j] >> 16)),
-                   xok[j] && inf.z > -(1 << 29) && gy >= 0 && gy < a.Hi && gx >= 0 && gx < a.Wi);
+      const bool ok = xok[j] && inf.z > -(1 << 29) && gy >= 0 && gy < a.Hi && gx >= 0 && gx < a.Wi;
+      xv[j] = ld16(a.x, (long)(unsigned)inf.y + (unsigned)((gy * a.Wi + gx) * Ci + (xoff[j] >> 16)), ok);
+      xval[j] = ok;
     }
   };
   auto store = [&](bf16_t* d, bf16_t* xx, const uint4 (&dv)[DJ], const uint4 (&xv)[WXJ]) {
 #pragma unroll
     for (int j = 0; j < DJ; ++j) *reinterpret_cast<uint4*>(d + drow[j] * WWOP + dch[j]) = dv[j];
 #pragma unroll
-    for (int j = 0; j < WXJ; ++j)
-      if (tid + 256 * j < WXC) *reinterpret_cast<uint4*>(xx + (xoff[j] & 0xffff)) = xv[j];
+    for (int j = 0; j < WXJ; ++j) {
+      if (tid + 256 * j >= WXC) continue;
+      uint4 t = xv[j];
+      if constexpr (MX == 1) {
+        // a padding / out-of-range chunk (loaded as zeros) must stay zero after the transform
+        float sc[8], sh[8];
+        const int c0 = xoff[j] >> 16;
+        const float4 s0 = *reinterpret_cast<const float4*>(xcoef + c0), s1 = *reinterpret_cast<const float4*>(xcoef + c0 + 4);
+        const float4 h0 = *reinterpret_cast<const float4*>(xcoef + Ci + c0),
+                     h1 = *reinterpret_cast<const float4*>(xcoef + Ci + c0 + 4);
+        sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+        sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w; sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
+        t = xval[j] ? bnrelu8(t, sc, sh) : make_uint4(0, 0, 0, 0);
+      }
+      *reinterpret_cast<uint4*>(xx + (xoff[j] & 0xffff)) = t;
+    }
   };
   constexpr int NTN = WWT / 2 / 16;  // 9 column tiles per wave
   f32x4_t acc[MTW][NTN];
@@ -1156,15 +1222,20 @@ DTF_API int dtf_convg_fwd(const CgArgs* a, int tc, int mode, int epi, int trans,
 // Stride-1 3x3 conv / data gradient with LDS-resident input rows (convg_t3_kernel).  w: image width (56: 8-row
 // tiles of 448 pixels, 64-channel tiles; 28: 7 rows, 14: whole 14-row images, 224-pixel tiles of 128 channels);
 // epi 4 (forward, statistics) or 6 (data gradient: mask + statistics, akm = 1).
-DTF_API int dtf_convg_t3(const CgArgs* a, int tc, int epi, int akm, int w, int nwork, hipStream_t stream) {
+// mode 1 (forward only): BN + ReLU of the input applied while its rows are staged (c_in), the folded forward
+DTF_API int dtf_convg_t3(const CgArgs* a, int tc, int epi, int akm, int w, int nwork, int mode, hipStream_t stream) {
   if (nwork <= 0) return 0;
   if (a->kh != 3 || a->kw != 3 || a->stride != 1 || a->pad != 1 || a->Wi != w || a->Hi != w || a->Ho != w ||
       a->Ci % 32 != 0 || (a->Co & 7) != 0)
     return -2;
   dim3 grid(nwork), block(256);
 #define T3_CASE(TC_, E_, AK_, W_, R_, TP_, WRN_)                                                              \
-  if (tc == TC_ && epi == E_ && akm == AK_ && w == W_) {                                                    \
+  if (tc == TC_ && epi == E_ && akm == AK_ && w == W_ && mode == 0) {                                       \
     hipLaunchKernelGGL((convg_t3_kernel<TC_, E_, AK_, W_, R_, TP_, WRN_>), grid, block, 0, stream, *a);     \
+    return DTF_CHECK_LAUNCH();                                                                              \
+  }                                                                                                         \
+  if (tc == TC_ && epi == E_ && akm == AK_ && w == W_ && mode == 1 && !AK_) {                               \
+    hipLaunchKernelGGL((convg_t3_kernel<TC_, E_, AK_, W_, R_, TP_, WRN_, !AK_>), grid, block, 0, stream, *a); \
     return DTF_CHECK_LAUNCH();                                                                              \
   }
 #define T3_GEO(E_, AK_) T3_CASE(64, E_, AK_, 56, 8, 448, 1) T3_CASE(128, E_, AK_, 28, 7, 224, 2) \
@@ -1206,24 +1277,29 @@ DTF_API int dtf_convg_wgrad(const CgArgs* a, int mode_x, int mode_dy, int nwork,
 
 // wide-column weight gradient with plain operands (work: (slot, p0, p1, o0 | n0/8 << 16)): wo x 288 tiles for 3x3
 // convs, wo x 256 for 1x1 convs with Ci % 256 == 0
-DTF_API int dtf_convg_wgrad_wide(const CgArgs* a, int wo, int wt, int nwork, hipStream_t stream) {
+// mode_x 1: x operand relu(BN(x)) applied while staging (c_in), 3x3 / 1x1 tiles only
+DTF_API int dtf_convg_wgrad_wide(const CgArgs* a, int wo, int wt, int nwork, int mode_x, hipStream_t stream) {
   if (nwork <= 0) return 0;
   const int K = a->kh * a->kw * a->Ci;
   if ((a->Ci & (a->Ci - 1)) != 0 || a->Ci < 8 || (a->Co & 7) != 0) return -2;
   if (wt != 416 && (a->Ci < 64 || K % wt != 0)) return -2;
-  if (wo == 128 && wt == 288)
-    hipLaunchKernelGGL((convg_wgrad_wide_kernel<128, 288>), dim3(nwork), dim3(256), 0, stream, *a);
-  else if (wo == 64 && wt == 288)
-    hipLaunchKernelGGL((convg_wgrad_wide_kernel<64, 288>), dim3(nwork), dim3(256), 0, stream, *a);
-  else if (wo == 128 && wt == 256)
-    hipLaunchKernelGGL((convg_wgrad_wide_kernel<128, 256>), dim3(nwork), dim3(256), 0, stream, *a);
-  else if (wo == 64 && wt == 256)
-    hipLaunchKernelGGL((convg_wgrad_wide_kernel<64, 256>), dim3(nwork), dim3(256), 0, stream, *a);
-  else if (wo == 64 && wt == 416)  // the 7x7 stem: 49 taps x 8 (3 real) channels in one tile
+  if (mode_x != 0 && (mode_x != 1 || wt == 416 || a->Ci > 4096)) return -2;
+  const size_t dyn = mode_x ? (size_t)2 * a->Ci * sizeof(float) : 0;
+#define WW_CASE(WO_, WT_)                                                                                     \
+  if (wo == WO_ && wt == WT_) {                                                                               \
+    if (mode_x)                                                                                               \
+      hipLaunchKernelGGL((convg_wgrad_wide_kernel<WO_, WT_, 1>), dim3(nwork), dim3(256), dyn, stream, *a);    \
+    else                                                                                                      \
+      hipLaunchKernelGGL((convg_wgrad_wide_kernel<WO_, WT_>), dim3(nwork), dim3(256), 0, stream, *a);         \
+    return DTF_CHECK_LAUNCH();                                                                                \
+  }
+  WW_CASE(128, 288) WW_CASE(64, 288) WW_CASE(128, 256) WW_CASE(64, 256)
+#undef WW_CASE
+  if (wo == 64 && wt == 416 && mode_x == 0) {  // the 7x7 stem: 49 taps x 8 (3 real) channels in one tile
     hipLaunchKernelGGL((convg_wgrad_wide_kernel<64, 416>), dim3(nwork), dim3(256), 0, stream, *a);
-  else
-    return -2;
-  return DTF_CHECK_LAUNCH();
+    return DTF_CHECK_LAUNCH();
+  }
+  return -2;
 }
 
 DTF_DEBUG_EXPORT(convg)

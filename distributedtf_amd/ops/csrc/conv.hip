@@ -2059,16 +2059,21 @@ __global__ __launch_bounds__(256) void slab_reduce_all_kernel(const SlabJob* __r
   for (int bx = blockIdx.x; bx * 32 < j.kel; bx += gridDim.x) {
     const int e = bx * 32 + el;
     const bool ok = e < j.kel;
-    float s0 = 0.f, s1 = 0.f;
+    // four slab loads in flight per thread and trip (the 2-deep chain left this latency-bound at small
+    // populations: 128 slabs per member of the standalone wgrad launches)
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
     int g = gg;
-    for (; g + 8 < rd.y; g += 16) {
-      if (ok) {
-        s0 += j.slab[(long)(rd.x + g) * j.kel + e];
-        s1 += j.slab[(long)(rd.x + g + 8) * j.kel + e];
-      }
+    const float* sp = j.slab + (long)rd.x * j.kel + (ok ? e : 0);
+    for (; g + 24 < rd.y; g += 32) {
+      const float a0 = sp[(long)g * j.kel], a1 = sp[(long)(g + 8) * j.kel], a2 = sp[(long)(g + 16) * j.kel],
+                  a3 = sp[(long)(g + 24) * j.kel];
+      s0 += a0;
+      s1 += a1;
+      s2 += a2;
+      s3 += a3;
     }
-    if (g < rd.y && ok) s0 += j.slab[(long)(rd.x + g) * j.kel + e];
-    part[gg * 33 + el] = s0 + s1;
+    for (; g < rd.y; g += 8) s0 += sp[(long)g * j.kel];
+    part[gg * 33 + el] = ok ? (s0 + s1) + (s2 + s3) : 0.f;
     __syncthreads();
     if (gg == 0 && ok) {
       float sum = 0.f;

@@ -48,15 +48,36 @@ DET_WG_PER_MEMBER = 64  # deterministic mode: statistic-producing launches use <
 DUAL_MAX_POP = 2          # dual (dgrad | wgrad role) backward launches up to this many members per GPU ...
 DUAL_CS = (32, 64)        # ... for these channel widths (C = 16 keeps the fused kernel)
 DUAL_WG = {16: 128, 32: 128, 64: 64}  # wgrad-role workgroups per member of a dual launch
-FWD_ITERS_PER_WG = 4      # forward: (image, band) iterations per workgroup (>= FWD_MIN_WG workgroups kept;
+FWD_ITERS_PER_WG = int(os.environ.get("DTF_FWD_ITERS", "4"))  # forward: (image, band) iterations per workgroup (>= FWD_MIN_WG workgroups kept;
 FWD_MIN_WG = 256          # 512 for up to DUAL_MAX_POP members: pop 1 1.059 -> 1.055, pop 2 1.427 -> 1.398 ms)
 FWD_MIN_WG_SMALL = 512
+FWD_RESIDENT = int(os.environ.get("DTF_FWD_RESIDENT", "0"))  # stride-1 forward: one round of resident workgroups
 HEAD_ITEMS = 512          # head / GAP+dense+CE work items
 WGRAD_WG_PER_MEMBER = 128  # standalone wgrad launches: workgroups per member (bounds the dW partial traffic)
 DENSE_REDUCE_BLOCKS = 256  # slab_reduce_all, dense jobs: max 32-element blocks per job
 FUSED_SLAB_BYTES = {16: 16e6, 32: 16e6, 64: 48e6}  # fused backward: per-launch dW slab budget -> workgroup count
 FUSED_MIN_WG = 256        # ... at least this many workgroups (one member would leave CUs idle otherwise)
 FUSED_MAX_WG = {32: 128}  # ... at most this many per member (C = 32: fewer, fuller workgroups)
+# ... and never a partial second round of workgroups: a count above the resident slots (CUs x WGs per CU of the
+# kernel's occupancy) is rounded down to a multiple of them (pop 8, C = 16: 1024 -> 768 workgroups of 6 bands
+# instead of 768 + a 256-workgroup tail at a third of the occupancy)
+FUSED_RESIDENT = int(os.environ.get("DTF_FUSED_RESIDENT", "1"))
+FUSED_ROUNDS = int(os.environ.get("DTF_FUSED_ROUNDS", "1"))  # > 0: at most this many rounds of resident workgroups
+N_CU = None  # compute units: the device's (256 on MI355X; 256 without a GPU)
+
+
+def _n_cu():
+    global N_CU
+    if N_CU is None:
+        N_CU = 256
+        if torch.cuda.is_available():
+            N_CU = max(1, torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count)
+    return N_CU
+
+
+def _fused_wgs_per_cu(C, mode_dy):
+    """Workgroups per CU of conv_bwd_fused_kernel<C, mode_dy> (conv.hip FUSED_WAVES, 4 waves per workgroup)."""
+    return 3 if C <= 16 and mode_dy != 3 else 2 if C <= 32 else 1
 PIGGYBACK_MAX_WG = 3000   # slab reductions ride on the next backward launch when they add <= this many workgroups
 DEFER_WG = {16: 64, 32: 32, 64: 16}  # deferred wgrad (small populations): workgroups per member and layer
 # deferred wgrad launches issued on a side stream (a parallel branch of the step graph) as soon as a stage's layers
@@ -971,6 +992,9 @@ class _StepPlan:
         lo = FWD_MIN_WG_SMALL if len(self.slots) <= DUAL_MAX_POP else FWD_MIN_WG
         n_wg = self._n_wg_iters(self.N * bands, per_wg=FWD_ITERS_PER_WG, lo=lo,
                                 hi=max(1024, self.N * bands // FWD_ITERS_PER_WG))
+        if FWD_RESIDENT and s1 and len(self.slots) > DUAL_MAX_POP:
+            # conv_fwd_s1_kernel occupancy: 4 WGs / CU (C <= 32), 3 (C = 64)
+            n_wg = self._det_cap(min(self.N * bands, _n_cu() * (4 if cin <= 32 else 3)))
         work = self._work_iters(bands, n_wg)
         a = self._base_args()
         a.x, a.y, a.res = _p(x), _p(y), _p(res)
@@ -1137,7 +1161,7 @@ class _StepPlan:
         if (self.dual and (C in DUAL_CS or self.defer_wg)) or C in self.defer_cs:
             return self._conv_bwd_dual(ci, c, C, H, rows, bands, dy, dz_out, x, mode_dy, dy2, dy_bn, x_bn, res,
                                        ident_x, dy3, dy_out)
-        n_wg = self._fused_nwg(C, bands)
+        n_wg = self._fused_nwg(C, bands, mode_dy)
         work = self._work_iters(bands, n_wg)
         a = self._base_args()
         a.x, a.x2, a.y, a.xm, a.res = _p(dy), _p(dy2), _p(dz_out), _p(x), _p(res)
@@ -1163,8 +1187,7 @@ class _StepPlan:
         a.Hi, a.Wi, a.Ho, a.Wo, a.rows = H, H, H, H, rows
         tsz = ((rows + 2) * _wpitch(C) * _cpad(C) + 8 + 63) // 64 * 64
         raw = C >= 64  # must match conv.hip RAWX
-        sb = C == 16 and mode_dy != 3  # must match conv.hip SB
-        nbuf = 2 if sb else 4
+        nbuf = 4  # double-buffered size even when conv.hip single-buffers (SB): C = 16 still fits 3 WGs per CU
         lds = 2304 + (nbuf * tsz + (2 * rows * H * _cpad(C) if raw else 0)) * 2  # dY/X tiles [+ raw-x interiors]
         lib = ops.lib()
         # dW partials: per-workgroup slabs.  C = 64: every layer its own slab, all reduced by ONE launch after the
@@ -1397,7 +1420,7 @@ class _StepPlan:
     def _slab_elems(C):
         return ((9 * C // 16 + 3) // 4) * (C // 16) * 4 * 256
 
-    def _fused_nwg(self, C, bands):
+    def _fused_nwg(self, C, bands, mode_dy=0):
         # per-launch budget for the dW partials (bytes of slab stores, or of atomics without slabs): bounds the
         # workgroup count of the fused kernel
         wn = 9 * C * C
@@ -1409,7 +1432,13 @@ class _StepPlan:
         # each): pop 1 1.52 -> 1.44-1.47 ms/step over two runs (profiles/r1_s7_variants.log); pop >= 2 unchanged
         if C in FUSED_MAX_WG:
             n_wg = min(n_wg, FUSED_MAX_WG[C] * len(self.slots))
-        return self._det_cap(min(n_wg, self.N * bands))
+        n_wg = min(n_wg, self.N * bands)
+        res = _n_cu() * _fused_wgs_per_cu(C, mode_dy)
+        if FUSED_RESIDENT and n_wg > res:
+            n_wg = n_wg // res * res
+            if FUSED_ROUNDS > 0:
+                n_wg = min(n_wg, FUSED_ROUNDS * res)
+        return self._det_cap(n_wg)
 
     def _slab_floats(self):
         cfg = self.be.L.cfg
@@ -1418,7 +1447,7 @@ class _StepPlan:
             C = cfg.num_filters * (2 ** st)
             H = cfg.image_size >> st
             if C in (16, 32, 64) and H == 512 // C:
-                need = max(need, self._fused_nwg(C, H // 8) * self._slab_elems(C))
+                need = max(need, max(self._fused_nwg(C, H // 8, m) for m in (0, 3)) * self._slab_elems(C))
         return need
 
     def _head_slab(self, ha, hwork):

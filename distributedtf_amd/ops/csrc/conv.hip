@@ -27,6 +27,9 @@
 
 #define BN_EPS 1e-5f
 // min waves / SIMD the fused backward kernel is register-capped for (C = 16 single-buffered: 3 WGs / CU)
+#ifndef DTF_FUSED_SB16
+#define DTF_FUSED_SB16 0  // (host allocates the double-buffered size either way: 3 x 46 KB fits the 160 KB LDS)
+#endif
 #define FUSED_WAVES(C, M) ((C) <= 16 && (M) != 3 ? 3 : (C) <= 32 ? 2 : 1)
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 #define NREP DTF_NREP
@@ -1571,7 +1574,7 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
   float* acc_lds = ecoef + 256;                    // 128
   bf16_t* t0 = reinterpret_cast<bf16_t*>(smem + 2304);
   // SB: single-buffered tiles (one extra barrier per iteration) so that C = 16 fits 3 workgroups per CU in LDS
-  constexpr bool SB = C == 16 && MODE_DY != 3 && ROLE == 0;
+  constexpr bool SB = DTF_FUSED_SB16 && C == 16 && MODE_DY != 3 && ROLE == 0;
   constexpr int BSTR = WG ? 2 * TSZ : TSZ;  // dgrad-only: dY tiles only
 #define FDBUF(i) (t0 + (SB ? 0 : ((i) & 1) * BSTR))
 #define FXBUF(i) (t0 + TSZ + (SB ? 0 : ((i) & 1) * BSTR))

@@ -1,42 +1,65 @@
-"""Static instruction mix per kernel of a gfx950 .s file (hipcc --cuda-device-only -S)."""
-import collections
-import re
+"""Static instruction mix of kernels in a hipcc -S output: python tools/isa_mix.py file.s name_substr..."""
 import sys
+from collections import Counter
 
 
-def main(path, pat):
-    cur, cnt = None, None
-    out = []
+def bodies(path):
+    cur, out = None, {}
     for line in open(path):
-        m = re.match(r"^(_Z\S+):\s*(;.*)?$", line)
-        if m:
-            if cur and pat in cur:
-                out.append((cur, cnt))
-            cur, cnt = m.group(1), collections.Counter()
+        if line and not line[0].isspace() and line.rstrip().endswith(':') is False and ':' in line and ' ; @' in line:
+            cur = line.split(':')[0]
+            out[cur] = []
             continue
-        if cur is None:
-            continue
-        t = line.strip()
-        if not t or t[0] in ".;_" or t.endswith(":"):
-            if t.startswith(".Lfunc_end"):
-                if pat in cur:
-                    out.append((cur, cnt))
-                cur = None
-            continue
-        op = t.split()[0]
-        cnt[op] += 1
-    for name, c in out:
-        mf = sum(v for k, v in c.items() if k.startswith("v_mfma"))
-        acc = sum(v for k, v in c.items() if k.startswith("v_accvgpr"))
-        valu = sum(v for k, v in c.items() if k.startswith("v_") and not k.startswith(("v_mfma", "v_accvgpr")))
-        lds = sum(v for k, v in c.items() if k.startswith("ds_"))
-        vm = sum(v for k, v in c.items() if k.startswith(("global_", "buffer_", "flat_")))
-        sa = sum(v for k, v in c.items() if k.startswith("s_"))
-        print("%s\n  mfma %d valu %d accvgpr %d lds %d vmem %d salu %d" % (name[:100], mf, valu, acc, lds, vm, sa))
-        top = sorted(((v, k) for k, v in c.items() if k.startswith("v_") and not k.startswith("v_mfma")),
-                     reverse=True)[:30]
-        print("  " + ", ".join("%s=%d" % (k, v) for v, k in top))
+        if cur and line.startswith('.Lfunc_end'):
+            cur = None
+        if cur and line.startswith('\t') and not line.strip().startswith(('.', ';')):
+            out[cur].append(line.strip())
+    return out
 
 
-if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+def mix(lines):
+    c = Counter()
+    for l in lines:
+        op = l.split()[0]
+        if 'mfma' in op:
+            k = 'mfma'
+        elif op.startswith('ds_read') or op.startswith('ds_load'):
+            k = 'ds_read'
+        elif op.startswith('ds_'):
+            k = 'ds_other'
+        elif op.startswith('scratch_'):
+            k = 'scratch'
+        elif op.startswith(('global_load', 'buffer_load')):
+            k = 'vmem_ld'
+        elif op.startswith(('global_', 'buffer_')):
+            k = 'vmem_st'
+        elif op.startswith('s_waitcnt'):
+            k = 'waitcnt'
+        elif op.startswith('s_'):
+            k = 'salu'
+        elif op.startswith('v_'):
+            k = 'valu'
+        else:
+            k = 'other'
+        c[k] += 1
+    return c
+
+
+if __name__ == '__main__':
+    b = bodies(sys.argv[1])
+    for name, lines in b.items():
+        if all(s in name for s in sys.argv[2:]):
+            print(name[:90], len(lines), dict(sorted(mix(lines).items())))
+
+
+def blocks(lines_raw):
+    """Split a kernel body (with labels) into basic blocks: [(label, [instr...])]."""
+    out, cur, name = [], [], 'entry'
+    for l in lines_raw:
+        if l.endswith(':') and not l.startswith('\t'):
+            out.append((name, cur))
+            name, cur = l[:-1], []
+        elif l.startswith('\t') and not l.strip().startswith(('.', ';')):
+            cur.append(l.strip())
+    out.append((name, cur))
+    return out

@@ -56,12 +56,13 @@ HEAD_ITEMS = 512          # head / GAP+dense+CE work items
 WGRAD_WG_PER_MEMBER = 128  # standalone wgrad launches: workgroups per member (bounds the dW partial traffic)
 DENSE_REDUCE_BLOCKS = 256  # slab_reduce_all, dense jobs: max 32-element blocks per job
 FUSED_SLAB_BYTES = {16: 16e6, 32: 16e6, 64: 48e6}  # fused backward: per-launch dW slab budget -> workgroup count
-FUSED_MIN_WG = 256        # ... at least this many workgroups (one member would leave CUs idle otherwise)
+FUSED_MIN_WG = int(os.environ.get("DTF_FUSED_MIN_WG", "256"))  # ... at least this many workgroups (one member would leave CUs idle otherwise)
 FUSED_MAX_WG = {32: 128}  # ... at most this many per member (C = 32: fewer, fuller workgroups)
 # ... and never a partial second round of workgroups: a count above the resident slots (CUs x WGs per CU of the
 # kernel's occupancy) is rounded down to a multiple of them (pop 8, C = 16: 1024 -> 768 workgroups of 6 bands
 # instead of 768 + a 256-workgroup tail at a third of the occupancy)
 FUSED_RESIDENT = int(os.environ.get("DTF_FUSED_RESIDENT", "1"))
+FUSED16_M3_WAVES = int(os.environ.get("DTF_FUSED16_M3_WAVES", "2"))  # must match conv.hip DTF_FUSED16_M3_WAVES
 FUSED_ROUNDS = int(os.environ.get("DTF_FUSED_ROUNDS", "1"))  # > 0: at most this many rounds of resident workgroups
 N_CU = None  # compute units: the device's (256 on MI355X; 256 without a GPU)
 
@@ -77,7 +78,9 @@ def _n_cu():
 
 def _fused_wgs_per_cu(C, mode_dy):
     """Workgroups per CU of conv_bwd_fused_kernel<C, mode_dy> (conv.hip FUSED_WAVES, 4 waves per workgroup)."""
-    return 3 if C <= 16 and mode_dy != 3 else 2 if C <= 32 else 1
+    if C <= 16:
+        return 3 if mode_dy != 3 else FUSED16_M3_WAVES
+    return 2 if C <= 32 else 1
 PIGGYBACK_MAX_WG = 3000   # slab reductions ride on the next backward launch when they add <= this many workgroups
 DEFER_WG = {16: 64, 32: 32, 64: 16}  # deferred wgrad (small populations): workgroups per member and layer
 # deferred wgrad launches issued on a side stream (a parallel branch of the step graph) as soon as a stage's layers

@@ -30,7 +30,10 @@
 #ifndef DTF_FUSED_SB16
 #define DTF_FUSED_SB16 0  // (host allocates the double-buffered size either way: 3 x 46 KB fits the 160 KB LDS)
 #endif
-#define FUSED_WAVES(C, M) ((C) <= 16 && (M) != 3 ? 3 : (C) <= 32 ? 2 : 1)
+#ifndef DTF_FUSED16_M3_WAVES
+#define DTF_FUSED16_M3_WAVES 2
+#endif
+#define FUSED_WAVES(C, M) ((C) <= 16 ? ((M) != 3 ? 3 : DTF_FUSED16_M3_WAVES) : (C) <= 32 ? 2 : 1)
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 #define NREP DTF_NREP
 #ifndef DTF_STAMP

@@ -63,6 +63,7 @@ FUSED_MAX_WG = {32: 128}  # ... at most this many per member (C = 32: fewer, ful
 # instead of 768 + a 256-workgroup tail at a third of the occupancy)
 FUSED_RESIDENT = int(os.environ.get("DTF_FUSED_RESIDENT", "1"))
 FUSED16_M3_WAVES = int(os.environ.get("DTF_FUSED16_M3_WAVES", "2"))  # must match conv.hip DTF_FUSED16_M3_WAVES
+FUSED16_WLDS = int(os.environ.get("DTF_FUSED16_WLDS", "1"))  # must match conv.hip DTF_FUSED16_WLDS
 FUSED_ROUNDS = int(os.environ.get("DTF_FUSED_ROUNDS", "1"))  # > 0: at most this many rounds of resident workgroups
 N_CU = None  # compute units: the device's (256 on MI355X; 256 without a GPU)
 
@@ -1192,6 +1193,8 @@ class _StepPlan:
         raw = C >= 64  # must match conv.hip RAWX
         nbuf = 4  # double-buffered size even when conv.hip single-buffers (SB): C = 16 still fits 3 WGs per CU
         lds = 2304 + (nbuf * tsz + (2 * rows * H * _cpad(C) if raw else 0)) * 2  # dY/X tiles [+ raw-x interiors]
+        if C == 16 and FUSED16_WLDS:
+            lds += 16 * (32 * 5 + 8) * 2  # conv.hip DTF_FUSED16_WLDS: the dgrad weights in LDS
         lib = ops.lib()
         # dW partials: per-workgroup slabs.  C = 64: every layer its own slab, all reduced by ONE launch after the
         # backward; C = 16 / 32: ping-pong slab buffers, each reduced by trailing workgroups of the next launch

@@ -30,6 +30,9 @@
 #ifndef DTF_FUSED_SB16
 #define DTF_FUSED_SB16 0  // (host allocates the double-buffered size either way: 3 x 46 KB fits the 160 KB LDS)
 #endif
+#ifndef DTF_FUSED16_WLDS
+#define DTF_FUSED16_WLDS 1  // C = 16 fused backward: dgrad weights read from LDS per MFMA instead of held in VGPRs
+#endif
 #ifndef DTF_FUSED16_M3_WAVES
 #define DTF_FUSED16_M3_WAVES 2
 #endif
@@ -1660,8 +1663,24 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
     if constexpr (WG) st.template load<1>(xv_, unused, xm, k_xm + cimg * IMG, nullptr, cgy0);
   }
   STAMP_FINE(10);
-  bf16x8_t afr[KS];
-  if constexpr (DG) {
+  // WLDS (C = 16: all four waves share the 16 x 144 weights): the weights are staged once into LDS rows of
+  // WLP elements (zero past KTOT) and read per MFMA, freeing the 20 VGPRs of afr for the pipelines
+  constexpr bool WLDS = DTF_FUSED16_WLDS && DG && C == 16 && ROLE == 0;
+  constexpr int WLP = 32 * KS + 8;
+  bf16_t* wl = t0 + 4 * TSZ;  // after the (double-buffered) dY / X tiles
+  bf16x8_t afr[WLDS ? 1 : KS];
+  uint4 wst[2];
+  if constexpr (WLDS) {
+    // 16 rows x (KS * 4) 16-byte chunks = 320 chunks: threads 0..255 + 0..63
+    const bf16_t* wb = k_w + (long)slot * k_w_mstride + k_w_off;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int idx = (int)threadIdx.x + 256 * j, r = idx / (KS * 4), k0 = (idx % (KS * 4)) * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (idx < 16 * KS * 4 && k0 < KTOT) v = *reinterpret_cast<const uint4*>(wb + (long)r * KTOT + k0);
+      wst[j] = v;
+    }
+  } else if constexpr (DG) {
     const bf16_t* wb = k_w + (long)slot * k_w_mstride + k_w_off + (long)(ct * 16 + (lane & 15)) * KTOT;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
@@ -1691,6 +1710,13 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
       ecoef[192 + c] = inv;
     }
     if (threadIdx.x < 128) acc_lds[threadIdx.x] = 0.f;
+  }
+  if constexpr (WLDS) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int idx = (int)threadIdx.x + 256 * j, r = idx / (KS * 4), k0 = (idx % (KS * 4)) * 8;
+      if (idx < 16 * KS * 4) *reinterpret_cast<uint4*>(wl + r * WLP + k0) = wst[j];
+    }
   }
   STAMP_FINE(11);
   // dgrad lane constants; k-chunks past KTOT have zero weights and read a valid in-tile address
@@ -1793,8 +1819,14 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
     for (int i = 0; i < MTD; ++i) {
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < KS; ++s)
-        acc = mfma16(afr[s], *reinterpret_cast<const bf16x8_t*>(dcur + tbo[i] + tapoff[s]), acc);
+      for (int s = 0; s < KS; ++s) {
+        bf16x8_t wa;
+        if constexpr (WLDS)
+          wa = *reinterpret_cast<const bf16x8_t*>(wl + (lane & 15) * WLP + 32 * s + 8 * (lane >> 4));
+        else
+          wa = afr[s];
+        acc = mfma16(wa, *reinterpret_cast<const bf16x8_t*>(dcur + tbo[i] + tapoff[s]), acc);
+      }
       f32x2_t v0 = {acc[0], acc[1]}, v1 = {acc[2], acc[3]};
       if constexpr (EPI & 1) {
         v0 += unpk2(rres[i].x);

@@ -10,8 +10,9 @@ LIBS=${AB_LIBS:-"default x1"}
 POPS=${AB_POPS:-"8"}
 REPS=${AB_REPS:-2}
 EXTRA=${AB_EXTRA:-""}
-libpath() { case "$1" in default|*=*) echo "";; *) echo "$GRAFT_REPO_ROOT/distributedtf_amd/ops/libdtf_kernels_$1.so";; esac; }
-venv() { case "$1" in *=*) echo "$1";; *) echo "DTF_AB_NONE=1";; esac; }
+# (lib:VAR=value: both)
+libpath() { local l=${1%%:*}; case "$l" in default|*=*) echo "";; *) echo "$GRAFT_REPO_ROOT/distributedtf_amd/ops/libdtf_kernels_$l.so";; esac; }
+venv() { local e=${1#*:}; case "$e" in *=*) echo "${e//,/ }";; *) echo "DTF_AB_NONE=1";; esac; }  # A=1,B=2
 for v in $LIBS; do
   [ "$v" = default ] && continue
   env $(venv $v) DTF_LIB=$(libpath $v) timeout -k 10 300 python -u -m pytest -x -q --timeout 250 --timeout-method thread \

@@ -1042,6 +1042,8 @@ class _StepPlan:
                 rows = r
                 break
         assert rows is not None, ("no valid band for dgrad", ci)
+        if S == 2 and K == 3:  # conv.hip conv_dgrad_body PAR: parity-class tiles of 8-row bands, Wi = 512 / cin
+            assert rows == 8 and Hi == 512 // c.cin, ("stride-2 dgrad geometry", ci, Hi, c.cin, rows)
         rows_t = rows + K - 1 if S == 1 else (rows + K + S - 2) // S + 1
         bands = Hi // rows
         n_wg = self._n_wg_iters(self.N * bands)

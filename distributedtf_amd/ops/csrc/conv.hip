@@ -1183,6 +1183,17 @@ __device__ __forceinline__ void conv_dgrad_body(const ConvArgs& a, const int bid
 #define TILEBUF(i) (tile0 + ((i) & 1) * tsz)
   const int ntiles = rows * a.Wi / 16;
   const long img_elems = (long)a.Ho * a.Wo * CO;
+  // PAR (stride-2 3x3 of the CIFAR stage transitions, Wi = 512 / CI, 8-row bands): tile i of a wave is parity
+  // class i -- its 16 pixels share (iy % 2, ix % 2) -- so only the 1-4 taps that reach the class are multiplied
+  // (9 of the 36 tap-tiles of a 2 x 2 pixel quad) and the LDS addresses need no per-k-step parity tests
+  constexpr bool PAR = S == 2 && K == 3 && (512 / CI) * 8 / 16 == 4 * WPT;
+  constexpr int WI = 512 / CI;
+  if constexpr (PAR) DTF_WG_CHECK(a.Wi == WI && rows == 8 && MAXT == 4);
+  auto par_pix = [&](int i, int iy0_, int& iy_, int& ix_) {
+    const int q = (wave / NT) * 16 + (lane & 15), cy = q / (WI / 2), cx = q % (WI / 2);
+    iy_ = iy0_ + 2 * cy + (i >> 1);
+    ix_ = 2 * cx + (i & 1);
+  };
   int tapoff[KS];  // stride 1: LDS offset of (dy row/col shift by the flipped tap, channel chunk)
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
@@ -1212,9 +1223,16 @@ __device__ __forceinline__ void conv_dgrad_body(const ConvArgs& a, const int bid
     uint2 rres[MAXT], xres[MAXT];  // epilogue operands, issued before the prefetch (counted vmcnt)
 #pragma unroll
     for (int i = 0; i < MAXT; ++i) {
-      const int t = min(wave / NT + WPT * i, ntiles - 1);
-      const int p = t * 16 + (lane & 15);
-      const long o = (((long)img * a.Hi + iy0 + p / a.Wi) * a.Wi + p % a.Wi) * CI + ct * 16 + (lane >> 4) * 4;
+      int py_, px_;
+      if constexpr (PAR) {
+        par_pix(i, iy0, py_, px_);
+      } else {
+        const int t = min(wave / NT + WPT * i, ntiles - 1);
+        const int p = t * 16 + (lane & 15);
+        py_ = iy0 + p / a.Wi;
+        px_ = p % a.Wi;
+      }
+      const long o = (((long)img * a.Hi + py_) * a.Wi + px_) * CI + ct * 16 + (lane >> 4) * 4;
       if constexpr (EPI & 1) rres[i] = *reinterpret_cast<const uint2*>(a.res + o);
       if constexpr (MASK) xres[i] = *reinterpret_cast<const uint2*>(a.xm + o);
     }
@@ -1225,8 +1243,14 @@ __device__ __forceinline__ void conv_dgrad_body(const ConvArgs& a, const int bid
       const int t = wave / NT + WPT * i;
       if (t >= ntiles) break;
       f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-      const int p = t * 16 + (lane & 15);
-      const int iy = iy0 + p / a.Wi, ix = p % a.Wi;
+      int iy, ix;
+      if constexpr (PAR) {
+        par_pix(i, iy0, iy, ix);
+      } else {
+        const int p = t * 16 + (lane & 15);
+        iy = iy0 + p / a.Wi;
+        ix = p % a.Wi;
+      }
       const int ci0 = ct * 16 + (lane >> 4) * 4;
       const long o = (((long)img * a.Hi + iy) * a.Wi + ix) * CI + ci0;
       uint2 rr = make_uint2(0, 0), xr = make_uint2(0, 0);
@@ -1234,6 +1258,24 @@ __device__ __forceinline__ void conv_dgrad_body(const ConvArgs& a, const int bid
       if constexpr (MASK) xr = xres[i];
       // stride 1: dy(iy+P-ky, ix+P-kx) lives at tile row iy+P-oy_lo-ky, col ix+P+1-kx
       const bf16_t* tb = tile + ((iy + P - oy_lo) * wp + ix + P + 1) * cpad<CO>();
+      if constexpr (PAR) {
+        // parity class (py, px) = (i >> 1, i & 1): dy(oy, ox) reaches dx(iy, ix) through ky = iy + 1 - 2 oy, so
+        // even rows take tap row 1 only and odd rows tap rows 0 and 2 (columns alike): 1, 2, 2 or 4 taps
+        constexpr int CJ = CO / 32;
+#pragma unroll
+        for (int ay = 0; ay < ((i >> 1) ? 2 : 1); ++ay) {
+          const int ky = (i >> 1) ? 2 * ay : 1;
+#pragma unroll
+          for (int ax = 0; ax < ((i & 1) ? 2 : 1); ++ax) {
+            const int kx = (i & 1) ? 2 * ax : 1;
+            const bf16_t* tp = tile + ((((iy + 1 - ky) >> 1) - oy_lo) * wp + ((ix + 1 - kx) >> 1) + 1) * cpad<CO>() +
+                               8 * (lane >> 4);
+#pragma unroll
+            for (int j = 0; j < CJ; ++j)
+              acc = mfma16(afr[(ky * 3 + kx) * CJ + j], *reinterpret_cast<const bf16x8_t*>(tp + 32 * j), acc);
+          }
+        }
+      } else {
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         const int k0 = 32 * s + 8 * (lane >> 4);
@@ -1256,6 +1298,7 @@ __device__ __forceinline__ void conv_dgrad_body(const ConvArgs& a, const int bid
             b = *reinterpret_cast<const bf16x8_t*>(tile + lds_off<CO>(lr, lc, wp, c0 >> 3));
         }
         acc = mfma16(afr[s], b, acc);
+      }
       }
       float v[4] = {acc[0], acc[1], acc[2], acc[3]};
       if constexpr (EPI & 1) {

@@ -22,7 +22,8 @@ def _relerr(a, b):
 
 @pytest.mark.parametrize("hw,c", [(56, 64), (28, 128), (14, 256)])
 @pytest.mark.parametrize("dgrad", [False, True])
-def test_convg_t3_matches_torch(hw, c, dgrad):
+@pytest.mark.parametrize("flags", [1, 0])  # 1: staged A (product default, hip_imagenet.T3_FLAGS); 0: direct A
+def test_convg_t3_matches_torch(hw, c, dgrad, flags):
     from distributedtf_amd import ops
     from distributedtf_amd.engine import hip_imagenet as hi
     hi._register()
@@ -59,9 +60,11 @@ def test_convg_t3_matches_torch(hw, c, dgrad):
     a.stride, a.pad = 1, 1
     a.cmax = CMAX
     a.log2ci = c.bit_length() - 1
+    a.flags = flags
     if dgrad:
         a.xm, a.c_ep = xmd.data_ptr(), epd.data_ptr()
-    rc = ops.lib().dtf_convg_t3(ctypes.byref(a), tc, 6 if dgrad else 4, int(dgrad), hw, work.shape[0], ops.stream())
+    rc = ops.lib().dtf_convg_t3(ctypes.byref(a), tc, 6 if dgrad else 4, int(dgrad), hw, work.shape[0], 0,
+                                ops.stream())  # mode 0: plain operand (no folded BN)
     assert rc == 0, rc
     torch.cuda.synchronize()
     yh, sth = y.float().cpu(), st.cpu()

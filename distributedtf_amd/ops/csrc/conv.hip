@@ -33,6 +33,12 @@
 #ifndef DTF_FUSED16_WLDS
 #define DTF_FUSED16_WLDS 1  // C = 16 fused backward: dgrad weights read from LDS per MFMA instead of held in VGPRs
 #endif
+#ifndef DTF_COEF_SPLIT
+#define DTF_COEF_SPLIT 0  // C < 64: wave 0's 64 / C lane groups split the statistic replicas (shuffle-summed)
+#endif
+#ifndef DTF_COEF_W0
+#define DTF_COEF_W0 0
+#endif
 #ifndef DTF_FUSED16_M3_WAVES
 #define DTF_FUSED16_M3_WAVES 2
 #endif
@@ -427,9 +433,41 @@ template <int C, int MODE>
 __device__ __forceinline__ void coef_issue(CoefLd<MODE>& L, const float* params, long p_mstride, int slot,
                                            const float* st_f, const float* st_b, int g_off, int b_off) {
   if constexpr (MODE == 0) return;
-  // branch-free: every thread loads (channel threadIdx % C; the copies hit the same lines), so no exec-mask branch
-  // makes the compiler consume -- and wait for -- the first statistics before the tile loads are issued
+  static_assert(C <= 64, "the coefficients' consumers are the threads c < C of wave 0");
+#if DTF_COEF_W0
+  // only wave 0 loads (its threads c < C are the only consumers): a wave-uniform scalar branch -- the other waves
+  // issued 3 x the statistics loads for nothing, all to the same few L2 lines as every other workgroup's
+  if (__builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6) != 0) return;
+#endif
+  // branch-free within the wave: every lane loads (channel threadIdx % C; the copies hit the same lines), so no
+  // exec-mask branch makes the compiler consume -- and wait for -- the first statistics before the tile loads
   const int c = (int)threadIdx.x & (C - 1);
+#if DTF_COEF_SPLIT
+  if constexpr (CREP == NREP && C < 64) {
+    // the wave's 64 / C lane groups split the replicas (coef_reduce sums the groups)
+    constexpr int G = 64 / C, RJ = NREP / G;
+    static_assert(NREP % G == 0, "replicas split evenly over the lane groups");
+    const int grp = ((int)threadIdx.x & 63) / C;
+    const float* rf = stats_row(st_f, slot) + c + grp * 128;
+#pragma unroll
+    for (int j = 0; j < CREP; ++j) {
+      L.fs[j] = j < RJ ? rf[j * G * 128] : 0.f;
+      L.fq[j] = j < RJ ? rf[j * G * 128 + 64] : 0.f;
+    }
+    if constexpr (MODE >= 2) {
+      const float* rb = stats_row(st_b, slot) + c + grp * 128;
+#pragma unroll
+      for (int j = 0; j < CREP; ++j) {
+        L.bs[j] = j < RJ ? rb[j * G * 128] : 0.f;
+        L.bq[j] = j < RJ ? rb[j * G * 128 + 64] : 0.f;
+      }
+    }
+    const float* prow = params + (long)slot * p_mstride;
+    L.g = prow[g_off + c];
+    if constexpr (MODE == 1) L.b = prow[b_off + c];
+    return;
+  }
+#endif
   {
     const float* rf = stats_row(st_f, slot) + c;
     if constexpr (CREP == NREP) {
@@ -465,6 +503,43 @@ __device__ __forceinline__ void coef_issue(CoefLd<MODE>& L, const float* params,
     L.g = prow[g_off + c];
     if constexpr (MODE == 1) L.b = prow[b_off + c];
   }
+}
+
+// DTF_COEF_SPLIT: sum the lane groups' replica partials (called by every lane of wave 0, outside divergent code)
+template <int C, int MODE>
+__device__ __forceinline__ void coef_reduce(CoefLd<MODE>& L) {
+#if DTF_COEF_SPLIT
+  if constexpr (MODE != 0 && CREP == NREP && C < 64) {
+    float a = 0.f, b = 0.f, d = 0.f, e = 0.f;
+#pragma unroll
+    for (int j = 0; j < CREP; ++j) {
+      a += L.fs[j];
+      b += L.fq[j];
+      if constexpr (MODE >= 2) {
+        d += L.bs[j];
+        e += L.bq[j];
+      }
+    }
+#pragma unroll
+    for (int off = C; off < 64; off *= 2) {
+      a += __shfl_xor(a, off);
+      b += __shfl_xor(b, off);
+      if constexpr (MODE >= 2) {
+        d += __shfl_xor(d, off);
+        e += __shfl_xor(e, off);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < CREP; ++j) {
+      L.fs[j] = j == 0 ? a : 0.f;
+      L.fq[j] = j == 0 ? b : 0.f;
+      if constexpr (MODE >= 2) {
+        L.bs[j] = j == 0 ? d : 0.f;
+        L.bq[j] = j == 0 ? e : 0.f;
+      }
+    }
+  }
+#endif
 }
 
 // mean / inv-std of the forward statistics in L
@@ -935,6 +1010,7 @@ __device__ __forceinline__ void conv_fwd_s1_body(const ConvArgs& a, const int bi
       afr[s] = v;
     }
   }
+  coef_reduce<C, MODE_IN == 0 ? 0 : 1>(cl);
   coef_finish<C, MODE_IN == 0 ? 0 : 1>(coef, cl, n_in);
   if (threadIdx.x < 128) acc_lds[threadIdx.x] = 0.f;
   int tapoff[KS];  // k-chunks past KTOT have zero weights and read a valid in-tile address
@@ -1734,6 +1810,8 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
     }
   }
   STAMP_FINE(12);
+  coef_reduce<C, MODE_DY == 0 ? 0 : 2>(cld);
+  if constexpr (!(EPI & 2) || (EPI & 8)) coef_reduce<C, 1>(cle);
   coef_finish<C, MODE_DY == 0 ? 0 : 2>(coef_d, cld, n_hw);
   STAMP_FINE(13);
   {

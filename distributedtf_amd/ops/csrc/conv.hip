@@ -34,10 +34,10 @@
 #define DTF_FUSED16_WLDS 1  // C = 16 fused backward: dgrad weights read from LDS per MFMA instead of held in VGPRs
 #endif
 #ifndef DTF_COEF_SPLIT
-#define DTF_COEF_SPLIT 0  // C < 64: wave 0's 64 / C lane groups split the statistic replicas (shuffle-summed)
+#define DTF_COEF_SPLIT 1  // C < 64: wave 0's 64 / C lane groups split the statistic replicas (shuffle-summed)
 #endif
 #ifndef DTF_COEF_W0
-#define DTF_COEF_W0 0
+#define DTF_COEF_W0 1
 #endif
 #ifndef DTF_FUSED16_M3_WAVES
 #define DTF_FUSED16_M3_WAVES 2

@@ -58,6 +58,9 @@ DENSE_REDUCE_BLOCKS = 256  # slab_reduce_all, dense jobs: max 32-element blocks 
 FUSED_SLAB_BYTES = {16: 16e6, 32: 16e6, 64: 48e6}  # fused backward: per-launch dW slab budget -> workgroup count
 FUSED_MIN_WG = int(os.environ.get("DTF_FUSED_MIN_WG", "256"))  # ... at least this many workgroups (one member would leave CUs idle otherwise)
 FUSED_MAX_WG = {32: 128}  # ... at most this many per member (C = 32: fewer, fuller workgroups)
+# ... and at most this many per launch (C = 16 at pop 8: 512 workgroups of 8 bands, 3.111 -> 3.091 ms; a 64-per-
+# member cap instead costs pop 4 +3.9 %: profiles/r4_fwd_wg_ab.txt)
+FUSED_TOTAL_MAX = {16: int(os.environ.get("DTF_FUSED_TOTAL16", "512"))}
 # ... and never a partial second round of workgroups: a count above the resident slots (CUs x WGs per CU of the
 # kernel's occupancy) is rounded down to a multiple of them (pop 8, C = 16: 1024 -> 768 workgroups of 6 bands
 # instead of 768 + a 256-workgroup tail at a third of the occupancy)
@@ -1440,6 +1443,8 @@ class _StepPlan:
         # each): pop 1 1.52 -> 1.44-1.47 ms/step over two runs (profiles/r1_s7_variants.log); pop >= 2 unchanged
         if C in FUSED_MAX_WG:
             n_wg = min(n_wg, FUSED_MAX_WG[C] * len(self.slots))
+        if C in FUSED_TOTAL_MAX and FUSED_TOTAL_MAX[C] > 0:
+            n_wg = min(n_wg, max(FUSED_TOTAL_MAX[C], FUSED_MIN_WG))
         n_wg = min(n_wg, self.N * bands)
         res = _n_cu() * _fused_wgs_per_cu(C, mode_dy)
         if FUSED_RESIDENT and n_wg > res:

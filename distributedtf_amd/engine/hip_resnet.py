@@ -60,7 +60,11 @@ FUSED_MIN_WG = int(os.environ.get("DTF_FUSED_MIN_WG", "256"))  # ... at least th
 FUSED_MAX_WG = {32: 128}  # ... at most this many per member (C = 32: fewer, fuller workgroups)
 # ... and at most this many per launch (C = 16 at pop 8: 512 workgroups of 8 bands, 3.111 -> 3.091 ms; a 64-per-
 # member cap instead costs pop 4 +3.9 %: profiles/r4_fwd_wg_ab.txt)
-FUSED_TOTAL_MAX = {16: int(os.environ.get("DTF_FUSED_TOTAL16", "512"))}
+# C = 32 at 8+ members: 256 (one workgroup of 8 bands per CU; half the dW slab bytes): pop 8 3.18 -> 3.11 ms;
+# pop 4 keeps its 512 (256 there: +0.4 %)
+FUSED_TOTAL_MAX = {16: int(os.environ.get("DTF_FUSED_TOTAL16", "512")),
+                   32: int(os.environ.get("DTF_FUSED_TOTAL32", "256"))}
+FUSED_TOTAL_MIN_POP = {16: 1, 32: 8}  # populations from which the per-launch cap applies
 # ... and never a partial second round of workgroups: a count above the resident slots (CUs x WGs per CU of the
 # kernel's occupancy) is rounded down to a multiple of them (pop 8, C = 16: 1024 -> 768 workgroups of 6 bands
 # instead of 768 + a 256-workgroup tail at a third of the occupancy)
@@ -1443,7 +1447,7 @@ class _StepPlan:
         # each): pop 1 1.52 -> 1.44-1.47 ms/step over two runs (profiles/r1_s7_variants.log); pop >= 2 unchanged
         if C in FUSED_MAX_WG:
             n_wg = min(n_wg, FUSED_MAX_WG[C] * len(self.slots))
-        if C in FUSED_TOTAL_MAX and FUSED_TOTAL_MAX[C] > 0:
+        if C in FUSED_TOTAL_MAX and FUSED_TOTAL_MAX[C] > 0 and len(self.slots) >= FUSED_TOTAL_MIN_POP[C]:
             n_wg = min(n_wg, max(FUSED_TOTAL_MAX[C], FUSED_MIN_WG))
         n_wg = min(n_wg, self.N * bands)
         res = _n_cu() * _fused_wgs_per_cu(C, mode_dy)

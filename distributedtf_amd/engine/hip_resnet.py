@@ -69,8 +69,6 @@ FUSED_TOTAL_MIN_POP = {16: 1, 32: 8}  # populations from which the per-launch ca
 # kernel's occupancy) is rounded down to a multiple of them (pop 8, C = 16: 1024 -> 768 workgroups of 6 bands
 # instead of 768 + a 256-workgroup tail at a third of the occupancy)
 FUSED_RESIDENT = int(os.environ.get("DTF_FUSED_RESIDENT", "1"))
-FUSED16_M3_WAVES = int(os.environ.get("DTF_FUSED16_M3_WAVES", "2"))  # must match conv.hip DTF_FUSED16_M3_WAVES
-FUSED16_WLDS = int(os.environ.get("DTF_FUSED16_WLDS", "1"))  # must match conv.hip DTF_FUSED16_WLDS
 FUSED_ROUNDS = int(os.environ.get("DTF_FUSED_ROUNDS", "1"))  # > 0: at most this many rounds of resident workgroups
 N_CU = None  # compute units: the device's (256 on MI355X; 256 without a GPU)
 
@@ -87,8 +85,19 @@ def _n_cu():
 def _fused_wgs_per_cu(C, mode_dy):
     """Workgroups per CU of conv_bwd_fused_kernel<C, mode_dy> (conv.hip FUSED_WAVES, 4 waves per workgroup)."""
     if C <= 16:
-        return 3 if mode_dy != 3 else FUSED16_M3_WAVES
+        return 3 if mode_dy != 3 else _lib_knob("dtf_fused16_m3_waves")
     return 2 if C <= 32 else 1
+_KNOBS = {}
+
+
+def _lib_knob(name):
+    """A compile-time knob of conv.hip as built into the loaded library (DTF_FUSED16_WLDS / DTF_FUSED16_M3_WAVES):
+    the launch geometry (dynamic LDS, workgroups per CU) must follow the kernel that runs, not the environment."""
+    if name not in _KNOBS:
+        _KNOBS[name] = int(getattr(ops.lib(), name)())
+    return _KNOBS[name]
+
+
 PIGGYBACK_MAX_WG = 3000   # slab reductions ride on the next backward launch when they add <= this many workgroups
 DEFER_WG = {16: 64, 32: 32, 64: 16}  # deferred wgrad (small populations): workgroups per member and layer
 # deferred wgrad launches issued on a side stream (a parallel branch of the step graph) as soon as a stage's layers
@@ -1172,6 +1181,9 @@ class _StepPlan:
             assert t is None or tuple(t.shape) == (self.N, H, H, C), (t.shape, C, H)
         bands = H // rows
         if (self.dual and (C in DUAL_CS or self.defer_wg)) or C in self.defer_cs:
+            # the dual / deferred launches have no epilogue for a chained BN's backward sums: a caller that marked
+            # the previous block as chained (v1 _build_v1) would silently lose them
+            assert chain_bn is None, "chain_bn needs the fused launch (dual / deferred paths are v2-only)"
             return self._conv_bwd_dual(ci, c, C, H, rows, bands, dy, dz_out, x, mode_dy, dy2, dy_bn, x_bn, res,
                                        ident_x, dy3, dy_out)
         n_wg = self._fused_nwg(C, bands, mode_dy)
@@ -1202,7 +1214,7 @@ class _StepPlan:
         raw = C >= 64  # must match conv.hip RAWX
         nbuf = 4  # double-buffered size even when conv.hip single-buffers (SB): C = 16 still fits 3 WGs per CU
         lds = 2304 + (nbuf * tsz + (2 * rows * H * _cpad(C) if raw else 0)) * 2  # dY/X tiles [+ raw-x interiors]
-        if C == 16 and FUSED16_WLDS:
+        if C == 16 and _lib_knob("dtf_fused16_wlds"):
             lds += 16 * (32 * 5 + 8) * 2  # conv.hip DTF_FUSED16_WLDS: the dgrad weights in LDS
         lib = ops.lib()
         # dW partials: per-workgroup slabs.  C = 64: every layer its own slab, all reduced by ONE launch after the

@@ -98,10 +98,39 @@ static __device__ int dtf_debug_err;
 // 2^39 for |y| < 30); gradients, BN-backward sums and the loss 2^36 (|value| < 1.3e8, resolution 1.5e-11).
 #define DTF_FX_STAT 24
 #define DTF_FX_GRAD 36
-__device__ __forceinline__ long long dtf_fx(float v, int shift) { return __float2ll_rn(ldexpf(v, shift)); }
+// Non-finite / out-of-range partials.  A fixed-point word cannot hold NaN or Inf, and an integer sum wraps silently,
+// so a partial that is not finite or whose scaled magnitude reaches 2^54 (room for 512 such adds below 2^63; at the
+// gradient scale |v| >= 2^18, at the statistics scale |v| >= 2^30 -- only a diverging member gets there) adds
+// nothing and instead sets its member's flag word.  The flags of every translation unit are read by
+// cg_det_finish (convg_aux.hip), which writes NaN into that member's loss and gradient row, so the engine's
+// non-finite check culls it exactly as in the float build (a diverged member used to keep a finite loss).
+#define DTF_POISON_SLOTS 1024
+#define DTF_FX_LIMIT 18014398509481984.0f  // 2^54
 __device__ __forceinline__ float dtf_unfx(long long v, int shift) { return (float)ldexp((double)v, -shift); }
-__device__ __forceinline__ void dtf_fx_add(long long* p, float v, int shift) {
-  atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)dtf_fx(v, shift));
+#ifdef DTF_DETERMINISTIC
+static __device__ unsigned dtf_poison[DTF_POISON_SLOTS];  // one array per translation unit (no relocatable device code)
+#define DTF_POISON_EXPORT(tu) \
+  DTF_API unsigned* dtf_poison_ptr_##tu() {                                             \
+    void* p = nullptr;                                                                  \
+    return hipGetSymbolAddress(&p, HIP_SYMBOL(dtf_poison)) == hipSuccess ? (unsigned*)p : nullptr; \
+  }
+__device__ __forceinline__ long long dtf_fx(float v, int shift, int slot) {
+  const float s = ldexpf(v, shift);
+  if (!(fabsf(s) < DTF_FX_LIMIT)) {  // also true for NaN
+    atomicOr(&dtf_poison[slot & (DTF_POISON_SLOTS - 1)], 1u);
+    return 0;
+  }
+  return __float2ll_rn(s);
+}
+#else
+#define DTF_POISON_EXPORT(tu)
+__device__ __forceinline__ long long dtf_fx(float v, int shift, int slot) {
+  (void)slot;
+  return __float2ll_rn(ldexpf(v, shift));
+}
+#endif
+__device__ __forceinline__ void dtf_fx_add(long long* p, float v, int shift, int slot) {
+  atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)dtf_fx(v, shift, slot));
 }
 __device__ __forceinline__ void dtf_fx_addi(long long* p, long long v) {
   atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v);
@@ -113,12 +142,13 @@ typedef long long dtf_acc_t;  // accumulator word of the ImageNet statistics / g
 #define DTF_FIXED_ACC 0
 typedef float dtf_acc_t;
 #endif
-// acc += v (float partial) / acc += w (an accumulated word, LDS -> global)
-__device__ __forceinline__ void dtf_acc_add(dtf_acc_t* p, float v, int shift) {
+// acc += v (float partial of member `slot`) / acc += w (an accumulated word, LDS -> global)
+__device__ __forceinline__ void dtf_acc_add(dtf_acc_t* p, float v, int shift, int slot) {
 #if DTF_FIXED_ACC
-  dtf_fx_add(p, v, shift);
+  dtf_fx_add(p, v, shift, slot);
 #else
   (void)shift;
+  (void)slot;
   atomicAdd(p, v);
 #endif
 }

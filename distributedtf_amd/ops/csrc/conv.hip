@@ -2384,6 +2384,10 @@ DTF_API int dtf_conv_trans_multi(const ConvArgs* c, const ConvArgs* a, const Con
   return -1;
 }
 // LDS row pitch of the stage kernels (the host sizes their dynamic LDS with it)
+// compile-time knobs the host plan must agree with (engine/hip_resnet.py reads these, not its environment)
+DTF_API int dtf_fused16_wlds() { return DTF_FUSED16_WLDS; }
+DTF_API int dtf_fused16_m3_waves() { return DTF_FUSED16_M3_WAVES; }
+
 DTF_API int dtf_wpitch(int c) { return c == 16 ? wpitch<16>() : c == 32 ? wpitch<32>() : c == 64 ? wpitch<64>() : -1; }
 
 DTF_API int dtf_conv_fwd(const ConvArgs* args, int cin, int cout, int s, int k, int mode, int resid, int stats,

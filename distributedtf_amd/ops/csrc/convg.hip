@@ -223,8 +223,8 @@ __device__ __forceinline__ void convg_epilogue(const CgArgs& a, f32x4_t (&acc)[T
       if (lane < CH && cok) {
         // forward statistics (y, y^2) or BN-backward sums (dz, dz*xhat): fixed-point scales of the deterministic build
         constexpr int FX = (EPI & 2) ? DTF_FX_GRAD : DTF_FX_STAT;
-        dtf_acc_add(&acc_lds[0][8 * ch + i], s_, FX);
-        dtf_acc_add(&acc_lds[1][8 * ch + i], q_, FX);
+        dtf_acc_add(&acc_lds[0][8 * ch + i], s_, FX, slot);
+        dtf_acc_add(&acc_lds[1][8 * ch + i], q_, FX, slot);
       }
     }
     __syncthreads();
@@ -968,7 +968,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PK == 32 ? 
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int o = o0 + wr * 64 + 16 * m + 4 * (lane >> 4) + r;
-        if (o < Co) dtf_acc_add(gr + (long)o * Kr + colr, acc[m][n][r], DTF_FX_GRAD);
+        if (o < Co) dtf_acc_add(gr + (long)o * Kr + colr, acc[m][n][r], DTF_FX_GRAD, slot);
       }
     }
   }
@@ -1155,7 +1155,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ?
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int o = o0 + wr * (WWO / 2) + 16 * m + 4 * (lane >> 4) + r;
-        if (o < Co) dtf_acc_add(gr + (long)o * Kr + col, acc[m][n][r], DTF_FX_GRAD);
+        if (o < Co) dtf_acc_add(gr + (long)o * Kr + col, acc[m][n][r], DTF_FX_GRAD, slot);
       }
     }
   }
@@ -1303,3 +1303,4 @@ DTF_API int dtf_convg_wgrad_wide(const CgArgs* a, int wo, int wt, int nwork, int
 }
 
 DTF_DEBUG_EXPORT(convg)
+DTF_POISON_EXPORT(convg)

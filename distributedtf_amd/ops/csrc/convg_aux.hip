@@ -430,8 +430,8 @@ __global__ __launch_bounds__(256) void cg_gap_bwd_reduce_kernel(GapArgs a) {
         q += g * (xv - mu) * iv;
       }
     }
-    dtf_acc_add(su + c, s, DTF_FX_GRAD);
-    dtf_acc_add(su + a.cmax + c, q, DTF_FX_GRAD);
+    dtf_acc_add(su + c, s, DTF_FX_GRAD, slot);
+    dtf_acc_add(su + a.cmax + c, q, DTF_FX_GRAD, slot);
   }
 }
 
@@ -500,12 +500,12 @@ __global__ __launch_bounds__(256) void cg_softmax_ce_kernel(const float* __restr
     float d = 0.f;
     if (j < ncls) {
       d = (__expf(lr[j] + bias[j] - lse) - (j == lab ? 1.f : 0.f)) / bsz;
-      if (grads != nullptr) dtf_acc_add(gb + j, d, DTF_FX_GRAD);
+      if (grads != nullptr) dtf_acc_add(gb + j, d, DTF_FX_GRAD, slot);
     }
     if (dl != nullptr) dl[img * ld + j] = f2bf(d);  // eval (no grads / dlogits): loss and correct count only
   }
   if (lane == 0) {
-    dtf_acc_add(loss + slot, (lse - (lr[lab] + bias[lab])) / bsz, DTF_FX_GRAD);
+    dtf_acc_add(loss + slot, (lse - (lr[lab] + bias[lab])) / bsz, DTF_FX_GRAD, slot);
     atomicAdd(correct + slot, arg == lab ? 1.f : 0.f);  // integer-valued: exact in any order
   }
 }
@@ -535,8 +535,8 @@ __global__ __launch_bounds__(256) void cg_chan_stats_kernel(const bf16_t* __rest
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      dtf_acc_add(&acc[0][c0 + k], s[k], DTF_FX_STAT);
-      dtf_acc_add(&acc[1][c0 + k], q[k], DTF_FX_STAT);
+      dtf_acc_add(&acc[0][c0 + k], s[k], DTF_FX_STAT, slot);
+      dtf_acc_add(&acc[1][c0 + k], q[k], DTF_FX_STAT, slot);
     }
   }
   __syncthreads();
@@ -673,9 +673,9 @@ __global__ __launch_bounds__(256) void cg_bn_bwd_sums_kernel(BnSumArgs a) {
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      dtf_acc_add(&acc[0][c0 + k], s[k], DTF_FX_GRAD);
-      dtf_acc_add(&acc[1][c0 + k], q[k], DTF_FX_GRAD);
-      if (two) dtf_acc_add(&acc[2][c0 + k], q2[k], DTF_FX_GRAD);
+      dtf_acc_add(&acc[0][c0 + k], s[k], DTF_FX_GRAD, slot);
+      dtf_acc_add(&acc[1][c0 + k], q[k], DTF_FX_GRAD, slot);
+      if (two) dtf_acc_add(&acc[2][c0 + k], q2[k], DTF_FX_GRAD, slot);
     }
   }
   __syncthreads();
@@ -693,39 +693,71 @@ __global__ __launch_bounds__(256) void cg_bn_bwd_sums_kernel(BnSumArgs a) {
 
 // Deterministic build: fold the fixed-point gradient accumulators of the step into the fp32 gradient rows (which
 // already hold the order-free contributions: the dense-layer GEMM and the BN gamma / beta sums) and the loss, and
-// clear the accumulators for the next step.  grid (chunks, members)
+// clear the accumulators for the next step.  A member whose step produced a non-finite or out-of-range partial
+// (flag words of convg.hip / this file, common.h dtf_fx) gets a NaN loss and NaN gradients instead.  grid (chunks,
+// members); the flags are cleared by cg_poison_clear_kernel after every block has read them.
 __global__ __launch_bounds__(256) void cg_det_finish_kernel(long long* __restrict__ gacc, float* __restrict__ grads,
                                                              long stride, long n, const int* __restrict__ slots,
-                                                             long long* __restrict__ loss64, float* __restrict__ loss) {
+                                                             long long* __restrict__ loss64, float* __restrict__ loss,
+                                                             const unsigned* __restrict__ pz0,
+                                                             const unsigned* __restrict__ pz1) {
   const int slot = slots[blockIdx.y];
+  const int ps = slot & (DTF_POISON_SLOTS - 1);
+  const bool bad = (pz0 != nullptr && pz0[ps] != 0u) || (pz1 != nullptr && pz1[ps] != 0u);
   long long* ga = gacc + (long)slot * stride;
   float* g = grads + (long)slot * stride;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const long long v = ga[i];
-    if (v != 0) {
+    if (bad) {
+      g[i] = __builtin_nanf("");
+      ga[i] = 0;
+    } else if (v != 0) {
       g[i] += dtf_unfx(v, DTF_FX_GRAD);
       ga[i] = 0;
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    loss[slot] = dtf_unfx(loss64[slot], DTF_FX_GRAD);
+    loss[slot] = bad ? __builtin_nanf("") : dtf_unfx(loss64[slot], DTF_FX_GRAD);
     loss64[slot] = 0;
   }
 }
 
+__global__ void cg_poison_clear_kernel(unsigned* __restrict__ pz0, unsigned* __restrict__ pz1,
+                                       const int* __restrict__ slots, int nslots) {
+  for (int i = threadIdx.x; i < nslots; i += blockDim.x) {
+    const int ps = slots[i] & (DTF_POISON_SLOTS - 1);
+    if (pz0 != nullptr) pz0[ps] = 0u;
+    if (pz1 != nullptr) pz1[ps] = 0u;
+  }
+}
+
 }  // namespace
+
+#ifdef DTF_DETERMINISTIC
+DTF_API unsigned* dtf_poison_ptr_convg();  // convg.hip
+DTF_API unsigned* dtf_poison_ptr_convg_aux();
+#else
+static unsigned* dtf_poison_ptr_convg() { return nullptr; }
+static unsigned* dtf_poison_ptr_convg_aux() { return nullptr; }
+#endif
 
 DTF_API int dtf_cg_det_finish(long long* gacc, float* grads, long stride, long n, const int* slots, int nslots,
                               long long* loss64, float* loss, hipStream_t stream) {
   if (nslots <= 0) return 0;
   long blocks = (n + 255) / 256;
   if (blocks > 512) blocks = 512;
+  static unsigned* const pz0 = dtf_poison_ptr_convg();  // looked up once (not inside a graph capture's hot path)
+  static unsigned* const pz1 = dtf_poison_ptr_convg_aux();
   hipLaunchKernelGGL(cg_det_finish_kernel, dim3((unsigned)blocks, nslots), dim3(256), 0, stream, gacc, grads, stride, n,
-                     slots, loss64, loss);
+                     slots, loss64, loss, pz0, pz1);
+  if (pz0 != nullptr || pz1 != nullptr)
+    hipLaunchKernelGGL(cg_poison_clear_kernel, dim3(1), dim3(256), 0, stream, pz0, pz1, slots, nslots);
   return DTF_CHECK_LAUNCH();
 }
 
 DTF_API int dtf_fixed_acc() { return DTF_FIXED_ACC; }
+
+DTF_POISON_EXPORT(convg_aux)
 
 DTF_API int dtf_bnadd_args_size() { return (int)sizeof(BnAddArgs); }
 DTF_API int dtf_bnsum_args_size() { return (int)sizeof(BnSumArgs); }

@@ -41,8 +41,9 @@ def parse():
     p.add_argument("--resnet_size", type=int, default=None, help="default 56 (CIFAR) / 50 (imagenet)")
     p.add_argument("--resnet_version", type=int, default=2, choices=[1, 2])
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
-    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
-                   help="compute dtype; fp32 = the reference's default (CIFAR ResNets: the fp32 HIP step)")
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp16"],
+                   help="compute dtype; fp32 = the reference's default (CIFAR ResNets: the fp32 HIP step); fp16 = the "
+                        "reference's fp16 mode (ResNet v2: the half build of the HIP kernels, static loss scale 128)")
     p.add_argument("--exploit_every", type=int, default=None,
                    help="steps between PBT exploit/explore cycles inside the timed region; default "
                         "min(25, max(1, steps // 2)) so every timed run holds at least one cycle; 0 = none")
@@ -83,6 +84,10 @@ def main():
     from distributedtf_amd.models.mnist_model import MNISTModel
     from distributedtf_amd.models.imagenet_model import ImageNetModel
 
+    if args.dtype == "fp16":
+        os.environ["DTF_HALF"] = "1"  # the fp16 build of the kernels (ops.lib(), loaded at first use)
+    from distributedtf_amd.utils.flags import get_loss_scale
+    loss_scale = get_loss_scale(args.dtype, None)
     comm = init_distributed()
     rank, world = comm.Get_rank(), comm.Get_size()
     if world != args.gpus and rank == 0:
@@ -107,11 +112,12 @@ def main():
         make = lambda i: ImageNetModel(begin + i, hps[begin + i], "/tmp/bench_savedata_%d/model_" % rank,  # noqa: E731
                                        seed=args.seed, resnet_size=args.resnet_size,
                                        resnet_version=args.resnet_version, device=dev, backend=args.backend,
+                                       dtype=args.dtype, loss_scale=loss_scale,
                                        capacity=max(1, cnt), use_synthetic_data=True, checkpoint_every_round=False)
     else:
         make = lambda i: Cifar10Model(begin + i, hps[begin + i], "/tmp/bench_savedata_%d/model_" % rank,  # noqa: E731
                                       seed=args.seed, resnet_size=args.resnet_size, resnet_version=args.resnet_version,
-                                      device=dev, backend=args.backend, dtype=args.dtype,
+                                      device=dev, backend=args.backend, dtype=args.dtype, loss_scale=loss_scale,
                                       capacity=max(1, cnt), use_synthetic_data=True, checkpoint_every_round=False)
     members = [make(i) for i in range(cnt)]
     eng = members[0].engine

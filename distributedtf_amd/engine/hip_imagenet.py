@@ -125,7 +125,7 @@ def _register():
                            c_int, c_int, c_void_p])
     reg("dtf_cg_gap", [P(GapArgs), c_int, c_int, c_void_p])
     reg("dtf_cg_softmax_ce", [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_long,
-                              c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p])
+                              c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_float, c_void_p])
     reg("dtf_cg_chan_stats", [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p])
     reg("dtf_cg_bn_add_relu", [P(BnAddArgs), c_void_p])
     reg("dtf_cg_bn_bwd_sums", [P(BnSumArgs), c_int, c_void_p])
@@ -178,20 +178,26 @@ class HipImageNetBackend:
         # reads it in place.  Only the stem needs a channel-padded (3 -> 8) copy.
         for c in prog.convs:
             assert c.off % 8 == 0, "conv weights must be 16-byte aligned in the shadow row"
-        self.shadow = torch.zeros(cap, engine.Pp, dtype=torch.bfloat16, device=self.dev)
+        self.shadow = torch.zeros(cap, engine.Pp, dtype=ops.act_dtype(), device=self.dev)
         st = prog.convs[prog.stem]
         self.wtot = (st.cout * st.k * st.k * 8 + 63) // 64 * 64
-        self.w = torch.zeros(cap, self.wtot, dtype=torch.bfloat16, device=self.dev)  # padded stem
+        self.w = torch.zeros(cap, self.wtot, dtype=ops.act_dtype(), device=self.dev)  # padded stem
         self.conv_table = torch.tensor([[st.off, st.cout, st.cin, st.k, 8, 0, -1, 0]], dtype=torch.int32,
                                        device=self.dev)
         self.ncls = cfg.num_classes
         assert self.ncls <= NPAD_CLS and cfg.final_size % 32 == 0
-        self.dense = torch.zeros(cap, NPAD_CLS * cfg.final_size, dtype=torch.bfloat16, device=self.dev)
+        self.dense = torch.zeros(cap, NPAD_CLS * cfg.final_size, dtype=ops.act_dtype(), device=self.dev)
         nb = len(prog.bns)
         # deterministic build (common.h DTF_FIXED_ACC): every cross-workgroup sum -- BN statistics, BN-backward sums,
         # conv weight gradients, dense bias gradient, loss -- accumulates as int64 fixed point (order-free integer
         # atomics); cg_det_finish folds the gradient / loss accumulators into the fp32 rows before the optimizer
         self.det = bool(ops.lib().dtf_fixed_acc())
+        # fp16 (half build): static loss scaling (resnet_run_loop.py:284-294): softmax-CE differentiates
+        # loss_scale * loss, the fused optimizer unscales
+        self.half = ops.build_half()
+        assert self.half == (engine.compute_dtype == torch.float16), \
+            "the loaded kernel library does not match compute dtype %s: fp16 needs DTF_HALF=1" % engine.compute_dtype
+        self.loss_scale = float(engine.loss_scale) if self.half else 1.0
         self.acc_dtype = torch.int64 if self.det else torch.float32
         self.sums = torch.zeros(2, nb, cap, 2, CMAX, dtype=self.acc_dtype, device=self.dev)   # [fwd|bwd]
         self.coef = torch.zeros(2, nb, cap, 4, CMAX, dtype=torch.float32, device=self.dev)   # [fwd|bwd]
@@ -315,7 +321,7 @@ class _ImageNetPlan:
         self.slots_t = torch.tensor(slots, dtype=torch.int32, device=dev)
         self.slots_long = torch.tensor(slots, dtype=torch.long, device=dev)
         self.loss_sel = torch.zeros(len(slots), dtype=be.loss.dtype, device=dev)
-        bf = torch.bfloat16
+        bf = ops.act_dtype()
         H = cfg.image_size
         self.H = H
         self.x_in = torch.zeros(N, H, H, cfg.in_channels, dtype=torch.float32, device=dev)
@@ -389,7 +395,7 @@ class _ImageNetPlan:
         key = (name, hw, c)
         t = self._tmp.get(key)
         if t is None:
-            t = torch.empty(self.N, hw, hw, c, dtype=torch.bfloat16, device=self.be.dev)
+            t = torch.empty(self.N, hw, hw, c, dtype=ops.act_dtype(), device=self.be.dev)
             self._tmp[key] = t
         return t
 
@@ -667,7 +673,7 @@ class _ImageNetPlan:
         self._add(L.dtf_cg_softmax_ce, _p(self.logits), NPAD_CLS, be.ncls, _p(self.labels), _p(self.img_slot),
                   _p(e.state), e.S, prog.dense_b_off, _p(be.acc_grads), e.Pp, _p(self.cnt), _p(be.acc_loss),
                   _p(be.correct),
-                  _p(self.dlog), N)
+                  _p(self.dlog), N, be.loss_scale)
         self._add("gemm", self.g_dgr)
         self._add("gemm", self.g_wgr)
         # ---- final BN backward -> gradient at the last block output
@@ -781,7 +787,7 @@ class _ImageNetPlan:
         self._add("gemm", self.g_fwd)
         self._add(L.dtf_cg_softmax_ce, _p(self.logits), NPAD_CLS, be.ncls, _p(self.labels), _p(self.img_slot),
                   _p(e.state), e.S, prog.dense_b_off, None, e.Pp, _p(self.cnt), _p(self.ev_loss),
-                  _p(self.ev_acc[0]), None, N)
+                  _p(self.ev_acc[0]), None, N, 1.0)
 
     # ------------------------------------------------------------------------------------ ResNet v1 program
     def bn_add_relu(self, h, s, out, coef_h, coef_s, hw, C):
@@ -885,7 +891,7 @@ class _ImageNetPlan:
         self._add(L.dtf_cg_softmax_ce, _p(self.logits), NPAD_CLS, be.ncls, _p(self.labels), _p(self.img_slot),
                   _p(e.state), e.S, prog.dense_b_off, _p(be.acc_grads), e.Pp, _p(self.cnt), _p(be.acc_loss),
                   _p(be.correct),
-                  _p(self.dlog), N)
+                  _p(self.dlog), N, be.loss_scale)
         self._add("gemm", self.g_dgr)
         self._add("gemm", self.g_wgr)
         # GAP backward: the gradient at the last block output, masked by its ReLU (cg_gap_bwd_apply, coef = null)
@@ -981,7 +987,7 @@ class _ImageNetPlan:
         self._add("gemm", self.g_fwd)
         self._add(L.dtf_cg_softmax_ce, _p(self.logits), NPAD_CLS, be.ncls, _p(self.labels), _p(self.img_slot),
                   _p(e.state), e.S, prog.dense_b_off, None, e.Pp, _p(self.cnt), _p(self.ev_loss),
-                  _p(self.ev_acc[0]), None, N)
+                  _p(self.ev_acc[0]), None, N, 1.0)
 
     def load_eval(self, x, y):
         """The same eval images for every member: [m, H, W, C] fp32 -> this plan's [members * m] input."""
@@ -1017,7 +1023,7 @@ class _ImageNetPlan:
             elif fn == "optim":
                 e.dp_sync_grads(self.slots)  # data-parallel member groups only (no-op otherwise)
                 ops.fused_optimizer(e.state, e.grads, e.hyper, e.Pp, e.P, e.n_reg, shadow=self.be.shadow,
-                                    zero_grads=True)
+                                    zero_grads=True, grad_scale=1.0 / self.be.loss_scale)
             elif fn == "step":
                 # step counters + per-member losses gathered inside the step (graph): a replay leaves one copy
                 advance_steps(e, self.slots_long, self.slots_t, self.be.loss, self.loss_sel)

@@ -179,7 +179,7 @@ class HeadArgs(ctypes.Structure):
         ("gamma_off", c_int), ("beta_off", c_int), ("dw_off", c_int), ("db_off", c_int), ("grads", c_void_p),
         ("g_mstride", c_long), ("st_f", c_void_p), ("st_b", c_void_p), ("cnt", c_void_p), ("dfeat", c_void_p),
         ("loss", c_void_p), ("correct", c_void_p), ("logits_out", c_void_p), ("hw", c_int), ("C", c_int),
-        ("ncls", c_int), ("train", c_int), ("slab", c_void_p), ("slab_b", c_void_p),
+        ("ncls", c_int), ("train", c_int), ("slab", c_void_p), ("slab_b", c_void_p), ("loss_scale", ctypes.c_float),
     ]
 
 
@@ -497,10 +497,17 @@ class HipResNetBackend:
         self.dev = engine.device
         self.L = _Layout(engine)
         cap = engine.capacity
-        self.wf = torch.zeros(cap, self.L.wtot, dtype=torch.bfloat16, device=self.dev)
-        self.wd = torch.zeros(cap, self.L.wtot, dtype=torch.bfloat16, device=self.dev)
+        self.wf = torch.zeros(cap, self.L.wtot, dtype=ops.act_dtype(), device=self.dev)
+        self.wd = torch.zeros(cap, self.L.wtot, dtype=ops.act_dtype(), device=self.dev)
         nb = len(self.L.prog.bns)
         self.det = ops.build_deterministic()  # what the loaded library was compiled as
+        # fp16 (the half build of the same kernels, ops.half_mode()): static loss scaling as the reference's fp16 mode
+        # (resnet_run_loop.py:284-294) -- the head differentiates loss_scale * loss, the optimizer unscales
+        self.half = ops.build_half()
+        assert self.half == (engine.compute_dtype == torch.float16), \
+            "the loaded kernel library (%s) does not match compute dtype %s: fp16 needs DTF_HALF=1" % (
+                "fp16" if self.half else "bf16", engine.compute_dtype)
+        self.loss_scale = float(engine.loss_scale) if self.half else 1.0
         NREP = self.nrep = _nrep()
         self.stats_bn_stride = cap * NREP * 128
         # [fwd | bwd] statistic accumulators: zeroed by ONE memset per step
@@ -711,7 +718,7 @@ class _StepPlan:
         H = cfg.image_size
         self.x_in = torch.zeros(N, H, H, 3, dtype=torch.float32, device=dev)
         self.labels = torch.zeros(N, dtype=torch.int32, device=dev)
-        self.xin16 = torch.zeros(N, H, H, 16, dtype=torch.bfloat16, device=dev)
+        self.xin16 = torch.zeros(N, H, H, 16, dtype=ops.act_dtype(), device=dev)
         self.src = src
         if src is not None:
             self.idx = torch.zeros(N, dtype=torch.long, device=dev)
@@ -721,15 +728,15 @@ class _StepPlan:
         # the residual stream ping-pongs between two)
         self.xs, self.hs, self.scs = [], [], []
         self.hb = []  # v1: conv_b outputs (pre-BN); hs = conv_a outputs, scs = projection outputs (pre-BN)
-        self.h0 = torch.empty(N, H, H, cfg.num_filters, dtype=torch.bfloat16, device=dev) if self.v1 else None
+        self.h0 = torch.empty(N, H, H, cfg.num_filters, dtype=ops.act_dtype(), device=dev) if self.v1 else None
         pool = {}
 
         def act(kind, hw_, c_, i_=0):
             if not self.eval:
-                return torch.empty(N, hw_, hw_, c_, dtype=torch.bfloat16, device=dev)
+                return torch.empty(N, hw_, hw_, c_, dtype=ops.act_dtype(), device=dev)
             key = (kind, hw_, c_, i_ % 2 if kind == "x" else 0)
             if key not in pool:
-                pool[key] = torch.empty(N, hw_, hw_, c_, dtype=torch.bfloat16, device=dev)
+                pool[key] = torch.empty(N, hw_, hw_, c_, dtype=ops.act_dtype(), device=dev)
             return pool[key]
 
         hw, c = H, cfg.num_filters
@@ -764,15 +771,15 @@ class _StepPlan:
             if st > 0:
                 hw //= 2
             cc = cfg.num_filters * (2 ** st)
-            self.tmp[hw] = dict(g=[torch.empty(N, hw, hw, cc, dtype=torch.bfloat16, device=dev) for _ in range(2)],
-                                dz2=torch.empty(N, hw, hw, cc, dtype=torch.bfloat16, device=dev),
-                                dz1=torch.empty(N, hw, hw, cc, dtype=torch.bfloat16, device=dev))
+            self.tmp[hw] = dict(g=[torch.empty(N, hw, hw, cc, dtype=ops.act_dtype(), device=dev) for _ in range(2)],
+                                dz2=torch.empty(N, hw, hw, cc, dtype=ops.act_dtype(), device=dev),
+                                dz1=torch.empty(N, hw, hw, cc, dtype=ops.act_dtype(), device=dev))
         self.pd = {}  # projection dgrad outputs at block-input resolution
         hw = H
         for blk in prog.blocks:
             if blk.proj is not None:
                 ci = prog.convs[blk.proj].cin
-                self.pd[id(blk)] = torch.empty(N, hw, hw, ci, dtype=torch.bfloat16, device=dev)
+                self.pd[id(blk)] = torch.empty(N, hw, hw, ci, dtype=ops.act_dtype(), device=dev)
             hw //= blk.stride
         self.dfeat = torch.zeros(N, cfg.final_size, dtype=torch.float32, device=dev)
         self._work_cache = {}
@@ -1564,6 +1571,7 @@ class _StepPlan:
         ha.dfeat, ha.loss, ha.correct = _p(self.dfeat), _p(be.loss), _p(be.correct)
         ha.logits_out = None
         ha.hw, ha.C, ha.ncls, ha.train = hw, cfg.final_size, cfg.num_classes, 1
+        ha.loss_scale = be.loss_scale
         self._head_slab(ha, hwork)
         self._keep(ha)
         self._add(lib.dtf_head, ctypes.byref(ha), hwork.shape[0])
@@ -1725,6 +1733,7 @@ class _StepPlan:
         ha.dfeat, ha.correct, ha.loss = None, _p(self.ev_acc[0]), _p(self.ev_acc[1])
         ha.logits_out = None
         ha.hw, ha.C, ha.ncls, ha.train = L.final_hw, cfg.final_size, cfg.num_classes, 0
+        ha.loss_scale = 1.0
         self._keep(ha)
         self._head_args = ha
         self._add(lib.dtf_head, ctypes.byref(ha), hwork.shape[0])
@@ -1827,6 +1836,7 @@ class _StepPlan:
         ha_.dfeat, ha_.loss, ha_.correct = _p(self.dfeat), _p(be.loss), _p(be.correct)
         ha_.logits_out = None
         ha_.hw, ha_.C, ha_.ncls, ha_.train = hw, cfg.final_size, cfg.num_classes, 1
+        ha_.loss_scale = be.loss_scale
         self._head_slab(ha_, hwork)
         self._keep(ha_)
         self._add(lib.dtf_head, ctypes.byref(ha_), hwork.shape[0])
@@ -1936,7 +1946,8 @@ class _StepPlan:
                                   lab32=self.labels)
             elif fn == "optim":
                 e.dp_sync_grads(self.slots)  # data-parallel member groups only (no-op otherwise)
-                ops.fused_optimizer(e.state, e.grads, e.hyper, e.Pp, e.P, e.n_reg, shadow=None, zero_grads=True)
+                ops.fused_optimizer(e.state, e.grads, e.hyper, e.Pp, e.P, e.n_reg, shadow=None, zero_grads=True,
+                                    grad_scale=1.0 / self.be.loss_scale)
             elif fn == "step":
                 # step counters + per-member losses gathered inside the step (graph) so a replay leaves one copy
                 # for loss_view

@@ -273,6 +273,12 @@ class TorchBackend:
         return e.arch.forward(e.params[slot], e.running[slot], x, training=False, dtype=e.compute_dtype)
 
 
+def _half_lib_loaded() -> bool:
+    """The process runs the fp16 kernel build (DTF_HALF=1): its 16-bit kernels cannot serve a bf16 engine."""
+    from .. import ops
+    return ops.half_mode()
+
+
 def _hip_f32_ok(engine) -> bool:
     """fp32 HIP step (engine/hip_f32.py): CIFAR-shape building-block ResNets."""
     if engine.compute_dtype != torch.float32:
@@ -280,17 +286,34 @@ def _hip_f32_ok(engine) -> bool:
     from .. import ops
     if ops.deterministic_mode():  # the deterministic build's shared bn_final reads int64 fixed-point sums
         return False
+    if ops.half_mode():  # the fp32 step shares 16-bit helper kernels (input packing) with the bf16 build
+        return False
     from .hip_f32 import supports
     return supports(engine.arch)
 
 
+def _hip_f16_ok(engine) -> bool:
+    """fp16 HIP step: the half build of the bf16 kernels (ops/csrc/common.h DTF_HALF; loaded for DTF_HALF=1, which
+    --dtype fp16 sets) for the ResNet v2 families -- the reference's fp16 mode exists for ResNet only and forbids v1
+    (resnet_run_loop.py:546-549)."""
+    if engine.compute_dtype != torch.float16:
+        return False
+    from .. import ops
+    if not ops.half_mode() or ops.deterministic_mode() or ops.debug_mode():
+        return False
+    cfg = getattr(engine.arch, "cfg", None)
+    return cfg is not None and getattr(cfg, "version", 0) == 2 and getattr(engine.arch, "name", "") != "mnist_cnn"
+
+
 def make_backend(engine: PopulationEngine, name: str):
+    ok16 = engine.compute_dtype == torch.bfloat16 and not (engine.device.type == "cuda" and _half_lib_loaded())
     if name == "auto":
         name = "hip" if (engine.device.type == "cuda" and getattr(engine.arch, "hip_supported", False)
-                         and (engine.compute_dtype == torch.bfloat16 or _hip_f32_ok(engine))) else "torch"
-    if name == "hip" and engine.compute_dtype != torch.bfloat16 and not _hip_f32_ok(engine):
-        raise ValueError("the HIP kernels of this model compute in bf16 (got %s; fp32 HIP runs the CIFAR ResNets): "
-                         "use the torch backend" % engine.compute_dtype)
+                         and (ok16 or _hip_f32_ok(engine) or _hip_f16_ok(engine))) else "torch"
+    if name == "hip" and not (ok16 or _hip_f32_ok(engine) or _hip_f16_ok(engine)):
+        raise ValueError("no HIP step for compute dtype %s here (bf16: every family; fp32: the CIFAR ResNets; fp16: "
+                         "the ResNet v2 families under DTF_HALF=1, which --dtype fp16 sets): use the torch backend"
+                         % engine.compute_dtype)
     if name == "torch":
         return TorchBackend(engine)
     if name == "hip" and engine.compute_dtype == torch.float32:

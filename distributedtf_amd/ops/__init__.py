@@ -25,7 +25,7 @@ c_void_p, c_int, c_long, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_long,
 # name -> argtypes (all return int = hipError_t of the launch)
 _SIGNATURES = {
     "dtf_fused_optimizer": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_long, c_long, c_long, c_long, c_int,
-                            c_void_p],
+                            c_float, c_void_p],
     "dtf_shadow_refresh": [c_void_p, c_void_p, c_void_p, c_int, c_long, c_long, c_long, c_void_p],
     "dtf_step_advance": [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_int, c_void_p],
     "dtf_step_end": [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p],
@@ -45,7 +45,11 @@ def lib():
             # DTF_LIB: an alternative build of the same sources (e.g. timing-only ablation builds of tools/)
             debug = debug_mode()
             det = deterministic_mode()
-            default = _build.LIB_DEBUG if debug else (_build.LIB_DET if det else _build.LIB)
+            half = half_mode()
+            if half and (debug or det):
+                raise RuntimeError("DTF_HALF=1 (fp16 kernels) has no debug / deterministic build")
+            default = (_build.LIB_DEBUG if debug else (_build.LIB_DET if det else
+                                                       (_build.LIB_HALF if half else _build.LIB)))
             path = os.environ.get("DTF_LIB") or default
             if path == default and (not os.path.isfile(path) or
                                     (os.environ.get("DTF_REBUILD") == "1" and _build.needs_build(path))):
@@ -53,6 +57,8 @@ def lib():
                     _build.build_debug(verbose=False)
                 elif det:
                     _build.build_det(verbose=False)
+                elif half:
+                    _build.build_half(verbose=False)
                 else:
                     _build.build(verbose=False)
             if not os.path.isfile(path):
@@ -80,6 +86,25 @@ def build_deterministic() -> bool:
     fn = lib().dtf_build_deterministic
     fn.argtypes, fn.restype = [], c_int
     return bool(fn())
+
+
+def build_half() -> bool:
+    """True if the loaded library is the half build (fp16 storage, ``dtf_build_half``)."""
+    fn = lib().dtf_build_half
+    fn.argtypes, fn.restype = [], c_int
+    return bool(fn())
+
+
+def half_mode() -> bool:
+    """DTF_HALF=1 (set by ``--dtype fp16``): load the fp16 build of the kernels (common.h DTF_HALF).  The library is
+    one per process, like the deterministic build: a process runs either bf16 or fp16 HIP steps."""
+    return os.environ.get("DTF_HALF", "0") == "1"
+
+
+def act_dtype():
+    """torch dtype of the kernels' 16-bit tensors (activations, weight shadows) in this process."""
+    import torch
+    return torch.float16 if half_mode() else torch.bfloat16
 
 
 def deterministic_mode() -> bool:
@@ -183,15 +208,16 @@ def check(err, name):
         raise RuntimeError("%s launch failed: hipError %d" % (name, err))
 
 
-def fused_optimizer(state, grads, hyper, Pp, P, n_reg, shadow=None, zero_grads=True):
-    """One launch: TF1-semantics optimizer step for every member row (see optim.hip)."""
+def fused_optimizer(state, grads, hyper, Pp, P, n_reg, shadow=None, zero_grads=True, grad_scale=1.0):
+    """One launch: TF1-semantics optimizer step for every member row (see optim.hip).  ``grad_scale`` multiplies every
+    gradient first (1 / loss_scale: the fp16 mode's static loss scaling, resnet_run_loop.py:284-294)."""
     assert state.is_cuda and state.dtype == torch.float32 and state.is_contiguous()
     assert grads.shape[1] == Pp and hyper.shape[1] == 8
     G = state.shape[0]
     if shadow is not None:
-        assert shadow.dtype == torch.bfloat16 and shadow.shape[1] == Pp
+        assert shadow.dtype in (torch.bfloat16, torch.float16) and shadow.shape[1] == Pp
     check(lib().dtf_fused_optimizer(ptr(state), ptr(grads), ptr(hyper), ptr(shadow), G, state.shape[1], Pp, P, n_reg,
-                                    1 if zero_grads else 0, stream()), "fused_optimizer")
+                                    1 if zero_grads else 0, float(grad_scale), stream()), "fused_optimizer")
 
 
 def shadow_refresh(state, shadow, rows, Pp, P):

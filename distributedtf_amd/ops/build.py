@@ -26,6 +26,11 @@ DEBUG_FLAGS = ["-DDTF_DEBUG=1", "-g"]
 # atomic add onto zero and the consumers sum the replicas in a fixed order -- bitwise-replayable statistics.
 LIB_DET = os.path.join(HERE, "libdtf_kernels_det.so")
 DET_FLAGS = ["-DDTF_DETERMINISTIC=1", "-DDTF_NREP=64"]
+# Half build (--dtype fp16 / DTF_HALF=1): the same kernels for IEEE fp16 activation / weight-shadow storage and
+# v_mfma_f32_16x16x32_f16 (common.h DTF_HALF); the static loss scale of the reference's fp16 mode is applied by the
+# head (dlogits x S) and removed by the fused optimizer (grads x 1/S)
+LIB_HALF = os.path.join(HERE, "libdtf_kernels_f16.so")
+HALF_FLAGS = ["-DDTF_HALF=1"]
 ARCH = os.environ.get("DTF_OFFLOAD_ARCH", "gfx950")
 
 
@@ -92,10 +97,16 @@ def build_det(force: bool = False, verbose: bool = True) -> str:
     return build(force=force, verbose=verbose, extra_flags=DET_FLAGS, out=LIB_DET)
 
 
+def build_half(force: bool = False, verbose: bool = True) -> str:
+    return build(force=force, verbose=verbose, extra_flags=HALF_FLAGS, out=LIB_HALF)
+
+
 if __name__ == "__main__":
     if "--debug" in sys.argv:
         build_debug(force="--force" in sys.argv)
     elif "--det" in sys.argv:
         build_det(force="--force" in sys.argv)
+    elif "--half" in sys.argv:
+        build_half(force="--force" in sys.argv)
     else:
         build(force="--force" in sys.argv)

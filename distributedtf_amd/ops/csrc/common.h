@@ -15,17 +15,53 @@
 
 #define DTF_API extern "C" __attribute__((visibility("default")))
 
+// 16-bit activation / weight-shadow element.  The default build stores bf16; the half build (ops/build.py
+// LIB_HALF, -DDTF_HALF=1, selected by --dtype fp16) compiles the SAME kernels for IEEE fp16 storage and the
+// v_mfma_f32_16x16x32_f16 matrix op (same rate and operand layout as the bf16 form): every 16-bit <-> fp32
+// conversion of the kernels goes through bf2f / f2bf / pack2bf / lo2f / hi2f / pk2 below, and every MFMA through
+// dtf_mfma16, so the element type is a build switch rather than a second set of kernels.  (The type keeps its
+// bf16_t name: it is "the 16-bit element" of either build.)  Bit tricks the kernels rely on hold for both
+// formats: a zero word is +0, bit 15 is the sign (ReLU as a signed-int16 max), 16-byte vectors hold 8 elements.
 typedef uint16_t bf16_t;
 typedef short bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
+#ifdef DTF_HALF
+typedef _Float16 dtf_h16_t;
+typedef _Float16 h16x8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 h16x2v_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float bf2f(bf16_t v) { return (float)__builtin_bit_cast(_Float16, v); }
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (_Float16)f); }
+__device__ __forceinline__ float lo2f(uint32_t w) { return bf2f((bf16_t)(w & 0xffffu)); }
+__device__ __forceinline__ float hi2f(uint32_t w) { return bf2f((bf16_t)(w >> 16)); }
+__device__ __forceinline__ uint32_t pk2(f32x2_t v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, h16x2v_t));
+}
+__device__ __forceinline__ f32x4_t dtf_mfma16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h16x8_t, a), __builtin_bit_cast(h16x8_t, b), c,
+                                                 0, 0, 0);
+}
+#define DTF_HALF_BUILD 1
+#else
+typedef __bf16 bf16x2v_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
-
 __device__ __forceinline__ bf16_t f2bf(float f) {
   __bf16 b = (__bf16)f;
   return __builtin_bit_cast(bf16_t, b);
 }
+// the low / high element of a packed pair as fp32 (one VALU op each for bf16)
+__device__ __forceinline__ float lo2f(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float hi2f(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+__device__ __forceinline__ uint32_t pk2(f32x2_t v) {  // v_cvt_pk_bf16_f32
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v_t));
+}
+__device__ __forceinline__ f32x4_t dtf_mfma16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+#define DTF_HALF_BUILD 0
+#endif
 
 __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
   return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);

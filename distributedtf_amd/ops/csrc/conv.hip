@@ -347,12 +347,12 @@ __device__ __forceinline__ uint4 transform8(uint4 v, uint4 v2, int c0, const flo
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int c = c0 + 2 * j;
-    float a0 = __uint_as_float(w32[j] << 16), a1 = __uint_as_float(w32[j] & 0xffff0000u);
+    float a0 = lo2f(w32[j]), a1 = hi2f(w32[j]);
     if constexpr (MODE == 1) {
       a0 = fmaxf(a0 * coef[c] + coef[64 + c], 0.f);
       a1 = fmaxf(a1 * coef[c + 1] + coef[64 + c + 1], 0.f);
     } else {
-      const float h0 = __uint_as_float(h32[j] << 16), h1 = __uint_as_float(h32[j] & 0xffff0000u);
+      const float h0 = lo2f(h32[j]), h1 = hi2f(h32[j]);
       a0 = coef[c] * a0 + coef[64 + c] * h0 + coef[128 + c];
       a1 = coef[c + 1] * a1 + coef[64 + c + 1] * h1 + coef[128 + c + 1];
     }
@@ -582,7 +582,7 @@ __device__ __forceinline__ void coef_finish(float* coef, const CoefLd<MODE>& L, 
 }
 
 __device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  return dtf_mfma16(a, b, c);
 }
 
 // Reduce per-lane partial channel sums (4 channels per lane, 16 lanes share them)
@@ -640,16 +640,10 @@ __device__ __forceinline__ void flush_stats(float* st_out, const float* acc_lds,
 }
 
 // Packed-math helpers (v_pk_fma_f32 / v_cvt_pk_bf16_f32 / v_pk_max_i16): two channels per VALU op.
-typedef float f32x2_t __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2v_t __attribute__((ext_vector_type(2)));
 typedef short s16x2_t __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ f32x2_t unpk2(uint32_t w) {
-  return (f32x2_t){__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
-}
-__device__ __forceinline__ uint32_t pk2(f32x2_t v) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v_t));
-}
+// (f32x2_t and pk2 -- v_cvt_pk_bf16_f32, or the fp16 pack of the half build -- are in common.h)
+__device__ __forceinline__ f32x2_t unpk2(uint32_t w) { return (f32x2_t){lo2f(w), hi2f(w)}; }
 // ReLU on two packed bf16: as int16, every negative bf16 (sign bit set) is < 0
 __device__ __forceinline__ uint32_t relu_pk2(uint32_t w) {
   return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2_t, w), (s16x2_t){0, 0}));

@@ -31,7 +31,7 @@ namespace {
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  return dtf_mfma16(a, b, c);
 }
 
 __device__ __forceinline__ s16x4_t ds_read_tr(const bf16_t* p) {
@@ -61,8 +61,8 @@ __device__ __forceinline__ uint4 bnrelu8(uint4 v, const float (&sc)[8], const fl
   uint32_t r[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const float lo = fmaxf(__uint_as_float(w[q] << 16) * sc[2 * q] + sh[2 * q], 0.f);
-    const float hi = fmaxf(__uint_as_float(w[q] & 0xffff0000u) * sc[2 * q + 1] + sh[2 * q + 1], 0.f);
+    const float lo = fmaxf(lo2f(w[q]) * sc[2 * q] + sh[2 * q], 0.f);
+    const float hi = fmaxf(hi2f(w[q]) * sc[2 * q + 1] + sh[2 * q + 1], 0.f);
     r[q] = pack2bf(lo, hi);
   }
   return make_uint4(r[0], r[1], r[2], r[3]);
@@ -177,11 +177,11 @@ __device__ __forceinline__ void convg_epilogue(const CgArgs& a, f32x4_t (&acc)[T
     float xv[8];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      xv[2 * q] = __uint_as_float(x32[q] << 16);
-      xv[2 * q + 1] = __uint_as_float(x32[q] & 0xffff0000u);
+      xv[2 * q] = lo2f(x32[q]);
+      xv[2 * q + 1] = hi2f(x32[q]);
       if constexpr (EPI & 1) {
-        v[2 * q] += __uint_as_float(r32[q] << 16);
-        v[2 * q + 1] += __uint_as_float(r32[q] & 0xffff0000u);
+        v[2 * q] += lo2f(r32[q]);
+        v[2 * q + 1] += hi2f(r32[q]);
       }
     }
     if constexpr (EPI & 2) {
@@ -195,7 +195,7 @@ __device__ __forceinline__ void convg_epilogue(const CgArgs& a, f32x4_t (&acc)[T
     if constexpr (EPI & 4) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float r0 = __uint_as_float(pk[q] << 16), r1 = __uint_as_float(pk[q] & 0xffff0000u);
+        const float r0 = lo2f(pk[q]), r1 = hi2f(pk[q]);
         ss[2 * q] += r0;
         ss[2 * q + 1] += r1;
         if constexpr (EPI & 2) {
@@ -411,12 +411,12 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int c = cch + 2 * q;
-          float x0 = __uint_as_float(w32[q] << 16), x1 = __uint_as_float(w32[q] & 0xffff0000u);
+          float x0 = lo2f(w32[q]), x1 = hi2f(w32[q]);
           if constexpr (MODE == 1) {
             x0 = fmaxf(x0 * dyn[c] + dyn[Ci + c], 0.f);
             x1 = fmaxf(x1 * dyn[c + 1] + dyn[Ci + c + 1], 0.f);
           } else {
-            const float h0 = __uint_as_float(h32[q] << 16), h1 = __uint_as_float(h32[q] & 0xffff0000u);
+            const float h0 = lo2f(h32[q]), h1 = hi2f(h32[q]);
             x0 = dyn[c] * x0 + dyn[Ci + c] * h0 + dyn[2 * Ci + c];
             x1 = dyn[c + 1] * x1 + dyn[Ci + c + 1] * h1 + dyn[2 * Ci + c + 1];
           }
@@ -877,12 +877,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PK == 32 ? 
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int c = dcol + 2 * q;
-          float x0 = __uint_as_float(w32[q] << 16), x1 = __uint_as_float(w32[q] & 0xffff0000u);
+          float x0 = lo2f(w32[q]), x1 = hi2f(w32[q]);
           if constexpr (MODE_DY == 1) {
             x0 = fmaxf(x0 * cd[c] + cd[Co + c], 0.f);
             x1 = fmaxf(x1 * cd[c + 1] + cd[Co + c + 1], 0.f);
           } else {
-            const float h0 = __uint_as_float(h32[q] << 16), h1 = __uint_as_float(h32[q] & 0xffff0000u);
+            const float h0 = lo2f(h32[q]), h1 = hi2f(h32[q]);
             x0 = cd[c] * x0 + cd[Co + c] * h0 + cd[2 * Co + c];
             x1 = cd[c + 1] * x1 + cd[Co + c + 1] * h1 + cd[2 * Co + c + 1];
           }
@@ -897,7 +897,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PK == 32 ? 
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int c = xci + 2 * q;
-          const float x0 = __uint_as_float(w32[q] << 16), x1 = __uint_as_float(w32[q] & 0xffff0000u);
+          const float x0 = lo2f(w32[q]), x1 = hi2f(w32[q]);
           w32[q] = pack2bf(fmaxf(x0 * cx[c] + cx[Ci + c], 0.f), fmaxf(x1 * cx[c + 1] + cx[Ci + c + 1], 0.f));
         }
         u = make_uint4(w32[0], w32[1], w32[2], w32[3]);

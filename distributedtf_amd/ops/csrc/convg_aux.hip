@@ -225,11 +225,11 @@ __global__ __launch_bounds__(256) void cg_bn_bwd_apply_kernel(EwArgs a) {
       uint32_t r[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float v0 = ca[2 * q] * __uint_as_float(d32[q] << 16) + cbv[2 * q] * __uint_as_float(h32[q] << 16) +
-                         cc[2 * q] + __uint_as_float(a32[q] << 16);
-        const float v1 = ca[2 * q + 1] * __uint_as_float(d32[q] & 0xffff0000u) +
-                         cbv[2 * q + 1] * __uint_as_float(h32[q] & 0xffff0000u) + cc[2 * q + 1] +
-                         __uint_as_float(a32[q] & 0xffff0000u);
+        const float v0 = ca[2 * q] * lo2f(d32[q]) + cbv[2 * q] * lo2f(h32[q]) +
+                         cc[2 * q] + lo2f(a32[q]);
+        const float v1 = ca[2 * q + 1] * hi2f(d32[q]) +
+                         cbv[2 * q + 1] * hi2f(h32[q]) + cc[2 * q + 1] +
+                         hi2f(a32[q]);
         r[q] = pack2bf(v0, v1);
       }
       ew_store<NT>(out + i * 8, make_uint4(r[0], r[1], r[2], r[3]));
@@ -267,8 +267,8 @@ __global__ __launch_bounds__(256) void cg_bn_relu_apply_kernel(EwArgs a) {
       uint32_t r[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float v0 = fmaxf(__uint_as_float(h32[q] << 16) * sc[2 * q] + sh[2 * q], 0.f);
-        const float v1 = fmaxf(__uint_as_float(h32[q] & 0xffff0000u) * sc[2 * q + 1] + sh[2 * q + 1], 0.f);
+        const float v0 = fmaxf(lo2f(h32[q]) * sc[2 * q] + sh[2 * q], 0.f);
+        const float v1 = fmaxf(hi2f(h32[q]) * sc[2 * q + 1] + sh[2 * q + 1], 0.f);
         r[q] = pack2bf(v0, v1);
       }
       ew_store<NT>(out + i * 8, make_uint4(r[0], r[1], r[2], r[3]));
@@ -465,7 +465,7 @@ __global__ __launch_bounds__(256) void cg_softmax_ce_kernel(const float* __restr
                                                              dtf_acc_t* __restrict__ grads, long g_mstride,
                                                              const float* __restrict__ cnt, dtf_acc_t* __restrict__ loss,
                                                              float* __restrict__ correct, bf16_t* __restrict__ dl,
-                                                             long nimg) {
+                                                             long nimg, float loss_scale) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long img = (long)blockIdx.x * 4 + wave;
   if (img >= nimg) return;
@@ -495,11 +495,12 @@ __global__ __launch_bounds__(256) void cg_softmax_ce_kernel(const float* __restr
   const float lse = mx + __logf(se);
   const int lab = labels[img];
   const float bsz = cnt[slot];
+  const float gsc = loss_scale / bsz;  // gradients of loss_scale * loss (fp16 static loss scaling; else 1)
   dtf_acc_t* gb = grads != nullptr ? grads + (long)slot * g_mstride + b_off : nullptr;
   for (int j = lane; j < ld; j += 64) {
     float d = 0.f;
     if (j < ncls) {
-      d = (__expf(lr[j] + bias[j] - lse) - (j == lab ? 1.f : 0.f)) / bsz;
+      d = (__expf(lr[j] + bias[j] - lse) - (j == lab ? 1.f : 0.f)) * gsc;
       if (grads != nullptr) dtf_acc_add(gb + j, d, DTF_FX_GRAD, slot);
     }
     if (dl != nullptr) dl[img * ld + j] = f2bf(d);  // eval (no grads / dlogits): loss and correct count only
@@ -602,10 +603,10 @@ __global__ __launch_bounds__(256) void cg_bn_add_relu_kernel(BnAddArgs a) {
       uint32_t r[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float v0 = __uint_as_float(h32[q] << 16) * sc[2 * q] + sh[2 * q] +
-                         __uint_as_float(s32[q] << 16) * ps[2 * q] + pt[2 * q];
-        const float v1 = __uint_as_float(h32[q] & 0xffff0000u) * sc[2 * q + 1] + sh[2 * q + 1] +
-                         __uint_as_float(s32[q] & 0xffff0000u) * ps[2 * q + 1] + pt[2 * q + 1];
+        const float v0 = lo2f(h32[q]) * sc[2 * q] + sh[2 * q] +
+                         lo2f(s32[q]) * ps[2 * q] + pt[2 * q];
+        const float v1 = hi2f(h32[q]) * sc[2 * q + 1] + sh[2 * q + 1] +
+                         hi2f(s32[q]) * ps[2 * q + 1] + pt[2 * q + 1];
         r[q] = pack2bf(fmaxf(v0, 0.f), fmaxf(v1, 0.f));
       }
       *reinterpret_cast<uint4*>(out + i * 8) = make_uint4(r[0], r[1], r[2], r[3]);
@@ -880,9 +881,10 @@ DTF_API int dtf_cg_gap(const GapArgs* a, int which, int nimg, hipStream_t stream
 DTF_API int dtf_cg_softmax_ce(const float* logits, int ld, int ncls, const int* labels, const int* img_slot,
                               const float* state, long s_mstride, int b_off, dtf_acc_t* grads, long g_mstride,
                               const float* cnt, dtf_acc_t* loss, float* correct, bf16_t* dl, long nimg,
-                              hipStream_t stream) {
+                              float loss_scale, hipStream_t stream) {
   if (nimg <= 0) return 0;
   hipLaunchKernelGGL(cg_softmax_ce_kernel, dim3((unsigned)((nimg + 3) / 4)), dim3(256), 0, stream, logits, ld, ncls,
-                     labels, img_slot, state, s_mstride, b_off, grads, g_mstride, cnt, loss, correct, dl, nimg);
+                     labels, img_slot, state, s_mstride, b_off, grads, g_mstride, cnt, loss, correct, dl, nimg,
+                     loss_scale);
   return DTF_CHECK_LAUNCH();
 }

@@ -34,3 +34,12 @@ extern "C" __attribute__((visibility("default"))) int dtf_build_deterministic() 
   return 0;
 #endif
 }
+// 1: the half build (-DDTF_HALF: fp16 activation / weight-shadow storage, v_mfma_f32_16x16x32_f16), selected by
+// --dtype fp16 (DTF_HALF=1); 0: bf16
+extern "C" __attribute__((visibility("default"))) int dtf_build_half() {
+#ifdef DTF_HALF
+  return 1;
+#else
+  return 0;
+#endif
+}

@@ -22,7 +22,7 @@ namespace {
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  return dtf_mfma16(a, b, c);
 }
 
 __device__ __forceinline__ s16x4_t ds_read_tr(const bf16_t* p) {

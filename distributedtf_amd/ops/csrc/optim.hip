@@ -55,7 +55,7 @@ __device__ __forceinline__ void update1(float& w, float& a, float& b, float g, c
 
 template <int OPT>
 __device__ void run_row(float* __restrict__ w, float* __restrict__ a, float* __restrict__ b, float* __restrict__ gr,
-                        bf16_t* __restrict__ sh, long P, long n_reg, const Hyper& h, int zero_grads) {
+                        bf16_t* __restrict__ sh, long P, long n_reg, const Hyper& h, int zero_grads, float gscale) {
   float lr_t = h.lr;
   if constexpr (OPT == 2) lr_t = h.lr * sqrtf(1.f - powf(0.999f, h.t)) / (1.f - powf(0.9f, h.t));
   const long stride = (long)gridDim.x * blockDim.x * 4;
@@ -71,7 +71,7 @@ __device__ void run_row(float* __restrict__ w, float* __restrict__ a, float* __r
     float bb[4] = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      float g = gg[j];
+      float g = gg[j] * gscale;  // static loss scaling (fp16): the gradients of S * loss, unscaled here
       if (h.reg != 0 && i + j < n_reg) g = reg_grad(g, ww[j], h.wd, h.reg);
       update1<OPT>(ww[j], aa[j], bb[j], g, h, lr_t);
     }
@@ -90,7 +90,8 @@ __device__ void run_row(float* __restrict__ w, float* __restrict__ a, float* __r
 
 __global__ __launch_bounds__(256) void fused_optimizer_kernel(float* __restrict__ state, float* __restrict__ grads,
                                                                const float* __restrict__ hyper, bf16_t* __restrict__ shadow,
-                                                               long S, long Pp, long P, long n_reg, int zero_grads) {
+                                                               long S, long Pp, long P, long n_reg, int zero_grads,
+                                                               float gscale) {
   const int g = blockIdx.y;
   const float* hp = hyper + g * 8;
   if (hp[7] == 0.f) return;
@@ -108,12 +109,12 @@ __global__ __launch_bounds__(256) void fused_optimizer_kernel(float* __restrict_
   float* gr = grads + (long)g * Pp;
   bf16_t* sh = shadow ? shadow + (long)g * Pp : nullptr;
   switch (h.opt) {
-    case 0: run_row<0>(w, a, b, gr, sh, P, n_reg, h, zero_grads); break;
-    case 1: run_row<1>(w, a, b, gr, sh, P, n_reg, h, zero_grads); break;
-    case 2: run_row<2>(w, a, b, gr, sh, P, n_reg, h, zero_grads); break;
-    case 3: run_row<3>(w, a, b, gr, sh, P, n_reg, h, zero_grads); break;
-    case 4: run_row<4>(w, a, b, gr, sh, P, n_reg, h, zero_grads); break;
-    default: run_row<5>(w, a, b, gr, sh, P, n_reg, h, zero_grads); break;
+    case 0: run_row<0>(w, a, b, gr, sh, P, n_reg, h, zero_grads, gscale); break;
+    case 1: run_row<1>(w, a, b, gr, sh, P, n_reg, h, zero_grads, gscale); break;
+    case 2: run_row<2>(w, a, b, gr, sh, P, n_reg, h, zero_grads, gscale); break;
+    case 3: run_row<3>(w, a, b, gr, sh, P, n_reg, h, zero_grads, gscale); break;
+    case 4: run_row<4>(w, a, b, gr, sh, P, n_reg, h, zero_grads, gscale); break;
+    default: run_row<5>(w, a, b, gr, sh, P, n_reg, h, zero_grads, gscale); break;
   }
 }
 
@@ -168,15 +169,16 @@ DTF_API int dtf_step_end(float* state, long S, long col, float* hyper, int h_ste
   return DTF_CHECK_LAUNCH();
 }
 
+// gscale: factor on every gradient before the update (1 / the static loss scale of the fp16 mode, else 1)
 DTF_API int dtf_fused_optimizer(float* state, float* grads, const float* hyper, bf16_t* shadow, int G, long S, long Pp,
-                                long P, long n_reg, int zero_grads, hipStream_t stream) {
+                                long P, long n_reg, int zero_grads, float gscale, hipStream_t stream) {
   if (G <= 0) return 0;
   long per_block = 256 * 4;
   long blocks = (P + per_block - 1) / per_block;
   if (blocks > 512) blocks = 512;  // grid-stride; G*512 blocks >> 256 CUs
   dim3 grid((unsigned)blocks, (unsigned)G);
   hipLaunchKernelGGL(fused_optimizer_kernel, grid, dim3(256), 0, stream, state, grads, hyper, shadow, S, Pp, P, n_reg,
-                     zero_grads);
+                     zero_grads, gscale);
   return DTF_CHECK_LAUNCH();
 }
 

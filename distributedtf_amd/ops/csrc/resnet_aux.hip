@@ -295,6 +295,7 @@ struct HeadArgs {
   int train;
   float* slab;            // optional [nblocks][ncls * C] per-workgroup dense-weight gradients (else atomics)
   float* slab_b;          // optional [nblocks][ncls] per-workgroup bias gradients
+  float loss_scale;       // the loss gradient is taken of loss_scale * loss (fp16 static loss scaling; else 1)
 };
 
 // Head of the CIFAR ResNet (C == 64 final channels, hw % 32 == 0, hw <= 128, ncls <= 16).  One image at a time
@@ -325,6 +326,7 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   const int cg = threadIdx.x & 7, c8 = cg * 8, pix0 = threadIdx.x >> 3;  // this thread's 8 channels / first pixel
   const float* prow = a.params + (long)slot * a.p_mstride;
   const float bsz = a.cnt[slot];
+  const float gsc = a.loss_scale / bsz;
   const int nk = a.hw / 32;
   // first image's loads before the coefficient math
   uint4 xv[HEAD_MAXK];
@@ -451,7 +453,7 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         if (j < ncls) {
-          const float dl = (__expf(logit[j] - lse) - (j == lab ? 1.f : 0.f)) / bsz;
+          const float dl = (__expf(logit[j] - lse) - (j == lab ? 1.f : 0.f)) * gsc;
           dfeat += wcol[j] * dl;
           if (wave == 0) {
             dw[j] += dl * f;

@@ -19,6 +19,7 @@ no fp16 with ResNet v1 (``resnet_run_loop.py:546-549``).
 from __future__ import annotations
 
 import argparse
+import os
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional
 
@@ -208,6 +209,9 @@ class MainArgs(argparse.Namespace):
             os.environ["DTF_DETERMINISTIC"] = "1"  # ops.lib() loads the deterministic build
             if self.backend == "auto" and not hip_deterministic(self):
                 self.backend = "torch"  # this family's HIP path still has order-dependent reductions
+        if (getattr(self, "dtype", "bf16") == "fp16" and self.backend != "torch"
+                and self.model in ("cifar10", "imagenet") and self.resnet_version == 2):
+            os.environ["DTF_HALF"] = "1"  # ops.lib() loads the fp16 build of the kernels (libdtf_kernels_f16.so)
 
     def inject_nan_schedule(self) -> Dict[int, List[int]]:
         out: Dict[int, List[int]] = {}
@@ -239,6 +243,14 @@ def parse_main_args(argv=None, defaults=None) -> MainArgs:
             if args.backend == "hip":
                 p.error("--loss_scale with --dtype fp32: the fp32 HIP step does not scale the loss; use --backend torch")
             args.backend = "torch"
+    elif args.dtype == "fp16" and args.model in ("cifar10", "imagenet") and args.resnet_version == 2:
+        # fp16 ResNet v2 runs the half build of the HIP kernels (ops/csrc/common.h DTF_HALF: fp16 storage,
+        # v_mfma_f32_16x16x32_f16) with the reference's static loss scaling (default 128, _performance.py:30-33):
+        # the head differentiates loss_scale * loss, the fused optimizer unscales (resnet_run_loop.py:284-294)
+        if (args.deterministic or args.debug_kernels) and args.backend != "torch":
+            p.error("--dtype fp16 with --deterministic / --debug_kernels: the fp16 kernel build has no "
+                    "deterministic or debug variant; use --backend torch")
+        # (apply_runtime_modes sets DTF_HALF=1: ops.lib() then loads libdtf_kernels_f16.so)
     elif args.dtype != "bf16" and args.model != "toy":
         # the other families' kernels compute in bf16 (fp32 master weights / statistics); their fp32 and fp16
         # (static loss scaling) run on the PyTorch backend

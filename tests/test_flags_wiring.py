@@ -90,7 +90,14 @@ def test_dtype_routing():
     with pytest.raises(SystemExit):
         parse_main_args(["--model", "cifar10", "--loss_scale", "8"])  # bf16 HIP path: no loss scaling
     a = parse_main_args(["--model", "cifar10", "--dtype", "fp16"])
-    assert a.backend == "torch" and a.model_kwargs()["loss_scale"] == 128
+    # fp16 ResNet v2: the half build of the HIP kernels (DTF_HALF, set by apply_runtime_modes) with loss scale 128
+    assert a.backend == "auto" and a.model_kwargs()["loss_scale"] == 128
+    assert parse_main_args(["--model", "imagenet", "--dtype", "fp16", "--backend", "hip"]).backend == "hip"
+    assert parse_main_args(["--model", "mnist", "--dtype", "fp16"]).backend == "torch"  # no fp16 MNIST kernels
+    with pytest.raises(SystemExit):  # the reference's validator: fp16 is not supported with ResNet v1
+        parse_main_args(["--model", "cifar10", "--dtype", "fp16", "--resnet_version", "1"])
+    with pytest.raises(SystemExit):  # no deterministic fp16 kernel build
+        parse_main_args(["--model", "cifar10", "--dtype", "fp16", "--deterministic", "--backend", "hip"])
     with pytest.raises(SystemExit):
         parse_main_args(["--benchmark_logger_type", "BenchmarkFileLogger"])
 

@@ -147,8 +147,29 @@ class SlabJob(ctypes.Structure):
 
 
 class WorkGenDesc(ctypes.Structure):
-    _fields_ = [("dst", c_void_p), ("per", c_int), ("bands", c_int), ("min_chunk", c_int), ("split", c_int),
-                ("pad0", c_int), ("pad1", c_int)]
+    _fields_ = [("dst", c_void_p), ("red", c_void_p), ("per", c_int), ("bands", c_int), ("min_chunk", c_int),
+                ("split", c_int), ("prop", c_int), ("pad", c_int)]
+
+
+# elastic work tables deal their rows out in proportion to the members' batch sizes (resnet_aux.hip work_gen_kernel,
+# prop = 1) instead of `per` rows per member; the deterministic build keeps the fixed split (its replay caps the
+# workgroups per member)
+ELASTIC_PROP = os.environ.get("DTF_ELASTIC_PROP", "1") == "1"
+
+
+def elastic_rows(totals, per, min_chunk, prop):
+    """Host mirror of work_gen_kernel: [(first row, rows, chunk)] per member for these iteration totals."""
+    M = len(totals)
+    R = per * M
+    if prop and R > M:
+        chunk = max(min_chunk, -(-sum(totals) // (R - M)), 1)
+        out, r0 = [], 0
+        for k, t in enumerate(totals):
+            n = max(1, -(-t // chunk)) if k + 1 < M else R - r0
+            out.append((r0, n, chunk))
+            r0 += n
+        return out
+    return [(k * per, per, max(min_chunk, -(-t // per), 1)) for k, t in enumerate(totals)]
 
 
 class DenseJob(ctypes.Structure):
@@ -857,24 +878,28 @@ class _StepPlan:
         sizes (work_gen_kernel; same split rule as _work_iters / _work_member, empty rows past a member's end)."""
         rows = 2 if split else 1
         host = []
-        for s, n in zip(self.slots, self.real_sizes):
+        prop = int(ELASTIC_PROP and not self.be.det)
+        layout = elastic_rows([n * bands for n in self.real_sizes], per, min_chunk, prop)
+        for (s, n), (r0, nrows, chunk) in zip(zip(self.slots, self.real_sizes), layout):
             total, f = n * bands, self.first[s] * bands
-            chunk = max(min_chunk, -(-total // per), 1)
-            for j in range(per):
+            for j in range(nrows):
                 st = j * chunk
                 nit = min(chunk, total - st) if st < total else 0
                 for z in range(rows):
                     host.append([f + st if nit > 0 else f, nit, z, s])
+        assert len(host) == per * len(self.slots) * rows
         w = torch.tensor(host, dtype=torch.int32, device=self.be.dev)
-        self._wgen.append((w, per, bands, min_chunk, int(split)))
+        self._wgen.append((w, per, bands, min_chunk, int(split), prop))
         self.__dict__.setdefault("_wgen_params", {})[w.data_ptr()] = (per, bands, min_chunk)
         return w
 
     def _work_gen_launch(self):
         """First launch of an elastic step: regenerate every work table from the per-member sizes (self.cnt)."""
         descs = (WorkGenDesc * len(self._wgen))()
-        for i, (w, per, bands, mc, sp) in enumerate(self._wgen):
-            descs[i] = WorkGenDesc(w.data_ptr(), per, bands, mc, sp, 0, 0)
+        red = getattr(self, "_elastic_red", {})
+        for i, (w, per, bands, mc, sp, prop) in enumerate(self._wgen):
+            # the slab-reduction table over this work table (one per member), rewritten with it every step
+            descs[i] = WorkGenDesc(w.data_ptr(), _p(red.get(w.data_ptr())), per, bands, mc, sp, prop, 0)
         dt = torch.frombuffer(bytearray(bytes(descs)), dtype=torch.uint8).to(self.be.dev)
         self._keep(dt)
         self.launches.insert(0, (ops.lib().dtf_work_gen, (_p(dt), len(self._wgen), _p(self.slots_t),
@@ -1513,7 +1538,11 @@ class _StepPlan:
         return self.slab_buf
 
     def _slab_table(self, work):
-        """(first wg, n wgs, 0, slot) per member of a work-item array grouped by member."""
+        """(first wg, n wgs, 0, slot) per member of a work-item array grouped by member.  An elastic work table's rows
+        per member change with the batch sizes: its table is shared and rewritten on the device by work_gen."""
+        red = self.__dict__.setdefault("_elastic_red", {})
+        if work.data_ptr() in red:
+            return red[work.data_ptr()]
         w = work.cpu().tolist()
         rows = []
         for i, it in enumerate(w):
@@ -1523,6 +1552,9 @@ class _StepPlan:
                 rows.append([i, 1, 0, it[3]])
         t = torch.tensor(rows, dtype=torch.int32, device=self.be.dev)
         self._keep(t)
+        if self.elastic and any(wg[0].data_ptr() == work.data_ptr() for wg in self._wgen):
+            assert len(rows) == len(self.slots), "elastic slab table: one row per member"
+            red[work.data_ptr()] = t
         return t
 
     def _stamp_row(self, kind, label=""):

@@ -145,33 +145,62 @@ __global__ __launch_bounds__(64) void bn_running_update_kernel(float* __restrict
 
 // Elastic (capacity-keyed) step plans: every work table of the captured step is regenerated on the device from
 // the per-member batch sizes (cnt) at the start of each replay, so a batch-size change needs no new plan or graph.
-// Member m owns `per` rows (x2 for a split table): row j covers iterations [j*chunk, j*chunk + chunk) of the
-// member's n * bands (image, band) iterations, chunk = max(min_chunk, ceil(n * bands / per)); rows past the end get
-// nit = 0 (the kernels skip their loop and write zero partials) and point at the member's first iteration.
+// The table holds R = per * M rows (x2 entries per row for a split table) for M members.
+//  prop = 0 (the deterministic build, whose replay needs <= `per` rows per member): member m owns rows
+//    [m*per, m*per + per); row j covers iterations [j*chunk_m, j*chunk_m + chunk_m) of the member's n * bands
+//    (image, band) iterations, chunk_m = max(min_chunk, ceil(n * bands / per)).
+//  prop = 1 (default): rows are dealt out in proportion to the members' sizes with ONE chunk for the whole table,
+//    chunk = max(min_chunk, ceil(sum_m n_m * bands / (R - M))), member m gets max(1, ceil(total_m / chunk)) rows
+//    (sum <= R) in member order and the last member also owns the unused tail.  With fixed rows per member a ragged
+//    population (PBT samples batch sizes 65..255, constants.py:91-93) ran every launch at the pace of its largest
+//    member: that member's rows carried up to 4x the iterations of the smallest member's.
+// Rows past a member's iterations get nit = 0 (the kernels skip their loop and write zero partials) and point at
+// the member's first iteration.  `red` (optional): the per-member (first entry, entries, 0, slot) table of the dW
+// slab reductions over this work table, rewritten to match.
 struct WorkGenDesc {
   int4* dst;
+  int4* red;
   int per, bands, min_chunk, split;
-  int pad0, pad1;
+  int prop, pad;
 };
 
 __global__ __launch_bounds__(256) void work_gen_kernel(const WorkGenDesc* __restrict__ descs,
                                                        const int* __restrict__ slots, const int* __restrict__ first,
-                                                       const float* __restrict__ cnt) {
+                                                       const float* __restrict__ cnt, int nslots) {
   const WorkGenDesc d = descs[blockIdx.x];
   const int m = blockIdx.y;
   const int slot = slots[m];
   const int total = (int)cnt[slot] * d.bands;
   const int f = first[m] * d.bands;
-  int chunk = (total + d.per - 1) / d.per;
-  if (chunk < d.min_chunk) chunk = d.min_chunk;
-  if (chunk < 1) chunk = 1;
   const int rows = d.split ? 2 : 1;
-  for (int j = threadIdx.x; j < d.per; j += blockDim.x) {
+  const int R = d.per * nslots;
+  int chunk, row0, nrows;
+  if (d.prop && R > nslots) {
+    int sum = 0, before = 0;  // rows of the members ahead of m (every member computes the same chunk)
+    for (int k = 0; k < nslots; ++k) sum += (int)cnt[slots[k]] * d.bands;
+    chunk = (sum + (R - nslots) - 1) / (R - nslots);
+    if (chunk < d.min_chunk) chunk = d.min_chunk;
+    if (chunk < 1) chunk = 1;
+    for (int k = 0; k < m; ++k) {
+      const int tk = (int)cnt[slots[k]] * d.bands;
+      before += max(1, (tk + chunk - 1) / chunk);
+    }
+    row0 = before;
+    nrows = m + 1 < nslots ? max(1, (total + chunk - 1) / chunk) : R - before;  // the last member takes the tail
+  } else {
+    chunk = (total + d.per - 1) / d.per;
+    if (chunk < d.min_chunk) chunk = d.min_chunk;
+    if (chunk < 1) chunk = 1;
+    row0 = m * d.per;
+    nrows = d.per;
+  }
+  for (int j = threadIdx.x; j < nrows; j += blockDim.x) {
     const int start = j * chunk;
     const int nit = start < total ? min(chunk, total - start) : 0;
     const int it0 = nit > 0 ? f + start : f;
-    for (int z = 0; z < rows; ++z) d.dst[((long)m * d.per + j) * rows + z] = make_int4(it0, nit, z, slot);
+    for (int z = 0; z < rows; ++z) d.dst[((long)row0 + j) * rows + z] = make_int4(it0, nit, z, slot);
   }
+  if (d.red != nullptr && threadIdx.x == 0) d.red[m] = make_int4(row0 * rows, nrows * rows, 0, slot);
 }
 
 // Eval mode: BatchNorm with the moving statistics.  Every consumer derives its coefficients from replicated
@@ -881,7 +910,7 @@ DTF_API int dtf_work_gen(const void* descs, int ndesc, const int* slots, const i
   if (ndesc <= 0 || nslots <= 0) return 0;
   DTF_HOST_CHECK(descs != nullptr && slots != nullptr && first != nullptr && cnt != nullptr && ndesc <= 65535);
   hipLaunchKernelGGL(work_gen_kernel, dim3(ndesc, nslots), dim3(256), 0, stream,
-                     reinterpret_cast<const WorkGenDesc*>(descs), slots, first, cnt);
+                     reinterpret_cast<const WorkGenDesc*>(descs), slots, first, cnt, nslots);
   return DTF_CHECK_LAUNCH();
 }
 

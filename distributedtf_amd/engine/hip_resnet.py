@@ -408,20 +408,45 @@ def note_step_advanced(e, slots):
                 dev[s][H_STEP] += 1.0
 
 
-def advance_steps(e, slots_long, slots_i32=None, loss=None, loss_sel=None):
+def advance_steps(e, slots_long, slots_i32=None, loss=None, loss_sel=None, ring=None):
     """Inside the captured step: per-member step counters (state column + hyper table) += 1 and, given
     ``loss``/``loss_sel``, the per-member losses gathered in slot-list order (one kernel when the int32 slot list is
-    given)."""
+    given).  ``ring`` = (rows [R, n] fp32, index int32 [1]): the losses go to the ring's next row instead of
+    ``loss_sel`` (LossRing)."""
     from .optim import H_STEP
     if slots_i32 is not None and e.device.type == "cuda":
+        rb, ri = (ring.rows, ring.idx) if ring is not None else (None, None)
         ops.check(ops.lib().dtf_step_end(_p(e.state), e.S, 3 * e.Pp + e.R, _p(e.hyper), H_STEP, _p(slots_i32),
-                                         slots_i32.numel(), _p(loss), _p(loss_sel), ops.stream()), "step_end")
+                                         slots_i32.numel(), _p(loss), _p(loss_sel) if ring is None else None,
+                                         _p(rb), _p(ri), rb.shape[0] if rb is not None else 0, ops.stream()),
+                  "step_end")
         return
     one = torch.ones(slots_long.numel(), device=e.device)
     e.step_col().index_add_(0, slots_long, one)
     e.hyper[:, H_STEP].index_add_(0, slots_long, one)
     if loss_sel is not None:
         torch.index_select(loss, 0, slots_long, out=loss_sel)
+
+
+class LossRing:
+    """Per-step member losses without a per-step copy: the captured step's step_end kernel writes each replay's
+    losses into the next row of a [rows, n] device ring (the row index lives on the device), and the host hands out
+    a VIEW of that row.  A view stays valid for ``rows`` later steps; engine_model._train_cycle clones a member's
+    last loss when the member leaves the active set (before its view can be overwritten)."""
+
+    ROWS = 4096
+
+    def __init__(self, n, device):
+        self.rows = torch.zeros(self.ROWS, n, dtype=torch.float32, device=device)
+        self.idx = torch.zeros(1, dtype=torch.int32, device=device)
+        self.k = 0  # host mirror of idx: steps executed
+
+    def advance(self):
+        self.k += 1
+
+    def last(self):
+        assert self.k > 0
+        return self.rows[(self.k - 1) % self.ROWS]
 
 
 _LIVE_GRAPH_PLANS = weakref.WeakSet()  # plans holding a captured step graph (released before RCCL teardown)
@@ -736,6 +761,7 @@ class _StepPlan:
         self.slots_t = torch.tensor(slots, dtype=torch.int32, device=dev)
         self.slots_long = torch.tensor(slots, dtype=torch.long, device=dev)
         self.loss_sel = torch.zeros(len(slots), dtype=be.loss.dtype, device=dev)
+        self.ring = LossRing(len(slots), dev) if (dev.type == "cuda" and not eval_mode and len(slots) <= 1024) else None
         H = cfg.image_size
         self.x_in = torch.zeros(N, H, H, 3, dtype=torch.float32, device=dev)
         self.labels = torch.zeros(N, dtype=torch.int32, device=dev)
@@ -1983,7 +2009,7 @@ class _StepPlan:
             elif fn == "step":
                 # step counters + per-member losses gathered inside the step (graph) so a replay leaves one copy
                 # for loss_view
-                advance_steps(e, self.slots_long, self.slots_t, self.be.loss, self.loss_sel)
+                advance_steps(e, self.slots_long, self.slots_t, self.be.loss, self.loss_sel, ring=self.ring)
             else:
                 err = fn(*args, ops.stream())
                 if err != 0:
@@ -1995,7 +2021,10 @@ class _StepPlan:
 
     def run(self, train=True):
         run_captured(self)
+        if self.ring is not None:
+            self.ring.advance()
 
     def loss_view(self):
-        # a copy: callers keep per-step losses across later replays (engine_model.loss_acc)
-        return self.loss_sel.clone()
+        # callers keep per-step losses across later replays (engine_model.loss_acc): a ring row (valid for
+        # LossRing.ROWS steps), else a copy
+        return self.ring.last() if self.ring is not None else self.loss_sel.clone()

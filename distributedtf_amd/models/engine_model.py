@@ -370,7 +370,9 @@ class EngineModel(ModelBase):
                     b = datasets.batch_len(batches[i])
                     by_slot[s].images_trained += b
                     n_img += b
-                    loss_acc[s] = losses[i]  # view, no host sync
+                    # a view (no host sync); a member's LAST step is copied: the view may be a LossRing row that later
+                    # steps of the still-active members overwrite
+                    loss_acc[s] = losses[i] if todo[s] > done + 1 else losses[i].clone()
                 done += 1
                 if hooks:
                     eng.hook_step += 1

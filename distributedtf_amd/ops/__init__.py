@@ -28,7 +28,8 @@ _SIGNATURES = {
                             c_float, c_void_p],
     "dtf_shadow_refresh": [c_void_p, c_void_p, c_void_p, c_int, c_long, c_long, c_long, c_void_p],
     "dtf_step_advance": [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_int, c_void_p],
-    "dtf_step_end": [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p],
+    "dtf_step_end": [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                     c_void_p, c_int, c_void_p],
 }
 
 

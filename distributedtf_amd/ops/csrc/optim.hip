@@ -138,16 +138,26 @@ __global__ __launch_bounds__(256) void shadow_refresh_kernel(const float* __rest
 // Per-member step counters after a captured step: state[slot][col] += 1 and hyper[slot][h_step] += 1 for every
 // ACTIVE listed member (hyper column 7; an elastic plan replayed for a subset of its members leaves the others
 // untouched); optionally the step's per-member losses gathered in slot-list order (loss_sel[i] = loss[slots[i]]).
+// ring (optional, single-block launches): the losses go to row (*ring_idx % ring_rows) of a [ring_rows][n] ring and
+// the index advances -- every replay of a captured step leaves its losses in a row of their own, so the host keeps
+// per-step loss views without a per-step copy launch
 __global__ void step_advance_kernel(float* __restrict__ state, long S, long col, float* __restrict__ hyper,
                                     int h_step, const int* __restrict__ slots, int n, const float* __restrict__ loss,
-                                    float* __restrict__ loss_sel) {
+                                    float* __restrict__ loss_sel, float* __restrict__ ring, int* __restrict__ ring_idx,
+                                    int ring_rows) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int r = ring != nullptr ? *ring_idx : 0;
   if (i < n) {
     const int s = slots[i];
     const float inc = hyper[s * 8 + 7] != 0.f ? 1.f : 0.f;
     state[(long)s * S + col] += inc;
     hyper[s * 8 + h_step] += inc;
     if (loss_sel != nullptr) loss_sel[i] = loss[s];
+    if (ring != nullptr) ring[(long)(r % ring_rows) * n + i] = loss[s];
+  }
+  if (ring != nullptr) {
+    __syncthreads();  // every thread has read the index
+    if (threadIdx.x == 0) *ring_idx = r + 1;
   }
 }
 
@@ -157,15 +167,18 @@ DTF_API int dtf_step_advance(float* state, long S, long col, float* hyper, int h
                              hipStream_t stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(step_advance_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, state, S, col, hyper, h_step,
-                     slots, n, (const float*)nullptr, (float*)nullptr);
+                     slots, n, (const float*)nullptr, (float*)nullptr, (float*)nullptr, (int*)nullptr, 1);
   return DTF_CHECK_LAUNCH();
 }
 
 DTF_API int dtf_step_end(float* state, long S, long col, float* hyper, int h_step, const int* slots, int n,
-                         const float* loss, float* loss_sel, hipStream_t stream) {
+                         const float* loss, float* loss_sel, float* ring, int* ring_idx, int ring_rows,
+                         hipStream_t stream) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(step_advance_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, state, S, col, hyper, h_step,
-                     slots, n, loss, loss_sel);
+  if (ring != nullptr && (n > 1024 || ring_idx == nullptr || ring_rows <= 0)) return -2;  // one block
+  const int threads = ring != nullptr ? ((n + 63) / 64) * 64 : 64;
+  hipLaunchKernelGGL(step_advance_kernel, dim3(ring != nullptr ? 1 : (n + 63) / 64), dim3(threads), 0, stream, state,
+                     S, col, hyper, h_step, slots, n, loss, loss_sel, ring, ring_idx, ring_rows);
   return DTF_CHECK_LAUNCH();
 }
 

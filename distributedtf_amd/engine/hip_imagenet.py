@@ -43,6 +43,9 @@ _CG_WIDE7 = True  # one 64 x 416 tile for the 7x7 stem
 _CG_WIDE1 = True  # the wide tiles for 1x1 convs with Ci % 256 == 0
 _CG_TP256_128 = True  # 128 x 256 tiles (2 x 2 waves of 64 x 128)
 _CG_TP256 = True  # 256-pixel forward / dgrad tiles for 64-channel outputs
+# v_mfma_f32_32x32x16_bf16 tiles for the plain-A forward convolutions with 128-channel tiles (1x1 / strided / 7x7-stage
+# convs with C_out >= 128): 32 x 32 MFMA tiles of each wave's 64 x 128 block (convg_fwd_kernel M32)
+_CG_M32 = os.environ.get("DTF_CG_M32", "0") == "1"
 _CG_WPK_WO64 = 32  # pixels per k-step of the 64-row tiles
 # stride-1 3x3 forward / data gradient with LDS-resident input rows (convg_t3_kernel): image width -> rows per tile
 _CG_T3 = {56: 8, 28: 7, 14: 14}  # must match dtf_convg_t3 (rows divide the image height)
@@ -520,6 +523,8 @@ class _ImageNetPlan:
         if (tc == 64 and _CG_TP256) or (tc == 128 and _CG_TP256_128):
             trans |= 8  # 256-pixel tiles (BK = 32): 1 x 4 waves of 64 x 64, or 2 x 2 of 64 x 128 for tc 128
             tp = 256
+            if _CG_M32 and tc == 128 and not dgrad:
+                trans |= 16  # 32x32x16 MFMA tiles
         elif _CG_BK == 64 and (not trans or a.Ci >= 64):
             trans |= 4  # k depth 64 per LDS stage
         work = (self._pix_work(hw_in, a.Co, tc, classes=(0, 1, 2, 3), tp=tp) if trans & 1

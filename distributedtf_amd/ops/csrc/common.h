@@ -43,6 +43,10 @@ __device__ __forceinline__ f32x4_t dtf_mfma16(const bf16x8_t& a, const bf16x8_t&
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h16x8_t, a), __builtin_bit_cast(h16x8_t, b), c,
                                                  0, 0, 0);
 }
+__device__ __forceinline__ f32x16_t dtf_mfma32(const bf16x8_t& a, const bf16x8_t& b, const f32x16_t& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h16x8_t, a), __builtin_bit_cast(h16x8_t, b), c,
+                                                 0, 0, 0);
+}
 #define DTF_HALF_BUILD 1
 #else
 typedef __bf16 bf16x2v_t __attribute__((ext_vector_type(2)));
@@ -59,6 +63,9 @@ __device__ __forceinline__ uint32_t pk2(f32x2_t v) {  // v_cvt_pk_bf16_f32
 }
 __device__ __forceinline__ f32x4_t dtf_mfma16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16_t dtf_mfma32(const bf16x8_t& a, const bf16x8_t& b, const f32x16_t& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 #define DTF_HALF_BUILD 0
 #endif

@@ -98,14 +98,14 @@ struct CgArgs {
 // Epilogue shared by the forward / data-gradient kernels: the fp32 accumulator tile (wave grid WRN x 4/WRN of
 // (TC/WRN) x (TP/(4/WRN)) per wave) goes through LDS (cst, NHALF passes), then [+ residual], [mask by BN(xm)+ReLU],
 // bf16 store and per-channel statistics.
-template <int TC, int EPI, bool TRANS, int TP, int WRN, int NHALF>
-__device__ __forceinline__ void convg_epilogue(const CgArgs& a, f32x4_t (&acc)[TC / WRN / 16][TP / (4 / WRN) / 16],
-                                               float* cst, dtf_acc_t (&acc_lds)[2][TC], int slot, int o0, int p0, int p1,
-                                               int HWo, int GW, int py, int px) {
-  constexpr int PW = TP / (4 / WRN), NTP = PW / 16, MT = TC / WRN / 16;
-  constexpr int CPF = TC + 4;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int wr = wave % WRN, wc = wave / WRN;
+// stage(h): writes staging part h (pixel rows [h * TP / NHALF, (h + 1) * TP / NHALF) of the tile) into cst as
+// [pixel][channel] fp32 rows of pitch TC + 4 (the MFMA-shape-specific half; convg_epilogue below for 16x16 tiles,
+// convg_epilogue32 for 32x32 ones)
+template <int TC, int EPI, bool TRANS, int TP, int NHALF, class StageFn>
+__device__ __forceinline__ void convg_epilogue_impl(const CgArgs& a, StageFn&& stage, float* cst,
+                                                    dtf_acc_t (&acc_lds)[2][TC], int slot, int o0, int p0, int p1,
+                                                    int HWo, int GW, int py, int px) {
+  const int tid = threadIdx.x, lane = tid & 63;
   // ---- epilogue through LDS: the fp32 tile is staged as [pixel][channel] rows (the k loop ended with a barrier,
   // so the operand buffers are free), then every thread owns one 16-byte channel chunk of a pixel row: the
   // residual / mask loads and the bf16 store are whole contiguous row segments (TC * 2 bytes per pixel) instead
@@ -133,18 +133,10 @@ __device__ __forceinline__ void convg_epilogue(const CgArgs& a, f32x4_t (&acc)[T
   float ss[8], sq[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) ss[i] = sq[i] = 0.f;
+  constexpr int CPF = TC + 4;
   for (int h = 0; h < NHALF; ++h) {
     if (h > 0) __syncthreads();  // the previous half's rows have been read
-#pragma unroll
-    for (int n = 0; n < NTP; ++n) {
-      const int pl = wc * PW + 16 * n - h * (TP / NHALF);  // staged row of this 16-pixel tile (wave-uniform)
-      if (NHALF == 1 || (pl >= 0 && pl < TP / NHALF)) {
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-          *reinterpret_cast<f32x4_t*>(cst + (pl + (lane & 15)) * CPF + wr * (TC / WRN) + 16 * m + 4 * (lane >> 4)) =
-              acc[m][n];
-      }
-    }
+    stage(h);
     __syncthreads();
     // all residual / mask rows of this half are loaded before the first store (the stores may alias them for the
     // compiler), so a thread keeps NPASS 16-byte loads in flight instead of one per pass
@@ -236,6 +228,58 @@ __device__ __forceinline__ void convg_epilogue(const CgArgs& a, f32x4_t (&acc)[T
   }
 }
 
+template <int TC, int EPI, bool TRANS, int TP, int WRN, int NHALF>
+__device__ __forceinline__ void convg_epilogue(const CgArgs& a, f32x4_t (&acc)[TC / WRN / 16][TP / (4 / WRN) / 16],
+                                               float* cst, dtf_acc_t (&acc_lds)[2][TC], int slot, int o0, int p0, int p1,
+                                               int HWo, int GW, int py, int px) {
+  constexpr int PW = TP / (4 / WRN), NTP = PW / 16, MT = TC / WRN / 16;
+  constexpr int CPF = TC + 4;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wave % WRN, wc = wave / WRN;
+  auto stage = [&](int h) {
+#pragma unroll
+    for (int n = 0; n < NTP; ++n) {
+      const int pl = wc * PW + 16 * n - h * (TP / NHALF);  // staged row of this 16-pixel tile (wave-uniform)
+      if (NHALF == 1 || (pl >= 0 && pl < TP / NHALF)) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          *reinterpret_cast<f32x4_t*>(cst + (pl + (lane & 15)) * CPF + wr * (TC / WRN) + 16 * m + 4 * (lane >> 4)) =
+              acc[m][n];
+      }
+    }
+  };
+  convg_epilogue_impl<TC, EPI, TRANS, TP, NHALF>(a, stage, cst, acc_lds, slot, o0, p0, p1, HWo, GW, py, px);
+}
+
+// 32x32 accumulator tiles (v_mfma_f32_32x32x16_bf16): register r of lane l holds D[row 8 (r >> 2) + 4 (l >> 5) +
+// (r & 3)][col l & 31] -- each group of 4 registers is 4 consecutive output channels of one pixel (one float4)
+template <int TC, int EPI, bool TRANS, int TP, int WRN, int NHALF>
+__device__ __forceinline__ void convg_epilogue32(const CgArgs& a, f32x16_t (&acc)[TC / WRN / 32][TP / (4 / WRN) / 32],
+                                                 float* cst, dtf_acc_t (&acc_lds)[2][TC], int slot, int o0, int p0,
+                                                 int p1, int HWo, int GW, int py, int px) {
+  constexpr int PW = TP / (4 / WRN), NT2 = PW / 32, MT2 = TC / WRN / 32;
+  constexpr int CPF = TC + 4;
+  static_assert((TP / NHALF) % 32 == 0, "32-pixel tiles must not straddle staging parts");
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wave % WRN, wc = wave / WRN;
+  auto stage = [&](int h) {
+#pragma unroll
+    for (int n = 0; n < NT2; ++n) {
+      const int pl = wc * PW + 32 * n - h * (TP / NHALF);
+      if (NHALF == 1 || (pl >= 0 && pl < TP / NHALF)) {
+#pragma unroll
+        for (int m = 0; m < MT2; ++m)
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<f32x4_t*>(cst + (pl + (lane & 31)) * CPF + wr * (TC / WRN) + 32 * m + 8 * g +
+                                        4 * (lane >> 5)) =
+                (f32x4_t){acc[m][n][4 * g], acc[m][n][4 * g + 1], acc[m][n][4 * g + 2], acc[m][n][4 * g + 3]};
+      }
+    }
+  };
+  convg_epilogue_impl<TC, EPI, TRANS, TP, NHALF>(a, stage, cst, acc_lds, slot, o0, p0, p1, HWo, GW, py, px);
+}
+
 // ---------------------------------------------------------------------------------------------- fwd / dgrad
 // MODE: 0 identity, 1 relu(x*s + t), 2 A*x + B*x2 + C.   EPI: bit0 residual, bit1 mask, bit2 stats (fwd: y, y^2;
 // with bit1: dz, dz*xhat).  TRANS: transposed (dgrad, stride > 1) gather.
@@ -247,9 +291,12 @@ __device__ __forceinline__ void convg_epilogue(const CgArgs& a, f32x4_t (&acc)[T
 // TP: pixels per workgroup tile.  128: 2 x 2 waves of (TC/2 rows x 64 pixels); 256: with TC = 64 1 x 4 waves of
 // 64 x 64 (twice the MFMA work per k-step and wave of the 32 x 64 wave tile a 64-row conv gets otherwise), with
 // TC = 128 2 x 2 waves of 64 x 128 (32 MFMAs per wave and k-step; the epilogue is staged in 64-pixel quarters).
-template <int TC, int MODE, int EPI, bool TRANS, bool AKM = false, int BK = 32, int TP = 128>
+// M32: v_mfma_f32_32x32x16_bf16 tiles (a wave's TC/WRN x PW block as 32 x 32 MFMA tiles: half the MFMA
+// instructions of the 16x16x32 form for the same fragment reads; plain-A (non-AKM) forward only)
+template <int TC, int MODE, int EPI, bool TRANS, bool AKM = false, int BK = 32, int TP = 128, bool M32 = false>
 __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   static_assert(TP == 128 || TP == 256, "pixel tile");
+  static_assert(!M32 || (!AKM && (TC / ((TP == 256 && TC == 64) ? 1 : 2)) % 32 == 0), "32x32 tiles: plain A");
   // wave grid: TC = 64 x TP = 256 -> 1 x 4 waves of 64 x 64; else 2 x 2 waves of (TC/2) x (TP/2)
   constexpr int WRN = (TP == 256 && TC == 64) ? 1 : 2;
   constexpr int PW = TP / (4 / WRN), NTP = PW / 16;  // pixels per wave, MFMA pixel tiles per wave
@@ -461,11 +508,22 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
         *reinterpret_cast<uint4*>(dst + (rB + RPT * j) * RP + 8 * cB) = v[j];
     }
   };
-  f32x4_t acc[MT][NTP];
+  constexpr int MT2 = M32 ? MT / 2 : 1, NT2 = M32 ? NTP / 2 : 1;
+  f32x4_t acc[M32 ? 1 : MT][M32 ? 1 : NTP];
+  f32x16_t acc32[MT2][NT2];
+  if constexpr (M32) {
 #pragma unroll
-  for (int m = 0; m < MT; ++m)
+    for (int m = 0; m < MT2; ++m)
 #pragma unroll
-    for (int n = 0; n < NTP; ++n) acc[m][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      for (int n = 0; n < NT2; ++n)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc32[m][n][r] = 0.f;
+  } else {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < NTP; ++n) acc[m][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  }
   __syncthreads();  // coefficients in LDS
   const int nk = (K + BK - 1) / BK;
   uint4 ra[AJ], rb[NJ], rb2[NJ];
@@ -486,6 +544,25 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
       load_a(BK * (ks + 1), ra);
       load_b(BK * (ks + 1), rb, rb2, ncch, okb);
     }
+    if constexpr (M32) {
+      // lane l: A row (l & 31), B pixel (l & 31), k = 16 s + 8 (l >> 5) .. + 7 of each 16-deep half step s
+#pragma unroll
+      for (int s2 = 0; s2 < BK / 16; ++s2) {
+        bf16x8_t fa[MT2], fb[NT2];
+#pragma unroll
+        for (int m = 0; m < MT2; ++m)
+          fa[m] = *reinterpret_cast<const bf16x8_t*>(sa[cur] + (wr * (TC / WRN) + 32 * m + (lane & 31)) * RP +
+                                                     16 * s2 + 8 * (lane >> 5));
+#pragma unroll
+        for (int n = 0; n < NT2; ++n)
+          fb[n] = *reinterpret_cast<const bf16x8_t*>(sb[cur] + (wc * PW + 32 * n + (lane & 31)) * RP + 16 * s2 +
+                                                     8 * (lane >> 5));
+#pragma unroll
+        for (int m = 0; m < MT2; ++m)
+#pragma unroll
+          for (int n = 0; n < NT2; ++n) acc32[m][n] = dtf_mfma32(fa[m], fb[n], acc32[m][n]);
+      }
+    } else
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
       bf16x8_t fa[MT], fb[NTP];
@@ -517,8 +594,12 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
     }
     __syncthreads();
   }
-  convg_epilogue<TC, EPI, TRANS, TP, WRN, NHALF>(a, acc, reinterpret_cast<float*>(smem_), acc_lds, slot, o0, p0, p1,
-                                                  HWo, GW, py, px);
+  if constexpr (M32)
+    convg_epilogue32<TC, EPI, TRANS, TP, WRN, NHALF>(a, acc32, reinterpret_cast<float*>(smem_), acc_lds, slot, o0, p0,
+                                                      p1, HWo, GW, py, px);
+  else
+    convg_epilogue<TC, EPI, TRANS, TP, WRN, NHALF>(a, acc, reinterpret_cast<float*>(smem_), acc_lds, slot, o0, p0, p1,
+                                                    HWo, GW, py, px);
 }
 
 // ------------------------------------------------------------------------ stride-1 3x3: LDS-resident input rows
@@ -1171,6 +1252,8 @@ DTF_API int dtf_convg_fwd(const CgArgs* a, int tc, int mode, int epi, int trans,
   const int akm = (trans >> 1) & 1;
   const int bk64 = (trans >> 2) & 1;
   const int tp256 = (trans >> 3) & 1;  // 256-pixel tiles (tc = 64, BK = 32)
+  const int m32 = (trans >> 4) & 1;    // 32x32x16 MFMA tiles (plain-A forward, tc = 128, 256-pixel tiles)
+  if (m32 && (akm || !tp256 || tc != 128)) return -2;
   if (tp256 && bk64) return -2;
   trans &= 1;
   if (nwork <= 0) return 0;
@@ -1181,7 +1264,10 @@ DTF_API int dtf_convg_fwd(const CgArgs* a, int tc, int mode, int epi, int trans,
   dim3 grid(nwork), block(256);
 #define CG_CASE(TC_, M_, E_, T_, AK_)                                                                      \
   if (tc == TC_ && mode == M_ && epi == E_ && trans == T_ && akm == AK_) {                                 \
-    if (tp256)                                                                                             \
+    if (m32)                                                                                               \
+      hipLaunchKernelGGL((convg_fwd_kernel<TC_, M_, E_, T_, AK_, 32, 256, (TC_ == 128 && !AK_)>), grid, block, dyn, \
+                         stream, *a);                                                                      \
+    else if (tp256)                                                                                        \
       hipLaunchKernelGGL((convg_fwd_kernel<TC_, M_, E_, T_, AK_, 32, 256>), grid, block, dyn, stream, *a); \
     else if (bk64)                                                                                         \
       hipLaunchKernelGGL((convg_fwd_kernel<TC_, M_, E_, T_, AK_, 64>), grid, block, dyn, stream, *a);     \

@@ -4,7 +4,7 @@ Counts, per launch of the population step, the activation bytes it must move thr
 tensor read or written by that launch, NHWC bf16; weights, BN tables and L2 re-reads of a 3x3 halo ignored) and
 compares the sum with the measured per-family GPU time of a kernel trace:
 
-    python tools/imagenet_roofline.py [--n 1024] [--bw 6.3] [gpurun_out/prof/run_kernel_trace.csv]
+    python tools/imagenet_roofline.py [--n 1024] [--bw 6.3] [--top N] [gpurun_out/prof/run_kernel_trace.csv]
 
 ``--bw`` is the achievable HBM bandwidth (TB/s; MI355X: 6.3 measured for a float4 copy, 8.0 spec).  The output
 lists bytes and floor time per launch family and, with a trace, the measured time per step of the same family.

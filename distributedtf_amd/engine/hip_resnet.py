@@ -2000,8 +2000,9 @@ class _StepPlan:
                 if err != 0:
                     raise RuntimeError("kernel launch %s failed with %d" % (getattr(fn, "__name__", fn), err))
             elif fn == "augment":
+                # crops keyed per member (its step counter + dataset row): placement-invariant (data.hip)
                 ops.augment_cifar(self.src.train_x, self.src.train_y, self.idx, self.rng, True, out16=self.xin16,
-                                  lab32=self.labels)
+                                  lab32=self.labels, member_keys=(self.img_slot, e.state, e.S, 3 * e.Pp + e.R))
             elif fn == "optim":
                 e.dp_sync_grads(self.slots)  # data-parallel member groups only (no-op otherwise)
                 ops.fused_optimizer(e.state, e.grads, e.hyper, e.Pp, e.P, e.n_reg, shadow=None, zero_grads=True,

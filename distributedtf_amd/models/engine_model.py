@@ -244,6 +244,7 @@ class EngineModel(ModelBase):
             b = self.dp.local_batch(b)  # this replica's shard of the member's batch
         if hasattr(ds, "batch_slice"):
             return ds.batch_slice(b)
+        gen = self._data_gen(ds, gen)
         if not hasattr(self, "_perm") or self._perm_pos + b > self._perm.numel():
             self._perm = torch.randperm(ds.num_train, device=ds.train_x.device, generator=gen)
             self._perm_pos = 0
@@ -252,6 +253,20 @@ class EngineModel(ModelBase):
         if getattr(ds, "hip_augment", False):
             return datasets.IndexBatch(ds, idx)
         return ds.batch(idx, gen)
+
+    def _data_gen(self, ds, shared=None):
+        """This member's own data-order / augmentation generator (seeded once from the member's rng): a member's
+        batches do not depend on which members share its rank or plan, so a PBT run reads the same data at any
+        placement of the population (tests/test_gpu_placement.py).  Replicas of a data-parallel group draw
+        different shards."""
+        if ds.device.type != "cuda":
+            return shared
+        g = getattr(self, "_gen", None)
+        if g is None or g.device != ds.device:
+            g = torch.Generator(device=ds.device)
+            g.manual_seed(int(self.rng.random() * 1e9) + (7919 * self.dp.rank if self.dp else 0))
+            self._gen = g
+        return g
 
     def n_steps(self, num_epoch: int) -> int:
         """Steps of one ``train`` call: ``ready_steps`` when set (a fixed PBT ready interval in steps), else
@@ -305,11 +320,7 @@ class EngineModel(ModelBase):
         for ms in groups.values():
             eng = ms[0].engine
             ds = ms[0].dataset()
-            gen = None
-            if ds.device.type == "cuda":
-                gen = torch.Generator(device=ds.device)
-                # replicas of a data-parallel group draw different shards (the member rng stays in lockstep)
-                gen.manual_seed(int(ms[0].rng.random() * 1e9) + (7919 * ms[0].dp.rank if ms[0].dp else 0))
+            gen = None  # each member draws from its own generator (_data_gen)
             hooks = cls._hooks(eng, ms[0])
             plan = {m.slot: m.cycle_steps(num_epoch) for m in ms}
             by_slot = {m.slot: m for m in ms}

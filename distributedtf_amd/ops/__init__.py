@@ -229,24 +229,31 @@ def shadow_refresh(state, shadow, rows, Pp, P):
 
 
 register("dtf_augment_cifar", [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
-                               c_void_p, c_void_p])
+                               c_void_p, c_void_p, c_void_p, c_long, c_long, c_void_p])
 
 
-def augment_cifar(images, labels, idx, rng, augment=True, out16=None, out32=None, lab32=None, lab64=None):
+def augment_cifar(images, labels, idx, rng, augment=True, out16=None, out32=None, lab32=None, lab64=None,
+                  member_keys=None):
     """Fused gather + pad/crop/flip + per-image standardization (data.hip).
 
     images [N,32,32,3] uint8, labels [N] int64, idx [n] int64 (dataset rows), rng [2] int32 (seed, counter; read
     on the device, so graph replays pick up updates).  Writes any of out16 [n,32,32,16] bf16 / out32 [n,32,32,3]
-    fp32 / lab32 [n] int32 / lab64 [n] int64.
+    fp32 / lab32 [n] int32 / lab64 [n] int64.  ``member_keys`` = (img_slot [n] int32, state, row stride, step column):
+    crops keyed by each image's member step counter and dataset row instead of the launch counter and batch
+    position (placement-invariant population steps, data.hip).
     """
     assert images.dtype == torch.uint8 and tuple(images.shape[1:]) == (32, 32, 3) and images.is_contiguous()
     assert labels.dtype == torch.int64 and idx.dtype == torch.int64 and rng.numel() >= 2
     n = int(idx.numel())
-    for t, shp, dt in ((out16, (32, 32, 16), torch.bfloat16), (out32, (32, 32, 3), torch.float32)):
+    for t, shp, dt in ((out16, (32, 32, 16), act_dtype()), (out32, (32, 32, 3), torch.float32)):
         if t is not None:
             assert t.dtype == dt and t.shape[0] >= n and tuple(t.shape[1:]) == shp and t.is_contiguous()
     for t, dt in ((lab32, torch.int32), (lab64, torch.int64)):
         if t is not None:
             assert t.dtype == dt and t.numel() >= n
+    ks, kst, kstride, kcol = member_keys if member_keys is not None else (None, None, 0, 0)
+    if ks is not None:
+        assert ks.dtype == torch.int32 and ks.numel() >= n and kst.dtype == torch.float32
     check(lib().dtf_augment_cifar(ptr(images), ptr(labels), ptr(idx), ptr(rng), n, 1 if augment else 0, ptr(out16),
-                                  ptr(out32), ptr(lab32), ptr(lab64), stream()), "augment_cifar")
+                                  ptr(out32), ptr(lab32), ptr(lab64), ptr(ks), ptr(kst), int(kstride), int(kcol),
+                                  stream()), "augment_cifar")

@@ -5,7 +5,11 @@
 //   one wave per image: 1024 pixels = 16 per lane, the 48 channel values stay in VGPRs for the two-pass
 //   mean / variance (tf.image.per_image_standardization: (x - mean) / max(std, 1/sqrt(N)), N = 3072).
 //   Random crop offsets and the flip bit come from a counter-based hash of (seed, counter, batch position);
-//   seed/counter are read from device memory so a captured HIP graph draws new crops on every replay.
+//   seed/counter are read from device memory so a captured HIP graph draws new crops on every replay.  With
+//   per-member keys (key_slot != null: the population step's images) the hash is of (seed, the member's own step
+//   counter read from its state row, dataset row) instead: a member's crops then depend only on the member -- not on
+//   which other members share its plan, its position in the packed batch, or how many launches its rank ran -- so a
+//   PBT run draws the same augmentation at any placement of the population over ranks (tests/test_gpu_placement.py).
 //   Outputs: bf16 NHWC with channels zero-padded to 16 (the HIP ResNet stem input) and/or fp32 NHWC (C=3).
 #include "common.h"
 
@@ -27,14 +31,21 @@ __global__ __launch_bounds__(256) void augment_cifar_kernel(const uint8_t* __res
                                                             const long* __restrict__ idx,
                                                             const uint32_t* __restrict__ rng, int n, int augment,
                                                             bf16_t* __restrict__ out16, float* __restrict__ out32,
-                                                            int* __restrict__ lab32, long* __restrict__ lab64) {
+                                                            int* __restrict__ lab32, long* __restrict__ lab64,
+                                                            const int* __restrict__ key_slot,
+                                                            const float* __restrict__ key_state, long key_stride,
+                                                            long key_col) {
   const int lane = threadIdx.x & 63;
   const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (p >= n) return;
   const long src = idx[p];
   int oy = PAD, ox = PAD, flip = 0;
   if (augment) {
-    const uint32_t h = mix32(rng[0] ^ mix32(rng[1] * 0x9E3779B9u + (uint32_t)p));
+    const uint32_t h =
+        key_slot != nullptr
+            ? mix32(rng[0] ^ mix32((uint32_t)(int)key_state[(long)key_slot[p] * key_stride + key_col] * 0x9E3779B9u +
+                                   (uint32_t)src))
+            : mix32(rng[0] ^ mix32(rng[1] * 0x9E3779B9u + (uint32_t)p));
     oy = (int)(h % 9u);
     ox = (int)((h >> 8) % 9u);
     flip = (int)((h >> 16) & 1u);
@@ -95,9 +106,10 @@ __global__ __launch_bounds__(256) void augment_cifar_kernel(const uint8_t* __res
 
 DTF_API int dtf_augment_cifar(const uint8_t* images, const long* labels_src, const long* idx, const uint32_t* rng,
                               int n, int augment, bf16_t* out16, float* out32, int* lab32, long* lab64,
+                              const int* key_slot, const float* key_state, long key_stride, long key_col,
                               hipStream_t stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(augment_cifar_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, images, labels_src, idx, rng, n,
-                     augment, out16, out32, lab32, lab64);
+                     augment, out16, out32, lab32, lab64, key_slot, key_state, key_stride, key_col);
   return DTF_CHECK_LAUNCH();
 }

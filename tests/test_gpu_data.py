@@ -85,12 +85,14 @@ def test_hip_step_consumes_index_batches(monkeypatch):
     for step in range(3):
         idxs = [torch.randint(0, 400, (n,), device="cuda") for n in sizes]
         ctr = ds.rng_counter + 1
-        la = a.train_step([0, 1], [datasets.IndexBatch(ds, i) for i in idxs], [hp, hp], [0.05, 0.05])
-        # same draws, materialised as fp32 (the kernel's own fp32 output: isolates the in-graph plumbing)
+        # same draws, materialised as fp32 (the kernel's own fp32 output: isolates the in-graph plumbing); the step
+        # keys its crops per member (member step counter + dataset row, data.hip), read before the step advances it
         allidx = torch.cat(idxs)
         xf = torch.empty(allidx.numel(), 32, 32, 3, device="cuda")
         rng = torch.tensor([ds.rng_seed, ctr], dtype=torch.int32, device="cuda")
-        ops.augment_cifar(x, y, allidx, rng, True, out32=xf)
+        slot_of = torch.tensor([0] * sizes[0] + [1] * sizes[1], dtype=torch.int32, device="cuda")
+        ops.augment_cifar(x, y, allidx, rng, True, out32=xf, member_keys=(slot_of, a.state, a.S, 3 * a.Pp + a.R))
+        la = a.train_step([0, 1], [datasets.IndexBatch(ds, i) for i in idxs], [hp, hp], [0.05, 0.05])
         batches = [(xf[:sizes[0]], y[idxs[0]]), (xf[sizes[0]:], y[idxs[1]])]
         lb = b.train_step([0, 1], batches, [hp, hp], [0.05, 0.05])
         torch.testing.assert_close(la, lb, rtol=2e-3, atol=2e-3)

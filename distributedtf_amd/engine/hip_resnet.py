@@ -751,7 +751,8 @@ class _StepPlan:
             cnt[s] = float(n)
         self.cnt = cnt.to(dev)
         # uniform population: work items of the stage kernels computed from blockIdx (ConvArgs.u_items)
-        self.uniform = len(set(sizes)) == 1 and list(slots) == list(range(len(slots))) and not self.elastic
+        self.uniform = (len(set(sizes)) == 1 and list(slots) == list(range(len(slots))) and not self.elastic
+                        and not be.det)
         if self.elastic:
             for s, n in zip(slots, self.real_sizes):
                 cnt[s] = float(n)
@@ -835,7 +836,9 @@ class _StepPlan:
         # run as two workgroup roles of ONE launch (conv_bwd_dual_kernel); the layer costs max(dgrad, wgrad) instead
         # of their sum while the population leaves CUs idle (C = 16 keeps the fused kernel: its single-band work
         # items already fill the GPU; profiles/r2_dual_pop1_breakdown.txt)
-        self.dual = dev.type == "cuda" and cfg.version == 2 and len(slots) <= DUAL_MAX_POP
+        # (the deterministic build never switches kernel families with the population size: a member's reduction
+        # order must not depend on how many members share its plan -- placement invariance, _work_iters)
+        self.dual = dev.type == "cuda" and cfg.version == 2 and len(slots) <= DUAL_MAX_POP and not be.det
         # Deferred weight gradients (the same small populations): each stride-1 layer's backward launch runs only
         # its dgrad role -- the critical path, serialised by the BatchNorm statistics -- and the wgrad work of all
         # those layers runs afterwards in two wide launches (conv_wgrad_all_kernel: widths 64 + 32, width 16).
@@ -849,7 +852,7 @@ class _StepPlan:
         # idle, and its 147 KB dW slab per workgroup cost more than re-reading dY / x once in the wide wgrad
         # launch; profiles/r3_defer_ab.log)
         v2gpu = dev.type == "cuda" and cfg.version == 2
-        large = DEFER_MID_CS if len(slots) <= DEFER_MID_POP else DEFER_LARGE_CS
+        large = DEFER_MID_CS if (len(slots) <= DEFER_MID_POP and not be.det) else DEFER_LARGE_CS
         self.defer_cs = {16, 32, 64} if self.defer_wg else (set(large) if v2gpu else set())
         self._wg_jobs = {}  # (C, wgrad dY mode) -> [(ConvArgs, work table, grad offset)]
         self.launches = []
@@ -870,21 +873,31 @@ class _StepPlan:
 
     # -------------------------------------------------------------------- work lists
     def _work_iters(self, bands, n_wg):
-        """(it0, nit, 0, slot) items over the flattened (image, band) iterations of each member."""
-        key = ("it", bands, n_wg)
+        """(it0, nit, 0, slot) items over the flattened (image, band) iterations of each member.
+
+        Deterministic build: ``n_wg`` is ignored -- every member gets exactly DET_WG_PER_MEMBER rows (empty ones,
+        nit = 0, past its iterations), so a member's split into workgroups, the statistic replica each of its
+        workgroups adds to (blockIdx % 64 = the row within the member) and the order its dW slabs are reduced in
+        depend on its own batch size only: the step of a member is bitwise the same whichever members share its
+        plan (a PBT run replays identically at any placement over ranks, tests/test_gpu_placement.py)."""
+        det = self.be.det
+        key = ("it", bands, "det" if det else n_wg)
         w = self._work_cache.get(key)
         if w is None and self.elastic:
-            w = self._elastic_table(max(1, n_wg // max(1, len(self.slots))), bands, 1)
+            per = DET_WG_PER_MEMBER if det else max(1, n_wg // max(1, len(self.slots)))
+            w = self._elastic_table(per, bands, 1)
             self._work_cache[key] = w
         if w is None:
             items = []
-            per_member = max(1, n_wg // max(1, len(self.slots)))
+            per_member = DET_WG_PER_MEMBER if det else max(1, n_wg // max(1, len(self.slots)))
             for s, n in zip(self.slots, self.sizes):
                 total = n * bands
                 f = self.first[s] * bands
                 chunk = max(1, -(-total // per_member))
                 for i in range(0, total, chunk):
                     items.append([f + i, min(chunk, total - i), 0, s])
+                if det:  # pad to exactly per_member rows (empty rows point at the member's first iteration)
+                    items += [[f, 0, 0, s]] * (per_member - -(-total // chunk))
                 # uniform geometry (identical for every member when self.uniform): items, chunk, iterations
                 geo = (-(-total // chunk), chunk, total)
             w = torch.tensor(items, dtype=torch.int32, device=self.be.dev)
@@ -1064,7 +1077,7 @@ class _StepPlan:
                 break
         assert rows is not None, ("no valid band for conv", ci)
         s1 = c.k == 3 and c.stride == 1 and cin == c.cout and Hi == 512 // cin and stats_bn is not None
-        if s1 and cin == 64 and self.N <= HALF_BANDS_MAX_IMGS and in_bn is not None:
+        if s1 and cin == 64 and self.N <= HALF_BANDS_MAX_IMGS and in_bn is not None and not be.det:
             rows = 4  # conv_fwd_s1_kernel<64, ., ., 4>
         bands = Ho // rows
         lo = FWD_MIN_WG_SMALL if len(self.slots) <= DUAL_MAX_POP else FWD_MIN_WG
@@ -1314,7 +1327,7 @@ class _StepPlan:
         epi = int(res is not None) | (2 if ident_x else 0)
         # ---- dgrad role: one (image, band) iteration per workgroup (larger populations: DG_ITERS_LARGE); the
         # deferred-wgrad dgrad launch of the C = 64 stage takes half-image bands at small populations
-        rows_dg = 4 if (C == 64 and C in self.defer_cs and self.N <= HALF_BANDS_MAX_IMGS) else rows
+        rows_dg = 4 if (C == 64 and C in self.defer_cs and self.N <= HALF_BANDS_MAX_IMGS and not be.det) else rows
         bands_dg = H // rows_dg
         n_dg = max(1, self.N * bands_dg)
         if not self.dual:
@@ -1506,6 +1519,8 @@ class _StepPlan:
         return ((9 * C // 16 + 3) // 4) * (C // 16) * 4 * 256
 
     def _fused_nwg(self, C, bands, mode_dy=0):
+        if self.be.det:
+            return DET_WG_PER_MEMBER * len(self.slots)  # = the rows _work_iters gives every member
         # per-launch budget for the dW partials (bytes of slab stores, or of atomics without slabs): bounds the
         # workgroup count of the fused kernel
         wn = 9 * C * C

@@ -246,6 +246,7 @@ class EngineModel(ModelBase):
             return ds.batch_slice(b)
         gen = self._data_gen(ds, gen)
         if not hasattr(self, "_perm") or self._perm_pos + b > self._perm.numel():
+            self._perm_gen_state = gen.get_state() if gen is not None else None  # (stream_state: exact resume)
             self._perm = torch.randperm(ds.num_train, device=ds.train_x.device, generator=gen)
             self._perm_pos = 0
         idx = self._perm[self._perm_pos:self._perm_pos + b]
@@ -253,6 +254,34 @@ class EngineModel(ModelBase):
         if getattr(ds, "hip_augment", False):
             return datasets.IndexBatch(ds, idx)
         return ds.batch(idx, gen)
+
+    def stream_state(self):
+        """Explore rng + the member's data stream (its generator state when the current epoch permutation was drawn,
+        the position in it, and the generator's current state): JSON-able, for the whole-run resume table."""
+        d = super().stream_state()
+        g = getattr(self, "_gen", None)
+        if g is not None and getattr(self, "_perm_gen_state", None) is not None:
+            d["data"] = {"perm_gen": self._perm_gen_state.cpu().numpy().tobytes().hex(), "perm_pos": self._perm_pos,
+                         "gen": g.get_state().cpu().numpy().tobytes().hex()}
+        return d
+
+    def restore_stream_state(self, d) -> None:
+        super().restore_stream_state(d)
+        data = (d or {}).get("data")
+        if data is None:
+            return
+        ds = self.dataset()
+        if getattr(ds, "num_train", None) is None:
+            return
+        g = self._data_gen(ds)
+        if g is None:
+            return
+        st = lambda h: torch.frombuffer(bytearray(bytes.fromhex(h)), dtype=torch.uint8)  # noqa: E731
+        g.set_state(st(data["perm_gen"]))
+        self._perm_gen_state = g.get_state()
+        self._perm = torch.randperm(ds.num_train, device=ds.train_x.device, generator=g)
+        self._perm_pos = int(data["perm_pos"])
+        g.set_state(st(data["gen"]))
 
     def _data_gen(self, ds, shared=None):
         """This member's own data-order / augmentation generator (seeded once from the member's rng): a member's

@@ -106,6 +106,17 @@ class ModelBase(object):
     # the TF tensor bundle (``--tf_checkpoint``) owns the ``checkpoint`` state file when set
     tf_checkpoint = False
 
+    def stream_state(self):
+        """JSON-able state of the member's random streams (the explore rng), saved in the whole-run resume table
+        so a resumed run draws the same perturbations as an uninterrupted one."""
+        v, st, gauss = self.rng.getstate()
+        return {"rng": [v, list(st), gauss]}
+
+    def restore_stream_state(self, d) -> None:
+        if d and "rng" in d:
+            v, st, gauss = d["rng"]
+            self.rng.setstate((v, tuple(st), gauss))
+
     def save_checkpoint(self, wait: bool = False) -> None:
         """Write ``savedata/model_<id>/model.ckpt`` (+ ``checkpoint`` state file).
 

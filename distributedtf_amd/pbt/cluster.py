@@ -305,6 +305,7 @@ class SPMDPopulation(_ReportMixin):
             self.start_round = int(state["next_round"])
             rows = [(m["model_id"], m["accuracy"], m["hparams"], m["epoches_trained"]) for m in state["members"]]
             csv_lines = {int(m["model_id"]): m.get("csv_lines", {}) for m in state["members"]}
+            streams = {int(m["model_id"]): m.get("stream_state") for m in state["members"]}
         self.pop_size = len(rows)
         blocks = partition(self.initial_pop_size, self.n_groups)
         self.id_owner = {}  # member id -> member group (= rank when dp_size == 1)
@@ -323,6 +324,8 @@ class SPMDPopulation(_ReportMixin):
                     raise RuntimeError("resume: member %d has no checkpoint%s in %s"
                                        % (mid, "" if tag is None else " of round %d" % tag, g.save_dir))
                 g.accuracy, g.epoches_trained = float(acc), int(epochs)
+                if streams.get(int(mid)) is not None and hasattr(g, "restore_stream_state"):
+                    g.restore_stream_state(streams[int(mid)])
                 # drop learning-curve rows a crashed round appended after the table was written
                 reports.truncate_member_csvs(g.save_dir, csv_lines.get(int(mid), {}))
             self.log("Resumed %d members at round %d" % (len(rows), self.start_round))
@@ -457,7 +460,8 @@ class SPMDPopulation(_ReportMixin):
                     g.export_tf_checkpoint()
         flush_checkpoints()  # every rank's checkpoints are on disk before the table that names them
         rows = self.comm.allgather([[g.cluster_id, g.get_accuracy(), g.hparams, g.epoches_trained,
-                                     reports.member_csv_lines(g.save_dir)]
+                                     reports.member_csv_lines(g.save_dir),
+                                     g.stream_state() if hasattr(g, "stream_state") else None]
                                     for g in self.worker.worker_graphs] if self.is_group_leader else [])
         if self.rank == 0:
             reports.write_population_state(self.savedata, next_round, self.initial_pop_size,

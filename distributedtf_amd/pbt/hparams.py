@@ -195,7 +195,11 @@ def perturb_hparams(hparams: Dict[str, Any], rng: Optional[_random.Random] = Non
     """
     rng = rng if rng is not None else _random
     rdef = get_hp_range_definition()
-    for key in list(hparams.keys()):
+    # keys in sorted (canonical) order: the draws a key receives must not depend on the dict's insertion order,
+    # which a JSON round trip (checkpoint blob, whole-run resume table, all-gathered values) does not keep -- a
+    # resumed or differently placed run then perturbs exactly like the original (the reference iterates its
+    # hyperopt sample's order with an unseeded rng, so no order is observable there)
+    for key in sorted(hparams.keys()):
         value = hparams[key]
         if isinstance(value, bool):
             continue

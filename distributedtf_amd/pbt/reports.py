@@ -72,6 +72,8 @@ def write_population_state(savedata: str, next_round: int, population_size: int,
         m = {"model_id": int(r[0]), "accuracy": float(r[1]), "hparams": r[2], "epoches_trained": int(r[3])}
         if len(r) > 4:
             m["csv_lines"] = dict(r[4])
+        if len(r) > 5 and r[5] is not None:
+            m["stream_state"] = r[5]  # explore rng (+ data stream) of the member: a resumed run replays the same draws
         members.append(m)
     blob = {"next_round": int(next_round), "population_size": int(population_size), "members": members}
     if ckpt_round is not None:

@@ -136,7 +136,15 @@ class HipResNetF32Backend:
         self.cfg = self.prog.cfg
         cap = engine.capacity
         nb = len(self.prog.bns)
-        self.sums = torch.zeros(2, nb, cap, 2, CMAX, dtype=torch.float32, device=self.dev)  # [fwd|bwd]
+        # deterministic build (--deterministic --dtype fp32): every cross-workgroup sum -- BN statistics, BN-backward
+        # sums, weight gradients, the loss -- accumulates as int64 fixed point with integer atomics (common.h
+        # DTF_FIXED_ACC, as the ImageNet step): order-free, so a replay is bitwise identical; cg_det_finish folds
+        # the gradient / loss accumulators into the fp32 rows before the optimizer
+        self.det = bool(ops.lib().dtf_fixed_acc())
+        self.acc_dtype = torch.int64 if self.det else torch.float32
+        self.sums = torch.zeros(2, nb, cap, 2, CMAX, dtype=self.acc_dtype, device=self.dev)  # [fwd|bwd]
+        self.gacc = torch.zeros(cap, engine.Pp, dtype=torch.int64, device=self.dev) if self.det else None
+        self.loss64 = torch.zeros(cap, dtype=torch.int64, device=self.dev) if self.det else None
         self.coef = torch.zeros(2, nb, cap, 4, CMAX, dtype=torch.float32, device=self.dev)
         self.loss = torch.zeros(cap, dtype=torch.float32, device=self.dev)
         self.correct = torch.zeros(cap, dtype=torch.float32, device=self.dev)
@@ -277,8 +285,9 @@ class _F32Plan:
         if self.eval:
             nb = len(prog.bns)
             self.ev_coef = torch.zeros(nb, e.capacity, 4, CMAX, dtype=f32, device=dev)
-            self.ev_sink = torch.zeros(e.capacity, 2, CMAX, dtype=f32, device=dev)
+            self.ev_sink = torch.zeros(e.capacity, 2, CMAX, dtype=be.acc_dtype, device=dev)
             self.ev_acc = torch.zeros(2, e.capacity, dtype=f32, device=dev)
+            self.ev_loss = torch.zeros(e.capacity, dtype=be.acc_dtype, device=dev)  # summed CE (accumulator words)
             self._build_eval()
         else:
             self._build()
@@ -398,6 +407,8 @@ class _F32Plan:
         a.kh = a.kw = c.k
         a.stride, a.pad = c.stride, (c.k - 1) // 2
         a.log2ci = _log2(a.Ci)
+        if self.be.det:  # weight gradients into the int64 accumulator rows (folded by cg_det_finish)
+            a.grads = _p(self.be.gacc)
         L = ops.lib()
         if (BAND_WGRAD and not stem and c.k == 3 and c.stride == 1 and c.cin == c.cout
                 and L.dtf_f32_wgrad_band_ok(c.cin, hw_in)):
@@ -460,9 +471,10 @@ class _F32Plan:
         h.state, h.s_mstride, h.w_off, h.b_off = _p(e.state), e.S, prog.dense_w_off, prog.dense_b_off
         h.feat, h.dlog, h.dfeat, h.cnt = _p(self.feat), _p(self.dlog), _p(self.dfeat), _p(self.cnt)
         if train:
-            h.loss, h.correct = _p(self.be.loss), _p(self.be.correct)
+            h.loss = _p(self.be.loss64 if self.be.det else self.be.loss)
+            h.correct = _p(self.be.correct)
         else:
-            h.loss, h.correct = _p(self.ev_acc[1]), _p(self.ev_acc[0])
+            h.loss, h.correct = _p(self.ev_loss), _p(self.ev_acc[0])
         if not self.v1 and train:
             h.sums, h.bcoef = _p(self.sb(prog.final_bn)), _p(self.cb(prog.final_bn))
         h.hw, h.C, h.ncls, h.cmax, h.train = self.HL * self.HL, self.CL, cfg.num_classes, CMAX, int(train)
@@ -602,6 +614,11 @@ class _F32Plan:
             self.ew(0, self.y0, dy0, self.cb(sbn), H, cfg.num_filters, dz=g)
             g = dy0
         self.wgrad(prog.stem, self.xin4, g, H)
+        if be.det:
+            from .hip_imagenet import _register as _reg_cg
+            _reg_cg()  # dtf_cg_det_finish signature
+            self._add(ops.lib().dtf_cg_det_finish, _p(be.gacc), _p(e.grads), e.Pp, e.Pp, _p(self.slots_t),
+                      len(self.slots), _p(be.loss64), _p(be.loss))
         self._add("optim", None)
         self._add("step", None)
 

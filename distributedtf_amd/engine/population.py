@@ -284,8 +284,6 @@ def _hip_f32_ok(engine) -> bool:
     if engine.compute_dtype != torch.float32:
         return False
     from .. import ops
-    if ops.deterministic_mode():  # the deterministic build's shared bn_final reads int64 fixed-point sums
-        return False
     if ops.half_mode():  # the fp32 step shares 16-bit helper kernels (input packing) with the bf16 build
         return False
     from .hip_f32 import supports

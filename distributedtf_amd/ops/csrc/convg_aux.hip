@@ -701,10 +701,12 @@ __global__ __launch_bounds__(256) void cg_det_finish_kernel(long long* __restric
                                                              long stride, long n, const int* __restrict__ slots,
                                                              long long* __restrict__ loss64, float* __restrict__ loss,
                                                              const unsigned* __restrict__ pz0,
-                                                             const unsigned* __restrict__ pz1) {
+                                                             const unsigned* __restrict__ pz1,
+                                                             const unsigned* __restrict__ pz2) {
   const int slot = slots[blockIdx.y];
   const int ps = slot & (DTF_POISON_SLOTS - 1);
-  const bool bad = (pz0 != nullptr && pz0[ps] != 0u) || (pz1 != nullptr && pz1[ps] != 0u);
+  const bool bad = (pz0 != nullptr && pz0[ps] != 0u) || (pz1 != nullptr && pz1[ps] != 0u) ||
+                   (pz2 != nullptr && pz2[ps] != 0u);
   long long* ga = gacc + (long)slot * stride;
   float* g = grads + (long)slot * stride;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -724,11 +726,12 @@ __global__ __launch_bounds__(256) void cg_det_finish_kernel(long long* __restric
 }
 
 __global__ void cg_poison_clear_kernel(unsigned* __restrict__ pz0, unsigned* __restrict__ pz1,
-                                       const int* __restrict__ slots, int nslots) {
+                                       unsigned* __restrict__ pz2, const int* __restrict__ slots, int nslots) {
   for (int i = threadIdx.x; i < nslots; i += blockDim.x) {
     const int ps = slots[i] & (DTF_POISON_SLOTS - 1);
     if (pz0 != nullptr) pz0[ps] = 0u;
     if (pz1 != nullptr) pz1[ps] = 0u;
+    if (pz2 != nullptr) pz2[ps] = 0u;
   }
 }
 
@@ -737,9 +740,11 @@ __global__ void cg_poison_clear_kernel(unsigned* __restrict__ pz0, unsigned* __r
 #ifdef DTF_DETERMINISTIC
 DTF_API unsigned* dtf_poison_ptr_convg();  // convg.hip
 DTF_API unsigned* dtf_poison_ptr_convg_aux();
+DTF_API unsigned* dtf_poison_ptr_f32conv();  // f32conv.hip (the fp32 CIFAR step)
 #else
 static unsigned* dtf_poison_ptr_convg() { return nullptr; }
 static unsigned* dtf_poison_ptr_convg_aux() { return nullptr; }
+static unsigned* dtf_poison_ptr_f32conv() { return nullptr; }
 #endif
 
 DTF_API int dtf_cg_det_finish(long long* gacc, float* grads, long stride, long n, const int* slots, int nslots,
@@ -749,10 +754,11 @@ DTF_API int dtf_cg_det_finish(long long* gacc, float* grads, long stride, long n
   if (blocks > 512) blocks = 512;
   static unsigned* const pz0 = dtf_poison_ptr_convg();  // looked up once (not inside a graph capture's hot path)
   static unsigned* const pz1 = dtf_poison_ptr_convg_aux();
+  static unsigned* const pz2 = dtf_poison_ptr_f32conv();
   hipLaunchKernelGGL(cg_det_finish_kernel, dim3((unsigned)blocks, nslots), dim3(256), 0, stream, gacc, grads, stride, n,
-                     slots, loss64, loss, pz0, pz1);
-  if (pz0 != nullptr || pz1 != nullptr)
-    hipLaunchKernelGGL(cg_poison_clear_kernel, dim3(1), dim3(256), 0, stream, pz0, pz1, slots, nslots);
+                     slots, loss64, loss, pz0, pz1, pz2);
+  if (pz0 != nullptr || pz1 != nullptr || pz2 != nullptr)
+    hipLaunchKernelGGL(cg_poison_clear_kernel, dim3(1), dim3(256), 0, stream, pz0, pz1, pz2, slots, nslots);
   return DTF_CHECK_LAUNCH();
 }
 

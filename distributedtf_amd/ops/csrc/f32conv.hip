@@ -40,7 +40,7 @@ struct F32Args {
   const float* c_in;  // [cap][4][cmax] transform coefficients of the gathered operand
   const float* c_dy;  // wgrad: of dy
   const float* c_ep;  // epilogue mask BN (scale, shift, mean, inv)
-  float* st_out;      // [cap][2][cmax] statistics (atomics)
+  dtf_acc_t* st_out;  // [cap][2][cmax] statistics (atomics; int64 fixed point in the deterministic build)
   const int4* work;   // (slot, p0, p1, o0 [| n0 / 16 << 16 for wgrad])
   int Hi, Wi, Ci;     // gathered tensor (fwd: x, dgrad: dy)
   int Ho, Wo, Co;     // output tensor (wgrad: dy)
@@ -96,9 +96,9 @@ __device__ __forceinline__ void f32_epi4(const F32Args& a, int slot, long p, int
 
 // Workgroup statistics: the 16 lanes of one lane / 16 group hold the same 4 channels -- butterfly, one LDS atomic
 // per group and channel, one global atomic per workgroup and channel.  acc_lds [2][TC] zeroed before the k loop.
-template <int TC, int MT>
+template <int TC, int FX, int MT>
 __device__ __forceinline__ void f32_stats_flush(const F32Args& a, int slot, int o0, float (&ss)[MT][4],
-                                                float (&sq)[MT][4], float (&acc_lds)[2][TC]) {
+                                                float (&sq)[MT][4], dtf_acc_t (&acc_lds)[2][TC]) {
   const int tid = threadIdx.x, lane = tid & 63;
 #pragma unroll
   for (int m = 0; m < MT; ++m)
@@ -111,15 +111,15 @@ __device__ __forceinline__ void f32_stats_flush(const F32Args& a, int slot, int 
         q_ += __shfl_xor(q_, o, 64);
       }
       if ((lane & 15) == 0) {
-        atomicAdd(&acc_lds[0][16 * m + 4 * (lane >> 4) + i], s_);
-        atomicAdd(&acc_lds[1][16 * m + 4 * (lane >> 4) + i], q_);
+        dtf_acc_add(&acc_lds[0][16 * m + 4 * (lane >> 4) + i], s_, FX, slot);
+        dtf_acc_add(&acc_lds[1][16 * m + 4 * (lane >> 4) + i], q_, FX, slot);
       }
     }
   __syncthreads();
   if (tid < TC && o0 + tid < a.Co) {
-    float* st = a.st_out + (long)slot * 2 * a.cmax;
-    atomicAdd(st + o0 + tid, acc_lds[0][tid]);
-    atomicAdd(st + a.cmax + o0 + tid, acc_lds[1][tid]);
+    dtf_acc_t* st = a.st_out + (long)slot * 2 * a.cmax;
+    dtf_acc_addw(st + o0 + tid, acc_lds[0][tid]);
+    dtf_acc_addw(st + a.cmax + o0 + tid, acc_lds[1][tid]);
   }
 }
 
@@ -131,7 +131,7 @@ __global__ __launch_bounds__(256) void f32conv_kernel(F32Args a) {
   constexpr int AE = TC * F_BK / 256;  // A elements per thread per stage
   __shared__ __attribute__((aligned(16))) float sA[2][F_BK * PA];
   __shared__ __attribute__((aligned(16))) float sB[2][F_BK * PB];
-  __shared__ float acc_lds[2][TC];
+  __shared__ dtf_acc_t acc_lds[2][TC];
   extern __shared__ float dyn[];  // transform coefficients: MODE 1: 2 * Ci, MODE 2: 3 * Ci
   const int4 wk = a.work[blockIdx.x];
   DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z >= wk.y && wk.z - wk.y <= TP);
@@ -147,7 +147,7 @@ __global__ __launch_bounds__(256) void f32conv_kernel(F32Args a) {
       if constexpr (MODE == 2) dyn[2 * Ci + i] = cb[2 * a.cmax + i];
     }
   }
-  for (int i = tid; i < 2 * TC; i += 256) (&acc_lds[0][0])[i] = 0.f;
+  for (int i = tid; i < 2 * TC; i += 256) (&acc_lds[0][0])[i] = 0;
   // this thread's B rows (pixels rB + 64 j) and k chunk (4 consecutive k of one tap: Ci % 4 == 0)
   const int rB = tid >> 2, cB = tid & 3;
   const int HWo = a.Ho * a.Wo;
@@ -307,7 +307,9 @@ __global__ __launch_bounds__(256) void f32conv_kernel(F32Args a) {
       f32_epi4<EPI>(a, slot, p, co, p < p1 && co < a.Co, acc[m][n], ss[m], sq[m]);
     }
   }
-  if constexpr (EPI & 4) f32_stats_flush<TC>(a, slot, o0, ss, sq, acc_lds);
+  // forward statistics (y, y^2) or, with the mask, BN-backward sums (dz, dz * xhat): fixed-point scales of the
+  // deterministic build (common.h)
+  if constexpr (EPI & 4) f32_stats_flush<TC, (EPI & 2) ? DTF_FX_GRAD : DTF_FX_STAT>(a, slot, o0, ss, sq, acc_lds);
 }
 
 // ------------------------------------------------------------------------------------------ band fwd / dgrad
@@ -334,7 +336,7 @@ __global__ __launch_bounds__(256) void f32conv_band_kernel(F32Args a) {
   static_assert(NPX % 64 == 0 && W % 4 == 0 && C % 16 == 0 && TCB % 16 == 0, "band geometry");
   __shared__ __attribute__((aligned(16))) float wL[SW];
   __shared__ __attribute__((aligned(16))) float xL[SX];
-  __shared__ float acc_lds[2][TCB];
+  __shared__ dtf_acc_t acc_lds[2][TCB];
   __shared__ float cf[3 * C];
   const int4 wk = a.work[blockIdx.x];
   DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z >= wk.y && wk.w >= 0 && wk.w + TCB <= C);
@@ -349,7 +351,7 @@ __global__ __launch_bounds__(256) void f32conv_band_kernel(F32Args a) {
       if constexpr (MODE == 2) cf[2 * C + i] = cb[2 * a.cmax + i];
     }
   }
-  for (int i = tid; i < 2 * TCB; i += 256) (&acc_lds[0][0])[i] = 0.f;
+  for (int i = tid; i < 2 * TCB; i += 256) (&acc_lds[0][0])[i] = 0;
   // ---- weights: wL[t][r][k] (r = output row o0 + r, k = reduction channel)
   const float* wrow = a.w + (long)slot * a.w_mstride + a.w_off;
   if constexpr (!DGRAD) {
@@ -462,7 +464,7 @@ __global__ __launch_bounds__(256) void f32conv_band_kernel(F32Args a) {
       for (int m = 0; m < MT; ++m)
         f32_epi4<EPI>(a, slot, pbase + pxl[n], o0 + 16 * m + 4 * j4, true, acc[m][n], ss[m], sq[m]);
   }
-  if constexpr (EPI & 4) f32_stats_flush<TCB>(a, slot, o0, ss, sq, acc_lds);
+  if constexpr (EPI & 4) f32_stats_flush<TCB, (EPI & 2) ? DTF_FX_GRAD : DTF_FX_STAT>(a, slot, o0, ss, sq, acc_lds);
 }
 
 // ------------------------------------------------------------------------------------------------------ wgrad
@@ -593,14 +595,14 @@ __global__ __launch_bounds__(256) void f32wgrad_kernel(F32Args a) {
   const int kcol = n0 + 16 * wave + (lane & 15);
   const int tapc = kcol >> a.log2ci, cic = kcol & (Ci - 1);
   if (kcol < K && cic < a.wci) {  // the stem's padded 4th channel has no weight
-    float* g = a.grads + (long)slot * a.g_mstride + a.g_off;
+    dtf_acc_t* g = reinterpret_cast<dtf_acc_t*>(a.grads) + (long)slot * a.g_mstride + a.g_off;
     const long Kw = (long)a.kh * a.kw * a.wci;
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int o = o0 + 16 * m + 4 * (lane >> 4) + i;
-        if (o < a.Co) atomicAdd(g + (long)o * Kw + (long)tapc * a.wci + cic, acc[m][i]);
+        if (o < a.Co) dtf_acc_add(g + (long)o * Kw + (long)tapc * a.wci + cic, acc[m][i], DTF_FX_GRAD, slot);
       }
   }
 }
@@ -770,12 +772,12 @@ __global__ __launch_bounds__(256) void f32wgrad_band_kernel(F32Args a) {
         for (int r = 0; r < 4; ++r) red[((m * 9 + t) * 4 + r) * 64 + lane] = acc[m][t][r];
   }
   __syncthreads();
-  float* g = a.grads + (long)slot * a.g_mstride + a.g_off;
+  dtf_acc_t* g = reinterpret_cast<dtf_acc_t*>(a.grads) + (long)slot * a.g_mstride + a.g_off;
   for (int idx = tid; idx < SRED; idx += 256) {
     const int l = idx & 63, r = (idx >> 6) & 3, mt = idx >> 8;
     const int m = mt / 9, t = mt - m * 9;
     const int o = 16 * m + 4 * (l >> 4) + r, ci = 16 * ct + (l & 15);
-    atomicAdd(g + (long)o * 9 * C + t * C + ci, red[idx]);
+    dtf_acc_add(g + (long)o * 9 * C + t * C + ci, red[idx], DTF_FX_GRAD, slot);
   }
 }
 
@@ -837,8 +839,8 @@ struct F32Sum {
   const float* h2;
   const float* fc;
   const float* fc2;
-  float* sums;
-  float* sums2;
+  dtf_acc_t* sums;
+  dtf_acc_t* sums2;
   const int* img_slot;
   int hw, C, cmax, pad;
 };
@@ -889,13 +891,13 @@ __global__ __launch_bounds__(256) void f32_bwd_sums_kernel(F32Sum a) {
     __syncthreads();
   }
   if (part != 0) return;
-  float* su = a.sums + (long)slot * 2 * a.cmax;
-  atomicAdd(su + c, red[0][c]);
-  atomicAdd(su + a.cmax + c, red[1][c]);
+  dtf_acc_t* su = a.sums + (long)slot * 2 * a.cmax;
+  dtf_acc_add(su + c, red[0][c], DTF_FX_GRAD, slot);
+  dtf_acc_add(su + a.cmax + c, red[1][c], DTF_FX_GRAD, slot);
   if (a.h2) {
-    float* s2 = a.sums2 + (long)slot * 2 * a.cmax;
-    atomicAdd(s2 + c, red[0][c]);
-    atomicAdd(s2 + a.cmax + c, red[2][c]);
+    dtf_acc_t* s2 = a.sums2 + (long)slot * 2 * a.cmax;
+    dtf_acc_add(s2 + c, red[0][c], DTF_FX_GRAD, slot);
+    dtf_acc_add(s2 + a.cmax + c, red[2][c], DTF_FX_GRAD, slot);
   }
 }
 
@@ -912,9 +914,9 @@ struct F32Head {
   float* dlog;          // [N][ncls]
   float* dfeat;         // [N][C]
   const float* cnt;     // images per member
-  float* loss;
+  dtf_acc_t* loss;      // summed mean CE (int64 fixed point in the deterministic build: cg_det_finish converts)
   float* correct;
-  float* sums;          // final-BN backward sums [cap][2][cmax]
+  dtf_acc_t* sums;      // final-BN backward sums [cap][2][cmax]
   const float* bcoef;   // final-BN backward coefficients
   float* gout;          // gradient at x
   int hw, C, ncls, cmax;
@@ -957,7 +959,7 @@ __global__ __launch_bounds__(256) void f32_head_kernel(F32Head a) {
     const float lse = mx + logf(se);
     const int lab = a.labels[img];
     const float bsz = a.cnt[slot];
-    atomicAdd(a.loss + slot, (lse - lg[lab]) / bsz);
+    dtf_acc_add(a.loss + slot, (lse - lg[lab]) / bsz, DTF_FX_GRAD, slot);
     atomicAdd(a.correct + slot, arg == lab ? 1.f : 0.f);
     for (int j = 0; j < a.ncls; ++j) lg[j] = (expf(lg[j] - lse) - (j == lab ? 1.f : 0.f)) / bsz;
   }
@@ -1011,9 +1013,9 @@ __global__ __launch_bounds__(256) void f32_gap_bwd_kernel(F32Head a) {
         q += g * (xv - mu) * iv;
       }
     }
-    float* su = a.sums + (long)slot * 2 * a.cmax;
-    atomicAdd(su + c, s);
-    atomicAdd(su + a.cmax + c, q);
+    dtf_acc_t* su = a.sums + (long)slot * 2 * a.cmax;
+    dtf_acc_add(su + c, s, DTF_FX_GRAD, slot);
+    dtf_acc_add(su + a.cmax + c, q, DTF_FX_GRAD, slot);
   } else {
     const float* bc = a.bcoef ? a.bcoef + (long)slot * 4 * a.cmax : nullptr;
     const long n = (long)a.hw * a.C;
@@ -1181,3 +1183,4 @@ DTF_API int dtf_f32_prep_input(const float* x, float* y, long npix, hipStream_t 
 }
 
 DTF_DEBUG_EXPORT(f32conv)
+DTF_POISON_EXPORT(f32conv)

@@ -226,7 +226,9 @@ def hip_deterministic(args) -> bool:
     statistic replicas, capped workgroups; v1's BN-backward reductions as per-image rows added in image order),
     MNIST (one workgroup per member for every accumulation) and the ImageNet bottleneck nets (every cross-workgroup
     sum as int64 fixed point with integer atomics, common.h DTF_FIXED_ACC)."""
-    return args.model in ("mnist", "cifar10", "imagenet") and getattr(args, "dtype", "bf16") == "bf16"  # fp32: atomics
+    dt = getattr(args, "dtype", "bf16")
+    # fp32: the CIFAR ResNets' fp32 step accumulates in int64 fixed point in the deterministic build too
+    return args.model in ("mnist", "cifar10", "imagenet") and (dt == "bf16" or (dt == "fp32" and args.model == "cifar10"))
 
 
 def parse_main_args(argv=None, defaults=None) -> MainArgs:

@@ -130,8 +130,11 @@ def test_deterministic_flag_selects_det_build(monkeypatch):
         c.apply_runtime_modes()
         assert c.backend == "auto"  # ImageNet: fixed-point (int64) accumulation in the deterministic build
         assert parse_main_args(["--model", "imagenet", "--deterministic", "--backend", "hip"]).backend == "hip"
+        # the fp32 CIFAR step has a deterministic build too (int64 fixed-point accumulation, f32conv.hip)
+        assert parse_main_args(["--model", "cifar10", "--dtype", "fp32", "--deterministic",
+                                "--backend", "hip"]).backend == "hip"
         with pytest.raises(SystemExit):  # an explicit --backend hip must not silently lose the guarantee
-            parse_main_args(["--model", "cifar10", "--dtype", "fp32", "--deterministic", "--backend", "hip"])
+            parse_main_args(["--model", "imagenet", "--dtype", "fp32", "--deterministic", "--backend", "hip"])
         with pytest.raises(SystemExit):  # the debug kernel build is not the deterministic one
             parse_main_args(["--model", "cifar10", "--deterministic", "--debug_kernels"])
         assert kb.LIB_DET.endswith("libdtf_kernels_det.so") and "-DDTF_NREP=64" in kb.DET_FLAGS

@@ -1,6 +1,7 @@
 """Deterministic HIP build check (run with DTF_DETERMINISTIC=1): two identically initialised engines train the same
 steps on the same batches (graph replay, ragged populations) and must hold bitwise-identical state rows -- the
-CIFAR ResNet v2, ResNet v1, ImageNet ResNet-50 v2 / v1 (fixed-point accumulation) and MNIST families.  Prints
+CIFAR ResNet v2, ResNet v1, ImageNet ResNet-50 v2 / v1 (fixed-point accumulation), MNIST and the fp32 CIFAR
+ResNet v2 / v1 (fixed-point accumulation) families.  Prints
 DET_OK."""
 import os
 import sys
@@ -15,7 +16,7 @@ from distributedtf_amd.models.resnet import ResNetArch, cifar_config, imagenet_c
 assert ops.deterministic_mode(), "run with DTF_DETERMINISTIC=1"
 
 
-def run(size, sizes, steps, opt="Momentum", version=2, image=32):
+def run(size, sizes, steps, opt="Momentum", version=2, image=32, dtype=torch.bfloat16):
     if image == 32:
         arch = ResNetArch(cifar_config(size, version=version))
     else:
@@ -23,7 +24,7 @@ def run(size, sizes, steps, opt="Momentum", version=2, image=32):
     dev = torch.device("cuda")
     out = []
     for rep in range(2):
-        e = PopulationEngine(arch, len(sizes), dev, backend="hip")
+        e = PopulationEngine(arch, len(sizes), dev, backend="hip", compute_dtype=dtype)
         hps = []
         for i, bs in enumerate(sizes):
             hp = {"opt_case": {"optimizer": opt, "lr": 0.05, "momentum": 0.9}, "batch_size": bs,
@@ -41,8 +42,9 @@ def run(size, sizes, steps, opt="Momentum", version=2, image=32):
         out.append((e.state.clone(), losses.cpu()))
     st, ls = torch.equal(out[0][0], out[1][0]), torch.equal(out[0][1], out[1][1])
     same = st and ls
-    print("image %d v%d size %d sizes %s steps %d: bitwise identical %s (state %s, losses %s), losses %s"
-          % (image, version, size, sizes, steps, same, st, ls, out[0][1].tolist()), flush=True)
+    print("image %d v%d size %d %s sizes %s steps %d: bitwise identical %s (state %s, losses %s), losses %s"
+          % (image, version, size, str(dtype).split(".")[-1], sizes, steps, same, st, ls, out[0][1].tolist()),
+          flush=True)
     return same
 
 
@@ -75,6 +77,8 @@ def run_mnist(sizes, steps):
 
 ok = all([run(20, [16, 24], 4), run(56, [128], 3), run(56, [128] * 4, 2), run(20, [16, 24], 4, version=1),
           run(56, [128] * 2, 2, version=1), run_mnist([40, 72], 4),
-          run(50, [4, 6], 3, image=64), run(50, [8, 8], 2, version=1, image=64)])
+          run(50, [4, 6], 3, image=64), run(50, [8, 8], 2, version=1, image=64),
+          # the fp32 CIFAR step (f32conv.hip: int64 fixed-point accumulation in this build)
+          run(20, [16, 24], 4, dtype=torch.float32), run(20, [16, 24], 3, version=1, dtype=torch.float32)])
 print("DET_OK" if ok else "DET_FAIL")
 sys.exit(0 if ok else 1)

@@ -42,7 +42,7 @@ def parse():
     p.add_argument("--resnet_version", type=int, default=2, choices=[1, 2])
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp16"],
-                   help="compute dtype; fp32 = the reference's default (CIFAR ResNets: the fp32 HIP step); fp16 = the "
+                   help="compute dtype; fp32 = the reference's default (CIFAR ResNets, MNIST: the fp32 HIP steps); fp16 = the "
                         "reference's fp16 mode (ResNet v2: the half build of the HIP kernels, static loss scale 128)")
     p.add_argument("--exploit_every", type=int, default=None,
                    help="steps between PBT exploit/explore cycles inside the timed region; default "
@@ -107,7 +107,7 @@ def main():
     if args.model == "mnist":
         make = lambda i: MNISTModel(begin + i, hps[begin + i], "/tmp/bench_savedata_%d/model_" % rank,  # noqa: E731
                                     seed=args.seed, device=dev, backend=args.backend, capacity=max(1, cnt),
-                                    use_synthetic_data=True, checkpoint_every_round=False)
+                                    dtype=args.dtype, use_synthetic_data=True, checkpoint_every_round=False)
     elif args.model == "imagenet":
         make = lambda i: ImageNetModel(begin + i, hps[begin + i], "/tmp/bench_savedata_%d/model_" % rank,  # noqa: E731
                                        seed=args.seed, resnet_size=args.resnet_size,

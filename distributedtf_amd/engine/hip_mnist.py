@@ -47,7 +47,7 @@ class MnistArgs(ctypes.Structure):
         ("rng", c_void_p), ("logits_out", c_void_p),
         ("off_c1w", c_int), ("off_c1b", c_int), ("off_c2w", c_int), ("off_c2b", c_int),
         ("off_d1w", c_int), ("off_d1b", c_int), ("off_d2w", c_int), ("off_d2b", c_int),
-        ("drop_rate", c_float), ("train", c_int),
+        ("drop_rate", c_float), ("train", c_int), ("dz32", c_void_p),
     ]
 
 

@@ -280,12 +280,15 @@ def _half_lib_loaded() -> bool:
 
 
 def _hip_f32_ok(engine) -> bool:
-    """fp32 HIP step (engine/hip_f32.py): CIFAR-shape building-block ResNets."""
+    """fp32 HIP steps: CIFAR-shape building-block ResNets (engine/hip_f32.py), the MNIST CNN
+    (engine/hip_mnist_f32.py)."""
     if engine.compute_dtype != torch.float32:
         return False
     from .. import ops
     if ops.half_mode():  # the fp32 step shares 16-bit helper kernels (input packing) with the bf16 build
         return False
+    if getattr(engine.arch, "name", "") == "mnist_cnn":
+        return True
     from .hip_f32 import supports
     return supports(engine.arch)
 
@@ -309,12 +312,15 @@ def make_backend(engine: PopulationEngine, name: str):
         name = "hip" if (engine.device.type == "cuda" and getattr(engine.arch, "hip_supported", False)
                          and (ok16 or _hip_f32_ok(engine) or _hip_f16_ok(engine))) else "torch"
     if name == "hip" and not (ok16 or _hip_f32_ok(engine) or _hip_f16_ok(engine)):
-        raise ValueError("no HIP step for compute dtype %s here (bf16: every family; fp32: the CIFAR ResNets; fp16: "
+        raise ValueError("no HIP step for compute dtype %s here (bf16: every family; fp32: the CIFAR ResNets and MNIST; fp16: "
                          "the ResNet v2 families under DTF_HALF=1, which --dtype fp16 sets): use the torch backend"
                          % engine.compute_dtype)
     if name == "torch":
         return TorchBackend(engine)
     if name == "hip" and engine.compute_dtype == torch.float32:
+        if getattr(engine.arch, "name", "") == "mnist_cnn":
+            from .hip_mnist_f32 import HipMnistF32Backend
+            return HipMnistF32Backend(engine)
         from .hip_f32 import HipResNetF32Backend
         return HipResNetF32Backend(engine)
     if name == "hip":

@@ -67,6 +67,7 @@ struct MnistArgs {
   int off_c1w, off_c1b, off_c2w, off_c2b, off_d1w, off_d1b, off_d2w, off_d2b;
   float drop_rate;
   int train;
+  float* dz32;           // fp32 step (engine/hip_mnist_f32.py): dz stored fp32 here instead of bf16 in ``dz``
 };
 
 // ------------------------------------------------------------------------------------------ conv1
@@ -550,8 +551,11 @@ __global__ __launch_bounds__(256) void mnist_head_kernel(MnistArgs a) {
         dzv[k] = pre[k] > 0.f ? dh * keep[k] : 0.f;
         db1[k] += dzv[k];
       }
-      *reinterpret_cast<uint2*>(a.dz + (long)img * 1024 + f0) =
-          make_uint2(pack2bf(dzv[0], dzv[1]), pack2bf(dzv[2], dzv[3]));
+      if (a.dz32)
+        *reinterpret_cast<float4*>(a.dz32 + (long)img * 1024 + f0) = make_float4(dzv[0], dzv[1], dzv[2], dzv[3]);
+      else
+        *reinterpret_cast<uint2*>(a.dz + (long)img * 1024 + f0) =
+            make_uint2(pack2bf(dzv[0], dzv[1]), pack2bf(dzv[2], dzv[3]));
     }
   }
   if (tid == 0) {
@@ -579,6 +583,95 @@ __global__ __launch_bounds__(256) void mnist_wd_prep_kernel(MnistArgs a, const i
   for (int e = blockIdx.x * 256 + threadIdx.x; e < 51200; e += gridDim.x * 256) {
     const int co = e & 63, rest = e >> 6, tp = rest % 25, ci = rest / 25;
     d[e] = f2bf(w[(co * 25 + 24 - tp) * 32 + ci]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------ fp32 step helpers
+// The fp32 step (engine/hip_mnist_f32.py) runs conv1 / conv2 / dense1 and their gradients on the generic fp32
+// MFMA conv kernels (f32conv.hip, v_mfma_f32_16x16x4_f32); these are the pieces around them: the 1 -> 4 channel
+// input packing, bias + ReLU + 2x2 max-pool (argmax kept) and its backward (un-pool, ReLU mask, bias gradient).
+struct PoolArgs {
+  const float* h;       // [N, H, H, C] conv output before the bias
+  float* p;             // [N, H/2, H/2, C] max-pool of relu(h + b)
+  uint8_t* am;          // [N, H/2, H/2, C] argmax (dy * 2 + dx)
+  const float* dp;      // backward: dL/dp
+  float* dh;            // backward: dL/dh
+  const int* img_slot;  // [N]
+  const int4* work;     // backward: (img0, nimg, 0, slot) image chunks of one member
+  const float* params;
+  long p_mstride;
+  dtf_acc_t* grads;     // bias gradient rows (the int64 accumulator rows in the deterministic build)
+  long g_mstride;
+  int b_off, H, C, pad_;
+  long nimg;
+};
+
+__global__ __launch_bounds__(256) void mnist_f32_prep_kernel(const float* __restrict__ x, float* __restrict__ x4,
+                                                             long npix) {
+  for (long p = (long)blockIdx.x * 256 + threadIdx.x; p < npix; p += (long)gridDim.x * 256)
+    *reinterpret_cast<float4*>(x4 + 4 * p) = make_float4(x[p], 0.f, 0.f, 0.f);
+}
+
+// one thread per pooled pixel and 4 channels; ties keep the first window position (the ReLU zeros carry no gradient)
+__global__ __launch_bounds__(256) void mnist_f32_pool_kernel(PoolArgs a) {
+  const int Ho = a.H >> 1, C4 = a.C >> 2;
+  const long total = a.nimg * Ho * Ho * C4;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int c = (int)(e % C4) * 4;
+    const long q = e / C4;
+    const long img = q / (Ho * Ho);
+    const int pix = (int)(q - img * Ho * Ho), oy = pix / Ho, ox = pix - oy * Ho;
+    const float* br = a.params + (long)a.img_slot[img] * a.p_mstride + a.b_off + c;
+    const float b[4] = {br[0], br[1], br[2], br[3]};
+    float best[4] = {-3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f};
+    uint32_t arg[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const float4 v = *reinterpret_cast<const float4*>(
+          a.h + ((img * a.H + 2 * oy + (d >> 1)) * a.H + 2 * ox + (d & 1)) * a.C + c);
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float t = fmaxf(vv[i] + b[i], 0.f);
+        if (t > best[i]) {
+          best[i] = t;
+          arg[i] = (uint32_t)d;
+        }
+      }
+    }
+    *reinterpret_cast<float4*>(a.p + q * a.C + c) = make_float4(best[0], best[1], best[2], best[3]);
+    *reinterpret_cast<uint32_t*>(a.am + q * a.C + c) = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+  }
+}
+
+// dh = un-pool(dp masked by p > 0); bias gradient = sum of the masked dp over the chunk's pixels (fixed in-workgroup
+// order, one accumulator add per workgroup and channel).  C in {32, 64}: thread = (pixel group, channel).
+__global__ __launch_bounds__(256) void mnist_f32_unpool_kernel(PoolArgs a) {
+  __shared__ float red[256];
+  const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 1 && wk.w >= 0);
+  const int img0 = wk.x, nimg = wk.y, slot = wk.w;
+  const int Ho = a.H >> 1, C = a.C, tid = threadIdx.x;
+  const int c = tid % C, G = 256 / C;
+  const long base = (long)img0 * Ho * Ho, n = (long)nimg * Ho * Ho;
+  float db = 0.f;
+  for (long q = tid / C; q < n; q += G) {
+    const long e = (base + q) * C + c;
+    const float v = a.p[e] > 0.f ? a.dp[e] : 0.f;
+    const int am = a.am[e];
+    db += v;
+    const long pq = base + q, img = pq / (Ho * Ho);
+    const int pix = (int)(pq - img * Ho * Ho), oy = pix / Ho, ox = pix - oy * Ho;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      a.dh[((img * a.H + 2 * oy + (d >> 1)) * a.H + 2 * ox + (d & 1)) * C + c] = d == am ? v : 0.f;
+  }
+  red[tid] = db;
+  __syncthreads();
+  if (tid < C) {
+    float s = 0.f;
+    for (int g = 0; g < G; ++g) s += red[g * C + tid];
+    dtf_acc_add(a.grads + (long)slot * a.g_mstride + a.b_off + tid, s, DTF_FX_GRAD, slot);
   }
 }
 
@@ -625,6 +718,34 @@ DTF_API int dtf_mnist_conv2_wgrad(const MnistArgs* a, int nwork, hipStream_t str
 DTF_API int dtf_mnist_conv1_wgrad(const MnistArgs* a, int nwork, hipStream_t stream) {
   if (nwork <= 0) return 0;
   hipLaunchKernelGGL(mnist_conv1_wgrad_kernel, dim3(nwork), dim3(256), 0, stream, *a);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_mnist_pool_args_size() { return (int)sizeof(PoolArgs); }
+
+DTF_API int dtf_mnist_f32_prep(const float* x, float* x4, long npix, hipStream_t stream) {
+  long blocks = (npix + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks <= 0) return 0;
+  DTF_HOST_CHECK(DTF_ALIGNED16(x4));
+  hipLaunchKernelGGL(mnist_f32_prep_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, x4, npix);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_mnist_f32_pool(const PoolArgs* a, hipStream_t stream) {
+  if (a->nimg <= 0) return 0;
+  if ((a->C & 3) != 0 || (a->H & 1) != 0) return -2;
+  DTF_HOST_CHECK(DTF_ALIGNED16(a->h) && DTF_ALIGNED16(a->p));
+  long blocks = (a->nimg * (a->H / 2) * (a->H / 2) * (a->C / 4) + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(mnist_f32_pool_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, *a);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_mnist_f32_unpool(const PoolArgs* a, int nwork, hipStream_t stream) {
+  if (nwork <= 0) return 0;
+  if (a->C != 32 && a->C != 64) return -2;
+  hipLaunchKernelGGL(mnist_f32_unpool_kernel, dim3(nwork), dim3(256), 0, stream, *a);
   return DTF_CHECK_LAUNCH();
 }
 

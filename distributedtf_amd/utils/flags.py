@@ -228,7 +228,8 @@ def hip_deterministic(args) -> bool:
     sum as int64 fixed point with integer atomics, common.h DTF_FIXED_ACC)."""
     dt = getattr(args, "dtype", "bf16")
     # fp32: the CIFAR ResNets' fp32 step accumulates in int64 fixed point in the deterministic build too
-    return args.model in ("mnist", "cifar10", "imagenet") and (dt == "bf16" or (dt == "fp32" and args.model == "cifar10"))
+    return args.model in ("mnist", "cifar10", "imagenet") and (dt == "bf16" or (dt == "fp32" and args.model in
+                                                                                  ("cifar10", "mnist")))
 
 
 def parse_main_args(argv=None, defaults=None) -> MainArgs:
@@ -238,9 +239,9 @@ def parse_main_args(argv=None, defaults=None) -> MainArgs:
         args.population_size = args.pop_size
     if args.resnet_version == 1 and args.dtype == "fp16":
         p.error("ResNet version 1 is not currently supported with fp16. Please use version 2 instead.")
-    if args.dtype == "fp32" and args.model == "cifar10":
-        # fp32 CIFAR ResNets run the fp32 HIP step (engine/hip_f32.py: v_mfma_f32_16x16x4_f32, fp32 tensors); a
-        # static loss scale is a PyTorch-path feature
+    if args.dtype == "fp32" and args.model in ("cifar10", "mnist"):
+        # fp32 CIFAR ResNets and the MNIST CNN run the fp32 HIP steps (engine/hip_f32.py, engine/hip_mnist_f32.py:
+        # v_mfma_f32_16x16x4_f32, fp32 tensors); a static loss scale is a PyTorch-path feature
         if args.loss_scale is not None and args.loss_scale != 1:
             if args.backend == "hip":
                 p.error("--loss_scale with --dtype fp32: the fp32 HIP step does not scale the loss; use --backend torch")

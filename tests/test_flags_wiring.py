@@ -86,7 +86,9 @@ def test_dtype_routing():
         parse_main_args(["--model", "cifar10", "--dtype", "fp32", "--loss_scale", "8", "--backend", "hip"])
     with pytest.raises(SystemExit):
         parse_main_args(["--model", "imagenet", "--dtype", "fp32", "--backend", "hip"])
-    assert parse_main_args(["--model", "mnist", "--dtype", "fp32"]).backend == "torch"
+    # MNIST fp32 stays on HIP (engine/hip_mnist_f32.py: the generic fp32 MFMA conv kernels)
+    assert parse_main_args(["--model", "mnist", "--dtype", "fp32"]).backend == "auto"
+    assert parse_main_args(["--model", "mnist", "--dtype", "fp32", "--backend", "hip"]).backend == "hip"
     with pytest.raises(SystemExit):
         parse_main_args(["--model", "cifar10", "--loss_scale", "8"])  # bf16 HIP path: no loss scaling
     a = parse_main_args(["--model", "cifar10", "--dtype", "fp16"])
@@ -132,6 +134,8 @@ def test_deterministic_flag_selects_det_build(monkeypatch):
         assert parse_main_args(["--model", "imagenet", "--deterministic", "--backend", "hip"]).backend == "hip"
         # the fp32 CIFAR step has a deterministic build too (int64 fixed-point accumulation, f32conv.hip)
         assert parse_main_args(["--model", "cifar10", "--dtype", "fp32", "--deterministic",
+                                "--backend", "hip"]).backend == "hip"
+        assert parse_main_args(["--model", "mnist", "--dtype", "fp32", "--deterministic",
                                 "--backend", "hip"]).backend == "hip"
         with pytest.raises(SystemExit):  # an explicit --backend hip must not silently lose the guarantee
             parse_main_args(["--model", "imagenet", "--dtype", "fp32", "--deterministic", "--backend", "hip"])

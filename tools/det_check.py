@@ -48,14 +48,15 @@ def run(size, sizes, steps, opt="Momentum", version=2, image=32, dtype=torch.bfl
     return same
 
 
-def run_mnist(sizes, steps):
-    """The MNIST HIP step (deterministic work splits: one accumulation workgroup per member, hip_mnist.py)."""
+def run_mnist(sizes, steps, dtype=torch.bfloat16):
+    """The MNIST HIP step (deterministic work splits: one accumulation workgroup per member, hip_mnist.py; fp32:
+    hip_mnist_f32.py, int64 fixed-point gradient accumulation)."""
     from distributedtf_amd.models.mnist import MnistArch
     arch = MnistArch()
     dev = torch.device("cuda")
     out = []
     for rep in range(2):
-        e = PopulationEngine(arch, len(sizes), dev, backend="hip")
+        e = PopulationEngine(arch, len(sizes), dev, backend="hip", compute_dtype=dtype)
         hps = []
         for i, bs in enumerate(sizes):
             hp = {"opt_case": {"optimizer": "Adam", "lr": 1e-3}, "batch_size": bs, "initializer": "he_init"}
@@ -70,7 +71,8 @@ def run_mnist(sizes, steps):
         torch.cuda.synchronize()
         out.append((e.state.clone(), losses.cpu()))
     same = torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
-    print("mnist sizes %s steps %d: bitwise identical %s, losses %s" % (sizes, steps, same, out[0][1].tolist()),
+    print("mnist %s sizes %s steps %d: bitwise identical %s, losses %s" % (str(dtype).split(".")[-1], sizes, steps,
+                                                                          same, out[0][1].tolist()),
           flush=True)
     return same
 
@@ -79,6 +81,7 @@ ok = all([run(20, [16, 24], 4), run(56, [128], 3), run(56, [128] * 4, 2), run(20
           run(56, [128] * 2, 2, version=1), run_mnist([40, 72], 4),
           run(50, [4, 6], 3, image=64), run(50, [8, 8], 2, version=1, image=64),
           # the fp32 CIFAR step (f32conv.hip: int64 fixed-point accumulation in this build)
-          run(20, [16, 24], 4, dtype=torch.float32), run(20, [16, 24], 3, version=1, dtype=torch.float32)])
+          run(20, [16, 24], 4, dtype=torch.float32), run(20, [16, 24], 3, version=1, dtype=torch.float32),
+          run_mnist([40, 72], 4, dtype=torch.float32)])
 print("DET_OK" if ok else "DET_FAIL")
 sys.exit(0 if ok else 1)

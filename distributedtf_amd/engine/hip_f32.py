@@ -49,7 +49,7 @@ class F32Args(ctypes.Structure):
         ("c_ep", c_void_p), ("st_out", c_void_p), ("work", c_void_p),
         ("Hi", c_int), ("Wi", c_int), ("Ci", c_int), ("Ho", c_int), ("Wo", c_int), ("Co", c_int),
         ("kh", c_int), ("kw", c_int), ("stride", c_int), ("pad", c_int), ("cmax", c_int), ("log2ci", c_int),
-        ("wci", c_int), ("pad_", c_int),
+        ("wci", c_int), ("wrows", c_int),
     ]
 
 

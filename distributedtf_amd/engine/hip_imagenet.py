@@ -162,6 +162,7 @@ def _log2(n):
 class HipImageNetBackend:
     name = "hip"
     accepts_index_batches = False
+    _plan_cls = None  # _ImageNetPlan (set below); the fp32 backend: engine/hip_imagenet_f32.py
 
     def __init__(self, engine):
         _register()
@@ -236,7 +237,7 @@ class HipImageNetBackend:
         if p is None:
             if len(self._plans) > 4:
                 self._plans.clear()
-            p = _ImageNetPlan(self, list(slots), list(sizes))
+            p = self._plan_cls(self, list(slots), list(sizes))
             self._plans[key] = p
         return p
 
@@ -266,7 +267,7 @@ class HipImageNetBackend:
         if p is None:
             if len(plans) >= 4:
                 plans.pop(next(iter(plans)))  # oldest first
-            p = _ImageNetPlan(self, list(slots), [int(m)] * len(slots), eval_mode=True)
+            p = self._plan_cls(self, list(slots), [int(m)] * len(slots), eval_mode=True)
             plans[key] = p
         return p
 
@@ -324,12 +325,12 @@ class _ImageNetPlan:
         self.slots_t = torch.tensor(slots, dtype=torch.int32, device=dev)
         self.slots_long = torch.tensor(slots, dtype=torch.long, device=dev)
         self.loss_sel = torch.zeros(len(slots), dtype=be.loss.dtype, device=dev)
-        bf = ops.act_dtype()
+        bf = self._act_dtype()
         H = cfg.image_size
         self.H = H
         self.x_in = torch.zeros(N, H, H, cfg.in_channels, dtype=torch.float32, device=dev)
         self.labels = torch.zeros(N, dtype=torch.int32, device=dev)
-        self.xin8 = torch.zeros(N, H, H, 8, dtype=bf, device=dev)
+        self.xin8 = torch.zeros(N, H, H, self._stem_cin(), dtype=bf, device=dev)  # channel-padded stem input
         H1 = H // 2
         H2 = (H1 + 1) // 2
         pool = {}
@@ -394,11 +395,17 @@ class _ImageNetPlan:
         self.graph = None
 
     # ----------------------------------------------------------------------------------------- helpers
+    def _act_dtype(self):
+        return ops.act_dtype()  # bf16 (fp16 in the half build)
+
+    def _stem_cin(self):
+        return 8  # the stem gathers 8-channel chunks of the 3-channel input
+
     def tmp(self, name, hw, c):
         key = (name, hw, c)
         t = self._tmp.get(key)
         if t is None:
-            t = torch.empty(self.N, hw, hw, c, dtype=ops.act_dtype(), device=self.be.dev)
+            t = torch.empty(self.N, hw, hw, c, dtype=self._act_dtype(), device=self.be.dev)
             self._tmp[key] = t
         return t
 
@@ -600,27 +607,84 @@ class _ImageNetPlan:
             self._add(ops.lib().dtf_cg_det_finish, _p(be.gacc), _p(e.grads), e.Pp, e.Pp, _p(self.slots_t),
                       len(self.slots), _p(be.loss64), _p(be.loss))
 
+    # ------------------------------------------------------------------------- kernel vocabulary (non-conv ops)
+    # The fp32 plan (engine/hip_imagenet_f32.py) runs the same program with fp32 kernels by overriding these, conv,
+    # wgrad, ew, bn_add_relu and bwd_sums.
+    def prep_weights(self):
+        """Padded stem copy and the [NPAD_CLS][C] bf16 dense operand of every member of the plan (every other conv
+        reads the optimizer's bf16 shadow)."""
+        be, e, prog, cfg = self.be, self.e, self.be.prog, self.be.cfg
+        L, ns = ops.lib(), len(self.slots)
+        self._add(L.dtf_cg_weight_prep, _p(e.state), e.S, _p(be.conv_table), 1, _p(self.slots_t), ns,
+                  _p(be.w), _p(be.w), be.wtot)
+        self._add(L.dtf_cg_dense_prep, _p(e.state), e.S, prog.dense_w_off, be.ncls, NPAD_CLS, cfg.final_size,
+                  _p(self.slots_t), ns, _p(be.dense), NPAD_CLS * cfg.final_size)
+
+    def prep_input(self):
+        self._add(ops.lib().dtf_cg_prep_input, _p(self.x_in), _p(self.xin8), self.N * self.H * self.H,
+                  self.be.cfg.in_channels)
+
+    def maxpool(self, x, y, H1, H2):
+        self._add(ops.lib().dtf_cg_maxpool, _p(x), _p(y), _p(self.am0), None, None, self.N, H1, H1, H2, H2,
+                  self.be.cfg.num_filters, 0)
+
+    def maxpool_bwd(self, g, dx, H1, H2):
+        self._add(ops.lib().dtf_cg_maxpool, None, None, _p(self.am0), _p(g), _p(dx), self.N, H1, H1, H2, H2,
+                  self.be.cfg.num_filters, 1)
+
+    def chan_stats(self, x, sums, hw, C):
+        self._add(ops.lib().dtf_cg_chan_stats, _p(x), _p(self.img_slot), _p(sums), self.N, hw, C, CMAX)
+
+    def gap(self, g, which):
+        self._add(ops.lib().dtf_cg_gap, ctypes.byref(g), which, self.N)
+
+    def dense_head(self, train):
+        """Dense layer + softmax CE on the GAP features: the grouped bf16 GEMM (padded to NPAD_CLS classes) per
+        member, cg_softmax_ce (bias, loss, correct count, dlogits, dbias); training adds dfeat = dlogits W and
+        dW += dlogits^T feat."""
+        be, e, prog, cfg = self.be, self.e, self.be.prog, self.be.cfg
+        L = ops.lib()
+        from .hip_mnist import GEMM_OUT_ACC, GEMM_OUT_F32, GroupedGemm
+        C = cfg.final_size
+        Dstride = NPAD_CLS * C
+        fwd, dgr, wgr = [], [], []
+        for s, n in zip(self.slots, self.sizes):
+            f0 = self.first[s]
+            fwd.append((f0 * C, s * Dstride, f0 * NPAD_CLS, n, NPAD_CLS, C))
+            dgr.append((f0 * NPAD_CLS, s * Dstride, f0 * C, n, C, NPAD_CLS))
+            wgr.append((f0 * NPAD_CLS, f0 * C, s * e.Pp + prog.dense_w_off, NPAD_CLS, C, n, be.ncls))
+        dev = be.dev
+        self.g_fwd = GroupedGemm(self.feat, be.dense, self.logits, C, C, NPAD_CLS, fwd, False, False, GEMM_OUT_F32, dev)
+        self._add("gemm", self.g_fwd)
+        if not train:
+            self._add(L.dtf_cg_softmax_ce, _p(self.logits), NPAD_CLS, be.ncls, _p(self.labels), _p(self.img_slot),
+                      _p(e.state), e.S, prog.dense_b_off, None, e.Pp, _p(self.cnt), _p(self.ev_loss),
+                      _p(self.ev_acc[0]), None, self.N, 1.0)
+            return
+        self.g_dgr = GroupedGemm(self.dlog, be.dense, self.dfeat, NPAD_CLS, C, C, dgr, False, True, GEMM_OUT_F32, dev)
+        self.g_wgr = GroupedGemm(self.dlog, self.feat, e.grads, NPAD_CLS, C, C, wgr, True, True, GEMM_OUT_ACC, dev)
+        self._add(L.dtf_cg_softmax_ce, _p(self.logits), NPAD_CLS, be.ncls, _p(self.labels), _p(self.img_slot),
+                  _p(e.state), e.S, prog.dense_b_off, _p(be.acc_grads), e.Pp, _p(self.cnt), _p(be.acc_loss),
+                  _p(be.correct), _p(self.dlog), self.N, be.loss_scale)
+        self._add("gemm", self.g_dgr)
+        self._add("gemm", self.g_wgr)
+
     # ------------------------------------------------------------------------------------------ program
     def _build(self):
         be, e, prog, cfg = self.be, self.e, self.be.prog, self.be.cfg
         L = ops.lib()
         N, H = self.N, self.H
         ns = len(self.slots)
-        self._add(L.dtf_cg_weight_prep, _p(e.state), e.S, _p(be.conv_table), 1, _p(self.slots_t), ns,
-                  _p(be.w), _p(be.w), be.wtot)  # padded stem only; every other conv reads the shadow
-        self._add(L.dtf_cg_dense_prep, _p(e.state), e.S, prog.dense_w_off, be.ncls, NPAD_CLS, cfg.final_size,
-                  _p(self.slots_t), ns, _p(be.dense), NPAD_CLS * cfg.final_size)
+        self.prep_weights()
         self._add("zero", be.sums)
         self._add("zero", be.loss)
         self._add("zero", be.correct)
-        self._add(L.dtf_cg_prep_input, _p(self.x_in), _p(self.xin8), N * H * H, cfg.in_channels)
+        self.prep_input()
         # ---- stem: conv 7x7/2 (no BN in v2) -> max-pool 3x3/2
         H1, H2 = H // 2, self.xs[0].shape[1]
         self.conv(prog.stem, self.xin8, self.y0, H, mode=0, epi=0)
-        self._add(L.dtf_cg_maxpool, _p(self.y0), _p(self.xs[0]), _p(self.am0), None, None, N, H1, H1, H2, H2,
-                  cfg.num_filters, 0)
-        self._add(L.dtf_cg_chan_stats, _p(self.xs[0]), _p(self.img_slot), _p(self.sf(prog.blocks[0].bns[0])), N,
-                  H2 * H2, cfg.num_filters, CMAX)
+        self.maxpool(self.y0, self.xs[0], H1, H2)
+        self.chan_stats(self.xs[0], self.sf(prog.blocks[0].bns[0]), H2 * H2, cfg.num_filters)
         nblk = len(prog.blocks)
         for i, blk in enumerate(prog.blocks):
             hi, ho, cin, f, fout = self.geo[i]
@@ -659,37 +723,18 @@ class _ImageNetPlan:
         g.dfeat, g.sums, g.bcoef = _p(self.dfeat), _p(self.sb(fb)), _p(self.cb(fb))
         g.hw, g.C, g.cmax = HL * HL, cfg.final_size, CMAX
         self._hold(g)
-        self._add(L.dtf_cg_gap, ctypes.byref(g), 0, N)
+        self.gap(g, 0)
         # ---- dense + softmax CE
-        from .hip_mnist import GEMM_OUT_ACC, GEMM_OUT_F32, GroupedGemm
-        C = cfg.final_size
-        Dstride = NPAD_CLS * C
-        fwd, dgr, wgr = [], [], []
-        for s, n in zip(self.slots, self.sizes):
-            f0 = self.first[s]
-            fwd.append((f0 * C, s * Dstride, f0 * NPAD_CLS, n, NPAD_CLS, C))
-            dgr.append((f0 * NPAD_CLS, s * Dstride, f0 * C, n, C, NPAD_CLS))
-            wgr.append((f0 * NPAD_CLS, f0 * C, s * e.Pp + prog.dense_w_off, NPAD_CLS, C, n, be.ncls))
-        dev = be.dev
-        self.g_fwd = GroupedGemm(self.feat, be.dense, self.logits, C, C, NPAD_CLS, fwd, False, False, GEMM_OUT_F32, dev)
-        self.g_dgr = GroupedGemm(self.dlog, be.dense, self.dfeat, NPAD_CLS, C, C, dgr, False, True, GEMM_OUT_F32, dev)
-        self.g_wgr = GroupedGemm(self.dlog, self.feat, e.grads, NPAD_CLS, C, C, wgr, True, True, GEMM_OUT_ACC, dev)
-        self._add("gemm", self.g_fwd)
-        self._add(L.dtf_cg_softmax_ce, _p(self.logits), NPAD_CLS, be.ncls, _p(self.labels), _p(self.img_slot),
-                  _p(e.state), e.S, prog.dense_b_off, _p(be.acc_grads), e.Pp, _p(self.cnt), _p(be.acc_loss),
-                  _p(be.correct),
-                  _p(self.dlog), N, be.loss_scale)
-        self._add("gemm", self.g_dgr)
-        self._add("gemm", self.g_wgr)
+        self.dense_head(True)
         # ---- final BN backward -> gradient at the last block output
-        self._add(L.dtf_cg_gap, ctypes.byref(g), 1, N)
+        self.gap(g, 1)
         self.bn_final(fb, HL, True)
-        gcur = self.tmp("g0", HL, C)
+        gcur = self.tmp("g0", HL, cfg.final_size)
         g2 = GapArgs()
         ctypes.memmove(ctypes.addressof(g2), ctypes.addressof(g), ctypes.sizeof(GapArgs))
         g2.out = _p(gcur)
         self._hold(g2)
-        self._add(L.dtf_cg_gap, ctypes.byref(g2), 2, N)
+        self.gap(g2, 2)
         # ---- blocks, reversed
         for i in range(nblk - 1, -1, -1):
             blk = prog.blocks[i]
@@ -731,7 +776,7 @@ class _ImageNetPlan:
             gcur = gnext
         # ---- stem: max-pool backward, stem wgrad (padded input, 3 real channels)
         dy0 = self.tmp("dy0", H1, cfg.num_filters)
-        self._add(L.dtf_cg_maxpool, None, None, _p(self.am0), _p(gcur), _p(dy0), N, H1, H1, H2, H2, cfg.num_filters, 1)
+        self.maxpool_bwd(gcur, dy0, H1, H2)
         self.wgrad(prog.stem, self.xin8, dy0, H, mode_x=0, mode_dy=0)
         self.det_finish()
         self._add("optim", None)
@@ -747,18 +792,14 @@ class _ImageNetPlan:
         N, H = self.N, self.H
         ns = len(self.slots)
         sink = self.ev_sink
-        self._add(L.dtf_cg_weight_prep, _p(e.state), e.S, _p(be.conv_table), 1, _p(self.slots_t), ns,
-                  _p(be.w), _p(be.w), be.wtot)
-        self._add(L.dtf_cg_dense_prep, _p(e.state), e.S, prog.dense_w_off, be.ncls, NPAD_CLS, cfg.final_size,
-                  _p(self.slots_t), ns, _p(be.dense), NPAD_CLS * cfg.final_size)
+        self.prep_weights()
         for b in range(len(prog.bns)):
             hw = 1  # the eval coefficients do not depend on the spatial size
             self.bn_final(b, hw, 2)
-        self._add(L.dtf_cg_prep_input, _p(self.x_in), _p(self.xin8), N * H * H, cfg.in_channels)
+        self.prep_input()
         H1, H2 = H // 2, self.xs[0].shape[1]
         self.conv(prog.stem, self.xin8, self.y0, H, mode=0, epi=0)
-        self._add(L.dtf_cg_maxpool, _p(self.y0), _p(self.xs[0]), _p(self.am0), None, None, N, H1, H1, H2, H2,
-                  cfg.num_filters, 0)
+        self.maxpool(self.y0, self.xs[0], H1, H2)
         relu = L.dtf_cg_bn_relu_apply
         for i, blk in enumerate(prog.blocks):
             hi, ho, cin, f, fout = self.geo[i]
@@ -781,18 +822,8 @@ class _ImageNetPlan:
         g.dfeat, g.sums, g.bcoef = _p(self.dfeat), _p(sink), _p(self.cf(fb))
         g.hw, g.C, g.cmax = HL * HL, cfg.final_size, CMAX
         self._hold(g)
-        self._add(L.dtf_cg_gap, ctypes.byref(g), 0, N)
-        from .hip_mnist import GEMM_OUT_F32, GroupedGemm
-        C = cfg.final_size
-        Dstride = NPAD_CLS * C
-        fwd = [(self.first[s] * C, s * Dstride, self.first[s] * NPAD_CLS, n, NPAD_CLS, C)
-               for s, n in zip(self.slots, self.sizes)]
-        self.g_fwd = GroupedGemm(self.feat, be.dense, self.logits, C, C, NPAD_CLS, fwd, False, False, GEMM_OUT_F32,
-                                 be.dev)
-        self._add("gemm", self.g_fwd)
-        self._add(L.dtf_cg_softmax_ce, _p(self.logits), NPAD_CLS, be.ncls, _p(self.labels), _p(self.img_slot),
-                  _p(e.state), e.S, prog.dense_b_off, None, e.Pp, _p(self.cnt), _p(self.ev_loss),
-                  _p(self.ev_acc[0]), None, N, 1.0)
+        self.gap(g, 0)
+        self.dense_head(False)
 
     # ------------------------------------------------------------------------------------ ResNet v1 program
     def bn_add_relu(self, h, s, out, coef_h, coef_s, hw, C):
@@ -830,8 +861,7 @@ class _ImageNetPlan:
         if train:
             self.bn_final(sb, H1, False)
         self.ew(relu, self.y0, self.a0, self.cf(sb), H1, cfg.num_filters)
-        self._add(L.dtf_cg_maxpool, _p(self.a0), _p(self.xs[0]), _p(self.am0), None, None, N, H1, H1, H2, H2,
-                  cfg.num_filters, 0)
+        self.maxpool(self.a0, self.xs[0], H1, H2)
         for i, blk in enumerate(prog.blocks):
             hi, ho, cin, f, fout = self.geo[i]
             b1, b2, b3 = blk.bns
@@ -862,14 +892,11 @@ class _ImageNetPlan:
         L = ops.lib()
         N, H = self.N, self.H
         ns = len(self.slots)
-        self._add(L.dtf_cg_weight_prep, _p(e.state), e.S, _p(be.conv_table), 1, _p(self.slots_t), ns,
-                  _p(be.w), _p(be.w), be.wtot)
-        self._add(L.dtf_cg_dense_prep, _p(e.state), e.S, prog.dense_w_off, be.ncls, NPAD_CLS, cfg.final_size,
-                  _p(self.slots_t), ns, _p(be.dense), NPAD_CLS * cfg.final_size)
+        self.prep_weights()
         self._add("zero", be.sums)
         self._add("zero", be.loss)
         self._add("zero", be.correct)
-        self._add(L.dtf_cg_prep_input, _p(self.x_in), _p(self.xin8), N * H * H, cfg.in_channels)
+        self.prep_input()
         self._forward_v1()
         H1, H2, HL = H // 2, self.xs[0].shape[1], self.HL
         C = cfg.final_size
@@ -879,33 +906,15 @@ class _ImageNetPlan:
         g.dfeat, g.sums, g.bcoef = _p(self.dfeat), None, None
         g.hw, g.C, g.cmax = HL * HL, C, CMAX
         self._hold(g)
-        self._add(L.dtf_cg_gap, ctypes.byref(g), 0, N)
-        from .hip_mnist import GEMM_OUT_ACC, GEMM_OUT_F32, GroupedGemm
-        Dstride = NPAD_CLS * C
-        fwd, dgr, wgr = [], [], []
-        for s, n in zip(self.slots, self.sizes):
-            f0 = self.first[s]
-            fwd.append((f0 * C, s * Dstride, f0 * NPAD_CLS, n, NPAD_CLS, C))
-            dgr.append((f0 * NPAD_CLS, s * Dstride, f0 * C, n, C, NPAD_CLS))
-            wgr.append((f0 * NPAD_CLS, f0 * C, s * e.Pp + prog.dense_w_off, NPAD_CLS, C, n, be.ncls))
-        dev = be.dev
-        self.g_fwd = GroupedGemm(self.feat, be.dense, self.logits, C, C, NPAD_CLS, fwd, False, False, GEMM_OUT_F32, dev)
-        self.g_dgr = GroupedGemm(self.dlog, be.dense, self.dfeat, NPAD_CLS, C, C, dgr, False, True, GEMM_OUT_F32, dev)
-        self.g_wgr = GroupedGemm(self.dlog, self.feat, e.grads, NPAD_CLS, C, C, wgr, True, True, GEMM_OUT_ACC, dev)
-        self._add("gemm", self.g_fwd)
-        self._add(L.dtf_cg_softmax_ce, _p(self.logits), NPAD_CLS, be.ncls, _p(self.labels), _p(self.img_slot),
-                  _p(e.state), e.S, prog.dense_b_off, _p(be.acc_grads), e.Pp, _p(self.cnt), _p(be.acc_loss),
-                  _p(be.correct),
-                  _p(self.dlog), N, be.loss_scale)
-        self._add("gemm", self.g_dgr)
-        self._add("gemm", self.g_wgr)
+        self.gap(g, 0)
+        self.dense_head(True)
         # GAP backward: the gradient at the last block output, masked by its ReLU (cg_gap_bwd_apply, coef = null)
         gz = self.tmp("gA" if (len(prog.blocks) % 2 == 0) else "gB", HL, C)
         g2 = GapArgs()
         ctypes.memmove(ctypes.addressof(g2), ctypes.addressof(g), ctypes.sizeof(GapArgs))
         g2.out = _p(gz)
         self._hold(g2)
-        self._add(L.dtf_cg_gap, ctypes.byref(g2), 2, N)
+        self.gap(g2, 2)
         bwd = L.dtf_cg_bn_bwd_apply
         # ---- blocks, reversed.  gz = dL/d(BN3(h3) + shortcut), already ReLU-masked (by the GAP backward, or by the
         # next block's conv1 data-gradient epilogue)
@@ -954,7 +963,7 @@ class _ImageNetPlan:
         # ---- stem: max-pool backward (gz is masked by the pooled ReLU output > 0), BN_stem backward, stem wgrad
         sbn = prog.stem_bn
         dz0 = self.tmp("dz0", H1, cfg.num_filters)
-        self._add(L.dtf_cg_maxpool, None, None, _p(self.am0), _p(gz), _p(dz0), N, H1, H1, H2, H2, cfg.num_filters, 1)
+        self.maxpool_bwd(gz, dz0, H1, H2)
         self.bwd_sums(dz0, self.y0, sbn, H1, cfg.num_filters)
         self.bn_final(sbn, H1, True)
         dy0 = self.tmp("dy0", H1, cfg.num_filters)
@@ -969,30 +978,18 @@ class _ImageNetPlan:
         L = ops.lib()
         N, H = self.N, self.H
         ns = len(self.slots)
-        self._add(L.dtf_cg_weight_prep, _p(e.state), e.S, _p(be.conv_table), 1, _p(self.slots_t), ns,
-                  _p(be.w), _p(be.w), be.wtot)
-        self._add(L.dtf_cg_dense_prep, _p(e.state), e.S, prog.dense_w_off, be.ncls, NPAD_CLS, cfg.final_size,
-                  _p(self.slots_t), ns, _p(be.dense), NPAD_CLS * cfg.final_size)
+        self.prep_weights()
         for b in range(len(prog.bns)):
             self.bn_final(b, 1, 2)
-        self._add(L.dtf_cg_prep_input, _p(self.x_in), _p(self.xin8), N * H * H, cfg.in_channels)
+        self.prep_input()
         self._forward_v1(sink=self.ev_sink)
         HL, C = self.HL, cfg.final_size
         g = GapArgs()
         g.x, g.coef, g.img_slot, g.feat = _p(self.xs[-1]), None, _p(self.img_slot), _p(self.feat)
         g.hw, g.C, g.cmax = HL * HL, C, CMAX
         self._hold(g)
-        self._add(L.dtf_cg_gap, ctypes.byref(g), 0, N)
-        from .hip_mnist import GEMM_OUT_F32, GroupedGemm
-        Dstride = NPAD_CLS * C
-        fwd = [(self.first[s] * C, s * Dstride, self.first[s] * NPAD_CLS, n, NPAD_CLS, C)
-               for s, n in zip(self.slots, self.sizes)]
-        self.g_fwd = GroupedGemm(self.feat, be.dense, self.logits, C, C, NPAD_CLS, fwd, False, False, GEMM_OUT_F32,
-                                 be.dev)
-        self._add("gemm", self.g_fwd)
-        self._add(L.dtf_cg_softmax_ce, _p(self.logits), NPAD_CLS, be.ncls, _p(self.labels), _p(self.img_slot),
-                  _p(e.state), e.S, prog.dense_b_off, None, e.Pp, _p(self.cnt), _p(self.ev_loss),
-                  _p(self.ev_acc[0]), None, N, 1.0)
+        self.gap(g, 0)
+        self.dense_head(False)
 
     def load_eval(self, x, y):
         """The same eval images for every member: [m, H, W, C] fp32 -> this plan's [members * m] input."""
@@ -1039,3 +1036,6 @@ class _ImageNetPlan:
 
     def run(self):
         run_captured(self)
+
+
+HipImageNetBackend._plan_cls = _ImageNetPlan

@@ -236,6 +236,7 @@ def _register():
     ops.register("dtf_bn_running_update", [c_void_p, c_long, c_long, c_void_p, c_int, c_void_p, c_long, c_void_p,
                                            c_int, c_void_p, c_void_p, c_long, c_void_p])
     ops.register("dtf_wpitch", [c_int])
+    ops.register("dtf_cpad_fwd", [c_int])
     ops.register("dtf_conv_trans_multi", [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p])
     ops.register("dtf_work_gen", [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p])
     ops.register("dtf_workgen_desc_size", [])
@@ -284,9 +285,17 @@ def _wpitch(c: int) -> int:
     return _WPITCH[c]
 
 
+_CPAD_FWD = {}
+
+
 def _cpad_fwd(c: int) -> int:
-    """conv_fwd_s1 pitch (conv.hip ``cpad_fwd<C>()``)."""
-    return 24 if c == 16 else _cpad(c)
+    """conv_fwd_s1 pitch (conv.hip ``cpad_fwd<C>()``), as compiled into the loaded library."""
+    if c != 16:
+        return _cpad(c)
+    if c not in _CPAD_FWD:
+        _CPAD_FWD[c] = int(ops.lib().dtf_cpad_fwd(c))
+        assert _CPAD_FWD[c] >= c, ("unexpected LDS pitch", c, _CPAD_FWD[c])
+    return _CPAD_FWD[c]
 
 
 def _p(t):

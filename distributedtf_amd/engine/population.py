@@ -281,7 +281,7 @@ def _half_lib_loaded() -> bool:
 
 def _hip_f32_ok(engine) -> bool:
     """fp32 HIP steps: CIFAR-shape building-block ResNets (engine/hip_f32.py), the MNIST CNN
-    (engine/hip_mnist_f32.py)."""
+    (engine/hip_mnist_f32.py), the ImageNet-shape bottleneck ResNets (engine/hip_imagenet_f32.py)."""
     if engine.compute_dtype != torch.float32:
         return False
     from .. import ops
@@ -290,7 +290,8 @@ def _hip_f32_ok(engine) -> bool:
     if getattr(engine.arch, "name", "") == "mnist_cnn":
         return True
     from .hip_f32 import supports
-    return supports(engine.arch)
+    from .hip_imagenet_f32 import supports as supports_bottleneck
+    return supports(engine.arch) or supports_bottleneck(engine.arch)
 
 
 def _hip_f16_ok(engine) -> bool:
@@ -312,7 +313,7 @@ def make_backend(engine: PopulationEngine, name: str):
         name = "hip" if (engine.device.type == "cuda" and getattr(engine.arch, "hip_supported", False)
                          and (ok16 or _hip_f32_ok(engine) or _hip_f16_ok(engine))) else "torch"
     if name == "hip" and not (ok16 or _hip_f32_ok(engine) or _hip_f16_ok(engine)):
-        raise ValueError("no HIP step for compute dtype %s here (bf16: every family; fp32: the CIFAR ResNets and MNIST; fp16: "
+        raise ValueError("no HIP step for compute dtype %s here (bf16 and fp32: every family; fp16: "
                          "the ResNet v2 families under DTF_HALF=1, which --dtype fp16 sets): use the torch backend"
                          % engine.compute_dtype)
     if name == "torch":
@@ -321,6 +322,9 @@ def make_backend(engine: PopulationEngine, name: str):
         if getattr(engine.arch, "name", "") == "mnist_cnn":
             from .hip_mnist_f32 import HipMnistF32Backend
             return HipMnistF32Backend(engine)
+        if getattr(getattr(engine.arch, "cfg", None), "bottleneck", False):
+            from .hip_imagenet_f32 import HipImageNetF32Backend
+            return HipImageNetF32Backend(engine)
         from .hip_f32 import HipResNetF32Backend
         return HipResNetF32Backend(engine)
     if name == "hip":

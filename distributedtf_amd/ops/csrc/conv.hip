@@ -209,16 +209,24 @@ __host__ __device__ constexpr int cpad() {
 // in disjoint bank halves of the ds_read_b128 lane groups (4 instead of 8 cycles per gather, tools/lds_banks.py;
 // the extra 6 columns are never staged).  Measured: no step-time change at pop 1 / pop 8 (these kernels wait on
 // global memory, not LDS; profiles/r2_wp64_ab.log), so the dense pitch (10) stays the default.
+#ifndef DTF_WP64
+#define DTF_WP64 10
+#endif
 template <int C>
 __host__ __device__ constexpr int wpitch() {
-  return 512 / C + 2;
+  return C == 64 ? DTF_WP64 : 512 / C + 2;
 }
 
-// Forward (conv_fwd_s1) pitch: the C = 16 forward measured faster with the +8 pad (1 vs 3 MFMA-operand
-// gathers per row pair, different occupancy) -- the fused backward keeps the unpadded pitch.
+// Forward (conv_fwd_s1) pitch.  C = 16: the unpadded pitch (16) -- the +8 pad of rounds 2-4 cost 3.6 extra bank
+// cycles per ds_read_b128 operand gather (tools/lds_banks.py: 7.6 vs 4.4 cycles, 373 SQ_LDS_BANK_CONFLICT per
+// wave); round 5 A/B: pop 1 1.016 -> 1.011 ms, pop 8 equal (profiles/r5_pitch_ab.log).  C = 64 keeps WP = 10
+// (DTF_WP64): WP = 16 removes its 4-cycle conflict per gather too but costs LDS (occupancy) and measured +0.5 %.
+#ifndef DTF_CPF16
+#define DTF_CPF16 16
+#endif
 template <int C>
 __host__ __device__ constexpr int cpad_fwd() {
-  return C == 16 ? 24 : cpad<C>();
+  return C == 16 ? DTF_CPF16 : cpad<C>();
 }
 
 template <int C>
@@ -2382,6 +2390,7 @@ DTF_API int dtf_conv_trans_multi(const ConvArgs* c, const ConvArgs* a, const Con
 DTF_API int dtf_fused16_wlds() { return DTF_FUSED16_WLDS; }
 DTF_API int dtf_fused16_m3_waves() { return DTF_FUSED16_M3_WAVES; }
 
+DTF_API int dtf_cpad_fwd(int c) { return c == 16 ? cpad_fwd<16>() : c == 32 ? cpad_fwd<32>() : c == 64 ? cpad_fwd<64>() : -1; }
 DTF_API int dtf_wpitch(int c) { return c == 16 ? wpitch<16>() : c == 32 ? wpitch<32>() : c == 64 ? wpitch<64>() : -1; }
 
 DTF_API int dtf_conv_fwd(const ConvArgs* args, int cin, int cout, int s, int k, int mode, int resid, int stats,

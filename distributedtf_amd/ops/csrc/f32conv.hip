@@ -47,7 +47,9 @@ struct F32Args {
   int kh, kw, stride, pad;  // FORWARD conv geometry
   int cmax, log2ci;
   int wci;            // input channels of the weight row (the stem's 3; Ci is its 4-channel padded gather)
-  int pad_;
+  int wrows;          // rows of the weight matrix present (0: all).  A dense layer run as a 1x1 conv with its
+                      // class count padded (1001 -> 1024): forward output channels / data-gradient dy channels /
+                      // weight-gradient rows past it read zero weights and write nothing
 };
 
 constexpr int F_BK = 16;  // k per LDS stage
@@ -236,9 +238,10 @@ __global__ __launch_bounds__(256) void f32conv_kernel(F32Args a) {
       long off;
       const int tap = k >> a.log2ci, ci = k & (Ci - 1);
       if constexpr (DGRAD) {  // ci = dy channel o
+        ok = ok && (a.wrows == 0 || ci < a.wrows);
         off = ((long)ci * kk + tap) * a.Co + o0 + m;
       } else {
-        ok = ok && ci < a.wci;
+        ok = ok && ci < a.wci && (a.wrows == 0 || o0 + m < a.wrows);
         off = ((long)(o0 + m) * kk + tap) * a.wci + ci;
       }
       ra[j] = ok ? wrow[off] : 0.f;
@@ -602,7 +605,8 @@ __global__ __launch_bounds__(256) void f32wgrad_kernel(F32Args a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int o = o0 + 16 * m + 4 * (lane >> 4) + i;
-        if (o < a.Co) dtf_acc_add(g + (long)o * Kw + (long)tapc * a.wci + cic, acc[m][i], DTF_FX_GRAD, slot);
+        if (o < a.Co && (a.wrows == 0 || o < a.wrows))
+          dtf_acc_add(g + (long)o * Kw + (long)tapc * a.wci + cic, acc[m][i], DTF_FX_GRAD, slot);
       }
   }
 }
@@ -855,11 +859,15 @@ __device__ __forceinline__ void kahan_add(float& s, float& c, float v) {
 // One workgroup per image: thread (channel c, part) sums the pixels part, part + P, .. (P = 256 / C parts) with
 // compensated (Kahan) accumulation, then the parts combine in LDS: a long serial fp32 sum over the image's pixels
 // loses ~1e-3 of these cancellation-heavy BN-backward sums.
+// C > 256 (the bottleneck nets): blockIdx.y = group of 256 channels, one part.  pad = 1: forward statistics (sum x,
+// sum x^2 with dz = h and identity coefficients) at the statistics fixed-point scale (a tensor no conv produced).
 __global__ __launch_bounds__(256) void f32_bwd_sums_kernel(F32Sum a) {
   __shared__ float red[3][256];
   const int img = blockIdx.x, slot = a.img_slot[img];
-  const int P = 256 / a.C;
-  const int c = threadIdx.x % a.C, part = threadIdx.x / a.C;
+  const int Cg = a.C < 256 ? a.C : 256;
+  const int P = 256 / Cg;
+  const int c = blockIdx.y * Cg + threadIdx.x % Cg, part = threadIdx.x / Cg;
+  const int cl = threadIdx.x % Cg;  // this thread's channel within the group (LDS column)
   const float* f1 = a.fc + (long)slot * 4 * a.cmax;
   const float mu = f1[2 * a.cmax + c], iv = f1[3 * a.cmax + c];
   float mu2 = 0.f, iv2 = 0.f;
@@ -884,20 +892,25 @@ __global__ __launch_bounds__(256) void f32_bwd_sums_kernel(F32Sum a) {
   __syncthreads();
   for (int w = P / 2; w >= 1; w >>= 1) {  // pairwise over the parts (P is a power of two)
     if (part < w) {
-      red[0][threadIdx.x] += red[0][threadIdx.x + w * a.C];
-      red[1][threadIdx.x] += red[1][threadIdx.x + w * a.C];
-      red[2][threadIdx.x] += red[2][threadIdx.x + w * a.C];
+      red[0][threadIdx.x] += red[0][threadIdx.x + w * Cg];
+      red[1][threadIdx.x] += red[1][threadIdx.x + w * Cg];
+      red[2][threadIdx.x] += red[2][threadIdx.x + w * Cg];
     }
     __syncthreads();
   }
   if (part != 0) return;
   dtf_acc_t* su = a.sums + (long)slot * 2 * a.cmax;
-  dtf_acc_add(su + c, red[0][c], DTF_FX_GRAD, slot);
-  dtf_acc_add(su + a.cmax + c, red[1][c], DTF_FX_GRAD, slot);
+  if (a.pad == 1) {
+    dtf_acc_add(su + c, red[0][cl], DTF_FX_STAT, slot);
+    dtf_acc_add(su + a.cmax + c, red[1][cl], DTF_FX_STAT, slot);
+    return;
+  }
+  dtf_acc_add(su + c, red[0][cl], DTF_FX_GRAD, slot);
+  dtf_acc_add(su + a.cmax + c, red[1][cl], DTF_FX_GRAD, slot);
   if (a.h2) {
     dtf_acc_t* s2 = a.sums2 + (long)slot * 2 * a.cmax;
-    dtf_acc_add(s2 + c, red[0][c], DTF_FX_GRAD, slot);
-    dtf_acc_add(s2 + a.cmax + c, red[2][c], DTF_FX_GRAD, slot);
+    dtf_acc_add(s2 + c, red[0][cl], DTF_FX_GRAD, slot);
+    dtf_acc_add(s2 + a.cmax + c, red[2][cl], DTF_FX_GRAD, slot);
   }
 }
 
@@ -1055,7 +1068,7 @@ DTF_API int dtf_f32_conv(const F32Args* a, int tc, int mode, int epi, int dgrad,
   if (nwork <= 0) return 0;
   if ((a->Ci & (a->Ci - 1)) != 0 || a->Ci < 4 || (a->Co & 3) != 0 || (1 << a->log2ci) != a->Ci) return -2;
   DTF_HOST_CHECK(DTF_ALIGNED16(a->x) && DTF_ALIGNED16(a->y));
-  const size_t dyn = (size_t)(mode == 0 ? 1 : (mode == 1 ? 2 : 3)) * a->Ci * sizeof(float);
+  const size_t dyn = (size_t)(mode == 0 ? 0 : (mode == 1 ? 2 : 3)) * a->Ci * sizeof(float);
 #define F_CASE(TC_, M_, E_, D_)                                                                          \
   if (tc == TC_ && mode == M_ && epi == E_ && dgrad == D_) {                                             \
     hipLaunchKernelGGL((f32conv_kernel<TC_, M_, E_, D_>), dim3(nwork), dim3(256), dyn, stream, *a);      \
@@ -1064,9 +1077,10 @@ DTF_API int dtf_f32_conv(const F32Args* a, int tc, int mode, int epi, int dgrad,
 #define F_TCS(M_, E_, D_) F_CASE(16, M_, E_, D_) F_CASE(32, M_, E_, D_) F_CASE(64, M_, E_, D_)
   // forward: stem / v1 (identity), v2 BN+ReLU prologue; statistics; + residual
   F_TCS(0, 4, false) F_TCS(0, 0, false) F_TCS(1, 4, false) F_TCS(1, 0, false) F_TCS(1, 5, false)
+  F_TCS(0, 5, false)  // bottleneck v2 conv3 (materialised BN+ReLU input) + shortcut (engine/hip_imagenet_f32.py)
   // data gradient: mask + statistics [+ residual], plain, residual + mask (v1)
   F_TCS(0, 6, true) F_TCS(0, 7, true) F_TCS(0, 0, true) F_TCS(2, 3, true) F_TCS(2, 6, true) F_TCS(2, 7, true)
-  F_TCS(2, 0, true)
+  F_TCS(2, 0, true) F_TCS(0, 3, true)
 #undef F_TCS
 #undef F_CASE
   return -1;
@@ -1075,7 +1089,8 @@ DTF_API int dtf_f32_conv(const F32Args* a, int tc, int mode, int epi, int dgrad,
 DTF_API int dtf_f32_wgrad(const F32Args* a, int tc, int mode_x, int mode_dy, int nwork, hipStream_t stream) {
   if (nwork <= 0) return 0;
   if ((a->Ci & (a->Ci - 1)) != 0 || a->Ci < 4 || (a->Co % tc) != 0 || (1 << a->log2ci) != a->Ci) return -2;
-  const size_t dyn = (size_t)(2 * a->Ci + 3 * a->Co) * sizeof(float);
+  // coefficient LDS only for the transforms that run (dy's start at 2 Ci either way)
+  const size_t dyn = (size_t)(mode_dy ? 2 * a->Ci + 3 * a->Co : (mode_x ? 2 * a->Ci : 0)) * sizeof(float);
 #define W_CASE(TC_, MX, MD)                                                                              \
   if (tc == TC_ && mode_x == MX && mode_dy == MD) {                                                      \
     hipLaunchKernelGGL((f32wgrad_kernel<TC_, MX, MD>), dim3(nwork), dim3(256), dyn, stream, *a);         \
@@ -1153,8 +1168,8 @@ DTF_API int dtf_f32_ew(const F32Ew* a, int which, hipStream_t stream) {
 
 DTF_API int dtf_f32_bwd_sums(const F32Sum* a, int nimg, hipStream_t stream) {
   if (nimg <= 0) return 0;
-  if (a->C > 256 || 256 % a->C) return -2;
-  hipLaunchKernelGGL(f32_bwd_sums_kernel, dim3(nimg), dim3(256), 0, stream, *a);
+  if (a->C > 256 ? (a->C % 256) != 0 : (256 % a->C) != 0) return -2;
+  hipLaunchKernelGGL(f32_bwd_sums_kernel, dim3(nimg, a->C > 256 ? a->C / 256 : 1), dim3(256), 0, stream, *a);
   return DTF_CHECK_LAUNCH();
 }
 

@@ -227,9 +227,8 @@ def hip_deterministic(args) -> bool:
     MNIST (one workgroup per member for every accumulation) and the ImageNet bottleneck nets (every cross-workgroup
     sum as int64 fixed point with integer atomics, common.h DTF_FIXED_ACC)."""
     dt = getattr(args, "dtype", "bf16")
-    # fp32: the CIFAR ResNets' fp32 step accumulates in int64 fixed point in the deterministic build too
-    return args.model in ("mnist", "cifar10", "imagenet") and (dt == "bf16" or (dt == "fp32" and args.model in
-                                                                                  ("cifar10", "mnist")))
+    # fp32: the fp32 steps accumulate every cross-workgroup sum in int64 fixed point in the deterministic build too
+    return args.model in ("mnist", "cifar10", "imagenet") and dt in ("bf16", "fp32")
 
 
 def parse_main_args(argv=None, defaults=None) -> MainArgs:
@@ -239,8 +238,8 @@ def parse_main_args(argv=None, defaults=None) -> MainArgs:
         args.population_size = args.pop_size
     if args.resnet_version == 1 and args.dtype == "fp16":
         p.error("ResNet version 1 is not currently supported with fp16. Please use version 2 instead.")
-    if args.dtype == "fp32" and args.model in ("cifar10", "mnist"):
-        # fp32 CIFAR ResNets and the MNIST CNN run the fp32 HIP steps (engine/hip_f32.py, engine/hip_mnist_f32.py:
+    if args.dtype == "fp32" and args.model in ("cifar10", "mnist", "imagenet"):
+        # every family has an fp32 HIP step (engine/hip_f32.py, hip_mnist_f32.py, hip_imagenet_f32.py:
         # v_mfma_f32_16x16x4_f32, fp32 tensors); a static loss scale is a PyTorch-path feature
         if args.loss_scale is not None and args.loss_scale != 1:
             if args.backend == "hip":
@@ -255,11 +254,11 @@ def parse_main_args(argv=None, defaults=None) -> MainArgs:
                     "deterministic or debug variant; use --backend torch")
         # (apply_runtime_modes sets DTF_HALF=1: ops.lib() then loads libdtf_kernels_f16.so)
     elif args.dtype != "bf16" and args.model != "toy":
-        # the other families' kernels compute in bf16 (fp32 master weights / statistics); their fp32 and fp16
-        # (static loss scaling) run on the PyTorch backend
+        # fp16 of the families without a half-build step (MNIST; ResNet v1 is rejected above) runs on the PyTorch
+        # backend with static loss scaling
         if args.backend == "hip":
-            p.error("--dtype %s: the %s HIP kernels compute in bf16; use --backend torch (or auto)"
-                    % (args.dtype, args.model))
+            p.error("--dtype %s: the %s HIP kernels have no %s build; use --backend torch (or auto)"
+                    % (args.dtype, args.model, args.dtype))
         args.backend = "torch"
     elif args.loss_scale is not None and args.loss_scale != 1 and args.backend != "torch" and args.model != "toy":
         p.error("--loss_scale applies to the fp16 / fp32 PyTorch path; bf16 needs no loss scaling "

@@ -84,8 +84,10 @@ def test_dtype_routing():
     assert parse_main_args(["--model", "cifar10", "--dtype", "fp32", "--loss_scale", "8"]).backend == "torch"
     with pytest.raises(SystemExit):
         parse_main_args(["--model", "cifar10", "--dtype", "fp32", "--loss_scale", "8", "--backend", "hip"])
+    # ImageNet fp32 too (engine/hip_imagenet_f32.py); MNIST fp16 has no half build -> torch
+    assert parse_main_args(["--model", "imagenet", "--dtype", "fp32", "--backend", "hip"]).backend == "hip"
     with pytest.raises(SystemExit):
-        parse_main_args(["--model", "imagenet", "--dtype", "fp32", "--backend", "hip"])
+        parse_main_args(["--model", "mnist", "--dtype", "fp16", "--backend", "hip"])
     # MNIST fp32 stays on HIP (engine/hip_mnist_f32.py: the generic fp32 MFMA conv kernels)
     assert parse_main_args(["--model", "mnist", "--dtype", "fp32"]).backend == "auto"
     assert parse_main_args(["--model", "mnist", "--dtype", "fp32", "--backend", "hip"]).backend == "hip"
@@ -137,8 +139,10 @@ def test_deterministic_flag_selects_det_build(monkeypatch):
                                 "--backend", "hip"]).backend == "hip"
         assert parse_main_args(["--model", "mnist", "--dtype", "fp32", "--deterministic",
                                 "--backend", "hip"]).backend == "hip"
+        assert parse_main_args(["--model", "imagenet", "--dtype", "fp32", "--deterministic",
+                                "--backend", "hip"]).backend == "hip"
         with pytest.raises(SystemExit):  # an explicit --backend hip must not silently lose the guarantee
-            parse_main_args(["--model", "imagenet", "--dtype", "fp32", "--deterministic", "--backend", "hip"])
+            parse_main_args(["--model", "mnist", "--dtype", "fp16", "--deterministic", "--backend", "hip"])
         with pytest.raises(SystemExit):  # the debug kernel build is not the deterministic one
             parse_main_args(["--model", "cifar10", "--deterministic", "--debug_kernels"])
         assert kb.LIB_DET.endswith("libdtf_kernels_det.so") and "-DDTF_NREP=64" in kb.DET_FLAGS

@@ -82,6 +82,8 @@ ok = all([run(20, [16, 24], 4), run(56, [128], 3), run(56, [128] * 4, 2), run(20
           run(50, [4, 6], 3, image=64), run(50, [8, 8], 2, version=1, image=64),
           # the fp32 CIFAR step (f32conv.hip: int64 fixed-point accumulation in this build)
           run(20, [16, 24], 4, dtype=torch.float32), run(20, [16, 24], 3, version=1, dtype=torch.float32),
-          run_mnist([40, 72], 4, dtype=torch.float32)])
+          run_mnist([40, 72], 4, dtype=torch.float32),
+          # the fp32 ImageNet step (hip_imagenet_f32.py, f32conv.hip + f32net.hip)
+          run(50, [4, 6], 2, image=64, dtype=torch.float32), run(50, [4, 4], 2, version=1, image=64, dtype=torch.float32)])
 print("DET_OK" if ok else "DET_FAIL")
 sys.exit(0 if ok else 1)

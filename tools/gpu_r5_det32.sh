@@ -9,3 +9,4 @@ DTF_DETERMINISTIC=1 timeout -k 10 600 python -u tools/det_check.py > gpurun_out/
 rc=$?; grep -v Warning gpurun_out/r5d32/det_check.log | tail -15; [ $rc -ne 0 ] && exit 1
 DTF_HALF=1 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_fp16.py > gpurun_out/r5d32/half.log 2>&1
 rc=$?; echo "half build: $(tail -1 gpurun_out/r5d32/half.log)"; [ $rc -ne 0 ] && { tail -30 gpurun_out/r5d32/half.log; exit 1; }
+exit 0

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-4 checkpoint: smoke(), every model family's bench (bf16 HIP, fp32 HIP, deterministic builds) -> gpurun_out/fam
+# round checkpoint: smoke(), every model family's bench (bf16 / fp32 / fp16 HIP, deterministic builds) -> gpurun_out/fam
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/fam
@@ -30,6 +30,11 @@ run "" --model imagenet --pop 1 --steps 10 --warmup 3
 run "" --model imagenet --resnet_version 1 --steps 10 --warmup 3
 run "" --dtype fp32 --steps 20 --warmup 3
 run "" --dtype fp32 --resnet_version 1 --steps 20 --warmup 3
+run "" --model mnist --dtype fp32 --steps 100 --warmup 10
+run "" --dtype fp16 --steps 100 --warmup 10
+run "" --model imagenet --dtype fp16 --steps 10 --warmup 3
 run "DTF_DETERMINISTIC=1" --steps 50 --warmup 5
+run "DTF_DETERMINISTIC=1" --dtype fp32 --steps 20 --warmup 3
 run "DTF_DETERMINISTIC=1" --model imagenet --steps 10 --warmup 3
+run "" --model imagenet --dtype fp32 --steps 4 --warmup 1
 echo FAMILIES_OK

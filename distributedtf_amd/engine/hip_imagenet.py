@@ -46,6 +46,14 @@ _CG_TP256 = True  # 256-pixel forward / dgrad tiles for 64-channel outputs
 # v_mfma_f32_32x32x16_bf16 tiles for the plain-A forward convolutions with 128-channel tiles (1x1 / strided / 7x7-stage
 # convs with C_out >= 128): 32 x 32 MFMA tiles of each wave's 64 x 128 block (convg_fwd_kernel M32)
 _CG_M32 = os.environ.get("DTF_CG_M32", "0") == "1"
+# space-to-depth stem: the 7x7/2 conv over the 3-channel image as a 4x4/1 conv over 2x2 pixel blocks (12 of 16
+# channels real): K = 256 instead of 7 x 7 x 8 = 392 padded, stride 1, half the input bytes (cg_prep_input_s2d,
+# cg_weight_prep s2d rows, convg_wgrad_wide cin_real = -3 remaps the weight gradient onto the 7x7x3 kernel)
+_CG_S2D = os.environ.get("DTF_CG_S2D", "1") == "1"
+# stride-1 3x3 weight gradients from LDS-resident row bands (convg_wgrad_t3_kernel): image width -> rows per band;
+# items per launch (each adds one 64 x 288 fp32 tile into the gradient row)
+_CG_WGT3 = {56: 4, 28: 7, 14: 14} if os.environ.get("DTF_CG_WGT3", "1") == "1" else {}
+_CG_WGT3_TARGET = int(os.environ.get("DTF_CG_WGT3_TARGET", "512"))
 _CG_WPK_WO64 = 32  # pixels per k-step of the 64-row tiles
 # stride-1 3x3 forward / data gradient with LDS-resident input rows (convg_t3_kernel): image width -> rows per tile
 _CG_T3 = {56: 8, 28: 7, 14: 14}  # must match dtf_convg_t3 (rows divide the image height)
@@ -116,6 +124,7 @@ def _register():
     reg("dtf_convg_t3", [P(CgArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
     reg("dtf_convg_wgrad", [P(CgArgs), c_int, c_int, c_int, c_void_p])
     reg("dtf_convg_wgrad_wide", [P(CgArgs), c_int, c_int, c_int, c_int, c_void_p])
+    reg("dtf_convg_wgrad_t3", [P(CgArgs), c_int, c_int, c_int, c_void_p])
     reg("dtf_cg_weight_prep", [c_void_p, c_long, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_long,
                                c_void_p])
     reg("dtf_cg_dense_prep", [c_void_p, c_long, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_long,
@@ -124,6 +133,7 @@ def _register():
     reg("dtf_cg_bn_bwd_apply", [P(EwArgs), c_void_p])
     reg("dtf_cg_bn_relu_apply", [P(EwArgs), c_void_p])
     reg("dtf_cg_prep_input", [c_void_p, c_void_p, c_long, c_int, c_void_p])
+    reg("dtf_cg_prep_input_s2d", [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p])
     reg("dtf_cg_maxpool", [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                            c_int, c_int, c_void_p])
     reg("dtf_cg_gap", [P(GapArgs), c_int, c_int, c_void_p])
@@ -184,10 +194,15 @@ class HipImageNetBackend:
             assert c.off % 8 == 0, "conv weights must be 16-byte aligned in the shadow row"
         self.shadow = torch.zeros(cap, engine.Pp, dtype=ops.act_dtype(), device=self.dev)
         st = prog.convs[prog.stem]
-        self.wtot = (st.cout * st.k * st.k * 8 + 63) // 64 * 64
-        self.w = torch.zeros(cap, self.wtot, dtype=ops.act_dtype(), device=self.dev)  # padded stem
-        self.conv_table = torch.tensor([[st.off, st.cout, st.cin, st.k, 8, 0, -1, 0]], dtype=torch.int32,
-                                       device=self.dev)
+        self.s2d = (_CG_S2D and st.cin == 3 and st.k == 7 and st.stride == 2 and cfg.image_size % 4 == 0)
+        if self.s2d:
+            self.wtot = (st.cout * 16 * 16 + 63) // 64 * 64
+            row = [st.off, st.cout, st.cin, st.k, 16, 0, -1, 1]
+        else:
+            self.wtot = (st.cout * st.k * st.k * 8 + 63) // 64 * 64
+            row = [st.off, st.cout, st.cin, st.k, 8, 0, -1, 0]
+        self.w = torch.zeros(cap, self.wtot, dtype=ops.act_dtype(), device=self.dev)  # padded / s2d stem
+        self.conv_table = torch.tensor([row], dtype=torch.int32, device=self.dev)
         self.ncls = cfg.num_classes
         assert self.ncls <= NPAD_CLS and cfg.final_size % 32 == 0
         self.dense = torch.zeros(cap, NPAD_CLS * cfg.final_size, dtype=ops.act_dtype(), device=self.dev)
@@ -330,7 +345,7 @@ class _ImageNetPlan:
         self.H = H
         self.x_in = torch.zeros(N, H, H, cfg.in_channels, dtype=torch.float32, device=dev)
         self.labels = torch.zeros(N, dtype=torch.int32, device=dev)
-        self.xin8 = torch.zeros(N, H, H, self._stem_cin(), dtype=bf, device=dev)  # channel-padded stem input
+        self.xin8 = torch.zeros(*self._stem_input_shape(N, H), dtype=bf, device=dev)  # stem input (padded / s2d)
         H1 = H // 2
         H2 = (H1 + 1) // 2
         pool = {}
@@ -398,8 +413,10 @@ class _ImageNetPlan:
     def _act_dtype(self):
         return ops.act_dtype()  # bf16 (fp16 in the half build)
 
-    def _stem_cin(self):
-        return 8  # the stem gathers 8-channel chunks of the 3-channel input
+    def _stem_input_shape(self, N, H):
+        """Space-to-depth [N, H/2, H/2, 16] (12 real channels), else the 3 channels padded to the stem's 8-channel
+        gather chunks."""
+        return (N, H // 2, H // 2, 16) if self.be.s2d else (N, H, H, 8)
 
     def tmp(self, name, hw, c):
         key = (name, hw, c)
@@ -513,6 +530,10 @@ class _ImageNetPlan:
             a.Ho = a.Wo = hw_out
             a.stride, a.pad = c.stride, k - 1 - pad
             trans = (1 if c.stride > 1 else 0) | 2  # | 2: A operand k-major from the forward layout
+        if ci == be.prog.stem and be.s2d:
+            assert not dgrad
+            a.Hi = a.Wi = a.Ho = a.Wo = hw_in // 2  # 4x4/1 over 2x2 blocks (pad 2 before, 1 after)
+            a.Ci, a.kh, a.kw, a.stride, a.pad = 16, 4, 4, 1, 2
         a.log2ci = _log2(a.Ci)
         tc = 128 if a.Co >= 128 else 64
         if (k == 3 and c.stride == 1 and (mode == 0 or (mode == 1 and not dgrad)) and hw_in in _CG_T3
@@ -557,14 +578,25 @@ class _ImageNetPlan:
         a.log2ci = _log2(cin)
         a.cin_real = c.cin
         K = c.k * c.k * cin
+        s2d = ci == be.prog.stem and be.s2d
+        if s2d:  # 4x4/1 over the 2x2-block input; the writer maps (tap', block channel) onto the 7x7x3 kernel
+            a.Hi = a.Wi = a.Ho = a.Wo = hw_out
+            a.Ci, a.kh, a.kw, a.stride, a.pad = 16, 4, 4, 1, 2
+            a.log2ci, a.cin_real = 4, -3
+            K = 256
+        if (c.k == 3 and c.stride == 1 and not s2d and hw_in in _CG_WGT3 and mode_x == 0 and mode_dy == 0
+                and cin % 32 == 0 and c.cout % 8 == 0):
+            self._wgrad_t3(a, hw_in, cin, c.cout)
+            return
         wide3 = c.k == 3 and cin % 64 == 0
         wide1 = c.k == 1 and cin % 256 == 0 and _CG_WIDE1
-        wide7 = ci == be.prog.stem and c.k == 7 and cin == 8 and c.cout == 64 and _CG_WIDE7
-        if _CG_WIDE and (wide3 or wide1 or wide7) and mode_x in (0, 1) and mode_dy == 0 and not (wide7 and mode_x):
-            # 64 / 128 x 288 (3x3), x 256 (1x1) or 64 x 416 (stem) tiles: 18 / 36, 16 / 32, 26 MFMAs per wave and
-            # 32-pixel k-step (convg_wgrad_wide_kernel)
+        wide7 = ci == be.prog.stem and c.k == 7 and cin == 8 and c.cout == 64 and _CG_WIDE7 and not s2d
+        if (_CG_WIDE and (wide3 or wide1 or wide7 or s2d) and mode_x in (0, 1) and mode_dy == 0
+                and not ((wide7 or s2d) and mode_x)):
+            # 64 / 128 x 288 (3x3), x 256 (1x1, and the 4x4 x 16 s2d stem) or 64 x 416 (7x7 stem) tiles: 18 / 36,
+            # 16 / 32, 26 MFMAs per wave and 32-pixel k-step (convg_wgrad_wide_kernel)
             wo = 128 if c.cout % 128 == 0 and _CG_WIDE128 else 64
-            wt = 288 if wide3 else (256 if wide1 else 416)
+            wt = 288 if wide3 else (256 if (wide1 or s2d) else 416)
             work = self._wgrad_work(hw_out, c.cout, K, wo, wt)
             a.work = _p(work)
             self._hold(a)
@@ -576,6 +608,25 @@ class _ImageNetPlan:
         self._hold(a)
         flags = (4 if (_CG_WPK_WO64 if wo == 64 else _CG_WPK) == 64 else 0) | (8 if wo == 64 else 0)
         self._add(ops.lib().dtf_convg_wgrad, ctypes.byref(a), mode_x, mode_dy | flags, work.shape[0])
+
+    def _wgrad_t3(self, a, hw, cin, cout):
+        """Row-band 3x3 weight gradient: items (slot, first band, end band, o0 | ci chunk << 16) -- per member, per
+        64-row output tile and 32-channel input chunk, the member's bands split into about _CG_WGT3_TARGET items."""
+        R = _CG_WGT3[hw]
+        bpi = hw // R
+        tiles = [(o0, cc) for o0 in range(0, cout, 64) for cc in range(cin // 32)]
+        total = sum(self.sizes) * bpi * len(tiles)
+        chunk = max(1, -(-total // _CG_WGT3_TARGET))
+        items = []
+        for s, n in zip(self.slots, self.sizes):
+            f = self.first[s]
+            for b in range(f * bpi, (f + n) * bpi, chunk):
+                for (o0, cc) in tiles:
+                    items.append([s, b, min(b + chunk, (f + n) * bpi), o0 | (cc << 16)])
+        work = self._hold(torch.tensor(items, dtype=torch.int32, device=self.be.dev))
+        a.work = _p(work)
+        self._hold(a)
+        self._add(ops.lib().dtf_convg_wgrad_t3, ctypes.byref(a), hw, R, work.shape[0])
 
     def bn_final(self, bn, hw, backward):
         be, e = self.be, self.e
@@ -621,6 +672,10 @@ class _ImageNetPlan:
                   _p(self.slots_t), ns, _p(be.dense), NPAD_CLS * cfg.final_size)
 
     def prep_input(self):
+        if self.be.s2d:
+            self._add(ops.lib().dtf_cg_prep_input_s2d, _p(self.x_in), _p(self.xin8), self.N, self.H, self.H,
+                      self.be.cfg.in_channels)
+            return
         self._add(ops.lib().dtf_cg_prep_input, _p(self.x_in), _p(self.xin8), self.N * self.H * self.H,
                   self.be.cfg.in_channels)
 

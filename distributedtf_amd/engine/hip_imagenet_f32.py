@@ -99,6 +99,7 @@ class HipImageNetF32Backend(HipImageNetBackend):
         self.acc_grads = self.gacc if self.det else engine.grads
         self.acc_loss = self.loss64 if self.det else self.loss
         self.v1 = self.cfg.version == 1
+        self.s2d = False  # the fp32 stem runs the 7x7/2 gather on the 4-channel padded input
         # identity coefficients (scale 1, shift 0, mean 0, inv 1): the v1 ReLU mask by the block input, and the
         # forward statistics of the pooled stem output through f32_bwd_sums (dz = h = x)
         self.ident = torch.zeros(cap, 4, CMAX, dtype=torch.float32, device=self.dev)
@@ -118,8 +119,8 @@ class _ImageNetF32Plan(_ImageNetPlan):
     def _act_dtype(self):
         return torch.float32
 
-    def _stem_cin(self):
-        return 4  # f32conv gathers 4-channel chunks: the 3-channel input padded to 4
+    def _stem_input_shape(self, N, H):
+        return (N, H, H, 4)  # f32conv gathers 4-channel chunks: the 3-channel input padded to 4
 
     # ---------------------------------------------------------------------------------------- convolutions
     def _f32args(self, w_off, Hi, Ci, wci, Ho, Co, k, stride, pad):

@@ -1223,14 +1223,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ?
     __syncthreads();
   }
   dtf_acc_t* gr = a.grads + (long)slot * a.g_mstride + a.g_off;
-  const int cr = a.cin_real > 0 ? a.cin_real : Ci;  // real input channels of a channel-padded operand (stem)
-  const int Kr = a.kh * a.kw * cr;
+  // real input channels of a channel-padded operand (stem); cin_real = -3: the space-to-depth stem (4x4 taps over
+  // 2x2 blocks of a 3-channel image): column (tap', (2 dy + dx) * 3 + c) is weight (2a + dy - 1, 2b + dx - 1, c) of
+  // the 7x7 kernel (cg_weight_prep s2d); each 7x7x3 weight is reached from exactly one column
+  const bool s2d = a.cin_real == -3;
+  const int cr = a.cin_real > 0 ? a.cin_real : (s2d ? 3 : Ci);
+  const int Kr = s2d ? 49 * 3 : a.kh * a.kw * cr;
 #pragma unroll
   for (int n = 0; n < NTN; ++n) {
     const int col0 = n0 + wc * (WWT / 2) + 16 * n + (lane & 15);
     const int ci_ = col0 & (Ci - 1);
-    if (col0 >= K || ci_ >= cr) continue;
-    const int col = (col0 >> a.log2ci) * cr + ci_;
+    int col;
+    if (s2d) {
+      const int tap = col0 >> a.log2ci, q = ci_ / 3, c = ci_ - 3 * q;
+      const int ky = 2 * (tap >> 2) + (q >> 1) - 1, kx = 2 * (tap & 3) + (q & 1) - 1;
+      if (col0 >= K || q >= 4 || ky < 0 || ky > 6 || kx < 0 || kx > 6) continue;
+      col = (ky * 7 + kx) * 3 + c;
+    } else {
+      if (col0 >= K || ci_ >= cr) continue;
+      col = (col0 >> a.log2ci) * cr + ci_;
+    }
 #pragma unroll
     for (int m = 0; m < MTW; ++m) {
 #pragma unroll
@@ -1239,6 +1251,142 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ?
         if (o < Co) dtf_acc_add(gr + (long)o * Kr + col, acc[m][n][r], DTF_FX_GRAD, slot);
       }
     }
+  }
+}
+
+// ----------------------------------------------------------------------------------------- row-band wgrad
+// Weight gradient of a stride-1 3x3 conv (plain operands) from LDS-resident row bands.  The wide kernel above
+// gathers its x operand per 32-pixel k-step as 288 (tap, ci) columns -- every input element is fetched once per tap
+// (9x) plus per-column addressing VALU, and with a 64-row tile (Co = 64) that traffic feeds only 18 MFMAs per wave
+// (311 B per MFMA; the stage-1 3x3 weight gradients ran at 4.6x their MFMA floor).  Here a workgroup stages ONE
+// band of R image rows: dy [R*W pixels][64 co] and the input halo [(R+2)][(W+2)][32 ci], and all 9 taps read their
+// B fragments from the halo at a constant offset (ds_read_b64_tr_b16 along the pixels), so x is fetched ~1.5x
+// (halo) instead of 9x.  Tile: 64 co x (9 taps x 32 ci) = 288 columns, 2 x 2 waves of 32 x 144 (18 MFMAs per wave
+// and k-step); the next band is prefetched into registers while the current one runs.
+// work: (slot, first band, end band, o0 | ci-chunk << 16); band b = image b / (H / R), rows (b % (H / R)) * R ..
+// Pixels past R * W in the last k-step (W = 28: 196 of 224) stage zero dY rows and contribute nothing.
+template <int W, int R>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void convg_wgrad_t3_kernel(CgArgs a) {
+  constexpr int WO = 64, BKC = 32;
+  constexpr int NPV = R * W, NKS = (NPV + 31) / 32, NPX = NKS * 32;
+  constexpr int WOP = WO + 8;            // dY tile pitch (bf16)
+  constexpr int CP = BKC + 8;            // halo pixel pitch (bf16)
+  constexpr int WS = W + 2, RT = R + 2;  // halo columns / rows
+  constexpr int MTW = WO / 32, NTW = 9;  // A tiles per wave (32 rows), B column tiles per wave (of 18)
+  constexpr int DCH = NPX * WO / 8, DJ = (DCH + 255) / 256;
+  constexpr int XCH = RT * WS * (BKC / 8), XJ = (XCH + 255) / 256;
+  __shared__ __attribute__((aligned(16))) bf16_t sd[NPX * WOP];
+  __shared__ __attribute__((aligned(16))) bf16_t sx[RT * WS * CP + 8];
+  const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z > wk.y && a.Wi == W && a.Wo == W && a.Ho == a.Hi && a.Hi % R == 0);
+  const int slot = wk.x, b0 = wk.y, b1 = wk.z, o0 = wk.w & 0xffff, cc = wk.w >> 16;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave & 1, wc = wave >> 1;
+  const int Ci = a.Ci, Co = a.Co, H = a.Hi, BPI = H / R;
+  // dY slots: chunk q = tid + 256 j -> band pixel q / 8, channels 8 (q % 8)
+  int dpx[DJ], dch[DJ];
+  unsigned dok = 0;
+#pragma unroll
+  for (int j = 0; j < DJ; ++j) {
+    const int q = tid + 256 * j;
+    dpx[j] = q / (WO / 8);
+    dch[j] = 8 * (q % (WO / 8));
+    dok |= (unsigned)(q < DCH && dpx[j] < NPV && o0 + dch[j] < Co) << j;
+  }
+  // halo slots: chunk q = tid + 256 j -> halo pixel (hr, hc), 8-channel piece c8
+  int xhr[XJ], xhc[XJ], xc8[XJ];
+#pragma unroll
+  for (int j = 0; j < XJ; ++j) {
+    const int q = tid + 256 * j, hp = q / (BKC / 8);
+    xc8[j] = q < XCH ? 8 * (q % (BKC / 8)) : 0;
+    xhr[j] = q < XCH ? hp / WS : RT;  // RT: inactive slot (never valid, stores into the slack)
+    xhc[j] = hp % WS;
+  }
+  uint4 dv[DJ], xv[XJ];
+  unsigned xok = 0;
+  auto load = [&](int band) {
+    const int img = band / BPI, y0 = (band - img * BPI) * R;
+    const long dbase = ((long)img * H + y0) * W * Co + o0;
+#pragma unroll
+    for (int j = 0; j < DJ; ++j) dv[j] = ld16(a.dy, dbase + (long)dpx[j] * Co + dch[j], (dok >> j) & 1u);
+    xok = 0;
+    const long xbase = (long)img * H * W * Ci + cc * BKC;
+#pragma unroll
+    for (int j = 0; j < XJ; ++j) {
+      const int gy = y0 - 1 + xhr[j], gx = xhc[j] - 1;
+      const bool ok = xhr[j] < RT && gy >= 0 && gy < H && gx >= 0 && gx < W;
+      xv[j] = ld16(a.x, xbase + ((long)gy * W + gx) * Ci + xc8[j], ok);
+      xok |= (unsigned)ok << j;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int j = 0; j < DJ; ++j) {
+      const int q = tid + 256 * j;
+      if (q < DCH) *reinterpret_cast<uint4*>(sd + dpx[j] * WOP + dch[j]) = (dok >> j) & 1u ? dv[j] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < XJ; ++j) {
+      const int off = xhr[j] < RT ? (xhr[j] * WS + xhc[j]) * CP + xc8[j] : RT * WS * CP;
+      *reinterpret_cast<uint4*>(sx + off) = (xok >> j) & 1u ? xv[j] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  // fragment lanes: g = lane / 16 (8 k-rows), q = k-row within the quad, p4 = 4-column piece
+  const int g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
+  f32x4_t acc[MTW][NTW];
+#pragma unroll
+  for (int m = 0; m < MTW; ++m)
+#pragma unroll
+    for (int n = 0; n < NTW; ++n) acc[m][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  load(b0);
+  store();
+  __syncthreads();
+  for (int b = b0; b < b1; ++b) {
+    const bool more = b + 1 < b1;
+    if (more) load(b + 1);
+#pragma unroll 1
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int pa = ks * 32 + 8 * g + q, pb = pa + 4;  // this lane's two k-rows (band pixels)
+      bf16x8_t fa[MTW];
+#pragma unroll
+      for (int m = 0; m < MTW; ++m) {
+        const int cb = wr * (WO / 2) + 16 * m + 4 * p4;
+        const s16x4_t lo = ds_read_tr(sd + pa * WOP + cb);
+        const s16x4_t hi = ds_read_tr(sd + pb * WOP + cb);
+        fa[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      const int qa = pa < NPV ? pa : 0, qb = pb < NPV ? pb : 0;  // padding pixels (zero dY) read pixel 0
+      const int ha = ((qa / W) * WS + qa % W) * CP + 4 * p4, hb = ((qb / W) * WS + qb % W) * CP + 4 * p4;
+#pragma unroll
+      for (int n = 0; n < NTW; ++n) {
+        const int j = NTW * wc + n, t = j >> 1;  // column tile j = (tap t, 16-channel half j & 1)
+        const int toff = ((t / 3) * WS + t % 3) * CP + 16 * (j & 1);
+        const s16x4_t lo = ds_read_tr(sx + ha + toff);
+        const s16x4_t hi = ds_read_tr(sx + hb + toff);
+        const bf16x8_t fb = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int m = 0; m < MTW; ++m) acc[m][n] = mfma16(fa[m], fb, acc[m][n]);
+      }
+    }
+    __syncthreads();
+    if (more) {
+      store();
+      __syncthreads();
+    }
+  }
+  // D: lane holds column (lane & 15) of tile (tap, half), rows 4 (lane >> 4) + r
+  dtf_acc_t* gr = a.grads + (long)slot * a.g_mstride + a.g_off;
+#pragma unroll
+  for (int n = 0; n < NTW; ++n) {
+    const int j = NTW * wc + n, t = j >> 1;
+    const int ci = cc * BKC + 16 * (j & 1) + (lane & 15);
+#pragma unroll
+    for (int m = 0; m < MTW; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = o0 + wr * (WO / 2) + 16 * m + 4 * (lane >> 4) + r;
+        if (o < Co) dtf_acc_add(gr + ((long)o * 9 + t) * Ci + ci, acc[m][n][r], DTF_FX_GRAD, slot);
+      }
   }
 }
 
@@ -1368,7 +1516,7 @@ DTF_API int dtf_convg_wgrad_wide(const CgArgs* a, int wo, int wt, int nwork, int
   if (nwork <= 0) return 0;
   const int K = a->kh * a->kw * a->Ci;
   if ((a->Ci & (a->Ci - 1)) != 0 || a->Ci < 8 || (a->Co & 7) != 0) return -2;
-  if (wt != 416 && (a->Ci < 64 || K % wt != 0)) return -2;
+  if (wt != 416 && ((a->Ci < 64 && a->cin_real != -3) || K % wt != 0)) return -2;  // -3: the s2d stem (16 ch)
   if (mode_x != 0 && (mode_x != 1 || wt == 416 || a->Ci > 4096)) return -2;
   const size_t dyn = mode_x ? (size_t)2 * a->Ci * sizeof(float) : 0;
 #define WW_CASE(WO_, WT_)                                                                                     \
@@ -1386,6 +1534,18 @@ DTF_API int dtf_convg_wgrad_wide(const CgArgs* a, int wo, int wt, int nwork, int
     return DTF_CHECK_LAUNCH();
   }
   return -2;
+}
+
+// stride-1 3x3 weight gradient from row bands (convg_wgrad_t3_kernel): W = image width, R = rows per band
+DTF_API int dtf_convg_wgrad_t3(const CgArgs* a, int W, int R, int nwork, hipStream_t stream) {
+  if (nwork <= 0) return 0;
+  if (a->kh != 3 || a->kw != 3 || a->stride != 1 || a->pad != 1 || a->Ci % 32 || a->Co % 8 || a->Wi != W ||
+      a->Hi % R)
+    return -2;
+#define WT3_CASE(W_, R_)                                                                                      if (W == W_ && R == R_) {                                                                                     hipLaunchKernelGGL((convg_wgrad_t3_kernel<W_, R_>), dim3(nwork), dim3(256), 0, stream, *a);                 return DTF_CHECK_LAUNCH();                                                                                }
+  WT3_CASE(56, 4) WT3_CASE(28, 7) WT3_CASE(14, 14)
+#undef WT3_CASE
+  return -1;
 }
 
 DTF_DEBUG_EXPORT(convg)

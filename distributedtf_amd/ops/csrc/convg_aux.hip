@@ -33,6 +33,20 @@ __global__ __launch_bounds__(256) void cg_weight_prep_kernel(const float* __rest
   const float* p = state + (long)slot * s_mstride + w_off;
   bf16_t* f = wf + (long)slot * w_mstride + fwd_off;
   const int t0 = blockIdx.y * blockDim.x + threadIdx.x, ts = gridDim.y * blockDim.x;
+  if (t[7] == 1) {
+    // space-to-depth stem: the 7x7/2 kernel W[co][ky][kx][c] (c < cin = 3) as a 4x4/1 kernel over 2x2 pixel blocks,
+    // W'[co][a][b][(2 dy + dx) * cin + c] = W[co][2a + dy - 1][2b + dx - 1][c] (zero outside 0..6 and for the pad
+    // channels): input row 2 oy + ky - 3 = 2 (oy + a - 2) + dy
+    const int nf = cout * 16 * cin_pad;
+    for (int i = t0; i < nf; i += ts) {
+      const int ci = i % cin_pad, rest = i / cin_pad, tap = rest % 16, co = rest / 16;
+      const int q = ci / cin, c = ci - q * cin;
+      const int ky = 2 * (tap >> 2) + (q >> 1) - 1, kx = 2 * (tap & 3) + (q & 1) - 1;
+      const bool ok = q < 4 && ky >= 0 && ky < k && kx >= 0 && kx < k;
+      f[i] = ok ? f2bf(p[((co * k + ky) * k + kx) * cin + c]) : (bf16_t)0;
+    }
+    return;
+  }
   const int nf = cout * kk * cin_pad;
   if (cin_pad == cin && (nf & 3) == 0) {
     for (int i = 4 * t0; i < nf; i += 4 * ts) {
@@ -284,6 +298,28 @@ __global__ __launch_bounds__(256) void cg_prep_input_kernel(const float* __restr
     for (int c = 0; c < c_in; ++c) v[c] = x[p * c_in + c];
     *reinterpret_cast<uint4*>(y + p * 8) =
         make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+  }
+}
+
+// space-to-depth stem input: x [N][H][W][c_in] fp32 -> y [N][H/2][W/2][16] with channel (2 dy + dx) * c_in + c =
+// x[2 by + dy][2 bx + dx][c] (channels 4 c_in .. 15 zero); thread = one 2x2 block
+__global__ __launch_bounds__(256) void cg_prep_input_s2d_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
+                                                                long nblk, int H, int W, int c_in) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  const int Wb = W / 2, Hb = H / 2;
+  for (long b = (long)blockIdx.x * blockDim.x + threadIdx.x; b < nblk; b += stride) {
+    const long img = b / ((long)Hb * Wb);
+    const int r = (int)(b - img * Hb * Wb), by = r / Wb, bx = r - by * Wb;
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = 0.f;
+    for (int q = 0; q < 4; ++q) {
+      const float* src = x + ((img * H + 2 * by + (q >> 1)) * W + 2 * bx + (q & 1)) * c_in;
+      for (int c = 0; c < c_in; ++c) v[q * c_in + c] = src[c];
+    }
+    uint4* dst = reinterpret_cast<uint4*>(y + b * 16);
+    dst[0] = make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+    dst[1] = make_uint4(pack2bf(v[8], v[9]), pack2bf(v[10], v[11]), pack2bf(v[12], v[13]), pack2bf(v[14], v[15]));
   }
 }
 
@@ -854,6 +890,16 @@ DTF_API int dtf_cg_prep_input(const float* x, bf16_t* y, long npix, int c_in, hi
   long blocks = (npix + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(cg_prep_input_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, y, npix, c_in);
+  return DTF_CHECK_LAUNCH();
+}
+
+DTF_API int dtf_cg_prep_input_s2d(const float* x, bf16_t* y, int N, int H, int W, int c_in, hipStream_t stream) {
+  if (N <= 0) return 0;
+  if ((H & 1) || (W & 1) || c_in * 4 > 16) return -2;
+  const long nblk = (long)N * (H / 2) * (W / 2);
+  long blocks = (nblk + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(cg_prep_input_s2d_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, y, nblk, H, W, c_in);
   return DTF_CHECK_LAUNCH();
 }
 

@@ -27,8 +27,8 @@ def launches(N: int, H: int = 224):
     B = 2 * N  # bytes per (pixel, channel) element over the population batch
     out = []
     H1, H2 = H // 2, H // 4
-    out.append(("prep_input", "input", N * H * H * (3 * 4 + 8 * 2), 0))
-    out.append(("conv fwd", "stem 7x7/2", B * (H * H * 8 + H1 * H1 * 64), 2 * N * H1 * H1 * 64 * 49 * 8))
+    out.append(("prep_input", "input", N * H * H * (3 * 4 + 4 * 2), 0))  # fp32 image -> s2d bf16 blocks
+    out.append(("conv fwd", "stem 7x7/2 (s2d 4x4)", B * (H1 * H1 * 16 + H1 * H1 * 64), 2 * N * H1 * H1 * 64 * 256))
     out.append(("maxpool fwd", "maxpool", B * (H1 * H1 * 64 + H2 * H2 * 64) + N * H2 * H2 * 64, 0))
     hw, cin = H2, 64
     geo = []
@@ -63,7 +63,8 @@ def launches(N: int, H: int = 224):
         out.append(("conv wgrad", t + "c1", B * (hi * hi * cin + hi * hi * f), 2 * N * hi * hi * cin * f))
         out.append(("bn_bwd_apply", t + "g", B * (3 if proj else 4) * hi * hi * cin, 0))
     out.append(("maxpool bwd", "maxpool", B * (H2 * H2 * 64 + H1 * H1 * 64) + N * H2 * H2 * 64, 0))
-    out.append(("conv wgrad", "stem", B * (H * H * 8 + H1 * H1 * 64), 2 * N * H1 * H1 * 64 * 49 * 8))
+    # space-to-depth stem (hip_imagenet.py _CG_S2D): a 4x4/1 conv over [H1][H1][16] blocks, K = 256
+    out.append(("conv wgrad", "stem", B * (H1 * H1 * 16 + H1 * H1 * 64), 2 * N * H1 * H1 * 64 * 256))
     return out
 
 

@@ -588,6 +588,9 @@ class _ImageNetPlan:
                 and cin % 32 == 0 and c.cout % 8 == 0):
             self._wgrad_t3(a, hw_in, cin, c.cout)
             return
+        if s2d and _CG_WGT3 and hw_out == 112 and mode_x == 0 and mode_dy == 0:  # the stem: 2-row bands of 112
+            self._wgrad_t3(a, hw_out, 16, c.cout, R=2, bkc=16)
+            return
         wide3 = c.k == 3 and cin % 64 == 0
         wide1 = c.k == 1 and cin % 256 == 0 and _CG_WIDE1
         wide7 = ci == be.prog.stem and c.k == 7 and cin == 8 and c.cout == 64 and _CG_WIDE7 and not s2d
@@ -609,12 +612,13 @@ class _ImageNetPlan:
         flags = (4 if (_CG_WPK_WO64 if wo == 64 else _CG_WPK) == 64 else 0) | (8 if wo == 64 else 0)
         self._add(ops.lib().dtf_convg_wgrad, ctypes.byref(a), mode_x, mode_dy | flags, work.shape[0])
 
-    def _wgrad_t3(self, a, hw, cin, cout):
-        """Row-band 3x3 weight gradient: items (slot, first band, end band, o0 | ci chunk << 16) -- per member, per
-        64-row output tile and 32-channel input chunk, the member's bands split into about _CG_WGT3_TARGET items."""
-        R = _CG_WGT3[hw]
+    def _wgrad_t3(self, a, hw, cin, cout, R=None, bkc=32):
+        """Row-band weight gradient (3x3, or the 4x4 space-to-depth stem with R = 2, bkc = 16): items (slot, first
+        band, end band, o0 | ci chunk << 16) -- per member, per 64-row output tile and bkc-channel input chunk, the
+        member's bands split into about _CG_WGT3_TARGET items."""
+        R = R or _CG_WGT3[hw]
         bpi = hw // R
-        tiles = [(o0, cc) for o0 in range(0, cout, 64) for cc in range(cin // 32)]
+        tiles = [(o0, cc) for o0 in range(0, cout, 64) for cc in range(cin // bkc)]
         total = sum(self.sizes) * bpi * len(tiles)
         chunk = max(1, -(-total // _CG_WGT3_TARGET))
         items = []

@@ -1265,20 +1265,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ?
 // and k-step); the next band is prefetched into registers while the current one runs.
 // work: (slot, first band, end band, o0 | ci-chunk << 16); band b = image b / (H / R), rows (b % (H / R)) * R ..
 // Pixels past R * W in the last k-step (W = 28: 196 of 224) stage zero dY rows and contribute nothing.
-template <int W, int R>
+// KT x KT taps, BKC input channels per column tile, PAD rows / columns before the image: <W, R, 3, 32, 1> for the
+// 3x3 convs; <112, 2, 4, 16, 2> for the space-to-depth stem (4x4 over 16 block channels, cin_real = -3: columns
+// remapped onto the 7x7x3 kernel as in the wide kernel)
+template <int W, int R, int KT = 3, int BKC = 32, int PAD = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void convg_wgrad_t3_kernel(CgArgs a) {
-  constexpr int WO = 64, BKC = 32;
+  constexpr int WO = 64, HPC = BKC / 16;  // HPC: 16-channel column tiles per tap
   constexpr int NPV = R * W, NKS = (NPV + 31) / 32, NPX = NKS * 32;
   constexpr int WOP = WO + 8;            // dY tile pitch (bf16)
   constexpr int CP = BKC + 8;            // halo pixel pitch (bf16)
-  constexpr int WS = W + 2, RT = R + 2;  // halo columns / rows
-  constexpr int MTW = WO / 32, NTW = 9;  // A tiles per wave (32 rows), B column tiles per wave (of 18)
+  constexpr int WS = W + KT - 1, RT = R + KT - 1;  // halo columns / rows
+  constexpr int NCT = KT * KT * HPC;     // column tiles of the workgroup (9 x 2 = 18; 16 x 1 = 16)
+  constexpr int MTW = WO / 32, NTW = NCT / 2;  // A tiles per wave (32 rows), B column tiles per wave
   constexpr int DCH = NPX * WO / 8, DJ = (DCH + 255) / 256;
   constexpr int XCH = RT * WS * (BKC / 8), XJ = (XCH + 255) / 256;
   __shared__ __attribute__((aligned(16))) bf16_t sd[NPX * WOP];
   __shared__ __attribute__((aligned(16))) bf16_t sx[RT * WS * CP + 8];
   const int4 wk = a.work[blockIdx.x];
-  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z > wk.y && a.Wi == W && a.Wo == W && a.Ho == a.Hi && a.Hi % R == 0);
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z > wk.y && a.Wi == W && a.Wo == W && a.Ho == a.Hi && a.Hi % R == 0 &&
+               a.kh == KT && a.pad == PAD);
   const int slot = wk.x, b0 = wk.y, b1 = wk.z, o0 = wk.w & 0xffff, cc = wk.w >> 16;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wr = wave & 1, wc = wave >> 1;
@@ -1313,7 +1318,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     const long xbase = (long)img * H * W * Ci + cc * BKC;
 #pragma unroll
     for (int j = 0; j < XJ; ++j) {
-      const int gy = y0 - 1 + xhr[j], gx = xhc[j] - 1;
+      const int gy = y0 - PAD + xhr[j], gx = xhc[j] - PAD;
       const bool ok = xhr[j] < RT && gy >= 0 && gy < H && gx >= 0 && gx < W;
       xv[j] = ld16(a.x, xbase + ((long)gy * W + gx) * Ci + xc8[j], ok);
       xok |= (unsigned)ok << j;
@@ -1359,8 +1364,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       const int ha = ((qa / W) * WS + qa % W) * CP + 4 * p4, hb = ((qb / W) * WS + qb % W) * CP + 4 * p4;
 #pragma unroll
       for (int n = 0; n < NTW; ++n) {
-        const int j = NTW * wc + n, t = j >> 1;  // column tile j = (tap t, 16-channel half j & 1)
-        const int toff = ((t / 3) * WS + t % 3) * CP + 16 * (j & 1);
+        const int j = NTW * wc + n, t = j / HPC;  // column tile j = (tap t, 16-channel piece j % HPC)
+        const int toff = ((t / KT) * WS + t % KT) * CP + 16 * (j % HPC);
         const s16x4_t lo = ds_read_tr(sx + ha + toff);
         const s16x4_t hi = ds_read_tr(sx + hb + toff);
         const bf16x8_t fb = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -1374,18 +1379,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       __syncthreads();
     }
   }
-  // D: lane holds column (lane & 15) of tile (tap, half), rows 4 (lane >> 4) + r
+  // D: lane holds column (lane & 15) of tile (tap, piece), rows 4 (lane >> 4) + r
   dtf_acc_t* gr = a.grads + (long)slot * a.g_mstride + a.g_off;
+  const bool s2d = a.cin_real == -3;
 #pragma unroll
   for (int n = 0; n < NTW; ++n) {
-    const int j = NTW * wc + n, t = j >> 1;
-    const int ci = cc * BKC + 16 * (j & 1) + (lane & 15);
+    const int j = NTW * wc + n, t = j / HPC;
+    const int ci = cc * BKC + 16 * (j % HPC) + (lane & 15);
+    long col = (long)t * Ci + ci;
+    int Kr = KT * KT * Ci;
+    if (s2d) {  // (tap', (2 dy + dx) * 3 + c) -> weight (2a + dy - 1, 2b + dx - 1, c) of the 7x7x3 kernel
+      const int qd = ci / 3, c = ci - 3 * qd;
+      const int ky = 2 * (t / KT) + (qd >> 1) - 1, kx = 2 * (t % KT) + (qd & 1) - 1;
+      if (qd >= 4 || ky < 0 || ky > 6 || kx < 0 || kx > 6) continue;
+      col = (ky * 7 + kx) * 3 + c;
+      Kr = 49 * 3;
+    }
 #pragma unroll
     for (int m = 0; m < MTW; ++m)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int o = o0 + wr * (WO / 2) + 16 * m + 4 * (lane >> 4) + r;
-        if (o < Co) dtf_acc_add(gr + ((long)o * 9 + t) * Ci + ci, acc[m][n][r], DTF_FX_GRAD, slot);
+        if (o < Co) dtf_acc_add(gr + (long)o * Kr + col, acc[m][n][r], DTF_FX_GRAD, slot);
       }
   }
 }
@@ -1539,9 +1554,16 @@ DTF_API int dtf_convg_wgrad_wide(const CgArgs* a, int wo, int wt, int nwork, int
 // stride-1 3x3 weight gradient from row bands (convg_wgrad_t3_kernel): W = image width, R = rows per band
 DTF_API int dtf_convg_wgrad_t3(const CgArgs* a, int W, int R, int nwork, hipStream_t stream) {
   if (nwork <= 0) return 0;
-  if (a->kh != 3 || a->kw != 3 || a->stride != 1 || a->pad != 1 || a->Ci % 32 || a->Co % 8 || a->Wi != W ||
-      a->Hi % R)
+  const bool stem = a->cin_real == -3;  // the space-to-depth stem: 4x4 taps over 16 block channels, pad 2
+  if (a->stride != 1 || a->Co % 8 || a->Wi != W || a->Hi % R ||
+      (stem ? (a->kh != 4 || a->kw != 4 || a->pad != 2 || a->Ci != 16)
+            : (a->kh != 3 || a->kw != 3 || a->pad != 1 || a->Ci % 32)))
     return -2;
+  if (stem && W == 112 && R == 2) {
+    hipLaunchKernelGGL((convg_wgrad_t3_kernel<112, 2, 4, 16, 2>), dim3(nwork), dim3(256), 0, stream, *a);
+    return DTF_CHECK_LAUNCH();
+  }
+  if (stem) return -1;
 #define WT3_CASE(W_, R_)                                                                                      if (W == W_ && R == R_) {                                                                                     hipLaunchKernelGGL((convg_wgrad_t3_kernel<W_, R_>), dim3(nwork), dim3(256), 0, stream, *a);                 return DTF_CHECK_LAUNCH();                                                                                }
   WT3_CASE(56, 4) WT3_CASE(28, 7) WT3_CASE(14, 14)
 #undef WT3_CASE

@@ -412,6 +412,58 @@ __global__ __launch_bounds__(256) void cg_maxpool_bwd_kernel(const bf16_t* __res
   }
 }
 
+// The same backward for even H, W with Ho = H / 2 (every ImageNet shape): thread = one 2 x 2 input block (by, bx)
+// and 8 channels.  The block's 4 pixels draw only on the windows {by - 1, by} x {bx - 1, bx}, so each window's
+// gradient / argmax is loaded once for 4 pixels (the per-pixel form above loads ~2.25 windows per pixel) and the
+// 4 output rows are written as 16-byte stores.  Pixel (dy, dx) of the block receives window (by - a, bx - b)'s
+// gradient when its argmax is tap (dy + 2a) * 3 + (dx + 2b) (a, b in {0, 1}; a = 1 only for dy = 0).
+__global__ __launch_bounds__(256) void cg_maxpool_bwd2_kernel(const bf16_t* __restrict__ g, const uint8_t* __restrict__ am,
+                                                               bf16_t* __restrict__ dx, int Ho, int Wo, int C,
+                                                               long total8) {
+  const unsigned stride = gridDim.x * blockDim.x, C8 = (unsigned)C / 8;
+  const int W = 2 * Wo;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < (unsigned)total8; i += stride) {
+    const unsigned blk = i / C8;
+    const int c0 = (int)(i - blk * C8) * 8;
+    const unsigned pr = blk / (unsigned)Wo;
+    const int bx = (int)(blk - pr * Wo), by = (int)(pr % (unsigned)Ho);
+    const long img = pr / (unsigned)Ho;
+    uint2 av[2][2];
+    uint4 gv[2][2];
+#pragma unroll
+    for (int a_ = 0; a_ < 2; ++a_)
+#pragma unroll
+      for (int b_ = 0; b_ < 2; ++b_) {
+        const bool ok = by - a_ >= 0 && bx - b_ >= 0;
+        const long o = ok ? ((img * Ho + by - a_) * Wo + bx - b_) * C + c0 : 0;
+        av[a_][b_] = *(ok ? reinterpret_cast<const uint2*>(am + o) : &g_mp_ff8);
+        gv[a_][b_] = *(ok ? reinterpret_cast<const uint4*>(g + o) : &g_mp_zero16);
+      }
+#pragma unroll
+    for (int py = 0; py < 2; ++py)
+#pragma unroll
+      for (int px = 0; px < 2; ++px) {
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int a_ = 0; a_ < 2; ++a_)
+#pragma unroll
+          for (int b_ = 0; b_ < 2; ++b_) {
+            if ((a_ && py) || (b_ && px)) continue;  // window by - 1 / bx - 1 covers only the block's first row / col
+            const uint32_t t = (uint32_t)((py + 2 * a_) * 3 + px + 2 * b_);
+            const uint32_t g32[4] = {gv[a_][b_].x, gv[a_][b_].y, gv[a_][b_].z, gv[a_][b_].w};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const uint32_t ak = ((k < 4 ? av[a_][b_].x : av[a_][b_].y) >> (8 * (k & 3))) & 0xffu;
+              if (ak == t) acc[k] += bf2f((bf16_t)((g32[k >> 1] >> (16 * (k & 1))) & 0xffff));
+            }
+          }
+        const long o = ((img * 2 * Ho + 2 * by + py) * W + 2 * bx + px) * C + c0;
+        *reinterpret_cast<uint4*>(dx + o) = make_uint4(pack2bf(acc[0], acc[1]), pack2bf(acc[2], acc[3]),
+                                                       pack2bf(acc[4], acc[5]), pack2bf(acc[6], acc[7]));
+      }
+  }
+}
+
 struct GapArgs {
   const bf16_t* x;      // [N][hw][C] last block output (pre final BN)
   const float* coef;    // final BN forward coefficients [cap][4][cmax] (nullptr: identity, v1)
@@ -910,7 +962,12 @@ DTF_API int dtf_cg_maxpool(const bf16_t* x, bf16_t* y, uint8_t* am, const bf16_t
   if (total8 >= (1L << 31)) return -2;  // 32-bit element indices in the kernels
   long blocks = (total8 + 255) / 256;
   if (blocks > 16384) blocks = 16384;
-  if (backward)
+  if (backward && H == 2 * Ho && W == 2 * Wo) {  // 2 x 2 input blocks per thread
+    const long tb8 = total8 / 4;
+    long b2 = (tb8 + 255) / 256;
+    if (b2 > 16384) b2 = 16384;
+    hipLaunchKernelGGL(cg_maxpool_bwd2_kernel, dim3((unsigned)b2), dim3(256), 0, stream, g, am, dx, Ho, Wo, C, tb8);
+  } else if (backward)
     hipLaunchKernelGGL(cg_maxpool_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, g, am, dx, H, W, Ho, Wo, C,
                        total8);
   else

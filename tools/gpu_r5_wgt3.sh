@@ -1,0 +1,20 @@
+#!/bin/bash
+# row-band weight gradients (3x3 + s2d stem): numerics (release + det) and A/B vs DTF_CG_WGT3=0 -> gpurun_out/r5wg
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out/r5wg
+timeout -k 10 500 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_imagenet_step.py > gpurun_out/r5wg/pytest.log 2>&1
+rc=$?; echo "imagenet tests: $(tail -1 gpurun_out/r5wg/pytest.log)"; [ $rc -ne 0 ] && { grep -E "rel|Error|assert" gpurun_out/r5wg/pytest.log | head -30; tail -20 gpurun_out/r5wg/pytest.log; exit 1; }
+DTF_DETERMINISTIC=1 timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_imagenet_step.py > gpurun_out/r5wg/det.log 2>&1
+rc=$?; echo "det build: $(tail -1 gpurun_out/r5wg/det.log)"; [ $rc -ne 0 ] && { tail -20 gpurun_out/r5wg/det.log; exit 1; }
+: > gpurun_out/r5wg/ab.log
+for pass in 1 2; do
+  for w in 1 0; do
+    DTF_CG_WGT3=$w timeout -k 10 300 python -u bench.py --model imagenet --steps 10 --warmup 3 ${BENCH_EXTRA:-} > gpurun_out/r5wg/b.log 2>&1 || { tail -5 gpurun_out/r5wg/b.log; exit 1; }
+    echo "WGT3=$w: $(grep '^{' gpurun_out/r5wg/b.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print(d['ms_per_step'], 'ms', d['value'], 'img/s')")" | tee -a gpurun_out/r5wg/ab.log
+  done
+done
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/wgp -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --model imagenet --steps 3 --warmup 2 --exploit_every 0 > "$GRAFT_REPO_ROOT/gpurun_out/r5wg/prof.log" 2>&1 || { tail -5 "$GRAFT_REPO_ROOT/gpurun_out/r5wg/prof.log"; exit 1; }
+find /tmp/wgp \( -name "*kernel_trace*" \) -exec cp {} "$GRAFT_REPO_ROOT/gpurun_out/r5wg/" \;
+cd "$GRAFT_REPO_ROOT" && python3 tools/imagenet_roofline.py gpurun_out/r5wg/run_kernel_trace.csv --top 30 > gpurun_out/r5wg/roofline.txt 2>&1; head -12 gpurun_out/r5wg/roofline.txt
+exit 0

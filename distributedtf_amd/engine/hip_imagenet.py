@@ -62,6 +62,10 @@ _CG_T3 = {56: 8, 28: 7, 14: 14}  # must match dtf_convg_t3 (rows divide the imag
 # weight gradient -- stages its input (convg MODE 1, convg_t3 XF, convg_wgrad_wide MX 1), so no relu(BN(.)) tensor
 # (ax / a1 / a2) is materialised: 3 elementwise passes per block fewer
 CG_FOLD = os.environ.get("DTF_CG_FOLD", "0") == "1"
+# selective fold: only BN2 + ReLU (conv1 output -> the 3x3 conv2) is applied by its consumers -- conv2's forward
+# (convg_t3 XF / convg MODE 1 when strided) and weight gradient (row-band MX 1 / wide MX 1) -- so the a1 = relu(BN2(h1))
+# tensor is never written (each element is transformed once per 32-channel chunk and output tile)
+CG_FOLD2 = os.environ.get("DTF_CG_FOLD2", "0") == "1"  # measured +2.7 ms: profiles/r5_imagenet_fold2_ab.log
 T3_FLAGS = int(os.environ.get("DTF_T3_FLAGS", "1"))  # direct: 81.61 vs staged 80.92 ms (profiles/r4_imagenet_t3_ab.log)
 _CG_WG_TARGET = 512
 _CG_WG_MINCHUNK = 2048
@@ -124,7 +128,7 @@ def _register():
     reg("dtf_convg_t3", [P(CgArgs), c_int, c_int, c_int, c_int, c_int, c_int, c_void_p])
     reg("dtf_convg_wgrad", [P(CgArgs), c_int, c_int, c_int, c_void_p])
     reg("dtf_convg_wgrad_wide", [P(CgArgs), c_int, c_int, c_int, c_int, c_void_p])
-    reg("dtf_convg_wgrad_t3", [P(CgArgs), c_int, c_int, c_int, c_void_p])
+    reg("dtf_convg_wgrad_t3", [P(CgArgs), c_int, c_int, c_int, c_int, c_void_p])
     reg("dtf_cg_weight_prep", [c_void_p, c_long, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_long,
                                c_void_p])
     reg("dtf_cg_dense_prep", [c_void_p, c_long, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_long,
@@ -370,6 +374,7 @@ class _ImageNetPlan:
         self.ax, self.a1, self.a2 = [], [], []
         # folded forward (CG_FOLD): v2 training plans keep no relu(BN(.)) tensors
         self.fold = CG_FOLD and not self.eval and not be.v1
+        self.fold2 = CG_FOLD2 and not self.fold and not self.eval and not be.v1
         # v1 (post-activation): h3 = conv3 output (BN3 input), sc = raw projection output (BN_p input), a0 = the
         # stem's relu(BN(y0)); no ax (the block input IS a ReLU output)
         self.v1 = be.v1
@@ -384,7 +389,7 @@ class _ImageNetPlan:
             self.h2.append(act("h2", ho, c2.cout))
             self.ax.append(act("ax", hw, cin) if not (self.v1 or self.fold) else None)
             self.h3.append(act("h3", ho, c3.cout) if self.v1 else None)
-            self.a1.append(act("a1", hw, c1.cout) if not self.fold else None)
+            self.a1.append(act("a1", hw, c1.cout) if not (self.fold or self.fold2) else None)
             self.a2.append(act("a2", ho, c2.cout) if not self.fold else None)
             self.sc.append(act("sc", ho, c3.cout) if blk.proj is not None else None)
             self.xs.append(act("x", ho, c3.cout, bi + 1))
@@ -584,9 +589,9 @@ class _ImageNetPlan:
             a.Ci, a.kh, a.kw, a.stride, a.pad = 16, 4, 4, 1, 2
             a.log2ci, a.cin_real = 4, -3
             K = 256
-        if (c.k == 3 and c.stride == 1 and not s2d and hw_in in _CG_WGT3 and mode_x == 0 and mode_dy == 0
+        if (c.k == 3 and c.stride == 1 and not s2d and hw_in in _CG_WGT3 and mode_x in (0, 1) and mode_dy == 0
                 and cin % 32 == 0 and c.cout % 8 == 0):
-            self._wgrad_t3(a, hw_in, cin, c.cout)
+            self._wgrad_t3(a, hw_in, cin, c.cout, mode_x=mode_x)
             return
         if s2d and _CG_WGT3 and hw_out == 112 and mode_x == 0 and mode_dy == 0:  # the stem: 2-row bands of 112
             self._wgrad_t3(a, hw_out, 16, c.cout, R=2, bkc=16)
@@ -612,7 +617,7 @@ class _ImageNetPlan:
         flags = (4 if (_CG_WPK_WO64 if wo == 64 else _CG_WPK) == 64 else 0) | (8 if wo == 64 else 0)
         self._add(ops.lib().dtf_convg_wgrad, ctypes.byref(a), mode_x, mode_dy | flags, work.shape[0])
 
-    def _wgrad_t3(self, a, hw, cin, cout, R=None, bkc=32):
+    def _wgrad_t3(self, a, hw, cin, cout, R=None, bkc=32, mode_x=0):
         """Row-band weight gradient (3x3, or the 4x4 space-to-depth stem with R = 2, bkc = 16): items (slot, first
         band, end band, o0 | ci chunk << 16) -- per member, per 64-row output tile and bkc-channel input chunk, the
         member's bands split into about _CG_WGT3_TARGET items."""
@@ -630,7 +635,7 @@ class _ImageNetPlan:
         work = self._hold(torch.tensor(items, dtype=torch.int32, device=self.be.dev))
         a.work = _p(work)
         self._hold(a)
-        self._add(ops.lib().dtf_convg_wgrad_t3, ctypes.byref(a), hw, R, work.shape[0])
+        self._add(ops.lib().dtf_convg_wgrad_t3, ctypes.byref(a), hw, R, work.shape[0], mode_x)
 
     def bn_final(self, bn, hw, backward):
         be, e = self.be, self.e
@@ -769,8 +774,11 @@ class _ImageNetPlan:
                 self.conv(blk.proj, self.ax[i], self.sc[i], hi, mode=0, epi=0)
             self.conv(c1, self.ax[i], self.h1[i], hi, mode=0, epi=4, st=self.sf(b2))
             self.bn_final(b2, hi, False)
-            self.ew(relu, self.h1[i], self.a1[i], self.cf(b2), hi, f)
-            self.conv(c2, self.a1[i], self.h2[i], hi, mode=0, epi=4, st=self.sf(b3))
+            if self.fold2:
+                self.conv(c2, self.h1[i], self.h2[i], hi, mode=1, c_in=self.cf(b2), epi=4, st=self.sf(b3))
+            else:
+                self.ew(relu, self.h1[i], self.a1[i], self.cf(b2), hi, f)
+                self.conv(c2, self.a1[i], self.h2[i], hi, mode=0, epi=4, st=self.sf(b3))
             self.bn_final(b3, ho, False)
             self.ew(relu, self.h2[i], self.a2[i], self.cf(b3), ho, f)
             self.conv(c3, self.a2[i], self.xs[i + 1], ho, mode=0, epi=5, res=res, st=self.sf(nxt))
@@ -815,7 +823,10 @@ class _ImageNetPlan:
             self.bn_final(b2, hi, True)
             dh1 = self.tmp("dh1", hi, f)
             self.ew(bwd, h1, dh1, self.cb(b2), hi, f, dz=dz2)
-            self.wgrad(c2, h1, dh2, hi, mode_x=1, c_x=self.cf(b2)) if self.fold else self.wgrad(c2, self.a1[i], dh2, hi)
+            if self.fold or self.fold2:
+                self.wgrad(c2, h1, dh2, hi, mode_x=1, c_x=self.cf(b2))
+            else:
+                self.wgrad(c2, self.a1[i], dh2, hi)
             pd = None
             if blk.proj is not None:
                 pd = self.tmp("pd", hi, cin)

@@ -1268,7 +1268,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ?
 // KT x KT taps, BKC input channels per column tile, PAD rows / columns before the image: <W, R, 3, 32, 1> for the
 // 3x3 convs; <112, 2, 4, 16, 2> for the space-to-depth stem (4x4 over 16 block channels, cin_real = -3: columns
 // remapped onto the 7x7x3 kernel as in the wide kernel)
-template <int W, int R, int KT = 3, int BKC = 32, int PAD = 1>
+// MX 1: x operand = relu(BN(x)) applied while the halo is staged (c_in scale / shift; padding stays zero) -- the
+// selectively folded forward (hip_imagenet.py CG_FOLD2) keeps no materialised relu(BN2(h1))
+template <int W, int R, int KT = 3, int BKC = 32, int PAD = 1, int MX = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void convg_wgrad_t3_kernel(CgArgs a) {
   constexpr int WO = 64, HPC = BKC / 16;  // HPC: 16-channel column tiles per tap
   constexpr int NPV = R * W, NKS = (NPV + 31) / 32, NPX = NKS * 32;
@@ -1281,6 +1283,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   constexpr int XCH = RT * WS * (BKC / 8), XJ = (XCH + 255) / 256;
   __shared__ __attribute__((aligned(16))) bf16_t sd[NPX * WOP];
   __shared__ __attribute__((aligned(16))) bf16_t sx[RT * WS * CP + 8];
+  __shared__ float xcf[MX ? 2 * BKC : 1];
   const int4 wk = a.work[blockIdx.x];
   DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z > wk.y && a.Wi == W && a.Wo == W && a.Ho == a.Hi && a.Hi % R == 0 &&
                a.kh == KT && a.pad == PAD);
@@ -1288,6 +1291,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wr = wave & 1, wc = wave >> 1;
   const int Ci = a.Ci, Co = a.Co, H = a.Hi, BPI = H / R;
+  if constexpr (MX == 1) {
+    if (tid < BKC) {
+      const float* cb = a.c_in + (long)slot * 4 * a.cmax + cc * BKC;
+      xcf[tid] = cb[tid];
+      xcf[BKC + tid] = cb[a.cmax + tid];
+    }
+    __syncthreads();
+  }
   // dY slots: chunk q = tid + 256 j -> band pixel q / 8, channels 8 (q % 8)
   int dpx[DJ], dch[DJ];
   unsigned dok = 0;
@@ -1330,10 +1341,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       const int q = tid + 256 * j;
       if (q < DCH) *reinterpret_cast<uint4*>(sd + dpx[j] * WOP + dch[j]) = (dok >> j) & 1u ? dv[j] : make_uint4(0, 0, 0, 0);
     }
+    float sc[8], sh[8];
+    if constexpr (MX == 1) {
+      const int c0 = xc8[0];  // the same 8 channels for every slot of this thread (256 % (BKC / 8) == 0)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        sc[k] = xcf[c0 + k];
+        sh[k] = xcf[BKC + c0 + k];
+      }
+    }
 #pragma unroll
     for (int j = 0; j < XJ; ++j) {
       const int off = xhr[j] < RT ? (xhr[j] * WS + xhc[j]) * CP + xc8[j] : RT * WS * CP;
-      *reinterpret_cast<uint4*>(sx + off) = (xok >> j) & 1u ? xv[j] : make_uint4(0, 0, 0, 0);
+      uint4 t = (xok >> j) & 1u ? xv[j] : make_uint4(0, 0, 0, 0);
+      if constexpr (MX == 1) t = (xok >> j) & 1u ? bnrelu8(t, sc, sh) : t;
+      *reinterpret_cast<uint4*>(sx + off) = t;
     }
   };
   // fragment lanes: g = lane / 16 (8 k-rows), q = k-row within the quad, p4 = 4-column piece
@@ -1552,7 +1574,7 @@ DTF_API int dtf_convg_wgrad_wide(const CgArgs* a, int wo, int wt, int nwork, int
 }
 
 // stride-1 3x3 weight gradient from row bands (convg_wgrad_t3_kernel): W = image width, R = rows per band
-DTF_API int dtf_convg_wgrad_t3(const CgArgs* a, int W, int R, int nwork, hipStream_t stream) {
+DTF_API int dtf_convg_wgrad_t3(const CgArgs* a, int W, int R, int nwork, int mode_x, hipStream_t stream) {
   if (nwork <= 0) return 0;
   const bool stem = a->cin_real == -3;  // the space-to-depth stem: 4x4 taps over 16 block channels, pad 2
   if (a->stride != 1 || a->Co % 8 || a->Wi != W || a->Hi % R ||
@@ -1564,7 +1586,15 @@ DTF_API int dtf_convg_wgrad_t3(const CgArgs* a, int W, int R, int nwork, hipStre
     return DTF_CHECK_LAUNCH();
   }
   if (stem) return -1;
-#define WT3_CASE(W_, R_)                                                                                      if (W == W_ && R == R_) {                                                                                     hipLaunchKernelGGL((convg_wgrad_t3_kernel<W_, R_>), dim3(nwork), dim3(256), 0, stream, *a);                 return DTF_CHECK_LAUNCH();                                                                                }
+  if (mode_x != 0 && (mode_x != 1 || stem)) return -2;
+#define WT3_CASE(W_, R_)                                                                                    \
+  if (W == W_ && R == R_) {                                                                                 \
+    if (mode_x)                                                                                             \
+      hipLaunchKernelGGL((convg_wgrad_t3_kernel<W_, R_, 3, 32, 1, 1>), dim3(nwork), dim3(256), 0, stream, *a); \
+    else                                                                                                    \
+      hipLaunchKernelGGL((convg_wgrad_t3_kernel<W_, R_>), dim3(nwork), dim3(256), 0, stream, *a);           \
+    return DTF_CHECK_LAUNCH();                                                                              \
+  }
   WT3_CASE(56, 4) WT3_CASE(28, 7) WT3_CASE(14, 14)
 #undef WT3_CASE
   return -1;

@@ -1,5 +1,5 @@
 #!/bin/bash
-# row-band weight gradients (3x3 + s2d stem): numerics (release + det) and A/B vs DTF_CG_WGT3=0 -> gpurun_out/r5wg
+# ImageNet kernel changes: numerics (release + det) and an A/B of DTF_CG_FOLD2 (selective BN2 fold) -> gpurun_out/r5wg
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/r5wg

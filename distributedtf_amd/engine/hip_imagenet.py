@@ -54,6 +54,9 @@ _CG_S2D = os.environ.get("DTF_CG_S2D", "1") == "1"
 # items per launch (each adds one 64 x 288 fp32 tile into the gradient row)
 _CG_WGT3 = {56: 4, 28: 7, 14: 14} if os.environ.get("DTF_CG_WGT3", "1") == "1" else {}
 _CG_WGT3_TARGET = int(os.environ.get("DTF_CG_WGT3_TARGET", "512"))
+# the s2d stem forward from 2-row bands (convg_stem_s2d_kernel) at 224 x 224; workgroups per launch
+_CG_STEM_BAND = os.environ.get("DTF_CG_STEM_BAND", "1") == "1"
+_CG_STEM_WG = int(os.environ.get("DTF_CG_STEM_WG", "1024"))
 _CG_WPK_WO64 = 32  # pixels per k-step of the 64-row tiles
 # stride-1 3x3 forward / data gradient with LDS-resident input rows (convg_t3_kernel): image width -> rows per tile
 _CG_T3 = {56: 8, 28: 7, 14: 14}  # must match dtf_convg_t3 (rows divide the image height)
@@ -129,6 +132,7 @@ def _register():
     reg("dtf_convg_wgrad", [P(CgArgs), c_int, c_int, c_int, c_void_p])
     reg("dtf_convg_wgrad_wide", [P(CgArgs), c_int, c_int, c_int, c_int, c_void_p])
     reg("dtf_convg_wgrad_t3", [P(CgArgs), c_int, c_int, c_int, c_int, c_void_p])
+    reg("dtf_convg_stem_s2d", [P(CgArgs), c_int, c_int, c_int, c_int, c_void_p])
     reg("dtf_cg_weight_prep", [c_void_p, c_long, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_long,
                                c_void_p])
     reg("dtf_cg_dense_prep", [c_void_p, c_long, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_long,
@@ -539,6 +543,21 @@ class _ImageNetPlan:
             assert not dgrad
             a.Hi = a.Wi = a.Ho = a.Wo = hw_in // 2  # 4x4/1 over 2x2 blocks (pad 2 before, 1 after)
             a.Ci, a.kh, a.kw, a.stride, a.pad = 16, 4, 4, 1, 2
+            if _CG_STEM_BAND and a.Hi == 112 and mode == 0 and epi in (0, 4) and c.cout == 64:
+                a.log2ci = 4
+                bpi = a.Hi // 2
+                total = self.N * bpi
+                chunk = max(1, -(-total // _CG_STEM_WG))
+                items = []
+                for s_, n_ in zip(self.slots, self.sizes):
+                    f_ = self.first[s_]
+                    for b in range(f_ * bpi, (f_ + n_) * bpi, chunk):
+                        items.append([s_, b, min(b + chunk, (f_ + n_) * bpi), 0])
+                work = self._hold(torch.tensor(items, dtype=torch.int32, device=be.dev))
+                a.work = _p(work)
+                self._hold(a)
+                self._add(ops.lib().dtf_convg_stem_s2d, ctypes.byref(a), a.Hi, 2, epi, work.shape[0])
+                return
         a.log2ci = _log2(a.Ci)
         tc = 128 if a.Co >= 128 else 64
         if (k == 3 and c.stride == 1 and (mode == 0 or (mode == 1 and not dgrad)) and hw_in in _CG_T3

@@ -624,6 +624,9 @@ __host__ __device__ constexpr int t3_nhalf() {
 #ifndef T3_DIRECT_A
 #define T3_DIRECT_A 1  // forward t3: A fragments loaded directly from the weight rows (no LDS staging of A)
 #endif
+#ifndef T3_A_AHEAD
+#define T3_A_AHEAD 1  // ... that many k-steps ahead (2: a 3-set register ring, measured flat: profiles/r5_imagenet_stem_ahead_ab.log)
+#endif
 // XF: the staged input rows get BN + ReLU (coefficients c_in: scale / shift of the input's BN) -- the folded forward
 template <int TC, int EPI, bool AKM, int W, int R, int TP, int WRN, bool XF = false>
 __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
@@ -763,13 +766,23 @@ __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
       for (int m = 0; m < MT; ++m)
         f[m] = __builtin_bit_cast(bf16x8_t, ld16(wl, (long)16 * m * 9 * Ci + t_ * Ci + c_ * BK, orow0 + 16 * m < a.Co));
     };
-    bf16x8_t fa[MT], fan[MT];
+    // A fragments T3_A_AHEAD k-steps ahead (2: a register ring of three sets -- one k-step of 28 MFMAs is ~450
+    // cycles per wave, less than an L2-hit round trip of the weight rows)
+    bf16x8_t fa[MT], fan[MT], fan2[MT];
     load_fa(0, 0, fa);
+    if (T3_A_AHEAD > 1 && nk > 1) load_fa(0, 1, fan);  // k-step 1 = (chunk 0, tap 1)
     __syncthreads();
     int c = 0, t = 0;
     for (int ks = 0; ks < nk; ++ks) {
       const bool more = ks + 1 < nk;
-      if (more) load_fa(t == 8 ? c + 1 : c, t == 8 ? 0 : t + 1, fan);
+      if constexpr (T3_A_AHEAD > 1) {
+        if (ks + 2 < nk) {  // k-step ks + 2 = (chunk, tap) two taps on
+          const int t2 = t + 2 > 8 ? t + 2 - 9 : t + 2, c2 = t + 2 > 8 ? c + 1 : c;
+          load_fa(c2, t2, fan2);
+        }
+      } else if (more) {
+        load_fa(t == 8 ? c + 1 : c, t == 8 ? 0 : t + 1, fan);
+      }
       if (t == 0 && c + 1 < nch) load_b(c + 1, rb);  // next chunk's rows: 9 k-steps of latency cover
       const int tapo = ((t / 3) * WT + t % 3) * RP;
       bf16x8_t fb[NTP];
@@ -785,7 +798,10 @@ __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
         __syncthreads();
       }
 #pragma unroll
-      for (int m = 0; m < MT; ++m) fa[m] = fan[m];
+      for (int m = 0; m < MT; ++m) {
+        fa[m] = fan[m];
+        if constexpr (T3_A_AHEAD > 1) fan[m] = fan2[m];
+      }
       if (++t == 9) {
         t = 0;
         ++c;
@@ -1427,6 +1443,136 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   }
 }
 
+// ------------------------------------------------------------------------------------ s2d stem forward
+// The space-to-depth stem (4x4/1 over 2x2 blocks of the image, 16 channels, pad 2 before / 1 after, Co = 64) from
+// LDS-resident row bands: a workgroup keeps the whole 64 x 256 weight tile in registers (wave w: output channels
+// 16 w .. 16 w + 15, 8 k-steps of 2 taps x 16 channels), stages a band of R output rows' input halo
+// [(R + 3) x (W + 3) x 16] once and reads every tap's B fragment from it; the next band's halo is prefetched into
+// registers.  Each input element is fetched ~1.3x (halo) instead of 16x (the generic gather: one k-step = 2 taps).
+// EPI 4: per-channel sum / sum of squares of the bf16 outputs (the v1 stem's BatchNorm) into st_out.
+// work: (slot, first band, end band, -); band b = image b / (H / R), rows (b % (H / R)) * R ..
+template <int W, int R, int EPI>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void convg_stem_s2d_kernel(CgArgs a) {
+  constexpr int CI = 16, KT = 4, PAD = 2, CO = 64, KS = KT * KT * CI / 32;
+  constexpr int NPV = R * W, NPT = (NPV + 15) / 16;  // pixels per band, 16-pixel tiles
+  constexpr int CP = CI + 8, WS = W + KT - 1, RT = R + KT - 1;
+  constexpr int XCH = RT * WS * (CI / 8), XJ = (XCH + 255) / 256;
+  __shared__ __attribute__((aligned(16))) bf16_t sx[RT * WS * CP + 8];
+  __shared__ dtf_acc_t acc_lds[2][CO];
+  const int4 wk = a.work[blockIdx.x];
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z > wk.y && a.Wi == W && a.Wo == W && a.Ci == CI && a.Co == CO &&
+               a.Hi % R == 0);
+  const int slot = wk.x, b0 = wk.y, b1 = wk.z;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int H = a.Hi, BPI = H / R;
+  if (tid < 2 * CO) (&acc_lds[0][0])[tid] = 0;
+  // weights: lane = output channel 16 wave + (lane & 15), k = 32 s + 8 (lane >> 4) .. + 7
+  bf16x8_t afr[KS];
+  {
+    const bf16_t* wr = a.w + (long)slot * a.w_mstride + a.w_off + (long)(16 * wave + (lane & 15)) * (KS * 32);
+#pragma unroll
+    for (int s_ = 0; s_ < KS; ++s_)
+      afr[s_] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(wr + 32 * s_ + 8 * (lane >> 4)));
+  }
+  // B fragment: lane = pixel (lane & 15) of the tile; k chunk (lane >> 4) = tap 2 s + (lane >> 5), channels
+  // 8 ((lane >> 4) & 1) .. + 7
+  int tapo[KS];
+#pragma unroll
+  for (int s_ = 0; s_ < KS; ++s_) {
+    const int t = 2 * s_ + (lane >> 5);
+    tapo[s_] = ((t / KT) * WS + t % KT) * CP + 8 * ((lane >> 4) & 1);
+  }
+  int xhr[XJ], xhc[XJ], xc8[XJ];
+#pragma unroll
+  for (int j = 0; j < XJ; ++j) {
+    const int q = tid + 256 * j, hp = q / (CI / 8);
+    xc8[j] = 8 * (q % (CI / 8));
+    xhr[j] = q < XCH ? hp / WS : RT;
+    xhc[j] = hp % WS;
+  }
+  uint4 xv[XJ];
+  unsigned xok = 0;
+  auto load = [&](int band) {
+    const int img = band / BPI, y0 = (band - img * BPI) * R;
+    const long xbase = (long)img * H * W * CI;
+    xok = 0;
+#pragma unroll
+    for (int j = 0; j < XJ; ++j) {
+      const int gy = y0 - PAD + xhr[j], gx = xhc[j] - PAD;
+      const bool ok = xhr[j] < RT && gy >= 0 && gy < H && gx >= 0 && gx < W;
+      xv[j] = ld16(a.x, xbase + ((long)gy * W + gx) * CI + xc8[j], ok);
+      xok |= (unsigned)ok << j;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int j = 0; j < XJ; ++j) {
+      const int off = xhr[j] < RT ? (xhr[j] * WS + xhc[j]) * CP + xc8[j] : RT * WS * CP;
+      *reinterpret_cast<uint4*>(sx + off) = (xok >> j) & 1u ? xv[j] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  const int co0 = 16 * wave + 4 * (lane >> 4);
+  float ss[4] = {0.f, 0.f, 0.f, 0.f}, sq[4] = {0.f, 0.f, 0.f, 0.f};
+  load(b0);
+  store();
+  __syncthreads();
+  for (int b = b0; b < b1; ++b) {
+    const bool more = b + 1 < b1;
+    if (more) load(b + 1);
+    const int img = b / BPI, y0 = (b - img * BPI) * R;
+    bf16_t* yb = a.y + (((long)img * H + y0) * W) * CO + co0;
+#pragma unroll 2
+    for (int n = 0; n < NPT; ++n) {
+      const int p = 16 * n + (lane & 15);
+      const int pc = p < NPV ? p : 0;
+      const int bo = ((pc / W) * WS + pc % W) * CP;
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s_ = 0; s_ < KS; ++s_)
+        acc = mfma16(afr[s_], *reinterpret_cast<const bf16x8_t*>(sx + bo + tapo[s_]), acc);
+      // D: lane holds channels co0 .. co0 + 3 of pixel 16 n + (lane & 15)
+      const uint32_t lo = pack2bf(acc[0], acc[1]), hi = pack2bf(acc[2], acc[3]);
+      if (p < NPV) {
+        *reinterpret_cast<uint2*>(yb + (long)p * CO) = make_uint2(lo, hi);
+        if constexpr (EPI & 4) {
+          const float r[4] = {lo2f(lo), hi2f(lo), lo2f(hi), hi2f(hi)};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            ss[i] += r[i];
+            sq[i] += r[i] * r[i];
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (more) {
+      store();
+      __syncthreads();
+    }
+  }
+  if constexpr (EPI & 4) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float s_ = ss[i], q_ = sq[i];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {  // the 16 lanes of a (lane >> 4) group hold the same 4 channels
+        s_ += __shfl_xor(s_, o, 64);
+        q_ += __shfl_xor(q_, o, 64);
+      }
+      if ((lane & 15) == 0) {
+        dtf_acc_add(&acc_lds[0][co0 + i], s_, DTF_FX_STAT, slot);
+        dtf_acc_add(&acc_lds[1][co0 + i], q_, DTF_FX_STAT, slot);
+      }
+    }
+    __syncthreads();
+    if (tid < CO) {
+      dtf_acc_t* st = a.st_out + (long)slot * 2 * a.cmax;
+      dtf_acc_addw(st + tid, acc_lds[0][tid]);
+      dtf_acc_addw(st + a.cmax + tid, acc_lds[1][tid]);
+    }
+  }
+}
+
 }  // namespace
 
 DTF_API int dtf_cg_args_size() { return (int)sizeof(CgArgs); }
@@ -1597,6 +1743,23 @@ DTF_API int dtf_convg_wgrad_t3(const CgArgs* a, int W, int R, int nwork, int mod
   }
   WT3_CASE(56, 4) WT3_CASE(28, 7) WT3_CASE(14, 14)
 #undef WT3_CASE
+  return -1;
+}
+
+// the space-to-depth stem forward from row bands (convg_stem_s2d_kernel): W = 112 (224 images), R = 2 rows per band
+DTF_API int dtf_convg_stem_s2d(const CgArgs* a, int W, int R, int epi, int nwork, hipStream_t stream) {
+  if (nwork <= 0) return 0;
+  if (a->Ci != 16 || a->Co != 64 || a->kh != 4 || a->kw != 4 || a->pad != 2 || a->stride != 1 || a->Wi != W ||
+      a->Wo != W || a->Hi % R)
+    return -2;
+  if (W == 112 && R == 2 && epi == 0) {
+    hipLaunchKernelGGL((convg_stem_s2d_kernel<112, 2, 0>), dim3(nwork), dim3(256), 0, stream, *a);
+    return DTF_CHECK_LAUNCH();
+  }
+  if (W == 112 && R == 2 && epi == 4) {
+    hipLaunchKernelGGL((convg_stem_s2d_kernel<112, 2, 4>), dim3(nwork), dim3(256), 0, stream, *a);
+    return DTF_CHECK_LAUNCH();
+  }
   return -1;
 }
 

@@ -10,8 +10,8 @@ rc=$?; echo "det build: $(tail -1 gpurun_out/r5wg/det.log)"; [ $rc -ne 0 ] && { 
 : > gpurun_out/r5wg/ab.log
 for pass in 1 2; do
   for w in 1 0; do
-    DTF_CG_WGT3=$w timeout -k 10 300 python -u bench.py --model imagenet --steps 10 --warmup 3 ${BENCH_EXTRA:-} > gpurun_out/r5wg/b.log 2>&1 || { tail -5 gpurun_out/r5wg/b.log; exit 1; }
-    echo "WGT3=$w: $(grep '^{' gpurun_out/r5wg/b.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print(d['ms_per_step'], 'ms', d['value'], 'img/s')")" | tee -a gpurun_out/r5wg/ab.log
+    DTF_CG_STEM_BAND=$w timeout -k 10 300 python -u bench.py --model imagenet --steps 10 --warmup 3 ${BENCH_EXTRA:-} > gpurun_out/r5wg/b.log 2>&1 || { tail -5 gpurun_out/r5wg/b.log; exit 1; }
+    echo "STEM_BAND=$w: $(grep '^{' gpurun_out/r5wg/b.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print(d['ms_per_step'], 'ms', d['value'], 'img/s')")" | tee -a gpurun_out/r5wg/ab.log
   done
 done
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/wgp -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --model imagenet --steps 3 --warmup 2 --exploit_every 0 > "$GRAFT_REPO_ROOT/gpurun_out/r5wg/prof.log" 2>&1 || { tail -5 "$GRAFT_REPO_ROOT/gpurun_out/r5wg/prof.log"; exit 1; }

@@ -68,7 +68,7 @@ def launches(N: int, H: int = 224):
     return out
 
 
-KERNEL_FAMILY = [("cg_bn_relu_apply", "bn_relu_apply"), ("cg_bn_bwd_apply", "bn_bwd_apply"),
+KERNEL_FAMILY = [("cg_bn_relu_apply", "bn_relu_apply"), ("cg_bn_bwd_apply", "bn_bwd_apply"), ("convg_stem_s2d", "conv fwd"),
                  ("convg_wgrad", "conv wgrad"), ("cg_maxpool_fwd", "maxpool fwd"), ("cg_maxpool_bwd", "maxpool bwd"),
                  ("cg_prep_input", "prep_input")]
 

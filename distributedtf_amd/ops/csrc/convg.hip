@@ -55,6 +55,13 @@ __device__ __forceinline__ uint4 ld16(const bf16_t* base, long off, bool ok) {
   return __builtin_bit_cast(uint4, *p);
 }
 
+typedef unsigned int u32x2v_t __attribute__((ext_vector_type(2)));
+typedef const __attribute__((address_space(1))) u32x2v_t guint2_t;
+__device__ __forceinline__ uint2 ld8(const bf16_t* base, long off, bool ok) {  // 8-byte form of ld16
+  guint2_t* p = ok ? (guint2_t*)(base + off) : (guint2_t*)&g_zero16;
+  return __builtin_bit_cast(uint2, *p);
+}
+
 // relu(x * sc + sh) of 8 bf16 channels (BN + ReLU applied while an operand is staged: the folded forward)
 __device__ __forceinline__ uint4 bnrelu8(uint4 v, const float (&sc)[8], const float (&sh)[8]) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -280,6 +287,122 @@ __device__ __forceinline__ void convg_epilogue32(const CgArgs& a, f32x16_t (&acc
   convg_epilogue_impl<TC, EPI, TRANS, TP, NHALF>(a, stage, cst, acc_lds, slot, o0, p0, p1, HWo, GW, py, px);
 }
 
+// Register-direct epilogue of the 16x16 accumulator tiles (no residual, TRANS = false): lane l of a wave holds, per
+// (m, n) tile, 4 consecutive output channels (rows 4 (l >> 4) .. + 3) of pixel l & 15 -- packed to 4 bf16 and stored
+// as one 8-byte piece (the 4 lanes of a pixel write 32 contiguous bytes; the wave's MT m-tiles complete 128-byte
+// lines back to back).  No LDS staging, hence none of the staged epilogue's 2 barriers per part (NHALF parts): the
+// convg_t3 stamps (tools/t3_bench.py --stamps) put that epilogue at 7 us of a 33 us k loop (forward, 28 x 28) and
+// 14 us (data gradient with the ReLU mask).  EPI bit 1: mask by BN(xm) + ReLU > 0 (xm loads issued together up
+// front); bit 2: per-channel statistics of the stored bf16 values, summed over the lane's pixels in registers, then
+// over the 16 pixel lanes by xor shuffles, one LDS add per wave and channel, one global add per workgroup and channel.
+// EPI bit 0: + residual (loaded like xm).  TRANS: the pixel index is on the parity-class grid (GW wide, HWo per
+// image) of output parity (py, px), as in convg_epilogue_impl.
+template <int TC, int EPI, int TP, int WRN, bool TRANS = false>
+__device__ __forceinline__ void convg_epilogue_regs(const CgArgs& a, f32x4_t (&acc)[TC / WRN / 16][TP / (4 / WRN) / 16],
+                                                    dtf_acc_t (&acc_lds)[2][TC], int slot, int o0, int p0, int p1,
+                                                    int HWo = 0, int GW = 0, int py = 0, int px = 0) {
+  constexpr int PW = TP / (4 / WRN), NTP = PW / 16, MT = TC / WRN / 16;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave % WRN, wc = wave / WRN;
+  const int cb = wr * (TC / WRN) + 4 * (lane >> 4);  // tile channel of register 0, m-tile 0
+  long prow[NTP];
+#pragma unroll
+  for (int n = 0; n < NTP; ++n) {
+    const int p = p0 + wc * PW + 16 * n + (lane & 15);
+    long pf = p;
+    if constexpr (TRANS) {
+      const int img = p / HWo, rem = p - img * HWo, qy = rem / GW, qx = rem - qy * GW;
+      pf = ((long)img * a.Ho + 2 * qy + py) * a.Wo + 2 * qx + px;
+    }
+    prow[n] = p < p1 ? pf * a.Co : -1;
+  }
+  uint2 xr[(EPI & 2) ? MT : 1][(EPI & 2) ? NTP : 1];
+  uint2 rr[(EPI & 1) ? MT : 1][(EPI & 1) ? NTP : 1];
+  if constexpr ((EPI & 3) != 0) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < NTP; ++n) {
+        const int oc = o0 + cb + 16 * m;
+        const bool ok = prow[n] >= 0 && oc < a.Co;
+        if constexpr (EPI & 2) xr[m][n] = ld8(a.xm, prow[n] + oc, ok);
+        if constexpr (EPI & 1) rr[m][n] = ld8(a.res, prow[n] + oc, ok);
+      }
+  }
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int oc = o0 + cb + 16 * m;
+    const bool cok = oc < a.Co;
+    float esc[4], esh[4], emu[4], eiv[4];
+    if constexpr (EPI & 2) {
+      const float* ep = a.c_ep + (long)slot * 4 * a.cmax + (cok ? oc : 0);
+      const float4 u0 = *reinterpret_cast<const float4*>(ep);
+      const float4 u1 = *reinterpret_cast<const float4*>(ep + a.cmax);
+      const float4 u2 = *reinterpret_cast<const float4*>(ep + 2 * a.cmax);
+      const float4 u3 = *reinterpret_cast<const float4*>(ep + 3 * a.cmax);
+      esc[0] = u0.x; esc[1] = u0.y; esc[2] = u0.z; esc[3] = u0.w;
+      esh[0] = u1.x; esh[1] = u1.y; esh[2] = u1.z; esh[3] = u1.w;
+      emu[0] = u2.x; emu[1] = u2.y; emu[2] = u2.z; emu[3] = u2.w;
+      eiv[0] = u3.x; eiv[1] = u3.y; eiv[2] = u3.z; eiv[3] = u3.w;
+    }
+    float ss[4] = {0.f, 0.f, 0.f, 0.f}, sq[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int n = 0; n < NTP; ++n) {
+      const bool ok = prow[n] >= 0 && cok;
+      float v[4] = {acc[m][n][0], acc[m][n][1], acc[m][n][2], acc[m][n][3]};
+      float xv[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI & 1) {
+        const uint2 r2 = rr[m][n];
+        v[0] += lo2f(r2.x); v[1] += hi2f(r2.x); v[2] += lo2f(r2.y); v[3] += hi2f(r2.y);
+      }
+      if constexpr (EPI & 2) {
+        const uint2 x2 = xr[m][n];
+        xv[0] = lo2f(x2.x); xv[1] = hi2f(x2.x); xv[2] = lo2f(x2.y); xv[3] = hi2f(x2.y);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = (xv[i] * esc[i] + esh[i] > 0.f) ? v[i] : 0.f;
+      }
+      const uint32_t k0 = pack2bf(v[0], v[1]), k1 = pack2bf(v[2], v[3]);
+      if (ok) *reinterpret_cast<uint2*>(a.y + prow[n] + oc) = make_uint2(k0, k1);
+      if constexpr (EPI & 4) {
+        const float r[4] = {lo2f(k0), hi2f(k0), lo2f(k1), hi2f(k1)};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float ri = ok ? r[i] : 0.f;
+          ss[i] += ri;
+          if constexpr (EPI & 2)
+            sq[i] += ri * (xv[i] - emu[i]) * eiv[i];
+          else
+            sq[i] += ri * ri;
+        }
+      }
+    }
+    if constexpr (EPI & 4) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float s_ = ss[i], q_ = sq[i];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s_ += __shfl_xor(s_, o, 64);
+          q_ += __shfl_xor(q_, o, 64);
+        }
+        if ((lane & 15) == 0 && cok) {
+          constexpr int FX = (EPI & 2) ? DTF_FX_GRAD : DTF_FX_STAT;
+          dtf_acc_add(&acc_lds[0][cb + 16 * m + i], s_, FX, slot);
+          dtf_acc_add(&acc_lds[1][cb + 16 * m + i], q_, FX, slot);
+        }
+      }
+    }
+  }
+  if constexpr (EPI & 4) {
+    __syncthreads();
+    if (tid < TC && o0 + tid < a.Co) {
+      dtf_acc_t* st = a.st_out + (long)slot * 2 * a.cmax;
+      dtf_acc_addw(st + o0 + tid, acc_lds[0][tid]);
+      dtf_acc_addw(st + a.cmax + o0 + tid, acc_lds[1][tid]);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------- fwd / dgrad
 // MODE: 0 identity, 1 relu(x*s + t), 2 A*x + B*x2 + C.   EPI: bit0 residual, bit1 mask, bit2 stats (fwd: y, y^2;
 // with bit1: dz, dz*xhat).  TRANS: transposed (dgrad, stride > 1) gather.
@@ -293,6 +416,9 @@ __device__ __forceinline__ void convg_epilogue32(const CgArgs& a, f32x16_t (&acc
 // TC = 128 2 x 2 waves of 64 x 128 (32 MFMAs per wave and k-step; the epilogue is staged in 64-pixel quarters).
 // M32: v_mfma_f32_32x32x16_bf16 tiles (a wave's TC/WRN x PW block as 32 x 32 MFMA tiles: half the MFMA
 // instructions of the 16x16x32 form for the same fragment reads; plain-A (non-AKM) forward only)
+#ifndef CG_EPI_REGS
+#define CG_EPI_REGS 0  // generic kernel: register-direct epilogue (convg_epilogue_regs) for the 16x16 tiles
+#endif
 template <int TC, int MODE, int EPI, bool TRANS, bool AKM = false, int BK = 32, int TP = 128, bool M32 = false>
 __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   static_assert(TP == 128 || TP == 256, "pixel tile");
@@ -597,6 +723,8 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   if constexpr (M32)
     convg_epilogue32<TC, EPI, TRANS, TP, WRN, NHALF>(a, acc32, reinterpret_cast<float*>(smem_), acc_lds, slot, o0, p0,
                                                       p1, HWo, GW, py, px);
+  else if constexpr (CG_EPI_REGS)
+    convg_epilogue_regs<TC, EPI, TP, WRN, TRANS>(a, acc, acc_lds, slot, o0, p0, p1, HWo, GW, py, px);
   else
     convg_epilogue<TC, EPI, TRANS, TP, WRN, NHALF>(a, acc, reinterpret_cast<float*>(smem_), acc_lds, slot, o0, p0, p1,
                                                     HWo, GW, py, px);
@@ -624,9 +752,44 @@ __host__ __device__ constexpr int t3_nhalf() {
 #ifndef T3_DIRECT_A
 #define T3_DIRECT_A 1  // forward t3: A fragments loaded directly from the weight rows (no LDS staging of A)
 #endif
+#ifndef T3_EPI_REGS
+#define T3_EPI_REGS 0  // 1: register-direct epilogue (convg_epilogue_regs) instead of the LDS-staged one
+#endif
+#ifndef T3_EPI_LDS
+// epilogue staging budget (bf16 elements; 0: the operand buffers' size).  30000 (59 KB, still 2 workgroups per CU)
+// stages the 28 / 14-wide tiles in 2 parts instead of 7: data gradient 429 -> 404 us (28), 334 -> 316 us (14), the
+// forward unchanged (tools/t3_bench.py, profiles/r5_t3_epilogue.log)
+#define T3_EPI_LDS 30000
+#endif
 #ifndef T3_A_AHEAD
 #define T3_A_AHEAD 1  // ... that many k-steps ahead (2: a 3-set register ring, measured flat: profiles/r5_imagenet_stem_ahead_ab.log)
 #endif
+#ifndef DTF_STAMP
+#define DTF_STAMP 0
+#endif
+#if DTF_STAMP  // diagnostic build (tools/t3_bench.py --stamps): per-workgroup phase stamps of convg_t3_kernel
+#define T3_STAMP_WGS 8192
+__device__ unsigned long long dtf_t3_stamps[T3_STAMP_WGS][8];
+#define T3_STAMP_DECL unsigned long long st_[8] = {0};
+#define T3_STAMP(i) (st_[i] = __builtin_amdgcn_s_memrealtime())
+#define T3_STAMP_FLUSH()                                                                  \
+  do {                                                                                    \
+    __builtin_amdgcn_s_waitcnt(0);                                                        \
+    st_[4] = __builtin_amdgcn_s_memrealtime();                                            \
+    unsigned hw_, xcc_;                                                                   \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));                     \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));                   \
+    st_[5] = hw_;                                                                         \
+    st_[6] = xcc_;                                                                        \
+    if (threadIdx.x == 0 && blockIdx.x < T3_STAMP_WGS)                                    \
+      for (int i_ = 0; i_ < 8; ++i_) dtf_t3_stamps[blockIdx.x][i_] = st_[i_];              \
+  } while (0)
+#else
+#define T3_STAMP_DECL
+#define T3_STAMP(i) ((void)0)
+#define T3_STAMP_FLUSH() ((void)0)
+#endif
+
 // XF: the staged input rows get BN + ReLU (coefficients c_in: scale / shift of the input's BN) -- the folded forward
 template <int TC, int EPI, bool AKM, int W, int R, int TP, int WRN, bool XF = false>
 __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
@@ -646,13 +809,15 @@ __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
   constexpr int NBC = NBP * CPR, MAXB = (NBC + 255) / 256;
   constexpr int SBT = RT * WT * RP + 8;  // + slack for the inactive staging slots
   constexpr int SOPS = 2 * SA + SBT;
-  constexpr int NHALF = t3_nhalf<TP, TC, SOPS>();
+  constexpr int NHALF = t3_nhalf<TP, TC, (T3_EPI_LDS > SOPS ? T3_EPI_LDS : SOPS)>();
   static_assert(NHALF > 0, "epilogue staging split");
   constexpr int SEPI = 2 * TP * (TC + 4) / NHALF;
   __shared__ __attribute__((aligned(16))) bf16_t smem_[SOPS > SEPI ? SOPS : SEPI];
   __shared__ dtf_acc_t acc_lds[2][TC];
   bf16_t (*sa)[SA] = reinterpret_cast<bf16_t (*)[SA]>(smem_);
   bf16_t* sbt = smem_ + 2 * SA;
+  T3_STAMP_DECL
+  T3_STAMP(0);
   const int4 wk = a.work[blockIdx.x];
   DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z > wk.y && wk.z - wk.y <= R * W && a.Wi == W && a.Hi % R == 0);
   const int slot = wk.x, p0 = wk.y, p1 = wk.z, o0 = wk.w;
@@ -807,9 +972,13 @@ __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
         ++c;
       }
     }
-    __syncthreads();  // the epilogue reuses the operand LDS
-    convg_epilogue<TC, EPI, false, TP, WRN, NHALF>(a, acc, reinterpret_cast<float*>(smem_), acc_lds, slot, o0, p0,
-                                                   p1, 0, 0, 0, 0);
+    if constexpr (T3_EPI_REGS) {
+      convg_epilogue_regs<TC, EPI, TP, WRN>(a, acc, acc_lds, slot, o0, p0, p1);
+    } else {
+      __syncthreads();  // the epilogue reuses the operand LDS
+      convg_epilogue<TC, EPI, false, TP, WRN, NHALF>(a, acc, reinterpret_cast<float*>(smem_), acc_lds, slot, o0, p0,
+                                                     p1, 0, 0, 0, 0);
+    }
     return;
   }
   // A (weights) is prefetched one k-step ahead (a two-deep register ring, loop unrolled by two, measured the same:
@@ -820,6 +989,7 @@ __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
   store_b(rb);
   store_a(sa[0], ra);
   __syncthreads();
+  T3_STAMP(1);
   int c = 0, t = 0;
   for (int ks = 0; ks < nk; ++ks) {
     const bool more = ks + 1 < nk;
@@ -860,8 +1030,14 @@ __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
       ++c;
     }
   }
-  convg_epilogue<TC, EPI, false, TP, WRN, NHALF>(a, acc, reinterpret_cast<float*>(smem_), acc_lds, slot, o0, p0, p1,
-                                                 0, 0, 0, 0);
+  T3_STAMP(2);
+  if constexpr (T3_EPI_REGS)
+    convg_epilogue_regs<TC, EPI, TP, WRN>(a, acc, acc_lds, slot, o0, p0, p1);
+  else
+    convg_epilogue<TC, EPI, false, TP, WRN, NHALF>(a, acc, reinterpret_cast<float*>(smem_), acc_lds, slot, o0, p0,
+                                                   p1, 0, 0, 0, 0);
+  T3_STAMP(3);
+  T3_STAMP_FLUSH();
 }
 
 // ---------------------------------------------------------------------------------------------- wgrad
@@ -1634,6 +1810,17 @@ DTF_API int dtf_convg_fwd(const CgArgs* a, int tc, int mode, int epi, int trans,
 #undef CG_ALL_TC
 #undef CG_CASE
   return -1;
+}
+
+DTF_API int dtf_t3_stamp_read(void* dst, long bytes) {
+#if DTF_STAMP
+  if (bytes > (long)sizeof(dtf_t3_stamps)) bytes = sizeof(dtf_t3_stamps);
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(dtf_t3_stamps), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
+#else
+  (void)dst;
+  (void)bytes;
+  return -1;
+#endif
 }
 
 // Stride-1 3x3 conv / data gradient with LDS-resident input rows (convg_t3_kernel).  w: image width (56: 8-row

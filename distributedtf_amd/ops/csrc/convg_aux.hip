@@ -290,6 +290,74 @@ __global__ __launch_bounds__(256) void cg_bn_relu_apply_kernel(EwArgs a) {
   }
 }
 
+// Channel-fixed forms of the two apply kernels (C / 8 a power of two <= 256): thread t always owns the 16-byte
+// channel chunk t % (C / 8) and walks pixels, so its 8 channels' coefficients are loaded ONCE into registers instead
+// of with every data chunk (the chunk-walking kernels above issue 2-3 coefficient loads of 32 bytes per 16-byte data
+// load; at C >= 1024 they streamed at 3.9-4.1 TB/s: profiles/r5_imagenet_roofline_epi.txt).  A wave still covers
+// 64 consecutive chunks (1 KB contiguous: the pixel rows are contiguous).  grid (images, pixel splits).
+#ifndef CG_EW_CF
+#define CG_EW_CF 1
+#endif
+template <bool RELU_APPLY>
+__global__ __launch_bounds__(256) void cg_ew_apply_cf_kernel(EwArgs a) {
+  const int img = blockIdx.x;
+  const int slot = a.img_slot[img];
+  const float* co = a.coef + (long)slot * 4 * a.cmax;
+  const int cpp = a.C >> 3, ppi = 256 / cpp;  // chunks per pixel, pixels per workgroup pass
+  const int cc = threadIdx.x & (cpp - 1);
+  const long P = a.hw, pstep = (long)gridDim.y * ppi;
+  const long base = (long)img * P * a.C + 8 * cc;
+  float c0[8], c1[8], c2[8];
+  coef8(co + 8 * cc, c0);
+  coef8(co + a.cmax + 8 * cc, c1);
+  if constexpr (!RELU_APPLY) coef8(co + 2 * a.cmax + 8 * cc, c2);
+  const bf16_t* __restrict__ h = a.h + base;
+  const bf16_t* __restrict__ dz = RELU_APPLY ? nullptr : a.dz + base;
+  const bf16_t* __restrict__ add = (!RELU_APPLY && a.add) ? a.add + base : nullptr;
+  bf16_t* __restrict__ out = a.out + base;
+  for (long p = (long)blockIdx.y * ppi + threadIdx.x / cpp; p < P; p += EW_U * pstep) {
+    uint4 hv[EW_U], dv[EW_U], av[EW_U];
+#pragma unroll
+    for (int u = 0; u < EW_U; ++u) {
+      const long pp = p + u * pstep;
+      hv[u] = dv[u] = av[u] = make_uint4(0, 0, 0, 0);
+      if (pp < P) {
+        hv[u] = *reinterpret_cast<const uint4*>(h + pp * a.C);
+        if constexpr (!RELU_APPLY) {
+          dv[u] = *reinterpret_cast<const uint4*>(dz + pp * a.C);
+          if (add) av[u] = *reinterpret_cast<const uint4*>(add + pp * a.C);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < EW_U; ++u) {
+      const long pp = p + u * pstep;
+      if (pp >= P) break;
+      const uint32_t h32[4] = {hv[u].x, hv[u].y, hv[u].z, hv[u].w}, d32[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w},
+                     a32[4] = {av[u].x, av[u].y, av[u].z, av[u].w};
+      uint32_t r[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float v0, v1;
+        if constexpr (RELU_APPLY) {
+          v0 = fmaxf(lo2f(h32[q]) * c0[2 * q] + c1[2 * q], 0.f);
+          v1 = fmaxf(hi2f(h32[q]) * c0[2 * q + 1] + c1[2 * q + 1], 0.f);
+        } else {
+          v0 = c0[2 * q] * lo2f(d32[q]) + c1[2 * q] * lo2f(h32[q]) + c2[2 * q] + lo2f(a32[q]);
+          v1 = c0[2 * q + 1] * hi2f(d32[q]) + c1[2 * q + 1] * hi2f(h32[q]) + c2[2 * q + 1] + hi2f(a32[q]);
+        }
+        r[q] = pack2bf(v0, v1);
+      }
+      *reinterpret_cast<uint4*>(out + pp * a.C) = make_uint4(r[0], r[1], r[2], r[3]);
+    }
+  }
+}
+
+__device__ __host__ inline bool ew_cf_ok(int C) {
+  const int cpp = C >> 3;
+  return CG_EW_CF && (C & 7) == 0 && cpp >= 1 && cpp <= 256 && (cpp & (cpp - 1)) == 0;
+}
+
 __global__ __launch_bounds__(256) void cg_prep_input_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
                                                              long npix, int c_in) {
   const long stride = (long)gridDim.x * blockDim.x;
@@ -923,6 +991,12 @@ DTF_API int dtf_cg_bn_bwd_apply(const EwArgs* a, hipStream_t stream) {
   const long ms = (n8 + 255) / 256;
   if (split > ms) split = ms;
   if (split < 1) split = 1;
+  if (ew_cf_ok(a->C)) {
+    const long ppi = 256 / (a->C >> 3), mp = (a->hw + ppi - 1) / ppi;  // at most one pass of pixels per thread row
+    const long sp = split < mp ? split : mp;
+    hipLaunchKernelGGL(cg_ew_apply_cf_kernel<false>, dim3((unsigned)a->nimg, (unsigned)sp), dim3(256), 0, stream, *a);
+    return DTF_CHECK_LAUNCH();
+  }
   hipLaunchKernelGGL(cg_bn_bwd_apply_kernel<false>, dim3((unsigned)a->nimg, (unsigned)split), dim3(256), 0, stream, *a);
   return DTF_CHECK_LAUNCH();
 }
@@ -934,6 +1008,12 @@ DTF_API int dtf_cg_bn_relu_apply(const EwArgs* a, hipStream_t stream) {
   const long ms = (n8 + 255) / 256;
   if (split > ms) split = ms;
   if (split < 1) split = 1;
+  if (ew_cf_ok(a->C)) {
+    const long ppi = 256 / (a->C >> 3), mp = (a->hw + ppi - 1) / ppi;  // at most one pass of pixels per thread row
+    const long sp = split < mp ? split : mp;
+    hipLaunchKernelGGL(cg_ew_apply_cf_kernel<true>, dim3((unsigned)a->nimg, (unsigned)sp), dim3(256), 0, stream, *a);
+    return DTF_CHECK_LAUNCH();
+  }
   hipLaunchKernelGGL(cg_bn_relu_apply_kernel<false>, dim3((unsigned)a->nimg, (unsigned)split), dim3(256), 0, stream, *a);
   return DTF_CHECK_LAUNCH();
 }

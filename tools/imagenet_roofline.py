@@ -78,6 +78,8 @@ def kernel_family(k: str):
         return "conv dgrad" if k.split(",")[4].strip().startswith("true") else "conv fwd"
     if "convg_t3_kernel" in k:  # <TC, EPI, AKM, ...>: AKM = data gradient
         return "conv dgrad" if k.split(",")[2].strip().startswith("true") else "conv fwd"
+    if "cg_ew_apply_cf_kernel" in k:  # <RELU_APPLY>: the channel-fixed apply kernels
+        return "bn_relu_apply" if "<true>" in k else "bn_bwd_apply"
     for pre, f in KERNEL_FAMILY:
         if pre in k:
             return f

@@ -38,6 +38,22 @@ __device__ __forceinline__ s16x4_t ds_read_tr(const bf16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p));
 }
 
+// k-major operand tiles read with ds_read_b64_tr_b16 (weight gradients): lane (g = lane >> 4, q = (lane & 15) >> 2)
+// reads k rows 8g + q and 8g + 4 + q.  With a row pitch of 4 (mod 64) dwords, rows r and r + 1 overlap in 4 of
+// their 8 banks and rows 8 apart coincide: every read 2-way (4 cycles per instruction instead of 2; PMC: 5.8k bank
+// conflict cycles per wave in convg_wgrad_wide_kernel).  The k order inside a 32-deep tile is free as long as both
+// operands use the same one, so tile row kperm(k) holds k: the 8 rows a 32-lane half reads (k 8g + {0..3},
+// 8g + 8 + {0..3}, or their +4 partners) land on 8 even (or odd) rows, whose segments tile the 64 banks for the
+// pitches used here (4 or 20 mod 64 dwords; tools/lds_banks.py).  Reads: rows 8g + 2q (k 8g + q) and 8g + 2q + 1.
+#ifndef CG_WG_KPERM
+#define CG_WG_KPERM 1
+#endif
+__device__ __forceinline__ int kperm(int k) {
+  return CG_WG_KPERM ? ((k & ~7) | ((k & 3) << 1) | ((k >> 2) & 1)) : k;
+}
+__device__ __forceinline__ int ktr_lo(int g, int q) { return CG_WG_KPERM ? 8 * g + 2 * q : 8 * g + q; }
+__device__ __forceinline__ int ktr_hi(int g, int q) { return CG_WG_KPERM ? 8 * g + 2 * q + 1 : 8 * g + 4 + q; }
+
 // Branch-free predicated 16-byte load: a masked-off lane reads a zero vector in global memory.  A conditional load
 // makes hipcc branch around it and wait vmcnt(0) per element, which serialises a thread's gathers (PMC before
 // the change: 5-12 VALU per MFMA in these kernels).
@@ -629,7 +645,7 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
 #pragma unroll
     for (int j = 0; j < AJ; ++j) {
       if constexpr (AKM)
-        *reinterpret_cast<uint4*>(dst + (tid / ACH + (256 / ACH) * j) * KPA + 8 * (tid % ACH)) = v[j];
+        *reinterpret_cast<uint4*>(dst + kperm(tid / ACH + (256 / ACH) * j) * KPA + 8 * (tid % ACH)) = v[j];
       else
         *reinterpret_cast<uint4*>(dst + (rB + RPT * j) * RP + 8 * cB) = v[j];
     }
@@ -697,8 +713,8 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
         if constexpr (AKM) {
           const int g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
           const int rb_ = wr * (TC / WRN) + 16 * m + 4 * p4;
-          const s16x4_t lo = ds_read_tr(sa[cur] + (32 * kk + 8 * g + q) * KPA + rb_);
-          const s16x4_t hi = ds_read_tr(sa[cur] + (32 * kk + 8 * g + 4 + q) * KPA + rb_);
+          const s16x4_t lo = ds_read_tr(sa[cur] + (32 * kk + ktr_lo(g, q)) * KPA + rb_);
+          const s16x4_t hi = ds_read_tr(sa[cur] + (32 * kk + ktr_hi(g, q)) * KPA + rb_);
           fa[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         } else {
           fa[m] = *reinterpret_cast<const bf16x8_t*>(sa[cur] + (wr * (TC / WRN) + 16 * m + (lane & 15)) * RP +
@@ -897,7 +913,7 @@ __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
 #pragma unroll
     for (int j = 0; j < AJ; ++j) {
       if constexpr (AKM)
-        *reinterpret_cast<uint4*>(dst + (tid / ACH + (256 / ACH) * j) * KPA + 8 * (tid % ACH)) = v[j];
+        *reinterpret_cast<uint4*>(dst + kperm(tid / ACH + (256 / ACH) * j) * KPA + 8 * (tid % ACH)) = v[j];
       else
         *reinterpret_cast<uint4*>(dst + (rB + RPT * j) * RP + 8 * cB) = v[j];
     }
@@ -1003,8 +1019,8 @@ __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
       if constexpr (AKM) {
         const int g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
         const int rb_ = wr * (TC / WRN) + 16 * m + 4 * p4;
-        const s16x4_t lo = ds_read_tr(sa_cur + (8 * g + q) * KPA + rb_);
-        const s16x4_t hi = ds_read_tr(sa_cur + (8 * g + 4 + q) * KPA + rb_);
+        const s16x4_t lo = ds_read_tr(sa_cur + ktr_lo(g, q) * KPA + rb_);
+        const s16x4_t hi = ds_read_tr(sa_cur + ktr_hi(g, q) * KPA + rb_);
         fa[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       } else {
         fa[m] = *reinterpret_cast<const bf16x8_t*>(sa_cur + (wr * (TC / WRN) + 16 * m + (lane & 15)) * RP +
@@ -1163,7 +1179,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PK == 32 ? 
         }
         t = make_uint4(w32[0], w32[1], w32[2], w32[3]);
       }
-      *reinterpret_cast<uint4*>(d + (kr + 16 * j) * KP + 8 * cc) = t;
+      *reinterpret_cast<uint4*>(d + kperm(kr + 16 * j) * KP + 8 * cc) = t;
       uint4 u = xv[j];
       if (MODE_X == 1 && ((okm >> (NJ + j)) & 1u)) {
         uint32_t w32[4] = {u.x, u.y, u.z, u.w};
@@ -1175,7 +1191,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PK == 32 ? 
         }
         u = make_uint4(w32[0], w32[1], w32[2], w32[3]);
       }
-      *reinterpret_cast<uint4*>(xx + (kr + 16 * j) * KP + 8 * cc) = u;
+      *reinterpret_cast<uint4*>(xx + kperm(kr + 16 * j) * KP + 8 * cc) = u;
     }
   };
   f32x4_t acc[4][NTN];
@@ -1207,15 +1223,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PK == 32 ? 
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const int cb = wr * 64 + 16 * m + 4 * p4;
-        const s16x4_t lo = ds_read_tr(sd[cur] + (32 * kk + 8 * g + q) * KP + cb);
-        const s16x4_t hi = ds_read_tr(sd[cur] + (32 * kk + 8 * g + 4 + q) * KP + cb);
+        const s16x4_t lo = ds_read_tr(sd[cur] + (32 * kk + ktr_lo(g, q)) * KP + cb);
+        const s16x4_t hi = ds_read_tr(sd[cur] + (32 * kk + ktr_hi(g, q)) * KP + cb);
         fa[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll
       for (int n = 0; n < NTN; ++n) {
         const int cb = wc * CWW + 16 * n + 4 * p4;
-        const s16x4_t lo = ds_read_tr(sx[cur] + (32 * kk + 8 * g + q) * KP + cb);
-        const s16x4_t hi = ds_read_tr(sx[cur] + (32 * kk + 8 * g + 4 + q) * KP + cb);
+        const s16x4_t lo = ds_read_tr(sx[cur] + (32 * kk + ktr_lo(g, q)) * KP + cb);
+        const s16x4_t hi = ds_read_tr(sx[cur] + (32 * kk + ktr_hi(g, q)) * KP + cb);
         fb[n] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll
@@ -1306,7 +1322,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ?
     xrow[j] = r;
     xky[j] = tap / a.kw;
     xkx[j] = tap - xky[j] * a.kw;
-    xoff[j] = r * WWP + 8 * ch;  // LDS element offset in the k-step tile
+    xoff[j] = kperm(r & 31) * WWP + 8 * ch;  // LDS element offset in the k-step tile (tile row kperm(pixel))
     xok[j] = c < WXC && col < K;
     xoff[j] += ci << 16;         // ci in the high half (unpacked at use)
   }
@@ -1355,7 +1371,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ?
   };
   auto store = [&](bf16_t* d, bf16_t* xx, const uint4 (&dv)[DJ], const uint4 (&xv)[WXJ]) {
 #pragma unroll
-    for (int j = 0; j < DJ; ++j) *reinterpret_cast<uint4*>(d + drow[j] * WWOP + dch[j]) = dv[j];
+    for (int j = 0; j < DJ; ++j) *reinterpret_cast<uint4*>(d + kperm(drow[j]) * WWOP + dch[j]) = dv[j];
 #pragma unroll
     for (int j = 0; j < WXJ; ++j) {
       if (tid + 256 * j >= WXC) continue;
@@ -1398,15 +1414,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ?
 #pragma unroll
     for (int m = 0; m < MTW; ++m) {
       const int cb = wr * (WWO / 2) + 16 * m + 4 * p4;
-      const s16x4_t lo = ds_read_tr(sd[cur] + (8 * g + q) * WWOP + cb);
-      const s16x4_t hi = ds_read_tr(sd[cur] + (8 * g + 4 + q) * WWOP + cb);
+      const s16x4_t lo = ds_read_tr(sd[cur] + ktr_lo(g, q) * WWOP + cb);
+      const s16x4_t hi = ds_read_tr(sd[cur] + ktr_hi(g, q) * WWOP + cb);
       fa[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     }
 #pragma unroll
     for (int n = 0; n < NTN; ++n) {
       const int cb = wc * (WWT / 2) + 16 * n + 4 * p4;
-      const s16x4_t lo = ds_read_tr(sx[cur] + (8 * g + q) * WWP + cb);
-      const s16x4_t hi = ds_read_tr(sx[cur] + (8 * g + 4 + q) * WWP + cb);
+      const s16x4_t lo = ds_read_tr(sx[cur] + ktr_lo(g, q) * WWP + cb);
+      const s16x4_t hi = ds_read_tr(sx[cur] + ktr_hi(g, q) * WWP + cb);
       const bf16x8_t fb = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
       for (int m = 0; m < MTW; ++m) acc[m][n] = mfma16(fa[m], fb, acc[m][n]);
@@ -1565,7 +1581,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     if (more) load(b + 1);
 #pragma unroll 1
     for (int ks = 0; ks < NKS; ++ks) {
-      const int pa = ks * 32 + 8 * g + q, pb = pa + 4;  // this lane's two k-rows (band pixels)
+      // this lane's two k-rows (band pixels); kperm order: the 8 pixels a 32-lane half reads are 2 apart, which
+      // spreads both the dY rows and the halo pixels over distinct banks
+      const int pa = ks * 32 + ktr_lo(g, q), pb = ks * 32 + ktr_hi(g, q);
       bf16x8_t fa[MTW];
 #pragma unroll
       for (int m = 0; m < MTW; ++m) {

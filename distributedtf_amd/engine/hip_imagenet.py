@@ -41,7 +41,7 @@ _CG_WIDE = True  # wide-column 3x3 weight-gradient tiles
 _CG_WIDE128 = True
 _CG_WIDE7 = True  # one 64 x 416 tile for the 7x7 stem
 _CG_WIDE1 = True  # the wide tiles for 1x1 convs with Ci % 256 == 0
-_CG_TP256_128 = True  # 128 x 256 tiles (2 x 2 waves of 64 x 128)
+_CG_TP256_128 = os.environ.get("DTF_CG_TP256_128", "1") == "1"  # 128 x 256 tiles (2 x 2 waves of 64 x 128)
 _CG_TP256 = True  # 256-pixel forward / dgrad tiles for 64-channel outputs
 # v_mfma_f32_32x32x16_bf16 tiles for the plain-A forward convolutions with 128-channel tiles (1x1 / strided / 7x7-stage
 # convs with C_out >= 128): 32 x 32 MFMA tiles of each wave's 64 x 128 block (convg_fwd_kernel M32)
@@ -74,7 +74,7 @@ CG_FOLD2 = os.environ.get("DTF_CG_FOLD2", "0") == "1"  # measured +2.7 ms: profi
 # 76.7 (0) -> 75.0 (1) -> 73.8 ms (2) (profiles/r5_xcd_order_ab.log)
 _CG_XCD = int(os.environ.get("DTF_CG_XCD", "2"))
 T3_FLAGS = int(os.environ.get("DTF_T3_FLAGS", "1"))  # direct: 81.61 vs staged 80.92 ms (profiles/r4_imagenet_t3_ab.log)
-_CG_WG_TARGET = 512
+_CG_WG_TARGET = int(os.environ.get("DTF_CG_WG_TARGET", "512"))
 _CG_WG_MINCHUNK = 2048
 
 

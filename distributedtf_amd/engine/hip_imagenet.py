@@ -73,6 +73,8 @@ CG_FOLD2 = os.environ.get("DTF_CG_FOLD2", "0") == "1"  # measured +2.7 ms: profi
 # on its own XCD when the population is a multiple of 8 with equal work per member.  ResNet-50 pop 8 x 128:
 # 76.7 (0) -> 75.0 (1) -> 73.8 ms (2) (profiles/r5_xcd_order_ab.log)
 _CG_XCD = int(os.environ.get("DTF_CG_XCD", "2"))
+# generic forward / dgrad launches with fewer 256-pixel workgroups than this take 128-pixel tiles (conv())
+_CG_SMALL = int(os.environ.get("DTF_CG_SMALL", "0"))
 T3_FLAGS = int(os.environ.get("DTF_T3_FLAGS", "1"))  # direct: 81.61 vs staged 80.92 ms (profiles/r4_imagenet_t3_ab.log)
 _CG_WG_TARGET = int(os.environ.get("DTF_CG_WG_TARGET", "512"))
 _CG_WG_MINCHUNK = 2048
@@ -611,7 +613,12 @@ class _ImageNetPlan:
         # (a 256-row tile, 128 x 64 per wave, measured slower: 111.7 -> 123.4 ms/step at pop 8 x 128,
         # profiles/r2_imagenet_tc256_ab.log -- removed)
         tp = 128
-        if (tc == 64 and _CG_TP256) or (tc == 128 and _CG_TP256_128):
+        # small launches (one member's 14x14 / 7x7 layers: 100-200 workgroups of 256 pixels on 256 CUs) take the
+        # 128-pixel tiles -- twice the workgroups
+        grid_px = (hw_in * hw_in) if trans & 1 else (hw_out * hw_out)
+        n256 = -(-(self.N * grid_px * (4 if trans & 1 else 1)) // 256) * -(-a.Co // tc)
+        small = n256 < _CG_SMALL
+        if not small and ((tc == 64 and _CG_TP256) or (tc == 128 and _CG_TP256_128)):
             trans |= 8  # 256-pixel tiles (BK = 32): 1 x 4 waves of 64 x 64, or 2 x 2 of 64 x 128 for tc 128
             tp = 256
             if _CG_M32 and tc == 128 and not dgrad:

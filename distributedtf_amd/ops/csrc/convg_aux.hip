@@ -381,9 +381,18 @@ __global__ __launch_bounds__(256) void cg_prep_input_s2d_kernel(const float* __r
     float v[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = 0.f;
-    for (int q = 0; q < 4; ++q) {
-      const float* src = x + ((img * H + 2 * by + (q >> 1)) * W + 2 * bx + (q & 1)) * c_in;
-      for (int c = 0; c < c_in; ++c) v[q * c_in + c] = src[c];
+    if (c_in == 3) {  // the image case: per input row the block's 2 pixels are 6 contiguous floats (3 x 8-byte loads)
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const float2* src = reinterpret_cast<const float2*>(x + ((img * H + 2 * by + r) * W + 2 * bx) * 3);
+        const float2 a = src[0], b = src[1], c = src[2];
+        v[6 * r] = a.x; v[6 * r + 1] = a.y; v[6 * r + 2] = b.x; v[6 * r + 3] = b.y; v[6 * r + 4] = c.x; v[6 * r + 5] = c.y;
+      }
+    } else {
+      for (int q = 0; q < 4; ++q) {
+        const float* src = x + ((img * H + 2 * by + (q >> 1)) * W + 2 * bx + (q & 1)) * c_in;
+        for (int c = 0; c < c_in; ++c) v[q * c_in + c] = src[c];
+      }
     }
     uint4* dst = reinterpret_cast<uint4*>(y + b * 16);
     dst[0] = make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
@@ -770,6 +779,58 @@ __global__ __launch_bounds__(256) void cg_bn_add_relu_kernel(BnAddArgs a) {
   }
 }
 
+// Channel-fixed form (the layout of cg_ew_apply_cf_kernel): the 4 coefficient vectors of the thread's 8 channels are
+// loaded once instead of 4 x 32 bytes per 16-byte data chunk
+__global__ __launch_bounds__(256) void cg_bn_add_relu_cf_kernel(BnAddArgs a) {
+  const int img = blockIdx.x;
+  const int slot = a.img_slot[img];
+  const int cpp = a.C >> 3, ppi = 256 / cpp;
+  const int cc = threadIdx.x & (cpp - 1);
+  const long P = a.hw, pstep = (long)gridDim.y * ppi;
+  const float* ch = a.coef_h + (long)slot * 4 * a.cmax + 8 * cc;
+  float sc[8], sh[8], ps[8], pt[8];
+  coef8(ch, sc);
+  coef8(ch + a.cmax, sh);
+  if (a.coef_s) {
+    const float* cs = a.coef_s + (long)slot * 4 * a.cmax + 8 * cc;
+    coef8(cs, ps);
+    coef8(cs + a.cmax, pt);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ps[k] = 1.f, pt[k] = 0.f;
+  }
+  const long base = (long)img * P * a.C + 8 * cc;
+  const bf16_t* __restrict__ h = a.h + base;
+  const bf16_t* __restrict__ s = a.s + base;
+  bf16_t* __restrict__ out = a.out + base;
+  for (long p = (long)blockIdx.y * ppi + threadIdx.x / cpp; p < P; p += EW_U * pstep) {
+    uint4 hv[EW_U], sv[EW_U];
+#pragma unroll
+    for (int u = 0; u < EW_U; ++u) {
+      const long pp = p + u * pstep;
+      hv[u] = sv[u] = make_uint4(0, 0, 0, 0);
+      if (pp < P) {
+        hv[u] = *reinterpret_cast<const uint4*>(h + pp * a.C);
+        sv[u] = *reinterpret_cast<const uint4*>(s + pp * a.C);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < EW_U; ++u) {
+      const long pp = p + u * pstep;
+      if (pp >= P) break;
+      const uint32_t h32[4] = {hv[u].x, hv[u].y, hv[u].z, hv[u].w}, s32[4] = {sv[u].x, sv[u].y, sv[u].z, sv[u].w};
+      uint32_t r[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float v0 = lo2f(h32[q]) * sc[2 * q] + sh[2 * q] + lo2f(s32[q]) * ps[2 * q] + pt[2 * q];
+        const float v1 = hi2f(h32[q]) * sc[2 * q + 1] + sh[2 * q + 1] + hi2f(s32[q]) * ps[2 * q + 1] + pt[2 * q + 1];
+        r[q] = pack2bf(fmaxf(v0, 0.f), fmaxf(v1, 0.f));
+      }
+      *reinterpret_cast<uint4*>(out + pp * a.C) = make_uint4(r[0], r[1], r[2], r[3]);
+    }
+  }
+}
+
 // BN-backward sums of post-activation BNs whose output gradient dz is already ReLU-masked (v1: the block output's
 // mask is applied by the consumer's data-gradient epilogue): sum dz and sum dz * xhat into [cap][2][cmax], for
 // the BN of h and optionally a second BN of h2 that received the same dz (v1 projection BN of the shortcut).
@@ -933,6 +994,12 @@ DTF_API int dtf_cg_bn_add_relu(const BnAddArgs* a, hipStream_t stream) {
   const long ms = (n8 + 255) / 256;
   if (split > ms) split = ms;
   if (split < 1) split = 1;
+  if (ew_cf_ok(a->C)) {
+    const long ppi = 256 / (a->C >> 3), mp = (a->hw + ppi - 1) / ppi;
+    const long sp = split < mp ? split : mp;
+    hipLaunchKernelGGL(cg_bn_add_relu_cf_kernel, dim3((unsigned)a->nimg, (unsigned)sp), dim3(256), 0, stream, *a);
+    return DTF_CHECK_LAUNCH();
+  }
   hipLaunchKernelGGL(cg_bn_add_relu_kernel, dim3((unsigned)a->nimg, (unsigned)split), dim3(256), 0, stream, *a);
   return DTF_CHECK_LAUNCH();
 }

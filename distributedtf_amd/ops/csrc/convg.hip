@@ -1638,6 +1638,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 }
 
 // ------------------------------------------------------------------------------------ s2d stem forward
+#ifndef STEM_LDS_OUT
+#define STEM_LDS_OUT 1
+#endif
 // The space-to-depth stem (4x4/1 over 2x2 blocks of the image, 16 channels, pad 2 before / 1 after, Co = 64) from
 // LDS-resident row bands: a workgroup keeps the whole 64 x 256 weight tile in registers (wave w: output channels
 // 16 w .. 16 w + 15, 8 k-steps of 2 taps x 16 channels), stages a band of R output rows' input halo
@@ -1652,6 +1655,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   constexpr int CP = CI + 8, WS = W + KT - 1, RT = R + KT - 1;
   constexpr int XCH = RT * WS * (CI / 8), XJ = (XCH + 255) / 256;
   __shared__ __attribute__((aligned(16))) bf16_t sx[RT * WS * CP + 8];
+  // STEM_LDS_OUT: the band's outputs are staged as [pixel][64 + 8] rows and stored as whole 128-byte pixel rows
+  // (each wave's fragments are 4-channel / 8-byte pieces, 32 bytes per pixel -- partial lines)
+  constexpr int OP = CO + 8;
+  __shared__ __attribute__((aligned(16))) bf16_t so[STEM_LDS_OUT ? NPT * 16 * OP : 8];
   __shared__ dtf_acc_t acc_lds[2][CO];
   const int4 wk = a.work[blockIdx.x];
   DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z > wk.y && a.Wi == W && a.Wo == W && a.Ci == CI && a.Co == CO &&
@@ -1727,7 +1734,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       // D: lane holds channels co0 .. co0 + 3 of pixel 16 n + (lane & 15)
       const uint32_t lo = pack2bf(acc[0], acc[1]), hi = pack2bf(acc[2], acc[3]);
       if (p < NPV) {
-        *reinterpret_cast<uint2*>(yb + (long)p * CO) = make_uint2(lo, hi);
+        if constexpr (STEM_LDS_OUT)
+          *reinterpret_cast<uint2*>(so + p * OP + co0) = make_uint2(lo, hi);
+        else
+          *reinterpret_cast<uint2*>(yb + (long)p * CO) = make_uint2(lo, hi);
         if constexpr (EPI & 4) {
           const float r[4] = {lo2f(lo), hi2f(lo), lo2f(hi), hi2f(hi)};
 #pragma unroll
@@ -1739,6 +1749,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       }
     }
     __syncthreads();
+    if constexpr (STEM_LDS_OUT) {  // whole pixel rows: chunk q = tid + 256 j -> pixel q / 8, channels 8 (q % 8)
+      bf16_t* yrow = a.y + (((long)img * H + y0) * W) * CO;
+#pragma unroll
+      for (int j = 0; j < (NPV * 8 + 255) / 256; ++j) {
+        const int q = tid + 256 * j, px = q >> 3, c8 = 8 * (q & 7);
+        if (px < NPV)
+          *reinterpret_cast<uint4*>(yrow + (long)px * CO + c8) = *reinterpret_cast<const uint4*>(so + px * OP + c8);
+      }
+    }
     if (more) {
       store();
       __syncthreads();

@@ -75,6 +75,9 @@ CG_FOLD2 = os.environ.get("DTF_CG_FOLD2", "0") == "1"  # measured +2.7 ms: profi
 _CG_XCD = int(os.environ.get("DTF_CG_XCD", "2"))
 # generic forward / dgrad launches with fewer 256-pixel workgroups than this take 128-pixel tiles (conv())
 _CG_SMALL = int(os.environ.get("DTF_CG_SMALL", "0"))
+# ... and so do the 1x1 launches whose GEMM depth (Ci of the gathered operand) is at most this (memory-bound: more,
+# smaller workgroups in flight)
+_CG_SHORTK = int(os.environ.get("DTF_CG_SHORTK", "0"))
 T3_FLAGS = int(os.environ.get("DTF_T3_FLAGS", "1"))  # direct: 81.61 vs staged 80.92 ms (profiles/r4_imagenet_t3_ab.log)
 _CG_WG_TARGET = int(os.environ.get("DTF_CG_WG_TARGET", "512"))
 _CG_WG_MINCHUNK = 2048
@@ -617,7 +620,7 @@ class _ImageNetPlan:
         # 128-pixel tiles -- twice the workgroups
         grid_px = (hw_in * hw_in) if trans & 1 else (hw_out * hw_out)
         n256 = -(-(self.N * grid_px * (4 if trans & 1 else 1)) // 256) * -(-a.Co // tc)
-        small = n256 < _CG_SMALL
+        small = n256 < _CG_SMALL or (k == 1 and a.Ci <= _CG_SHORTK)
         if not small and ((tc == 64 and _CG_TP256) or (tc == 128 and _CG_TP256_128)):
             trans |= 8  # 256-pixel tiles (BK = 32): 1 x 4 waves of 64 x 64, or 2 x 2 of 64 x 128 for tc 128
             tp = 256

@@ -80,7 +80,8 @@ _CG_SMALL = int(os.environ.get("DTF_CG_SMALL", "0"))
 _CG_SHORTK = int(os.environ.get("DTF_CG_SHORTK", "0"))
 T3_FLAGS = int(os.environ.get("DTF_T3_FLAGS", "1"))  # direct: 81.61 vs staged 80.92 ms (profiles/r4_imagenet_t3_ab.log)
 _CG_WG_TARGET = int(os.environ.get("DTF_CG_WG_TARGET", "512"))
-_CG_WG_MINCHUNK = 2048
+_CG_WG_MINCHUNK = int(os.environ.get("DTF_CG_WG_MINCHUNK", "2048"))
+_CG_WG_BALANCED = os.environ.get("DTF_CG_WG_BALANCED", "0") == "1"
 
 
 class CgArgs(ctypes.Structure):
@@ -522,8 +523,12 @@ class _ImageNetPlan:
         for s, n in zip(self.slots, self.sizes):
             f = self.first[s]
             p_beg, p_end = f * hw_out * hw_out, (f + n) * hw_out * hw_out
-            chunk = max(_CG_WG_MINCHUNK, -(-(p_end - p_beg) // per_member))
-            chunk = (chunk + 63) // 64 * 64
+            if _CG_WG_BALANCED:  # equal splits (the rounded chunk could leave a short last one)
+                nsplit = max(1, min(per_member, (p_end - p_beg) // _CG_WG_MINCHUNK))
+                chunk = (-(-(p_end - p_beg) // nsplit) + 63) // 64 * 64
+            else:
+                chunk = max(_CG_WG_MINCHUNK, -(-(p_end - p_beg) // per_member))
+                chunk = (chunk + 63) // 64 * 64
             for p0 in range(p_beg, p_end, chunk):
                 for o0 in range(0, co, wo):
                     for n0 in range(0, K, wt):

@@ -111,6 +111,12 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
+def _xcd_order(items, ng):
+    """XCD-aware work order (engine/hip_imagenet.py xcd_order; DTF_CG_XCD)."""
+    from .hip_imagenet import xcd_order
+    return xcd_order(items, ng)
+
+
 def _log2(n):
     assert n > 0 and n & (n - 1) == 0, n
     return n.bit_length() - 1
@@ -368,6 +374,7 @@ class _F32Plan:
             for p0 in range(f * hwo, (f + n) * hwo, tp):
                 for o0 in range(0, a.Co, tc):
                     items.append([s, p0, min(p0 + tp, (f + n) * hwo), o0])
+        items = _xcd_order(items, -(-a.Co // tc))
         work = self._hold(torch.tensor(items, dtype=torch.int32, device=self.be.dev))
         a.work = _p(work)
         self._hold(a)
@@ -388,6 +395,7 @@ class _F32Plan:
             for b0 in range(f * bpi, (f + n) * bpi, chunk):
                 for t in tiles:
                     items.append([s, b0, min(b0 + chunk, (f + n) * bpi), t])
+        items = _xcd_order(items, len(tiles))
         work = self._hold(torch.tensor(items, dtype=torch.int32, device=self.be.dev))
         a.work = _p(work)
         self._hold(a)
@@ -425,6 +433,7 @@ class _F32Plan:
                 for o0 in range(0, c.cout, tc):
                     for n0 in range(0, K, 64):
                         items.append([s, p0, min(p0 + WG_CHUNK, (f + n) * hwo), o0 | ((n0 // 16) << 16)])
+        items = _xcd_order(items, -(-c.cout // tc) * -(-K // 64))
         work = self._hold(torch.tensor(items, dtype=torch.int32, device=self.be.dev))
         a.work = _p(work)
         self._hold(a)

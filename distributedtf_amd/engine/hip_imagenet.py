@@ -129,6 +129,37 @@ class BnSumArgs(ctypes.Structure):
 _REGISTERED = False
 
 
+def xcd_order(items, ng):
+    """XCD-aware dispatch order: consecutive runs of ``ng`` items share an operand tile (the co-tiles of one
+    pixel tile; the dW tiles of one pixel chunk).  Workgroup k runs on XCD k % 8, each XCD with its own L2, so
+    the run is spread over positions 8 apart -- every item of a run lands on the same XCD, dispatched close in
+    time, and the shared tile is fetched into one L2 instead of ng of them."""
+    if not _CG_XCD:
+        return items
+    # items are member-major (slot order); with a multiple of 8 members of equal work, member m's items all go
+    # to XCD m % 8 (its weights and activations then live in one L2; positions 8 apart, runs kept adjacent)
+    nm = len(items) and len({it[0] for it in items})
+    if _CG_XCD >= 2 and nm and nm % 8 == 0 and len(items) % nm == 0:
+        per = len(items) // nm
+        mem = [items[m * per:(m + 1) * per] for m in range(nm)]
+        if all(len({it[0] for it in blk}) == 1 for blk in mem):
+            out = []
+            for g8 in range(0, nm, 8):
+                grp = mem[g8:g8 + 8]
+                for j in range(per):
+                    out.extend(blk[j] for blk in grp)
+            return out
+    if ng <= 1 or len(items) % ng:
+        return items
+    runs = [items[i:i + ng] for i in range(0, len(items), ng)]
+    out = []
+    for b in range(0, len(runs), 8):
+        blk = runs[b:b + 8]
+        for c in range(ng):
+            out.extend(r[c] for r in blk)
+    return out
+
+
 def _register():
     global _REGISTERED
     if _REGISTERED:
@@ -454,34 +485,7 @@ class _ImageNetPlan:
 
     @staticmethod
     def _xcd_order(items, ng):
-        """XCD-aware dispatch order: consecutive runs of ``ng`` items share an operand tile (the co-tiles of one
-        pixel tile; the dW tiles of one pixel chunk).  Workgroup k runs on XCD k % 8, each XCD with its own L2, so
-        the run is spread over positions 8 apart -- every item of a run lands on the same XCD, dispatched close in
-        time, and the shared tile is fetched into one L2 instead of ng of them."""
-        if not _CG_XCD:
-            return items
-        # items are member-major (slot order); with a multiple of 8 members of equal work, member m's items all go
-        # to XCD m % 8 (its weights and activations then live in one L2; positions 8 apart, runs kept adjacent)
-        nm = len(items) and len({it[0] for it in items})
-        if _CG_XCD >= 2 and nm % 8 == 0 and len(items) % nm == 0:
-            per = len(items) // nm
-            mem = [items[m * per:(m + 1) * per] for m in range(nm)]
-            if all(len({it[0] for it in blk}) == 1 for blk in mem):
-                out = []
-                for g8 in range(0, nm, 8):
-                    grp = mem[g8:g8 + 8]
-                    for j in range(per):
-                        out.extend(blk[j] for blk in grp)
-                return out
-        if ng <= 1 or len(items) % ng:
-            return items
-        runs = [items[i:i + ng] for i in range(0, len(items), ng)]
-        out = []
-        for b in range(0, len(runs), 8):
-            blk = runs[b:b + 8]
-            for c in range(ng):
-                out.extend(r[c] for r in blk)
-        return out
+        return xcd_order(items, ng)
 
     def _pix_work(self, hw_grid, co, tc, classes=(0,), tp=128):
         """(slot, p0, p1, o0 | class << 16) tiles of 128 grid pixels x tc output channels per member; a

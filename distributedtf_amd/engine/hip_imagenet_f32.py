@@ -152,6 +152,7 @@ class _ImageNetF32Plan(_ImageNetPlan):
             for p0 in range(f * hwo, (f + n) * hwo, TP[tc]):
                 for o0 in range(0, a.Co, tc):
                     items.append([s, p0, min(p0 + TP[tc], (f + n) * hwo), o0])
+        items = self._xcd_order(items, a.Co // tc)
         work = self._hold(torch.tensor(items, dtype=torch.int32, device=self.be.dev))
         a.work = _p(work)
         self._hold(a)
@@ -195,6 +196,7 @@ class _ImageNetF32Plan(_ImageNetPlan):
                 for o0 in range(0, a.Co, tc):
                     for n0 in range(0, K, 64):
                         items.append([s, p0, min(p0 + WG_CHUNK, (f + n) * hwo), o0 | ((n0 // 16) << 16)])
+        items = self._xcd_order(items, (a.Co // tc) * -(-K // 64))
         work = self._hold(torch.tensor(items, dtype=torch.int32, device=self.be.dev))
         a.work = _p(work)
         self._hold(a)

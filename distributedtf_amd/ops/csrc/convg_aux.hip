@@ -1007,7 +1007,12 @@ DTF_API int dtf_cg_bn_add_relu(const BnAddArgs* a, hipStream_t stream) {
 DTF_API int dtf_cg_bn_bwd_sums(const BnSumArgs* a, int nimg, hipStream_t stream) {
   if (nimg <= 0) return 0;
   if (a->C > 2048 || a->C % 8 || 2048 % a->C) return -2;
-  hipLaunchKernelGGL(cg_bn_bwd_sums_kernel, dim3(nimg, 8), dim3(256), 0, stream, *a);
+  // workgroups per image: every workgroup ends with 2-3 x C global atomic adds, so wide layers get fewer (C = 2048:
+  // 1 instead of 8 -- 6.3M instead of 50M atomics per launch); split * 2048 stays a multiple of C (the kernel's
+  // fixed-channel condition)
+  int split = 2048 / a->C;
+  split = split < 1 ? 1 : (split > 8 ? 8 : split);
+  hipLaunchKernelGGL(cg_bn_bwd_sums_kernel, dim3(nimg, split), dim3(256), 0, stream, *a);
   return DTF_CHECK_LAUNCH();
 }
 
@@ -1015,7 +1020,9 @@ DTF_API int dtf_cg_chan_stats(const bf16_t* x, const int* img_slot, dtf_acc_t* s
                               hipStream_t stream) {
   if (nimg <= 0) return 0;
   if (C > 2048 || C % 8 || 2048 % C) return -2;
-  hipLaunchKernelGGL(cg_chan_stats_kernel, dim3(nimg, 8), dim3(256), 0, stream, x, img_slot, sums, hw, C, cmax);
+  int split = 2048 / C;  // as dtf_cg_bn_bwd_sums: fewer workgroups (each ends with 2 x C global atomics) for wide C
+  split = split < 1 ? 1 : (split > 8 ? 8 : split);
+  hipLaunchKernelGGL(cg_chan_stats_kernel, dim3(nimg, split), dim3(256), 0, stream, x, img_slot, sums, hw, C, cmax);
   return DTF_CHECK_LAUNCH();
 }
 

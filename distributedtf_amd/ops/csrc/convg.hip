@@ -1657,7 +1657,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   __shared__ __attribute__((aligned(16))) bf16_t sx[RT * WS * CP + 8];
   // STEM_LDS_OUT: the band's outputs are staged as [pixel][64 + 8] rows and stored as whole 128-byte pixel rows
   // (each wave's fragments are 4-channel / 8-byte pieces, 32 bytes per pixel -- partial lines)
-  constexpr int OP = CO + 8;
+  // rows of 64 channels (128 B), 16-byte chunk c of pixel p at chunk c ^ (p & 7): the fragment writes (8-byte pieces,
+  // 16 pixels) and the row reads (8 pixels x 8 chunks per wave) spread over all banks (tools/lds_banks.py model:
+  // reads 4 cycles per instruction instead of 8 with a padded 72-element row)
+  constexpr int OP = CO;
   __shared__ __attribute__((aligned(16))) bf16_t so[STEM_LDS_OUT ? NPT * 16 * OP : 8];
   __shared__ dtf_acc_t acc_lds[2][CO];
   const int4 wk = a.work[blockIdx.x];
@@ -1735,7 +1738,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       const uint32_t lo = pack2bf(acc[0], acc[1]), hi = pack2bf(acc[2], acc[3]);
       if (p < NPV) {
         if constexpr (STEM_LDS_OUT)
-          *reinterpret_cast<uint2*>(so + p * OP + co0) = make_uint2(lo, hi);
+          *reinterpret_cast<uint2*>(so + p * OP + (((co0 >> 3) ^ (p & 7)) << 3) + (co0 & 7)) = make_uint2(lo, hi);
         else
           *reinterpret_cast<uint2*>(yb + (long)p * CO) = make_uint2(lo, hi);
         if constexpr (EPI & 4) {
@@ -1755,7 +1758,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       for (int j = 0; j < (NPV * 8 + 255) / 256; ++j) {
         const int q = tid + 256 * j, px = q >> 3, c8 = 8 * (q & 7);
         if (px < NPV)
-          *reinterpret_cast<uint4*>(yrow + (long)px * CO + c8) = *reinterpret_cast<const uint4*>(so + px * OP + c8);
+          *reinterpret_cast<uint4*>(yrow + (long)px * CO + c8) =
+              *reinterpret_cast<const uint4*>(so + px * OP + (((q & 7) ^ (px & 7)) << 3));
       }
     }
     if (more) {

@@ -56,7 +56,7 @@ _CG_WGT3 = {56: 4, 28: 7, 14: 14} if os.environ.get("DTF_CG_WGT3", "1") == "1" e
 _CG_WGT3_TARGET = int(os.environ.get("DTF_CG_WGT3_TARGET", "512"))
 # the s2d stem forward from 2-row bands (convg_stem_s2d_kernel) at 224 x 224; workgroups per launch
 _CG_STEM_BAND = os.environ.get("DTF_CG_STEM_BAND", "1") == "1"
-_CG_STEM_WG = int(os.environ.get("DTF_CG_STEM_WG", "1024"))
+_CG_STEM_WG = int(os.environ.get("DTF_CG_STEM_WG", "2048"))
 _CG_WPK_WO64 = 32  # pixels per k-step of the 64-row tiles
 # stride-1 3x3 forward / data gradient with LDS-resident input rows (convg_t3_kernel): image width -> rows per tile
 _CG_T3 = {56: 8, 28: 7, 14: 14}  # must match dtf_convg_t3 (rows divide the image height)

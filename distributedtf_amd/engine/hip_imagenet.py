@@ -70,7 +70,8 @@ CG_FOLD = os.environ.get("DTF_CG_FOLD", "0") == "1"
 # tensor is never written (each element is transformed once per 32-channel chunk and output tile)
 CG_FOLD2 = os.environ.get("DTF_CG_FOLD2", "0") == "1"  # measured +2.7 ms: profiles/r5_imagenet_fold2_ab.log
 # XCD-aware work order (_xcd_order): 0 off, 1 operand-sharing runs on one XCD, 2 (default) additionally every member
-# on its own XCD when the population is a multiple of 8 with equal work per member.  ResNet-50 pop 8 x 128:
+# on its own XCD when the population is a multiple of 8 with equal work per member, 3 also members on XCD subsets when
+# the population divides 8.  ResNet-50 pop 8 x 128:
 # 76.7 (0) -> 75.0 (1) -> 73.8 ms (2) (profiles/r5_xcd_order_ab.log)
 _CG_XCD = int(os.environ.get("DTF_CG_XCD", "2"))
 # generic forward / dgrad launches with fewer 256-pixel workgroups than this take 128-pixel tiles (conv())
@@ -139,22 +140,34 @@ def xcd_order(items, ng):
     # items are member-major (slot order); with a multiple of 8 members of equal work, member m's items all go
     # to XCD m % 8 (its weights and activations then live in one L2; positions 8 apart, runs kept adjacent)
     nm = len(items) and len({it[0] for it in items})
-    if _CG_XCD >= 2 and nm and nm % 8 == 0 and len(items) % nm == 0:
+    if _CG_XCD >= 2 and nm and (nm % 8 == 0 or (_CG_XCD >= 3 and 8 % nm == 0)) and len(items) % nm == 0:
         per = len(items) // nm
         mem = [items[m * per:(m + 1) * per] for m in range(nm)]
         if all(len({it[0] for it in blk}) == 1 for blk in mem):
+            # mode 3, nm | 8 (pop 1 / 2 / 4 per GPU; opt-in, not yet measured): member m owns XCDs m, m + nm, ..;
+            # its own items run-ordered over those
+            # 8 / nm XCDs (position j * nm + m of the launch holds its j-th item)
+            q = 8 // nm if 8 % nm == 0 else 1
+            if q > 1:
+                mem = [_run_order(blk, ng, q) for blk in mem]
             out = []
-            for g8 in range(0, nm, 8):
-                grp = mem[g8:g8 + 8]
+            g = min(nm, 8)
+            for g0 in range(0, nm, g):
+                grp = mem[g0:g0 + g]
                 for j in range(per):
                     out.extend(blk[j] for blk in grp)
             return out
+    return _run_order(items, ng, 8)
+
+
+def _run_order(items, ng, lanes):
+    """Runs of ``ng`` consecutive items spread ``lanes`` apart (one dispatch lane = one XCD of the sub-machine)."""
     if ng <= 1 or len(items) % ng:
         return items
     runs = [items[i:i + ng] for i in range(0, len(items), ng)]
     out = []
-    for b in range(0, len(runs), 8):
-        blk = runs[b:b + 8]
+    for b in range(0, len(runs), lanes):
+        blk = runs[b:b + lanes]
         for c in range(ng):
             out.extend(r[c] for r in blk)
     return out

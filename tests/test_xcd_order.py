@@ -10,7 +10,7 @@ def _items(nmem, per_mem_runs, ng):
     return [[s, p, p + 1, c] for s in range(nmem) for p in range(per_mem_runs) for c in range(ng)]
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3])
 @pytest.mark.parametrize("nmem,runs,ng", [(8, 5, 3), (8, 16, 1), (2, 9, 4), (1, 13, 2), (16, 3, 2)])
 def test_xcd_order_is_a_permutation_with_locality(monkeypatch, mode, nmem, runs, ng):
     monkeypatch.setattr(H, "_CG_XCD", mode)
@@ -20,9 +20,16 @@ def test_xcd_order_is_a_permutation_with_locality(monkeypatch, mode, nmem, runs,
     xcd = {}
     for k, it in enumerate(out):
         xcd.setdefault((it[0], it[1]), set()).add(k % 8)
-    if mode == 2 and nmem % 8 == 0:
+    if mode >= 2 and nmem % 8 == 0:
         for k, it in enumerate(out):
             assert it[0] % 8 == k % 8  # member m on XCD m % 8
+    elif mode == 3 and 8 % nmem == 0:  # member m on XCDs m, m + nmem, ..; its complete blocks of 8 / nmem runs local
+        q = 8 // nmem
+        for k, it in enumerate(out):
+            assert k % nmem == it[0] % nmem
+        for (s, p), xs in xcd.items():
+            if p < runs // q * q:
+                assert len(xs) == 1, (s, p, xs)
     else:
         full = (len(items) // ng) // 8 * 8  # runs in complete blocks of 8
         for (s, p), xs in xcd.items():

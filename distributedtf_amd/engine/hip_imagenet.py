@@ -69,11 +69,11 @@ CG_FOLD = os.environ.get("DTF_CG_FOLD", "0") == "1"
 # (convg_t3 XF / convg MODE 1 when strided) and weight gradient (row-band MX 1 / wide MX 1) -- so the a1 = relu(BN2(h1))
 # tensor is never written (each element is transformed once per 32-channel chunk and output tile)
 CG_FOLD2 = os.environ.get("DTF_CG_FOLD2", "0") == "1"  # measured +2.7 ms: profiles/r5_imagenet_fold2_ab.log
-# XCD-aware work order (_xcd_order): 0 off, 1 operand-sharing runs on one XCD, 2 (default) additionally every member
-# on its own XCD when the population is a multiple of 8 with equal work per member, 3 also members on XCD subsets when
-# the population divides 8.  ResNet-50 pop 8 x 128:
+# XCD-aware work order (_xcd_order): 0 off, 1 operand-sharing runs on one XCD, 2 additionally every member on its own
+# XCD when the population is a multiple of 8 with equal work per member, 3 (default) also members on XCD subsets when
+# the population divides 8 (pop 4: 39.73 -> 38.95 ms).  ResNet-50 pop 8 x 128:
 # 76.7 (0) -> 75.0 (1) -> 73.8 ms (2) (profiles/r5_xcd_order_ab.log)
-_CG_XCD = int(os.environ.get("DTF_CG_XCD", "2"))
+_CG_XCD = int(os.environ.get("DTF_CG_XCD", "3"))
 # generic forward / dgrad launches with fewer 256-pixel workgroups than this take 128-pixel tiles (conv())
 _CG_SMALL = int(os.environ.get("DTF_CG_SMALL", "0"))
 # ... and so do the 1x1 launches whose GEMM depth (Ci of the gathered operand) is at most this (memory-bound: more,
@@ -144,7 +144,7 @@ def xcd_order(items, ng):
         per = len(items) // nm
         mem = [items[m * per:(m + 1) * per] for m in range(nm)]
         if all(len({it[0] for it in blk}) == 1 for blk in mem):
-            # mode 3, nm | 8 (pop 1 / 2 / 4 per GPU; opt-in, not yet measured): member m owns XCDs m, m + nm, ..;
+            # mode 3, nm | 8 (pop 1 / 2 / 4 per GPU): member m owns XCDs m, m + nm, ..;
             # its own items run-ordered over those
             # 8 / nm XCDs (position j * nm + m of the launch holds its j-th item)
             q = 8 // nm if 8 % nm == 0 else 1

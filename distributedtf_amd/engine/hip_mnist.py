@@ -165,6 +165,10 @@ class HipMnistBackend:
         self.rng_counter = 0
         self.drop_rate = float(getattr(arch, "dropout", 0.4))
         self._plans: Dict[tuple, "_MnistPlan"] = {}
+        # training plans also write the head's logits (the "probabilities" hook, reference mnist_model.py:149-151);
+        # set before the first step (EngineModel._hooks): the flag is baked into a plan's captured launches
+        self.keep_probs = False
+        self._last_plan = None
         self.use_graph = (os.environ.get("DTF_HIP_GRAPH", "1") == "1" and os.environ.get("DTF_DEBUG", "0") != "1")
 
     # engine hooks ----------------------------------------------------------------------------
@@ -206,6 +210,7 @@ class HipMnistBackend:
         self._upload_rng(self.last_rng)
         p.load_batch(batches)
         p.run()
+        self._last_plan = p
         note_step_advanced(e, slots)
         return p.loss_sel.clone()  # gathered inside the step graph
 
@@ -215,6 +220,21 @@ class HipMnistBackend:
     def train_correct(self, slots):
         """Correct predictions of each member's last training batch (head kernel count; device tensor)."""
         return self.correct[torch.as_tensor(list(slots), dtype=torch.long, device=self.dev)]
+
+    def train_probabilities(self, slots):
+        """Softmax of each member's last training batch (with dropout, as the reference's ``softmax_tensor`` in
+        training mode): a list of [batch, 10] device tensors, or None when the plans do not keep logits."""
+        p = self._last_plan
+        if p is None or p.logits is None or p.eval:
+            return None
+        out = []
+        for s in slots:
+            if s not in p.first:
+                out.append(None)
+                continue
+            f, n = p.first[s], p.sizes[p.slots.index(s)]
+            out.append(torch.softmax(p.logits[f:f + n], dim=1))
+        return out
 
     def eval_plan(self, slots, m):
         """Eval plans live in their own bounded cache: an eval pass never evicts the captured training graph."""
@@ -307,6 +327,9 @@ class _MnistPlan:
         a.z, a.dz, a.dp2, a.dp1 = _p(self.z), _p(self.dz), _p(self.dp2), _p(self.dp1)
         a.loss, a.correct, a.cnt, a.rng = _p(be.loss), _p(be.correct), _p(self.cnt), _p(be.rng)
         a.logits_out = None
+        if be.keep_probs and not self.eval:
+            self.logits = torch.zeros(N, 10, dtype=torch.float32, device=dev)
+            a.logits_out = _p(self.logits)
         a.off_c1w, a.off_c1b, a.off_c2w, a.off_c2b = o["conv1_w"], o["conv1_b"], o["conv2_w"], o["conv2_b"]
         a.off_d1w, a.off_d1b, a.off_d2w, a.off_d2b = o["dense1_w"], o["dense1_b"], o["dense2_w"], o["dense2_b"]
         a.drop_rate = be.drop_rate

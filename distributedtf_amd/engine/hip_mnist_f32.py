@@ -103,6 +103,8 @@ class HipMnistF32Backend(HipMnistBackend):
         self.rng_counter = 0
         self.drop_rate = float(getattr(arch, "dropout", 0.4))
         self._plans = {}
+        self.keep_probs = False
+        self._last_plan = None
         self.use_graph = (os.environ.get("DTF_HIP_GRAPH", "1") == "1" and os.environ.get("DTF_DEBUG", "0") != "1")
 
     def on_params_changed(self, slots):
@@ -186,6 +188,9 @@ class _MnistF32Plan:
         if self.eval:
             a.loss, a.correct = _p(self.ev_acc[1]), _p(self.ev_acc[0])
         self.head_args = a
+        if be.keep_probs and not self.eval:  # the "probabilities" hook (HipMnistBackend.train_probabilities)
+            self.logits = torch.zeros(N, 10, dtype=torch.float32, device=dev)
+            a.logits_out = _p(self.logits)
         # head chunks (img0, nimg, 0, slot): deterministic build -> one workgroup per member
         self.w_head = self._chunks(1 << 30 if be.det else 16)
         self._build()

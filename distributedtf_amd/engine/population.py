@@ -252,12 +252,22 @@ class TorchBackend:
     def shadow_weights(self):
         return None
 
+    keep_probs = False  # the "probabilities" hook: keep each member's training softmax (train_probabilities)
+
+    def train_probabilities(self, slots):
+        probs = getattr(self, "_probs", {})
+        return [probs.get(s) for s in slots]
+
     def forward_backward(self, slots, batches):
         e = self.e
         losses = []
+        if self.keep_probs:
+            self._probs = {}
         for s, (x, y) in zip(slots, batches):
             p = e.params[s].detach().clone().requires_grad_(True)
             logits = e.arch.forward(p, e.running[s], x, training=True, dtype=e.compute_dtype)
+            if self.keep_probs:
+                self._probs[s] = torch.softmax(logits.detach().float(), dim=1)
             loss = F.cross_entropy(logits.float(), y.long())
             if e.loss_scale != 1.0:
                 g, = torch.autograd.grad(loss * e.loss_scale, p)

@@ -35,9 +35,10 @@ class _LazyValues(dict):
     """Hook values: host scalars up front, device-derived ones (``cross_entropy``, ``train_accuracy``: one
     readback) only when a hook asks for them."""
 
-    def __init__(self, fetch, base):
+    def __init__(self, fetch, base, extra=None):
         super().__init__(base)
         self._fetch = fetch
+        self._extra = dict(extra or {})  # key -> fetch() for other device-derived values (``probabilities``)
 
     def _device(self):
         if not dict.__contains__(self, "cross_entropy"):
@@ -46,16 +47,27 @@ class _LazyValues(dict):
             if h.get("acc") is not None:
                 dict.__setitem__(self, "train_accuracy", h["acc"])
 
+    def _other(self, key):
+        f = self._extra.pop(key, None)
+        if f is not None:
+            v = f()
+            if v is not None:
+                dict.__setitem__(self, key, v)
+
     def __missing__(self, key):
         if key in ("cross_entropy", "train_accuracy"):
             self._device()
-            if dict.__contains__(self, key):
-                return dict.__getitem__(self, key)
+        else:
+            self._other(key)
+        if dict.__contains__(self, key):
+            return dict.__getitem__(self, key)
         raise KeyError(key)
 
     def __contains__(self, key):
         if key in ("cross_entropy", "train_accuracy"):
             self._device()
+        else:
+            self._other(key)
         return dict.__contains__(self, key)
 
     def get(self, key, default=None):
@@ -86,13 +98,15 @@ class EngineModel(ModelBase):
     def __init__(self, cluster_id, hparams, save_base_dir, seed=None, device=None, backend="auto",
                  capacity=8, use_synthetic_data=None, data_dir=None, max_train_steps=None,
                  checkpoint_every_round=True, eval_every_round=True, dp=None, tf_checkpoint=False, ready_steps=None,
-                 stop_threshold=None, batch_size=None, dtype="bf16", loss_scale=1.0, **kw):
+                 stop_threshold=None, batch_size=None, dtype="bf16", loss_scale=1.0, epochs_between_evals=1, **kw):
         super().__init__(cluster_id, hparams, save_base_dir, seed=seed)
         from ..utils.flags import get_dtype
         self.compute_dtype = get_dtype(dtype)  # --dtype: bf16 (HIP kernels) | fp32 / fp16 (PyTorch backend)
         self.loss_scale = float(loss_scale or 1.0)
         self.ready_steps = int(ready_steps) if ready_steps else None  # PBT ready interval in steps (--ready_steps)
         self.stop_threshold = stop_threshold  # --stop_threshold: end a member's train call once eval passes it
+        # --epochs_between_evals: epochs per train -> eval cycle (reference _base.py:74-79, resnet_run_loop.py:446-447)
+        self.epochs_between_evals = max(1, int(epochs_between_evals or 1))
         self.batch_size_override = int(batch_size) if batch_size else None  # --batch_size
         self._pin_batch_size()
         self.dp = dp  # parallel.dataparallel.DPContext: this member is one replica of a data-parallel group
@@ -309,16 +323,19 @@ class EngineModel(ModelBase):
 
     def cycle_steps(self, num_epoch: int) -> List[int]:
         """Steps of each train -> eval cycle of one call.  The reference evaluates (and appends a CSV row, checks
-        the stop threshold) after every epoch (``resnet_run_loop.py:446-508``, ``mnist_model.py:161-172``);
+        the stop threshold) after every ``epochs_between_evals`` epochs -- 1 in the PBT runs
+        (``resnet_run_loop.py:446-508``: ``train_epochs // epochs_between_evals`` cycles; ``mnist_model.py:161-172``);
         with ``ready_steps`` the whole call is one cycle."""
         total = self.n_steps(num_epoch)
-        if self.ready_steps or num_epoch <= 1:
+        ebe = self.epochs_between_evals
+        if self.ready_steps or num_epoch <= ebe:
             return [total]
-        spe = self.steps_per_epoch()
+        per = ebe * self.steps_per_epoch()
         out = []
-        for _ in range(num_epoch):
-            n = min(spe, total - sum(out))
+        for _ in range(num_epoch // ebe):
+            n = min(per, total - sum(out))
             out.append(max(0, n))
+        out[-1] += max(0, total - sum(out))  # a remainder of epochs (num_epoch % ebe) joins the last cycle
         return out
 
     @classmethod
@@ -330,11 +347,16 @@ class EngineModel(ModelBase):
             from ..utils.hooks import get_train_hooks
             names = m.options.get("hooks") or ""
             n = int(m.options.get("hook_every_n") or 100)
+            pn = int(getattr(m, "probabilities_every_n", 0) or 0)
+            if pn > 0 and "probabilities" not in names.lower():
+                names = ",".join(x for x in (names, "probabilities") if x)  # MNIST default (mnist_model.py:149-151)
             hs = get_train_hooks(names, batch_size=int(m.hparams["batch_size"]), every_n_iter=n, every_n_steps=n,
-                                 every_n_secs_steps=n, warm_steps=min(5, n),
+                                 every_n_secs_steps=n, warm_steps=min(5, n), probabilities_every_n=pn or 50,
                                  model_dir=m.options.get("model_dir") or os.path.dirname(m.save_dir) or ".")
             for h in hs:
                 h.begin()
+            if any(getattr(h, "needs_probabilities", False) for h in hs) and hasattr(eng.backend, "keep_probs"):
+                eng.backend.keep_probs = True  # before the first step: plans then keep the head's logits
             eng.train_hooks = hs
             eng.hook_step = 0
         return hs
@@ -457,8 +479,14 @@ class EngineModel(ModelBase):
                                                       for v, m in zip(c.cpu().tolist(), active)]
             return host
 
+        def probabilities():
+            fn = getattr(eng.backend, "train_probabilities", None)
+            pr = fn([m.slot for m in active]) if fn is not None else None
+            return None if pr is None else [None if t is None else t.cpu().numpy() for t in pr]
+
         values = _LazyValues(device_values, {"images": n_img, "model_ids": [m.cluster_id for m in active],
-                                             "learning_rate": list(lrs), "sync": eng.device.type == "cuda"})
+                                             "learning_rate": list(lrs), "sync": eng.device.type == "cuda"},
+                             extra={"probabilities": probabilities})
         for h in due:
             h.after_step(step, values)
 

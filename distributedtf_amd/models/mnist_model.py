@@ -8,7 +8,8 @@ Changed: the dataset is loaded once and kept on the device (the reference
 re-reads the gz files on every call); an "epoch" is a full pass
 (``60000 / batch`` steps) unless ``debug_steps`` (the reference's 10-step debug
 epoch, Appendix A4) or ``max_train_steps`` is given; data is synthetic when
-``./datasets/`` is absent.
+``./datasets/`` is absent.  The training softmax is logged every 50 steps, as the reference's
+``LoggingTensorHook`` does (``--log_probabilities_every_n``; 0 = off).
 """
 
 from __future__ import annotations
@@ -23,8 +24,11 @@ from ..engine import schedule
 
 class MNISTModel(EngineModel):
     def __init__(self, cluster_id, hparams, save_base_dir, seed=None, data_dir="./datasets/", debug_steps=None,
-                 normalize=False, **kw):
+                 normalize=False, probabilities_every_n=50, **kw):
         self.debug_steps = debug_steps
+        # the reference logs the training softmax every 50 iterations (mnist_model.py:149-151): the
+        # "probabilities" hook (utils/hooks.py ProbabilitiesHook) is on by default for MNIST; 0 turns it off
+        self.probabilities_every_n = int(probabilities_every_n or 0)
         self.normalize = normalize
         super().__init__(cluster_id, hparams, save_base_dir, seed=seed, data_dir=data_dir, **kw)
 

@@ -96,11 +96,20 @@ def build_parser(defaults: Optional[Dict[str, Any]] = None) -> argparse.Argument
     p.add_argument("--model", default=d["model"], help="toy | mnist | cifar10 | imagenet")
     p.add_argument("--mode", default="spmd", choices=["spmd", "master_worker"])
     p.add_argument("--rounds", "--train_round", dest="train_round", type=int, default=d["train_round"])
-    p.add_argument("--epochs_per_round", type=int, default=d["epochs_per_round"])
+    p.add_argument("--epochs_per_round", "--train_epochs", dest="epochs_per_round", type=int,
+                   default=d["epochs_per_round"],
+                   help="epochs each member trains per PBT round (the reference passes train_epochs = "
+                        "epochs_per_round to every member's main(), cifar10_main.py:321-327, mnist_model.py:128)")
+    p.add_argument("--epochs_between_evals", type=int, default=1,
+                   help="epochs per train -> eval cycle inside a round: a round of E epochs runs E // this cycles, "
+                        "each appending one learning_curve.csv row (reference _base.py:74-79, "
+                        "resnet_run_loop.py:446-447)")
     p.add_argument("--do_exploit", type=_str2bool, default=d["do_exploit"])
     p.add_argument("--do_explore", type=_str2bool, default=d["do_explore"])
     p.add_argument("--seed", type=int, default=None)
-    p.add_argument("--savedata", default="savedata")
+    p.add_argument("--savedata", "--model_dir", dest="savedata", default="savedata",
+                   help="base directory of the member directories model_<id>/ (reference: save_base_dir, passed to "
+                        "each member as model_dir = save_base_dir + id, cifar10_main.py:323)")
     p.add_argument("--results_file", default="test_results.txt")
     p.add_argument("--exploit_transport", default="dataplane", choices=["dataplane", "files"])
     p.add_argument("--inject_nan_member", action="append", default=[],
@@ -124,6 +133,9 @@ def build_parser(defaults: Optional[Dict[str, Any]] = None) -> argparse.Argument
                         "steps into savedata/), metric (the logging values into the benchmark logger)")
     p.add_argument("--log_every_n_steps", type=int, default=100,
                    help="period of the logging / metric / examples_per_second hooks (reference: 100 steps)")
+    p.add_argument("--log_probabilities_every_n", type=int, default=50,
+                   help="MNIST: print each member's training softmax every N steps (the reference's LoggingTensorHook "
+                        "on softmax_tensor, mnist_model.py:149-151); 0 = off")
     p.add_argument("--stop_threshold", type=float, default=None,
                    help="a member's train call ends once its eval accuracy reaches this (resnet_run_loop.py:505)")
     p.add_argument("--export_dir", default=None, help="export the best member's inference weights here at the end")
@@ -168,6 +180,7 @@ class MainArgs(argparse.Namespace):
             kw["hooks"] = self.hooks
             kw["hook_every_n"] = self.log_every_n_steps
             kw["model_dir"] = self.savedata
+            kw["epochs_between_evals"] = getattr(self, "epochs_between_evals", 1)
             if self.stop_threshold is not None:
                 kw["stop_threshold"] = self.stop_threshold
             if self.ready_steps:
@@ -180,6 +193,8 @@ class MainArgs(argparse.Namespace):
             kw["resnet_version"] = self.resnet_version
         if self.model == "mnist" and self.debug_steps:
             kw["debug_steps"] = self.debug_steps
+        if self.model == "mnist":
+            kw["probabilities_every_n"] = getattr(self, "log_probabilities_every_n", 50)
         return kw
 
     def apply_runtime_modes(self) -> None:
@@ -266,6 +281,8 @@ def parse_main_args(argv=None, defaults=None) -> MainArgs:
     if args.deterministic and args.backend == "hip" and args.model != "toy" and not hip_deterministic(args):
         p.error("--deterministic with --backend hip: the %s HIP step has no deterministic build yet; use --backend "
                 "auto (deterministic PyTorch algorithms) or torch" % args.model)
+    if args.epochs_between_evals < 1:
+        p.error("--epochs_between_evals must be >= 1")
     if args.deterministic and args.debug_kernels:
         # the debug kernel build keeps the release reductions (8 replicas, atomics): not replayable
         p.error("--deterministic cannot be combined with --debug_kernels (the debug build is not the "

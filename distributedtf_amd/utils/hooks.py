@@ -143,6 +143,35 @@ class LoggingMetricHook(LoggingHook):
                     self.logger.log_metric(k, float(x), global_step=step, extras={"model_id": mid})
 
 
+class ProbabilitiesHook(StepHook):
+    """The MNIST ``LoggingTensorHook(tensors={"probabilities": "softmax_tensor"}, every_n_iter=50)`` of the reference
+    (``mnist_model.py:149-151``): every ``every_n_steps`` steps, each member's softmax over its last training batch
+    (dropout on, as in the reference's training graph) is printed -- numpy's summarised repr, as TF prints a tensor.
+    The backend keeps the logits only while this hook is registered (one [batch, 10] fp32 store in the head kernel);
+    they are read back on logging steps only."""
+
+    needs_probabilities = True
+
+    def __init__(self, every_n_steps: int = 50, printer: Callable = None):
+        self.every_n_steps = every_n_steps
+        self.printer = printer or (lambda s: print(s, flush=True))
+        self.records: List[Dict[str, Any]] = []
+
+    def after_step(self, step, values):
+        probs = values.get("probabilities")
+        ids = values.get("model_ids") or [None]
+        if probs is None:
+            return
+        if not isinstance(probs, list):
+            probs = [probs]
+        for mid, pr in zip(ids, probs):
+            if pr is None:
+                continue
+            self.records.append({"step": step, "model_id": mid, "probabilities": pr})
+            head = "step = %d, " % step + ("model_id = %d, " % mid if mid is not None else "")
+            self.printer(head + "probabilities = %s" % (pr,))
+
+
 class ProfilerHook(StepHook):
     """Chrome-trace window every ``save_steps`` steps via ``torch.profiler``.
 
@@ -187,6 +216,10 @@ def _logging(**kw):
     return LoggingHook(every_n_steps=kw.get("every_n_iter", 100), printer=kw.get("printer"))
 
 
+def _probabilities(**kw):
+    return ProbabilitiesHook(every_n_steps=kw.get("probabilities_every_n", 50), printer=kw.get("printer"))
+
+
 def _profiler(**kw):
     return ProfilerHook(save_steps=kw.get("save_steps", 1000), output_dir=kw.get("model_dir", "."))
 
@@ -209,6 +242,7 @@ HOOKS = {
     "examples_per_second": _eps,
     "loggingmetrichook": _metric,
     "metric": _metric,
+    "probabilities": _probabilities,
 }
 
 

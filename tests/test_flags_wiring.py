@@ -150,3 +150,53 @@ def test_deterministic_flag_selects_det_build(monkeypatch):
         os.environ.pop("DTF_DETERMINISTIC", None)
         import torch
         torch.use_deterministic_algorithms(False)
+
+
+def test_reference_base_flags_train_epochs_ebe_model_dir(tmp_path, monkeypatch):
+    """--train_epochs / --epochs_between_evals / --model_dir (reference official/utils/flags/_base.py:56-80):
+    train_epochs is the epochs a member trains per round, the round runs train_epochs // epochs_between_evals
+    train -> eval cycles (resnet_run_loop.py:446-447), model_dir is the member-directory base."""
+    from distributedtf_amd.utils.flags import parse_main_args
+    a = parse_main_args(["--model", "cifar10", "--train_epochs", "4", "--epochs_between_evals", "2",
+                         "--model_dir", "md"])
+    assert a.epochs_per_round == 4 and a.savedata == "md" and a.model_kwargs()["epochs_between_evals"] == 2
+    with pytest.raises(SystemExit):
+        parse_main_args(["--epochs_between_evals", "0"])
+    monkeypatch.setattr("distributedtf_amd.models.cifar10_model.Cifar10Model.steps_per_epoch", lambda self: 2)
+    _run(tmp_path, monkeypatch, "--rounds", "1", "--train_epochs", "4", "--epochs_between_evals", "2",
+         "--model_dir", "md")
+    rows = _curves("md")
+    assert len(rows) == 2 and all(len(r) == 2 for r in rows.values()), rows  # 4 // 2 cycles per round
+    recs = [json.loads(l) for l in open("md/metrics.jsonl")]
+    assert recs[0]["images"] > 0
+
+
+def test_mnist_probabilities_hook(tmp_path, monkeypatch, capsys):
+    """The reference logs MNIST's training softmax every 50 iterations (mnist_model.py:149-151): on by default,
+    rows are probability distributions over the 10 classes, one line per member."""
+    from distributedtf_amd.utils.hooks import ProbabilitiesHook, get_train_hooks
+    monkeypatch.chdir(tmp_path)
+    EngineModel.reset_engines()
+    assert main_manager.main(["2", "--model", "mnist", "--use_synthetic_data", "true", "--seed", "3",
+                              "--backend", "torch", "--rounds", "1", "--max_train_steps", "5",
+                              "--log_probabilities_every_n", "2", "--batch_size", "16"]) == 0
+    out = capsys.readouterr().out
+    lines = [l for l in out.splitlines() if "probabilities = " in l]
+    assert len(lines) == 2 * 2, out[-2000:]  # steps 2 and 4, two members
+    assert "model_id = 0" in out and "model_id = 1" in out
+    h = [h for h in get_train_hooks("probabilities", probabilities_every_n=3)][0]
+    assert isinstance(h, ProbabilitiesHook) and h.every_n_steps == 3
+    eng = next(iter(EngineModel._engines.values()))
+    hk = [x for x in eng.train_hooks if isinstance(x, ProbabilitiesHook)][0]
+    import numpy as np
+    pr = hk.records[-1]["probabilities"]
+    assert pr.shape == (16, 10) and np.allclose(pr.sum(axis=1), 1.0, atol=1e-5)
+    # off switch
+    EngineModel.reset_engines()
+    monkeypatch.chdir(tmp_path / "..")
+    (tmp_path / "off").mkdir()
+    monkeypatch.chdir(tmp_path / "off")
+    assert main_manager.main(["2", "--model", "mnist", "--use_synthetic_data", "true", "--seed", "3",
+                              "--backend", "torch", "--rounds", "1", "--max_train_steps", "5",
+                              "--log_probabilities_every_n", "0", "--batch_size", "16"]) == 0
+    assert "probabilities = " not in capsys.readouterr().out

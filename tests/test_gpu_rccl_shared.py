@@ -27,11 +27,11 @@ def _port():
     return p
 
 
-def _torchrun(args, tmp, extra_env=None, timeout=150, tag=None):
+def _torchrun(args, tmp, extra_env=None, timeout=150, tag=None, nproc=2):
     env = dict(os.environ)
     env.update(DTF_SHARE_GPU="1", DTF_RCCL_OUT=str(tmp), HSA_ENABLE_IPC_MODE_LEGACY="0")
     env.update(extra_env or {})
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
     # the rank logs go to a file (kept under gpurun_out/ on the GPU box) so a hang still leaves its stacks
     # (tests/_rccl_worker.py dumps every thread's stack before the timeout)
@@ -121,3 +121,22 @@ def test_rccl_bench_two_ranks(tmp_path):
     rec = lines[0]
     assert rec["n_gpus"] == 2 and rec["config"]["exploits_timed"] >= 2 and rec["value"] > 0
     assert rec["config"]["p2p_preconnected"] is True and rec["config"]["step_graph"] == "captured"
+
+
+@pytest.mark.timeout(400)
+def test_rccl_bench_eight_ranks(tmp_path):
+    """The driver's N = 8 headline command, rehearsed on the 1-GPU box: 8 ranks, one member
+    each (the per-GPU work of the 8-GPU headline), an 8-rank RCCL communicator with every pair pre-connected, and
+    >= 2 exploit cycles inside the timed region -- each k = 2 cycle moves two disjoint cross-rank winner->loser
+    pairs in one batch_isend_irecv (parallel/dataplane.py)."""
+    rc, log = _torchrun(["bench.py", "--gpus", "8", "--steps", "40"], tmp_path, tag="bench8", nproc=8,
+                        timeout=360)
+    assert rc == 0, log[-4000:]
+    lines = [json.loads(x) for x in log.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, log[-3000:]
+    rec = lines[0]
+    print(json.dumps(rec))
+    assert rec["n_gpus"] == 8 and rec["steps"] == 40 and rec["value"] > 0, rec
+    assert rec["config"]["exploits_timed"] >= 2, rec
+    assert rec["config"]["p2p_preconnected"] is True and rec["config"]["step_graph"] == "captured", rec
+    assert rec["config"]["parallelism"] == "pbt_pop8_1members_per_gpu", rec

@@ -47,15 +47,18 @@ def lib():
             debug = debug_mode()
             det = deterministic_mode()
             half = half_mode()
-            if half and (debug or det):
-                raise RuntimeError("DTF_HALF=1 (fp16 kernels) has no debug / deterministic build")
-            default = (_build.LIB_DEBUG if debug else (_build.LIB_DET if det else
-                                                       (_build.LIB_HALF if half else _build.LIB)))
+            if half and debug:
+                raise RuntimeError("DTF_HALF=1 (fp16 kernels) has no debug build")
+            default = (_build.LIB_DEBUG if debug else
+                       (_build.LIB_HALF_DET if half and det else
+                        (_build.LIB_DET if det else (_build.LIB_HALF if half else _build.LIB))))
             path = os.environ.get("DTF_LIB") or default
             if path == default and (not os.path.isfile(path) or
                                     (os.environ.get("DTF_REBUILD") == "1" and _build.needs_build(path))):
                 if debug:
                     _build.build_debug(verbose=False)
+                elif half and det:
+                    _build.build_half_det(verbose=False)
                 elif det:
                     _build.build_det(verbose=False)
                 elif half:

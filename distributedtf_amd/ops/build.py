@@ -31,6 +31,9 @@ DET_FLAGS = ["-DDTF_DETERMINISTIC=1", "-DDTF_NREP=64"]
 # head (dlogits x S) and removed by the fused optimizer (grads x 1/S)
 LIB_HALF = os.path.join(HERE, "libdtf_kernels_f16.so")
 HALF_FLAGS = ["-DDTF_HALF=1"]
+# Deterministic half build (--dtype fp16 --deterministic): the half kernels with the deterministic build's fixed-order
+# reductions (DTF_HALF + DTF_DETERMINISTIC; the two switches are orthogonal in common.h)
+LIB_HALF_DET = os.path.join(HERE, "libdtf_kernels_f16_det.so")
 ARCH = os.environ.get("DTF_OFFLOAD_ARCH", "gfx950")
 
 
@@ -101,9 +104,15 @@ def build_half(force: bool = False, verbose: bool = True) -> str:
     return build(force=force, verbose=verbose, extra_flags=HALF_FLAGS, out=LIB_HALF)
 
 
+def build_half_det(force: bool = False, verbose: bool = True) -> str:
+    return build(force=force, verbose=verbose, extra_flags=HALF_FLAGS + DET_FLAGS, out=LIB_HALF_DET)
+
+
 if __name__ == "__main__":
     if "--debug" in sys.argv:
         build_debug(force="--force" in sys.argv)
+    elif "--half" in sys.argv and "--det" in sys.argv:
+        build_half_det(force="--force" in sys.argv)
     elif "--det" in sys.argv:
         build_det(force="--force" in sys.argv)
     elif "--half" in sys.argv:

@@ -242,7 +242,10 @@ def hip_deterministic(args) -> bool:
     MNIST (one workgroup per member for every accumulation) and the ImageNet bottleneck nets (every cross-workgroup
     sum as int64 fixed point with integer atomics, common.h DTF_FIXED_ACC)."""
     dt = getattr(args, "dtype", "bf16")
-    # fp32: the fp32 steps accumulate every cross-workgroup sum in int64 fixed point in the deterministic build too
+    # fp32: the fp32 steps accumulate every cross-workgroup sum in int64 fixed point in the deterministic build too;
+    # fp16 (ResNet v2): the deterministic half build (libdtf_kernels_f16_det.so)
+    if dt == "fp16":
+        return args.model in ("cifar10", "imagenet") and getattr(args, "resnet_version", 2) == 2
     return args.model in ("mnist", "cifar10", "imagenet") and dt in ("bf16", "fp32")
 
 
@@ -264,9 +267,11 @@ def parse_main_args(argv=None, defaults=None) -> MainArgs:
         # fp16 ResNet v2 runs the half build of the HIP kernels (ops/csrc/common.h DTF_HALF: fp16 storage,
         # v_mfma_f32_16x16x32_f16) with the reference's static loss scaling (default 128, _performance.py:30-33):
         # the head differentiates loss_scale * loss, the fused optimizer unscales (resnet_run_loop.py:284-294)
-        if (args.deterministic or args.debug_kernels) and args.backend != "torch":
-            p.error("--dtype fp16 with --deterministic / --debug_kernels: the fp16 kernel build has no "
-                    "deterministic or debug variant; use --backend torch")
+        # --deterministic loads the deterministic half build (libdtf_kernels_f16_det.so: DTF_HALF + the
+        # deterministic build's fixed-order reductions)
+        if args.debug_kernels and args.backend != "torch":
+            p.error("--dtype fp16 with --debug_kernels: the fp16 kernel build has no debug variant; use "
+                    "--backend torch")
         # (apply_runtime_modes sets DTF_HALF=1: ops.lib() then loads libdtf_kernels_f16.so)
     elif args.dtype != "bf16" and args.model != "toy":
         # fp16 of the families without a half-build step (MNIST; ResNet v1 is rejected above) runs on the PyTorch

@@ -100,8 +100,11 @@ def test_dtype_routing():
     assert parse_main_args(["--model", "mnist", "--dtype", "fp16"]).backend == "torch"  # no fp16 MNIST kernels
     with pytest.raises(SystemExit):  # the reference's validator: fp16 is not supported with ResNet v1
         parse_main_args(["--model", "cifar10", "--dtype", "fp16", "--resnet_version", "1"])
-    with pytest.raises(SystemExit):  # no deterministic fp16 kernel build
-        parse_main_args(["--model", "cifar10", "--dtype", "fp16", "--deterministic", "--backend", "hip"])
+    # fp16 + --deterministic: the deterministic half build (libdtf_kernels_f16_det.so)
+    assert parse_main_args(["--model", "cifar10", "--dtype", "fp16", "--deterministic",
+                            "--backend", "hip"]).backend == "hip"
+    with pytest.raises(SystemExit):  # no debug fp16 kernel build
+        parse_main_args(["--model", "cifar10", "--dtype", "fp16", "--debug_kernels", "--backend", "hip"])
     with pytest.raises(SystemExit):
         parse_main_args(["--benchmark_logger_type", "BenchmarkFileLogger"])
 
@@ -146,6 +149,7 @@ def test_deterministic_flag_selects_det_build(monkeypatch):
         with pytest.raises(SystemExit):  # the debug kernel build is not the deterministic one
             parse_main_args(["--model", "cifar10", "--deterministic", "--debug_kernels"])
         assert kb.LIB_DET.endswith("libdtf_kernels_det.so") and "-DDTF_NREP=64" in kb.DET_FLAGS
+        assert kb.LIB_HALF_DET.endswith("libdtf_kernels_f16_det.so")
     finally:
         os.environ.pop("DTF_DETERMINISTIC", None)
         import torch

@@ -108,3 +108,17 @@ def test_fp16_hip_step_matches_fp32_oracle():
     out = r.stdout + r.stderr
     print(out[-4000:])
     assert r.returncode == 0 and "FP16_OK" in r.stdout, out[-4000:]
+
+
+def test_fp16_deterministic_build_replays_bitwise():
+    """--dtype fp16 --deterministic: the deterministic half build (libdtf_kernels_f16_det.so: DTF_HALF with the
+    deterministic build's fixed-order / fixed-point reductions) replays the fp16 ResNet v2 steps bitwise --
+    CIFAR at pop 1 / 2 / 4 and the ImageNet-shape bottleneck net (tools/det_check.py, fp16 branch)."""
+    env = dict(os.environ, DTF_HALF="1", DTF_DETERMINISTIC="1",
+               PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "det_check.py")], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=280)
+    out = r.stdout + r.stderr
+    print(out[-4000:])
+    assert r.returncode == 0 and "DET_OK" in r.stdout, out[-4000:]
+    assert "library: " in out and "libdtf_kernels_f16_det.so" in out, out[-2000:]

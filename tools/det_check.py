@@ -1,7 +1,8 @@
 """Deterministic HIP build check (run with DTF_DETERMINISTIC=1): two identically initialised engines train the same
 steps on the same batches (graph replay, ragged populations) and must hold bitwise-identical state rows -- the
 CIFAR ResNet v2, ResNet v1, ImageNet ResNet-50 v2 / v1 (fixed-point accumulation), MNIST and the fp32 CIFAR
-ResNet v2 / v1 (fixed-point accumulation) families.  Prints
+ResNet v2 / v1 (fixed-point accumulation) families.  With DTF_HALF=1 as well: the deterministic half build
+(libdtf_kernels_f16_det.so) on the fp16 ResNet v2 families (CIFAR, ImageNet shape; static loss scale 128).  Prints
 DET_OK."""
 import os
 import sys
@@ -14,9 +15,11 @@ from distributedtf_amd.engine.population import PopulationEngine  # noqa: E402
 from distributedtf_amd.models.resnet import ResNetArch, cifar_config, imagenet_config  # noqa: E402
 
 assert ops.deterministic_mode(), "run with DTF_DETERMINISTIC=1"
+_L = ops.lib()
+print("library: %s" % getattr(getattr(_L, "_lib", _L), "_name", _L), flush=True)
 
 
-def run(size, sizes, steps, opt="Momentum", version=2, image=32, dtype=torch.bfloat16):
+def run(size, sizes, steps, opt="Momentum", version=2, image=32, dtype=torch.bfloat16, loss_scale=1.0):
     if image == 32:
         arch = ResNetArch(cifar_config(size, version=version))
     else:
@@ -24,7 +27,7 @@ def run(size, sizes, steps, opt="Momentum", version=2, image=32, dtype=torch.bfl
     dev = torch.device("cuda")
     out = []
     for rep in range(2):
-        e = PopulationEngine(arch, len(sizes), dev, backend="hip", compute_dtype=dtype)
+        e = PopulationEngine(arch, len(sizes), dev, backend="hip", compute_dtype=dtype, loss_scale=loss_scale)
         hps = []
         for i, bs in enumerate(sizes):
             hp = {"opt_case": {"optimizer": opt, "lr": 0.05, "momentum": 0.9}, "batch_size": bs,
@@ -77,6 +80,12 @@ def run_mnist(sizes, steps, dtype=torch.bfloat16):
     return same
 
 
+if ops.half_mode():
+    h = dict(dtype=torch.float16, loss_scale=128.0)
+    ok = all([run(20, [16, 24], 4, **h), run(56, [128], 3, **h), run(56, [128] * 4, 2, **h),
+              run(50, [4, 6], 3, image=64, **h)])
+    print("DET_OK" if ok else "DET_FAIL")
+    sys.exit(0 if ok else 1)
 ok = all([run(20, [16, 24], 4), run(56, [128], 3), run(56, [128] * 4, 2), run(20, [16, 24], 4, version=1),
           run(56, [128] * 2, 2, version=1), run_mnist([40, 72], 4),
           run(50, [4, 6], 3, image=64), run(50, [8, 8], 2, version=1, image=64),

@@ -69,6 +69,11 @@ CG_FOLD = os.environ.get("DTF_CG_FOLD", "0") == "1"
 # (convg_t3 XF / convg MODE 1 when strided) and weight gradient (row-band MX 1 / wide MX 1) -- so the a1 = relu(BN2(h1))
 # tensor is never written (each element is transformed once per 32-channel chunk and output tile)
 CG_FOLD2 = os.environ.get("DTF_CG_FOLD2", "0") == "1"  # measured +2.7 ms: profiles/r5_imagenet_fold2_ab.log
+# read-once fold: BN1 + ReLU applied by conv1 (the 1x1 reduce) only where that consumer transforms each input element
+# exactly once -- blocks without a projection (the block input's only forward consumer is conv1) whose conv1 runs a
+# single output-channel tile (Co <= 128: every workgroup holds all output channels of its pixels) -- and by conv1's
+# weight gradient (wide 1x1 tiles, MX 1), so relu(BN1(x)) is never written for those blocks
+CG_FOLD1 = os.environ.get("DTF_CG_FOLD1", "1") == "1"  # 73.24 -> 72.87 ms at pop 8 (profiles/r6_imagenet_fold1_ab.log)
 # XCD-aware work order (_xcd_order): 0 off, 1 operand-sharing runs on one XCD, 2 additionally every member on its own
 # XCD when the population is a multiple of 8 with equal work per member, 3 (default) also members on XCD subsets when
 # the population divides 8 (pop 4: 39.73 -> 38.95 ms).  ResNet-50 pop 8 x 128:
@@ -433,6 +438,7 @@ class _ImageNetPlan:
         # folded forward (CG_FOLD): v2 training plans keep no relu(BN(.)) tensors
         self.fold = CG_FOLD and not self.eval and not be.v1
         self.fold2 = CG_FOLD2 and not self.fold and not self.eval and not be.v1
+        self.fold1 = CG_FOLD1 and not self.fold and not self.eval and not be.v1 and self.FOLD1_OK
         # v1 (post-activation): h3 = conv3 output (BN3 input), sc = raw projection output (BN_p input), a0 = the
         # stem's relu(BN(y0)); no ax (the block input IS a ReLU output)
         self.v1 = be.v1
@@ -824,6 +830,15 @@ class _ImageNetPlan:
         self._add("gemm", self.g_dgr)
         self._add("gemm", self.g_wgr)
 
+    FOLD1_OK = True  # the fp32 plan (hip_imagenet_f32.py) keeps the materialised relu(BN1(x))
+
+    def _fold1(self, i):
+        """Block i's BN1 + ReLU is applied by conv1 itself (CG_FOLD1: no projection, one output-channel tile)."""
+        if not getattr(self, "fold1", False):
+            return False
+        blk = self.be.prog.blocks[i]
+        return blk.proj is None and self.be.prog.convs[blk.convs[0]].cout <= 128
+
     # ------------------------------------------------------------------------------------------ program
     def _build(self):
         be, e, prog, cfg = self.be, self.e, self.be.prog, self.be.cfg
@@ -860,10 +875,14 @@ class _ImageNetPlan:
                 self.conv(c3, self.h2[i], self.xs[i + 1], ho, mode=1, c_in=self.cf(b3), epi=5, res=res,
                           st=self.sf(nxt))
                 continue
-            self.ew(relu, x, self.ax[i], self.cf(b1), hi, cin)
+            if self._fold1(i):
+                self.conv(c1, x, self.h1[i], hi, mode=1, c_in=self.cf(b1), epi=4, st=self.sf(b2))
+            else:
+                self.ew(relu, x, self.ax[i], self.cf(b1), hi, cin)
             if blk.proj is not None:
                 self.conv(blk.proj, self.ax[i], self.sc[i], hi, mode=0, epi=0)
-            self.conv(c1, self.ax[i], self.h1[i], hi, mode=0, epi=4, st=self.sf(b2))
+            if not self._fold1(i):
+                self.conv(c1, self.ax[i], self.h1[i], hi, mode=0, epi=4, st=self.sf(b2))
             self.bn_final(b2, hi, False)
             if self.fold2:
                 self.conv(c2, self.h1[i], self.h2[i], hi, mode=1, c_in=self.cf(b2), epi=4, st=self.sf(b3))
@@ -931,7 +950,10 @@ class _ImageNetPlan:
             self.conv(c1, dh1, dz1, hi, mode=0, epi=6 | (1 if pd is not None else 0), res=pd, xm=x,
                       c_ep=self.cf(b1), st=self.sb(b1), dgrad=True)
             self.bn_final(b1, hi, True)
-            self.wgrad(c1, x, dh1, hi, mode_x=1, c_x=self.cf(b1)) if self.fold else self.wgrad(c1, self.ax[i], dh1, hi)
+            if self.fold or self._fold1(i):
+                self.wgrad(c1, x, dh1, hi, mode_x=1, c_x=self.cf(b1))
+            else:
+                self.wgrad(c1, self.ax[i], dh1, hi)
             gnext = self.tmp("gA" if (i % 2 == 0) else "gB", hi, cin)
             self.ew(bwd, x, gnext, self.cb(b1), hi, cin, dz=dz1, add=None if blk.proj is not None else gcur)
             gcur = gnext

@@ -116,6 +116,8 @@ class HipImageNetF32Backend(HipImageNetBackend):
 
 
 class _ImageNetF32Plan(_ImageNetPlan):
+    FOLD1_OK = False  # (the fp32 conv kernels are not exercised with the read-once BN1 fold)
+
     def _act_dtype(self):
         return torch.float32
 

@@ -55,6 +55,9 @@ FWD_RESIDENT = int(os.environ.get("DTF_FWD_RESIDENT", "0"))  # stride-1 forward:
 HEAD_ITEMS = 512          # head / GAP+dense+CE work items
 WGRAD_WG_PER_MEMBER = 128  # standalone wgrad launches: workgroups per member (bounds the dW partial traffic)
 DENSE_REDUCE_BLOCKS = 256  # slab_reduce_all, dense jobs: max 32-element blocks per job
+# slab_reduce_all, conv slab jobs: at most this many 256-element blocks per (job, member) -- each loops over the
+# job's chunks (0: one block per chunk, the round-5 form)
+SLAB_X_BLOCKS = int(os.environ.get("DTF_SLAB_X_BLOCKS", "16"))
 FUSED_SLAB_BYTES = {16: 16e6, 32: 16e6, 64: 48e6}  # fused backward: per-launch dW slab budget -> workgroup count
 FUSED_MIN_WG = int(os.environ.get("DTF_FUSED_MIN_WG", "256"))  # ... at least this many workgroups (one member would leave CUs idle otherwise)
 FUSED_MAX_WG = {32: 128}  # ... at most this many per member (C = 32: fewer, fuller workgroups)
@@ -881,24 +884,28 @@ class _StepPlan:
         self.graph = None
 
     # -------------------------------------------------------------------- work lists
-    def _work_iters(self, bands, n_wg):
+    def _work_iters(self, bands, n_wg, det_per=None):
         """(it0, nit, 0, slot) items over the flattened (image, band) iterations of each member.
 
         Deterministic build: ``n_wg`` is ignored -- every member gets exactly DET_WG_PER_MEMBER rows (empty ones,
         nit = 0, past its iterations), so a member's split into workgroups, the statistic replica each of its
         workgroups adds to (blockIdx % 64 = the row within the member) and the order its dW slabs are reduced in
         depend on its own batch size only: the step of a member is bitwise the same whichever members share its
-        plan (a PBT run replays identically at any placement over ranks, tests/test_gpu_placement.py)."""
+        plan (a PBT run replays identically at any placement over ranks, tests/test_gpu_placement.py).
+        ``det_per``: launches that produce no BatchNorm statistics (the deferred weight-gradient jobs) take that
+        fixed number of rows per member instead (any population-independent count keeps the dW slab order a
+        function of the member alone; 64 rows wrote 8x the slab bytes of the release plan at pop 8)."""
         det = self.be.det
-        key = ("it", bands, "det" if det else n_wg)
+        dper = (det_per or DET_WG_PER_MEMBER) if det else None
+        key = ("it", bands, ("det", dper) if det else n_wg)
         w = self._work_cache.get(key)
         if w is None and self.elastic:
-            per = DET_WG_PER_MEMBER if det else max(1, n_wg // max(1, len(self.slots)))
+            per = dper if det else max(1, n_wg // max(1, len(self.slots)))
             w = self._elastic_table(per, bands, 1)
             self._work_cache[key] = w
         if w is None:
             items = []
-            per_member = DET_WG_PER_MEMBER if det else max(1, n_wg // max(1, len(self.slots)))
+            per_member = dper if det else max(1, n_wg // max(1, len(self.slots)))
             for s, n in zip(self.slots, self.sizes):
                 total = n * bands
                 f = self.first[s] * bands
@@ -978,10 +985,30 @@ class _StepPlan:
             return min(n_wg, DET_WG_PER_MEMBER * len(self.slots))
         return n_wg
 
-    def _head_items(self):
-        # deterministic mode: one head workgroup per member (its dense-gradient / statistic atomics are then the
-        # only writers)
-        return len(self.slots) if self.be.det else HEAD_ITEMS
+    def _head_work(self):
+        """Head work items (img0, nimg, 0, slot).  Deterministic build: exactly DET_WG_PER_MEMBER items per member
+        (empty ones past its images): each workgroup then adds its final-BN backward partial to its own statistic
+        replica (the row within the member), its dense gradients go to its own slab (reduced in a fixed order),
+        and its loss partial is rounded to 2^-16 (order-free sum) -- a member's head depends on its own batch only.
+        (One workgroup per member serialised the pop-8 deterministic step: 627 us vs 34 us,
+        profiles/r6_det_vs_release_kstats.txt.)"""
+        if not self.be.det:
+            return self._work_member(target_items=HEAD_ITEMS)
+        if self.elastic:  # the device-generated table: `per` rows per member, empty ones past its images
+            return self._work_member(target_items=DET_WG_PER_MEMBER * len(self.slots))
+        key = ("head_det",)
+        w = self._work_cache.get(key)
+        if w is None:
+            items = []
+            per = DET_WG_PER_MEMBER
+            for s, n in zip(self.slots, self.sizes):
+                f = self.first[s]
+                chunk = max(1, -(-n // per))
+                rows = [[f + i, min(chunk, n - i), 0, s] for i in range(0, n, chunk)]
+                items += rows + [[f, 0, 0, s]] * (per - len(rows))
+            w = torch.tensor(items, dtype=torch.int32, device=self.be.dev)
+            self._work_cache[key] = w
+        return w
 
     def _work_member(self, target_items=256, min_chunk=1):
         key = ("m", target_items)
@@ -1420,7 +1447,7 @@ class _StepPlan:
             wmode = 2
             assert mode_dy == 2 and dy2 is not None and dy_bn is not None
         per = DEFER_WG[C] if self.defer_wg else DEFER_LARGE_WG[C]
-        wwork = self._work_iters(bands, max(1, min(self.N * bands, per * len(self.slots))))
+        wwork = self._work_iters(bands, max(1, min(self.N * bands, per * len(self.slots))), det_per=per)
         w.work = _p(wwork)
         w.n_main = wwork.shape[0]
         self._set_uniform(w, wwork)
@@ -1501,7 +1528,8 @@ class _StepPlan:
         for i, (buf, red, goff, C) in enumerate(self._deferred):
             sj[i] = SlabJob(buf, _p(red), goff, red.shape[0], C)
             nmax = max(nmax, red.shape[0])
-            bmax = max(bmax, self._slab_elems(C) // 256)
+            nb = self._slab_elems(C) // 256
+            bmax = max(bmax, min(nb, SLAB_X_BLOCKS) if SLAB_X_BLOCKS > 0 else nb)
         for i, (buf, red, goff, kel) in enumerate(self._deferred_dense):
             dj[i] = DenseJob(buf, _p(red), goff, kel, red.shape[0])
             nmax = max(nmax, red.shape[0])
@@ -1642,7 +1670,7 @@ class _StepPlan:
         # head (fwd + bwd of GAP/dense/CE + final-BN reductions)
         fb = prog.final_bn
         hw = L.final_hw
-        hwork = self._work_member(target_items=self._head_items())
+        hwork = self._head_work()
         ha = HeadArgs()
         ha.x, ha.labels, ha.work = _p(self.xs[-1]), _p(self.labels), _p(hwork)
         ha.params, ha.p_mstride = _p(e.state), e.S
@@ -1907,7 +1935,7 @@ class _StepPlan:
         self._forward_v1()
         # head: GAP + dense + CE on the last block output (no final BN: gamma_off = -1)
         hw = L.final_hw
-        hwork = self._work_member(target_items=HEAD_ITEMS)
+        hwork = self._head_work()
         ha_ = HeadArgs()
         ha_.x, ha_.labels, ha_.work = _p(self.xs[-1]), _p(self.labels), _p(hwork)
         ha_.params, ha_.p_mstride = _p(e.state), e.S

@@ -287,7 +287,11 @@ class EngineModel(ModelBase):
         ds = self.dataset()
         if getattr(ds, "num_train", None) is None:
             return
+        # the generator is created here only to receive the saved state: its seed draw must not advance the
+        # just-restored explore rng (the uninterrupted run drew that seed rounds ago, before the saved rng state)
+        rs = self.rng.getstate()
         g = self._data_gen(ds)
+        self.rng.setstate(rs)
         if g is None:
             return
         st = lambda h: torch.frombuffer(bytearray(bytes.fromhex(h)), dtype=torch.uint8)  # noqa: E731

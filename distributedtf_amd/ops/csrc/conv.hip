@@ -451,23 +451,48 @@ __device__ __forceinline__ void coef_issue(CoefLd<MODE>& L, const float* params,
   // exec-mask branch makes the compiler consume -- and wait for -- the first statistics before the tile loads
   const int c = (int)threadIdx.x & (C - 1);
 #if DTF_COEF_SPLIT
-  if constexpr (CREP == NREP && C < 64) {
-    // the wave's 64 / C lane groups split the replicas (coef_reduce sums the groups)
+  if constexpr ((CREP == NREP || CREP == 1) && C < 64) {
+    // the wave's 64 / C lane groups split the replicas (coef_reduce sums the groups).  Many replicas (CREP = 1,
+    // the deterministic build's 64): each group sums its NREP / G replicas in replica order as they arrive -- a
+    // fixed order, so the coefficients stay bitwise reproducible -- and a lane issues G x fewer loads (C = 16: 64
+    // instead of 256 statistics loads in the prologue of every launch)
     constexpr int G = 64 / C, RJ = NREP / G;
     static_assert(NREP % G == 0, "replicas split evenly over the lane groups");
     const int grp = ((int)threadIdx.x & 63) / C;
     const float* rf = stats_row(st_f, slot) + c + grp * 128;
+    if constexpr (CREP == 1) {
+      float a = 0.f, b = 0.f;
 #pragma unroll
-    for (int j = 0; j < CREP; ++j) {
-      L.fs[j] = j < RJ ? rf[j * G * 128] : 0.f;
-      L.fq[j] = j < RJ ? rf[j * G * 128 + 64] : 0.f;
+      for (int j = 0; j < RJ; ++j) {
+        a += rf[j * G * 128];
+        b += rf[j * G * 128 + 64];
+      }
+      L.fs[0] = a;
+      L.fq[0] = b;
+    } else {
+#pragma unroll
+      for (int j = 0; j < CREP; ++j) {
+        L.fs[j] = j < RJ ? rf[j * G * 128] : 0.f;
+        L.fq[j] = j < RJ ? rf[j * G * 128 + 64] : 0.f;
+      }
     }
     if constexpr (MODE >= 2) {
       const float* rb = stats_row(st_b, slot) + c + grp * 128;
+      if constexpr (CREP == 1) {
+        float a = 0.f, b = 0.f;
 #pragma unroll
-      for (int j = 0; j < CREP; ++j) {
-        L.bs[j] = j < RJ ? rb[j * G * 128] : 0.f;
-        L.bq[j] = j < RJ ? rb[j * G * 128 + 64] : 0.f;
+        for (int j = 0; j < RJ; ++j) {
+          a += rb[j * G * 128];
+          b += rb[j * G * 128 + 64];
+        }
+        L.bs[0] = a;
+        L.bq[0] = b;
+      } else {
+#pragma unroll
+        for (int j = 0; j < CREP; ++j) {
+          L.bs[j] = j < RJ ? rb[j * G * 128] : 0.f;
+          L.bq[j] = j < RJ ? rb[j * G * 128 + 64] : 0.f;
+        }
       }
     }
     const float* prow = params + (long)slot * p_mstride;
@@ -517,7 +542,7 @@ __device__ __forceinline__ void coef_issue(CoefLd<MODE>& L, const float* params,
 template <int C, int MODE>
 __device__ __forceinline__ void coef_reduce(CoefLd<MODE>& L) {
 #if DTF_COEF_SPLIT
-  if constexpr (MODE != 0 && CREP == NREP && C < 64) {
+  if constexpr (MODE != 0 && (CREP == NREP || CREP == 1) && C < 64) {
     float a = 0.f, b = 0.f, d = 0.f, e = 0.f;
 #pragma unroll
     for (int j = 0; j < CREP; ++j) {
@@ -2179,35 +2204,40 @@ __global__ __launch_bounds__(256) void slab_reduce_all_kernel(const SlabJob* __r
     if ((int)blockIdx.y >= j.nmem || (int)blockIdx.x * 256 >= E) return;
     const int4 rd = j.red[blockIdx.y];
     const int q = threadIdx.x & 63, gg = threadIdx.x >> 6;
-    const int e0 = blockIdx.x * 256;
-    const float4* p = reinterpret_cast<const float4*>(j.slab + (long)rd.x * E + e0) + q;
     const long E4 = E / 4;
-    float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0, s3 = s0;
-    int g = gg;
-    for (; g + 12 < rd.y; g += 16) {
-      const float4 a0 = p[(long)g * E4], a1 = p[(long)(g + 4) * E4], a2 = p[(long)(g + 8) * E4],
-                   a3 = p[(long)(g + 12) * E4];
-      s0.x += a0.x; s0.y += a0.y; s0.z += a0.z; s0.w += a0.w;
-      s1.x += a1.x; s1.y += a1.y; s1.z += a1.z; s1.w += a1.w;
-      s2.x += a2.x; s2.y += a2.y; s2.z += a2.z; s2.w += a2.w;
-      s3.x += a3.x; s3.y += a3.y; s3.z += a3.z; s3.w += a3.w;
-    }
-    for (; g < rd.y; g += 4) {
-      const float4 a0 = p[(long)g * E4];
-      s0.x += a0.x; s0.y += a0.y; s0.z += a0.z; s0.w += a0.w;
-    }
-    part4[gg][q] = make_float4((s0.x + s1.x) + (s2.x + s3.x), (s0.y + s1.y) + (s2.y + s3.y),
-                               (s0.z + s1.z) + (s2.z + s3.z), (s0.w + s1.w) + (s2.w + s3.w));
-    __syncthreads();
-    const float* pf = reinterpret_cast<const float*>(part4);
-    const int t0 = threadIdx.x;
-    const float sum = (pf[t0] + pf[256 + t0]) + (pf[512 + t0] + pf[768 + t0]);
-    const int e = e0 + t0;
-    const int r = e & 3, t = (e >> 2) & 255, m = (e >> 10) % MT, jj = (e >> 10) / MT;  // slab [j][m][t][r]
-    const int wave = t >> 6, lane = t & 63, nt = wave + 4 * jj;
-    if (nt < NTN) {
-      const int tap = (nt * 16) / C, ci = (nt * 16) % C + (lane & 15), co = m * 16 + 4 * (lane >> 4) + r;
-      grads[(long)rd.w * g_mstride + j.g_off + ((long)co * 9 + tap) * C + ci] += sum;
+    // a block walks every gridDim.x-th 256-element chunk of the job (the host caps gridDim.x: one chunk per block
+    // made 20k blocks of 8 KB each at pop 8 -- launch-bound); the per-element summation order is unchanged
+    for (int xb = blockIdx.x; xb * 256 < E; xb += gridDim.x) {
+      const int e0 = xb * 256;
+      const float4* p = reinterpret_cast<const float4*>(j.slab + (long)rd.x * E + e0) + q;
+      float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0, s3 = s0;
+      int g = gg;
+      for (; g + 12 < rd.y; g += 16) {
+        const float4 a0 = p[(long)g * E4], a1 = p[(long)(g + 4) * E4], a2 = p[(long)(g + 8) * E4],
+                     a3 = p[(long)(g + 12) * E4];
+        s0.x += a0.x; s0.y += a0.y; s0.z += a0.z; s0.w += a0.w;
+        s1.x += a1.x; s1.y += a1.y; s1.z += a1.z; s1.w += a1.w;
+        s2.x += a2.x; s2.y += a2.y; s2.z += a2.z; s2.w += a2.w;
+        s3.x += a3.x; s3.y += a3.y; s3.z += a3.z; s3.w += a3.w;
+      }
+      for (; g < rd.y; g += 4) {
+        const float4 a0 = p[(long)g * E4];
+        s0.x += a0.x; s0.y += a0.y; s0.z += a0.z; s0.w += a0.w;
+      }
+      part4[gg][q] = make_float4((s0.x + s1.x) + (s2.x + s3.x), (s0.y + s1.y) + (s2.y + s3.y),
+                                 (s0.z + s1.z) + (s2.z + s3.z), (s0.w + s1.w) + (s2.w + s3.w));
+      __syncthreads();
+      const float* pf = reinterpret_cast<const float*>(part4);
+      const int t0 = threadIdx.x;
+      const float sum = (pf[t0] + pf[256 + t0]) + (pf[512 + t0] + pf[768 + t0]);
+      const int e = e0 + t0;
+      const int r = e & 3, t = (e >> 2) & 255, m = (e >> 10) % MT, jj = (e >> 10) / MT;  // slab [j][m][t][r]
+      const int wave = t >> 6, lane = t & 63, nt = wave + 4 * jj;
+      if (nt < NTN) {
+        const int tap = (nt * 16) / C, ci = (nt * 16) % C + (lane & 15), co = m * 16 + 4 * (lane >> 4) + r;
+        grads[(long)rd.w * g_mstride + j.g_off + ((long)co * 9 + tap) * C + ci] += sum;
+      }
+      __syncthreads();  // part4 is rewritten by the next chunk
     }
     return;
   }

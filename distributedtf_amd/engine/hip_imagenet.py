@@ -73,6 +73,8 @@ CG_FOLD2 = os.environ.get("DTF_CG_FOLD2", "0") == "1"  # measured +2.7 ms: profi
 # exactly once -- blocks without a projection (the block input's only forward consumer is conv1) whose conv1 runs a
 # single output-channel tile (Co <= 128: every workgroup holds all output channels of its pixels) -- and by conv1's
 # weight gradient (wide 1x1 tiles, MX 1), so relu(BN1(x)) is never written for those blocks
+# ... up to this conv1 width (128: one output-channel tile; 256 / 512 re-transform each element 2 / 4 times)
+CG_FOLD1_MAXC = int(os.environ.get("DTF_CG_FOLD1_MAXC", "128"))
 CG_FOLD1 = os.environ.get("DTF_CG_FOLD1", "1") == "1"  # 73.24 -> 72.87 ms at pop 8 (profiles/r6_imagenet_fold1_ab.log)
 # XCD-aware work order (_xcd_order): 0 off, 1 operand-sharing runs on one XCD, 2 additionally every member on its own
 # XCD when the population is a multiple of 8 with equal work per member, 3 (default) also members on XCD subsets when
@@ -837,7 +839,7 @@ class _ImageNetPlan:
         if not getattr(self, "fold1", False):
             return False
         blk = self.be.prog.blocks[i]
-        return blk.proj is None and self.be.prog.convs[blk.convs[0]].cout <= 128
+        return blk.proj is None and self.be.prog.convs[blk.convs[0]].cout <= CG_FOLD1_MAXC
 
     # ------------------------------------------------------------------------------------------ program
     def _build(self):

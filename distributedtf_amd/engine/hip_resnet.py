@@ -57,7 +57,7 @@ WGRAD_WG_PER_MEMBER = 128  # standalone wgrad launches: workgroups per member (b
 DENSE_REDUCE_BLOCKS = 256  # slab_reduce_all, dense jobs: max 32-element blocks per job
 # slab_reduce_all, conv slab jobs: at most this many 256-element blocks per (job, member) -- each loops over the
 # job's chunks (0: one block per chunk, the round-5 form)
-SLAB_X_BLOCKS = int(os.environ.get("DTF_SLAB_X_BLOCKS", "16"))
+SLAB_X_BLOCKS = int(os.environ.get("DTF_SLAB_X_BLOCKS", "0"))  # 16 / 32 measured flat (profiles/r6_slab_xblocks_ab.log)
 FUSED_SLAB_BYTES = {16: 16e6, 32: 16e6, 64: 48e6}  # fused backward: per-launch dW slab budget -> workgroup count
 FUSED_MIN_WG = int(os.environ.get("DTF_FUSED_MIN_WG", "256"))  # ... at least this many workgroups (one member would leave CUs idle otherwise)
 FUSED_MAX_WG = {32: 128}  # ... at most this many per member (C = 32: fewer, fuller workgroups)

@@ -110,10 +110,11 @@ DEFER_WG = {16: 64, 32: 32, 64: 16}  # deferred wgrad (small populations): workg
 # dependencies cost more than the idle CUs it fills
 WG_OVERLAP = os.environ.get("DTF_WG_OVERLAP", "0") == "1"  # measured slower: profiles/r4_wg_overlap_ab.log
 OVERLAP_CHUNK = int(os.environ.get("DTF_WG_OVERLAP_CHUNK", "0"))  # 0: stage boundaries only
-DEFER_MID_POP = 4         # up to this many members: defer the wgrad of DEFER_MID_CS ...
+DEFER_MID_POP = int(os.environ.get("DTF_DEFER_MID_POP", "4"))  # up to this many members: defer the wgrad of DEFER_MID_CS ...
 DEFER_MID_CS = (32, 64)
 DEFER_LARGE_CS = (64,)    # larger populations defer the wgrad of these channel widths only ...
-DEFER_LARGE_WG = {16: 16, 32: 8, 64: 8}  # ... with this many workgroups per member and layer
+DEFER_LARGE_WG = {16: 16, 32: int(os.environ.get("DTF_DEFER32_WG", "8")),
+                  64: int(os.environ.get("DTF_DEFER64_WG", "8"))}  # ... with this many workgroups per member and layer
 V1_CHAIN_BN = os.environ.get("DTF_V1_CHAIN_BN", "1") == "1"  # v1: BN_b backward sums in the next conv_a epilogue
 # small populations: each stage's run of stride-1 forward convs in one persistent launch with a software grid
 # barrier between layers instead of a kernel boundary (conv_fwd_s1_persist_kernel); up to PERSIST_MAX_POP members

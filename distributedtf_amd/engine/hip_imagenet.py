@@ -75,6 +75,7 @@ CG_FOLD2 = os.environ.get("DTF_CG_FOLD2", "0") == "1"  # measured +2.7 ms: profi
 # weight gradient (wide 1x1 tiles, MX 1), so relu(BN1(x)) is never written for those blocks
 # ... up to this conv1 width (128: one output-channel tile; 256 / 512 re-transform each element 2 / 4 times)
 CG_FOLD1_MAXC = int(os.environ.get("DTF_CG_FOLD1_MAXC", "128"))
+CG_CLASS_LPT = os.environ.get("DTF_CG_CLASS_LPT", "0") == "1"  # stride-2 3x3 data gradient: heavy parity class first
 CG_FOLD1 = os.environ.get("DTF_CG_FOLD1", "1") == "1"  # 73.24 -> 72.87 ms at pop 8 (profiles/r6_imagenet_fold1_ab.log)
 # XCD-aware work order (_xcd_order): 0 off, 1 operand-sharing runs on one XCD, 2 additionally every member on its own
 # XCD when the population is a multiple of 8 with equal work per member, 3 (default) also members on XCD subsets when
@@ -658,7 +659,10 @@ class _ImageNetPlan:
                 trans |= 16  # 32x32x16 MFMA tiles
         elif _CG_BK == 64 and (not trans or a.Ci >= 64):
             trans |= 4  # k depth 64 per LDS stage
-        work = (self._pix_work(hw_in, a.Co, tc, classes=(0, 1, 2, 3), tp=tp) if trans & 1
+        # parity classes of a stride-2 data gradient carry 1 / 2 / 2 / 4 taps (3x3, pad 1): CG_CLASS_LPT dispatches the
+        # 4-tap class first (longest-processing-time order) so the launch does not end on a round of its heaviest items
+        cls = (3, 1, 2, 0) if (CG_CLASS_LPT and k == 3) else (0, 1, 2, 3)
+        work = (self._pix_work(hw_in, a.Co, tc, classes=cls, tp=tp) if trans & 1
                 else self._pix_work(hw_out, a.Co, tc, tp=tp))
         a.work = _p(work)
         self._hold(a)

@@ -36,6 +36,7 @@ import torch
 from distributedtf_amd.data import datasets
 from distributedtf_amd.engine.population import PopulationEngine
 from distributedtf_amd.models.resnet import ResNetArch, cifar_config
+from distributedtf_amd.utils.curves import curve_check, windowed_means
 
 pytestmark = pytest.mark.gpu
 
@@ -53,9 +54,7 @@ def _hp(opt, lr):
 
 
 def _windows(losses):
-    L = torch.stack(losses).float().cpu()  # [steps, members]
-    n = L.shape[0] // WINDOW
-    return L[:n * WINDOW].view(n, WINDOW, -1).mean(dim=1)  # [windows, members]
+    return windowed_means(losses, WINDOW)
 
 
 def _rel(a, b):
@@ -76,28 +75,6 @@ def _recompute_bn_stats(eng, arch, slots, x):
             eng.running[s].copy_(run)
     finally:
         rn.BN_MOMENTUM = mom
-
-
-def _window_check(w_ref, w_r16, w_hip):
-    """Per window and member: (passes, printable [gap, bound, which test passed]) -- see the module docstring."""
-    nw, nm = w_ref.shape
-    ok = torch.zeros(nw, nm, dtype=torch.bool)
-    rows = []
-    for i in range(nw):
-        row = []
-        for s in range(nm):
-            r, h = float(w_ref[i, s]), float(w_hip[i, s])
-            gap = abs(h - r)
-            band = 0.12 + 0.15 * r
-            yard = 2.5 * abs(float(w_r16[i, s]) - r) + 0.05
-            lo_i, hi_i = max(i - 1, 0), min(i + 1, nw - 1)
-            nb = [float(w_ref[j, s]) for j in range(lo_i, hi_i + 1)]
-            shift = min(nb) - band <= h <= max(nb) + band
-            which = "band" if gap <= band else "bf16" if gap <= yard else "shift" if shift else "FAIL"
-            ok[i, s] = which != "FAIL"
-            row.append("[%.3f %.3f %s]" % (gap, max(band, yard), which))
-        rows.append(" ".join(row))
-    return ok, rows
 
 
 @pytest.mark.timeout(900)
@@ -141,7 +118,7 @@ def test_resnet56_trajectory_hip_vs_fp32_oracle(seed):
     ex, ey = ds.eval_set()
     acc_ref = ref.evaluate_population(slots, ex, ey)
     acc_hip = hip.evaluate_population(slots, ex, ey)
-    ok, gap_rows = _window_check(w_ref, w_r16, w_hip)
+    ok, gap_rows = curve_check(w_ref, w_r16, w_hip)
     report = ["window means (ref | bf16 torch | hip) and per-member [gap, bound, test]:"] + [
         "  %s | %s | %s   %s" % (["%.3f" % v for v in r.tolist()], ["%.3f" % v for v in q.tolist()],
                                  ["%.3f" % v for v in h.tolist()], g)

@@ -120,3 +120,24 @@ def test_member_dp_batch_split():
 def test_serving_spec():
     s = serving_input_spec((32, 32, 3), batch_size=8)
     assert s["shape"] == [8, 32, 32, 3]
+
+
+def test_curve_check_bounds():
+    """The trajectory test's per-window bound (utils/curves.py): the round-5 driver failure (Momentum window 2, HIP
+    1.105 vs oracle 0.819, neighbours 1.668 / 0.422) passes as a one-window lag; a curve that stays 0.5 above the
+    oracle on a flat stretch fails; a window where torch bf16 itself sits far from fp32 widens the bound."""
+    import torch
+    from distributedtf_amd.utils.curves import curve_check, windowed_means
+    ref = torch.tensor([[2.273], [1.668], [0.819], [0.422], [0.220]])
+    hip = torch.tensor([[2.269], [1.798], [1.105], [0.588], [0.255]])
+    ok, rows = curve_check(ref, ref, hip)
+    assert ok.all(), rows
+    assert "shift" in rows[2]
+    flat_ref = torch.full((6, 1), 0.05)
+    ok, rows = curve_check(flat_ref, flat_ref, flat_ref + 0.5)
+    assert not ok.any(), rows
+    yard = torch.full((6, 1), 0.45)
+    ok, rows = curve_check(flat_ref, yard, flat_ref + 0.5)
+    assert ok.all() and all("bf16" in r for r in rows), rows
+    w = windowed_means([torch.tensor([1.0, 2.0]), torch.tensor([3.0, 4.0]), torch.tensor([5.0, 6.0])], 2)
+    assert w.shape == (1, 2) and w.tolist() == [[2.0, 3.0]]

@@ -115,6 +115,8 @@ DEFER_MID_CS = (32, 64)
 DEFER_LARGE_CS = (64,)    # larger populations defer the wgrad of these channel widths only ...
 DEFER_LARGE_WG = {16: 16, 32: int(os.environ.get("DTF_DEFER32_WG", "8")),
                   64: int(os.environ.get("DTF_DEFER64_WG", "8"))}  # ... with this many workgroups per member and layer
+DEFER_ATOMIC = os.environ.get("DTF_DEFER_ATOMIC", "0") == "1"  # deferred wgrad jobs: fp32 atomics instead of dW slabs
+DEFER_ATOMIC_CS = tuple(int(c) for c in os.environ.get("DTF_DEFER_ATOMIC_CS", "16,32,64").split(",") if c)
 V1_CHAIN_BN = os.environ.get("DTF_V1_CHAIN_BN", "1") == "1"  # v1: BN_b backward sums in the next conv_a epilogue
 # small populations: each stage's run of stride-1 forward convs in one persistent launch with a software grid
 # barrier between layers instead of a kernel boundary (conv_fwd_s1_persist_kernel); up to PERSIST_MAX_POP members
@@ -1452,7 +1454,10 @@ class _StepPlan:
         w.work = _p(wwork)
         w.n_main = wwork.shape[0]
         self._set_uniform(w, wwork)
-        w.slab = _p(self._layer_slab(wwork.shape[0] * self._slab_elems(C)))
+        # DEFER_ATOMIC (release build): the job's workgroups add their dW partials straight into the gradient rows
+        # (fp32 atomics, a handful of workgroups per address) instead of writing slabs for slab_reduce_all
+        atomic = DEFER_ATOMIC and not self.be.det and C in DEFER_ATOMIC_CS
+        w.slab = None if atomic else _p(self._layer_slab(wwork.shape[0] * self._slab_elems(C)))
         w.cin_real = -1
         self._wg_jobs.setdefault((C, wmode), []).append((w, wwork, c.off))
 
@@ -1477,7 +1482,8 @@ class _StepPlan:
                     j = len(arr_l)
                     arr_l.append(w)
                     wmap += [(j, k, C, wmode) for k in range(w.n_main)]
-                    self._deferred.append((w.slab, self._slab_table(work), goff, C))
+                    if w.slab:  # (None: the job accumulates with atomics, DEFER_ATOMIC)
+                        self._deferred.append((w.slab, self._slab_table(work), goff, C))
             if not arr_l:
                 continue
             arr = (ConvArgs * len(arr_l))(*arr_l)

@@ -157,3 +157,34 @@ def test_hip_mnist_repeat_learns():
     L = torch.stack(L)
     assert torch.isfinite(L).all()
     assert (L[-3:].mean(0) < L[:3].mean(0)).all(), L
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_mnist_train_probabilities(dtype):
+    """The "probabilities" hook's source (reference mnist_model.py:149-151): with keep_probs set before the first
+    step, the HIP training plan also writes the head's logits, and train_probabilities returns each member's softmax
+    of its last batch -- rows sum to 1 and their argmax agrees with the head kernel's own correct count."""
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    sizes = [40, 72]
+    e = PopulationEngine(MnistArch(), len(sizes), dev, backend="hip", compute_dtype=dtype)
+    e.backend.keep_probs = True
+    hps = []
+    for i, bs in enumerate(sizes):
+        hp = {"opt_case": {"optimizer": "Adam", "lr": 1e-3}, "batch_size": bs, "initializer": "he_init"}
+        e.add_member(None, hp, seed=5 + i)
+        hps.append(hp)
+    g = torch.Generator().manual_seed(1)
+    batches = [((torch.rand(bs, 28, 28, 1, generator=g) * 255).to(dev), torch.randint(0, 10, (bs,), generator=g).to(dev))
+               for bs in sizes]
+    for _ in range(2):
+        e.train_step([0, 1], batches, hps, [1e-3, 1e-3])
+    torch.cuda.synchronize()
+    probs = e.backend.train_probabilities([0, 1])
+    corr = e.backend.train_correct([0, 1]).cpu().tolist()
+    for s, (p, (x, y)) in enumerate(zip(probs, batches)):
+        assert p is not None and tuple(p.shape) == (sizes[s], 10)
+        assert torch.isfinite(p).all()
+        torch.testing.assert_close(p.sum(dim=1), torch.ones(sizes[s], device=dev), atol=1e-5, rtol=0)
+        hits = int((p.argmax(dim=1) == y).sum())
+        assert hits == int(round(corr[s])), (s, hits, corr[s])

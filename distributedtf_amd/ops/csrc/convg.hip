@@ -432,6 +432,9 @@ __device__ __forceinline__ void convg_epilogue_regs(const CgArgs& a, f32x4_t (&a
 // TC = 128 2 x 2 waves of 64 x 128 (32 MFMAs per wave and k-step; the epilogue is staged in 64-pixel quarters).
 // M32: v_mfma_f32_32x32x16_bf16 tiles (a wave's TC/WRN x PW block as 32 x 32 MFMA tiles: half the MFMA
 // instructions of the 16x16x32 form for the same fragment reads; plain-A (non-AKM) forward only)
+#ifndef CG_XF_VEC
+#define CG_XF_VEC 1  // generic kernel: BN transform coefficients of a k-step read as 16-byte LDS rows (else per element)
+#endif
 #ifndef CG_EPI_REGS
 #define CG_EPI_REGS 0  // generic kernel: register-direct epilogue (convg_epilogue_regs) for the 16x16 tiles
 #endif
@@ -457,7 +460,7 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t smem_[SOPS > SEPI ? SOPS : SEPI];
   bf16_t (*sa)[SA] = reinterpret_cast<bf16_t (*)[SA]>(smem_);
   bf16_t (*sb)[TP * RP] = reinterpret_cast<bf16_t (*)[TP * RP]>(smem_ + 2 * SA);
-  extern __shared__ float dyn[];  // transform coefficients: MODE 1: 2*Ci, MODE 2: 3*Ci
+  extern __shared__ __attribute__((aligned(16))) float dyn[];  // transform coefficients: MODE 1: 2*Ci, MODE 2: 3*Ci
   __shared__ dtf_acc_t acc_lds[2][TC];
   const int4 wk = a.work[blockIdx.x];
   DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z >= wk.y);
@@ -589,6 +592,31 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
     }
   };
   auto xform_store = [&](bf16_t* dst, const uint4 (&v)[NJ], const uint4 (&v2)[NJ], int cch, unsigned okb) {
+    // this thread's 8 channels cch..cch+7 are the same for all NJ chunks of the k-step: their coefficients are read
+    // once per k-step as 16-byte LDS rows (CG_XF_VEC; the element-wise form issued 2-3 scalar LDS reads per element)
+    float ca[8], cb[8], cc[8];
+    if constexpr (MODE != 0) {
+#if CG_XF_VEC
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float4 a4 = *reinterpret_cast<const float4*>(dyn + cch + 4 * h);
+        const float4 b4 = *reinterpret_cast<const float4*>(dyn + Ci + cch + 4 * h);
+        ca[4 * h] = a4.x, ca[4 * h + 1] = a4.y, ca[4 * h + 2] = a4.z, ca[4 * h + 3] = a4.w;
+        cb[4 * h] = b4.x, cb[4 * h + 1] = b4.y, cb[4 * h + 2] = b4.z, cb[4 * h + 3] = b4.w;
+        if constexpr (MODE == 2) {
+          const float4 c4 = *reinterpret_cast<const float4*>(dyn + 2 * Ci + cch + 4 * h);
+          cc[4 * h] = c4.x, cc[4 * h + 1] = c4.y, cc[4 * h + 2] = c4.z, cc[4 * h + 3] = c4.w;
+        }
+      }
+#else
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        ca[e] = dyn[cch + e];
+        cb[e] = dyn[Ci + cch + e];
+        if constexpr (MODE == 2) cc[e] = dyn[2 * Ci + cch + e];
+      }
+#endif
+    }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       uint4 t = v[j];
@@ -599,15 +627,14 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
         const uint32_t h32[4] = {v2[j].x, v2[j].y, v2[j].z, v2[j].w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int c = cch + 2 * q;
           float x0 = lo2f(w32[q]), x1 = hi2f(w32[q]);
           if constexpr (MODE == 1) {
-            x0 = fmaxf(x0 * dyn[c] + dyn[Ci + c], 0.f);
-            x1 = fmaxf(x1 * dyn[c + 1] + dyn[Ci + c + 1], 0.f);
+            x0 = fmaxf(x0 * ca[2 * q] + cb[2 * q], 0.f);
+            x1 = fmaxf(x1 * ca[2 * q + 1] + cb[2 * q + 1], 0.f);
           } else {
             const float h0 = lo2f(h32[q]), h1 = hi2f(h32[q]);
-            x0 = dyn[c] * x0 + dyn[Ci + c] * h0 + dyn[2 * Ci + c];
-            x1 = dyn[c + 1] * x1 + dyn[Ci + c + 1] * h1 + dyn[2 * Ci + c + 1];
+            x0 = ca[2 * q] * x0 + cb[2 * q] * h0 + cc[2 * q];
+            x1 = ca[2 * q + 1] * x1 + cb[2 * q + 1] * h1 + cc[2 * q + 1];
           }
           w32[q] = pack2bf(x0, x1);
         }

@@ -124,19 +124,20 @@ def test_rccl_bench_two_ranks(tmp_path):
 
 
 @pytest.mark.timeout(400)
-def test_rccl_bench_eight_ranks(tmp_path):
-    """The driver's N = 8 headline command, rehearsed on the 1-GPU box: 8 ranks, one member
-    each (the per-GPU work of the 8-GPU headline), an 8-rank RCCL communicator with every pair pre-connected, and
-    >= 2 exploit cycles inside the timed region -- each k = 2 cycle moves two disjoint cross-rank winner->loser
-    pairs in one batch_isend_irecv (parallel/dataplane.py)."""
-    rc, log = _torchrun(["bench.py", "--gpus", "8", "--steps", "40"], tmp_path, tag="bench8", nproc=8,
+@pytest.mark.parametrize("n", [4, 8])
+def test_rccl_bench_eight_ranks(tmp_path, n):
+    """The driver's N = 4 / 8 headline commands, rehearsed on the 1-GPU box: n ranks, 8 / n
+    members each (N = 8: the per-GPU work of the 8-GPU headline), an n-rank RCCL communicator with every pair
+    pre-connected, and >= 2 exploit cycles inside the timed region -- at N = 8 each k = 2 cycle moves two disjoint
+    cross-rank winner->loser pairs in one batch_isend_irecv (parallel/dataplane.py)."""
+    rc, log = _torchrun(["bench.py", "--gpus", str(n), "--steps", "40"], tmp_path, tag="bench%d" % n, nproc=n,
                         timeout=360)
     assert rc == 0, log[-4000:]
     lines = [json.loads(x) for x in log.splitlines() if x.startswith("{")]
     assert len(lines) == 1, log[-3000:]
     rec = lines[0]
     print(json.dumps(rec))
-    assert rec["n_gpus"] == 8 and rec["steps"] == 40 and rec["value"] > 0, rec
+    assert rec["n_gpus"] == n and rec["steps"] == 40 and rec["value"] > 0, rec
     assert rec["config"]["exploits_timed"] >= 2, rec
     assert rec["config"]["p2p_preconnected"] is True and rec["config"]["step_graph"] == "captured", rec
-    assert rec["config"]["parallelism"] == "pbt_pop8_1members_per_gpu", rec
+    assert rec["config"]["parallelism"] == "pbt_pop8_%dmembers_per_gpu" % (8 // n), rec

@@ -33,6 +33,12 @@
 #ifndef DTF_FUSED16_WLDS
 #define DTF_FUSED16_WLDS 1  // C = 16 fused backward: dgrad weights read from LDS per MFMA instead of held in VGPRs
 #endif
+#ifndef DTF_WGRAD_PF2
+#define DTF_WGRAD_PF2 0  // 1: deferred wgrad jobs with tiles prefetched two iterations ahead (conv_wgrad_pf2_body): measured +0.8 % at pop 8, flat at C = 16 only (profiles/r6_wgrad_pf2_ab.log)
+#endif
+#ifndef DTF_WGRAD_PF2_MAXC
+#define DTF_WGRAD_PF2_MAXC 64  // ... for the channel widths up to this
+#endif
 #ifndef DTF_COEF_SPLIT
 #define DTF_COEF_SPLIT 1  // C < 64: wave 0's 64 / C lane groups split the statistic replicas (shuffle-summed)
 #endif
@@ -2094,6 +2100,183 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
   STAMP_FLUSH(a.cin_real, nit);
 }
 
+// Weight-gradient role with the input tiles prefetched TWO (image, band) iterations ahead (two register sets; the
+// loop unrolled by two so each set is a compile-time array).  Same operands, staging transforms, MFMA order and slab
+// layout as conv_bwd_body<C, MODE_DY, 0, 2> -- bitwise the same partials -- for the deferred jobs of
+// conv_wgrad_all_kernel: one round of staging loads in flight behind the MFMAs was not enough to cover the L2 /
+// MALL latency of these 1-2-workgroups-per-CU launches (C = 64: ~1 TB/s of traffic, 3x its MFMA + HBM floor).
+template <int C, int MODE_DY>
+__device__ __forceinline__ void conv_wgrad_pf2_body(const ConvArgs& a, const int bid, char* smem) {
+  static_assert(MODE_DY == 0 || MODE_DY == 2, "deferred wgrad jobs: plain dY or BN-backward(dz, h)");
+  constexpr int ROWS = 8, W = 512 / C, H = W, BANDS = H / ROWS;
+  constexpr int MT = C / 16, NTN = 9 * C / 16, NJ = (NTN + 3) / 4;
+  constexpr int CP = cpad<C>(), RT = ROWS + 2, WP = wpitch<C>();
+  constexpr int TSZ = (RT * WP * CP + 8 + 63) & ~63;
+  constexpr int IMG = H * W * C;
+  constexpr int NK = ROWS * W / 32, RSTEP = 32 / W, KINC = RSTEP * WP * CP;
+  using St = Stage<C, RT, W, H, CP, WP>;
+  constexpr int MAXC = St::MAXC;
+  float* coef_d = reinterpret_cast<float*>(smem);
+  float* ecoef = coef_d + 192;
+  bf16_t* t0 = reinterpret_cast<bf16_t*>(smem + 2304);
+#define PDBUF(i) (t0 + ((i) & 1) * 2 * TSZ)
+#define PXBUF(i) (t0 + TSZ + ((i) & 1) * 2 * TSZ)
+  const bf16_t* k_x = a.x;
+  const bf16_t* k_x2 = a.x2;
+  const bf16_t* k_xm = a.xm;
+  const float* k_st_in = a.st_in;
+  const float* k_st_in_b = a.st_in_b;
+  const float* k_st_ep = a.st_ep;
+  const float* k_params = a.params;
+  const float* k_cnt = a.cnt;
+  float* k_slab = a.slab;
+  float* k_grads = a.grads;
+  const int4* k_work = a.work;
+  int k_in_gamma = a.in_gamma, k_in_beta = a.in_beta, k_ep_gamma = a.ep_gamma, k_ep_beta = a.ep_beta;
+  long k_p_mstride = a.p_mstride, k_g_mstride = a.g_mstride, k_g_off = a.g_off;
+  int k_u_items = a.u_items, k_u_chunk = a.u_chunk, k_u_per = a.u_per;
+  kpin(k_x); kpin(k_x2); kpin(k_xm); kpin(k_st_in); kpin(k_st_in_b); kpin(k_st_ep); kpin(k_params); kpin(k_cnt);
+  kpin(k_slab); kpin(k_grads); kpin(k_work); kpin(k_in_gamma); kpin(k_in_beta); kpin(k_ep_gamma); kpin(k_ep_beta);
+  kpin(k_p_mstride); kpin(k_g_mstride); kpin(k_g_off); kpin(k_u_items); kpin(k_u_chunk); kpin(k_u_per);
+  int4 wk;
+  if (k_u_items > 0) {
+    const int m = bid / k_u_items, kk = bid - m * k_u_items, it0_ = kk * k_u_chunk;
+    wk = make_int4(m * k_u_per + it0_, min(k_u_chunk, k_u_per - it0_), 0, m);
+  } else {
+    wk = k_work[bid];
+    wk = make_int4(__builtin_amdgcn_readfirstlane(wk.x), __builtin_amdgcn_readfirstlane(wk.y),
+                   __builtin_amdgcn_readfirstlane(wk.z), __builtin_amdgcn_readfirstlane(wk.w));
+  }
+  DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.w >= 0 && wk.z >= 0 && a.Hi > 0 && a.Wi > 0 && a.rows > 0);
+  const int it0 = wk.x, nit = wk.y, slot = wk.w;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  CoefLd<MODE_DY == 0 ? 0 : 2> cld;
+  coef_issue<C, MODE_DY == 0 ? 0 : 2>(cld, k_params, k_p_mstride, slot, k_st_in, k_st_in_b, k_in_gamma, k_in_beta);
+  CoefLd<1> cle;
+  coef_issue<C, 1>(cle, k_params, k_p_mstride, slot, k_st_ep, nullptr, k_ep_gamma, k_ep_beta);
+  const float n_hw = k_cnt[slot] * (float)(H * W);
+  St st;
+  st.init();
+  // two register sets: set A holds the even iterations' tiles, set B the odd ones
+  uint4 dA[MAXC], d2A[MAXC], xA[MAXC], dB[MAXC], d2B[MAXC], xB[MAXC], unused[MAXC];
+  unsigned mA = 0, mB = 0;
+  int gA = 0, gB = 0;  // first tile row of the staged band (for the staging masks)
+  auto issue = [&](int it, uint4 (&d)[MAXC], uint4 (&d2)[MAXC], uint4 (&xv)[MAXC], unsigned& m, int& gy0) {
+    const int img = it / BANDS;
+    gy0 = (it % BANDS) * ROWS - 1;
+    m = st.mask(gy0);
+    st.template load<MODE_DY>(d, d2, m, k_x + img * IMG, k_x2 + img * IMG, gy0);
+    st.template load<1>(xv, unused, m, k_xm + img * IMG, nullptr, gy0);
+  };
+  auto put = [&](int k, const uint4 (&d)[MAXC], const uint4 (&d2)[MAXC], const uint4 (&xv)[MAXC], unsigned m,
+                 int gy0) {
+    if constexpr (MODE_DY >= 2)
+      st.template store_x<2>(PDBUF(k), d, d2, unused, m, coef_d, nullptr, gy0);
+    else
+      st.template store<MODE_DY>(PDBUF(k), d, d2, m, coef_d);
+    st.template store<1>(PXBUF(k), xv, unused, m, ecoef);
+  };
+  issue(it0, dA, d2A, xA, mA, gA);
+  if (nit > 1) issue(it0 + 1, dB, d2B, xB, mB, gB);
+  coef_reduce<C, MODE_DY == 0 ? 0 : 2>(cld);
+  coef_reduce<C, 1>(cle);
+  coef_finish<C, MODE_DY == 0 ? 0 : 2>(coef_d, cld, n_hw);
+  if (threadIdx.x < C) {
+    float mean, inv;
+    coef_moments<1>(cle, n_hw, mean, inv);
+    const float scale = cle.g * inv;
+    ecoef[threadIdx.x] = scale;
+    ecoef[64 + threadIdx.x] = cle.b - mean * scale;
+  }
+  const int g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
+  const int pa = 8 * g + q, pb = pa + 4;
+  const int da_off = ((pa / W + 1) * WP + pa % W + 1) * CP + 4 * p4;
+  const int db_off = ((pb / W + 1) * WP + pb % W + 1) * CP + 4 * p4;
+  const int xa_off = ((pa / W) * WP + pa % W) * CP + 4 * p4, xb_off = ((pb / W) * WP + pb % W) * CP + 4 * p4;
+  int boff[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int nt = min(wave + 4 * j, NTN - 1);
+    const int tap = (nt * 16) / C, cb = (nt * 16) % C;
+    boff[j] = ((tap / 3) * WP + (tap % 3)) * CP + cb;
+  }
+  f32x4_t wacc[NJ][MT];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) wacc[j][m] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  __syncthreads();  // coefficients
+  put(0, dA, d2A, xA, mA, gA);
+  __syncthreads();
+  auto mfmas = [&](int k) {
+    const bf16_t* dcur = PDBUF(k);
+    const bf16_t* xcur = PXBUF(k);
+#pragma unroll
+    for (int ks = 0; ks < NK; ++ks) {
+      bf16x8_t af[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        s16x4_t lo = ds_read_tr(dcur + da_off + ks * KINC + m * 16);
+        s16x4_t hi = ds_read_tr(dcur + db_off + ks * KINC + m * 16);
+        af[m] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      bf16x8_t bfr[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        s16x4_t lo = ds_read_tr(xcur + xa_off + ks * KINC + boff[j]);
+        s16x4_t hi = ds_read_tr(xcur + xb_off + ks * KINC + boff[j]);
+        bfr[j] = (bf16x8_t){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) wacc[j][m] = mfma16(af[m], bfr[j], wacc[j][m]);
+    }
+  };
+  // iteration k: tiles of k + 1 sit in the other register set (loaded an iteration ago), k + 2 is issued into the set
+  // that held k (already in LDS)
+  for (int k = 0; k < nit; k += 2) {
+    if (k + 2 < nit) issue(it0 + k + 2, dA, d2A, xA, mA, gA);
+    mfmas(k);
+    if (k + 1 < nit) put(k + 1, dB, d2B, xB, mB, gB);
+    __syncthreads();
+    if (k + 1 >= nit) break;
+    if (k + 3 < nit) issue(it0 + k + 3, dB, d2B, xB, mB, gB);
+    mfmas(k + 1);
+    if (k + 2 < nit) put(k + 2, dA, d2A, xA, mA, gA);
+    __syncthreads();
+  }
+#undef PDBUF
+#undef PXBUF
+  if (k_slab) {
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(k_slab + (long)bid * (NJ * MT * 4 * 256), 0,
+                                                       NJ * MT * 4 * 256 * 4, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, wacc[j][m]), rsrc,
+                                               (((j * MT + m) * 256) + (int)threadIdx.x) * 16, 0, 16);
+    return;
+  }
+  float* gb = k_grads + (long)slot * k_g_mstride + k_g_off;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int nt = wave + 4 * j;
+    if (nt < NTN) {
+      const int tap = (nt * 16) / C, ci = (nt * 16) % C + (lane & 15);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = m * 16 + 4 * (lane >> 4) + r;
+          atomicAdd(gb + ((long)co * 9 + tap) * C + ci, wacc[j][m][r]);
+        }
+      }
+    }
+  }
+}
+
 // Trailing workgroups of a backward launch: dW slab reduction of the PREVIOUS launch (r = index among them).
 __device__ __forceinline__ void trailing_reduce(const ConvArgs& a, int r, char* smem) {
   float* part = reinterpret_cast<float*>(smem);
@@ -2158,10 +2341,20 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_all_kernel(const ConvArgs* 
   const int4 m = map[blockIdx.x];
   const int j = __builtin_amdgcn_readfirstlane(m.x), bid = __builtin_amdgcn_readfirstlane(m.y);
   const int c = __builtin_amdgcn_readfirstlane(m.z), mode = __builtin_amdgcn_readfirstlane(m.w);
+  // (the <64, 32> kernel runs one wave per SIMD either way: 300 VGPRs one-ahead, 502 with the two C = 64 register
+  // sets; <16, 16> stays LDS-bound at 3 workgroups per CU: 108 -> 140 VGPRs)
   if (c == CA) {
-    if (mode == 0) conv_bwd_body<CA, 0, 0, 2>(jobs[j], bid, smem); else conv_bwd_body<CA, 2, 0, 2>(jobs[j], bid, smem);
+    if constexpr (DTF_WGRAD_PF2 && CA <= DTF_WGRAD_PF2_MAXC) {
+      if (mode == 0) conv_wgrad_pf2_body<CA, 0>(jobs[j], bid, smem); else conv_wgrad_pf2_body<CA, 2>(jobs[j], bid, smem);
+    } else {
+      if (mode == 0) conv_bwd_body<CA, 0, 0, 2>(jobs[j], bid, smem); else conv_bwd_body<CA, 2, 0, 2>(jobs[j], bid, smem);
+    }
   } else if constexpr (CB != CA) {
-    if (mode == 0) conv_bwd_body<CB, 0, 0, 2>(jobs[j], bid, smem); else conv_bwd_body<CB, 2, 0, 2>(jobs[j], bid, smem);
+    if constexpr (DTF_WGRAD_PF2 && CB <= DTF_WGRAD_PF2_MAXC) {
+      if (mode == 0) conv_wgrad_pf2_body<CB, 0>(jobs[j], bid, smem); else conv_wgrad_pf2_body<CB, 2>(jobs[j], bid, smem);
+    } else {
+      if (mode == 0) conv_bwd_body<CB, 0, 0, 2>(jobs[j], bid, smem); else conv_bwd_body<CB, 2, 0, 2>(jobs[j], bid, smem);
+    }
   }
 }
 

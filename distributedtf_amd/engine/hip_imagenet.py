@@ -75,6 +75,9 @@ CG_FOLD2 = os.environ.get("DTF_CG_FOLD2", "0") == "1"  # measured +2.7 ms: profi
 # weight gradient (wide 1x1 tiles, MX 1), so relu(BN1(x)) is never written for those blocks
 # ... up to this conv1 width (128: one output-channel tile; 256 / 512 re-transform each element 2 / 4 times)
 CG_FOLD1_MAXC = int(os.environ.get("DTF_CG_FOLD1_MAXC", "128"))
+# stride-2 projection data gradient computed / stored compact at the dy resolution (3/4 of its full-resolution
+# tensor is zeros) and added by conv1's epilogue at even pixels
+CG_COMPACT_PD = os.environ.get("DTF_CG_COMPACT_PD", "1") == "1"
 CG_CLASS_LPT = os.environ.get("DTF_CG_CLASS_LPT", "0") == "1"  # stride-2 3x3 data gradient: heavy parity class first
 CG_FOLD1 = os.environ.get("DTF_CG_FOLD1", "1") == "1"  # 73.24 -> 72.87 ms at pop 8 (profiles/r6_imagenet_fold1_ab.log)
 # XCD-aware work order (_xcd_order): 0 off, 1 operand-sharing runs on one XCD, 2 additionally every member on its own
@@ -584,8 +587,11 @@ class _ImageNetPlan:
         return self.be.sums[1, bn]
 
     def conv(self, ci, src, out, hw_in, mode=0, c_in=None, x2=None, epi=0, res=None, xm=None, c_ep=None, st=None,
-             dgrad=False):
-        """Forward conv (dgrad=False) or data gradient (dgrad=True) of conv `ci` through convg_fwd."""
+             dgrad=False, compact=False):
+        """Forward conv (dgrad=False) or data gradient (dgrad=True) of conv `ci` through convg_fwd.  ``compact``
+        (the data gradient of a stride-2 1x1 conv): only the even output rows / columns are nonzero, so the gradient
+        is computed and stored at the dy resolution, [N, hw_in, hw_in, cin] -- a plain 1x1 GEMM with no zero-filled
+        parity classes; its consumer reads it with convg EPI bit 8."""
         be = self.be
         c = self.be.prog.convs[ci]
         k = c.k
@@ -605,6 +611,13 @@ class _ImageNetPlan:
             a.Ho = a.Wo = hw_out
             a.stride, a.pad = c.stride, pad
             trans = 0
+        elif compact:
+            assert k == 1 and c.stride == 2 and pad == 0, (ci, k, c.stride)
+            hw_out = hw_in
+            a.Hi = a.Wi = a.Ho = a.Wo = hw_in
+            a.Ci, a.Co = c.cout, c.cin
+            a.stride, a.pad = 1, 0
+            trans = 2
         else:
             # gathered = dy at the conv's output resolution; output = dx at its input resolution
             hw_out = hw_in * c.stride
@@ -837,6 +850,7 @@ class _ImageNetPlan:
         self._add("gemm", self.g_wgr)
 
     FOLD1_OK = True  # the fp32 plan (hip_imagenet_f32.py) keeps the materialised relu(BN1(x))
+    COMPACT_PD_OK = True  # ... and the full-resolution projection data gradient
 
     def _fold1(self, i):
         """Block i's BN1 + ReLU is applied by conv1 itself (CG_FOLD1: no projection, one output-channel tile)."""
@@ -944,17 +958,22 @@ class _ImageNetPlan:
             else:
                 self.wgrad(c2, self.a1[i], dh2, hi)
             pd = None
+            cpd = False
             if blk.proj is not None:
-                pd = self.tmp("pd", hi, cin)
-                self.conv(blk.proj, gcur, pd, ho, mode=0, epi=0, dgrad=True)
+                pc = prog.convs[blk.proj]
+                # a stride-2 projection's data gradient is zero at odd rows / columns: kept compact at the dy
+                # resolution and added by conv1's epilogue at the even pixels (CG_COMPACT_PD)
+                cpd = CG_COMPACT_PD and self.COMPACT_PD_OK and pc.stride == 2 and pc.k == 1
+                pd = self.tmp("pdc" if cpd else "pd", ho if cpd else hi, cin)
+                self.conv(blk.proj, gcur, pd, ho, mode=0, epi=0, dgrad=True, compact=cpd)
                 if self.fold:
                     self.wgrad(blk.proj, x, gcur, hi, mode_x=1, c_x=self.cf(b1))
                 else:
                     self.wgrad(blk.proj, self.ax[i], gcur, hi)
             # conv1: dz1 = (dgrad(dh1) [+ projection dgrad]) masked by BN1(x); g_in = BN1-backward(dz1, x) [+ g]
             dz1 = self.tmp("dz1", hi, cin)
-            self.conv(c1, dh1, dz1, hi, mode=0, epi=6 | (1 if pd is not None else 0), res=pd, xm=x,
-                      c_ep=self.cf(b1), st=self.sb(b1), dgrad=True)
+            self.conv(c1, dh1, dz1, hi, mode=0, epi=6 | (1 if pd is not None else 0) | (8 if cpd else 0), res=pd,
+                      xm=x, c_ep=self.cf(b1), st=self.sb(b1), dgrad=True)
             self.bn_final(b1, hi, True)
             if self.fold or self._fold1(i):
                 self.wgrad(c1, x, dh1, hi, mode_x=1, c_x=self.cf(b1))

@@ -117,6 +117,7 @@ class HipImageNetF32Backend(HipImageNetBackend):
 
 class _ImageNetF32Plan(_ImageNetPlan):
     FOLD1_OK = False  # (the fp32 conv kernels are not exercised with the read-once BN1 fold)
+    COMPACT_PD_OK = False  # (nor with the compact stride-2 projection gradient: f32conv has no EPI bit 8)
 
     def _act_dtype(self):
         return torch.float32
@@ -161,7 +162,8 @@ class _ImageNetF32Plan(_ImageNetPlan):
         self._add(ops.lib().dtf_f32_conv, ctypes.byref(a), tc, mode, epi, int(dgrad), work.shape[0])
 
     def conv(self, ci, src, out, hw_in, mode=0, c_in=None, x2=None, epi=0, res=None, xm=None, c_ep=None, st=None,
-             dgrad=False):
+             dgrad=False, compact=False):
+        assert not compact and not (epi & 8), "the fp32 plan keeps the full-resolution projection gradient"
         be = self.be
         c = be.prog.convs[ci]
         stem = ci == be.prog.stem

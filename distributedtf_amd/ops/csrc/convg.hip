@@ -176,7 +176,17 @@ __device__ __forceinline__ void convg_epilogue_impl(const CgArgs& a, StageFn&& s
       }
       orow[it] = (p < p1 && cok) ? pf * a.Co + oc : -1;
       rrv[it] = xrv[it] = make_uint4(0, 0, 0, 0);
-      if constexpr (EPI & 1) rrv[it] = ld16(a.res, orow[it], orow[it] >= 0);
+      if constexpr ((EPI & 8) != 0) {
+        // EPI bit 8: the residual is a stride-2 1x1 projection's data gradient stored compact, [N][Ho/2][Wo/2][Co]
+        // (it is zero at every odd row / column of the full-resolution output): read it at even (y, x) only
+        static_assert(!TRANS && (EPI & 1), "compact residual: full-grid output, residual add");
+        const int img = p / HWo, rem = p - img * HWo, y = rem / GW, x = rem - y * GW;
+        const bool ev = orow[it] >= 0 && ((y | x) & 1) == 0;
+        const long ro = (((long)img * (a.Ho >> 1) + (y >> 1)) * (a.Wo >> 1) + (x >> 1)) * a.Co + oc;
+        rrv[it] = ld16(a.res, ro, ev);
+      } else if constexpr (EPI & 1) {
+        rrv[it] = ld16(a.res, orow[it], orow[it] >= 0);
+      }
       if constexpr (EPI & 2) xrv[it] = ld16(a.xm, orow[it], orow[it] >= 0);
     }
 #pragma unroll
@@ -317,6 +327,7 @@ template <int TC, int EPI, int TP, int WRN, bool TRANS = false>
 __device__ __forceinline__ void convg_epilogue_regs(const CgArgs& a, f32x4_t (&acc)[TC / WRN / 16][TP / (4 / WRN) / 16],
                                                     dtf_acc_t (&acc_lds)[2][TC], int slot, int o0, int p0, int p1,
                                                     int HWo = 0, int GW = 0, int py = 0, int px = 0) {
+  static_assert(!(EPI & 8), "the compact projection residual is read by the LDS-staged epilogue only");
   constexpr int PW = TP / (4 / WRN), NTP = PW / 16, MT = TC / WRN / 16;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wr = wave % WRN, wc = wave / WRN;
@@ -1866,6 +1877,7 @@ DTF_API int dtf_convg_fwd(const CgArgs* a, int tc, int mode, int epi, int trans,
   CG_ALL_TC(2, 6, false, 1)
   CG_ALL_TC(2, 7, false, 1)
   CG_ALL_TC(0, 7, false, 1)
+  CG_ALL_TC(0, 15, false, 1)  // + the compact stride-2 projection gradient (v2 bottleneck conv1 of a stage's first block)
   CG_ALL_TC(0, 0, false, 1)
   CG_ALL_TC(2, 0, false, 1)
   CG_ALL_TC(0, 3, false, 1)  // v1 bottleneck conv1: + shortcut gradient, masked by the block input's ReLU

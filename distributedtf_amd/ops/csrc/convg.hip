@@ -1407,6 +1407,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ?
       xval[j] = ok;
     }
   };
+  // MX 1: the BN scale / shift of chunk j's 8 channels.  When 256 is a multiple of the chunks per tile row
+  // (WWT = 256: the 1x1 tiles), every chunk j of a thread sits in the same column, so its 16 coefficients are read
+  // from LDS once for the whole kernel (XCOL) instead of 4 16-byte reads per chunk and k-step -- as many LDS reads
+  // as the k-step's MFMA operand fetches
+  constexpr bool XCOL = MX == 1 && (256 % (WWT / 8)) == 0;
+  float xsc[XCOL ? 8 : 1], xsh[XCOL ? 8 : 1];
+  auto coef8 = [&](int c0, float (&sc)[8], float (&sh)[8]) {
+    const float4 s0 = *reinterpret_cast<const float4*>(xcoef + c0), s1 = *reinterpret_cast<const float4*>(xcoef + c0 + 4);
+    const float4 h0 = *reinterpret_cast<const float4*>(xcoef + Ci + c0),
+                 h1 = *reinterpret_cast<const float4*>(xcoef + Ci + c0 + 4);
+    sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+    sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w; sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
+  };
   auto store = [&](bf16_t* d, bf16_t* xx, const uint4 (&dv)[DJ], const uint4 (&xv)[WXJ]) {
 #pragma unroll
     for (int j = 0; j < DJ; ++j) *reinterpret_cast<uint4*>(d + kperm(drow[j]) * WWOP + dch[j]) = dv[j];
@@ -1416,14 +1429,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ?
       uint4 t = xv[j];
       if constexpr (MX == 1) {
         // a padding / out-of-range chunk (loaded as zeros) must stay zero after the transform
-        float sc[8], sh[8];
-        const int c0 = xoff[j] >> 16;
-        const float4 s0 = *reinterpret_cast<const float4*>(xcoef + c0), s1 = *reinterpret_cast<const float4*>(xcoef + c0 + 4);
-        const float4 h0 = *reinterpret_cast<const float4*>(xcoef + Ci + c0),
-                     h1 = *reinterpret_cast<const float4*>(xcoef + Ci + c0 + 4);
-        sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
-        sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w; sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
-        t = xval[j] ? bnrelu8(t, sc, sh) : make_uint4(0, 0, 0, 0);
+        if constexpr (XCOL) {
+          t = xval[j] ? bnrelu8(t, xsc, xsh) : make_uint4(0, 0, 0, 0);
+        } else {
+          float sc[8], sh[8];
+          coef8(xoff[j] >> 16, sc, sh);
+          t = xval[j] ? bnrelu8(t, sc, sh) : make_uint4(0, 0, 0, 0);
+        }
       }
       *reinterpret_cast<uint4*>(xx + (xoff[j] & 0xffff)) = t;
     }
@@ -1438,6 +1450,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ?
   make_pinfo(p0);
   if (nk > 1) make_pinfo(p0 + 32);
   __syncthreads();
+  if constexpr (XCOL) coef8(xoff[0] >> 16, xsc, xsh);  // (the xcoef rows are visible after the barrier above)
   uint4 dv[DJ], xv[WXJ];
   load(p0, dv, xv);
   store(sd[0], sx[0], dv, xv);

@@ -73,8 +73,10 @@ CG_FOLD2 = os.environ.get("DTF_CG_FOLD2", "0") == "1"  # measured +2.7 ms: profi
 # exactly once -- blocks without a projection (the block input's only forward consumer is conv1) whose conv1 runs a
 # single output-channel tile (Co <= 128: every workgroup holds all output channels of its pixels) -- and by conv1's
 # weight gradient (wide 1x1 tiles, MX 1), so relu(BN1(x)) is never written for those blocks
-# ... up to this conv1 width (128: one output-channel tile; 256 / 512 re-transform each element 2 / 4 times)
-CG_FOLD1_MAXC = int(os.environ.get("DTF_CG_FOLD1_MAXC", "128"))
+# ... up to this conv1 width (128: one output-channel tile; 256 / 512 re-transform each element 2 / 4 times).  With the
+# wide wgrad's coefficients read once per kernel, 256 measured 70.2 vs 70.7 ms (128) and 70.4 ms (512)
+# (profiles/r6_imagenet_fold_xcol_ab.log)
+CG_FOLD1_MAXC = int(os.environ.get("DTF_CG_FOLD1_MAXC", "256"))
 # stride-2 projection data gradient computed / stored compact at the dy resolution (3/4 of its full-resolution
 # tensor is zeros) and added by conv1's epilogue at even pixels
 CG_COMPACT_PD = os.environ.get("DTF_CG_COMPACT_PD", "1") == "1"

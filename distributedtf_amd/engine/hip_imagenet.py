@@ -81,7 +81,12 @@ CG_FOLD1_MAXC = int(os.environ.get("DTF_CG_FOLD1_MAXC", "256"))
 # tensor is zeros) and added by conv1's epilogue at even pixels
 CG_COMPACT_PD = os.environ.get("DTF_CG_COMPACT_PD", "1") == "1"
 CG_CLASS_LPT = os.environ.get("DTF_CG_CLASS_LPT", "0") == "1"  # stride-2 3x3 data gradient: heavy parity class first
-CG_FOLD1 = os.environ.get("DTF_CG_FOLD1", "1") == "1"  # 73.24 -> 72.87 ms at pop 8 (profiles/r6_imagenet_fold1_ab.log)
+CG_FOLD1 = os.environ.get("DTF_CG_FOLD1", "1") == "1"
+# BN3 + ReLU applied by conv3 (the 1x1 expand, its only forward consumer) and by conv3's weight gradient in the blocks
+# whose conv3 has at most this many output channels (each a2 element is transformed once per 128-channel tile), so
+# a2 = relu(BN3(h2)) is never written for them (0: off; 256 / 512 / 1024 / 2048 measured -0.1 / +0.0 / +0.3 / +0.4 ms,
+# within box noise at 256: profiles/r6_imagenet_fold3_ab.log)
+CG_FOLD3_MAXC = int(os.environ.get("DTF_CG_FOLD3_MAXC", "0"))  # 73.24 -> 72.87 ms at pop 8 (profiles/r6_imagenet_fold1_ab.log)
 # XCD-aware work order (_xcd_order): 0 off, 1 operand-sharing runs on one XCD, 2 additionally every member on its own
 # XCD when the population is a multiple of 8 with equal work per member, 3 (default) also members on XCD subsets when
 # the population divides 8 (pop 4: 39.73 -> 38.95 ms).  ResNet-50 pop 8 x 128:
@@ -447,6 +452,7 @@ class _ImageNetPlan:
         self.fold = CG_FOLD and not self.eval and not be.v1
         self.fold2 = CG_FOLD2 and not self.fold and not self.eval and not be.v1
         self.fold1 = CG_FOLD1 and not self.fold and not self.eval and not be.v1 and self.FOLD1_OK
+        self.fold3 = CG_FOLD3_MAXC > 0 and not self.fold and not self.eval and not be.v1 and self.FOLD1_OK
         # v1 (post-activation): h3 = conv3 output (BN3 input), sc = raw projection output (BN_p input), a0 = the
         # stem's relu(BN(y0)); no ax (the block input IS a ReLU output)
         self.v1 = be.v1
@@ -462,7 +468,7 @@ class _ImageNetPlan:
             self.ax.append(act("ax", hw, cin) if not (self.v1 or self.fold) else None)
             self.h3.append(act("h3", ho, c3.cout) if self.v1 else None)
             self.a1.append(act("a1", hw, c1.cout) if not (self.fold or self.fold2) else None)
-            self.a2.append(act("a2", ho, c2.cout) if not self.fold else None)
+            self.a2.append(act("a2", ho, c2.cout) if not (self.fold or self._fold3(bi)) else None)
             self.sc.append(act("sc", ho, c3.cout) if blk.proj is not None else None)
             self.xs.append(act("x", ho, c3.cout, bi + 1))
             self.geo.append((hw, ho, cin, c1.cout, c3.cout))
@@ -854,6 +860,12 @@ class _ImageNetPlan:
     FOLD1_OK = True  # the fp32 plan (hip_imagenet_f32.py) keeps the materialised relu(BN1(x))
     COMPACT_PD_OK = True  # ... and the full-resolution projection data gradient
 
+    def _fold3(self, i):
+        """Block i's BN3 + ReLU is applied by conv3 (forward, MODE 1) and its weight gradient (CG_FOLD3_MAXC)."""
+        if not getattr(self, "fold3", False):
+            return False
+        return self.be.prog.convs[self.be.prog.blocks[i].convs[2]].cout <= CG_FOLD3_MAXC
+
     def _fold1(self, i):
         """Block i's BN1 + ReLU is applied by conv1 itself (CG_FOLD1: no projection, one output-channel tile)."""
         if not getattr(self, "fold1", False):
@@ -912,6 +924,10 @@ class _ImageNetPlan:
                 self.ew(relu, self.h1[i], self.a1[i], self.cf(b2), hi, f)
                 self.conv(c2, self.a1[i], self.h2[i], hi, mode=0, epi=4, st=self.sf(b3))
             self.bn_final(b3, ho, False)
+            if self._fold3(i):
+                self.conv(c3, self.h2[i], self.xs[i + 1], ho, mode=1, c_in=self.cf(b3), epi=5, res=res,
+                          st=self.sf(nxt))
+                continue
             self.ew(relu, self.h2[i], self.a2[i], self.cf(b3), ho, f)
             self.conv(c3, self.a2[i], self.xs[i + 1], ho, mode=0, epi=5, res=res, st=self.sf(nxt))
         fb = prog.final_bn
@@ -948,7 +964,10 @@ class _ImageNetPlan:
             self.bn_final(b3, ho, True)
             dh2 = self.tmp("dh2", ho, f)
             self.ew(bwd, h2, dh2, self.cb(b3), ho, f, dz=dz3)
-            self.wgrad(c3, h2, gcur, ho, mode_x=1, c_x=self.cf(b3)) if self.fold else self.wgrad(c3, self.a2[i], gcur, ho)
+            if self.fold or self._fold3(i):
+                self.wgrad(c3, h2, gcur, ho, mode_x=1, c_x=self.cf(b3))
+            else:
+                self.wgrad(c3, self.a2[i], gcur, ho)
             # conv2 (3x3 / s): dz2 = dgrad(dh2) masked by BN2(h1); dh1 = BN2-backward(dz2, h1)
             dz2 = self.tmp("dz2", hi, f)
             self.conv(c2, dh2, dz2, ho, mode=0, epi=6, xm=h1, c_ep=self.cf(b2), st=self.sb(b2), dgrad=True)

@@ -33,6 +33,9 @@
 #ifndef DTF_FUSED16_WLDS
 #define DTF_FUSED16_WLDS 1  // C = 16 fused backward: dgrad weights read from LDS per MFMA instead of held in VGPRs
 #endif
+#ifndef DTF_FWD_COEFREG
+#define DTF_FWD_COEFREG 1  // conv_fwd_s1<16> MODE 1: BN scale / shift of the staged channels held in VGPRs (pop 8 3.078 -> 3.063 ms, profiles/r6_fwd_coefreg_ab.log)
+#endif
 #ifndef DTF_WGRAD_PF2
 #define DTF_WGRAD_PF2 0  // 1: deferred wgrad jobs with tiles prefetched two iterations ahead (conv_wgrad_pf2_body): measured +0.8 % at pop 8, flat at C = 16 only (profiles/r6_wgrad_pf2_ab.log)
 #endif
@@ -802,6 +805,31 @@ struct Stage {
       *reinterpret_cast<uint4*>(buf + loff[j]) = t;
     }
   }
+  // MODE 1 with the thread's 8 scale / shift coefficients in registers (its channels c0..c0+7 are the same for
+  // every slot): no LDS coefficient reads per staged band
+  __device__ __forceinline__ void load_coef1(float (&sc)[8], float (&sh)[8], const float* coef) const {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      sc[i] = coef[c0 + i];
+      sh[i] = coef[64 + c0 + i];
+    }
+  }
+  __device__ __forceinline__ void store1r(bf16_t* buf, const uint4 (&v)[MAXC], unsigned m, const float (&sc)[8],
+                                         const float (&sh)[8]) const {
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j) {
+      uint4 t = make_uint4(0, 0, 0, 0);
+      if ((m >> j) & 1u) {
+        uint32_t w[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          w[q] = relu_pk2(pk2(unpk2(w[q]) * (f32x2_t){sc[2 * q], sc[2 * q + 1]} +
+                              (f32x2_t){sh[2 * q], sh[2 * q + 1]}));
+        t = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      *reinterpret_cast<uint4*>(buf + loff[j]) = t;
+    }
+  }
   // The untransformed band-interior chunks (tile rows 1..RT-2, image columns) into `raw` ([RT-2][W][CP]).
   __device__ __forceinline__ void store_raw(bf16_t* raw, const uint4 (&v)[MAXC], unsigned m) const {
     const unsigned interior = m & ~top & ~bot;
@@ -1072,7 +1100,15 @@ __device__ __forceinline__ void conv_fwd_s1_body(const ConvArgs& a, const int bi
   }
   __syncthreads();  // coefficients
   STAMP(1);
-  st.template store<LMODE>(SBUF(0), tv, unused, tm, coef);
+  // C = 16 (VGPR headroom below the 128 of 4 waves / SIMD): the staging coefficients held in registers
+  constexpr bool CREG = DTF_FWD_COEFREG && LMODE == 1 && C == 16;
+  float csc[8], csh[8];
+  if constexpr (CREG) {
+    st.load_coef1(csc, csh, coef);
+    st.store1r(SBUF(0), tv, tm, csc, csh);
+  } else {
+    st.template store<LMODE>(SBUF(0), tv, unused, tm, coef);
+  }
   __syncthreads();
   STAMP(2);
   for (int k = 0; k < nit; ++k) {
@@ -1117,7 +1153,12 @@ __device__ __forceinline__ void conv_fwd_s1_body(const ConvArgs& a, const int bi
       ssq[0] += r0v * r0v;
       ssq[1] += r1v * r1v;
     }
-    if (more) st.template store<LMODE>(SBUF(k + 1), tv, unused, tm, coef);
+    if (more) {
+      if constexpr (CREG)
+        st.store1r(SBUF(k + 1), tv, tm, csc, csh);
+      else
+        st.template store<LMODE>(SBUF(k + 1), tv, unused, tm, coef);
+    }
     __syncthreads();
   }
 #undef SBUF

@@ -33,6 +33,9 @@
 #ifndef DTF_FUSED16_WLDS
 #define DTF_FUSED16_WLDS 1  // C = 16 fused backward: dgrad weights read from LDS per MFMA instead of held in VGPRs
 #endif
+#ifndef DTF_BWD_COEFREG
+#define DTF_BWD_COEFREG 1  // conv_bwd_fused<16, 3>: staging + epilogue BN coefficients held in VGPRs
+#endif
 #ifndef DTF_FWD_COEFREG
 #define DTF_FWD_COEFREG 1  // conv_fwd_s1<16> MODE 1: BN scale / shift of the staged channels held in VGPRs (pop 8 3.078 -> 3.063 ms, profiles/r6_fwd_coefreg_ab.log)
 #endif
@@ -830,6 +833,15 @@ struct Stage {
       *reinterpret_cast<uint4*>(buf + loff[j]) = t;
     }
   }
+  // MODE 2 / 3 coefficients of the thread's 8 channels (A, B, C of xform8r) in registers
+  __device__ __forceinline__ void load_coef3(float (&ka)[8], float (&kb)[8], float (&kc)[8], const float* coef) const {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      ka[i] = coef[c0 + i];
+      kb[i] = coef[64 + c0 + i];
+      kc[i] = coef[128 + c0 + i];
+    }
+  }
   // The untransformed band-interior chunks (tile rows 1..RT-2, image columns) into `raw` ([RT-2][W][CP]).
   __device__ __forceinline__ void store_raw(bf16_t* raw, const uint4 (&v)[MAXC], unsigned m) const {
     const unsigned interior = m & ~top & ~bot;
@@ -839,10 +851,12 @@ struct Stage {
   }
   // MODE 2 / 3 (BN-backward apply [+ residual v3]) staging that also writes the transformed band-interior
   // chunks (tile rows 1..RT-2, image columns) to `out` (the image base; null: LDS only).
-  template <int MODE>
+  // (KR: the coefficients come from ka / kb / kc -- load_coef3 -- instead of LDS)
+  template <int MODE, bool KR = false>
   __device__ __forceinline__ void store_x(bf16_t* buf, const uint4 (&v)[MAXC], const uint4 (&v2)[MAXC],
                                           const uint4 (&v3)[MAXC], unsigned m, const float* coef, bf16_t* out,
-                                          int gy0) const {
+                                          int gy0, const float* ka = nullptr, const float* kb = nullptr,
+                                          const float* kc = nullptr) const {
     const unsigned interior = m & ~top & ~bot;
     const int rb = gy0 * ROW * 2;
 #if DTF_WT_ACT
@@ -851,7 +865,23 @@ struct Stage {
 #pragma unroll
     for (int j = 0; j < MAXC; ++j) {
       uint4 t = make_uint4(0, 0, 0, 0);
-      if ((m >> j) & 1u) t = xform8r<MODE>(v[j], v2[j], v3[j], c0, coef);
+      if ((m >> j) & 1u) {
+        if constexpr (KR) {
+          const uint32_t w[4] = {v[j].x, v[j].y, v[j].z, v[j].w}, h[4] = {v2[j].x, v2[j].y, v2[j].z, v2[j].w},
+                         r[4] = {v3[j].x, v3[j].y, v3[j].z, v3[j].w};
+          uint32_t o[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            f32x2_t u = unpk2(w[q]) * (f32x2_t){ka[2 * q], ka[2 * q + 1]} +
+                        unpk2(h[q]) * (f32x2_t){kb[2 * q], kb[2 * q + 1]} + (f32x2_t){kc[2 * q], kc[2 * q + 1]};
+            if constexpr (MODE == 3) u += unpk2(r[q]);
+            o[q] = pk2(u);
+          }
+          t = make_uint4(o[0], o[1], o[2], o[3]);
+        } else {
+          t = xform8r<MODE>(v[j], v2[j], v3[j], c0, coef);
+        }
+      }
       *reinterpret_cast<uint4*>(buf + loff[j]) = t;
       if (out != nullptr && ((interior >> j) & 1u)) {
 #if DTF_WT_ACT
@@ -1966,13 +1996,31 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
 
   __syncthreads();  // coefficients
   STAMP(1);
+  // KREG (C = 16 with the BN-backward + residual dY, 2 waves / SIMD: VGPRs to spare): every staging and epilogue
+  // coefficient of the thread's channels held in registers for the whole launch instead of re-read from LDS per band
+  constexpr bool KREG = DTF_BWD_COEFREG && C == 16 && MODE_DY == 3 && ROLE == 0;
+  float ka[KREG ? 8 : 1], kb[KREG ? 8 : 1], kc[KREG ? 8 : 1], xsc[KREG ? 8 : 1], xsh[KREG ? 8 : 1];
+  if constexpr (KREG) {
+    st.load_coef3(ka, kb, kc, coef_d);
+    st.load_coef1(xsc, xsh, ecoef);
+  }
   if constexpr (XSTORE)  // (the wgrad role stages the same transform but never writes xout)
-    st.template store_x<MODE_DY == 3 ? 3 : 2>(FDBUF(0), dv, dv2, dv3, dm, coef_d,
-                                              (DG && k_xout) ? k_xout + cimg * IMG : nullptr, cgy0);
+    st.template store_x<MODE_DY == 3 ? 3 : 2, KREG>(FDBUF(0), dv, dv2, dv3, dm, coef_d,
+                                                    (DG && k_xout) ? k_xout + cimg * IMG : nullptr, cgy0, ka, kb, kc);
   else
     st.template store<MODE_DY>(FDBUF(0), dv, dv2, dm, coef_d);
-  if constexpr (WG) st.template store<1>(FXBUF(0), xv_, unused, xm, ecoef);
+  if constexpr (KREG)
+    st.store1r(FXBUF(0), xv_, xm, xsc, xsh);
+  else if constexpr (WG)
+    st.template store<1>(FXBUF(0), xv_, unused, xm, ecoef);
   if constexpr (RAWX) st.store_raw(FXRAW(0), xv_, xm);
+  f32x2_t esc0, esc1, esh0, esh1, enm0, enm1, eiv0, eiv1;
+  if constexpr (KREG) {
+    esc0 = lds2(ecoef + ci0), esc1 = lds2(ecoef + ci0 + 2);
+    esh0 = lds2(ecoef + 64 + ci0), esh1 = lds2(ecoef + 64 + ci0 + 2);
+    enm0 = lds2(ecoef + 128 + ci0), enm1 = lds2(ecoef + 128 + ci0 + 2);
+    eiv0 = lds2(ecoef + 192 + ci0), eiv1 = lds2(ecoef + 192 + ci0 + 2);
+  }
   __syncthreads();
   STAMP(2);
   for (int k = 0; k < nit; ++k) {
@@ -2004,11 +2052,11 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
     }
     const bf16_t* dcur = FDBUF(k);
     const bf16_t* xcur = FXBUF(k);
-    // ---- dgrad
-    const f32x2_t sc0 = lds2(ecoef + ci0), sc1 = lds2(ecoef + ci0 + 2);
-    const f32x2_t sh0 = lds2(ecoef + 64 + ci0), sh1 = lds2(ecoef + 64 + ci0 + 2);
-    const f32x2_t nm0 = lds2(ecoef + 128 + ci0), nm1 = lds2(ecoef + 128 + ci0 + 2);
-    const f32x2_t iv0 = lds2(ecoef + 192 + ci0), iv1 = lds2(ecoef + 192 + ci0 + 2);
+    // ---- dgrad (KREG: the epilogue coefficients are loop-invariant registers, read before the loop)
+    const f32x2_t sc0 = KREG ? esc0 : lds2(ecoef + ci0), sc1 = KREG ? esc1 : lds2(ecoef + ci0 + 2);
+    const f32x2_t sh0 = KREG ? esh0 : lds2(ecoef + 64 + ci0), sh1 = KREG ? esh1 : lds2(ecoef + 64 + ci0 + 2);
+    const f32x2_t nm0 = KREG ? enm0 : lds2(ecoef + 128 + ci0), nm1 = KREG ? enm1 : lds2(ecoef + 128 + ci0 + 2);
+    const f32x2_t iv0 = KREG ? eiv0 : lds2(ecoef + 192 + ci0), iv1 = KREG ? eiv1 : lds2(ecoef + 192 + ci0 + 2);
     if constexpr (DG) {
 #pragma unroll
     for (int i = 0; i < MTD; ++i) {
@@ -2076,11 +2124,15 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
     if (more) {
       if constexpr (SB) __syncthreads();  // every wave is done with the current tiles
       if constexpr (XSTORE)
-        st.template store_x<MODE_DY == 3 ? 3 : 2>(FDBUF(k + 1), dv, dv2, dv3, dm, coef_d,
-                                                  (DG && k_xout) ? k_xout + cimg * IMG : nullptr, cgy0);
+        st.template store_x<MODE_DY == 3 ? 3 : 2, KREG>(FDBUF(k + 1), dv, dv2, dv3, dm, coef_d,
+                                                        (DG && k_xout) ? k_xout + cimg * IMG : nullptr, cgy0, ka, kb,
+                                                        kc);
       else
         st.template store<MODE_DY>(FDBUF(k + 1), dv, dv2, dm, coef_d);
-      if constexpr (WG) st.template store<1>(FXBUF(k + 1), xv_, unused, xm, ecoef);
+      if constexpr (KREG)
+        st.store1r(FXBUF(k + 1), xv_, xm, xsc, xsh);
+      else if constexpr (WG)
+        st.template store<1>(FXBUF(k + 1), xv_, unused, xm, ecoef);
       if constexpr (RAWX) st.store_raw(FXRAW(k + 1), xv_, xm);
     }
     __syncthreads();

@@ -1996,26 +1996,31 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
 
   __syncthreads();  // coefficients
   STAMP(1);
-  // KREG (C = 16 with the BN-backward + residual dY, 2 waves / SIMD: VGPRs to spare): every staging and epilogue
-  // coefficient of the thread's channels held in registers for the whole launch instead of re-read from LDS per band
-  constexpr bool KREG = DTF_BWD_COEFREG && C == 16 && MODE_DY == 3 && ROLE == 0;
-  float ka[KREG ? 8 : 1], kb[KREG ? 8 : 1], kc[KREG ? 8 : 1], xsc[KREG ? 8 : 1], xsh[KREG ? 8 : 1];
-  if constexpr (KREG) {
-    st.load_coef3(ka, kb, kc, coef_d);
-    st.load_coef1(xsc, xsh, ecoef);
-  }
+  // Coefficients of the thread's channels held in registers for the whole launch instead of re-read from LDS per
+  // band, where the VGPR budget of the launch's occupancy has room: KREG_D the dY staging transform (BN-backward
+  // [+ residual]), KREG_X the x staging (BN + ReLU), KREG_E the dgrad epilogue's mask / x-hat coefficients.
+  // C = 16 fused with MODE_DY 3 (2 waves / SIMD: 176 -> 222 VGPRs); the dgrad-only role (2 waves / SIMD) at every C,
+  // its epilogue set up to C = 32 (C = 64 would pass 256)
+  constexpr bool KREG_F = DTF_BWD_COEFREG && C == 16 && MODE_DY == 3 && ROLE == 0;
+  constexpr bool KREG_D = KREG_F || (DTF_BWD_COEFREG && ROLE == 1 && XSTORE);
+  constexpr bool KREG_X = KREG_F;
+  constexpr bool KREG_E = KREG_F || (DTF_BWD_COEFREG && ROLE == 1 && C <= 32);
+  float ka[KREG_D ? 8 : 1], kb[KREG_D ? 8 : 1], kc[KREG_D ? 8 : 1], xsc[KREG_X ? 8 : 1], xsh[KREG_X ? 8 : 1];
+  if constexpr (KREG_D) st.load_coef3(ka, kb, kc, coef_d);
+  if constexpr (KREG_X) st.load_coef1(xsc, xsh, ecoef);
   if constexpr (XSTORE)  // (the wgrad role stages the same transform but never writes xout)
-    st.template store_x<MODE_DY == 3 ? 3 : 2, KREG>(FDBUF(0), dv, dv2, dv3, dm, coef_d,
-                                                    (DG && k_xout) ? k_xout + cimg * IMG : nullptr, cgy0, ka, kb, kc);
+    st.template store_x<MODE_DY == 3 ? 3 : 2, KREG_D>(FDBUF(0), dv, dv2, dv3, dm, coef_d,
+                                                      (DG && k_xout) ? k_xout + cimg * IMG : nullptr, cgy0, ka, kb,
+                                                      kc);
   else
     st.template store<MODE_DY>(FDBUF(0), dv, dv2, dm, coef_d);
-  if constexpr (KREG)
+  if constexpr (KREG_X)
     st.store1r(FXBUF(0), xv_, xm, xsc, xsh);
   else if constexpr (WG)
     st.template store<1>(FXBUF(0), xv_, unused, xm, ecoef);
   if constexpr (RAWX) st.store_raw(FXRAW(0), xv_, xm);
   f32x2_t esc0, esc1, esh0, esh1, enm0, enm1, eiv0, eiv1;
-  if constexpr (KREG) {
+  if constexpr (KREG_E) {
     esc0 = lds2(ecoef + ci0), esc1 = lds2(ecoef + ci0 + 2);
     esh0 = lds2(ecoef + 64 + ci0), esh1 = lds2(ecoef + 64 + ci0 + 2);
     enm0 = lds2(ecoef + 128 + ci0), enm1 = lds2(ecoef + 128 + ci0 + 2);
@@ -2052,11 +2057,11 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
     }
     const bf16_t* dcur = FDBUF(k);
     const bf16_t* xcur = FXBUF(k);
-    // ---- dgrad (KREG: the epilogue coefficients are loop-invariant registers, read before the loop)
-    const f32x2_t sc0 = KREG ? esc0 : lds2(ecoef + ci0), sc1 = KREG ? esc1 : lds2(ecoef + ci0 + 2);
-    const f32x2_t sh0 = KREG ? esh0 : lds2(ecoef + 64 + ci0), sh1 = KREG ? esh1 : lds2(ecoef + 64 + ci0 + 2);
-    const f32x2_t nm0 = KREG ? enm0 : lds2(ecoef + 128 + ci0), nm1 = KREG ? enm1 : lds2(ecoef + 128 + ci0 + 2);
-    const f32x2_t iv0 = KREG ? eiv0 : lds2(ecoef + 192 + ci0), iv1 = KREG ? eiv1 : lds2(ecoef + 192 + ci0 + 2);
+    // ---- dgrad (KREG_E: the epilogue coefficients are loop-invariant registers, read before the loop)
+    const f32x2_t sc0 = KREG_E ? esc0 : lds2(ecoef + ci0), sc1 = KREG_E ? esc1 : lds2(ecoef + ci0 + 2);
+    const f32x2_t sh0 = KREG_E ? esh0 : lds2(ecoef + 64 + ci0), sh1 = KREG_E ? esh1 : lds2(ecoef + 64 + ci0 + 2);
+    const f32x2_t nm0 = KREG_E ? enm0 : lds2(ecoef + 128 + ci0), nm1 = KREG_E ? enm1 : lds2(ecoef + 128 + ci0 + 2);
+    const f32x2_t iv0 = KREG_E ? eiv0 : lds2(ecoef + 192 + ci0), iv1 = KREG_E ? eiv1 : lds2(ecoef + 192 + ci0 + 2);
     if constexpr (DG) {
 #pragma unroll
     for (int i = 0; i < MTD; ++i) {
@@ -2124,12 +2129,12 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
     if (more) {
       if constexpr (SB) __syncthreads();  // every wave is done with the current tiles
       if constexpr (XSTORE)
-        st.template store_x<MODE_DY == 3 ? 3 : 2, KREG>(FDBUF(k + 1), dv, dv2, dv3, dm, coef_d,
-                                                        (DG && k_xout) ? k_xout + cimg * IMG : nullptr, cgy0, ka, kb,
-                                                        kc);
+        st.template store_x<MODE_DY == 3 ? 3 : 2, KREG_D>(FDBUF(k + 1), dv, dv2, dv3, dm, coef_d,
+                                                          (DG && k_xout) ? k_xout + cimg * IMG : nullptr, cgy0, ka,
+                                                          kb, kc);
       else
         st.template store<MODE_DY>(FDBUF(k + 1), dv, dv2, dm, coef_d);
-      if constexpr (KREG)
+      if constexpr (KREG_X)
         st.store1r(FXBUF(k + 1), xv_, xm, xsc, xsh);
       else if constexpr (WG)
         st.template store<1>(FXBUF(k + 1), xv_, unused, xm, ecoef);

@@ -37,7 +37,7 @@
 #define DTF_BWD_COEFREG 1  // conv_bwd_fused<16, 3>: staging + epilogue BN coefficients held in VGPRs
 #endif
 #ifndef DTF_FWD_COEFREG
-#define DTF_FWD_COEFREG 1  // conv_fwd_s1<16> MODE 1: BN scale / shift of the staged channels held in VGPRs (pop 8 3.078 -> 3.063 ms, profiles/r6_fwd_coefreg_ab.log)
+#define DTF_FWD_COEFREG 1  // conv_fwd_s1 MODE 1: BN scale / shift of the staged channels held in VGPRs (pop 8 3.078 -> 3.063 ms, profiles/r6_fwd_coefreg_ab.log)
 #endif
 #ifndef DTF_WGRAD_PF2
 #define DTF_WGRAD_PF2 0  // 1: deferred wgrad jobs with tiles prefetched two iterations ahead (conv_wgrad_pf2_body): measured +0.8 % at pop 8, flat at C = 16 only (profiles/r6_wgrad_pf2_ab.log)
@@ -1130,8 +1130,9 @@ __device__ __forceinline__ void conv_fwd_s1_body(const ConvArgs& a, const int bi
   }
   __syncthreads();  // coefficients
   STAMP(1);
-  // C = 16 (VGPR headroom below the 128 of 4 waves / SIMD): the staging coefficients held in registers
-  constexpr bool CREG = DTF_FWD_COEFREG && LMODE == 1 && C == 16;
+  // the staging coefficients held in registers for the whole launch (every width stays within its occupancy's VGPR
+  // budget: C = 16 / 32 at <= 128 for 4 waves / SIMD, C = 64 at <= 168 for 3)
+  constexpr bool CREG = DTF_FWD_COEFREG && LMODE == 1;
   float csc[8], csh[8];
   if constexpr (CREG) {
     st.load_coef1(csc, csh, coef);
@@ -2000,10 +2001,11 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
   // band, where the VGPR budget of the launch's occupancy has room: KREG_D the dY staging transform (BN-backward
   // [+ residual]), KREG_X the x staging (BN + ReLU), KREG_E the dgrad epilogue's mask / x-hat coefficients.
   // C = 16 fused with MODE_DY 3 (2 waves / SIMD: 176 -> 222 VGPRs); the dgrad-only role (2 waves / SIMD) at every C,
-  // its epilogue set up to C = 32 (C = 64 would pass 256)
+  // its epilogue set up to C = 32 (C = 64 would pass 256); the deferred wgrad role's staging sets at every C
+  // (conv_wgrad_all: <64, 32> runs one wave per SIMD anyway, <16, 16> is LDS-bound at 3 workgroups per CU)
   constexpr bool KREG_F = DTF_BWD_COEFREG && C == 16 && MODE_DY == 3 && ROLE == 0;
-  constexpr bool KREG_D = KREG_F || (DTF_BWD_COEFREG && ROLE == 1 && XSTORE);
-  constexpr bool KREG_X = KREG_F;
+  constexpr bool KREG_D = KREG_F || (DTF_BWD_COEFREG && ROLE != 0 && XSTORE);
+  constexpr bool KREG_X = KREG_F || (DTF_BWD_COEFREG && ROLE == 2);
   constexpr bool KREG_E = KREG_F || (DTF_BWD_COEFREG && ROLE == 1 && C <= 32);
   float ka[KREG_D ? 8 : 1], kb[KREG_D ? 8 : 1], kc[KREG_D ? 8 : 1], xsc[KREG_X ? 8 : 1], xsh[KREG_X ? 8 : 1];
   if constexpr (KREG_D) st.load_coef3(ka, kb, kc, coef_d);

@@ -88,7 +88,7 @@ def _n_cu():
 def _fused_wgs_per_cu(C, mode_dy):
     """Workgroups per CU of conv_bwd_fused_kernel<C, mode_dy> (conv.hip FUSED_WAVES, 4 waves per workgroup)."""
     if C <= 16:
-        return 3 if mode_dy != 3 else _lib_knob("dtf_fused16_m3_waves")
+        return _lib_knob("dtf_fused16_m2_waves") if mode_dy != 3 else _lib_knob("dtf_fused16_m3_waves")
     return 2 if C <= 32 else 1
 _KNOBS = {}
 

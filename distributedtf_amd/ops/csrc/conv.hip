@@ -54,7 +54,10 @@
 #ifndef DTF_FUSED16_M3_WAVES
 #define DTF_FUSED16_M3_WAVES 2
 #endif
-#define FUSED_WAVES(C, M) ((C) <= 16 ? ((M) != 3 ? 3 : DTF_FUSED16_M3_WAVES) : (C) <= 32 ? 2 : 1)
+#ifndef DTF_FUSED16_M2_WAVES
+#define DTF_FUSED16_M2_WAVES 3  // 2: room for register-held coefficients in conv_bwd_fused<16, 2, *> (measured flat: profiles/r6_fused16_m2_waves2_ab.log)
+#endif
+#define FUSED_WAVES(C, M) ((C) <= 16 ? ((M) != 3 ? DTF_FUSED16_M2_WAVES : DTF_FUSED16_M3_WAVES) : (C) <= 32 ? 2 : 1)
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 #define NREP DTF_NREP
 #ifndef DTF_STAMP
@@ -2003,7 +2006,7 @@ __device__ __forceinline__ void conv_bwd_body(const ConvArgs& a, const int bid, 
   // C = 16 fused with MODE_DY 3 (2 waves / SIMD: 176 -> 222 VGPRs); the dgrad-only role (2 waves / SIMD) at every C,
   // its epilogue set up to C = 32 (C = 64 would pass 256); the deferred wgrad role's staging sets at every C
   // (conv_wgrad_all: <64, 32> runs one wave per SIMD anyway, <16, 16> is LDS-bound at 3 workgroups per CU)
-  constexpr bool KREG_F = DTF_BWD_COEFREG && C == 16 && MODE_DY == 3 && ROLE == 0;
+  constexpr bool KREG_F = DTF_BWD_COEFREG && C == 16 && ROLE == 0 && (MODE_DY == 3 || (MODE_DY == 2 && DTF_FUSED16_M2_WAVES == 2));
   constexpr bool KREG_D = KREG_F || (DTF_BWD_COEFREG && ROLE != 0 && XSTORE);
   constexpr bool KREG_X = KREG_F || (DTF_BWD_COEFREG && ROLE == 2);
   constexpr bool KREG_E = KREG_F || (DTF_BWD_COEFREG && ROLE == 1 && C <= 32);
@@ -2712,6 +2715,7 @@ DTF_API int dtf_conv_trans_multi(const ConvArgs* c, const ConvArgs* a, const Con
 // compile-time knobs the host plan must agree with (engine/hip_resnet.py reads these, not its environment)
 DTF_API int dtf_fused16_wlds() { return DTF_FUSED16_WLDS; }
 DTF_API int dtf_fused16_m3_waves() { return DTF_FUSED16_M3_WAVES; }
+DTF_API int dtf_fused16_m2_waves() { return DTF_FUSED16_M2_WAVES; }
 
 DTF_API int dtf_cpad_fwd(int c) { return c == 16 ? cpad_fwd<16>() : c == 32 ? cpad_fwd<32>() : c == 64 ? cpad_fwd<64>() : -1; }
 DTF_API int dtf_wpitch(int c) { return c == 16 ? wpitch<16>() : c == 32 ? wpitch<32>() : c == 64 ? wpitch<64>() : -1; }

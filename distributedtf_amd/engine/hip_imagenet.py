@@ -82,6 +82,13 @@ CG_FOLD1_MAXC = int(os.environ.get("DTF_CG_FOLD1_MAXC", "256"))
 CG_COMPACT_PD = os.environ.get("DTF_CG_COMPACT_PD", "1") == "1"
 CG_CLASS_LPT = os.environ.get("DTF_CG_CLASS_LPT", "0") == "1"  # stride-2 3x3 data gradient: heavy parity class first
 CG_FOLD1 = os.environ.get("DTF_CG_FOLD1", "1") == "1"
+# backward fold of the block-input gradient: g = BN1-backward(dz1, x) [+ g of the next block] is computed by its first
+# consumer -- the previous block's conv3 data gradient (a stride-1 1x1 over g with one output-channel tile when that
+# block's width f <= this: convg MODE 3) -- while it stages g, and stored from there (xout), instead of a standalone
+# apply pass that conv3's data gradient then re-reads (0: off).  Numerics and det replay pass (bitwise the same
+# values as the standalone pass), but 64 / 128 measured +0.2 / +0.5 ms: the conv's one-ahead pipeline streams the
+# three extra operands slower than the apply pass does (profiles/r6_imagenet_gfold_ab.log)
+CG_GFOLD_MAXF = int(os.environ.get("DTF_CG_GFOLD_MAXF", "0"))
 # BN3 + ReLU applied by conv3 (the 1x1 expand, its only forward consumer) and by conv3's weight gradient in the blocks
 # whose conv3 has at most this many output channels (each a2 element is transformed once per 128-channel tile), so
 # a2 = relu(BN3(h2)) is never written for them (0: off; 256 / 512 / 1024 / 2048 measured -0.1 / +0.0 / +0.3 / +0.4 ms,
@@ -111,7 +118,7 @@ class CgArgs(ctypes.Structure):
         ("c_ep", c_void_p), ("st_out", c_void_p), ("work", c_void_p),
         ("Hi", c_int), ("Wi", c_int), ("Ci", c_int), ("Ho", c_int), ("Wo", c_int), ("Co", c_int),
         ("kh", c_int), ("kw", c_int), ("stride", c_int), ("pad", c_int), ("cmax", c_int), ("log2ci", c_int),
-        ("cin_real", c_int), ("flags", c_int),
+        ("cin_real", c_int), ("flags", c_int), ("x3", c_void_p), ("xout", c_void_p),
     ]
 
 
@@ -595,7 +602,7 @@ class _ImageNetPlan:
         return self.be.sums[1, bn]
 
     def conv(self, ci, src, out, hw_in, mode=0, c_in=None, x2=None, epi=0, res=None, xm=None, c_ep=None, st=None,
-             dgrad=False, compact=False):
+             dgrad=False, compact=False, x3=None, xout=None):
         """Forward conv (dgrad=False) or data gradient (dgrad=True) of conv `ci` through convg_fwd.  ``compact``
         (the data gradient of a stride-2 1x1 conv): only the even output rows / columns are nonzero, so the gradient
         is computed and stored at the dy resolution, [N, hw_in, hw_in, cin] -- a plain 1x1 GEMM with no zero-filled
@@ -610,6 +617,8 @@ class _ImageNetPlan:
         if ci == be.prog.stem:
             a.w, a.w_mstride, a.w_off = _p(be.w), be.wtot, 0
         a.c_in, a.c_ep, a.st_out = _p(c_in), _p(c_ep), _p(st)
+        a.x3, a.xout = _p(x3), _p(xout)
+        assert mode != 3 or (dgrad and k == 1 and c.stride == 1 and xout is not None), "MODE 3: 1x1 data gradient"
         a.kh = a.kw = k
         if not dgrad:
             cin = 8 if ci == be.prog.stem else c.cin
@@ -858,6 +867,7 @@ class _ImageNetPlan:
         self._add("gemm", self.g_wgr)
 
     FOLD1_OK = True  # the fp32 plan (hip_imagenet_f32.py) keeps the materialised relu(BN1(x))
+    GFOLD_OK = True  # ... and the standalone block-input gradient apply
     COMPACT_PD_OK = True  # ... and the full-resolution projection data gradient
 
     def _fold3(self, i):
@@ -865,6 +875,14 @@ class _ImageNetPlan:
         if not getattr(self, "fold3", False):
             return False
         return self.be.prog.convs[self.be.prog.blocks[i].convs[2]].cout <= CG_FOLD3_MAXC
+
+    def _gfold(self, i):
+        """Block i's input gradient g is applied by block i - 1's conv3 data gradient (MODE 3, CG_GFOLD_MAXF)."""
+        if not (self.GFOLD_OK and CG_GFOLD_MAXF > 0 and i > 0 and not self.eval and not self.be.v1):
+            return False
+        prog = self.be.prog
+        c3 = prog.convs[prog.blocks[i - 1].convs[2]]
+        return c3.k == 1 and c3.stride == 1 and c3.cin <= min(CG_GFOLD_MAXF, 128)
 
     def _fold1(self, i):
         """Block i's BN1 + ReLU is applied by conv1 itself (CG_FOLD1: no projection, one output-channel tile)."""
@@ -951,6 +969,7 @@ class _ImageNetPlan:
         self._hold(g2)
         self.gap(g2, 2)
         # ---- blocks, reversed
+        gpend = None  # a block-input gradient left to its consumer (CG_GFOLD_MAXF): (dz1, x, BN1 coefficients, add)
         for i in range(nblk - 1, -1, -1):
             blk = prog.blocks[i]
             hi, ho, cin, f, fout = self.geo[i]
@@ -960,7 +979,13 @@ class _ImageNetPlan:
             bwd = L.dtf_cg_bn_bwd_apply
             # conv3: dz3 = dgrad(g) masked by BN3(h2) (+ BN3 reductions); dh2 = BN3-backward(dz3, h2)
             dz3 = self.tmp("dz3", ho, f)
-            self.conv(c3, gcur, dz3, ho, mode=0, epi=6, xm=h2, c_ep=self.cf(b3), st=self.sb(b3), dgrad=True)
+            if gpend is not None:  # g of block i + 1 computed (and stored into gcur) while this dgrad stages it
+                pdz, px, pcb, padd = gpend
+                self.conv(c3, pdz, dz3, ho, mode=3, c_in=pcb, x2=px, x3=padd, xout=gcur, epi=6, xm=h2,
+                          c_ep=self.cf(b3), st=self.sb(b3), dgrad=True)
+                gpend = None
+            else:
+                self.conv(c3, gcur, dz3, ho, mode=0, epi=6, xm=h2, c_ep=self.cf(b3), st=self.sb(b3), dgrad=True)
             self.bn_final(b3, ho, True)
             dh2 = self.tmp("dh2", ho, f)
             self.ew(bwd, h2, dh2, self.cb(b3), ho, f, dz=dz3)
@@ -1001,7 +1026,10 @@ class _ImageNetPlan:
             else:
                 self.wgrad(c1, self.ax[i], dh1, hi)
             gnext = self.tmp("gA" if (i % 2 == 0) else "gB", hi, cin)
-            self.ew(bwd, x, gnext, self.cb(b1), hi, cin, dz=dz1, add=None if blk.proj is not None else gcur)
+            if self._gfold(i):
+                gpend = (dz1, x, self.cb(b1), None if blk.proj is not None else gcur)
+            else:
+                self.ew(bwd, x, gnext, self.cb(b1), hi, cin, dz=dz1, add=None if blk.proj is not None else gcur)
             gcur = gnext
         # ---- stem: max-pool backward, stem wgrad (padded input, 3 real channels)
         dy0 = self.tmp("dy0", H1, cfg.num_filters)

@@ -118,6 +118,7 @@ class HipImageNetF32Backend(HipImageNetBackend):
 class _ImageNetF32Plan(_ImageNetPlan):
     FOLD1_OK = False  # (the fp32 conv kernels are not exercised with the read-once BN1 fold)
     COMPACT_PD_OK = False  # (nor with the compact stride-2 projection gradient: f32conv has no EPI bit 8)
+    GFOLD_OK = False  # (nor with the block-input gradient applied by conv3's data gradient: no f32conv MODE 3)
 
     def _act_dtype(self):
         return torch.float32

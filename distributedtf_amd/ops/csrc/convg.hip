@@ -115,6 +115,8 @@ struct CgArgs {
   int log2ci;
   int cin_real;       // wgrad: real input channels of a channel-padded operand (stem: 3 of 8); 0 = Ci
   int flags;          // convg_t3 forward: bit 0 keeps the LDS-staged weights (A/B of the direct fragment loads)
+  const bf16_t* x3;   // MODE 3: residual-stream gradient added by the gathered operand's BN-backward transform
+  bf16_t* xout;       // MODE 3: the transformed gathered operand written out (1x1 stride-1 data gradient, co tile 0)
 };
 
 
@@ -431,7 +433,9 @@ __device__ __forceinline__ void convg_epilogue_regs(const CgArgs& a, f32x4_t (&a
 }
 
 // ---------------------------------------------------------------------------------------------- fwd / dgrad
-// MODE: 0 identity, 1 relu(x*s + t), 2 A*x + B*x2 + C.   EPI: bit0 residual, bit1 mask, bit2 stats (fwd: y, y^2;
+// MODE: 0 identity, 1 relu(x*s + t), 2 A*x + B*x2 + C, 3 A*x + B*x2 + C + x3 also stored to xout (the BN-backward
+// apply of the next block's input gradient done by its consumer: a stride-1 1x1 data gradient whose single co tile
+// gathers each element once).   EPI: bit0 residual, bit1 mask, bit2 stats (fwd: y, y^2;
 // with bit1: dz, dz*xhat).  TRANS: transposed (dgrad, stride > 1) gather.
 // AKM (data gradient): the A operand (rows = dx channels i, k = (tap', dy channel o)) is read straight from the
 // FORWARD weight layout W[o][tap][i] (k-major: 8 consecutive i per 16-byte load, fragments via
@@ -471,7 +475,7 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t smem_[SOPS > SEPI ? SOPS : SEPI];
   bf16_t (*sa)[SA] = reinterpret_cast<bf16_t (*)[SA]>(smem_);
   bf16_t (*sb)[TP * RP] = reinterpret_cast<bf16_t (*)[TP * RP]>(smem_ + 2 * SA);
-  extern __shared__ __attribute__((aligned(16))) float dyn[];  // transform coefficients: MODE 1: 2*Ci, MODE 2: 3*Ci
+  extern __shared__ __attribute__((aligned(16))) float dyn[];  // transform coefficients: MODE 1: 2*Ci, MODE 2/3: 3*Ci
   __shared__ dtf_acc_t acc_lds[2][TC];
   const int4 wk = a.work[blockIdx.x];
   DTF_WG_CHECK(wk.x >= 0 && wk.y >= 0 && wk.z >= wk.y);
@@ -498,7 +502,7 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
     for (int i = tid; i < Ci; i += 256) {
       dyn[i] = cb[i];
       dyn[Ci + i] = cb[a.cmax + i];
-      if constexpr (MODE == 2) dyn[2 * Ci + i] = cb[2 * a.cmax + i];
+      if constexpr (MODE >= 2) dyn[2 * Ci + i] = cb[2 * a.cmax + i];
     }
   }
   for (int i = tid; i < 2 * TC; i += 256) (&acc_lds[0][0])[i] = 0;
@@ -586,11 +590,17 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
       }
     }
   };
-  auto load_b = [&](int k0, uint4 (&v)[NJ], uint4 (&v2)[NJ], int& cch, unsigned& okb) {
+  static_assert(MODE != 3 || (AKM && !TRANS), "MODE 3: stride-1 data gradient");
+  constexpr int NJ3 = MODE == 3 ? NJ : 1;
+  // MODE 3: xout is written by the co-tile-0 workgroups only (with one tile, every element exactly once)
+  bf16_t* const xo = (MODE == 3 && wk.w == 0) ? a.xout : nullptr;
+  const bool has3 = MODE == 3 && a.x3 != nullptr;
+  auto load_b = [&](int k0, uint4 (&v)[NJ], uint4 (&v2)[NJ], uint4 (&v3)[NJ3], int& cch, int& tof, unsigned& okb) {
     const int k = k0 + 8 * cB;
     const int ty = cur_ty, tx = cur_tx, ci0 = cur_ci;
     const int toff = (ty * a.Wi + tx) * Ci + ci0;
     cch = ci0;
+    tof = toff;
     okb = 0;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -598,11 +608,13 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
       const long off = pbase[j] + toff;
       v[j] = ld16(a.x, off, ok);
       v2[j] = make_uint4(0, 0, 0, 0);
-      if constexpr (MODE == 2) v2[j] = ld16(a.x2, off, ok);
+      if constexpr (MODE >= 2) v2[j] = ld16(a.x2, off, ok);
+      if constexpr (MODE == 3) v3[j] = ld16(a.x3, off, ok && has3);  // (no x3: a projection block's g)
       okb |= (unsigned)ok << j;  // unset: zero padding (stays zero after the transform)
     }
   };
-  auto xform_store = [&](bf16_t* dst, const uint4 (&v)[NJ], const uint4 (&v2)[NJ], int cch, unsigned okb) {
+  auto xform_store = [&](bf16_t* dst, const uint4 (&v)[NJ], const uint4 (&v2)[NJ], const uint4 (&v3)[NJ3], int cch,
+                         int tof, unsigned okb) {
     // this thread's 8 channels cch..cch+7 are the same for all NJ chunks of the k-step: their coefficients are read
     // once per k-step as 16-byte LDS rows (CG_XF_VEC; the element-wise form issued 2-3 scalar LDS reads per element)
     float ca[8], cb[8], cc[8];
@@ -614,7 +626,7 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
         const float4 b4 = *reinterpret_cast<const float4*>(dyn + Ci + cch + 4 * h);
         ca[4 * h] = a4.x, ca[4 * h + 1] = a4.y, ca[4 * h + 2] = a4.z, ca[4 * h + 3] = a4.w;
         cb[4 * h] = b4.x, cb[4 * h + 1] = b4.y, cb[4 * h + 2] = b4.z, cb[4 * h + 3] = b4.w;
-        if constexpr (MODE == 2) {
+        if constexpr (MODE >= 2) {
           const float4 c4 = *reinterpret_cast<const float4*>(dyn + 2 * Ci + cch + 4 * h);
           cc[4 * h] = c4.x, cc[4 * h + 1] = c4.y, cc[4 * h + 2] = c4.z, cc[4 * h + 3] = c4.w;
         }
@@ -624,7 +636,7 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
       for (int e = 0; e < 8; ++e) {
         ca[e] = dyn[cch + e];
         cb[e] = dyn[Ci + cch + e];
-        if constexpr (MODE == 2) cc[e] = dyn[2 * Ci + cch + e];
+        if constexpr (MODE >= 2) cc[e] = dyn[2 * Ci + cch + e];
       }
 #endif
     }
@@ -646,10 +658,17 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
             const float h0 = lo2f(h32[q]), h1 = hi2f(h32[q]);
             x0 = ca[2 * q] * x0 + cb[2 * q] * h0 + cc[2 * q];
             x1 = ca[2 * q + 1] * x1 + cb[2 * q + 1] * h1 + cc[2 * q + 1];
+            if constexpr (MODE == 3) {  // (the order of cg_ew_apply_cf_kernel: A dz + B h + C + add)
+              const uint32_t r32 = q == 0 ? v3[j].x : q == 1 ? v3[j].y : q == 2 ? v3[j].z : v3[j].w;
+              x0 += lo2f(r32);
+              x1 += hi2f(r32);
+            }
           }
           w32[q] = pack2bf(x0, x1);
         }
         t = make_uint4(w32[0], w32[1], w32[2], w32[3]);
+        if constexpr (MODE == 3)
+          if (xo != nullptr) *reinterpret_cast<uint4*>(xo + pbase[j] + tof) = t;
       }
       *reinterpret_cast<uint4*>(dst + (rB + RPT * j) * RP + 8 * cB) = t;
     }
@@ -706,23 +725,23 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
   }
   __syncthreads();  // coefficients in LDS
   const int nk = (K + BK - 1) / BK;
-  uint4 ra[AJ], rb[NJ], rb2[NJ];
-  int cch;
+  uint4 ra[AJ], rb[NJ], rb2[NJ], rb3[NJ3];
+  int cch, tof;
   unsigned okb;
   next_pos(0);
   load_a(0, ra);
-  load_b(0, rb, rb2, cch, okb);
+  load_b(0, rb, rb2, rb3, cch, tof, okb);
   store_a(sa[0], ra);
-  xform_store(sb[0], rb, rb2, cch, okb);
+  xform_store(sb[0], rb, rb2, rb3, cch, tof, okb);
   __syncthreads();
   for (int ks = 0; ks < nk; ++ks) {
     const int cur = ks & 1;
     const bool more = ks + 1 < nk;
-    int ncch = 0;
+    int ncch = 0, ntof = 0;
     if (more) {
       next_pos(BK * (ks + 1));
       load_a(BK * (ks + 1), ra);
-      load_b(BK * (ks + 1), rb, rb2, ncch, okb);
+      load_b(BK * (ks + 1), rb, rb2, rb3, ncch, ntof, okb);
     }
     if constexpr (M32) {
       // lane l: A row (l & 31), B pixel (l & 31), k = 16 s + 8 (l >> 5) .. + 7 of each 16-deep half step s
@@ -770,7 +789,7 @@ __global__ __launch_bounds__(256) void convg_fwd_kernel(CgArgs a) {
     }
     if (more) {
       store_a(sa[cur ^ 1], ra);
-      xform_store(sb[cur ^ 1], rb, rb2, ncch, okb);
+      xform_store(sb[cur ^ 1], rb, rb2, rb3, ncch, ntof, okb);
     }
     __syncthreads();
   }
@@ -1888,6 +1907,7 @@ DTF_API int dtf_convg_fwd(const CgArgs* a, int tc, int mode, int epi, int trans,
   // epilogue, or plain
   CG_ALL_TC(0, 6, false, 1)
   CG_ALL_TC(2, 6, false, 1)
+  CG_ALL_TC(3, 6, false, 1)  // v2 bottleneck conv3: dy = the next block's BN1-backward apply, also stored (xout)
   CG_ALL_TC(2, 7, false, 1)
   CG_ALL_TC(0, 7, false, 1)
   CG_ALL_TC(0, 15, false, 1)  // + the compact stride-2 projection gradient (v2 bottleneck conv1 of a stage's first block)

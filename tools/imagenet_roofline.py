@@ -21,9 +21,11 @@ import sys
 STAGES = [(64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)]  # (filters, blocks, first stride)
 
 
-def launches(N: int, H: int = 224):
+def launches(N: int, H: int = 224, fold1_maxc: int = 256, compact_pd: bool = True):
     """(family, label, bytes, flops) of every launch of one training step that moves activations, in the plan's
-    execution order (engine/hip_imagenet.py _build, non-folded path)."""
+    execution order (engine/hip_imagenet.py _build).  ``fold1_maxc``: blocks without a projection whose conv1 has at
+    most that many output channels apply BN1 + ReLU inside conv1 (CG_FOLD1: no "ax" pass); ``compact_pd``: a
+    stride-2 projection's data gradient is stored at the dy resolution (CG_COMPACT_PD).  0 / False: the plain path."""
     B = 2 * N  # bytes per (pixel, channel) element over the population batch
     out = []
     H1, H2 = H // 2, H // 4
@@ -39,7 +41,8 @@ def launches(N: int, H: int = 224):
             hw, cin = hw // st, 4 * f
     for si, b, hi, ho, cin, f, fo, proj in geo:
         t = "s%db%d " % (si + 1, b)
-        out.append(("bn_relu_apply", t + "ax", B * 2 * hi * hi * cin, 0))
+        if proj or f > fold1_maxc:
+            out.append(("bn_relu_apply", t + "ax", B * 2 * hi * hi * cin, 0))
         if proj:
             out.append(("conv fwd", t + "proj 1x1", B * (ho * ho * cin + ho * ho * fo), 2 * N * ho * ho * cin * fo))
         out.append(("conv fwd", t + "c1 1x1", B * (hi * hi * cin + hi * hi * f), 2 * N * hi * hi * cin * f))
@@ -55,10 +58,12 @@ def launches(N: int, H: int = 224):
         out.append(("conv dgrad", t + "c2 3x3", B * (ho * ho * f + 2 * hi * hi * f), 2 * N * ho * ho * 9 * f * f))
         out.append(("bn_bwd_apply", t + "dh1", B * 3 * hi * hi * f, 0))
         out.append(("conv wgrad", t + "c2", B * (hi * hi * f + ho * ho * f), 2 * N * ho * ho * 9 * f * f))
+        cpd = proj and compact_pd and ho < hi
+        pd = ho * ho * cin if cpd else hi * hi * cin  # the projection data gradient's pixels x channels
         if proj:
-            out.append(("conv dgrad", t + "proj 1x1", B * (ho * ho * fo + hi * hi * cin), 2 * N * ho * ho * cin * fo))
+            out.append(("conv dgrad", t + "proj 1x1", B * (ho * ho * fo + pd), 2 * N * ho * ho * cin * fo))
             out.append(("conv wgrad", t + "proj", B * (ho * ho * cin + ho * ho * fo), 2 * N * ho * ho * cin * fo))
-        out.append(("conv dgrad", t + "c1 1x1", B * (hi * hi * f + (3 if proj else 2) * hi * hi * cin),
+        out.append(("conv dgrad", t + "c1 1x1", B * (hi * hi * f + 2 * hi * hi * cin + (pd if proj else 0)),
                     2 * N * hi * hi * cin * f))
         out.append(("conv wgrad", t + "c1", B * (hi * hi * cin + hi * hi * f), 2 * N * hi * hi * cin * f))
         out.append(("bn_bwd_apply", t + "g", B * (3 if proj else 4) * hi * hi * cin, 0))
@@ -86,7 +91,7 @@ def kernel_family(k: str):
     return None
 
 
-def per_launch(trace_csv: str, N: int):
+def per_launch(trace_csv: str, N: int, **kw):
     """Zip the last complete step of the trace with launches(): (family, label, bytes, flops, measured us)."""
     rows = list(csv.DictReader(open(trace_csv)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -95,7 +100,7 @@ def per_launch(trace_csv: str, N: int):
     seq = [(kernel_family(r["Kernel_Name"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
            for r in rows[lo:ends[-1]]]
     seq = [x for x in seq if x[0] is not None]
-    ls = launches(N)
+    ls = launches(N, **kw)
     assert [x[0] for x in seq] == [x[0] for x in ls], "trace does not match the launch model"
     return [l + (m[1],) for l, m in zip(ls, seq)]
 
@@ -107,8 +112,11 @@ def main():
     ap.add_argument("--bw", type=float, default=6.3, help="achievable HBM TB/s")
     ap.add_argument("--pf", type=float, default=2.5, help="dense bf16 MFMA peak, PFLOP/s")
     ap.add_argument("--top", type=int, default=25, help="launches listed by excess over their floor")
+    ap.add_argument("--fold1-maxc", type=int, default=256, help="CG_FOLD1_MAXC of the traced plan (0: no fold)")
+    ap.add_argument("--no-compact-pd", action="store_true", help="the traced plan ran without CG_COMPACT_PD")
     a = ap.parse_args()
-    rows = per_launch(a.trace, a.n) if a.trace else [l + (0.0,) for l in launches(a.n)]
+    kw = dict(fold1_maxc=a.fold1_maxc, compact_pd=not a.no_compact_pd)
+    rows = per_launch(a.trace, a.n, **kw) if a.trace else [l + (0.0,) for l in launches(a.n, **kw)]
     fam = collections.defaultdict(lambda: [0.0, 0.0, 0.0])
     for f, lab, b, fl, m in rows:
         floor = max(b / (a.bw * 1e12), fl / (a.pf * 1e15)) * 1e6

@@ -120,6 +120,9 @@ struct CgArgs {
 };
 
 
+#ifndef CG_EPI_EARLY
+#define CG_EPI_EARLY 1  // generic epilogue: residual / mask loads issued before the accumulator staging + barrier
+#endif
 // Epilogue shared by the forward / data-gradient kernels: the fp32 accumulator tile (wave grid WRN x 4/WRN of
 // (TC/WRN) x (TP/(4/WRN)) per wave) goes through LDS (cst, NHALF passes), then [+ residual], [mask by BN(xm)+ReLU],
 // bf16 store and per-channel statistics.
@@ -160,12 +163,15 @@ __device__ __forceinline__ void convg_epilogue_impl(const CgArgs& a, StageFn&& s
   for (int i = 0; i < 8; ++i) ss[i] = sq[i] = 0.f;
   constexpr int CPF = TC + 4;
   for (int h = 0; h < NHALF; ++h) {
-    if (h > 0) __syncthreads();  // the previous half's rows have been read
-    stage(h);
-    __syncthreads();
     // all residual / mask rows of this half are loaded before the first store (the stores may alias them for the
-    // compiler), so a thread keeps NPASS 16-byte loads in flight instead of one per pass
+    // compiler), so a thread keeps NPASS 16-byte loads in flight instead of one per pass; they are issued before the
+    // accumulator staging and its barrier(s) (CG_EPI_EARLY), whose LDS traffic then covers part of their latency
     constexpr int NPASS = TP / NHALF / PPP;
+    if constexpr (!CG_EPI_EARLY) {
+      if (h > 0) __syncthreads();  // the previous half's rows have been read
+      stage(h);
+      __syncthreads();
+    }
     long orow[NPASS];
     uint4 rrv[NPASS], xrv[NPASS];
 #pragma unroll
@@ -190,6 +196,11 @@ __device__ __forceinline__ void convg_epilogue_impl(const CgArgs& a, StageFn&& s
         rrv[it] = ld16(a.res, orow[it], orow[it] >= 0);
       }
       if constexpr (EPI & 2) xrv[it] = ld16(a.xm, orow[it], orow[it] >= 0);
+    }
+    if constexpr (CG_EPI_EARLY) {
+      if (h > 0) __syncthreads();  // the previous half's rows have been read
+      stage(h);
+      __syncthreads();
     }
 #pragma unroll
   for (int it = 0; it < NPASS; ++it) {

@@ -120,8 +120,8 @@ struct CgArgs {
 };
 
 
-#ifndef CG_EPI_EARLY
-#define CG_EPI_EARLY 1  // generic epilogue: residual / mask loads issued before the accumulator staging + barrier
+#ifndef CG_EPI_AHEAD
+#define CG_EPI_AHEAD 1  // generic epilogue: the next part's residual / mask loads issued while a part is processed
 #endif
 // Epilogue shared by the forward / data-gradient kernels: the fp32 accumulator tile (wave grid WRN x 4/WRN of
 // (TC/WRN) x (TP/(4/WRN)) per wave) goes through LDS (cst, NHALF passes), then [+ residual], [mask by BN(xm)+ReLU],
@@ -129,7 +129,7 @@ struct CgArgs {
 // stage(h): writes staging part h (pixel rows [h * TP / NHALF, (h + 1) * TP / NHALF) of the tile) into cst as
 // [pixel][channel] fp32 rows of pitch TC + 4 (the MFMA-shape-specific half; convg_epilogue below for 16x16 tiles,
 // convg_epilogue32 for 32x32 ones)
-template <int TC, int EPI, bool TRANS, int TP, int NHALF, class StageFn>
+template <int TC, int EPI, bool TRANS, int TP, int NHALF, bool AHEAD, class StageFn>
 __device__ __forceinline__ void convg_epilogue_impl(const CgArgs& a, StageFn&& stage, float* cst,
                                                     dtf_acc_t (&acc_lds)[2][TC], int slot, int o0, int p0, int p1,
                                                     int HWo, int GW, int py, int px) {
@@ -162,18 +162,16 @@ __device__ __forceinline__ void convg_epilogue_impl(const CgArgs& a, StageFn&& s
 #pragma unroll
   for (int i = 0; i < 8; ++i) ss[i] = sq[i] = 0.f;
   constexpr int CPF = TC + 4;
-  for (int h = 0; h < NHALF; ++h) {
-    // all residual / mask rows of this half are loaded before the first store (the stores may alias them for the
-    // compiler), so a thread keeps NPASS 16-byte loads in flight instead of one per pass; they are issued before the
-    // accumulator staging and its barrier(s) (CG_EPI_EARLY), whose LDS traffic then covers part of their latency
-    constexpr int NPASS = TP / NHALF / PPP;
-    if constexpr (!CG_EPI_EARLY) {
-      if (h > 0) __syncthreads();  // the previous half's rows have been read
-      stage(h);
-      __syncthreads();
-    }
-    long orow[NPASS];
-    uint4 rrv[NPASS], xrv[NPASS];
+  // all residual / mask rows of a part are loaded before the first store (the stores may alias them for the
+  // compiler), so a thread keeps NPASS 16-byte loads in flight instead of one per pass; part 0's are issued before
+  // the accumulator staging and its barrier (their latency overlaps that LDS traffic), and with CG_EPI_AHEAD part
+  // h + 1's while part h is processed (two register sets)
+  constexpr int NPASS = TP / NHALF / PPP;
+  // (two sets only where they fit: one epilogue operand, and not in the register-bound t3 kernels -- AHEAD)
+  constexpr int NB = (CG_EPI_AHEAD && AHEAD && NHALF > 1 && (EPI & 3) != 3) ? 2 : 1;
+  long orow_[NB][NPASS];
+  uint4 rrv_[NB][NPASS], xrv_[NB][NPASS];
+  auto issue = [&](int h, long (&orow)[NPASS], uint4 (&rrv)[NPASS], uint4 (&xrv)[NPASS]) {
 #pragma unroll
     for (int it = 0; it < NPASS; ++it) {
       const int p = p0 + h * (TP / NHALF) + pr + PPP * it;
@@ -197,11 +195,18 @@ __device__ __forceinline__ void convg_epilogue_impl(const CgArgs& a, StageFn&& s
       }
       if constexpr (EPI & 2) xrv[it] = ld16(a.xm, orow[it], orow[it] >= 0);
     }
-    if constexpr (CG_EPI_EARLY) {
-      if (h > 0) __syncthreads();  // the previous half's rows have been read
-      stage(h);
-      __syncthreads();
-    }
+  };
+#pragma unroll
+  for (int h = 0; h < NHALF; ++h) {
+    const int b = NB == 2 ? (h & 1) : 0;
+    if (NB == 1 || h == 0) issue(h, orow_[b], rrv_[b], xrv_[b]);
+    if (h > 0) __syncthreads();  // the previous part's rows have been read
+    stage(h);
+    __syncthreads();
+    if (NB == 2 && h + 1 < NHALF) issue(h + 1, orow_[b ^ 1], rrv_[b ^ 1], xrv_[b ^ 1]);
+    const long (&orow)[NPASS] = orow_[b];
+    const uint4 (&rrv)[NPASS] = rrv_[b];
+    const uint4 (&xrv)[NPASS] = xrv_[b];
 #pragma unroll
   for (int it = 0; it < NPASS; ++it) {
     const int pl = pr + PPP * it;  // staged row
@@ -274,7 +279,7 @@ __device__ __forceinline__ void convg_epilogue_impl(const CgArgs& a, StageFn&& s
   }
 }
 
-template <int TC, int EPI, bool TRANS, int TP, int WRN, int NHALF>
+template <int TC, int EPI, bool TRANS, int TP, int WRN, int NHALF, bool AHEAD = true>
 __device__ __forceinline__ void convg_epilogue(const CgArgs& a, f32x4_t (&acc)[TC / WRN / 16][TP / (4 / WRN) / 16],
                                                float* cst, dtf_acc_t (&acc_lds)[2][TC], int slot, int o0, int p0, int p1,
                                                int HWo, int GW, int py, int px) {
@@ -294,7 +299,7 @@ __device__ __forceinline__ void convg_epilogue(const CgArgs& a, f32x4_t (&acc)[T
       }
     }
   };
-  convg_epilogue_impl<TC, EPI, TRANS, TP, NHALF>(a, stage, cst, acc_lds, slot, o0, p0, p1, HWo, GW, py, px);
+  convg_epilogue_impl<TC, EPI, TRANS, TP, NHALF, AHEAD>(a, stage, cst, acc_lds, slot, o0, p0, p1, HWo, GW, py, px);
 }
 
 // 32x32 accumulator tiles (v_mfma_f32_32x32x16_bf16): register r of lane l holds D[row 8 (r >> 2) + 4 (l >> 5) +
@@ -323,7 +328,7 @@ __device__ __forceinline__ void convg_epilogue32(const CgArgs& a, f32x16_t (&acc
       }
     }
   };
-  convg_epilogue_impl<TC, EPI, TRANS, TP, NHALF>(a, stage, cst, acc_lds, slot, o0, p0, p1, HWo, GW, py, px);
+  convg_epilogue_impl<TC, EPI, TRANS, TP, NHALF, true>(a, stage, cst, acc_lds, slot, o0, p0, p1, HWo, GW, py, px);
 }
 
 // Register-direct epilogue of the 16x16 accumulator tiles (no residual, TRANS = false): lane l of a wave holds, per
@@ -1060,7 +1065,7 @@ __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
       convg_epilogue_regs<TC, EPI, TP, WRN>(a, acc, acc_lds, slot, o0, p0, p1);
     } else {
       __syncthreads();  // the epilogue reuses the operand LDS
-      convg_epilogue<TC, EPI, false, TP, WRN, NHALF>(a, acc, reinterpret_cast<float*>(smem_), acc_lds, slot, o0, p0,
+      convg_epilogue<TC, EPI, false, TP, WRN, NHALF, false>(a, acc, reinterpret_cast<float*>(smem_), acc_lds, slot, o0, p0,
                                                      p1, 0, 0, 0, 0);
     }
     return;
@@ -1118,7 +1123,7 @@ __global__ __launch_bounds__(256, 2) void convg_t3_kernel(CgArgs a) {
   if constexpr (T3_EPI_REGS)
     convg_epilogue_regs<TC, EPI, TP, WRN>(a, acc, acc_lds, slot, o0, p0, p1);
   else
-    convg_epilogue<TC, EPI, false, TP, WRN, NHALF>(a, acc, reinterpret_cast<float*>(smem_), acc_lds, slot, o0, p0,
+    convg_epilogue<TC, EPI, false, TP, WRN, NHALF, false>(a, acc, reinterpret_cast<float*>(smem_), acc_lds, slot, o0, p0,
                                                    p1, 0, 0, 0, 0);
   T3_STAMP(3);
   T3_STAMP_FLUSH();

@@ -38,7 +38,7 @@ _CG_BK = 32  # K depth of one LDS stage of the forward / dgrad tiles
 _CG_WPK = 32
 _CG_WO64 = True
 _CG_WIDE = True  # wide-column 3x3 weight-gradient tiles
-_CG_WIDE128 = True
+_CG_WIDE128 = os.environ.get("DTF_CG_WIDE128", "1") == "1"  # 128-row wide wgrad tiles (0: 64-row: twice the items, half the splits)
 _CG_WIDE7 = True  # one 64 x 416 tile for the 7x7 stem
 _CG_WIDE1 = True  # the wide tiles for 1x1 convs with Ci % 256 == 0
 _CG_TP256_128 = os.environ.get("DTF_CG_TP256_128", "1") == "1"  # 128 x 256 tiles (2 x 2 waves of 64 x 128)

@@ -106,6 +106,9 @@ _CG_SMALL = int(os.environ.get("DTF_CG_SMALL", "0"))
 _CG_SHORTK = int(os.environ.get("DTF_CG_SHORTK", "0"))
 T3_FLAGS = int(os.environ.get("DTF_T3_FLAGS", "1"))  # direct: 81.61 vs staged 80.92 ms (profiles/r4_imagenet_t3_ab.log)
 _CG_WG_TARGET = int(os.environ.get("DTF_CG_WG_TARGET", "512"))
+# generic forward / dgrad launches whose images are at most this wide take 64-channel output tiles (more, smaller
+# workgroups for the 7x7 stage's few-round launches; 0: off -- 7 / 14 measured +1.0 / +3.1 ms, profiles/r6_imagenet_tc64_ab.log)
+_CG_TC64_HW = int(os.environ.get("DTF_CG_TC64_HW", "0"))
 _CG_WG_MINCHUNK = int(os.environ.get("DTF_CG_WG_MINCHUNK", "2048"))
 _CG_WG_BALANCED = os.environ.get("DTF_CG_WG_BALANCED", "0") == "1"
 
@@ -664,7 +667,7 @@ class _ImageNetPlan:
                 self._add(ops.lib().dtf_convg_stem_s2d, ctypes.byref(a), a.Hi, 2, epi, work.shape[0])
                 return
         a.log2ci = _log2(a.Ci)
-        tc = 128 if a.Co >= 128 else 64
+        tc = 128 if a.Co >= 128 and max(hw_in, hw_out) > _CG_TC64_HW else 64
         if (k == 3 and c.stride == 1 and (mode == 0 or (mode == 1 and not dgrad)) and hw_in in _CG_T3
                 and ci != be.prog.stem and epi == (6 if dgrad else 4) and a.Ci % 32 == 0 and a.Ci <= 512):
             rows = _CG_T3[hw_in]

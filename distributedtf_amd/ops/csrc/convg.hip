@@ -120,6 +120,9 @@ struct CgArgs {
 };
 
 
+#ifndef CG_WIDE_P1
+#define CG_WIDE_P1 1  // wide 1x1 weight gradients: stride-1 table-free addressing (convg_wgrad_wide_kernel P1)
+#endif
 #ifndef CG_EPI_AHEAD
 #define CG_EPI_AHEAD 1  // generic epilogue: the next part's residual / mask loads issued while a part is processed
 #endif
@@ -1349,7 +1352,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PK == 32 ? 
 // 49 taps x 8 channels, one tile).
 // MX 1: x operand = relu(BN(x)) applied while staging (c_in scale / shift per channel, staged in LDS; the folded
 // forward keeps no materialised BN+ReLU output)
-template <int WWO, int WWT, int MX = 0>
+template <int WWO, int WWT, int MX = 0, bool P1 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ? 3 : 2))) void convg_wgrad_wide_kernel(CgArgs a) {
   constexpr int WWOP = WWO + 8, MTW = WWO / 32, DJ = WWO / 64, WWP = WWT + 8;
   constexpr int WXC = 32 * (WWT / 8);  // x chunks (8 columns) per k-step
@@ -1426,7 +1429,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ?
     }
   };
   bool xval[WXJ];  // MX 1: the chunk of xv holds real pixels (not padding)
+  // P1 (stride-1 1x1 conv: the x pixel of a k row IS its dy pixel): per-thread base offsets advanced by a
+  // wave-uniform k-step stride -- no per-k-step pixel table (make_pinfo's divides, an LDS int4 read per chunk) and
+  // no bounds arithmetic beyond the item's pixel range
+  long dbase[P1 ? DJ : 1], xbase[P1 ? WXJ : 1];
+  if constexpr (P1) {
+#pragma unroll
+    for (int j = 0; j < DJ; ++j) dbase[j] = (long)(p0 + drow[j]) * Co + o0 + dch[j];
+#pragma unroll
+    for (int j = 0; j < WXJ; ++j) xbase[j] = (long)(p0 + xrow[j]) * Ci + (xoff[j] >> 16);
+  }
   auto load = [&](int pk0, uint4 (&dv)[DJ], uint4 (&xv)[WXJ]) {
+    if constexpr (P1) {
+      const long dk = (long)(pk0 - p0) * Co, xk = (long)(pk0 - p0) * Ci;
+#pragma unroll
+      for (int j = 0; j < DJ; ++j) dv[j] = ld16(a.dy, dbase[j] + dk, pk0 + drow[j] < p1 && dok[j]);
+#pragma unroll
+      for (int j = 0; j < WXJ; ++j) {
+        const bool ok = xok[j] && pk0 + xrow[j] < p1;
+        xv[j] = ld16(a.x, xbase[j] + xk, ok);
+        xval[j] = ok;
+      }
+      return;
+    }
     const int par = (pk0 - p0) / 32 & 1;
 #pragma unroll
     for (int j = 0; j < DJ; ++j) {
@@ -1482,8 +1507,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ?
 #pragma unroll
     for (int n = 0; n < NTN; ++n) acc[m][n] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
   const int nk = (p1 - p0 + 31) / 32;
-  make_pinfo(p0);
-  if (nk > 1) make_pinfo(p0 + 32);
+  if constexpr (!P1) {
+    make_pinfo(p0);
+    if (nk > 1) make_pinfo(p0 + 32);
+  }
   __syncthreads();
   if constexpr (XCOL) coef8(xoff[0] >> 16, xsc, xsh);  // (the xcoef rows are visible after the barrier above)
   uint4 dv[DJ], xv[WXJ];
@@ -1495,7 +1522,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WWO == 64 ?
     const int cur = ks & 1;
     const bool more = ks + 1 < nk;
     if (more) load(p0 + 32 * (ks + 1), dv, xv);
-    if (ks + 2 < nk) make_pinfo(p0 + 32 * (ks + 2));
+    if constexpr (!P1)
+      if (ks + 2 < nk) make_pinfo(p0 + 32 * (ks + 2));
     bf16x8_t fa[MTW];
 #pragma unroll
     for (int m = 0; m < MTW; ++m) {
@@ -2018,6 +2046,9 @@ DTF_API int dtf_convg_wgrad_wide(const CgArgs* a, int wo, int wt, int nwork, int
   if (wt != 416 && ((a->Ci < 64 && a->cin_real != -3) || K % wt != 0)) return -2;  // -3: the s2d stem (16 ch)
   if (mode_x != 0 && (mode_x != 1 || wt == 416 || a->Ci > 4096)) return -2;
   const size_t dyn = mode_x ? (size_t)2 * a->Ci * sizeof(float) : 0;
+  // a stride-1 1x1 conv (x pixel = dy pixel): the table-free P1 addressing (CG_WIDE_P1)
+  const bool p1x1 = CG_WIDE_P1 && a->kh == 1 && a->kw == 1 && a->stride == 1 && a->pad == 0 && a->Hi == a->Ho &&
+                    a->Wi == a->Wo && a->cin_real == a->Ci;
 #define WW_CASE(WO_, WT_)                                                                                     \
   if (wo == WO_ && wt == WT_) {                                                                               \
     if (mode_x)                                                                                               \
@@ -2026,8 +2057,18 @@ DTF_API int dtf_convg_wgrad_wide(const CgArgs* a, int wo, int wt, int nwork, int
       hipLaunchKernelGGL((convg_wgrad_wide_kernel<WO_, WT_>), dim3(nwork), dim3(256), 0, stream, *a);         \
     return DTF_CHECK_LAUNCH();                                                                                \
   }
+#define WW_CASE_P1(WO_)                                                                                           \
+  if (p1x1 && wo == WO_ && wt == 256) {                                                                           \
+    if (mode_x)                                                                                                   \
+      hipLaunchKernelGGL((convg_wgrad_wide_kernel<WO_, 256, 1, true>), dim3(nwork), dim3(256), dyn, stream, *a);  \
+    else                                                                                                          \
+      hipLaunchKernelGGL((convg_wgrad_wide_kernel<WO_, 256, 0, true>), dim3(nwork), dim3(256), 0, stream, *a);    \
+    return DTF_CHECK_LAUNCH();                                                                                    \
+  }
+  WW_CASE_P1(128) WW_CASE_P1(64)
   WW_CASE(128, 288) WW_CASE(64, 288) WW_CASE(128, 256) WW_CASE(64, 256)
 #undef WW_CASE
+#undef WW_CASE_P1
   if (wo == 64 && wt == 416 && mode_x == 0) {  // the 7x7 stem: 49 taps x 8 (3 real) channels in one tile
     hipLaunchKernelGGL((convg_wgrad_wide_kernel<64, 416>), dim3(nwork), dim3(256), 0, stream, *a);
     return DTF_CHECK_LAUNCH();

@@ -1141,7 +1141,7 @@ constexpr int KP = WT + 8;
 // whose 128-row tile would be half padding)
 // occupancy matters more than anything else here (the k-step loads are latency-bound): ask for 4 workgroups per
 // CU (<= 128 registers); measured: the 140-register build at 3 per CU, and a prefetch-2 build at 2 per CU, slower
-template <int MODE_X, int MODE_DY, int PK = 32, int WO = 128>
+template <int MODE_X, int MODE_DY, int PK = 32, int WO = 128, bool P1 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PK == 32 ? 4 : 2))) void convg_wgrad_kernel(CgArgs a) {
   constexpr int NJ = PK / 16;  // pixel rows per thread per k-step
   constexpr int WRN = WO / 64, WCN = 4 / WRN;  // wave grid (rows x columns)
@@ -1213,8 +1213,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PK == 32 ? 
       pinfo[(pk0 - p0) / PK & 1][tid] = inf;
     }
   };
+  // P1 (stride-1 1x1 conv, x pixel = dy pixel): base offsets advanced by a wave-uniform k-step stride instead of
+  // the per-k-step pixel table (as convg_wgrad_wide_kernel P1)
+  const long dbase = (long)(p0 + kr) * Co + dcol, xbase = (long)(p0 + kr) * Ci + xci;
   auto load = [&](int pk0, uint4 (&dv)[NJ], uint4 (&dv2)[NJ], uint4 (&xv)[NJ], unsigned& okm) {
     okm = 0;
+    if constexpr (P1) {
+      const long dk = (long)(pk0 - p0) * Co, xk = (long)(pk0 - p0) * Ci;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const bool pin = pk0 + kr + 16 * j < p1;
+        const bool dok = pin && dcol_ok, xok = pin && xcol_ok;
+        const long dofs = dbase + dk + (long)(16 * j) * Co;
+        dv[j] = ld16(a.dy, dofs, dok);
+        dv2[j] = make_uint4(0, 0, 0, 0);
+        if constexpr (MODE_DY == 2) dv2[j] = ld16(a.dy2, dofs, dok);
+        xv[j] = ld16(a.x, xbase + xk + (long)(16 * j) * Ci, xok);
+        okm |= ((unsigned)dok << j) | (((unsigned)xok << NJ) << j);
+      }
+      return;
+    }
     const int par = (pk0 - p0) / PK & 1;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -1278,8 +1296,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PK == 32 ? 
   // (A two-register-stage variant -- loads of k-step ks + 2 in flight while ks computes -- measured slower:
   // 22.5 -> 27.3 ms of wgrad per pop-8 ResNet-50 step, occupancy 3 -> 2; profiles/r2_s3_imagenet_wgrad_pf2.log)
   const int nk = (p1 - p0 + PK - 1) / PK;
-  make_pinfo(p0);
-  if (nk > 1) make_pinfo(p0 + PK);
+  if constexpr (!P1) {
+    make_pinfo(p0);
+    if (nk > 1) make_pinfo(p0 + PK);
+  }
   __syncthreads();  // coefficients + the first two pixel tables
   uint4 dv[NJ], dv2[NJ], xv[NJ];
   unsigned okm;
@@ -1292,7 +1312,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PK == 32 ? 
     const bool more = ks + 1 < nk;
     if (more) load(p0 + PK * (ks + 1), dv, dv2, xv, okm);
     // table of k-step ks + 2 into the slot k-step ks read (its readers passed the previous barrier)
-    if (ks + 2 < nk) make_pinfo(p0 + PK * (ks + 2));
+    if constexpr (!P1)
+      if (ks + 2 < nk) make_pinfo(p0 + PK * (ks + 2));
 #pragma unroll
     for (int kk = 0; kk < PK / 32; ++kk) {
       bf16x8_t fa[4], fb[NTN];
@@ -2016,9 +2037,13 @@ DTF_API int dtf_convg_wgrad(const CgArgs* a, int mode_x, int mode_dy, int nwork,
   if ((a->Ci & (a->Ci - 1)) != 0 || a->Ci < 8 || (a->Co & 7) != 0) return -2;
   const size_t dyn = (size_t)(2 * a->Ci + 3 * a->Co) * sizeof(float);
   dim3 grid(nwork), block(256);
+  const bool p1x1 = CG_WIDE_P1 && a->kh == 1 && a->kw == 1 && a->stride == 1 && a->pad == 0 && a->Hi == a->Ho &&
+                    a->Wi == a->Wo && a->cin_real == a->Ci;
 #define WG_CASE(MX, MD)                                                                     \
   if (mode_x == MX && mode_dy == MD) {                                                      \
-    if (pk64 && wo64)                                                                       \
+    if (p1x1 && !pk64 && !wo64)                                                             \
+      hipLaunchKernelGGL((convg_wgrad_kernel<MX, MD, 32, 128, true>), grid, block, dyn, stream, *a); \
+    else if (pk64 && wo64)                                                                  \
       hipLaunchKernelGGL((convg_wgrad_kernel<MX, MD, 64, 64>), grid, block, dyn, stream, *a); \
     else if (pk64)                                                                          \
       hipLaunchKernelGGL((convg_wgrad_kernel<MX, MD, 64>), grid, block, dyn, stream, *a);   \

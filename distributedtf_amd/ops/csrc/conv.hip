@@ -33,6 +33,9 @@
 #ifndef DTF_FUSED16_WLDS
 #define DTF_FUSED16_WLDS 1  // C = 16 fused backward: dgrad weights read from LDS per MFMA instead of held in VGPRs
 #endif
+#ifndef DTF_TRANSFORM8_PK
+#define DTF_TRANSFORM8_PK 1  // strided / generic CIFAR conv staging: packed two-channel BN transforms
+#endif
 #ifndef DTF_BWD_COEFREG
 #define DTF_BWD_COEFREG 1  // conv_bwd_fused<16, 3>: staging + epilogue BN coefficients held in VGPRs
 #endif
@@ -363,8 +366,14 @@ __device__ __forceinline__ void tile_load(TileRegs<C, MODE, MAXC>& R, const Tile
 }
 
 template <int MODE>
+__device__ __forceinline__ uint4 xform8(uint4 v, uint4 v2, int c0, const float* __restrict__ coef);
+
+template <int MODE>
 __device__ __forceinline__ uint4 transform8(uint4 v, uint4 v2, int c0, const float* __restrict__ coef) {
   if constexpr (MODE == 0) return v;
+  // DTF_TRANSFORM8_PK: the packed two-channel form (v_pk_fma_f32 on 8-byte coefficient pairs, xform8) instead of
+  // per-element f32 math and 4-byte coefficient reads
+  if constexpr (DTF_TRANSFORM8_PK) return xform8<MODE>(v, v2, c0, coef);
   uint32_t w32[4] = {v.x, v.y, v.z, v.w};
   uint32_t h32[4] = {v2.x, v2.y, v2.z, v2.w};
 #pragma unroll

@@ -81,7 +81,7 @@ CG_FOLD1_MAXC = int(os.environ.get("DTF_CG_FOLD1_MAXC", "256"))
 # tensor is zeros) and added by conv1's epilogue at even pixels
 CG_COMPACT_PD = os.environ.get("DTF_CG_COMPACT_PD", "1") == "1"
 CG_CLASS_LPT = os.environ.get("DTF_CG_CLASS_LPT", "0") == "1"  # stride-2 3x3 data gradient: heavy parity class first
-CG_FOLD1 = os.environ.get("DTF_CG_FOLD1", "1") == "1"
+CG_FOLD1 = os.environ.get("DTF_CG_FOLD1", "1") == "1"  # 73.24 -> 72.87 ms at pop 8 (profiles/r6_imagenet_fold1_ab.log)
 # backward fold of the block-input gradient: g = BN1-backward(dz1, x) [+ g of the next block] is computed by its first
 # consumer -- the previous block's conv3 data gradient (a stride-1 1x1 over g with one output-channel tile when that
 # block's width f <= this: convg MODE 3) -- while it stages g, and stored from there (xout), instead of a standalone
@@ -93,7 +93,7 @@ CG_GFOLD_MAXF = int(os.environ.get("DTF_CG_GFOLD_MAXF", "0"))
 # whose conv3 has at most this many output channels (each a2 element is transformed once per 128-channel tile), so
 # a2 = relu(BN3(h2)) is never written for them (0: off; 256 / 512 / 1024 / 2048 measured -0.1 / +0.0 / +0.3 / +0.4 ms,
 # within box noise at 256: profiles/r6_imagenet_fold3_ab.log)
-CG_FOLD3_MAXC = int(os.environ.get("DTF_CG_FOLD3_MAXC", "0"))  # 73.24 -> 72.87 ms at pop 8 (profiles/r6_imagenet_fold1_ab.log)
+CG_FOLD3_MAXC = int(os.environ.get("DTF_CG_FOLD3_MAXC", "0"))
 # XCD-aware work order (_xcd_order): 0 off, 1 operand-sharing runs on one XCD, 2 additionally every member on its own
 # XCD when the population is a multiple of 8 with equal work per member, 3 (default) also members on XCD subsets when
 # the population divides 8 (pop 4: 39.73 -> 38.95 ms).  ResNet-50 pop 8 x 128:

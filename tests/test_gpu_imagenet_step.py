@@ -101,6 +101,19 @@ def test_hip_imagenet_step_matches_reference(monkeypatch, image, sizes, graph, v
     torch.testing.assert_close(hip.running, ref.running, rtol=3e-2, atol=5e-3)
 
 
+@pytest.mark.parametrize("knobs", [{"CG_GFOLD_MAXF": 128}, {"CG_FOLD3_MAXC": 2048}, {"CG_FOLD": True},
+                                   {"CG_FOLD1": False, "CG_COMPACT_PD": False}])
+def test_hip_imagenet_step_plan_variants(monkeypatch, knobs):
+    """The off-by-default plan switches of engine/hip_imagenet.py against the same fp32 oracle: the block-input
+    gradient applied inside conv3's data gradient (convg MODE 3 + xout, with and without the residual operand),
+    the BN3 fold into conv3, the full BN fold, and the plain path without the read-once BN1 fold and the compact
+    projection gradient.  (Module constants are read when a plan is built, so patching them selects the path.)"""
+    from distributedtf_amd.engine import hip_imagenet
+    for k, v in knobs.items():
+        monkeypatch.setattr(hip_imagenet, k, v)
+    test_hip_imagenet_step_matches_reference(monkeypatch, 64, (4, 6), "1", 2)
+
+
 @pytest.mark.parametrize("version", [1, 2])
 def test_hip_imagenet_block_local_error(version):
     """The loss bound above has to absorb the chaotic growth of bf16 rounding through 16 blocks; this pins the

@@ -48,6 +48,9 @@ DET_WG_PER_MEMBER = 64  # deterministic mode: statistic-producing launches use <
 DUAL_MAX_POP = 2          # dual (dgrad | wgrad role) backward launches up to this many members per GPU ...
 DUAL_CS = (32, 64)        # ... for these channel widths (C = 16 keeps the fused kernel)
 DUAL_WG = {16: 128, 32: 128, 64: 64}  # wgrad-role workgroups per member of a dual launch
+# small populations: every layer's wgrad deferred past the dgrad chain (1) or run by the dual launches (0: C = 32 / 64
+# dual, C = 16 fused -- the round-2 form, kept as an A/B switch)
+SMALL_DEFER = os.environ.get("DTF_SMALL_DEFER", "1") == "1"
 FWD_ITERS_PER_WG = int(os.environ.get("DTF_FWD_ITERS", "4"))  # forward: (image, band) iterations per workgroup (>= FWD_MIN_WG workgroups kept;
 FWD_MIN_WG = 256          # 512 for up to DUAL_MAX_POP members: pop 1 1.059 -> 1.055, pop 2 1.427 -> 1.398 ms)
 FWD_MIN_WG_SMALL = 512
@@ -858,7 +861,7 @@ class _StepPlan:
         # its dgrad role -- the critical path, serialised by the BatchNorm statistics -- and the wgrad work of all
         # those layers runs afterwards in two wide launches (conv_wgrad_all_kernel: widths 64 + 32, width 16).
         # Their dY / x operands stay alive for the whole backward (per-block buffers instead of ping-pong ones).
-        self.defer_wg = self.dual
+        self.defer_wg = self.dual and SMALL_DEFER
         self.persist_fwd = (PERSIST_FWD and dev.type == "cuda" and len(slots) <= PERSIST_MAX_POP
                             and not self.be.det and not self.eval)
         self.overlap_wg = self.defer_wg and WG_OVERLAP and dev.type == "cuda"
@@ -868,7 +871,7 @@ class _StepPlan:
         # launch; profiles/r3_defer_ab.log)
         v2gpu = dev.type == "cuda" and cfg.version == 2
         large = DEFER_MID_CS if (len(slots) <= DEFER_MID_POP and not be.det) else DEFER_LARGE_CS
-        self.defer_cs = {16, 32, 64} if self.defer_wg else (set(large) if v2gpu else set())
+        self.defer_cs = {16, 32, 64} if self.defer_wg else (set(large) if v2gpu and not self.dual else set())
         self._wg_jobs = {}  # (C, wgrad dY mode) -> [(ConvArgs, work table, grad offset)]
         self.launches = []
         self._pending_slab = None  # (slab ptr, reduce table, C, grad offset) of the last fused launch

@@ -52,6 +52,10 @@ DUAL_WG = {16: 128, 32: 128, 64: 64}  # wgrad-role workgroups per member of a du
 # dual, C = 16 fused -- the round-2 form, kept as an A/B switch)
 SMALL_DEFER = os.environ.get("DTF_SMALL_DEFER", "1") == "1"
 FWD_ITERS_PER_WG = int(os.environ.get("DTF_FWD_ITERS", "4"))  # forward: (image, band) iterations per workgroup (>= FWD_MIN_WG workgroups kept;
+# ... per channel width: C = 64 (the 8x8 stage: one band per image) at 2 -- pop 8 3.006 -> 2.989 ms, 512 workgroups of
+# 2 images instead of 256 of 4 (1: +1.2 %; C = 32 at 2: +0.5 %; profiles/r6_fwd_iters_per_width_ab.log)
+FWD_ITERS_C = {64: 2}
+FWD_ITERS_C.update({c: int(os.environ["DTF_FWD_ITERS%d" % c]) for c in (16, 32, 64) if "DTF_FWD_ITERS%d" % c in os.environ})
 FWD_MIN_WG = 256          # 512 for up to DUAL_MAX_POP members: pop 1 1.059 -> 1.055, pop 2 1.427 -> 1.398 ms)
 FWD_MIN_WG_SMALL = 512
 FWD_RESIDENT = int(os.environ.get("DTF_FWD_RESIDENT", "0"))  # stride-1 forward: one round of resident workgroups
@@ -1123,8 +1127,8 @@ class _StepPlan:
             rows = 4  # conv_fwd_s1_kernel<64, ., ., 4>
         bands = Ho // rows
         lo = FWD_MIN_WG_SMALL if len(self.slots) <= DUAL_MAX_POP else FWD_MIN_WG
-        n_wg = self._n_wg_iters(self.N * bands, per_wg=FWD_ITERS_PER_WG, lo=lo,
-                                hi=max(1024, self.N * bands // FWD_ITERS_PER_WG))
+        iters = FWD_ITERS_C.get(cin, FWD_ITERS_PER_WG)
+        n_wg = self._n_wg_iters(self.N * bands, per_wg=iters, lo=lo, hi=max(1024, self.N * bands // iters))
         if FWD_RESIDENT and s1 and len(self.slots) > DUAL_MAX_POP:
             # conv_fwd_s1_kernel occupancy: 4 WGs / CU (C <= 32), 3 (C = 64)
             n_wg = self._det_cap(min(self.N * bands, _n_cu() * (4 if cin <= 32 else 3)))

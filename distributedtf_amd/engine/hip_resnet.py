@@ -133,7 +133,7 @@ PERSIST_FENCE = int(os.environ.get("DTF_PERSIST_FENCE", "0"))  # conv.hip persis
 HALF_BANDS_MAX_IMGS = 128  # C = 64 stage (8x8): 4-row half-image bands for the forward / dgrad launches up to this many
 #                            images per step (one member: whole-image items left half the CUs idle; pop 2 and the
 #                            C = 32 stage are slower with half bands: profiles/r3_half_bands_ab.log)
-DG_ITERS_LARGE = 2        # ... and (image, band) iterations per dgrad workgroup (the weights load once per workgroup)
+DG_ITERS_LARGE = int(os.environ.get("DTF_DG_ITERS", "2"))  # ... and (image, band) iterations per dgrad workgroup (the weights load once per workgroup)
 DG_MIN_WG = 512           # ... keeping at least this many dgrad workgroups
 c_void_p, c_int, c_long = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
 

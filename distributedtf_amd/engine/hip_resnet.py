@@ -55,6 +55,9 @@ FWD_ITERS_PER_WG = int(os.environ.get("DTF_FWD_ITERS", "4"))  # forward: (image,
 # ... per channel width: C = 64 (the 8x8 stage: one band per image) at 2 -- pop 8 3.006 -> 2.989 ms, 512 workgroups of
 # 2 images instead of 256 of 4 (1: +1.2 %; C = 32 at 2: +0.5 %; profiles/r6_fwd_iters_per_width_ab.log)
 FWD_ITERS_C = {64: 2}
+# ... and C = 16 (32x32, 4 bands per image) at no more than 512 workgroups: 8 iterations at pop 8 (3.020 -> 2.999 ms,
+# ResNet-110 -0.4 %), unchanged at pop <= 4 (a flat 8 cost pop 4 +3 %: 256 workgroups; profiles/r6_fwd_iters16_ab.log)
+FWD_WG_TARGET = {16: int(os.environ.get("DTF_FWD_WG16", "512"))}
 FWD_ITERS_C.update({c: int(os.environ["DTF_FWD_ITERS%d" % c]) for c in (16, 32, 64) if "DTF_FWD_ITERS%d" % c in os.environ})
 FWD_MIN_WG = 256          # 512 for up to DUAL_MAX_POP members: pop 1 1.059 -> 1.055, pop 2 1.427 -> 1.398 ms)
 FWD_MIN_WG_SMALL = 512
@@ -1128,6 +1131,8 @@ class _StepPlan:
         bands = Ho // rows
         lo = FWD_MIN_WG_SMALL if len(self.slots) <= DUAL_MAX_POP else FWD_MIN_WG
         iters = FWD_ITERS_C.get(cin, FWD_ITERS_PER_WG)
+        if cin in FWD_WG_TARGET:  # no more than this many workgroups: longer ones once the population allows
+            iters = max(iters, min(8, self.N * bands // FWD_WG_TARGET[cin]))  # (16 at 256 workgroups: +2.4 %)
         n_wg = self._n_wg_iters(self.N * bands, per_wg=iters, lo=lo, hi=max(1024, self.N * bands // iters))
         if FWD_RESIDENT and s1 and len(self.slots) > DUAL_MAX_POP:
             # conv_fwd_s1_kernel occupancy: 4 WGs / CU (C <= 32), 3 (C = 64)
